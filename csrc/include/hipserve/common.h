@@ -1,0 +1,93 @@
+// hipserve — common device helpers for gfx950 (CDNA4, wave64).
+//
+// Everything here is written for MI355X directly: 64-lane wavefronts, 16-byte
+// vector memory ops, bf16 <-> f32 via the native gfx950 converts.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HS_DEVICE __device__ __forceinline__
+#define HS_HOST_DEVICE __host__ __device__ __forceinline__
+
+namespace hipserve {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+// 16-byte vector register types (8 x bf16 as raw 16-bit lanes)
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+
+HS_DEVICE float bf16_to_f32(unsigned short x) {
+  return __uint_as_float(static_cast<unsigned int>(x) << 16);
+}
+
+// Round-to-nearest-even; on gfx950 -O3 lowers to v_cvt_pk_bf16_f32 (NaN-safe).
+HS_DEVICE unsigned short f32_to_bf16(float f) {
+  __bf16 b = static_cast<__bf16>(f);
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+HS_DEVICE unsigned int pack_bf16x2(float lo, float hi) {
+  return static_cast<unsigned int>(f32_to_bf16(lo)) |
+         (static_cast<unsigned int>(f32_to_bf16(hi)) << 16);
+}
+
+// ---- wave64 reductions (xor butterflies over all 64 lanes) ----
+HS_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+HS_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (16 waves). `scratch` needs >= 16 floats.
+HS_DEVICE float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = (lane < nw) ? scratch[lane] : 0.f;
+  r = wave_sum(r);
+  __syncthreads();
+  return r;
+}
+
+HS_DEVICE float block_max(float v, float* scratch) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = (lane < nw) ? scratch[lane] : -INFINITY;
+  r = wave_max(r);
+  __syncthreads();
+  return r;
+}
+
+HS_HOST_DEVICE int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Bijective XCD-aware block remap (MI355X: 8 XCDs, blocks dealt round-robin).
+// Blocks that share operand panels end up on the same XCD's L2.
+HS_DEVICE int xcd_remap(int bid, int nwg) {
+  constexpr int kXcd = 8;
+  if (nwg < kXcd) return bid;
+  const int q = nwg / kXcd, r = nwg % kXcd;
+  const int xcd = bid % kXcd;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / kXcd;
+}
+
+}  // namespace hipserve

@@ -1,0 +1,49 @@
+// hipserve — host-side launchers of the gfx950 kernels. Raw pointers + stream
+// only (no torch types) so each .hip translation unit compiles without the
+// heavy ATen headers; csrc/torch_bindings.cpp validates tensors and calls these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace hipserve {
+
+// norm.hip — residual != nullptr selects the fused add (residual updated in place)
+void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
+                    bool weight_f32, int rows, int hidden, long x_stride,
+                    long out_stride, float eps, hipStream_t s);
+
+// activation.hip
+void launch_silu_and_mul(void* out, const void* in, long rows, int inter,
+                         long in_stride, long out_stride, hipStream_t s);
+
+// rope_cache.hip
+void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
+                       const long* slots, const float* cos_sin, void* k_cache,
+                       void* v_cache, int T, int nq, int nkv, int D,
+                       int block_size, int mode, hipStream_t s);
+
+// attention_decode.hip
+size_t paged_decode_smem_bytes(int D);
+void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
+                         const void* k_cache, const void* v_cache,
+                         const int* block_tables, int bt_stride,
+                         const int* context_lens, float* tmp_out, float* tmp_ml,
+                         int B, int nq, int nkv, int D, int block_size,
+                         int part_size, int max_parts, float scale,
+                         hipStream_t s);
+
+// attention_prefill.hip
+void launch_prefill_attention(void* out, long out_stride, const void* q,
+                              long q_stride, const void* k_cache,
+                              const void* v_cache, const int* block_tables,
+                              int bt_stride, const int* cu_q, const int* ctx_lens,
+                              const int* tiles, int ntiles, int nq, int nkv, int D,
+                              int block_size, float scale, hipStream_t s);
+
+// sampling.hip
+void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf16,
+                   long stride, int rows, int V, const float* temperature,
+                   const int* top_k, const float* top_p, const long* seeds,
+                   const long* steps, hipStream_t s);
+
+}  // namespace hipserve

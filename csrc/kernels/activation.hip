@@ -1,0 +1,41 @@
+// SiLU(gate) * up for the merged gate_up projection output.
+// in: [T, 2*I] (gate | up), out: [T, I]. 16-byte vectors, grid-stride loop
+// capped at 8 workgroups per CU (memory-bound op, HBM roofline target).
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+__global__ __launch_bounds__(256) void silu_and_mul_kernel(
+    unsigned short* __restrict__ out, const unsigned short* __restrict__ in,
+    long rows, int inter, long in_stride, long out_stride) {
+  const int vpr = inter >> 3;  // vectors per row
+  const long total = rows * vpr;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const long r = v / vpr;
+    const int c = (int)(v - r * vpr);
+    const u16x8 g = *reinterpret_cast<const u16x8*>(in + r * in_stride + c * 8);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(in + r * in_stride + inter + c * 8);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf16_to_f32(g[j]);
+      const float s = gf / (1.f + __expf(-gf));
+      o[j] = f32_to_bf16(s * bf16_to_f32(u[j]));
+    }
+    *reinterpret_cast<u16x8*>(out + r * out_stride + c * 8) = o;
+  }
+}
+
+void launch_silu_and_mul(void* out, const void* in, long rows, int inter,
+                         long in_stride, long out_stride, hipStream_t s) {
+  const long total = rows * (inter / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  silu_and_mul_kernel<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(
+      static_cast<unsigned short*>(out), static_cast<const unsigned short*>(in),
+      rows, inter, in_stride, out_stride);
+}
+
+}  // namespace hipserve

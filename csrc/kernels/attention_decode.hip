@@ -1,0 +1,258 @@
+// Paged decode attention for gfx950: one query token per sequence,
+// GQA-packed, split over the context ("partitions") with a separate reduce.
+//
+// Design (MI355X-first, not a CUDA warp-tiling port):
+//  * workgroup = (partition of PS tokens, kv head, sequence); 4 waves; each wave
+//    streams 32-token chunks (chunk c = wave, wave+4, ...) of its partition.
+//  * QK^T runs on MFMA v_mfma_f32_16x16x32_bf16 in the *swapped* form
+//    S^T = K . Q^T: A = 16 K rows (tokens), B = Q^T with the G query heads of the
+//    kv group on the 16 MFMA columns (G <= 16; padding columns are zero).
+//    The 16 A rows of the two 16-row tiles of a chunk are chosen so that lane
+//    group g (= lane>>4) ends up holding tokens 8g..8g+7 of the chunk — exactly
+//    the k-slots the PV MFMA wants in its A operand: P needs no lane movement.
+//  * PV runs on the same MFMA with A = P (rows = heads), B = V. The V cache is
+//    stored transposed per block ([D][block_size]) so each B fragment (8
+//    consecutive tokens of one d column) is ONE 16-byte global load to VGPRs:
+//    no LDS round trip on the memory-bound path (guide: GEMV / M<=16 row).
+//  * online softmax in the log2 domain; the 4 waves are merged through LDS.
+//  * num_partitions == 1 writes the bf16 output directly; otherwise partials
+//    (normalised O + (max, sum)) go to a workspace reduced by a second kernel.
+// Grid dims are fixed by (B, nkv, max_partitions) so the launch is hipGraph
+// capturable for a batch-size bucket; partitions past a sequence's end exit.
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+constexpr int kDecWaves = 4;
+constexpr int kChunk = 32;
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+__global__ __launch_bounds__(256) void paged_decode_kernel(
+    unsigned short* __restrict__ out, long out_stride,
+    const unsigned short* __restrict__ q, long q_stride,
+    const unsigned short* __restrict__ k_cache,
+    const unsigned short* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, float* __restrict__ tmp_out,
+    float* __restrict__ tmp_ml, int nq, int nkv, int block_size, int part_size,
+    int max_parts, float scale) {
+  static_assert(D == 128 || D == 64, "head_dim 64 or 128");
+  constexpr int KS = D / 32;  // k-steps of the QK MFMA
+  constexpr int NB = D / 16;  // 16-column blocks of the PV output
+  const int part = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
+  const int ctx = context_lens[b];
+  const int start = part * part_size;
+  if (start >= ctx) return;
+  const int end = min(start + part_size, ctx);
+  const int G = nq / nkv;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* bt = reinterpret_cast<int*>(smem);                       // <= 256 block ids
+  float* red = reinterpret_cast<float*>(smem + 1024);          // m,l per wave/head
+  float* olds = red + 2 * kDecWaves * 16;                      // [4][16][D]
+
+  const int first_blk = start / block_size;
+  const int nbt = (end - 1) / block_size - first_blk + 1;
+  const int* btab = block_tables + (long)b * bt_stride + first_blk;
+  for (int i = threadIdx.x; i < nbt; i += blockDim.x) bt[i] = btab[i];
+  __syncthreads();
+
+  // Q fragment: B[k = d][n = head]; lane holds head `col`, d = 8*grp + 32*ks + j
+  bf16x8 qf[KS];
+  {
+    const int h = kh * G + col;
+    const unsigned short* qrow = q + (long)b * q_stride + (long)h * D;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      u16x8 v = (col < G) ? *reinterpret_cast<const u16x8*>(qrow + 8 * grp + 32 * ks)
+                          : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  const float sl2 = scale * kLog2e;
+  f32x4 o[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f, l_run = 0.f;
+
+  const long kv_head_stride = (long)block_size * D;  // elements per (block, head)
+  const int nchunks = (end - start + kChunk - 1) / kChunk;
+  const int last_tok = ctx - 1;
+  const int bt_base_tok = first_blk * block_size;
+
+  for (int c = wave; c < nchunks; c += kDecWaves) {
+    const int cs = start + c * kChunk;
+    // ---- K loads: tile a row m -> token 8*(m>>2) + (m&3); tile b -> +4
+    const int m = col;
+    int ta = cs + 8 * (m >> 2) + (m & 3);
+    int tb = ta + 4;
+    ta = min(ta, last_tok);
+    tb = min(tb, last_tok);
+    const unsigned short* ka = k_cache +
+        ((long)bt[(ta - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
+        (long)(ta % block_size) * D + 8 * grp;
+    const unsigned short* kb = k_cache +
+        ((long)bt[(tb - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
+        (long)(tb % block_size) * D + 8 * grp;
+    u16x8 kav[KS], kbv[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kav[ks] = *reinterpret_cast<const u16x8*>(ka + 32 * ks);
+      kbv[ks] = *reinterpret_cast<const u16x8*>(kb + 32 * ks);
+    }
+    // ---- V loads: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
+    int tv = cs + 8 * grp;
+    if (tv > last_tok) tv = last_tok & ~7;
+    const unsigned short* vb = v_cache +
+        ((long)bt[(tv - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
+        (tv % block_size) + (long)col * block_size;
+    u16x8 vv[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      vv[n] = *reinterpret_cast<const u16x8*>(vb + (long)16 * n * block_size);
+
+    // ---- S^T = K . Q^T
+    f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kav[ks]), qf[ks], sa, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kbv[ks]), qf[ks], sb, 0, 0, 0);
+    }
+    // lane holds scores of tokens cs + 8*grp + r (sa) and + 4 + r (sb) for head col
+    float s[8];
+    float mx = -1e30f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t0 = cs + 8 * grp + r;
+      s[r] = (t0 <= last_tok) ? sa[r] * sl2 : -1e30f;
+      s[r + 4] = (t0 + 4 <= last_tok) ? sb[r] * sl2 : -1e30f;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) mx = fmaxf(mx, s[r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float psum = 0.f;
+    bf16x8 pf;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float p = exp2f(s[r] - m_new);
+      psum += p;
+      pf[r] = static_cast<__bf16>(p);
+    }
+    l_run = l_run * alpha + psum;
+    // rescale O: rows of the PV output are heads 4*grp + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a_r = __shfl(alpha, 4 * grp + r, 64);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) o[n][r] *= a_r;
+    }
+    // ---- O += P . V
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vv[n]), o[n], 0, 0, 0);
+  }
+
+  // ---- per-wave row sums, then merge the 4 waves through LDS
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (lane < 16) {
+    red[(wave * 16 + lane) * 2 + 0] = m_run;
+    red[(wave * 16 + lane) * 2 + 1] = l_run;
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 4 * grp + r;
+      olds[(wave * 16 + h) * D + 16 * n + col] = o[n][r];
+    }
+  __syncthreads();
+
+  const int nparts_seq = (ctx + part_size - 1) / part_size;
+  for (int it = threadIdx.x; it < G * D; it += blockDim.x) {
+    const int h = it / D, d = it % D;
+    float M = -1e30f;
+#pragma unroll
+    for (int w = 0; w < kDecWaves; ++w) M = fmaxf(M, red[(w * 16 + h) * 2]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < kDecWaves; ++w) {
+      const float f = exp2f(red[(w * 16 + h) * 2] - M);
+      L += red[(w * 16 + h) * 2 + 1] * f;
+      acc += olds[(w * 16 + h) * D + d] * f;
+    }
+    const int hq = kh * G + h;
+    if (nparts_seq == 1) {
+      out[(long)b * out_stride + (long)hq * D + d] = f32_to_bf16(acc / L);
+    } else {
+      const long base = ((long)b * nq + hq) * max_parts + part;
+      tmp_out[base * D + d] = acc / L;
+      if (d == 0) {
+        tmp_ml[base * 2 + 0] = M;
+        tmp_ml[base * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+// Merge partitions: one workgroup per (head, sequence), one lane per d.
+template <int D>
+__global__ __launch_bounds__(D) void paged_decode_reduce_kernel(
+    unsigned short* __restrict__ out, long out_stride,
+    const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
+    const int* __restrict__ context_lens, int nq, int part_size, int max_parts) {
+  const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const int ctx = context_lens[b];
+  const int np = (ctx + part_size - 1) / part_size;
+  if (np <= 1) return;
+  const long base = ((long)b * nq + h) * max_parts;
+  float M = -1e30f;
+  for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
+  float L = 0.f, acc = 0.f;
+  for (int p = 0; p < np; ++p) {
+    const float w = exp2f(tmp_ml[(base + p) * 2] - M) * tmp_ml[(base + p) * 2 + 1];
+    L += w;
+    acc += w * tmp_out[(base + p) * D + d];
+  }
+  out[(long)b * out_stride + (long)h * D + d] = f32_to_bf16(acc / L);
+}
+
+size_t paged_decode_smem_bytes(int D) {
+  return 1024 + (size_t)2 * kDecWaves * 16 * sizeof(float) +
+         (size_t)kDecWaves * 16 * D * sizeof(float);
+}
+
+void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
+                         const void* k_cache, const void* v_cache,
+                         const int* block_tables, int bt_stride,
+                         const int* context_lens, float* tmp_out, float* tmp_ml,
+                         int B, int nq, int nkv, int D, int block_size,
+                         int part_size, int max_parts, float scale,
+                         hipStream_t s) {
+  if (B <= 0) return;
+  dim3 grid(max_parts, nkv, B), block(256);
+  const size_t smem = paged_decode_smem_bytes(D);
+  auto* o = static_cast<unsigned short*>(out);
+  auto* qq = static_cast<const unsigned short*>(q);
+  auto* kc = static_cast<const unsigned short*>(k_cache);
+  auto* vc = static_cast<const unsigned short*>(v_cache);
+  if (D == 128) {
+    paged_decode_kernel<128><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, block_size, part_size, max_parts, scale);
+    if (max_parts > 1)
+      paged_decode_reduce_kernel<128><<<dim3(nq, B), dim3(128), 0, s>>>(o, out_stride, tmp_out, tmp_ml, context_lens, nq, part_size, max_parts);
+  } else {
+    paged_decode_kernel<64><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, block_size, part_size, max_parts, scale);
+    if (max_parts > 1)
+      paged_decode_reduce_kernel<64><<<dim3(nq, B), dim3(64), 0, s>>>(o, out_stride, tmp_out, tmp_ml, context_lens, nq, part_size, max_parts);
+  }
+}
+
+}  // namespace hipserve

@@ -1,0 +1,106 @@
+// RMSNorm and fused residual-add + RMSNorm.
+//
+// One 256-thread workgroup per token row; each lane owns VPT 16-byte vectors of
+// the row, held in registers between the sum-of-squares pass and the scale
+// pass, so the row is read from HBM exactly once and written once.
+// fp32 accumulation, bf16 I/O. Weight may be bf16 (HF checkpoints) or fp32
+// (GGUF stores norm weights as F32).
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+template <int VPT, bool kAdd, bool kWF32>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(
+    unsigned short* __restrict__ out, unsigned short* __restrict__ residual,
+    const unsigned short* __restrict__ x, const void* __restrict__ weight,
+    int hidden, long x_stride, long out_stride, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + row * x_stride);
+  u16x8* rr = kAdd ? reinterpret_cast<u16x8*>(residual + (long)row * hidden) : nullptr;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    if (idx < nvec) {
+      u16x8 a = xr[idx];
+      if constexpr (kAdd) {
+        u16x8 b = rr[idx];
+        u16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float f = bf16_to_f32(a[j]) + bf16_to_f32(b[j]);
+          s[j] = f32_to_bf16(f);
+          v[i][j] = bf16_to_f32(s[j]);  // normalise the bf16-rounded residual
+        }
+        rr[idx] = s;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf16_to_f32(a[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / hidden + eps);
+  u16x8* orow = reinterpret_cast<u16x8*>(out + row * out_stride);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    if (idx < nvec) {
+      float w[8];
+      if constexpr (kWF32) {
+        const f32x4* wp = reinterpret_cast<const f32x4*>(weight) + idx * 2;
+        f32x4 w0 = wp[0], w1 = wp[1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { w[j] = w0[j]; w[j + 4] = w1[j]; }
+      } else {
+        u16x8 wv = reinterpret_cast<const u16x8*>(weight)[idx];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = bf16_to_f32(wv[j]);
+      }
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv * w[j]);
+      orow[idx] = o;
+    }
+  }
+}
+
+template <bool kAdd, bool kWF32>
+static void launch_rmsnorm_t(unsigned short* out, unsigned short* residual,
+                             const unsigned short* x, const void* w, int rows,
+                             int hidden, long x_stride, long out_stride, float eps,
+                             hipStream_t s) {
+  const int nvec = hidden / 8;
+  dim3 grid(rows), block(256);
+  if (nvec <= 256)
+    rmsnorm_kernel<1, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+  else if (nvec <= 512)
+    rmsnorm_kernel<2, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+  else if (nvec <= 1024)
+    rmsnorm_kernel<4, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+  else
+    rmsnorm_kernel<8, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+}
+
+void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
+                    bool weight_f32, int rows, int hidden, long x_stride,
+                    long out_stride, float eps, hipStream_t s) {
+  auto* o = static_cast<unsigned short*>(out);
+  auto* r = static_cast<unsigned short*>(residual);
+  auto* xi = static_cast<const unsigned short*>(x);
+  if (residual) {
+    if (weight_f32) launch_rmsnorm_t<true, true>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
+    else launch_rmsnorm_t<true, false>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
+  } else {
+    if (weight_f32) launch_rmsnorm_t<false, true>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
+    else launch_rmsnorm_t<false, false>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
+  }
+}
+
+}  // namespace hipserve

@@ -1,0 +1,166 @@
+// torch.ops.hipserve.* — operator registration for the gfx950 kernel library.
+//
+// All ops write into caller-provided outputs (no allocation, no host sync), so
+// the decode step can be captured into a hipGraph by torch.cuda.CUDAGraph.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "hipserve/kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+
+#define CHECK_DEV(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_ROWMAJOR(x) TORCH_CHECK((x).stride(-1) == 1, #x " must have unit inner stride")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+
+void rmsnorm(at::Tensor& out, const at::Tensor& x, const at::Tensor& weight, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "rmsnorm expects 2-D [rows, hidden]");
+  const int hidden = x.size(1);
+  TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384, "hidden must be a multiple of 8, <= 16384");
+  TORCH_CHECK(weight.numel() == hidden && weight.is_contiguous());
+  TORCH_CHECK(weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_rmsnorm(out.data_ptr(), nullptr, x.data_ptr(), weight.data_ptr(),
+                           weight.scalar_type() == at::kFloat, x.size(0), hidden,
+                           x.stride(0), out.stride(0), (float)eps, cur_stream());
+}
+
+void fused_add_rmsnorm(at::Tensor& out, const at::Tensor& x, at::Tensor& residual,
+                       const at::Tensor& weight, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_BF16(residual);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out); CHECK_CONTIG(residual);
+  TORCH_CHECK(x.dim() == 2 && residual.sizes() == x.sizes());
+  const int hidden = x.size(1);
+  TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384);
+  TORCH_CHECK(weight.numel() == hidden && weight.is_contiguous());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_rmsnorm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), weight.data_ptr(),
+                           weight.scalar_type() == at::kFloat, x.size(0), hidden,
+                           x.stride(0), out.stride(0), (float)eps, cur_stream());
+}
+
+void silu_and_mul(at::Tensor& out, const at::Tensor& x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0));
+  TORCH_CHECK(out.size(1) % 8 == 0);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_silu_and_mul(out.data_ptr(), x.data_ptr(), x.size(0), out.size(1),
+                                x.stride(0), out.stride(0), cur_stream());
+}
+
+void rope_cache(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& slots,
+                const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
+                int64_t nq, int64_t nkv, int64_t head_dim, int64_t mode) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_ROWMAJOR(qkv);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= (nq + 2 * nkv) * head_dim);
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong);
+  TORCH_CHECK(positions.numel() >= qkv.size(0) && slots.numel() >= qkv.size(0));
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim && cos_sin.is_contiguous());
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim, "k_cache [blocks, nkv, bs, D]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == nkv && v_cache.size(2) == head_dim, "v_cache [blocks, nkv, D, bs]");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous());
+  TORCH_CHECK(head_dim % 16 == 0 && (mode == 0 || mode == 1));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  hipserve::launch_rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int64_t>(),
+                              slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                              k_cache.data_ptr(), v_cache.data_ptr(), qkv.size(0), nq, nkv,
+                              head_dim, k_cache.size(2), mode, cur_stream());
+}
+
+void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
+                  const at::Tensor& v_cache, const at::Tensor& block_tables,
+                  const at::Tensor& context_lens, at::Tensor& tmp_out, at::Tensor& tmp_ml,
+                  int64_t nq, int64_t nkv, int64_t part_size, double scale) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_ROWMAJOR(q); CHECK_ROWMAJOR(out);
+  const int D = k_cache.size(3), bs = k_cache.size(2);
+  TORCH_CHECK(D == 64 || D == 128, "paged_decode: head_dim 64/128");
+  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "paged_decode: GQA group <= 16");
+  TORCH_CHECK(bs % 16 == 0, "block_size multiple of 16");
+  TORCH_CHECK(part_size % 128 == 0 && part_size / bs < 255);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && context_lens.scalar_type() == at::kInt);
+  TORCH_CHECK(block_tables.stride(1) == 1);
+  const int B = q.size(0);
+  const int max_parts = tmp_ml.size(2);
+  TORCH_CHECK(tmp_out.is_contiguous() && tmp_ml.is_contiguous());
+  TORCH_CHECK(tmp_ml.dim() == 4 && tmp_ml.size(0) >= B && tmp_ml.size(1) == nq && tmp_ml.size(3) == 2);
+  TORCH_CHECK(tmp_out.dim() == 4 && tmp_out.size(2) == max_parts && tmp_out.size(3) == D);
+  TORCH_CHECK((long)max_parts * part_size >= (long)block_tables.size(1) * bs,
+              "workspace partitions must cover block_tables capacity");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  hipserve::launch_paged_decode(out.data_ptr(), out.stride(0), q.data_ptr(), q.stride(0),
+                                k_cache.data_ptr(), v_cache.data_ptr(),
+                                block_tables.data_ptr<int>(), block_tables.stride(0),
+                                context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
+                                tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size,
+                                max_parts, (float)scale, cur_stream());
+}
+
+void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
+                       const at::Tensor& v_cache, const at::Tensor& block_tables,
+                       const at::Tensor& cu_q, const at::Tensor& ctx_lens,
+                       const at::Tensor& tiles, int64_t nq, int64_t nkv, double scale) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_ROWMAJOR(q); CHECK_ROWMAJOR(out);
+  const int D = k_cache.size(3), bs = k_cache.size(2);
+  TORCH_CHECK(D == 64 || D == 128, "prefill_attention: head_dim 64/128");
+  TORCH_CHECK(bs % 16 == 0 && nq % nkv == 0);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && cu_q.scalar_type() == at::kInt &&
+              ctx_lens.scalar_type() == at::kInt && tiles.scalar_type() == at::kInt);
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 2 && tiles.is_contiguous());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  hipserve::launch_prefill_attention(out.data_ptr(), out.stride(0), q.data_ptr(), q.stride(0),
+                                     k_cache.data_ptr(), v_cache.data_ptr(),
+                                     block_tables.data_ptr<int>(), block_tables.stride(0),
+                                     cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(),
+                                     tiles.data_ptr<int>(), tiles.size(0), nq, nkv, D, bs,
+                                     (float)scale, cur_stream());
+}
+
+void sample(at::Tensor& out_tok, at::Tensor& out_lp, const at::Tensor& logits,
+            const at::Tensor& temperature, const at::Tensor& top_k, const at::Tensor& top_p,
+            const at::Tensor& seeds, const at::Tensor& steps) {
+  CHECK_DEV(logits); CHECK_ROWMAJOR(logits);
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat);
+  TORCH_CHECK(out_tok.scalar_type() == at::kLong && out_lp.scalar_type() == at::kFloat);
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat &&
+              top_k.scalar_type() == at::kInt && seeds.scalar_type() == at::kLong &&
+              steps.scalar_type() == at::kLong);
+  const int rows = logits.size(0);
+  TORCH_CHECK(out_tok.numel() >= rows && temperature.numel() >= rows && top_k.numel() >= rows &&
+              top_p.numel() >= rows && seeds.numel() >= rows && steps.numel() >= rows);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  hipserve::launch_sample(out_tok.data_ptr<int64_t>(), out_lp.numel() ? out_lp.data_ptr<float>() : nullptr,
+                          logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
+                          logits.stride(0), rows, logits.size(1), temperature.data_ptr<float>(),
+                          top_k.data_ptr<int>(), top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(),
+                          steps.data_ptr<int64_t>(), cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(hipserve, m) {
+  m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps) -> ()");
+  m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps) -> ()");
+  m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
+  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale) -> ()");
+  m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale) -> ()");
+  m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.impl("silu_and_mul", &silu_and_mul);
+  m.impl("rope_cache", &rope_cache);
+  m.impl("paged_decode", &paged_decode);
+  m.impl("prefill_attention", &prefill_attention);
+  m.impl("sample", &sample);
+}

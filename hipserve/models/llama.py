@@ -1,0 +1,241 @@
+"""Llama-family decoder (Llama-2/3, TinyLlama, Mistral-style GQA) and Mixtral MoE,
+written against the hipserve op set (SURVEY §3.F hot loop).
+
+Per layer: fused add+RMSNorm -> merged QKV GEMM (hipBLASLt) -> fused RoPE +
+paged-cache write -> paged attention (prefill and/or decode kernels) -> o_proj GEMM
+-> TP all-reduce -> fused add+RMSNorm -> merged gate/up GEMM -> SiLU*up ->
+down GEMM -> TP all-reduce. Weights are held as plain tensors already laid out
+for the kernels ([out, in] row-major, TP-sharded on load), no nn.Module tracing.
+
+The reference never contains model code — it runs `vllm/vllm-openai:v0.11.0`
+with `--tensor-parallel-size <gpuRequestCount>`
+(vllm-models/helm-chart/templates/model-deployments.yaml:26-39); this is the
+in-house replacement for that engine's model executor.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+from ..config import ModelConfig
+from ..ops import reference as ref
+from ..parallel.comm import TPGroup
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention metadata (prefill rows first, then decode rows)."""
+    num_prefill_tokens: int
+    num_decode: int
+    positions: torch.Tensor            # long [T]
+    slot_mapping: torch.Tensor         # long [T]
+    # prefill
+    bt_prefill: torch.Tensor | None = None   # int32 [np, max_blocks]
+    cu_q: torch.Tensor | None = None         # int32 [np+1]
+    ctx_prefill: torch.Tensor | None = None  # int32 [np]
+    tiles: torch.Tensor | None = None        # int32 [nt, 2]
+    # decode
+    bt_decode: torch.Tensor | None = None    # int32 [nd, max_blocks]
+    ctx_decode: torch.Tensor | None = None   # int32 [nd]
+    tmp_out: torch.Tensor | None = None
+    tmp_ml: torch.Tensor | None = None
+
+
+@dataclass
+class LayerWeights:
+    ln1: torch.Tensor
+    wqkv: torch.Tensor
+    wo: torch.Tensor
+    ln2: torch.Tensor
+    # dense MLP
+    wgu: torch.Tensor | None = None
+    wd: torch.Tensor | None = None
+    # MoE
+    router: torch.Tensor | None = None       # [E, H]
+    w13: torch.Tensor | None = None          # [E, 2*I/TP, H]
+    w2: torch.Tensor | None = None           # [E, H, I/TP]
+    quant: dict = field(default_factory=dict)  # GGUF-quantized GEMM weights by name
+
+
+def shard_sizes(cfg: ModelConfig, tp: int):
+    assert cfg.num_heads % tp == 0, f"num_heads {cfg.num_heads} not divisible by TP {tp}"
+    nq = cfg.num_heads // tp
+    if cfg.num_kv_heads >= tp:
+        assert cfg.num_kv_heads % tp == 0
+        nkv = cfg.num_kv_heads // tp
+    else:
+        assert tp % cfg.num_kv_heads == 0
+        nkv = 1  # kv heads replicated across ranks
+    assert cfg.intermediate_size % tp == 0
+    inter = cfg.intermediate_size // tp
+    vpad = (cfg.vocab_size + tp - 1) // tp
+    return nq, nkv, inter, vpad
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,
+                 max_pos: int | None = None):
+        self.cfg = cfg
+        self.tp = tp
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.ops = ops
+        self.nq, self.nkv, self.inter, self.vpad = shard_sizes(cfg, tp.world_size)
+        self.D = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.layers: list[LayerWeights] = []
+        self.embed: torch.Tensor | None = None
+        self.norm: torch.Tensor | None = None
+        self.lm_head: torch.Tensor | None = None
+        mp = max_pos or cfg.max_position_embeddings
+        self.cos_sin = ref.rope_cos_sin(self.D, mp, cfg.rope_theta, cfg.rope_scaling).to(self.device)
+        self.decode_partition = 512
+        self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
+
+    # ---------------------------------------------------------------- weights
+    def allocate_random(self, seed: int = 0, std: float = 0.02):
+        """Random-init weights directly on the device (synthetic benchmarks)."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed * 1000 + self.tp.rank)
+        H, D = cfg.hidden_size, self.D
+
+        def rnd(*shape):
+            return (torch.randn(*shape, generator=g, device=dev, dtype=torch.float32) * std).to(dt) \
+                if math.prod(shape) < (1 << 26) else _randn_chunked(shape, g, dev, dt, std)
+
+        self.embed = rnd(self.vpad, H)
+        self.norm = torch.ones(H, device=dev, dtype=dt)
+        self.lm_head = self.embed if cfg.tie_word_embeddings else rnd(self.vpad, H)
+        qkv_w = (self.nq + 2 * self.nkv) * D
+        self.layers = []
+        for _ in range(cfg.num_layers):
+            lw = LayerWeights(
+                ln1=torch.ones(H, device=dev, dtype=dt),
+                wqkv=rnd(qkv_w, H),
+                wo=rnd(H, self.nq * D),
+                ln2=torch.ones(H, device=dev, dtype=dt),
+            )
+            if cfg.num_experts:
+                E = cfg.num_experts
+                lw.router = rnd(E, H)
+                lw.w13 = rnd(E, 2 * self.inter, H)
+                lw.w2 = rnd(E, H, self.inter)
+            else:
+                lw.wgu = rnd(2 * self.inter, H)
+                lw.wd = rnd(H, self.inter)
+            self.layers.append(lw)
+
+    # ---------------------------------------------------------------- forward
+    def linear(self, x: torch.Tensor, w, name: str | None = None) -> torch.Tensor:
+        if isinstance(w, torch.Tensor):
+            return F.linear(x, w)
+        return self.quant_linear(x, w)
+
+    def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.tp.world_size == 1:
+            return F.embedding(ids, self.embed)
+        start = self.tp.rank * self.vpad
+        local = ids - start
+        mask = (local >= 0) & (local < self.vpad)
+        h = F.embedding(local.clamp(0, self.vpad - 1), self.embed)
+        h = h * mask.unsqueeze(-1).to(h.dtype)
+        return self.tp.all_reduce(h)
+
+    def forward(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        ops, cfg = self.ops, self.cfg
+        T = ids.shape[0]
+        H, D, nq, nkv = cfg.hidden_size, self.D, self.nq, self.nkv
+        eps = cfg.rms_norm_eps
+        Tp, Td = meta.num_prefill_tokens, meta.num_decode
+        h = self.embed_tokens(ids)
+        residual = torch.empty_like(h)
+        xn = torch.empty_like(h)
+        attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
+        for i, lw in enumerate(self.layers):
+            if i == 0:
+                residual.copy_(h)
+                ops.rmsnorm(xn, h, lw.ln1, eps)
+            else:
+                ops.fused_add_rmsnorm(xn, h, residual, lw.ln1, eps)
+            qkv = self.linear(xn, lw.wqkv)
+            kc, vc = kv_caches[i]
+            ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
+                           cfg.rope_mode)
+            if Tp:
+                ops.prefill_attention(attn[:Tp], qkv[:Tp], kc, vc, meta.bt_prefill, meta.cu_q,
+                                      meta.ctx_prefill, meta.tiles, nq, nkv, self.scale)
+            if Td:
+                ops.paged_decode(attn[Tp:], qkv[Tp:], kc, vc, meta.bt_decode, meta.ctx_decode,
+                                 meta.tmp_out, meta.tmp_ml, nq, nkv, self.decode_partition, self.scale)
+            o = self.linear(attn, lw.wo)
+            self.tp.all_reduce(o)
+            ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
+            if lw.router is not None:
+                h = self.moe(xn, lw)
+            else:
+                gu = self.linear(xn, lw.wgu)
+                act = torch.empty(T, self.inter, device=h.device, dtype=h.dtype)
+                ops.silu_and_mul(act, gu)
+                h = self.linear(act, lw.wd)
+            self.tp.all_reduce(h)
+        ops.fused_add_rmsnorm(xn, h, residual, self.norm, eps)
+        return xn
+
+    def moe(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
+        """Mixtral sparse MoE (top-k of E experts, renormalised softmax weights)."""
+        cfg = self.cfg
+        k = cfg.num_experts_per_tok
+        T = x.shape[0]
+        logits = F.linear(x, lw.router).float()
+        w, idx = torch.topk(torch.softmax(logits, dim=-1), k, dim=-1)
+        w = w / w.sum(-1, keepdim=True)
+        if hasattr(self.ops, "moe") and self.ops.name == "hip":
+            return self.ops.moe(x, lw.w13, lw.w2, w, idx, self.inter)
+        out = torch.zeros(T, cfg.hidden_size, device=x.device, dtype=torch.float32)
+        flat_idx = idx.reshape(-1)
+        flat_tok = torch.arange(T, device=x.device).repeat_interleave(k)
+        flat_w = w.reshape(-1)
+        order = torch.argsort(flat_idx)
+        counts = torch.bincount(flat_idx, minlength=cfg.num_experts).tolist()
+        start = 0
+        for e, n in enumerate(counts):
+            if n == 0:
+                continue
+            sel = order[start:start + n]
+            start += n
+            toks = flat_tok[sel]
+            gu = F.linear(x[toks], lw.w13[e])
+            act = torch.empty(n, self.inter, device=x.device, dtype=x.dtype)
+            self.ops.silu_and_mul(act, gu)
+            y = F.linear(act, lw.w2[e]).float() * flat_w[sel].unsqueeze(-1)
+            out.index_add_(0, toks, y)
+        return out.to(x.dtype)
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(hidden, self.lm_head)
+        logits = self.tp.all_gather_lastdim(logits)
+        return logits[:, : self.cfg.vocab_size]
+
+    # ---------------------------------------------------------------- kv cache
+    def kv_bytes_per_block(self, block_size: int) -> int:
+        return 2 * self.cfg.num_layers * self.nkv * block_size * self.D * torch.finfo(self.dtype).bits // 8
+
+    def allocate_kv_cache(self, num_blocks: int, block_size: int):
+        L = self.cfg.num_layers
+        k = torch.zeros(L, num_blocks, self.nkv, block_size, self.D, device=self.device, dtype=self.dtype)
+        v = torch.zeros(L, num_blocks, self.nkv, self.D, block_size, device=self.device, dtype=self.dtype)
+        return [(k[i], v[i]) for i in range(L)]
+
+
+def _randn_chunked(shape, g, dev, dt, std):
+    out = torch.empty(*shape, device=dev, dtype=dt)
+    flat = out.view(-1)
+    step = 1 << 26
+    for s in range(0, flat.numel(), step):
+        n = min(step, flat.numel() - s)
+        flat[s:s + n] = (torch.randn(n, generator=g, device=dev, dtype=torch.float32) * std).to(dt)
+    return out

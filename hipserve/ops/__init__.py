@@ -1,0 +1,144 @@
+"""hipserve op library.
+
+``KernelOps`` calls the hand-written gfx950 kernels in ``hipserve/_C.so``
+(``torch.ops.hipserve.*``). ``ReferenceOps`` is the plain-PyTorch oracle used by
+the CPU plumbing engine and by the numerics tests. The choice is made ONCE, when
+an engine is built for a device — never per call. On a GPU device the native
+library is mandatory: a missing/unloadable ``_C.so`` raises instead of silently
+falling back to PyTorch.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+from . import reference as ref
+
+_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+_lock = threading.Lock()
+_loaded = False
+
+
+def library_path() -> str:
+    return _LIB
+
+
+def load_library(build_if_missing: bool = False) -> str:
+    """Load hipserve/_C.so into torch.ops (idempotent). Raises if unavailable."""
+    global _loaded
+    with _lock:
+        if _loaded:
+            return _LIB
+        if not os.path.exists(_LIB) and build_if_missing:
+            from .._build import build_kernels
+
+            build_kernels()
+        if not os.path.exists(_LIB):
+            raise RuntimeError(
+                f"hipserve native kernels not built ({_LIB} missing): run `python -m hipserve._build`")
+        torch.ops.load_library(_LIB)
+        _loaded = True
+        return _LIB
+
+
+def native_available() -> bool:
+    try:
+        load_library()
+        return True
+    except Exception:
+        return False
+
+
+class KernelOps:
+    """gfx950 HIP kernels (all outputs written in place; graph-capturable)."""
+
+    name = "hip"
+
+    def __init__(self):
+        load_library()
+        self._op = torch.ops.hipserve
+
+    def rmsnorm(self, out, x, w, eps):
+        self._op.rmsnorm(out, x, w, eps)
+        return out
+
+    def fused_add_rmsnorm(self, out, x, residual, w, eps):
+        self._op.fused_add_rmsnorm(out, x, residual, w, eps)
+        return out
+
+    def silu_and_mul(self, out, x):
+        self._op.silu_and_mul(out, x)
+        return out
+
+    def rope_cache(self, qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode):
+        self._op.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
+
+    def paged_decode(self, out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
+                     nq, nkv, part_size, scale):
+        self._op.paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
+                              nq, nkv, part_size, scale)
+        return out
+
+    def prefill_attention(self, out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
+                          nq, nkv, scale):
+        self._op.prefill_attention(out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
+                                   nq, nkv, scale)
+        return out
+
+    def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
+        self._op.sample(out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps)
+
+
+class ReferenceOps:
+    """PyTorch reference path (CPU plumbing engine / numerics oracle)."""
+
+    name = "reference"
+
+    def rmsnorm(self, out, x, w, eps):
+        out.copy_(ref.rmsnorm(x, w, eps))
+        return out
+
+    def fused_add_rmsnorm(self, out, x, residual, w, eps):
+        y, r = ref.fused_add_rmsnorm(x, residual, w, eps)
+        residual.copy_(r)
+        out.copy_(y)
+        return out
+
+    def silu_and_mul(self, out, x):
+        out.copy_(ref.silu_and_mul(x))
+        return out
+
+    def rope_cache(self, qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode):
+        ref.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
+
+    def paged_decode(self, out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
+                     nq, nkv, part_size, scale):
+        B = context_lens.shape[0]
+        D = k_cache.shape[3]
+        out[:B, : nq * D].copy_(ref.paged_decode(q, k_cache, v_cache, block_tables, context_lens,
+                                                 nq, nkv, scale).view(B, nq * D))
+        return out
+
+    def prefill_attention(self, out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
+                          nq, nkv, scale):
+        D = k_cache.shape[3]
+        T = int(cu_q[-1])
+        out[:T, : nq * D].copy_(ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q,
+                                                      ctx_lens, nq, nkv, scale).view(T, nq * D))
+        return out
+
+    def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
+        t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps)
+        n = t.shape[0]
+        out_tok[:n].copy_(t)
+        if out_lp.numel():
+            out_lp[:n].copy_(lp)
+
+
+def get_ops(device: torch.device | str):
+    device = torch.device(device)
+    if device.type == "cuda":
+        return KernelOps()
+    return ReferenceOps()

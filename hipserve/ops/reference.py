@@ -1,0 +1,202 @@
+"""Plain-PyTorch fp32 reference implementations of every hipserve kernel.
+
+These are the numerics oracles for the gfx950 kernels (tests compare the HIP op
+against these) and the compute path of the CPU plumbing engine (tests/CI without
+a GPU). They use exactly the same tensor layouts as the kernels:
+
+* ``k_cache [num_blocks, nkv, block_size, D]``
+* ``v_cache [num_blocks, nkv, D, block_size]`` (transposed per block)
+* ``cos_sin [max_pos, D]`` = ``[cos(D/2) | sin(D/2)]`` fp32
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    inv = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * inv * w.float()).to(x.dtype)
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """Returns (normed, new_residual); residual is rounded to x.dtype first."""
+    r = (x.float() + residual.float()).to(x.dtype)
+    return rmsnorm(r, w, eps), r
+
+
+def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
+    inter = x.shape[-1] // 2
+    g, u = x[..., :inter].float(), x[..., inter:].float()
+    return (torch.nn.functional.silu(g) * u).to(x.dtype)
+
+
+def rope_cos_sin(head_dim: int, max_pos: int, theta: float, scaling: dict | None = None,
+                 rotary_dim: int | None = None) -> torch.Tensor:
+    """fp32 [max_pos, D] table = [cos | sin] with optional Llama-3 frequency scaling."""
+    rd = rotary_dim or head_dim
+    inv_freq = 1.0 / (theta ** (torch.arange(0, rd, 2, dtype=torch.float64) / rd))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv_freq
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > lo_wl, inv_freq / factor, inv_freq)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv_freq / factor + smooth * inv_freq, scaled)
+        inv_freq = scaled
+    elif scaling and scaling.get("rope_type", scaling.get("type")) == "linear":
+        inv_freq = inv_freq / scaling["factor"]
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv_freq)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float().contiguous()
+
+
+def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, mode: int) -> torch.Tensor:
+    """x [T, H, D] -> rotated (fp32 math, x.dtype out)."""
+    D = x.shape[-1]
+    half = D // 2
+    cs = cos_sin[pos.long()]  # [T, D]
+    c, s = cs[:, None, :half], cs[:, None, half:]
+    xf = x.float()
+    if mode == 0:
+        a, b = xf[..., :half], xf[..., half:]
+        out = torch.cat([a * c - b * s, b * c + a * s], dim=-1)
+    else:
+        a, b = xf[..., 0::2], xf[..., 1::2]
+        out = torch.stack([a * c - b * s, b * c + a * s], dim=-1).flatten(-2)
+    return out.to(x.dtype)
+
+
+def rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode):
+    """In-place: rotates q inside qkv, writes rotated k and raw v into the caches."""
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    q = qkv[:, : nq * D].view(T, nq, D)
+    k = qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
+    v = qkv[:, (nq + nkv) * D:(nq + 2 * nkv) * D].view(T, nkv, D)
+    q.copy_(apply_rope(q, positions[:T], cos_sin, mode))
+    kr = apply_rope(k, positions[:T], cos_sin, mode)
+    bs = k_cache.shape[2]
+    sl = slots[:T].long()
+    valid = sl >= 0
+    if valid.any():
+        sv = sl[valid]
+        blk, off = sv // bs, sv % bs
+        k_cache[blk, :, off, :] = kr[valid].to(k_cache.dtype)
+        v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
+
+
+def _gather_kv(k_cache, v_cache, block_table, n):
+    bs = k_cache.shape[2]
+    idx = torch.arange(n, device=k_cache.device)
+    blk = block_table[(idx // bs)].long()
+    off = idx % bs
+    k = k_cache[blk, :, off, :]          # [n, nkv, D]
+    v = v_cache[blk, :, :, off]          # [n, nkv, D]
+    return k, v
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nq, nkv, scale):
+    """q [B, nq*D (+extra)] -> out [B, nq, D] (fp32 math)."""
+    D = k_cache.shape[3]
+    B = context_lens.shape[0]
+    G = nq // nkv
+    out = torch.empty(B, nq, D, dtype=q.dtype, device=q.device)
+    for b in range(B):
+        n = int(context_lens[b])
+        k, v = _gather_kv(k_cache, v_cache, block_tables[b], n)
+        qb = q[b, : nq * D].view(nq, D).float()
+        kf = k.float().repeat_interleave(G, dim=1)  # [n, nq, D]
+        vf = v.float().repeat_interleave(G, dim=1)
+        s = torch.einsum("hd,nhd->hn", qb, kf) * scale
+        p = torch.softmax(s, dim=-1)
+        out[b] = torch.einsum("hn,nhd->hd", p, vf).to(q.dtype)
+    return out
+
+
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nq, nkv, scale):
+    """q [T, nq*D (+extra)] -> out [T, nq, D]; causal over absolute positions."""
+    D = k_cache.shape[3]
+    G = nq // nkv
+    T = int(cu_q[-1])
+    out = torch.empty(T, nq, D, dtype=q.dtype, device=q.device)
+    for s_ in range(len(ctx_lens)):
+        q0, q1 = int(cu_q[s_]), int(cu_q[s_ + 1])
+        ql, ctx = q1 - q0, int(ctx_lens[s_])
+        if ql == 0:
+            continue
+        k, v = _gather_kv(k_cache, v_cache, block_tables[s_], ctx)
+        qs = q[q0:q1, : nq * D].view(ql, nq, D).float()
+        kf = k.float().repeat_interleave(G, dim=1)
+        vf = v.float().repeat_interleave(G, dim=1)
+        s = torch.einsum("qhd,nhd->hqn", qs, kf) * scale
+        qpos = torch.arange(ctx - ql, ctx, device=q.device)[:, None]
+        kpos = torch.arange(ctx, device=q.device)[None, :]
+        s = s.masked_fill((kpos > qpos)[None], float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        out[q0:q1] = torch.einsum("hqn,nhd->qhd", p, vf).to(q.dtype)
+    return out
+
+
+# ---- sampling: the same counter-based RNG as csrc/kernels/sampling.hip ----
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def uniform01(seed: int, step: int, n: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint64) + np.uint64(1)
+        x = (np.uint64(seed & 0xFFFFFFFFFFFFFFFF) * np.uint64(0x9E3779B97F4A7C15)) ^ (
+            (np.uint64(step & 0xFFFFFFFFFFFFFFFF) + np.uint64(0xD1B54A32D192ED03)) * np.uint64(0xBF58476D1CE4E5B9)
+        ) ^ (i * np.uint64(0x94D049BB133111EB))
+        x ^= x >> np.uint64(31)
+        x *= np.uint64(0x7FB5D329728EA185)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x81DADEF4BC2DD44D)
+        x ^= x >> np.uint64(33)
+        u = ((x >> np.uint64(40)).astype(np.float64) + 0.5) / 16777216.0
+    return u.astype(np.float32)
+
+
+def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, steps):
+    """Returns (tokens int64 [B], logprobs f32 [B]) with the kernel's semantics:
+    greedy if T<=1e-5; else top-k then top-p (on the top-k-renormalised mass) then
+    a Gumbel-max draw with u = hash(seed, step, index)."""
+    B, V = logits.shape
+    toks = torch.empty(B, dtype=torch.long)
+    lps = torch.empty(B, dtype=torch.float32)
+    lf = logits.float().cpu()
+    for r in range(B):
+        x = lf[r]
+        lse = torch.logsumexp(x, 0)
+        t = float(temperature[r])
+        if not t > 1e-5:
+            i = int(torch.argmax(x))
+            toks[r], lps[r] = i, float(x[i] - lse)
+            continue
+        keep = torch.ones(V, dtype=torch.bool)
+        k = int(top_k[r])
+        if 0 < k < V:
+            kth = torch.topk(x, k).values[-1]
+            keep &= x >= kth
+        p = float(top_p[r])
+        if p < 1.0:
+            w = torch.exp((x - x.max()) / t) * keep
+            order = torch.argsort(x, descending=True)
+            cum = torch.cumsum(w[order].double(), 0)
+            target = p * float(cum[-1])
+            n = int(torch.searchsorted(cum, torch.tensor([target], dtype=torch.float64))[0])
+            thr = x[order[min(n, V - 1)]]
+            keep &= x >= thr
+        u = torch.from_numpy(uniform01(int(seeds[r]), int(steps[r]), V))
+        g = (x - x.max()) / t - torch.log(-torch.log(u))
+        g = torch.where(keep, g, torch.full_like(g, float("-inf")))
+        i = int(torch.argmax(g))
+        toks[r], lps[r] = i, float(x[i] - lse)
+    return toks, lps

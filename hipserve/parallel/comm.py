@@ -1,0 +1,102 @@
+"""Tensor-parallel communication (SURVEY §2.D, C1–C4).
+
+One process per GPU (SPMD). ``TPGroup`` wraps a ``torch.distributed`` process
+group: backend ``nccl`` on ROCm *is* RCCL, which runs its rings over the xGMI
+point-to-point links of an 8xMI355X node; ``gloo`` is used for the CPU tests.
+
+Collectives on the hot path:
+  * ``all_reduce``  — sum after the row-parallel o_proj / down_proj (2 per layer)
+    and after the vocab-parallel embedding;
+  * ``all_gather``  — LM-head logits shards -> full vocab on every rank;
+  * ``broadcast_obj`` — step metadata from the rank-0 scheduler to workers.
+All ops are in place / into preallocated outputs so decode steps are capturable
+into hipGraphs (RCCL collectives are graph-capturable on ROCm).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class TPGroup:
+    def __init__(self, rank: int = 0, world_size: int = 1, group=None, device=None):
+        self.rank = rank
+        self.world_size = world_size
+        self.group = group
+        self.device = device
+        self._cpu_group = None
+
+    @property
+    def is_first(self):
+        return self.rank == 0
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world_size > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_lastdim(self, t: torch.Tensor) -> torch.Tensor:
+        """[n, V/TP] on every rank -> [n, V] on every rank."""
+        if self.world_size == 1:
+            return t
+        parts = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(parts, t.contiguous(), group=self.group)
+        return parts.permute(1, 0, 2).reshape(t.shape[0], -1)
+
+    def broadcast_obj(self, obj=None):
+        """Rank 0 -> all ranks over the CPU (gloo) group; returns the object."""
+        if self.world_size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=0, group=self._cpu_group)
+        return lst[0]
+
+    def barrier(self):
+        if self.world_size > 1:
+            dist.barrier(group=self._cpu_group)
+
+
+_TP: TPGroup | None = None
+
+
+def init_tp(world_size: int | None = None, backend: str | None = None, device_type: str = "cuda") -> TPGroup:
+    """Initialise the TP group from torchrun-style env vars (RANK/WORLD_SIZE/
+    MASTER_ADDR/MASTER_PORT). world_size 1 needs no process group."""
+    global _TP
+    ws = world_size if world_size is not None else int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if ws == 1:
+        dev = torch.device(device_type, int(os.environ.get("LOCAL_RANK", "0"))) if device_type == "cuda" else torch.device("cpu")
+        _TP = TPGroup(0, 1, None, dev)
+        return _TP
+    if backend is None:
+        backend = "nccl" if device_type == "cuda" else "gloo"
+    if device_type == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", rank))
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws,
+                                timeout=datetime.timedelta(seconds=600))
+    g = TPGroup(rank, ws, dist.group.WORLD, dev)
+    g._cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
+    _TP = g
+    return g
+
+
+def get_tp() -> TPGroup:
+    global _TP
+    if _TP is None:
+        _TP = TPGroup()
+    return _TP
+
+
+def set_tp(g: TPGroup):
+    global _TP
+    _TP = g

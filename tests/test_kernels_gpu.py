@@ -1,0 +1,169 @@
+"""Numerics of every gfx950 kernel against the fp32 PyTorch reference."""
+import math
+
+import pytest
+import torch
+
+from hipserve.ops import KernelOps
+from hipserve.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    return KernelOps()
+
+
+def _close(a, b, atol, rtol=0.0, frac=1.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    bad = (a - b).abs() > (atol + rtol * b.abs())
+    assert bad.float().mean().item() <= 1.0 - frac, f"max err {(a - b).abs().max().item()}"
+
+
+@pytest.mark.parametrize("rows,hidden", [(7, 4096), (33, 8192), (3, 2048), (1, 64)])
+@pytest.mark.parametrize("wf32", [False, True])
+def test_rmsnorm(ops, rows, hidden, wf32):
+    torch.manual_seed(0)
+    x = torch.randn(rows, hidden, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(hidden, device=DEV, dtype=torch.float32 if wf32 else torch.bfloat16)
+    out = torch.empty_like(x)
+    ops.rmsnorm(out, x, w, 1e-5)
+    _close(out, ref.rmsnorm(x.cpu(), w.cpu(), 1e-5), atol=2e-2, rtol=1e-2)
+    # fused add
+    r = torch.randn_like(x)
+    r_ref = r.clone().cpu()
+    ops.fused_add_rmsnorm(out, x, r, w, 1e-5)
+    y_ref, rr = ref.fused_add_rmsnorm(x.cpu(), r_ref, w.cpu(), 1e-5)
+    _close(r, rr, atol=1e-6)
+    _close(out, y_ref, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("rows,inter", [(5, 14336), (64, 1792), (1, 8)])
+def test_silu_and_mul(ops, rows, inter):
+    x = torch.randn(rows, 2 * inter, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty(rows, inter, device=DEV, dtype=torch.bfloat16)
+    ops.silu_and_mul(out, x)
+    _close(out, ref.silu_and_mul(x.cpu()), atol=1e-2, rtol=1e-2)
+
+
+def _caches(nblocks, nkv, bs, D, fill=True):
+    kc = torch.randn(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16) if fill else \
+        torch.zeros(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(nblocks, nkv, D, bs, device=DEV, dtype=torch.bfloat16) if fill else \
+        torch.zeros(nblocks, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+    return kc, vc
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("bs", [16, 32])
+def test_rope_cache(ops, mode, bs):
+    torch.manual_seed(1)
+    T, nq, nkv, D = 37, 32, 8, 128
+    qkv = torch.randn(T, (nq + 2 * nkv) * D + 64, device=DEV, dtype=torch.bfloat16)[:, : (nq + 2 * nkv) * D]
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    slots = torch.randperm(64 * bs, device=DEV)[:T]
+    slots[3] = -1
+    cs = ref.rope_cos_sin(D, 4096, 500000.0).to(DEV)
+    kc, vc = _caches(64, nkv, bs, D, fill=False)
+    kc_r, vc_r, qkv_r = kc.cpu().clone(), vc.cpu().clone(), qkv.cpu().clone()
+    ops.rope_cache(qkv, pos, slots, cs, kc, vc, nq, nkv, D, mode)
+    ref.rope_cache(qkv_r, pos.cpu(), slots.cpu(), cs.cpu(), kc_r, vc_r, nq, nkv, D, mode)
+    _close(qkv[:, : nq * D], qkv_r[:, : nq * D], atol=2e-2, rtol=1e-2)
+    _close(kc, kc_r, atol=2e-2, rtol=1e-2)
+    _close(vc, vc_r, atol=0)
+
+
+@pytest.mark.parametrize("nq,nkv,D", [(32, 8, 128), (64, 8, 128), (32, 32, 64), (32, 4, 64)])
+@pytest.mark.parametrize("bs", [16, 32])
+def test_paged_decode(ops, nq, nkv, D, bs):
+    torch.manual_seed(2)
+    ctx = [1, 17, 100, 600, 1300, 512, 33]
+    B = len(ctx)
+    max_blocks = 96
+    nblocks = B * max_blocks
+    kc, vc = _caches(nblocks, nkv, bs, D)
+    perm = torch.randperm(nblocks, device=DEV).int()
+    bt = perm.view(B, max_blocks).contiguous()
+    cl = torch.tensor(ctx, device=DEV, dtype=torch.int32)
+    q = torch.randn(B, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    part = 512
+    max_parts = math.ceil(max_blocks * bs / part)
+    tmp_out = torch.empty(B, nq, max_parts, D, device=DEV, dtype=torch.float32)
+    tmp_ml = torch.empty(B, nq, max_parts, 2, device=DEV, dtype=torch.float32)
+    out = torch.zeros(B, nq * D, device=DEV, dtype=torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    ops.paged_decode(out, q, kc, vc, bt, cl, tmp_out, tmp_ml, nq, nkv, part, scale)
+    want = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), nq, nkv, scale)
+    _close(out.view(B, nq, D), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv,D", [(32, 8, 128), (16, 2, 64)])
+def test_prefill_attention(ops, nq, nkv, D):
+    torch.manual_seed(3)
+    bs = 16
+    # (ctx_len, q_len): plain prefill, tiny, chunked prefill with prefix context
+    seqs = [(1, 1), (37, 37), (200, 200), (300, 50), (129, 129)]
+    max_blocks = 32
+    nblocks = len(seqs) * max_blocks
+    kc, vc = _caches(nblocks, nkv, bs, D)
+    bt = torch.randperm(nblocks, device=DEV).int().view(len(seqs), max_blocks).contiguous()
+    cu = [0]
+    tiles = []
+    for i, (c, ql) in enumerate(seqs):
+        for r in range(0, ql, 128):
+            tiles.append((i, r))
+        cu.append(cu[-1] + ql)
+    T = cu[-1]
+    q = torch.randn(T, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16) * 2
+    cu_t = torch.tensor(cu, device=DEV, dtype=torch.int32)
+    ctx_t = torch.tensor([c for c, _ in seqs], device=DEV, dtype=torch.int32)
+    tiles_t = torch.tensor(tiles, device=DEV, dtype=torch.int32)
+    out = torch.zeros(T, nq * D, device=DEV, dtype=torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    ops.prefill_attention(out, q, kc, vc, bt, cu_t, ctx_t, tiles_t, nq, nkv, scale)
+    want = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(), nq, nkv, scale)
+    _close(out.view(T, nq, D), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sample(ops, dtype):
+    torch.manual_seed(4)
+    B, V = 12, 32000
+    logits = (torch.randn(B, V, device=DEV) * 3).to(dtype)
+    temp = torch.tensor([0.0, 1.0, 0.7, 1.0, 1.3, 0.9, 1.0, 0.5, 1.0, 2.0, 0.0, 1.0], device=DEV)
+    top_k = torch.tensor([0, 0, 50, 1, 0, 20, 0, 0, 1000, 5, 0, 7], device=DEV, dtype=torch.int32)
+    top_p = torch.tensor([1.0, 1.0, 1.0, 1.0, 0.9, 0.5, 0.1, 0.95, 0.8, 1.0, 1.0, 0.3], device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.long) * 7919 + 1
+    steps = torch.arange(B, device=DEV, dtype=torch.long)
+    tok = torch.empty(B, device=DEV, dtype=torch.long)
+    lp = torch.empty(B, device=DEV, dtype=torch.float32)
+    ops.sample(tok, lp, logits, temp, top_k, top_p, seeds, steps)
+    rt, rlp = ref.sample(logits.cpu(), temp.cpu(), top_k.cpu(), top_p.cpu(), seeds.cpu(), steps.cpu())
+    mism = (tok.cpu() != rt).sum().item()
+    assert mism <= 1, (tok.cpu(), rt)
+    ok = tok.cpu() == rt
+    assert torch.allclose(lp.cpu()[ok], rlp[ok], atol=1e-3)
+    # greedy rows must be exact
+    assert tok[0].item() == int(logits[0].float().argmax())
+    assert tok[3].item() == int(logits[3].float().argmax())  # top_k = 1
+
+
+def test_sample_distribution(ops):
+    """Empirical frequencies follow softmax(x/T) restricted to top-k."""
+    V, N = 16, 4096
+    base = torch.linspace(-2, 2, V)
+    logits = base.repeat(N, 1).to(DEV)
+    temp = torch.full((N,), 1.0, device=DEV)
+    top_k = torch.full((N,), 8, device=DEV, dtype=torch.int32)
+    top_p = torch.ones(N, device=DEV)
+    seeds = torch.arange(N, device=DEV, dtype=torch.long)
+    steps = torch.zeros(N, device=DEV, dtype=torch.long)
+    tok = torch.empty(N, device=DEV, dtype=torch.long)
+    lp = torch.empty(N, device=DEV)
+    ops.sample(tok, lp, logits, temp, top_k, top_p, seeds, steps)
+    cnt = torch.bincount(tok.cpu(), minlength=V).float() / N
+    p = torch.softmax(base[8:], 0)
+    assert cnt[:8].sum() == 0
+    assert (cnt[8:] - p).abs().max() < 0.03
