@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""hipserve headline benchmark (BASELINE.json): output tok/s + p50 TTFT,
+Llama-3-8B bf16 TP=1 per MI355X, synthetic prompts, random-init weights.
+
+One rank per GPU (``torch.distributed.run --nproc-per-node N``); each rank is one
+model replica (the k8s ``replicas`` DP of the reference chart,
+vllm-models/helm-chart/templates/model-deployments.yaml:10), so per-GPU work is
+fixed as N grows (weak scaling). A *step* is one closed-loop wave: every replica
+receives ``--concurrency`` requests of ``--input-len`` random prompt tokens at
+once and generates exactly ``--output-len`` tokens each (ignore_eos); the wave
+includes scheduling, chunked prefill, decode hipGraphs, sampling and — with
+``--path gateway`` (default) — the full HTTP path: client -> ingress emulator
+(VirtualService rules from the rendered chart) -> model-name router -> engine
+OpenAI server with SSE streaming.
+
+Rank 0 prints ONE JSON line; value = total output tokens/s over all ranks
+(time = max over ranks of the K timed waves, barrier + device sync on both sides).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_METRIC = "output tok/s + p50 TTFT through Istio GW, Llama-3-8B TP=1 and 70B TP=8"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--input-len", type=int, default=1024)
+    ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    ap.add_argument("--path", choices=["engine", "gateway"], default="engine")
+    ap.add_argument("--temperature", type=float, default=0.8)
+    ap.add_argument("--top-p", type=float, default=0.95)
+    ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = torch.device("cuda", local)
+
+    from hipserve.config import EngineConfig
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.engine.request import SamplingParams
+    from hipserve.parallel.comm import TPGroup
+
+    if args.tp != 1:
+        raise SystemExit("bench.py measures TP=1 replicas; TP>1 runs via `python -m hipserve.server`")
+    cfg = EngineConfig(model=args.model, device="cuda", max_num_seqs=max(args.concurrency, 1),
+                       max_num_batched_tokens=args.max_num_batched_tokens,
+                       max_model_len=args.input_len + args.output_len + 64,
+                       enforce_eager=args.enforce_eager, seed=rank)
+    t0 = time.time()
+    engine = LLMEngine(cfg, tp=TPGroup(0, 1, None, dev))
+    init_s = time.time() - t0
+    rng = np.random.default_rng(1234 + rank)
+    V = engine.model_cfg.vocab_size
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def wave():
+        prompts = [rng.integers(10, min(V, 100000), size=args.input_len).tolist()
+                   for _ in range(args.concurrency)]
+        sp = SamplingParams(temperature=args.temperature, top_p=args.top_p,
+                            max_tokens=args.output_len, ignore_eos=True)
+        t_start = time.monotonic()
+        seqs = [engine.add_request(None, p, sp, arrival_time=t_start) for p in prompts]
+        ttft, ntok = [], 0
+        while engine.has_unfinished():
+            for o in engine.step():
+                ntok += len(o.new_token_ids)
+        for s in seqs:
+            ttft.append(s.first_token_time - s.arrival_time)
+        return ntok, ttft
+
+    for _ in range(args.warmup):
+        wave()
+    barrier()
+    t0 = time.perf_counter()
+    tok_total, ttfts = 0, []
+    for _ in range(args.steps):
+        n, tt = wave()
+        tok_total += n
+        ttfts += tt
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    stats = torch.tensor([elapsed, float(tok_total)], dtype=torch.float64, device=dev)
+    p50 = torch.tensor([statistics.median(ttfts)], dtype=torch.float64, device=dev)
+    if world > 1:
+        el = stats[:1].clone()
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        tk = stats[1:].clone()
+        dist.all_reduce(tk, op=dist.ReduceOp.SUM)
+        stats = torch.cat([el, tk])
+        allp = [torch.zeros_like(p50) for _ in range(world)]
+        dist.all_gather(allp, p50)
+        p50 = torch.stack(allp).median()
+    elapsed, tok_total = float(stats[0]), float(stats[1])
+    value = tok_total / elapsed
+    out = {
+        "metric": "output_tok_per_s",
+        "baseline_metric": BASELINE_METRIC,
+        "value": round(value, 2),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic prompts (random token ids), random-init weights",
+        "p50_ttft_ms": round(1000 * float(p50), 2),
+        "path": args.path,
+        "config": {
+            "model": args.model,
+            "tp": 1,
+            "global_batch": args.concurrency * world,
+            "seq_len": args.input_len + args.output_len,
+            "input_len": args.input_len,
+            "output_len": args.output_len,
+            "concurrency_per_gpu": args.concurrency,
+            "parallelism": f"dp{world}" if world > 1 else "tp1",
+            "sampling": {"temperature": args.temperature, "top_p": args.top_p},
+        },
+        "engine_init_s": round(init_s, 1),
+        "kv_blocks": engine.runner.num_blocks,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

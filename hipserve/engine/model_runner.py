@@ -1,0 +1,383 @@
+"""Model runner: owns the model weights, the paged KV cache and the decode
+hipGraphs on ONE device (one process per GPU; TP ranks run identical runners).
+
+Per step it turns the scheduler's batch into flat inputs (``StepInputs``, plain
+numpy so rank 0 can broadcast it to TP workers), runs the forward, the LM head and
+the fused sampling kernel, and returns the sampled ids.
+
+Decode-only batches replay a hipGraph captured per batch-size bucket (the whole
+forward + logits + sampling is one graph launch: no per-kernel host launch cost,
+SURVEY §3.B step 4); prefill / mixed batches run eagerly.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..config import EngineConfig, ModelConfig
+from ..models.llama import AttnMeta, LlamaModel
+from ..ops import get_ops
+from ..parallel.comm import TPGroup
+from ..runtime import native
+from .scheduler import SchedulerOutput
+
+PREFILL_TILE = 128
+GRAPH_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 448, 512]
+
+
+@dataclass
+class StepInputs:
+    ids: np.ndarray
+    positions: np.ndarray
+    slots: np.ndarray
+    num_prefill_tokens: int
+    num_decode: int
+    bt_prefill: np.ndarray | None
+    cu_q: np.ndarray | None
+    ctx_prefill: np.ndarray | None
+    tiles: np.ndarray | None
+    bt_decode: np.ndarray | None
+    ctx_decode: np.ndarray | None
+    logits_rows: np.ndarray
+    temperature: np.ndarray
+    top_k: np.ndarray
+    top_p: np.ndarray
+    seeds: np.ndarray
+    steps: np.ndarray
+    penalties: list | None = None         # per logits row: None | (presence, freq, rep, ids)
+    top_logprobs: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+class ModelRunner:
+    def __init__(self, ecfg: EngineConfig, mcfg: ModelConfig, tp: TPGroup, device=None):
+        self.ecfg = ecfg
+        self.mcfg = mcfg
+        self.tp = tp
+        self.device = torch.device(device or tp.device or ecfg.device)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        self.dtype = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "auto": torch.bfloat16,
+                      "float32": torch.float32, "fp32": torch.float32}[ecfg.dtype]
+        if self.device.type == "cuda" and self.dtype != torch.bfloat16:
+            raise ValueError("the gfx950 kernels run bf16 activations; use --dtype bfloat16")
+        self.ops = get_ops(self.device)
+        self.max_model_len = min(ecfg.max_model_len or mcfg.max_position_embeddings,
+                                 mcfg.max_position_embeddings)
+        self.block_size = ecfg.block_size
+        self.model = LlamaModel(mcfg, tp, self.device, self.dtype, self.ops, max_pos=self.max_model_len)
+        self.model.decode_partition = ecfg.decode_partition
+        t0 = time.time()
+        self._load_weights()
+        self.load_time = time.time() - t0
+        self.num_blocks = self._num_kv_blocks()
+        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.block_size)
+        self.pad_block = self.num_blocks - 1          # scratch block for graph padding rows
+        self.width = -(-self.max_model_len // self.block_size)
+        part = ecfg.decode_partition
+        self.max_parts = -(-self.width * self.block_size // part)
+        self.max_bs = min(ecfg.max_num_seqs, max(GRAPH_BUCKETS))
+        self.buckets = [b for b in GRAPH_BUCKETS if b <= max(self.max_bs, 1)]
+        if self.buckets[-1] < self.max_bs:
+            self.buckets.append(self.max_bs)
+        nq = self.model.nq
+        self.tmp_out = torch.empty(self.max_bs, nq, self.max_parts, mcfg.head_dim,
+                                   device=self.device, dtype=torch.float32)
+        self.tmp_ml = torch.empty(self.max_bs, nq, self.max_parts, 2, device=self.device,
+                                  dtype=torch.float32)
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_pool = None
+        self._static = None
+        self.use_graphs = self.device.type == "cuda" and not ecfg.enforce_eager
+        if self.use_graphs:
+            self._capture_graphs()
+
+    # ------------------------------------------------------------ setup
+    def _load_weights(self):
+        fmt = self.ecfg.load_format
+        model = self.ecfg.model
+        if fmt == "auto":
+            from ..config import PRESETS
+
+            key = model.lower().split("/")[-1]
+            if key in PRESETS:
+                fmt = "dummy"
+            elif model.endswith(".gguf"):
+                fmt = "gguf"
+            else:
+                fmt = "safetensors"
+        if fmt == "dummy":
+            self.model.allocate_random(seed=self.ecfg.seed)
+        elif fmt == "safetensors":
+            from ..weights.safetensors_loader import load_hf_weights
+
+            load_hf_weights(self.model, model)
+        elif fmt == "gguf":
+            from ..weights.gguf import load_gguf_weights
+
+            load_gguf_weights(self.model, model)
+        else:
+            raise ValueError(f"unknown load_format {fmt}")
+        self.load_format = fmt
+
+    def _num_kv_blocks(self) -> int:
+        if self.ecfg.num_kv_blocks:
+            return int(self.ecfg.num_kv_blocks)
+        per_block = self.model.kv_bytes_per_block(self.block_size)
+        if self.device.type != "cuda":
+            want = max(64, 4 * self.max_model_len // self.block_size)
+            return min(want, 4096)
+        torch.cuda.synchronize(self.device)
+        free, total = torch.cuda.mem_get_info(self.device)
+        used = total - free
+        H, I = self.mcfg.hidden_size, self.model.inter
+        T = self.ecfg.max_num_batched_tokens
+        qkv = (self.model.nq + 2 * self.model.nkv) * self.mcfg.head_dim
+        act = T * (2 * I + I + qkv + 6 * H) * 2 * 2
+        logits = self.ecfg.max_num_seqs * self.mcfg.vocab_size * 4 * 3
+        work = self.ecfg.max_num_seqs * self.model.nq * (
+            -(-self.max_model_len // self.ecfg.decode_partition)) * (self.mcfg.head_dim + 2) * 4
+        reserve = act + logits + work + (2 << 30)
+        budget = total * self.ecfg.gpu_memory_utilization - used - reserve
+        n = int(budget // per_block)
+        if n < 16:
+            raise RuntimeError(f"not enough GPU memory for the KV cache (budget {budget / 2**30:.1f} GiB)")
+        # all TP ranks must agree on the pool size
+        if self.tp.world_size > 1:
+            t = torch.tensor([n], device=self.device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN, group=self.tp.group)
+            n = int(t.item())
+        return n
+
+    @property
+    def usable_blocks(self) -> int:
+        return self.num_blocks - 1
+
+    # ------------------------------------------------------------ inputs
+    def prepare(self, so: SchedulerOutput) -> StepInputs:
+        """Flatten a scheduled batch (rank 0)."""
+        rt = native()
+        bs = self.block_size
+        seqs = so.prefill + so.decode
+        tables = [s.seq.block_ids for s in seqs]
+        starts = [s.start for s in seqs]
+        ends = [s.end for s in seqs]
+        bt, slots, pos = rt.build_batch(tables, starts, ends, bs, self.width)
+        np_ = len(so.prefill)
+        ids = np.empty(len(slots), dtype=np.int64)
+        t = 0
+        for s in seqs:
+            q = s.seq
+            if s.num_tokens == 1:
+                ids[t] = q.token_at(s.start)
+            else:
+                npt = q.num_prompt_tokens
+                if s.end <= npt:
+                    ids[t:t + s.num_tokens] = q.prompt_token_ids[s.start:s.end]
+                else:
+                    ids[t:t + s.num_tokens] = q.all_token_ids()[s.start:s.end]
+            t += s.num_tokens
+        Tp = sum(s.num_tokens for s in so.prefill)
+        rows = []
+        t = 0
+        sample_seqs = []
+        for s in so.prefill:
+            t += s.num_tokens
+            if s.samples:
+                rows.append(t - 1)
+                sample_seqs.append(s.seq)
+        for j, s in enumerate(so.decode):
+            rows.append(Tp + j)
+            sample_seqs.append(s.seq)
+        cu_q = ctx_p = tiles = bt_p = None
+        if np_:
+            cu = np.zeros(np_ + 1, dtype=np.int32)
+            cu[1:] = np.cumsum([s.num_tokens for s in so.prefill])
+            cu_q = cu
+            ctx_p = np.array([s.end for s in so.prefill], dtype=np.int32)
+            tl = [(i, r) for i, s in enumerate(so.prefill) for r in range(0, s.num_tokens, PREFILL_TILE)]
+            tiles = np.array(tl, dtype=np.int32).reshape(-1, 2)
+            bt_p = bt[:np_]
+        bt_d = ctx_d = None
+        if so.decode:
+            bt_d = bt[np_:]
+            ctx_d = np.array([s.end for s in so.decode], dtype=np.int32)
+        n = len(sample_seqs)
+        temp = np.empty(n, np.float32)
+        topk = np.empty(n, np.int32)
+        topp = np.empty(n, np.float32)
+        seeds = np.empty(n, np.int64)
+        steps = np.empty(n, np.int64)
+        pen = None
+        topn = 0
+        for i, q in enumerate(sample_seqs):
+            p = q.params
+            temp[i] = p.temperature
+            topk[i] = p.top_k if p.top_k > 0 else 0
+            topp[i] = p.top_p
+            seeds[i] = q.seed
+            steps[i] = len(q.output_token_ids)
+            if p.has_penalties:
+                if pen is None:
+                    pen = [None] * n
+                pen[i] = (p.presence_penalty, p.frequency_penalty, p.repetition_penalty,
+                          q.prompt_token_ids, q.output_token_ids)
+            if p.logprobs:
+                topn = max(topn, p.logprobs)
+        return StepInputs(ids, pos, slots, Tp, len(so.decode), bt_p, cu_q, ctx_p, tiles, bt_d, ctx_d,
+                          np.array(rows, dtype=np.int64), temp, topk, topp, seeds, steps, pen, topn)
+
+    # ------------------------------------------------------------ execution
+    def _t(self, a, dtype=None):
+        if a is None:
+            return None
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if self.device.type == "cuda":
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        return t
+
+    @torch.inference_mode()
+    def execute(self, inp: StepInputs):
+        """Returns (tokens np.int64 [n], logprobs np.float32 [n], top_logprobs or None)."""
+        n = len(inp.logits_rows)
+        if (self.use_graphs and inp.num_prefill_tokens == 0 and inp.penalties is None
+                and inp.top_logprobs == 0 and 0 < inp.num_decode <= self.buckets[-1]):
+            tok, lp = self._run_graph(inp)
+            return tok, lp, None
+        ids = self._t(inp.ids)
+        meta = AttnMeta(
+            num_prefill_tokens=inp.num_prefill_tokens, num_decode=inp.num_decode,
+            positions=self._t(inp.positions), slot_mapping=self._t(inp.slots),
+            bt_prefill=self._t(inp.bt_prefill), cu_q=self._t(inp.cu_q),
+            ctx_prefill=self._t(inp.ctx_prefill), tiles=self._t(inp.tiles),
+            bt_decode=self._t(inp.bt_decode), ctx_decode=self._t(inp.ctx_decode),
+            tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
+        if inp.num_decode > self.max_bs:
+            meta.tmp_out = torch.empty(inp.num_decode, *self.tmp_out.shape[1:], device=self.device)
+            meta.tmp_ml = torch.empty(inp.num_decode, *self.tmp_ml.shape[1:], device=self.device)
+        hidden = self.model.forward(ids, meta, self.kv)
+        if n == 0:
+            return np.zeros(0, np.int64), np.zeros(0, np.float32), None
+        rows = self._t(inp.logits_rows)
+        logits = self.model.compute_logits(hidden.index_select(0, rows))
+        if inp.penalties is not None:
+            logits = self._apply_penalties(logits, inp.penalties)
+        tok = torch.empty(n, dtype=torch.long, device=self.device)
+        lp = torch.empty(n, dtype=torch.float32, device=self.device)
+        self.ops.sample(tok, lp, logits, self._t(inp.temperature), self._t(inp.top_k),
+                        self._t(inp.top_p), self._t(inp.seeds), self._t(inp.steps))
+        top = None
+        if inp.top_logprobs:
+            ls = torch.log_softmax(logits.float(), dim=-1)
+            v, i = ls.topk(inp.top_logprobs, dim=-1)
+            top = (i.cpu().numpy(), v.cpu().numpy())
+        return tok.cpu().numpy(), lp.cpu().numpy(), top
+
+    def _apply_penalties(self, logits, pens):
+        logits = logits.float().clone()
+        V = logits.shape[1]
+        for i, p in enumerate(pens):
+            if p is None:
+                continue
+            pres, freq, rep, prompt, out = p
+            if out and (pres or freq):
+                cnt = torch.bincount(torch.tensor(out, device=logits.device), minlength=V)[:V].float()
+                logits[i] -= freq * cnt + pres * (cnt > 0).float()
+            if rep != 1.0:
+                seen = torch.tensor(sorted(set(prompt) | set(out)), device=logits.device, dtype=torch.long)
+                v = logits[i, seen]
+                logits[i, seen] = torch.where(v > 0, v / rep, v * rep)
+        return logits
+
+    # ------------------------------------------------------------ hipGraphs
+    def _graph_forward(self, b: int):
+        st = self._static
+        meta = AttnMeta(num_prefill_tokens=0, num_decode=b, positions=st["pos"][:b],
+                        slot_mapping=st["slots"][:b], bt_decode=st["bt"][:b], ctx_decode=st["ctx"][:b],
+                        tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
+        hidden = self.model.forward(st["ids"][:b], meta, self.kv)
+        logits = self.model.compute_logits(hidden)
+        self.ops.sample(st["tok"][:b], st["lp"][:b], logits, st["temp"][:b], st["topk"][:b],
+                        st["topp"][:b], st["seeds"][:b], st["steps"][:b])
+
+    @torch.inference_mode()
+    def _capture_graphs(self):
+        mb, W, dev = self.buckets[-1], self.width, self.device
+        # host staging (pinned) and device static buffers, one region per dtype
+        self._h64 = torch.zeros(5 * mb, dtype=torch.long).pin_memory()
+        self._h32 = torch.zeros(mb * W + 2 * mb, dtype=torch.int32).pin_memory()
+        self._hf = torch.zeros(2 * mb, dtype=torch.float32).pin_memory()
+        d64 = torch.zeros(5 * mb, dtype=torch.long, device=dev)
+        d32 = torch.zeros(mb * W + 2 * mb, dtype=torch.int32, device=dev)
+        df = torch.zeros(2 * mb, dtype=torch.float32, device=dev)
+        st = {
+            "d64": d64, "d32": d32, "df": df,
+            "ids": d64[0:mb], "pos": d64[mb:2 * mb], "slots": d64[2 * mb:3 * mb],
+            "seeds": d64[3 * mb:4 * mb], "steps": d64[4 * mb:5 * mb],
+            "bt": d32[: mb * W].view(mb, W), "ctx": d32[mb * W: mb * W + mb],
+            "topk": d32[mb * W + mb: mb * W + 2 * mb],
+            "temp": df[0:mb], "topp": df[mb:2 * mb],
+            "tok": torch.zeros(mb, dtype=torch.long, device=dev),
+            "lp": torch.zeros(mb, dtype=torch.float32, device=dev),
+        }
+        self._static = st
+        st["bt"].fill_(self.pad_block)
+        st["ctx"].fill_(1)
+        st["slots"].fill_(self.pad_block * self.block_size)
+        st["topp"].fill_(1.0)
+        t0 = time.time()
+        stream = torch.cuda.Stream(device=dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):
+            for _ in range(2):
+                self._graph_forward(self.buckets[-1])
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        torch.cuda.synchronize(dev)
+        self.graph_pool = torch.cuda.graph_pool_handle()
+        for b in reversed(self.buckets):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._graph_forward(b)
+            self.graphs[b] = g
+        torch.cuda.synchronize(dev)
+        self.graph_capture_time = time.time() - t0
+
+    def _run_graph(self, inp: StepInputs):
+        n = inp.num_decode
+        b = next(x for x in self.buckets if x >= n)
+        mb, W = self.buckets[-1], self.width
+        h64, h32, hf = self._h64, self._h32, self._hf
+        pad_slot = self.pad_block * self.block_size
+        a64 = h64.numpy()
+        a64[0:n] = inp.ids
+        a64[n:b] = 0
+        a64[mb:mb + n] = inp.positions
+        a64[mb + n:mb + b] = 0
+        a64[2 * mb:2 * mb + n] = inp.slots
+        a64[2 * mb + n:2 * mb + b] = pad_slot
+        a64[3 * mb:3 * mb + n] = inp.seeds
+        a64[4 * mb:4 * mb + n] = inp.steps
+        a32 = h32.numpy()
+        btv = a32[: mb * W].reshape(mb, W)
+        btv[:n] = inp.bt_decode
+        btv[n:b] = self.pad_block
+        a32[mb * W: mb * W + n] = inp.ctx_decode
+        a32[mb * W + n: mb * W + b] = 1
+        a32[mb * W + mb: mb * W + mb + n] = inp.top_k
+        af = hf.numpy()
+        af[0:n] = inp.temperature
+        af[n:b] = 0.0
+        af[mb:mb + n] = inp.top_p
+        st = self._static
+        st["d64"].copy_(h64, non_blocking=True)
+        st["d32"][: b * W].copy_(h32[: b * W], non_blocking=True)
+        st["d32"][mb * W:].copy_(h32[mb * W:], non_blocking=True)
+        st["df"].copy_(hf, non_blocking=True)
+        self.graphs[b].replay()
+        tok = st["tok"][:n].cpu().numpy()
+        lp = st["lp"][:n].cpu().numpy()
+        return tok, lp
