@@ -1,0 +1,133 @@
+"""Asyncio front of the engine: the engine loop runs in its own thread (GPU work
+is launched from there, the GIL is released while the device runs), the HTTP
+side submits requests and receives per-step output batches through
+``loop.call_soon_threadsafe`` — one cross-thread hop per engine step, not per
+token."""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+import traceback
+
+from ..engine.llm_engine import LLMEngine
+from ..engine.request import RequestOutput, SamplingParams
+
+log = logging.getLogger("hipserve.engine")
+
+
+class EngineDeadError(RuntimeError):
+    pass
+
+
+class AsyncEngine:
+    def __init__(self, engine: LLMEngine, loop: asyncio.AbstractEventLoop | None = None):
+        self.engine = engine
+        self.loop = loop
+        self._submit: queue.SimpleQueue = queue.SimpleQueue()
+        self._wake = threading.Event()
+        self._queues: dict[str, asyncio.Queue] = {}
+        self._stop = False
+        self.error: BaseException | None = None
+        self.thread: threading.Thread | None = None
+        self.heartbeat = time.monotonic()
+        self.steps = 0
+
+    def start(self, loop: asyncio.AbstractEventLoop | None = None):
+        self.loop = loop or asyncio.get_event_loop()
+        self.thread = threading.Thread(target=self._run, name="hipserve-engine", daemon=True)
+        self.thread.start()
+
+    def stop(self):
+        self._stop = True
+        self._wake.set()
+        if self.thread:
+            self.thread.join(timeout=10)
+
+    @property
+    def alive(self) -> bool:
+        return self.thread is not None and self.thread.is_alive() and self.error is None
+
+    # ------------------------------------------------------------ engine thread
+    def _run(self):
+        eng = self.engine
+        try:
+            while not self._stop:
+                self.heartbeat = time.monotonic()
+                self._drain()
+                if not eng.has_unfinished():
+                    self._wake.wait(timeout=0.5)
+                    self._wake.clear()
+                    continue
+                outs = eng.step()
+                self.steps += 1
+                if outs:
+                    self.loop.call_soon_threadsafe(self._dispatch, outs)
+        except BaseException as e:  # surface to /health and every waiter
+            self.error = e
+            log.error("engine loop died: %s", traceback.format_exc())
+            self.loop.call_soon_threadsafe(self._fail_all, e)
+
+    def _drain(self):
+        while True:
+            try:
+                kind, args = self._submit.get_nowait()
+            except queue.Empty:
+                return
+            if kind == "add":
+                rid, prompt, params, arrival = args
+                try:
+                    self.engine.add_request(rid, prompt, params, arrival_time=arrival)
+                except Exception as e:  # validation errors go back to the request
+                    self.loop.call_soon_threadsafe(self._deliver_error, rid, e)
+            elif kind == "abort":
+                self.engine.abort(args)
+
+    # ------------------------------------------------------------ loop side
+    def _dispatch(self, outs: list[RequestOutput]):
+        for o in outs:
+            q = self._queues.get(o.request_id)
+            if q is not None:
+                q.put_nowait(o)
+                if o.finished:
+                    self._queues.pop(o.request_id, None)
+
+    def _deliver_error(self, rid, e):
+        q = self._queues.pop(rid, None)
+        if q is not None:
+            q.put_nowait(e)
+
+    def _fail_all(self, e):
+        for q in self._queues.values():
+            q.put_nowait(EngineDeadError(str(e)))
+        self._queues.clear()
+
+    async def generate(self, request_id: str, prompt, params: SamplingParams):
+        """Async iterator of RequestOutput deltas for one request."""
+        if self.error is not None:
+            raise EngineDeadError(str(self.error))
+        q: asyncio.Queue = asyncio.Queue()
+        self._queues[request_id] = q
+        self._submit.put(("add", (request_id, prompt, params, time.monotonic())))
+        self._wake.set()
+        try:
+            while True:
+                o = await q.get()
+                if isinstance(o, BaseException):
+                    raise o
+                yield o
+                if o.finished:
+                    return
+        except (asyncio.CancelledError, GeneratorExit):
+            self.abort(request_id)
+            raise
+        finally:
+            self._queues.pop(request_id, None)
+
+    def abort(self, request_id: str):
+        if request_id in self._queues:
+            self._queues.pop(request_id, None)
+        self._submit.put(("abort", request_id))
+        self._wake.set()
