@@ -1,0 +1,136 @@
+"""OpenAI API of the engine pod, alone and behind ingress -> router (CPU tiny model)."""
+import asyncio
+import json
+
+import aiohttp
+import pytest
+from aiohttp import web
+
+from hipserve.config import EngineConfig
+from hipserve.engine.llm_engine import LLMEngine
+from hipserve.gateway.ingress import IngressEmulator, load_rules
+from hipserve.gateway.router import ModelRouter
+from hipserve.parallel.comm import TPGroup
+from hipserve.server.api_server import OpenAIServer
+from hipserve.server.async_engine import AsyncEngine
+
+from .test_gateway import VS
+
+
+async def start_engine_server(name="tiny", model="tiny-llama"):
+    eng = LLMEngine(EngineConfig(model=model, served_model_name=name, device="cpu", dtype="float32",
+                                 max_num_seqs=8, max_num_batched_tokens=64, num_kv_blocks=256,
+                                 max_model_len=512), tp=TPGroup())
+    ae = AsyncEngine(eng)
+    ae.start(asyncio.get_running_loop())
+    srv = OpenAIServer(ae, name, eng.max_model_len)
+    runner = web.AppRunner(srv.app())
+    await runner.setup()
+    site = web.TCPSite(runner, "127.0.0.1", 0)
+    await site.start()
+    port = site._server.sockets[0].getsockname()[1]
+    return ae, runner, port
+
+
+async def sse_events(resp):
+    out = []
+    async for line in resp.content:
+        line = line.strip()
+        if line.startswith(b"data: "):
+            d = line[6:]
+            if d == b"[DONE]":
+                out.append("[DONE]")
+            else:
+                out.append(json.loads(d))
+    return out
+
+
+def test_openai_endpoints():
+    async def main():
+        ae, runner, port = await start_engine_server()
+        base = f"http://127.0.0.1:{port}"
+        async with aiohttp.ClientSession() as s:
+            assert (await s.get(base + "/health")).status == 200
+            j = await (await s.get(base + "/v1/models")).json()
+            assert j["data"][0]["id"] == "tiny"
+            # completions: text prompt, non-streaming
+            r = await s.post(base + "/v1/completions", json={"model": "tiny", "prompt": "hello",
+                                                             "max_tokens": 5, "temperature": 0})
+            j = await r.json()
+            assert r.status == 200, j
+            assert j["object"] == "text_completion" and j["usage"]["completion_tokens"] <= 5
+            # token-id prompt, streaming, with usage
+            r = await s.post(base + "/v1/completions", json={
+                "model": "tiny", "prompt": [1, 5, 6, 7], "max_tokens": 6, "stream": True,
+                "ignore_eos": True, "temperature": 0, "stream_options": {"include_usage": True}})
+            ev = await sse_events(r)
+            assert ev[-1] == "[DONE]"
+            assert ev[-2]["usage"]["completion_tokens"] == 6
+            fin = [e for e in ev[:-2] if e["choices"][0]["finish_reason"]]
+            assert fin and fin[-1]["choices"][0]["finish_reason"] == "length"
+            # chat streaming
+            r = await s.post(base + "/v1/chat/completions", json={
+                "model": "tiny", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 4,
+                "stream": True, "ignore_eos": True})
+            ev = await sse_events(r)
+            assert ev[0]["choices"][0]["delta"]["role"] == "assistant"
+            assert ev[-1] == "[DONE]"
+            # chat non-streaming with n=2
+            r = await s.post(base + "/v1/chat/completions", json={
+                "model": "tiny", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3,
+                "n": 2, "ignore_eos": True})
+            j = await r.json()
+            assert len(j["choices"]) == 2 and j["choices"][0]["message"]["role"] == "assistant"
+            # errors: unknown model (404), bad body (400), too long prompt (400)
+            r = await s.post(base + "/v1/completions", json={"model": "other", "prompt": "x"})
+            assert r.status == 404
+            r = await s.post(base + "/v1/completions", data=b"{")
+            assert r.status == 400
+            r = await s.post(base + "/v1/completions", json={"prompt": [3] * 600})
+            assert r.status == 400
+            # tokenize + metrics
+            j = await (await s.post(base + "/tokenize", json={"prompt": "ab"})).json()
+            assert j["count"] == 3
+            m = await (await s.get(base + "/metrics")).text()
+            assert "hipserve_generation_tokens" in m
+        ae.stop()
+        await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_full_path_ingress_router_two_models():
+    """client -> ingress (VirtualService rules) -> router (body.model) -> engine pods."""
+    async def main():
+        ae1, r1, p1 = await start_engine_server("llama", "tiny-llama")
+        ae2, r2, p2 = await start_engine_server("mixtral", "tiny-mixtral")
+        router = ModelRouter([("llama", [f"127.0.0.1:{p1}"]), ("mixtral", [f"127.0.0.1:{p2}"])])
+        await router.start("127.0.0.1", 0)
+        ing = IngressEmulator(load_rules(VS), {"api-gateway": ("127.0.0.1", router.port)})
+        await ing.start("127.0.0.1", 0)
+        base = f"http://127.0.0.1:{ing.port}"
+        async with aiohttp.ClientSession() as s:
+            j = await (await s.get(base + "/v1/models")).json()
+            assert [m["id"] for m in j["data"]] == ["llama", "mixtral"]
+            for name in ("llama", "mixtral"):
+                r = await s.post(base + "/v1/chat/completions", json={
+                    "model": name, "messages": [{"role": "user", "content": "hey"}],
+                    "max_tokens": 5, "stream": True, "ignore_eos": True})
+                ev = await sse_events(r)
+                assert ev[-1] == "[DONE]" and ev[0]["model"] == name
+            # concurrent streams through the whole path
+            async def one(i):
+                r = await s.post(base + "/v1/completions", json={
+                    "model": "llama", "prompt": [1, i + 3, 7], "max_tokens": 8, "stream": True,
+                    "ignore_eos": True})
+                ev = await sse_events(r)
+                return sum(1 for e in ev if e != "[DONE]" and e["choices"])
+            counts = await asyncio.gather(*[one(i) for i in range(12)])
+            assert all(c == 8 for c in counts)
+        for x in (ing, router):
+            await x.stop()
+        for ae, rr in ((ae1, r1), (ae2, r2)):
+            ae.stop()
+            await rr.cleanup()
+
+    asyncio.run(main())
