@@ -76,6 +76,9 @@ def backends_from_env(env: dict | None = None) -> list[tuple[str, list[str]]]:
     renders it from .Values.models, like the reference's BACKENDS dict)."""
     env = env or os.environ
     raw = env.get("HIPSERVE_BACKENDS")
+    if not raw and env.get("HIPSERVE_BACKENDS_FILE"):
+        with open(env["HIPSERVE_BACKENDS_FILE"]) as f:
+            raw = f.read()
     if not raw:
         return []
     out = []
