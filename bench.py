@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--input-len", type=int, default=1024)
     ap.add_argument("--output-len", type=int, default=256)
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
-    ap.add_argument("--path", choices=["engine", "gateway"], default="engine")
+    ap.add_argument("--path", choices=["engine", "gateway"], default="gateway")
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
     ap.add_argument("--enforce-eager", action="store_true")
@@ -59,6 +59,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    stack = lg = None
+    if args.path == "gateway":
+        # client-side processes start BEFORE this process touches the GPU
+        from hipserve.bench.local_stack import GatewayStack, LoadgenProc, free_port, wait_http
+
+        eport = free_port()
+        stack = GatewayStack({args.model: [eport]}).start()
+        lg = LoadgenProc()
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -88,20 +98,36 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def wave():
-        prompts = [rng.integers(10, min(V, 100000), size=args.input_len).tolist()
-                   for _ in range(args.concurrency)]
-        sp = SamplingParams(temperature=args.temperature, top_p=args.top_p,
-                            max_tokens=args.output_len, ignore_eos=True)
-        t_start = time.monotonic()
-        seqs = [engine.add_request(None, p, sp, arrival_time=t_start) for p in prompts]
-        ttft, ntok = [], 0
-        while engine.has_unfinished():
-            for o in engine.step():
-                ntok += len(o.new_token_ids)
-        for s in seqs:
-            ttft.append(s.first_token_time - s.arrival_time)
-        return ntok, ttft
+    if args.path == "gateway":
+        import asyncio
+        import threading
+
+        from hipserve.server.api_server import serve
+
+        def run_server():
+            asyncio.run(serve(engine, "127.0.0.1", eport, args.model))
+
+        threading.Thread(target=run_server, name="http", daemon=True).start()
+        wait_http(f"http://127.0.0.1:{eport}/health", 120)
+
+        def wave():
+            res = lg.wave(url=stack.url, model=args.model, concurrency=args.concurrency,
+                          input_len=args.input_len, output_len=args.output_len,
+                          vocab=min(V, 100000), temperature=args.temperature, top_p=args.top_p)
+            return sum(r["tokens"] for r in res), [r["ttft"] for r in res]
+    else:
+        def wave():
+            prompts = [rng.integers(10, min(V, 100000), size=args.input_len).tolist()
+                       for _ in range(args.concurrency)]
+            sp = SamplingParams(temperature=args.temperature, top_p=args.top_p,
+                                max_tokens=args.output_len, ignore_eos=True)
+            t_start = time.monotonic()
+            seqs = [engine.add_request(None, p, sp, arrival_time=t_start) for p in prompts]
+            ntok = 0
+            while engine.has_unfinished():
+                for o in engine.step():
+                    ntok += len(o.new_token_ids)
+            return ntok, [s.first_token_time - s.arrival_time for s in seqs]
 
     for _ in range(args.warmup):
         wave()
@@ -129,7 +155,7 @@ def main():
     elapsed, tok_total = float(stats[0]), float(stats[1])
     value = tok_total / elapsed
     out = {
-        "metric": "output_tok_per_s",
+        "metric": "output tok/s through gateway (p50 TTFT reported)" if args.path == "gateway" else "output tok/s (engine, no HTTP)",
         "baseline_metric": BASELINE_METRIC,
         "value": round(value, 2),
         "unit": "tokens/s",
@@ -158,6 +184,9 @@ def main():
         "engine_init_s": round(init_s, 1),
         "kv_blocks": engine.runner.num_blocks,
     }
+    if lg is not None:
+        lg.close()
+        stack.stop()
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

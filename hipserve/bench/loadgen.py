@@ -1,0 +1,168 @@
+"""OpenAI streaming load generator: output tok/s, TTFT, ITL
+measured client-side, i.e. through whatever sits in front of the engine
+(ingress emulator -> router -> engine, or a real Istio gateway URL).
+
+Closed-loop "waves": ``concurrency`` requests sent at once, each a synthetic
+prompt of ``input_len`` random token ids asking for exactly ``output_len`` tokens
+(``ignore_eos``). CLI: ``python -m hipserve.bench.loadgen --url http://host:port``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import random
+import statistics
+import time
+
+import aiohttp
+
+
+async def one_request(session, url, model, prompt, output_len, temperature, top_p, seed=None):
+    body = {"model": model, "prompt": prompt, "max_tokens": output_len, "stream": True,
+            "ignore_eos": True, "temperature": temperature, "top_p": top_p,
+            "stream_options": {"include_usage": True}}
+    if seed is not None:
+        body["seed"] = seed
+    t0 = time.perf_counter()
+    ttft = None
+    last = t0
+    itls = []
+    ntok = 0
+    usage = None
+    async with session.post(url + "/v1/completions", json=body) as r:
+        if r.status != 200:
+            raise RuntimeError(f"HTTP {r.status}: {(await r.text())[:300]}")
+        buf = b""
+        async for chunk in r.content.iter_any():
+            buf += chunk
+            while b"\n\n" in buf:
+                ev, buf = buf.split(b"\n\n", 1)
+                if not ev.startswith(b"data: "):
+                    continue
+                data = ev[6:]
+                if data == b"[DONE]":
+                    continue
+                j = json.loads(data)
+                if j.get("usage"):
+                    usage = j["usage"]
+                if j.get("choices"):
+                    now = time.perf_counter()
+                    if ttft is None:
+                        ttft = now - t0
+                    else:
+                        itls.append(now - last)
+                    last = now
+                    ntok += 1
+    n = usage["completion_tokens"] if usage else ntok
+    return {"ttft": ttft, "tokens": n, "latency": time.perf_counter() - t0, "itl": itls}
+
+
+async def wave(url, model, concurrency, input_len, output_len, vocab, temperature=0.8, top_p=0.95,
+               rng=None, session=None):
+    rng = rng or random.Random(0)
+    prompts = [[rng.randrange(10, vocab) for _ in range(input_len)] for _ in range(concurrency)]
+    own = session is None
+    if own:
+        session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
+                                        connector=aiohttp.TCPConnector(limit=0))
+    try:
+        res = await asyncio.gather(*[one_request(session, url, model, p, output_len, temperature, top_p)
+                                     for p in prompts])
+    finally:
+        if own:
+            await session.close()
+    return res
+
+
+def summarize(results, elapsed):
+    toks = sum(r["tokens"] for r in results)
+    ttfts = sorted(r["ttft"] for r in results if r["ttft"] is not None)
+    itls = sorted(x for r in results for x in r["itl"])
+    pct = lambda xs, q: xs[min(len(xs) - 1, int(q * len(xs)))] if xs else None  # noqa: E731
+    return {"requests": len(results), "output_tokens": toks, "elapsed_s": elapsed,
+            "output_tok_per_s": toks / elapsed if elapsed > 0 else 0.0,
+            "p50_ttft_ms": 1000 * statistics.median(ttfts) if ttfts else None,
+            "p90_ttft_ms": 1000 * pct(ttfts, 0.9) if ttfts else None,
+            "p50_itl_ms": 1000 * statistics.median(itls) if itls else None,
+            "p90_itl_ms": 1000 * pct(itls, 0.9) if itls else None}
+
+
+async def run(url, model, concurrency, input_len, output_len, vocab, waves, warmup, **kw):
+    rng = random.Random(1234)
+    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
+                                     connector=aiohttp.TCPConnector(limit=0)) as s:
+        for _ in range(warmup):
+            await wave(url, model, concurrency, input_len, output_len, vocab, rng=rng, session=s, **kw)
+        t0 = time.perf_counter()
+        res = []
+        for _ in range(waves):
+            res += await wave(url, model, concurrency, input_len, output_len, vocab, rng=rng, session=s, **kw)
+        return summarize(res, time.perf_counter() - t0)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", required=True)
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--input-len", type=int, default=1024)
+    ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--waves", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args(argv)
+
+    async def go():
+        model = a.model
+        if model is None:
+            async with aiohttp.ClientSession() as s:
+                j = await (await s.get(a.url + "/v1/models")).json()
+                model = j["data"][0]["id"]
+        return await run(a.url, model, a.concurrency, a.input_len, a.output_len, a.vocab, a.waves, a.warmup)
+
+    print(json.dumps(asyncio.run(go())))
+
+
+
+
+def serve_stdio():
+    """Line-oriented JSON command loop (used by bench.py so the client runs in its
+    own process and never competes with the engine for the GIL)."""
+    import sys
+
+    loop = asyncio.new_event_loop()
+    session = None
+    rng = random.Random(1234)
+    for line in sys.stdin:
+        cmd = json.loads(line)
+        if cmd["op"] == "quit":
+            break
+        if session is None:
+            async def mk():
+                return aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
+                                             connector=aiohttp.TCPConnector(limit=0))
+            session = loop.run_until_complete(mk())
+        if cmd["op"] == "wave":
+            t0 = time.perf_counter()
+            try:
+                res = loop.run_until_complete(wave(cmd["url"], cmd["model"], cmd["concurrency"],
+                                                   cmd["input_len"], cmd["output_len"], cmd["vocab"],
+                                                   cmd.get("temperature", 0.8), cmd.get("top_p", 0.95),
+                                                   rng=rng, session=session))
+                out = {"ok": True, "results": res, "elapsed": time.perf_counter() - t0}
+            except Exception as e:
+                out = {"ok": False, "error": repr(e)}
+            sys.stdout.write(json.dumps(out) + "\n")
+            sys.stdout.flush()
+    if session is not None:
+        loop.run_until_complete(session.close())
+
+
+if __name__ == "__main__":
+    import sys as _sys
+
+    if "--serve" in _sys.argv:
+        serve_stdio()
+    else:
+        main()
