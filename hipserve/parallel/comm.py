@@ -42,8 +42,13 @@ class TPGroup:
         """[n, V/TP] on every rank -> [n, V] on every rank."""
         if self.world_size == 1:
             return t
+        t = t.contiguous()
+        if t.device.type == "cpu":  # gloo: list form
+            parts = [torch.empty_like(t) for _ in range(self.world_size)]
+            dist.all_gather(parts, t, group=self.group)
+            return torch.cat(parts, dim=-1)
         parts = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(parts, t.contiguous(), group=self.group)
+        dist.all_gather_into_tensor(parts, t, group=self.group)
         return parts.permute(1, 0, 2).reshape(t.shape[0], -1)
 
     def broadcast_obj(self, obj=None):
