@@ -146,22 +146,30 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nq, nkv
 
 
 # ---- sampling: the same counter-based RNG as csrc/kernels/sampling.hip ----
-_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def row_key(seed: int, step: int) -> int:
+    M = (1 << 64) - 1
+    x = ((seed & M) * 0x9E3779B97F4A7C15 & M) ^ (((step & M) + 0xD1B54A32D192ED03) & M) * 0xBF58476D1CE4E5B9 & M
+    x ^= x >> 31
+    x = x * 0x7FB5D329728EA185 & M
+    x ^= x >> 27
+    x = x * 0x81DADEF4BC2DD44D & M
+    x ^= x >> 33
+    return (x ^ (x >> 32)) & 0xFFFFFFFF
 
 
 def uniform01(seed: int, step: int, n: int) -> np.ndarray:
+    key = np.uint32(row_key(seed, step))
     with np.errstate(over="ignore"):
-        i = np.arange(n, dtype=np.uint64) + np.uint64(1)
-        x = (np.uint64(seed & 0xFFFFFFFFFFFFFFFF) * np.uint64(0x9E3779B97F4A7C15)) ^ (
-            (np.uint64(step & 0xFFFFFFFFFFFFFFFF) + np.uint64(0xD1B54A32D192ED03)) * np.uint64(0xBF58476D1CE4E5B9)
-        ) ^ (i * np.uint64(0x94D049BB133111EB))
-        x ^= x >> np.uint64(31)
-        x *= np.uint64(0x7FB5D329728EA185)
-        x ^= x >> np.uint64(27)
-        x *= np.uint64(0x81DADEF4BC2DD44D)
-        x ^= x >> np.uint64(33)
-        u = ((x >> np.uint64(40)).astype(np.float64) + 0.5) / 16777216.0
-    return u.astype(np.float32)
+        i = np.arange(n, dtype=np.uint32)
+        h = key ^ (i * np.uint32(0x9E3779B9) + np.uint32(0x7F4A7C15))
+        h ^= h >> np.uint32(16)
+        h *= np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h *= np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+    return (((h >> np.uint32(8)).astype(np.float64) + 0.5) / 16777216.0).astype(np.float32)
 
 
 def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, steps):
@@ -171,7 +179,8 @@ def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, steps):
     B, V = logits.shape
     toks = torch.empty(B, dtype=torch.long)
     lps = torch.empty(B, dtype=torch.float32)
-    lf = logits.float().cpu()
+    # the kernel holds the row as bf16 in registers: sample on bf16-rounded logits
+    lf = logits.float().cpu().to(torch.bfloat16).float()
     for r in range(B):
         x = lf[r]
         lse = torch.logsumexp(x, 0)

@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Micro-benchmarks of individual hipserve kernels on the GPU (HIP-event timing,
+median of N launches). Prints one JSON line per case.
+
+    python tools/bench_ops.py [sample|decode|prefill|gemm|norm|all]
+"""
+import json
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from hipserve.ops import KernelOps  # noqa: E402
+
+DEV = "cuda"
+
+
+def timeit(fn, n=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    evs = []
+    for _ in range(n):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) * 1000 for a, b in evs)
+    return ts[len(ts) // 2]
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def bench_sample(ops):
+    for V, B in [(128256, 64), (128256, 256), (32000, 64), (128256, 1)]:
+        logits = (torch.randn(B, V, device=DEV) * 3).to(torch.bfloat16)
+        tok = torch.empty(B, dtype=torch.long, device=DEV)
+        lp = torch.empty(B, device=DEV)
+        for name, t, k, p in [("greedy", 0.0, 0, 1.0), ("temp", 0.8, 0, 1.0), ("top_p", 0.8, 0, 0.95),
+                              ("top_k_p", 0.8, 50, 0.95)]:
+            temp = torch.full((B,), t, device=DEV)
+            tk = torch.full((B,), k, dtype=torch.int32, device=DEV)
+            tp = torch.full((B,), p, device=DEV)
+            seeds = torch.arange(B, device=DEV)
+            steps = torch.zeros(B, dtype=torch.long, device=DEV)
+            us = timeit(lambda: ops.sample(tok, lp, logits, temp, tk, tp, seeds, steps))
+            emit(op="sample", mode=name, V=V, B=B, us=round(us, 1))
+
+
+def bench_decode(ops):
+    D, bs, part = 128, 16, 512
+    for B, ctx, nq, nkv in [(64, 1152, 32, 8), (256, 1152, 32, 8), (1, 4096, 32, 8), (64, 4096, 64, 8)]:
+        mb = math.ceil(ctx / bs) + 1
+        nblocks = B * mb
+        kc = torch.randn(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+        vc = torch.randn(nblocks, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+        bt = torch.randperm(nblocks, device=DEV).int().view(B, mb)
+        cl = torch.full((B,), ctx, device=DEV, dtype=torch.int32)
+        q = torch.randn(B, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+        mp = math.ceil(mb * bs / part)
+        to = torch.empty(B, nq, mp, D, device=DEV)
+        tm = torch.empty(B, nq, mp, 2, device=DEV)
+        out = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.paged_decode(out, q, kc, vc, bt, cl, to, tm, nq, nkv, part, 1 / math.sqrt(D)))
+        byts = 2 * B * ctx * nkv * D * 2
+        emit(op="paged_decode", B=B, ctx=ctx, nq=nq, nkv=nkv, us=round(us, 1), TBps=round(byts / us / 1e6, 2))
+
+
+def bench_prefill(ops):
+    D, bs = 128, 16
+    for S, nseq, nq, nkv in [(1024, 8, 32, 8), (4096, 2, 32, 8), (8192, 1, 32, 8)]:
+        mb = S // bs
+        kc = torch.randn(nseq * mb, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+        vc = torch.randn(nseq * mb, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+        bt = torch.arange(nseq * mb, device=DEV).int().view(nseq, mb)
+        cu = torch.arange(0, (nseq + 1) * S, S, device=DEV, dtype=torch.int32)
+        ctx = torch.full((nseq,), S, device=DEV, dtype=torch.int32)
+        tiles = torch.tensor([(s, r) for s in range(nseq) for r in range(0, S, 128)], device=DEV,
+                             dtype=torch.int32)
+        q = torch.randn(nseq * S, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+        out = torch.empty(nseq * S, nq * D, device=DEV, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.prefill_attention(out, q, kc, vc, bt, cu, ctx, tiles, nq, nkv,
+                                                  1 / math.sqrt(D)), n=10)
+        flops = 4 * nseq * (S * S / 2) * D * nq
+        emit(op="prefill_attention", S=S, nseq=nseq, us=round(us, 1), TFLOPs=round(flops / us / 1e6, 1))
+
+
+def bench_gemm(ops):
+    for M in (1, 16, 64, 128, 256):
+        for N, K, name in [(6144, 4096, "qkv"), (4096, 4096, "o"), (28672, 4096, "gate_up"),
+                           (4096, 14336, "down"), (128256, 4096, "lm_head")]:
+            x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+            w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+            us = timeit(lambda: torch.nn.functional.linear(x, w))
+            emit(op="hipblaslt_linear", name=name, M=M, N=N, K=K, us=round(us, 1),
+                 TBps=round(N * K * 2 / us / 1e6, 2))
+
+
+def bench_norm(ops):
+    for T, H in [(64, 4096), (8192, 4096)]:
+        x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+        r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+        out = torch.empty_like(x)
+        us = timeit(lambda: ops.fused_add_rmsnorm(out, x, r, w, 1e-5))
+        emit(op="fused_add_rmsnorm", T=T, H=H, us=round(us, 1), TBps=round(4 * T * H * 2 / us / 1e6, 2))
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    ops = KernelOps()
+    for name, fn in [("sample", bench_sample), ("decode", bench_decode), ("prefill", bench_prefill),
+                     ("gemm", bench_gemm), ("norm", bench_norm)]:
+        if which in ("all", name):
+            fn(ops)
+
+
+if __name__ == "__main__":
+    main()
