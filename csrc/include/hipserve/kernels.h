@@ -46,4 +46,11 @@ void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf1
                    const int* top_k, const float* top_p, const long* seeds,
                    const long* steps, hipStream_t s);
 
+// gguf.hip — qtype: 0 Q4_0, 1 Q4_1, 2 Q8_0, 3 Q4_K, 4 Q5_K, 5 Q6_K (repacked layouts)
+void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long out_stride,
+                      const void* q, const void* d, const void* m, int qtype, long row_bytes,
+                      int M, int N, int K, int splits, hipStream_t s);
+void launch_gguf_dequant(void* out, const void* q, const void* d, const void* m, int qtype,
+                         long row_bytes, int N, int K, hipStream_t s);
+
 }  // namespace hipserve

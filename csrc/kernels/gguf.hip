@@ -1,0 +1,292 @@
+// GGUF block-quantized matmul for the GGUF tier on gfx950.
+//
+// Weight formats as laid out in HBM (repacked once at load by hipserve/ops/quant.py):
+//   Q4_K  native 144-byte super-blocks (d, dmin, 12 B packed 6-bit scales/mins, 128 B nibbles)
+//   Q5_K  native 176-byte super-blocks (+32 B high bits)
+//   Q6_K  210-byte super-blocks padded to 224 B (16-byte aligned loads)
+//   Q8_0  SoA: int8 qs [N][K] then fp16 d [N][K/32]
+//   Q4_0  SoA: nibble qs [N][K/2] then fp16 d [N][K/32]      (Q4_1: + fp16 m [N][K/32])
+//
+// qgemm (decode, M <= 64): out[M,N] = x[M,K] . dequant(W)[N,K]^T on MFMA
+// v_mfma_f32_16x16x32_bf16 in the form out^T = W . x^T. Weights are dequantised
+// in registers straight into A fragments — never written back — so HBM traffic is
+// the quantised bytes (4.5 b/w for Q4_K) + x. The MFMA k order is permuted per
+// format so that each lane decodes whole contiguous byte runs of ONE block
+// (64 k per lane per 256-k super-block); x fragments follow the same permutation
+// from an LDS-staged x chunk shared by the workgroup's 4 waves (64 rows).
+// Split-K over workgroups (fp32 atomics into a workspace) fills the 256 CUs when
+// N is small.
+//
+// qdequant (prefill, large M): the same decoders write a bf16 copy that feeds a
+// hipBLASLt GEMM (compute-bound regime, dequant traffic is noise there).
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+enum QT { QT_Q4_0 = 0, QT_Q4_1 = 1, QT_Q8_0 = 2, QT_Q4_K = 3, QT_Q5_K = 4, QT_Q6_K = 5 };
+
+struct QParams {
+  const unsigned char* q;   // quant bytes / super-blocks
+  const unsigned short* d;  // SoA scales (fp16), Q8_0/Q4_0/Q4_1
+  const unsigned short* m;  // SoA mins (fp16), Q4_1
+  int K;
+  long row_bytes;           // bytes per row of q
+};
+
+HS_DEVICE float h2f(unsigned short h) { return static_cast<float>(__builtin_bit_cast(_Float16, h)); }
+
+HS_DEVICE u32x4 ld16(const unsigned char* p) { return *reinterpret_cast<const u32x4*>(p); }
+
+HS_DEVICE unsigned int byte_of(const u32x4 (&v)[2], int i) {  // i in [0, 32)
+  return (v[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
+}
+
+HS_DEVICE void scale_min_k4(int j, const unsigned char* s, float& sc, float& mn) {
+  if (j < 4) {
+    sc = s[j] & 63;
+    mn = s[j + 4] & 63;
+  } else {
+    sc = (s[j + 4] & 0xF) | ((s[j - 4] >> 6) << 4);
+    mn = (s[j + 4] >> 4) | ((s[j] >> 6) << 4);
+  }
+}
+
+// k index (within a 256-k super-chunk) of fragment element j, step s, lane group g
+template <int QT>
+HS_DEVICE int kbase(int g, int s) {
+  if constexpr (QT == QT_Q6_K) {
+    const int q = (g & 1) + 2 * (s >> 2);
+    return 128 * (g >> 1) + 32 * q + 8 * (s & 3);
+  } else {
+    return 64 * g + 32 * (s >> 2) + 8 * (s & 3);
+  }
+}
+
+// Decode the 64 weights lane group g owns in super-chunk sb of `row` into the 8
+// bf16x8 A fragments of the 8 MFMA k-steps.
+template <int QT>
+HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a)[8]) {
+  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
+    constexpr int BB = QT == QT_Q4_K ? 144 : 176;
+    const unsigned char* bp = p.q + row * p.row_bytes + (long)sb * BB;
+    const u32x4 hdr = ld16(bp);
+    unsigned char sc12[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) sc12[i] = (hdr[1 + i / 4] >> (8 * (i & 3))) & 0xFF;
+    const float d = h2f(hdr[0] & 0xFFFF), dmin = h2f(hdr[0] >> 16);
+    float s1, m1, s2, m2;
+    scale_min_k4(2 * g, sc12, s1, m1);
+    scale_min_k4(2 * g + 1, sc12, s2, m2);
+    const float d1 = d * s1, mm1 = dmin * m1, d2 = d * s2, mm2 = dmin * m2;
+    const int qoff = QT == QT_Q4_K ? 16 : 48;
+    u32x4 qs[2] = {ld16(bp + qoff + 32 * g), ld16(bp + qoff + 32 * g + 16)};
+    u32x4 qh[2];
+    if constexpr (QT == QT_Q5_K) { qh[0] = ld16(bp + 16); qh[1] = ld16(bp + 32); }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = 8 * (s & 3) + j;
+        const unsigned int b = byte_of(qs, l);
+        float q = (s < 4) ? (float)(b & 0xF) : (float)(b >> 4);
+        if constexpr (QT == QT_Q5_K) {
+          const unsigned int hb = byte_of(qh, l);
+          q += ((hb >> (2 * g + (s >> 2))) & 1) ? 16.f : 0.f;
+        }
+        a[s][j] = static_cast<__bf16>((s < 4) ? d1 * q - mm1 : d2 * q - mm2);
+      }
+  } else if constexpr (QT == QT_Q6_K) {
+    const unsigned char* bp = p.q + row * p.row_bytes + (long)sb * 224;
+    const int h = g >> 1, odd = g & 1;
+    u32x4 ql[2] = {ld16(bp + 64 * h + 32 * odd), ld16(bp + 64 * h + 32 * odd + 16)};
+    u32x4 qh[2] = {ld16(bp + 128 + 32 * h), ld16(bp + 128 + 32 * h + 16)};
+    const u32x4 scv = ld16(bp + 192);
+    const u32x4 dv = ld16(bp + 208);
+    const float d = h2f(dv[0] & 0xFFFF);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int q = odd + 2 * (s >> 2);
+      const int si = 8 * h + 2 * q + ((s & 3) >= 2 ? 1 : 0);
+      const float sc = (float)(signed char)((scv[si >> 2] >> (8 * (si & 3))) & 0xFF);
+      const float ds = d * sc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = 8 * (s & 3) + j;
+        const unsigned int b = byte_of(ql, l);
+        const unsigned int lo = (s < 4) ? (b & 0xF) : (b >> 4);
+        const unsigned int hi = (byte_of(qh, l) >> (2 * q)) & 3;
+        a[s][j] = static_cast<__bf16>(ds * (float)((int)(lo | (hi << 4)) - 32));
+      }
+    }
+  } else if constexpr (QT == QT_Q8_0) {
+    const unsigned char* qp = p.q + row * (long)p.K + (long)sb * 256 + 64 * g;
+    const unsigned short* dp = p.d + row * (long)(p.K / 32) + sb * 8 + 2 * g;
+    const float dA = h2f(dp[0]), dB = h2f(dp[1]);
+    u32x4 v[4] = {ld16(qp), ld16(qp + 16), ld16(qp + 32), ld16(qp + 48)};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float dd = (s < 4) ? dA : dB;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * s + j;  // byte within the lane's 64
+        const signed char c = (signed char)((v[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFF);
+        a[s][j] = static_cast<__bf16>(dd * (float)c);
+      }
+    }
+  } else {  // Q4_0 / Q4_1 SoA
+    const unsigned char* qp = p.q + row * (long)(p.K / 2) + (long)sb * 128 + 32 * g;
+    const long di = row * (long)(p.K / 32) + sb * 8 + 2 * g;
+    const float dA = h2f(p.d[di]), dB = h2f(p.d[di + 1]);
+    float mA = 0.f, mB = 0.f;
+    if constexpr (QT == QT_Q4_1) { mA = h2f(p.m[di]); mB = h2f(p.m[di + 1]); }
+    u32x4 v[2] = {ld16(qp), ld16(qp + 16)};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int blk = s >> 2;
+      const float dd = blk ? dB : dA, mm = blk ? mB : mA;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = 8 * (s & 3) + j;       // element in the 32-block
+        const unsigned int b = byte_of(v, 16 * blk + (e & 15));
+        const float q = (e < 16) ? (float)(b & 0xF) : (float)(b >> 4);
+        a[s][j] = static_cast<__bf16>(QT == QT_Q4_0 ? dd * (q - 8.f) : dd * q + mm);
+      }
+    }
+  }
+}
+
+constexpr int kXPad = 8;  // LDS row padding (bf16) for conflict-free b128 reads
+
+template <int QT, int MT>
+__global__ __launch_bounds__(256) void qgemm_kernel(
+    unsigned short* __restrict__ out, float* __restrict__ ws, const unsigned short* __restrict__ x,
+    long x_stride, long out_stride, QParams p, int M, int N, int K, int sb_per_split) {
+  constexpr int XR = 16 * MT;            // staged x rows
+  constexpr int XS = 256 + kXPad;        // LDS row stride (elements)
+  __shared__ __attribute__((aligned(16))) unsigned short xs[XR * XS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.x * 64 + wave * 16;
+  const int nsb = K / 256;
+  const int sb0 = blockIdx.y * sb_per_split;
+  const int sb1 = min(nsb, sb0 + sb_per_split);
+  const long row = min(n0 + c, N - 1);
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int sb = sb0; sb < sb1; ++sb) {
+    __syncthreads();
+    // stage x[:, sb*256 .. +256] (rows >= M are zero)
+    for (int i = threadIdx.x; i < XR * 32; i += 256) {
+      const int r = i >> 5, cc = i & 31;
+      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (r < M) v = *reinterpret_cast<const u16x8*>(x + r * x_stride + sb * 256 + cc * 8);
+      *reinterpret_cast<u16x8*>(xs + r * XS + cc * 8) = v;
+    }
+    __syncthreads();
+    bf16x8 a[8];
+    decode_lane<QT>(p, row, sb, g, a);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int kb = kbase<QT>(g, s);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const u16x8 bv = *reinterpret_cast<const u16x8*>(xs + (16 * t + c) * XS + kb);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], __builtin_bit_cast(bf16x8, bv), acc[t], 0, 0, 0);
+      }
+    }
+  }
+  // C layout: col = m (lane & 15), rows n = 4*g + r
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = 16 * t + c;
+    if (m >= M) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 4 * g + r;
+      if (n >= N) continue;
+      if (ws) atomicAdd(ws + (long)m * N + n, acc[t][r]);
+      else out[m * out_stride + n] = f32_to_bf16(acc[t][r]);
+    }
+  }
+}
+
+__global__ void f32_to_bf16_kernel(unsigned short* __restrict__ out, const float* __restrict__ in,
+                                   int M, int N, long out_stride) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= (long)M * N) return;
+  const int m = i / N, n = i % N;
+  out[m * out_stride + n] = f32_to_bf16(in[i]);
+}
+
+template <int QT>
+__global__ __launch_bounds__(256) void qdequant_kernel(unsigned short* __restrict__ out, QParams p, int N,
+                                                       int K) {
+  const long t = blockIdx.x * 256L + threadIdx.x;  // (row, sb, g)
+  const int nsb = K / 256;
+  if (t >= (long)N * nsb * 4) return;
+  const int g = t & 3;
+  const long rs = t >> 2;
+  const long row = rs / nsb;
+  const int sb = rs % nsb;
+  bf16x8 a[8];
+  decode_lane<QT>(p, row, sb, g, a);
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    *reinterpret_cast<bf16x8*>(out + row * K + sb * 256 + kbase<QT>(g, s)) = a[s];
+}
+
+template <int QT>
+static void launch_qgemm_t(void* out, float* ws, const void* x, long x_stride, long out_stride,
+                           const QParams& p, int M, int N, int K, int splits, hipStream_t s) {
+  const int nsb = K / 256;
+  const int per = (nsb + splits - 1) / splits;
+  dim3 grid((N + 63) / 64, (nsb + per - 1) / per), block(256);
+  auto* o = static_cast<unsigned short*>(out);
+  auto* xi = static_cast<const unsigned short*>(x);
+  if (M <= 16) qgemm_kernel<QT, 1><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
+  else if (M <= 32) qgemm_kernel<QT, 2><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
+  else qgemm_kernel<QT, 4><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
+}
+
+void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long out_stride,
+                      const void* q, const void* d, const void* m, int qtype, long row_bytes,
+                      int M, int N, int K, int splits, hipStream_t s) {
+  QParams p{static_cast<const unsigned char*>(q), static_cast<const unsigned short*>(d),
+            static_cast<const unsigned short*>(m), K, row_bytes};
+  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * M * N, s);
+  switch (qtype) {
+    case QT_Q4_0: launch_qgemm_t<QT_Q4_0>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+    case QT_Q4_1: launch_qgemm_t<QT_Q4_1>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+    case QT_Q8_0: launch_qgemm_t<QT_Q8_0>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+    case QT_Q4_K: launch_qgemm_t<QT_Q4_K>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+    case QT_Q5_K: launch_qgemm_t<QT_Q5_K>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+    case QT_Q6_K: launch_qgemm_t<QT_Q6_K>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+  }
+  if (ws) {
+    const long n = (long)M * N;
+    f32_to_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(static_cast<unsigned short*>(out), ws, M, N,
+                                                                   out_stride);
+  }
+}
+
+void launch_gguf_dequant(void* out, const void* q, const void* d, const void* m, int qtype,
+                         long row_bytes, int N, int K, hipStream_t s) {
+  QParams p{static_cast<const unsigned char*>(q), static_cast<const unsigned short*>(d),
+            static_cast<const unsigned short*>(m), K, row_bytes};
+  const long threads = (long)N * (K / 256) * 4;
+  dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+  auto* o = static_cast<unsigned short*>(out);
+  switch (qtype) {
+    case QT_Q4_0: qdequant_kernel<QT_Q4_0><<<grid, block, 0, s>>>(o, p, N, K); break;
+    case QT_Q4_1: qdequant_kernel<QT_Q4_1><<<grid, block, 0, s>>>(o, p, N, K); break;
+    case QT_Q8_0: qdequant_kernel<QT_Q8_0><<<grid, block, 0, s>>>(o, p, N, K); break;
+    case QT_Q4_K: qdequant_kernel<QT_Q4_K><<<grid, block, 0, s>>>(o, p, N, K); break;
+    case QT_Q5_K: qdequant_kernel<QT_Q5_K><<<grid, block, 0, s>>>(o, p, N, K); break;
+    case QT_Q6_K: qdequant_kernel<QT_Q6_K><<<grid, block, 0, s>>>(o, p, N, K); break;
+  }
+}
+
+}  // namespace hipserve

@@ -143,6 +143,38 @@ void sample(at::Tensor& out_tok, at::Tensor& out_lp, const at::Tensor& logits,
                           steps.data_ptr<int64_t>(), cur_stream());
 }
 
+void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const at::Tensor& d,
+               const at::Tensor& mn, int64_t qtype, int64_t row_bytes, int64_t N, int64_t K,
+               at::Tensor& ws, int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.is_contiguous());
+  TORCH_CHECK(K % 256 == 0, "gguf_gemm: K must be a multiple of 256");
+  TORCH_CHECK(x.size(1) >= K && out.size(1) >= N && out.size(0) == x.size(0));
+  const int M = x.size(0);
+  TORCH_CHECK(M <= 64, "gguf_gemm handles M <= 64 (use gguf_dequant + GEMM above)");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
+  TORCH_CHECK(qtype >= 0 && qtype <= 5);
+  if (qtype <= 2) TORCH_CHECK(d.numel() >= N * (K / 32), "missing SoA scales");
+  if (qtype == 1) TORCH_CHECK(mn.numel() >= N * (K / 32), "missing SoA mins");
+  if (splits > 1) TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (long)M * N);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_gguf_gemm(out.data_ptr(), splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(),
+                             x.stride(0), out.stride(0), q.data_ptr(), d.numel() ? d.data_ptr() : nullptr,
+                             mn.numel() ? mn.data_ptr() : nullptr, qtype, row_bytes, M, N, K,
+                             splits, cur_stream());
+}
+
+void gguf_dequant(at::Tensor& out, const at::Tensor& q, const at::Tensor& d, const at::Tensor& mn,
+                  int64_t qtype, int64_t row_bytes, int64_t N, int64_t K) {
+  CHECK_DEV(q); CHECK_BF16(out); TORCH_CHECK(out.is_contiguous() && out.numel() >= N * K);
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.is_contiguous() && K % 256 == 0);
+  TORCH_CHECK(qtype >= 0 && qtype <= 5);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  hipserve::launch_gguf_dequant(out.data_ptr(), q.data_ptr(), d.numel() ? d.data_ptr() : nullptr,
+                                mn.numel() ? mn.data_ptr() : nullptr, qtype, row_bytes, N, K,
+                                cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
@@ -152,6 +184,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale) -> ()");
+  m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
+  m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
 
@@ -163,4 +197,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
+  m.impl("gguf_gemm", &gguf_gemm);
+  m.impl("gguf_dequant", &gguf_dequant);
 }

@@ -216,7 +216,7 @@ class LlamaModel:
         return out.to(x.dtype)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(hidden, self.lm_head)
+        logits = self.linear(hidden, self.lm_head)
         logits = self.tp.all_gather_lastdim(logits)
         return logits[:, : self.cfg.vocab_size]
 
