@@ -54,3 +54,9 @@ void launch_gguf_dequant(void* out, const void* q, const void* d, const void* m,
                          long row_bytes, int N, int K, hipStream_t s);
 
 }  // namespace hipserve
+
+namespace hipserve {
+// skinny_gemm.hip — decode GEMM out[M,N] = x[M,K] . W[N,K]^T (M <= 64, K % (256*kw) == 0)
+bool launch_skinny_gemm(void* out, const void* x, long x_stride, const void* w, long out_stride, int M,
+                        int N, int K, int rt, int kw, hipStream_t s);
+}  // namespace hipserve

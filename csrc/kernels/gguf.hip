@@ -24,7 +24,7 @@
 
 namespace hipserve {
 
-enum QT { QT_Q4_0 = 0, QT_Q4_1 = 1, QT_Q8_0 = 2, QT_Q4_K = 3, QT_Q5_K = 4, QT_Q6_K = 5 };
+enum QT { QT_Q4_0 = 0, QT_Q4_1 = 1, QT_Q8_0 = 2, QT_Q4_K = 3, QT_Q5_K = 4, QT_Q6_K = 5, QT_BF16 = 6 };
 
 struct QParams {
   const unsigned char* q;   // quant bytes / super-blocks
@@ -67,7 +67,11 @@ HS_DEVICE int kbase(int g, int s) {
 // bf16x8 A fragments of the 8 MFMA k-steps.
 template <int QT>
 HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a)[8]) {
-  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
+  if constexpr (QT == QT_BF16) {  // plain bf16 rows: 128 contiguous bytes per lane
+    const unsigned char* rp = p.q + row * p.row_bytes + (long)sb * 512 + 128 * g;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) a[s] = __builtin_bit_cast(bf16x8, ld16(rp + 16 * s));
+  } else if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
     constexpr int BB = QT == QT_Q4_K ? 144 : 176;
     const unsigned char* bp = p.q + row * p.row_bytes + (long)sb * BB;
     const u32x4 hdr = ld16(bp);
@@ -264,6 +268,7 @@ void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long o
     case QT_Q4_K: launch_qgemm_t<QT_Q4_K>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
     case QT_Q5_K: launch_qgemm_t<QT_Q5_K>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
     case QT_Q6_K: launch_qgemm_t<QT_Q6_K>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
+    case QT_BF16: launch_qgemm_t<QT_BF16>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
   }
   if (ws) {
     const long n = (long)M * N;

@@ -153,7 +153,7 @@ void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const 
   const int M = x.size(0);
   TORCH_CHECK(M <= 64, "gguf_gemm handles M <= 64 (use gguf_dequant + GEMM above)");
   TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
-  TORCH_CHECK(qtype >= 0 && qtype <= 5);
+  TORCH_CHECK(qtype >= 0 && qtype <= 6);
   if (qtype <= 2) TORCH_CHECK(d.numel() >= N * (K / 32), "missing SoA scales");
   if (qtype == 1) TORCH_CHECK(mn.numel() >= N * (K / 32), "missing SoA mins");
   if (splits > 1) TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (long)M * N);
@@ -175,6 +175,20 @@ void gguf_dequant(at::Tensor& out, const at::Tensor& q, const at::Tensor& d, con
                                 cur_stream());
 }
 
+void skinny_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t rt, int64_t kw) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out); CHECK_CONTIG(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) >= N);
+  TORCH_CHECK(M >= 1 && M <= 64, "skinny_gemm: 1 <= M <= 64");
+  TORCH_CHECK(kw >= 1 && K % (256 * kw) == 0, "skinny_gemm: K must be a multiple of 256*kw");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_skinny_gemm(out.data_ptr(), x.data_ptr(), x.stride(0), w.data_ptr(),
+                                           out.stride(0), M, N, K, rt, kw, cur_stream()),
+              "skinny_gemm: unsupported (rt, kw)");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
@@ -186,6 +200,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale) -> ()");
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
+  m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
 
@@ -198,5 +213,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
   m.impl("gguf_gemm", &gguf_gemm);
+  m.impl("skinny_gemm", &skinny_gemm);
   m.impl("gguf_dequant", &gguf_dequant);
 }

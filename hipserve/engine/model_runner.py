@@ -93,6 +93,12 @@ class ModelRunner:
         self.graph_pool = None
         self._static = None
         self.use_graphs = self.device.type == "cuda" and not ecfg.enforce_eager
+        self.gemm_report = []
+        if self.device.type == "cuda" and ecfg.extra.get("gemm_autotune", True):
+            from ..ops import gemm
+
+            ms = [b for b in self.buckets if b <= 64]
+            self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms)
         if self.use_graphs:
             self._capture_graphs()
 

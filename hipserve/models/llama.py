@@ -21,6 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from ..config import ModelConfig
+from ..ops import gemm
 from ..ops import reference as ref
 from ..parallel.comm import TPGroup
 
@@ -132,8 +133,19 @@ class LlamaModel:
     # ---------------------------------------------------------------- forward
     def linear(self, x: torch.Tensor, w, name: str | None = None) -> torch.Tensor:
         if isinstance(w, torch.Tensor):
-            return F.linear(x, w)
+            return gemm.linear(x, w)
         return self.quant_linear(x, w)
+
+    def gemm_shapes(self):
+        """(N, K) of every dense bf16 projection (for the decode GEMM autotune)."""
+        out = set()
+        for lw in self.layers[:1]:
+            for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
+                if isinstance(w, torch.Tensor) and w.dim() == 2:
+                    out.add(tuple(w.shape))
+        if isinstance(self.lm_head, torch.Tensor):
+            out.add(tuple(self.lm_head.shape))
+        return sorted(out)
 
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.tp.world_size == 1:

@@ -167,3 +167,31 @@ def test_sample_distribution(ops):
     p = torch.softmax(base[8:], 0)
     assert cnt[:8].sum() == 0
     assert (cnt[8:] - p).abs().max() < 0.03
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (200, 1024), (6144, 4096), (4096, 14336)])
+@pytest.mark.parametrize("rt,kw", [(1, 1), (1, 4), (1, 8), (2, 2), (2, 8)])
+def test_skinny_gemm(ops, M, N, K, rt, kw):
+    if K % (256 * kw):
+        pytest.skip("K not divisible")
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.skinny_gemm(out, x, w, rt, kw)
+    want = x.float() @ w.float().T
+    _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 20, 64])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_splitk_bf16_gemm(ops, M, splits):
+    from hipserve.ops.gemm import splitk_gemm
+    N, K = 4096, 4096
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    splitk_gemm(out, x, w, splits)
+    want = x.float() @ w.float().T
+    _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)

@@ -123,5 +123,20 @@ def main():
             fn(ops)
 
 
+
+
+def bench_tune():
+    from hipserve.ops import gemm
+    shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]
+    for r in gemm.TUNER.tune(shapes, torch.device("cuda"), [1, 16, 32, 64]):
+        emit(op="gemm_tune", **r)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "tune":
+    KernelOps()
+    bench_tune()
+    sys.exit(0)
+
+
 if __name__ == "__main__":
     main()
