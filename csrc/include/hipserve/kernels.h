@@ -60,3 +60,15 @@ namespace hipserve {
 bool launch_skinny_gemm(void* out, const void* x, long x_stride, const void* w, long out_stride, int M,
                         int N, int K, int rt, int kw, hipStream_t s);
 }  // namespace hipserve
+
+namespace hipserve {
+// moe.hip — tile in {16, 32, 64}
+void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
+                             hipStream_t s);
+void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
+                      int tiles_cap, int* num_tiles, int* pair_slot, hipStream_t s);
+void launch_moe_gemm(void* out, long out_stride, const void* x, long x_stride, const void* w, const int* slots,
+                     const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, hipStream_t s);
+void launch_moe_combine(void* out, const void* y, const float* w, const int* pair_slot, int T, int k, int H,
+                        hipStream_t s);
+}  // namespace hipserve

@@ -1,0 +1,222 @@
+// Mixture-of-experts kernels for Mixtral-style sparse MLPs on
+// gfx950. Graph-capturable: every grid is sized from static upper bounds and the
+// data-dependent parts (tile count, expert of a tile) are read on the device.
+//
+//   moe_topk_softmax  router logits -> top-k experts + renormalised weights
+//                     (one wave per token, experts on lanes, wave64 reductions)
+//   moe_align         token/expert pairs sorted by expert into 16-row tiles,
+//                     padding slots = -1 (one 1024-thread workgroup, LDS counts)
+//   moe_gemm          per tile: out[slot] = x[row(slot)] . W_e^T on MFMA, rows
+//                     gathered through the slot list (token rows for w13, slot rows
+//                     for w2); each expert's weights stream once per 16-row tile
+//   moe_combine       y rows of a token's k pairs, weighted sum -> hidden state
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+template <typename T>
+HS_DEVICE float ld_f(const T* p, long i);
+template <>
+HS_DEVICE float ld_f<unsigned short>(const unsigned short* p, long i) { return bf16_to_f32(p[i]); }
+template <>
+HS_DEVICE float ld_f<float>(const float* p, long i) { return p[i]; }
+
+template <typename T>
+__global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restrict__ logits, float* __restrict__ w,
+                                                               int* __restrict__ ids, int Tn, int E, int k) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= Tn) return;
+  float v = lane < E ? ld_f<T>(logits, (long)t * E + lane) : -INFINITY;
+  const float mx = wave_max(v);
+  const float e = lane < E ? __expf(v - mx) : 0.f;
+  const float s = wave_sum(e);
+  float p = e / s;
+  float sel_sum = 0.f;
+  float mine = 0.f;
+  int rank = -1;
+  for (int j = 0; j < k; ++j) {
+    // argmax over lanes (ties -> lower expert id)
+    float bv = (rank < 0 && lane < E) ? p : -1.f;
+    int bi = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(bv, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (v2 > bv || (v2 == bv && i2 < bi)) { bv = v2; bi = i2; }
+    }
+    if (lane == bi) { rank = j; mine = p; }
+    sel_sum += bv;
+  }
+  if (rank >= 0) {
+    w[(long)t * k + rank] = mine / sel_sum;
+    ids[(long)t * k + rank] = lane;
+  }
+}
+
+__global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ ids, int npairs, int E, int tile,
+                                                         int* __restrict__ slots, int slots_cap,
+                                                         int* __restrict__ tile_expert, int tiles_cap,
+                                                         int* __restrict__ num_tiles, int* __restrict__ pair_slot) {
+  __shared__ int cnt[64], off[65], cur[64];
+  const int tid = threadIdx.x;
+  if (tid < 64) { cnt[tid] = 0; cur[tid] = 0; }
+  __syncthreads();
+  for (int p = tid; p < npairs; p += 1024) atomicAdd(&cnt[ids[p]], 1);
+  __syncthreads();
+  if (tid == 0) {
+    off[0] = 0;
+    for (int e = 0; e < E; ++e) off[e + 1] = off[e] + (cnt[e] + tile - 1) / tile * tile;
+    *num_tiles = off[E] / tile;
+  }
+  __syncthreads();
+  for (int s = tid; s < slots_cap; s += 1024) slots[s] = -1;
+  for (int t = tid; t < tiles_cap; t += 1024) {
+    int e = -1;
+    if (t * tile < off[E]) {
+      for (int q = 0; q < E; ++q)
+        if (t * tile >= off[q] && t * tile < off[q + 1]) e = q;
+    }
+    tile_expert[t] = e;
+  }
+  __syncthreads();
+  for (int p = tid; p < npairs; p += 1024) {
+    const int e = ids[p];
+    const int pos = off[e] + atomicAdd(&cur[e], 1);
+    slots[pos] = p;
+    pair_slot[p] = pos;
+  }
+}
+
+// out[slot, N] = x[row(slot), K] . W[e, N, K]^T; row(slot) = pair / k (gather) or slot.
+// A tile = 16*MT consecutive slots of one expert; each W fragment feeds MT MFMAs.
+template <int MT, int KW>
+__global__ __launch_bounds__(64 * KW) void moe_gemm_kernel(
+    unsigned short* __restrict__ out, long out_stride, const unsigned short* __restrict__ x, long x_stride,
+    const unsigned short* __restrict__ w, const int* __restrict__ slots, const int* __restrict__ tile_expert,
+    int gather_k, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [KW][MT][64][4]
+  const int tile = blockIdx.y;
+  const int e = tile_expert[tile];
+  if (e < 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.x * 16;
+  int pr[MT];
+  const unsigned short* xr[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int slot = tile * 16 * MT + 16 * t + c;
+    pr[t] = slots[slot];
+    const long xrow = pr[t] < 0 ? 0 : (gather_k > 0 ? pr[t] / gather_k : slot);
+    xr[t] = x + xrow * x_stride + 64 * g;
+  }
+  const unsigned short* wr = w + ((long)e * N + min(n0 + c, N - 1)) * K + 64 * g;
+  const int kw = K / KW, k0 = wave * kw, k1 = k0 + kw;
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kk = k0; kk < k1; kk += 256) {
+    u16x8 a[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) a[s] = *reinterpret_cast<const u16x8*>(wr + kk + 8 * s);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const u16x8 b = *reinterpret_cast<const u16x8*>(xr[t] + kk + 8 * s);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s]),
+                                                         __builtin_bit_cast(bf16x8, b), acc[t], 0, 0, 0);
+      }
+  }
+  if constexpr (KW > 1) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) *reinterpret_cast<f32x4*>(red + ((wave * MT + t) * 64 + lane) * 4) = acc[t];
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+      for (int q = 1; q < KW; ++q) acc[t] += *reinterpret_cast<const f32x4*>(red + ((q * MT + t) * 64 + lane) * 4);
+  }
+  // C: col = slot-in-tile (lane & 15), rows n = n0 + 4g + j
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    if (pr[t] < 0) continue;
+    const long slot = tile * 16 * MT + 16 * t + c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + 4 * g + j;
+      if (n < N) out[slot * out_stride + n] = f32_to_bf16(acc[t][j]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void moe_combine_kernel(unsigned short* __restrict__ out, const unsigned short* __restrict__ y,
+                                                          const float* __restrict__ w, const int* __restrict__ pair_slot,
+                                                          int k, int H) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const float wt = w[(long)t * k + j];
+      const u16x8 v = *reinterpret_cast<const u16x8*>(y + (long)pair_slot[t * k + j] * H + 8 * c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += wt * bf16_to_f32(v[e]);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f32_to_bf16(acc[e]);
+    *reinterpret_cast<u16x8*>(out + (long)t * H + 8 * c) = o;
+  }
+}
+
+void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
+                             hipStream_t s) {
+  if (T <= 0) return;
+  dim3 grid((T + 3) / 4), block(256);
+  if (logits_f32)
+    moe_topk_softmax_kernel<float><<<grid, block, 0, s>>>(static_cast<const float*>(logits), w, ids, T, E, k);
+  else
+    moe_topk_softmax_kernel<unsigned short><<<grid, block, 0, s>>>(static_cast<const unsigned short*>(logits), w, ids,
+                                                                   T, E, k);
+}
+
+void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
+                      int tiles_cap, int* num_tiles, int* pair_slot, hipStream_t s) {
+  moe_align_kernel<<<1, 1024, 0, s>>>(ids, npairs, E, tile, slots, slots_cap, tile_expert, tiles_cap, num_tiles,
+                                      pair_slot);
+}
+
+template <int MT>
+static void moe_gemm_mt(void* out, long out_stride, const void* x, long x_stride, const void* w, const int* slots,
+                        const int* tile_expert, int tiles_cap, int gather_k, int N, int K, hipStream_t s) {
+  const int kw = (K % 1024 == 0) ? 4 : ((K % 512 == 0) ? 2 : 1);
+  dim3 grid((N + 15) / 16, tiles_cap), block(64 * kw);
+  const size_t smem = kw > 1 ? (size_t)kw * MT * 64 * 4 * sizeof(float) : 0;
+  auto* o = static_cast<unsigned short*>(out);
+  auto* xi = static_cast<const unsigned short*>(x);
+  auto* wi = static_cast<const unsigned short*>(w);
+  if (kw == 4)
+    moe_gemm_kernel<MT, 4><<<grid, block, smem, s>>>(o, out_stride, xi, x_stride, wi, slots, tile_expert, gather_k, N, K);
+  else if (kw == 2)
+    moe_gemm_kernel<MT, 2><<<grid, block, smem, s>>>(o, out_stride, xi, x_stride, wi, slots, tile_expert, gather_k, N, K);
+  else
+    moe_gemm_kernel<MT, 1><<<grid, block, smem, s>>>(o, out_stride, xi, x_stride, wi, slots, tile_expert, gather_k, N, K);
+}
+
+void launch_moe_gemm(void* out, long out_stride, const void* x, long x_stride, const void* w, const int* slots,
+                     const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, hipStream_t s) {
+  if (tile == 16) moe_gemm_mt<1>(out, out_stride, x, x_stride, w, slots, tile_expert, tiles_cap, gather_k, N, K, s);
+  else if (tile == 32) moe_gemm_mt<2>(out, out_stride, x, x_stride, w, slots, tile_expert, tiles_cap, gather_k, N, K, s);
+  else moe_gemm_mt<4>(out, out_stride, x, x_stride, w, slots, tile_expert, tiles_cap, gather_k, N, K, s);
+}
+
+void launch_moe_combine(void* out, const void* y, const float* w, const int* pair_slot, int T, int k, int H,
+                        hipStream_t s) {
+  if (T <= 0) return;
+  moe_combine_kernel<<<T, 256, 0, s>>>(static_cast<unsigned short*>(out), static_cast<const unsigned short*>(y), w,
+                                       pair_slot, k, H);
+}
+
+}  // namespace hipserve

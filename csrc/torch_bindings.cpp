@@ -189,9 +189,68 @@ void skinny_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int6
               "skinny_gemm: unsupported (rt, kw)");
 }
 
+void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, int64_t k) {
+  CHECK_DEV(logits); CHECK_CONTIG(logits); CHECK_CONTIG(w); CHECK_CONTIG(ids);
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 64, "moe: <= 64 experts");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && ids.scalar_type() == at::kInt);
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16);
+  const int T = logits.size(0);
+  TORCH_CHECK(w.numel() >= T * k && ids.numel() >= T * k && k >= 1 && k <= logits.size(1));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  hipserve::launch_moe_topk_softmax(logits.data_ptr(), logits.scalar_type() == at::kFloat, w.data_ptr<float>(),
+                                    ids.data_ptr<int>(), T, logits.size(1), k, cur_stream());
+}
+
+void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,
+               at::Tensor& num_tiles, at::Tensor& pair_slot) {
+  CHECK_DEV(ids);
+  TORCH_CHECK(ids.scalar_type() == at::kInt && slots.scalar_type() == at::kInt &&
+              tile_expert.scalar_type() == at::kInt && pair_slot.scalar_type() == at::kInt);
+  TORCH_CHECK(E <= 64 && (tile == 16 || tile == 32 || tile == 64));
+  const int npairs = ids.numel();
+  TORCH_CHECK(slots.numel() >= npairs + E * (tile - 1) && slots.numel() % tile == 0,
+              "slots capacity must cover padding and be a multiple of the tile");
+  TORCH_CHECK(tile_expert.numel() * tile >= slots.numel() && pair_slot.numel() >= npairs);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ids.device());
+  hipserve::launch_moe_align(ids.data_ptr<int>(), npairs, E, tile, slots.data_ptr<int>(), slots.numel(),
+                             tile_expert.data_ptr<int>(), tile_expert.numel(), num_tiles.data_ptr<int>(),
+                             pair_slot.data_ptr<int>(), cur_stream());
+}
+
+void moe_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& slots,
+              const at::Tensor& tile_expert, int64_t tile, int64_t gather_k) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  CHECK_CONTIG(w);
+  TORCH_CHECK(w.dim() == 3, "w [E, N, K]");
+  const int N = w.size(1), K = w.size(2);
+  TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && out.size(1) >= N);
+  TORCH_CHECK(out.size(0) >= slots.numel() && x.stride(0) % 8 == 0);
+  TORCH_CHECK(tile_expert.numel() * tile >= slots.numel());
+  TORCH_CHECK(gather_k > 0 || x.size(0) >= slots.numel(), "ungathered x needs one row per slot");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_moe_gemm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(),
+                            slots.data_ptr<int>(), tile_expert.data_ptr<int>(), slots.numel() / tile, tile,
+                            gather_k, N, K, cur_stream());
+}
+
+void moe_combine(at::Tensor& out, const at::Tensor& y, const at::Tensor& w, const at::Tensor& pair_slot,
+                 int64_t k) {
+  CHECK_DEV(y); CHECK_BF16(y); CHECK_BF16(out); CHECK_CONTIG(y); CHECK_CONTIG(out);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && pair_slot.scalar_type() == at::kInt);
+  const int T = out.size(0), H = out.size(1);
+  TORCH_CHECK(y.size(1) == H && H % 8 == 0 && w.numel() >= T * k && pair_slot.numel() >= T * k);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
+  hipserve::launch_moe_combine(out.data_ptr(), y.data_ptr(), w.data_ptr<float>(), pair_slot.data_ptr<int>(), T, k,
+                               H, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
+  m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k) -> ()");
+  m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot) -> ()");
+  m.def("moe_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k) -> ()");
+  m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor w, Tensor pair_slot, int k) -> ()");
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
@@ -214,5 +273,9 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("gguf_gemm", &gguf_gemm);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("moe_topk_softmax", &moe_topk_softmax);
+  m.impl("moe_align", &moe_align);
+  m.impl("moe_gemm", &moe_gemm);
+  m.impl("moe_combine", &moe_combine);
   m.impl("gguf_dequant", &gguf_dequant);
 }

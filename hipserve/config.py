@@ -127,6 +127,11 @@ PRESETS: dict[str, ModelConfig] = {
                                num_kv_heads=2, head_dim=64, intermediate_size=1024,
                                vocab_size=1024, rope_theta=10000.0, max_position_embeddings=4096,
                                bos_token_id=1, eos_token_id=(2,)),
+    "small-mixtral": ModelConfig(name="small-mixtral", architecture="mixtral", hidden_size=512,
+                                 num_layers=2, num_heads=8, num_kv_heads=2, head_dim=64,
+                                 intermediate_size=768, vocab_size=1024, rope_theta=1e6,
+                                 max_position_embeddings=4096, num_experts=8,
+                                 num_experts_per_tok=2, bos_token_id=1, eos_token_id=(2,)),
 }
 
 

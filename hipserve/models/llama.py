@@ -25,6 +25,8 @@ from ..ops import gemm
 from ..ops import reference as ref
 from ..parallel.comm import TPGroup
 
+MOE_KERNEL_MAX_PAIRS = 2048  # larger (prefill) batches use per-expert hipBLASLt GEMMs
+
 
 @dataclass
 class AttnMeta:
@@ -202,11 +204,12 @@ class LlamaModel:
         cfg = self.cfg
         k = cfg.num_experts_per_tok
         T = x.shape[0]
+        if (self.ops.name == "hip" and T * k <= MOE_KERNEL_MAX_PAIRS and cfg.num_experts <= 64
+                and cfg.hidden_size % 256 == 0 and self.inter % 256 == 0):
+            return self.moe_hip(x, lw)
         logits = F.linear(x, lw.router).float()
         w, idx = torch.topk(torch.softmax(logits, dim=-1), k, dim=-1)
         w = w / w.sum(-1, keepdim=True)
-        if hasattr(self.ops, "moe") and self.ops.name == "hip":
-            return self.ops.moe(x, lw.w13, lw.w2, w, idx, self.inter)
         out = torch.zeros(T, cfg.hidden_size, device=x.device, dtype=torch.float32)
         flat_idx = idx.reshape(-1)
         flat_tok = torch.arange(T, device=x.device).repeat_interleave(k)
@@ -226,6 +229,36 @@ class LlamaModel:
             y = F.linear(act, lw.w2[e]).float() * flat_w[sel].unsqueeze(-1)
             out.index_add_(0, toks, y)
         return out.to(x.dtype)
+
+    def moe_hip(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
+        """Graph-capturable MoE on the gfx950 kernels (decode-sized batches): top-k
+        routing, expert-sorted 16/32/64-row tiles, two gathered MFMA GEMMs with the
+        SiLU*up in between, weighted combine. No host synchronisation."""
+        op = torch.ops.hipserve
+        cfg = self.cfg
+        E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
+        T, dev = x.shape[0], x.device
+        P = T * k
+        tile = 16 if P <= 8 * E else (32 if P <= 32 * E else 64)
+        cap = -(-(P + E * (tile - 1)) // tile) * tile
+        logits = gemm.linear(x, lw.router)
+        w = torch.empty(T, k, dtype=torch.float32, device=dev)
+        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
+        op.moe_topk_softmax(w, ids, logits, k)
+        slots = torch.empty(cap, dtype=torch.int32, device=dev)
+        tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
+        ntiles = torch.empty(1, dtype=torch.int32, device=dev)
+        pair_slot = torch.empty(P, dtype=torch.int32, device=dev)
+        op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot)
+        gu = torch.empty(cap, 2 * self.inter, dtype=x.dtype, device=dev)
+        op.moe_gemm(gu, x, lw.w13, slots, tile_expert, tile, k)
+        act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+        self.ops.silu_and_mul(act, gu)
+        y = torch.empty(cap, H, dtype=x.dtype, device=dev)
+        op.moe_gemm(y, act, lw.w2, slots, tile_expert, tile, 0)
+        out = torch.empty(T, H, dtype=x.dtype, device=dev)
+        op.moe_combine(out, y, w, pair_slot, k)
+        return out
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = self.linear(hidden, self.lm_head)

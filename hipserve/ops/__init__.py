@@ -130,7 +130,7 @@ class ReferenceOps:
         return out
 
     def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
-        t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps)
+        t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, bf16_row=False)
         n = t.shape[0]
         out_tok[:n].copy_(t)
         if out_lp.numel():

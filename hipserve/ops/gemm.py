@@ -64,7 +64,10 @@ class GemmTuner:
         del g
         return v[len(v) // 2] * 1000.0 / n
 
+    @torch.inference_mode()
     def tune(self, shapes, device, ms=None):
+        # inference mode like the engine's graph capture: the generator state tensors a
+        # capture registers must not switch between inference and normal tensors
         ms = [m for m in (ms or TUNE_MS) if m <= 64]
         for (N, K) in sorted(set(shapes)):
             w = torch.randn(N, K, device=device, dtype=torch.bfloat16)

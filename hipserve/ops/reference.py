@@ -172,15 +172,18 @@ def uniform01(seed: int, step: int, n: int) -> np.ndarray:
     return (((h >> np.uint32(8)).astype(np.float64) + 0.5) / 16777216.0).astype(np.float32)
 
 
-def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, steps):
+def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, steps, bf16_row: bool = True):
     """Returns (tokens int64 [B], logprobs f32 [B]) with the kernel's semantics:
     greedy if T<=1e-5; else top-k then top-p (on the top-k-renormalised mass) then
-    a Gumbel-max draw with u = hash(seed, step, index)."""
+    a Gumbel-max draw with u = hash(seed, step, index). ``bf16_row`` mirrors the
+    kernel, which holds an fp32 row as bf16; the CPU engine samples full fp32."""
     B, V = logits.shape
     toks = torch.empty(B, dtype=torch.long)
     lps = torch.empty(B, dtype=torch.float32)
     # the kernel holds the row as bf16 in registers: sample on bf16-rounded logits
-    lf = logits.float().cpu().to(torch.bfloat16).float()
+    lf = logits.float().cpu()
+    if bf16_row:
+        lf = lf.to(torch.bfloat16).float()
     for r in range(B):
         x = lf[r]
         lse = torch.logsumexp(x, 0)

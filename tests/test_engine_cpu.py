@@ -62,6 +62,16 @@ def dense_logits(model, ids):
     return x[-1] @ model.lm_head.float().T
 
 
+def assert_greedy(model, prompt, toks, tol=1e-4):
+    """Teacher-forced check: every generated token is an argmax (within fp32
+    reduction-order noise) of the dense forward over the tokens before it."""
+    ids = list(prompt)
+    for i, t in enumerate(toks):
+        lg = dense_logits(model, ids)
+        assert lg[t] >= lg.max() - tol, (i, t, int(torch.argmax(lg)), float(lg.max() - lg[t]))
+        ids.append(t)
+
+
 def dense_greedy(model, ids, n):
     ids = list(ids)
     out = []
@@ -75,12 +85,17 @@ def dense_greedy(model, ids, n):
 @pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
 def test_engine_matches_dense(model):
     eng = make_engine(model)
+    for lw in eng.runner.model.layers:
+        if lw.router is not None:
+            # decisive routing: with std-0.02 routers the 2nd/3rd expert probabilities tie
+            # to ~1e-5, below fp32 reduction-order noise between batched and dense forwards
+            lw.router.mul_(50.0)
     prompts = [[1, 5, 9, 33, 70], list(range(3, 100)), [7] * 20, list(range(200, 261))]
     sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
     res = eng.generate(prompts, sp)
     for p, (toks, _, reason) in zip(prompts, res):
         assert reason == "length"
-        assert toks == dense_greedy(eng.runner.model, p, 10)
+        assert_greedy(eng.runner.model, p, toks)
 
 
 def test_chunked_prefill_and_prefix_cache_consistent():
@@ -91,7 +106,7 @@ def test_chunked_prefill_and_prefix_cache_consistent():
     b = eng.generate([p], sp)[0][0]  # second time: prefix-cache hit
     assert a == b
     assert eng.blocks.prefix_hit_tokens >= 96
-    assert a == dense_greedy(eng.runner.model, p, 6)
+    assert_greedy(eng.runner.model, p, a)
 
 
 def test_preemption_recompute_is_exact():
@@ -103,7 +118,7 @@ def test_preemption_recompute_is_exact():
     res = eng.generate(prompts, sp)
     assert eng.scheduler.num_preemptions > 0
     for p, r in zip(prompts, res):
-        assert r[0] == dense_greedy(eng.runner.model, p, 40)
+        assert_greedy(eng.runner.model, p, r[0])
 
 
 def test_stop_conditions():
