@@ -59,6 +59,11 @@ namespace hipserve {
 // skinny_gemm.hip — decode GEMM out[M,N] = x[M,K] . W[N,K]^T (M <= 64, K % (256*kw) == 0)
 bool launch_skinny_gemm(void* out, const void* x, long x_stride, const void* w, long out_stride, int M,
                         int N, int K, int rt, int kw, hipStream_t s);
+
+// decode_gemm.hip — split-K LDS-shared decode GEMM (M <= 64, K % (256*S) == 0). S > 1 needs
+// ws >= S*M*N fp32 and N % 8 == 0. Returns false for an uncompiled rt.
+bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
+                        int N, int K, int rt, int S, hipStream_t s);
 }  // namespace hipserve
 
 namespace hipserve {

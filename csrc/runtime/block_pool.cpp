@@ -204,8 +204,11 @@ py::tuple build_batch(const std::vector<std::vector<int>>& tables, const std::ve
 
 }  // namespace
 
+void register_shm_broadcast(py::module_& m);  // shm_broadcast.cpp
+
 PYBIND11_MODULE(_runtime, m) {
-  m.doc() = "hipserve native runtime (KV block pool, batch builder)";
+  m.doc() = "hipserve native runtime (KV block pool, batch builder, shared-memory step broadcast)";
+  register_shm_broadcast(m);
   py::class_<BlockPool>(m, "BlockPool")
       .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"),
            py::arg("prefix_caching") = true)

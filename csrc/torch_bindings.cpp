@@ -201,6 +201,26 @@ void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, 
                                     ids.data_ptr<int>(), T, logits.size(1), k, cur_stream());
 }
 
+void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::Tensor& ws, int64_t rt,
+                 int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  CHECK_CONTIG(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "decode_gemm: shape mismatch");
+  TORCH_CHECK(M >= 1 && M <= 64, "decode_gemm: 1 <= M <= 64");
+  TORCH_CHECK(splits >= 1 && K % (256 * splits) == 0, "decode_gemm: K must be a multiple of 256*splits");
+  TORCH_CHECK(N % 4 == 0 && out.stride(0) % 4 == 0 && x.stride(0) % 8 == 0, "decode_gemm: alignment");
+  if (splits > 1) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * N && N % 8 == 0,
+                "decode_gemm: fp32 workspace of S*M*N (N % 8 == 0) required for split-K");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
+                                           splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
+                                           w.data_ptr(), M, N, K, rt, splits, cur_stream()),
+              "decode_gemm: unsupported rt");
+}
+
 void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,
                at::Tensor& num_tiles, at::Tensor& pair_slot) {
   CHECK_DEV(ids);
@@ -259,6 +279,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale) -> ()");
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
+  m.def("decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int rt, int splits) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
@@ -273,6 +294,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("gguf_gemm", &gguf_gemm);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("decode_gemm", &decode_gemm);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

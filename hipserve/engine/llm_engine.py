@@ -10,6 +10,8 @@ import itertools
 import random
 import time
 
+import numpy as np
+
 from ..config import EngineConfig, ModelConfig, resolve_model_config
 from ..parallel.comm import TPGroup, get_tp
 from ..tokenizer import IncrementalDetokenizer, get_tokenizer
@@ -17,7 +19,9 @@ from .block_manager import BlockManager
 from .metrics import EngineMetrics
 from .model_runner import ModelRunner
 from .request import RequestOutput, SamplingParams, Sequence, Status
-from .scheduler import Scheduler
+from .scheduler import ScheduledSeq, Scheduler, SchedulerOutput
+
+PLACEHOLDER = -1  # output token whose value is still on the GPU (decode lookahead)
 
 
 class LLMEngine:
@@ -40,6 +44,8 @@ class LLMEngine:
         self.metrics = EngineMetrics()
         self.eos_ids = tuple(self.tokenizer.eos_token_ids or self.model_cfg.eos_token_id or ())
         self.last_step_time = time.monotonic()
+        self.lookahead = bool(cfg.extra.get("decode_lookahead", True)) and self.runner.use_graphs
+        self._inflight = None
 
     # ---------------------------------------------------------------- requests
     def new_request_id(self) -> str:
@@ -76,10 +82,20 @@ class LLMEngine:
         return seq
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_unfinished()
+        return self.scheduler.has_unfinished() or self._inflight is not None
 
     # ---------------------------------------------------------------- stepping
     def step(self) -> list[RequestOutput]:
+        """One engine iteration. Decode-only batches are pipelined one step deep
+        (``decode_lookahead``): step k+1 is scheduled with a placeholder for each
+        sequence's not-yet-known token, staged and launched on the GPU — its input
+        ids are taken on the device from step k's sampler output — BEFORE step k's
+        tokens are read back and processed on the host. The host bookkeeping
+        (stop checks, detokenisation, streaming) then overlaps GPU work instead of
+        leaving the GPU idle between steps. Anything else (prefill, admissions,
+        preemption, penalties, logprobs) runs synchronously."""
+        if self._inflight is not None:
+            return self._step_pipelined()
         so = self.scheduler.schedule()
         outputs: list[RequestOutput] = []
         for s in so.preempted:
@@ -89,30 +105,102 @@ class LLMEngine:
             return outputs
         t0 = time.monotonic()
         inp = self.runner.prepare(so)
+        if self.lookahead and self.runner.graph_eligible(inp):
+            self._inflight = self._launch(so, inp, t0)
+            return outputs
         if self.tp.world_size > 1:
             self.tp.broadcast_obj(("step", inp))
+        sampled = self._commit(so)
         toks, lps, top = self.runner.execute(inp)
         now = time.monotonic()
         self.metrics.on_step(so, now - t0, self.blocks.usage(), self.scheduler)
-        k = 0
+        outputs += self._process(so, sampled, toks, lps, top, now)
+        return outputs
+
+    # -- pipelined decode ---------------------------------------------------
+    def _launch(self, so, inp, t0, src=None):
+        inp.src = src
+        if self.tp.world_size > 1:
+            self.tp.broadcast_obj(("step", inp))
+        sampled = self._commit(so)
+        return (so, sampled, self.runner.launch(inp), t0)
+
+    def _step_pipelined(self) -> list[RequestOutput]:
+        so, sampled, handle, t0 = self._inflight
+        nxt = self._schedule_lookahead(sampled)
+        t1 = time.monotonic()
+        self._inflight = None
+        if nxt is not None:
+            so2, src = nxt
+            inp = self.runner.prepare(so2)
+            self._inflight = self._launch(so2, inp, t1, src)
+        toks, lps = self.runner.wait(handle)
+        now = time.monotonic()
+        self.metrics.on_step(so, now - t0, self.blocks.usage(), self.scheduler)
+        return self._process(so, sampled, toks, lps, None, now)
+
+    def _schedule_lookahead(self, sampled):
+        """Next decode-only batch while the previous step is still in flight, or
+        None when the batch composition cannot be predicted without its tokens."""
+        sch = self.scheduler
+        if sch.waiting or not sch.running:
+            return None
+        row = {id(seq): j for j, (seq, _) in enumerate(sampled)}
+        so = SchedulerOutput()
+        src = []
+        for seq in sch.running:
+            j = row.get(id(seq))
+            if j is None or seq.is_prefill:
+                return None
+            p = seq.params
+            if p.has_penalties or p.logprobs:
+                return None
+            n_out = len(seq.output_token_ids)
+            if (p.max_tokens is not None and n_out >= p.max_tokens) or seq.num_tokens >= self.max_model_len:
+                continue  # finishes with the in-flight token: not scheduled again
+            target = seq.num_computed_tokens + 1
+            if not self.blocks.can_grow(seq, target):
+                return None
+            self.blocks.grow(seq, target)
+            so.decode.append(ScheduledSeq(seq, seq.num_computed_tokens, target))
+            src.append(j)
+        if not so.decode or len(so.decode) > self.runner.max_graph_batch:
+            return None
+        return so, np.array(src, dtype=np.int64)
+
+    # -- bookkeeping ----------------------------------------------------------
+    def _commit(self, so):
+        """At launch: KV of the scheduled tokens counts as computed; each sampling
+        sequence gets a placeholder output token (filled in by ``_process``)."""
+        sampled = []
         for ss in so.prefill + so.decode:
             seq = ss.seq
+            samples = ss.samples
             seq.num_computed_tokens = ss.end
-            self.blocks.register(seq)
-            if not ss.samples:
-                continue
-            tok = int(toks[k])
-            lp = float(lps[k])
+            if samples:
+                seq.output_token_ids.append(PLACEHOLDER)
+                seq.output_logprobs.append(0.0)
+                sampled.append((seq, len(seq.output_token_ids) - 1))
+        return sampled
+
+    def _process(self, so, sampled, toks, lps, top, now):
+        outputs = []
+        for k, (seq, idx) in enumerate(sampled):
+            if seq.status == Status.FINISHED or seq.request_id not in self.seqs:
+                continue  # finished / aborted while this step was in flight
             top_k = None
             if top is not None and seq.params.logprobs:
                 n = seq.params.logprobs
                 top_k = [(int(i), float(v)) for i, v in zip(top[0][k][:n], top[1][k][:n])]
-            k += 1
-            outputs.append(self._append(seq, tok, lp, top_k, now))
+            outputs.append(self._append(seq, idx, int(toks[k]), float(lps[k]), top_k, now))
+        for ss in so.prefill + so.decode:
+            if ss.seq.status != Status.FINISHED:
+                self.blocks.register(ss.seq)
         self.last_step_time = now
+        self.metrics.flush()
         return outputs
 
-    def _append(self, seq: Sequence, tok: int, lp: float, top, now: float) -> RequestOutput:
+    def _append(self, seq: Sequence, idx: int, tok: int, lp: float, top, now: float) -> RequestOutput:
         p = seq.params
         if seq.first_token_time is None:
             seq.first_token_time = now
@@ -120,10 +208,10 @@ class LLMEngine:
         else:
             self.metrics.on_token(seq, now)
         seq.last_token_time = now
-        seq.output_token_ids.append(tok)
-        seq.output_logprobs.append(lp)
+        seq.output_token_ids[idx] = tok
+        seq.output_logprobs[idx] = lp
         reason = None
-        n_out = len(seq.output_token_ids)
+        n_out = idx + 1
         if not p.ignore_eos and tok in seq.eos_token_ids and n_out > p.min_tokens:
             reason = "stop"
         elif tok in p.stop_token_ids and n_out > p.min_tokens:
@@ -144,12 +232,14 @@ class LLMEngine:
         seq.output_text += text
         if reason is None and p.max_tokens is not None and n_out >= p.max_tokens:
             reason = "length"
-        if reason is None and seq.num_tokens >= self.max_model_len:
+        if reason is None and seq.num_prompt_tokens + n_out >= self.max_model_len:
             reason = "length"
         out = RequestOutput(seq.request_id, [tok], text, reason is not None, reason,
                             seq.num_prompt_tokens, n_out, [lp] if top is None else [lp, top],
                             seq.output_text)
         if reason is not None:
+            del seq.output_token_ids[n_out:]  # drop a look-ahead placeholder
+            del seq.output_logprobs[n_out:]
             self.scheduler.finish(seq, reason)
             self.metrics.on_finish(seq, now)
             self.seqs.pop(seq.request_id, None)
@@ -191,4 +281,7 @@ def worker_loop(runner: ModelRunner, tp: TPGroup):
         kind, inp = tp.broadcast_obj(None)
         if kind == "stop":
             return
-        runner.execute(inp)
+        if runner.graph_eligible(inp):
+            runner.launch(inp)  # no host readback on workers: keep the GPU queue fed
+        else:
+            runner.execute(inp)

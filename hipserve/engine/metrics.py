@@ -31,6 +31,15 @@ class EngineMetrics:
                                    buckets=_LAT_BUCKETS, registry=r)
         self.preemptions = Counter("hipserve_num_preemptions", "preempted sequences", lbl, registry=r)
         self.model_name = model_name
+        # bound label children: .labels() is a dict lookup + lock per call, too slow
+        # for the per-token path (64+ calls per decode step)
+        m = {"model_name": model_name}
+        self._ttft, self._itl, self._e2e = self.ttft.labels(**m), self.itl.labels(**m), self.e2e.labels(**m)
+        self._prompt, self._gen = self.prompt_tokens.labels(**m), self.gen_tokens.labels(**m)
+        self._running, self._waiting = self.running.labels(**m), self.waiting.labels(**m)
+        self._kv, self._step = self.kv_usage.labels(**m), self.step_time.labels(**m)
+        self._preempt = self.preemptions.labels(**m)
+        self._pending_gen = 0
         self.num_steps = 0
         self.total_gen = 0
         self.total_prompt = 0
@@ -44,31 +53,38 @@ class EngineMetrics:
 
     def on_step(self, so, dt, kv_usage, sched):
         self.num_steps += 1
-        self.step_time.labels(**self._l()).observe(dt)
+        self._step.observe(dt)
         n_prompt = sum(s.num_tokens for s in so.prefill)
         self.total_prompt += n_prompt
-        self.prompt_tokens.labels(**self._l()).inc(n_prompt)
-        self.running.labels(**self._l()).set(sched.num_running)
-        self.waiting.labels(**self._l()).set(sched.num_waiting)
-        self.kv_usage.labels(**self._l()).set(kv_usage)
+        if n_prompt:
+            self._prompt.inc(n_prompt)
+        self._running.set(sched.num_running)
+        self._waiting.set(sched.num_waiting)
+        self._kv.set(kv_usage)
         if so.preempted:
-            self.preemptions.labels(**self._l()).inc(len(so.preempted))
+            self._preempt.inc(len(so.preempted))
+        self.flush()
+
+    def flush(self):
+        if self._pending_gen:
+            self._gen.inc(self._pending_gen)
+            self._pending_gen = 0
 
     def on_first_token(self, seq, now):
         t = now - seq.arrival_time
         self.ttfts.append(t)
-        self.ttft.labels(**self._l()).observe(t)
+        self._ttft.observe(t)
         self.total_gen += 1
-        self.gen_tokens.labels(**self._l()).inc()
+        self._pending_gen += 1
 
     def on_token(self, seq, now):
         if seq.last_token_time is not None:
-            self.itl.labels(**self._l()).observe(now - seq.last_token_time)
+            self._itl.observe(now - seq.last_token_time)
         self.total_gen += 1
-        self.gen_tokens.labels(**self._l()).inc()
+        self._pending_gen += 1
 
     def on_finish(self, seq, now):
-        self.e2e.labels(**self._l()).observe(now - seq.arrival_time)
+        self._e2e.observe(now - seq.arrival_time)
         self.finished.labels(finished_reason=seq.finish_reason or "stop", **self._l()).inc()
 
 

@@ -50,6 +50,9 @@ class StepInputs:
     steps: np.ndarray
     penalties: list | None = None         # per logits row: None | (presence, freq, rep, ids)
     top_logprobs: int = 0
+    # decode lookahead: per decode row, the row of the PREVIOUS graph step's sampled
+    # tokens that is this row's input id (-1: use ids[row]); consumed on the device
+    src: np.ndarray | None = None
     extra: dict = field(default_factory=dict)
 
 
@@ -231,7 +234,7 @@ class ModelRunner:
                 if pen is None:
                     pen = [None] * n
                 pen[i] = (p.presence_penalty, p.frequency_penalty, p.repetition_penalty,
-                          q.prompt_token_ids, q.output_token_ids)
+                          q.prompt_token_ids, list(q.output_token_ids))
             if p.logprobs:
                 topn = max(topn, p.logprobs)
         return StepInputs(ids, pos, slots, Tp, len(so.decode), bt_p, cu_q, ctx_p, tiles, bt_d, ctx_d,
@@ -246,14 +249,23 @@ class ModelRunner:
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t
 
+    @property
+    def max_graph_batch(self) -> int:
+        return self.buckets[-1] if self.use_graphs else 0
+
+    def graph_eligible(self, inp: StepInputs) -> bool:
+        return (self.use_graphs and inp.num_prefill_tokens == 0 and inp.penalties is None
+                and inp.top_logprobs == 0 and 0 < inp.num_decode <= self.buckets[-1])
+
     @torch.inference_mode()
     def execute(self, inp: StepInputs):
         """Returns (tokens np.int64 [n], logprobs np.float32 [n], top_logprobs or None)."""
         n = len(inp.logits_rows)
-        if (self.use_graphs and inp.num_prefill_tokens == 0 and inp.penalties is None
-                and inp.top_logprobs == 0 and 0 < inp.num_decode <= self.buckets[-1]):
-            tok, lp = self._run_graph(inp)
+        if self.graph_eligible(inp):
+            tok, lp = self.wait(self.launch(inp))
             return tok, lp, None
+        if inp.src is not None:
+            raise RuntimeError("device-side input ids (lookahead) need the hipGraph decode path")
         ids = self._t(inp.ids)
         meta = AttnMeta(
             num_prefill_tokens=inp.num_prefill_tokens, num_decode=inp.num_decode,
@@ -305,7 +317,9 @@ class ModelRunner:
         meta = AttnMeta(num_prefill_tokens=0, num_decode=b, positions=st["pos"][:b],
                         slot_mapping=st["slots"][:b], bt_decode=st["bt"][:b], ctx_decode=st["ctx"][:b],
                         tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
-        hidden = self.model.forward(st["ids"][:b], meta, self.kv)
+        src = st["src"][:b]
+        ids = torch.where(src >= 0, st["tok"].index_select(0, src.clamp(min=0)), st["ids"][:b])
+        hidden = self.model.forward(ids, meta, self.kv)
         logits = self.model.compute_logits(hidden)
         self.ops.sample(st["tok"][:b], st["lp"][:b], logits, st["temp"][:b], st["topk"][:b],
                         st["topp"][:b], st["seeds"][:b], st["steps"][:b])
@@ -313,17 +327,26 @@ class ModelRunner:
     @torch.inference_mode()
     def _capture_graphs(self):
         mb, W, dev = self.buckets[-1], self.width, self.device
-        # host staging (pinned) and device static buffers, one region per dtype
-        self._h64 = torch.zeros(5 * mb, dtype=torch.long).pin_memory()
-        self._h32 = torch.zeros(mb * W + 2 * mb, dtype=torch.int32).pin_memory()
-        self._hf = torch.zeros(2 * mb, dtype=torch.float32).pin_memory()
-        d64 = torch.zeros(5 * mb, dtype=torch.long, device=dev)
+        # host staging (pinned, double-buffered by launch parity so step k+1 can be
+        # staged while step k runs) and device static buffers, one region per dtype
+        self._stage = []
+        for _ in range(2):
+            self._stage.append({
+                "h64": torch.zeros(6 * mb, dtype=torch.long).pin_memory(),
+                "h32": torch.zeros(mb * W + 2 * mb, dtype=torch.int32).pin_memory(),
+                "hf": torch.zeros(2 * mb, dtype=torch.float32).pin_memory(),
+                "tok": torch.zeros(mb, dtype=torch.long).pin_memory(),
+                "lp": torch.zeros(mb, dtype=torch.float32).pin_memory(),
+                "done": None,
+            })
+        self._launches = 0
+        d64 = torch.zeros(6 * mb, dtype=torch.long, device=dev)
         d32 = torch.zeros(mb * W + 2 * mb, dtype=torch.int32, device=dev)
         df = torch.zeros(2 * mb, dtype=torch.float32, device=dev)
         st = {
             "d64": d64, "d32": d32, "df": df,
             "ids": d64[0:mb], "pos": d64[mb:2 * mb], "slots": d64[2 * mb:3 * mb],
-            "seeds": d64[3 * mb:4 * mb], "steps": d64[4 * mb:5 * mb],
+            "seeds": d64[3 * mb:4 * mb], "steps": d64[4 * mb:5 * mb], "src": d64[5 * mb:6 * mb],
             "bt": d32[: mb * W].view(mb, W), "ctx": d32[mb * W: mb * W + mb],
             "topk": d32[mb * W + mb: mb * W + 2 * mb],
             "temp": df[0:mb], "topp": df[mb:2 * mb],
@@ -335,6 +358,7 @@ class ModelRunner:
         st["ctx"].fill_(1)
         st["slots"].fill_(self.pad_block * self.block_size)
         st["topp"].fill_(1.0)
+        st["src"].fill_(-1)
         t0 = time.time()
         stream = torch.cuda.Stream(device=dev)
         stream.wait_stream(torch.cuda.current_stream(dev))
@@ -352,11 +376,19 @@ class ModelRunner:
         torch.cuda.synchronize(dev)
         self.graph_capture_time = time.time() - t0
 
-    def _run_graph(self, inp: StepInputs):
+    @torch.inference_mode()
+    def launch(self, inp: StepInputs):
+        """Stage inputs and replay the decode hipGraph WITHOUT waiting; the sampled
+        ids are copied into pinned host memory behind the graph. Returns a handle
+        for ``wait``. Safe to call again before waiting (parity double buffer)."""
         n = inp.num_decode
         b = next(x for x in self.buckets if x >= n)
         mb, W = self.buckets[-1], self.width
-        h64, h32, hf = self._h64, self._h32, self._hf
+        sg = self._stage[self._launches & 1]
+        self._launches += 1
+        if sg["done"] is not None:
+            sg["done"].synchronize()  # the launch two steps ago read this staging set
+        h64, h32, hf = sg["h64"], sg["h32"], sg["hf"]
         pad_slot = self.pad_block * self.block_size
         a64 = h64.numpy()
         a64[0:n] = inp.ids
@@ -367,6 +399,11 @@ class ModelRunner:
         a64[2 * mb + n:2 * mb + b] = pad_slot
         a64[3 * mb:3 * mb + n] = inp.seeds
         a64[4 * mb:4 * mb + n] = inp.steps
+        if inp.src is not None:
+            a64[5 * mb:5 * mb + n] = inp.src
+        else:
+            a64[5 * mb:5 * mb + n] = -1
+        a64[5 * mb + n:5 * mb + b] = -1
         a32 = h32.numpy()
         btv = a32[: mb * W].reshape(mb, W)
         btv[:n] = inp.bt_decode
@@ -384,6 +421,14 @@ class ModelRunner:
         st["d32"][mb * W:].copy_(h32[mb * W:], non_blocking=True)
         st["df"].copy_(hf, non_blocking=True)
         self.graphs[b].replay()
-        tok = st["tok"][:n].cpu().numpy()
-        lp = st["lp"][:n].cpu().numpy()
-        return tok, lp
+        sg["tok"][:n].copy_(st["tok"][:n], non_blocking=True)
+        sg["lp"][:n].copy_(st["lp"][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        sg["done"] = ev
+        return (sg, n, ev)
+
+    def wait(self, handle):
+        sg, n, ev = handle
+        ev.synchronize()
+        return sg["tok"][:n].numpy().copy(), sg["lp"][:n].numpy().copy()

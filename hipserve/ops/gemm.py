@@ -1,9 +1,13 @@
-"""bf16 linear layers: hipBLASLt (``F.linear``) or the hand-written skinny MFMA
-GEMM (``csrc/kernels/skinny_gemm.hip``) for decode batches.
+"""bf16 linear layers: hipBLASLt (``F.linear``) or a hand-written MFMA GEMM for
+decode batches — the split-K LDS-shared ``decode_gemm`` (csrc/kernels/decode_gemm.hip)
+or the skinny weight-streaming GEMM (csrc/kernels/skinny_gemm.hip).
 
-The choice is made per (M, N, K) by timing both on the device once, before the
-decode hipGraphs are captured (``GemmTuner.tune``); the captured graphs then bake
-in the winner. Nothing is dispatched per call at run time except a dict lookup.
+The choice is made per (M, N, K) by timing the candidates on the device once,
+before the decode hipGraphs are captured (``GemmTuner.tune``); the captured graphs
+then bake in the winner. Nothing is dispatched per call at run time except a dict
+lookup. Timing is cold-cache: every timed call reads a different copy of the
+weight, cycling through >= 1 GiB so the 256 MiB MALL cannot serve a weight that a
+real decode step streams from HBM once per layer.
 """
 from __future__ import annotations
 
@@ -17,6 +21,9 @@ log = logging.getLogger("hipserve.gemm")
 SKINNY_CONFIGS = [(1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (2, 1), (2, 2), (2, 4), (2, 8)]
 # split-K MFMA GEMM with an LDS-staged x chunk shared by 64 rows (gguf.hip, qtype 6 = bf16)
 SPLITK_CONFIGS = [1, 2, 4, 8]
+DG_RT = [1, 2]
+DG_SPLITS = [1, 2, 4, 7, 8, 14, 16]
+COLD_BYTES = 1 << 30
 _EMPTY = {}
 TUNE_MS = [1, 2, 4, 8, 16, 24, 32, 48, 64]
 
@@ -37,19 +44,20 @@ class GemmTuner:
     @staticmethod
     def _time(fn, n=16, reps=5):
         """Device time per call inside a hipGraph (how decode runs), so host
-        launch cost — which differs between hipBLASLt and our ops — is excluded."""
-        for _ in range(3):
-            fn()
+        launch cost — which differs between hipBLASLt and our ops — is excluded.
+        ``fn(i)`` is called with the call index (to rotate weight copies)."""
+        for i in range(3):
+            fn(i)
         torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            fn()
+            fn(0)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(n):
-                fn()
+            for i in range(n):
+                fn(i)
         g.replay()
         torch.cuda.synchronize()
         ts = []
@@ -70,29 +78,40 @@ class GemmTuner:
         # capture registers must not switch between inference and normal tensors
         ms = [m for m in (ms or TUNE_MS) if m <= 64]
         for (N, K) in sorted(set(shapes)):
-            w = torch.randn(N, K, device=device, dtype=torch.bfloat16)
+            ncopy = max(1, min(16, -(-COLD_BYTES // (N * K * 2))))
+            ws_ = [torch.randn(N, K, device=device, dtype=torch.bfloat16) for _ in range(ncopy)]
+            n = max(16, ncopy)
             for M in ms:
                 x = torch.randn(M, K, device=device, dtype=torch.bfloat16)
                 out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
-                best, best_t = "blas", self._time(lambda: F.linear(x, w))
+                best, best_t = "blas", self._time(lambda i: F.linear(x, ws_[i % ncopy]), n=n)
                 t_blas = best_t
-                for rt, kw in SKINNY_CONFIGS:
-                    if K % (256 * kw):
-                        continue
-                    t = self._time(lambda: torch.ops.hipserve.skinny_gemm(out, x, w, rt, kw))
+                for cfg in self.candidates(M, N, K):
+                    t = self._time(lambda i: run_choice(cfg, out, x, ws_[i % ncopy]), n=n)
                     if t < best_t * 0.97:
-                        best, best_t = (rt, kw), t
-                for sp in SPLITK_CONFIGS:
-                    if (K // 256) < sp:
-                        continue
-                    t = self._time(lambda: splitk_gemm(out, x, w, sp))
-                    if t < best_t * 0.97:
-                        best, best_t = ("splitk", sp), t
+                        best, best_t = cfg, t
                 self.table[(M, N, K)] = best
                 self.report.append({"M": M, "N": N, "K": K, "blas_us": round(t_blas, 1),
-                                    "best": str(best), "best_us": round(best_t, 1)})
-            del w
+                                    "best": str(best), "best_us": round(best_t, 1),
+                                    "best_TBps": round(N * K * 2 / best_t / 1e6, 2)})
+            del ws_
         return self.report
+
+    @staticmethod
+    def candidates(M, N, K):
+        out = []
+        for rt in DG_RT:
+            tiles = -(-N // (64 * rt))
+            for sp in DG_SPLITS:
+                if K % (256 * sp) or (sp > 1 and N % 8) or tiles * sp > 4096:
+                    continue
+                if sp > 1 and tiles * sp // 2 >= 1024:  # plenty of workgroups already
+                    continue
+                out.append(("dg", rt, sp))
+        for rt, kw in SKINNY_CONFIGS:
+            if K % (256 * kw) == 0:
+                out.append(("sk", rt, kw))
+        return out
 
 
 TUNER = GemmTuner()
@@ -115,14 +134,30 @@ def splitk_gemm(out, x, w, splits):
     return out
 
 
+def decode_gemm(out, x, w, rt, splits):
+    M, N = x.shape[0], w.shape[0]
+    ws = (torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1
+          else _empty(x.device)[1])
+    torch.ops.hipserve.decode_gemm(out, x, w, ws, rt, splits)
+    return out
+
+
+def run_choice(c, out, x, w):
+    if c[0] == "dg":
+        return decode_gemm(out, x, w, c[1], c[2])
+    if c[0] == "sk":
+        torch.ops.hipserve.skinny_gemm(out, x, w, c[1], c[2])
+        return out
+    if c[0] == "splitk":
+        return splitk_gemm(out, x, w, c[1])
+    raise ValueError(c)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     M = x.shape[0]
     if M <= 64 and x.is_cuda and TUNER.table:
         c = TUNER.choose(M, w.shape[0], w.shape[1])
         if c != "blas" and x.stride(1) == 1 and x.stride(0) % 8 == 0:
             out = torch.empty(M, w.shape[0], device=x.device, dtype=x.dtype)
-            if c[0] == "splitk":
-                return splitk_gemm(out, x, w, c[1])
-            torch.ops.hipserve.skinny_gemm(out, x, w, c[0], c[1])
-            return out
+            return run_choice(c, out, x, w)
     return F.linear(x, w)

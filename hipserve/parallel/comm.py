@@ -8,7 +8,10 @@ Collectives on the hot path:
   * ``all_reduce``  — sum after the row-parallel o_proj / down_proj (2 per layer)
     and after the vocab-parallel embedding;
   * ``all_gather``  — LM-head logits shards -> full vocab on every rank;
-  * ``broadcast_obj`` — step metadata from the rank-0 scheduler to workers.
+  * ``broadcast_obj`` — step metadata from the rank-0 scheduler to workers, over
+    the native shared-memory ring (csrc/runtime/shm_broadcast.cpp) when all ranks
+    share a host (always, for TP inside one pod), gloo otherwise / for oversize
+    messages.
 All ops are in place / into preallocated outputs so decode steps are capturable
 into hipGraphs (RCCL collectives are graph-capturable on ROCm).
 """
@@ -16,6 +19,9 @@ from __future__ import annotations
 
 import datetime
 import os
+import pickle
+import socket
+import uuid
 
 import torch
 import torch.distributed as dist
@@ -28,6 +34,34 @@ class TPGroup:
         self.group = group
         self.device = device
         self._cpu_group = None
+        self._ring = None
+
+    SHM_SLOT_BYTES = 8 << 20
+    SHM_SLOTS = 4
+
+    def setup_shm_ring(self):
+        """Attach the shared-memory step ring (collective over the CPU group)."""
+        if self.world_size == 1 or os.environ.get("HIPSERVE_SHM_BROADCAST", "1") == "0":
+            return False
+        try:
+            from .. import runtime
+            rt = runtime.native()
+        except Exception:  # native runtime unavailable: stay on gloo
+            rt = None
+        hosts = [None] * self.world_size
+        dist.all_gather_object(hosts, (socket.gethostname(), rt is not None), group=self._cpu_group)
+        if not all(h == hosts[0][0] and ok for h, ok in hosts):
+            return False
+        name = [f"/hipserve_tp_{uuid.uuid4().hex[:12]}" if self.rank == 0 else None]
+        if self.rank == 0:
+            self._ring = rt.ShmBroadcast(name[0], self.world_size - 1, self.SHM_SLOT_BYTES,
+                                         self.SHM_SLOTS, 0, True)
+        dist.broadcast_object_list(name, src=0, group=self._cpu_group)
+        if self.rank != 0:
+            self._ring = rt.ShmBroadcast(name[0], self.world_size - 1, self.SHM_SLOT_BYTES,
+                                         self.SHM_SLOTS, self.rank, False)
+        dist.barrier(group=self._cpu_group)
+        return True
 
     @property
     def is_first(self):
@@ -52,9 +86,21 @@ class TPGroup:
         return parts.permute(1, 0, 2).reshape(t.shape[0], -1)
 
     def broadcast_obj(self, obj=None):
-        """Rank 0 -> all ranks over the CPU (gloo) group; returns the object."""
+        """Rank 0 -> all ranks; returns the object. Shared-memory ring when set up
+        (tag byte 0 = inline pickle, 1 = too large, follows over gloo)."""
         if self.world_size == 1:
             return obj
+        if self._ring is not None:
+            if self.rank == 0:
+                data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+                if len(data) + 1 <= self._ring.slot_capacity:
+                    self._ring.publish(b"\x00" + data)
+                    return obj
+                self._ring.publish(b"\x01")
+            else:
+                msg = self._ring.recv()
+                if msg[:1] == b"\x00":
+                    return pickle.loads(msg[1:])
         lst = [obj]
         dist.broadcast_object_list(lst, src=0, group=self._cpu_group)
         return lst[0]
@@ -91,6 +137,7 @@ def init_tp(world_size: int | None = None, backend: str | None = None, device_ty
                                 timeout=datetime.timedelta(seconds=600))
     g = TPGroup(rank, ws, dist.group.WORLD, dev)
     g._cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
+    g.setup_shm_ring()
     _TP = g
     return g
 

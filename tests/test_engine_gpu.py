@@ -100,3 +100,44 @@ def test_mixtral_graph_matches_eager_and_cpu():
         assert a[0][:2] == b[0][:2]
     first = sum(a[0][0] == b[0][0] for a, b in zip(rg, rc))
     assert first >= len(PROMPTS) - 1, (rg, rc)
+
+
+def _engine_la(lookahead, **kw):
+    base = dict(model="small-llama", device="cuda", max_num_seqs=16, max_num_batched_tokens=256,
+                max_model_len=2048, num_kv_blocks=512, extra={"decode_lookahead": lookahead})
+    base.update(kw)
+    return LLMEngine(EngineConfig(**base), tp=TPGroup(0, 1, None, torch.device("cuda", 0)))
+
+
+def test_decode_lookahead_matches_sync():
+    """Pipelined decode (device-side input ids, host bookkeeping one step behind)
+    must produce exactly the synchronous engine's tokens."""
+    a, b = _engine_la(True), _engine_la(False)
+    assert a.lookahead and not b.lookahead
+    prompts = PROMPTS + [[1, 2, 3], list(range(50, 90))]
+    sps = [SamplingParams(temperature=0.0 if i % 2 else 0.7, seed=i, max_tokens=5 + 7 * i, ignore_eos=True)
+           for i in range(len(prompts))]
+    ra, rb = a.generate(prompts, sps), b.generate(prompts, sps)
+    for x, y, sp in zip(ra, rb, sps):
+        assert len(x[0]) == sp.max_tokens and x[2] == "length"
+        assert x[0] == y[0]
+    assert not a.has_unfinished() and a.scheduler.num_running == 0
+    assert a.blocks.num_free() == b.blocks.num_free()
+
+
+def test_decode_lookahead_stop_tokens():
+    """A sequence stopping on a token while the next step is already in flight:
+    no token past the stop is emitted and its placeholder is dropped."""
+    e = _engine_la(True)
+    free0 = e.blocks.num_free()
+    g = e.generate([PROMPTS[0]], SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True))[0][0]
+    stop = g[5]
+    first = g.index(stop)
+    res = e.generate([PROMPTS[0], PROMPTS[2]],
+                     [SamplingParams(temperature=0.0, max_tokens=12, stop_token_ids=[stop]),
+                      SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)])
+    assert res[0][0] == g[:first + 1] and res[0][2] == "stop"
+    assert len(res[1][0]) == 12
+    assert not e.has_unfinished()
+    e.blocks.reset_prefix_cache()
+    assert e.blocks.num_free() == free0

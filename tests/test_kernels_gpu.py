@@ -197,6 +197,25 @@ def test_splitk_bf16_gemm(ops, M, splits):
     _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
 
 
+@pytest.mark.parametrize("M", [1, 7, 16, 23, 32, 50, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 512), (6144, 1792)])
+@pytest.mark.parametrize("rt", [1, 2])
+@pytest.mark.parametrize("splits", [1, 2, 7])
+def test_decode_gemm(ops, M, N, K, rt, splits):
+    """Split-K LDS-shared decode GEMM vs fp32 torch (incl. ragged M, N tails, strided x)."""
+    from hipserve.ops.gemm import decode_gemm
+    if K % (256 * splits):
+        pytest.skip("K not divisible")
+    torch.manual_seed(M * 7 + N)
+    xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
+    x = xb[:, :K]  # row stride != K
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    decode_gemm(out, x, w, rt, splits)
+    want = x.float() @ w.float().T
+    _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
+
+
 @pytest.mark.parametrize("T,E,k", [(1, 8, 2), (13, 8, 2), (64, 8, 2), (200, 8, 2), (5, 4, 1)])
 def test_moe_kernels_match_reference(ops, T, E, k):
     """HIP MoE (topk softmax, align, gathered GEMMs, combine) vs the torch path."""

@@ -128,8 +128,39 @@ def main():
 def bench_tune():
     from hipserve.ops import gemm
     shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]
-    for r in gemm.TUNER.tune(shapes, torch.device("cuda"), [1, 16, 32, 64]):
+    import time
+    t0 = time.time()
+    ms = [int(m) for m in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 16, 32, 64]
+    for r in gemm.TUNER.tune(shapes, torch.device("cuda"), ms):
         emit(op="gemm_tune", **r)
+    emit(op="gemm_tune_total_s", seconds=round(time.time() - t0, 1))
+
+
+def bench_gemm_sweep():
+    """Every decode-GEMM candidate vs hipBLASLt, cold weights (tuner timing)."""
+    import torch.nn.functional as F
+    from hipserve.ops import gemm
+    T = gemm.GemmTuner
+    shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
+    ms = [int(m) for m in sys.argv[2].split(",")] if len(sys.argv) > 2 else [64]
+    for N, K in shapes:
+        ncopy = max(1, min(16, -(-gemm.COLD_BYTES // (N * K * 2))))
+        ws_ = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) for _ in range(ncopy)]
+        n = max(16, ncopy)
+        for M in ms:
+            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            res = {"blas": T._time(lambda i: F.linear(x, ws_[i % ncopy]), n=n)}
+            for cfg in T.candidates(M, N, K):
+                res[str(cfg)] = T._time(lambda i: gemm.run_choice(cfg, out, x, ws_[i % ncopy]), n=n)
+            emit(op="gemm_sweep", M=M, N=N, K=K, **{k: round(v, 1) for k, v in sorted(res.items(), key=lambda kv: kv[1])[:8]})
+        del ws_
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
+    KernelOps()
+    bench_gemm_sweep()
+    sys.exit(0)
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "tune":

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 rocpd SQLite database (``--kernel-trace --stats`` writes
+``<dir>/<name>_results.db``) into a markdown report for ``profiles/``:
+
+* per-kernel-family totals (same grouping as ``prof_summary.py``),
+* the engine timeline split into steps at each ``sample_kernel`` dispatch, with
+  decode-only steps (no prefill attention) separated from prefill/mixed steps,
+* per-decode-step kernel breakdown and GPU idle time (gaps between kernels,
+  i.e. host/launch overhead not hidden by the hipGraph).
+
+usage: python tools/prof_db.py run_results.db [out.md] [title]
+"""
+import sqlite3
+import statistics
+import sys
+
+from prof_summary import family
+
+
+def load(path):
+    c = sqlite3.connect(path)
+    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    return [(family(n), s, e) for n, s, e in rows]
+
+
+def steps(rows):
+    out, cur = [], []
+    for r in rows:
+        cur.append(r)
+        if "sample_kernel" in r[0]:
+            out.append(cur)
+            cur = []
+    return out
+
+
+def summarize(path, title="rocprofv3 kernel trace"):
+    rows = load(path)
+    tot = {}
+    for f, s, e in rows:
+        a = tot.setdefault(f, [0, 0])
+        a[0] += 1
+        a[1] += e - s
+    total = sum(v[1] for v in tot.values())
+    L = [f"# {title}", "", f"kernels: {len(rows)}, total kernel time {total / 1e6:.1f} ms", "",
+         "## all kernels by family", "", "| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
+    for f, (n, d) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:40]:
+        L.append(f"| `{f}` | {n} | {d / 1e6:.1f} | {d / n / 1e3:.1f} | {100 * d / total:.1f} |")
+    st = steps(rows)
+    dec = [s for s in st if not any("prefill_attn" in r[0] for r in s)]
+    pre = [s for s in st if any("prefill_attn" in r[0] for r in s)]
+    # drop the capture/warm-up outliers: keep decode steps with the modal kernel count
+    if dec:
+        mode = statistics.mode(len(s) for s in dec)
+        dec = [s for s in dec if len(s) == mode]
+
+    def span(s):
+        return (s[-1][2] - s[0][1]) / 1e3
+
+    def busy(s):
+        return sum(e - b for _, b, e in s) / 1e3
+
+    L += ["", "## engine steps", "",
+          f"steps: {len(st)} ({len(pre)} with prefill, {len(dec)} decode-only of the modal shape)"]
+    if pre:
+        sp = [span(s) for s in pre]
+        L.append(f"prefill/mixed step: median span {statistics.median(sp):.0f} us, "
+                 f"kernel-busy {statistics.median(busy(s) for s in pre):.0f} us")
+    if dec:
+        sp = [span(s) for s in dec]
+        bz = [busy(s) for s in dec]
+        L += [f"decode step: median span {statistics.median(sp):.0f} us, kernel-busy "
+              f"{statistics.median(bz):.0f} us, idle {statistics.median(sp) - statistics.median(bz):.0f} us "
+              f"({len(dec[0])} kernels/step)", "", "### per decode step (median over steps)", "",
+              "| kernel | calls/step | us/step | avg us |", "|---|---:|---:|---:|"]
+        per = {}
+        for s in dec:
+            acc = {}
+            for f, b, e in s:
+                a = acc.setdefault(f, [0, 0])
+                a[0] += 1
+                a[1] += e - b
+            for f, (n, d) in acc.items():
+                per.setdefault(f, []).append((n, d))
+        agg = sorted(((f, v[0][0], statistics.median(d for _, d in v) / 1e3) for f, v in per.items()),
+                     key=lambda x: -x[2])
+        for f, n, d in agg:
+            L.append(f"| `{f}` | {n} | {d:.1f} | {d / n:.2f} |")
+    return "\n".join(L) + "\n"
+
+
+if __name__ == "__main__":
+    text = summarize(sys.argv[1], *(sys.argv[3:4] or []))
+    if len(sys.argv) > 2:
+        open(sys.argv[2], "w").write(text)
+    print(text)
