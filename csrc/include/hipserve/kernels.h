@@ -60,6 +60,19 @@ namespace hipserve {
 bool launch_skinny_gemm(void* out, const void* x, long x_stride, const void* w, long out_stride, int M,
                         int N, int K, int rt, int kw, hipStream_t s);
 
+// allreduce.hip — custom all-reduce over HIP-IPC peer memory (one-shot / two-shot)
+void* car_create(int rank, int world, size_t max_bytes);
+void car_get_handle(void* state, void* handle_out);
+void car_open(void* state, int peer, const void* handle);
+bool car_error(void* state);
+void car_destroy(void* state);
+size_t car_max_bytes(void* state);
+void launch_car(void* state, const void* inp, void* out, size_t bytes, bool two_shot, int blocks, hipStream_t s);
+
+// init.hip — on-device synthetic weights keyed by global coordinates (TP-invariant)
+void launch_fill_uniform(void* out, long ld, int rows, int cols, long row0, long col0, long gcols,
+                         unsigned int key, float scale, hipStream_t s);
+
 // decode_gemm.hip — split-K LDS-shared decode GEMM (M <= 64, K % (256*S) == 0). S > 1 needs
 // ws >= S*M*N fp32 and N % 8 == 0. Returns false for an uncompiled rt.
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,

@@ -3,14 +3,16 @@
 //
 // Why not the skinny kernel (one x read per 16 W rows): at M = 64 the activation
 // re-reads from L2 (M/16 = 4x the weight bytes) throttle the HBM stream. Here
-//  * a workgroup owns NW = 16*RT*NWAVES weight rows and one K slice; the x slice
-//    [16*MT, 256] for the current 256-k step is staged in LDS (double-buffered,
+//  * a workgroup owns NW = 128 weight rows and one K slice; the x slice
+//    [16*MT, 256] for the current 256-k step is staged in LDS (3-deep ring,
 //    528 B rows = conflict-free ds_read_b128) and shared by all waves, so L2->CU
 //    activation traffic drops to M/NW of the weight bytes;
 //  * MFMA k order is permuted so that each 16-byte load instruction of a wave
 //    covers 16 rows x 64 contiguous bytes (4 lane groups side by side) rather than
 //    64 scattered 16-byte pieces; two 256-k steps (512 B per row each) are kept
-//    in flight in a VGPR ring ahead of the MFMAs — weights are read exactly once;
+//    in flight in a VGPR ring ahead of the MFMAs (non-temporal: read once) —
+//    and they are issued AFTER the next x slice so the in-order vmcnt wait before
+//    the LDS store does not drain them;
 //  * out^T = W . x^T on v_mfma_f32_16x16x32_bf16: each W fragment feeds MT MFMAs
 //    and each LDS x fragment feeds RT MFMAs;
 //  * small-N projections (o_proj / down N = 4096 -> 32 workgroups of 128 rows) are
@@ -26,7 +28,7 @@ namespace hipserve {
 
 constexpr int DG_LDS_ROW = 264;  // 256 + 8 bf16 pad -> 528 B row stride
 
-template <int MT, int RT, int NWAVES>
+template <int MT, int RT, int NWAVES, int NSTEPS>
 __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     unsigned short* __restrict__ out, long out_stride, float* __restrict__ ws,
     const unsigned short* __restrict__ x, long x_stride, const unsigned short* __restrict__ w,
@@ -35,12 +37,14 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
   constexpr int XR = 16 * MT;                 // x rows staged (padded M)
   constexpr int NT = 64 * NWAVES;             // threads
   constexpr int XPASS = XR * 32 / NT;         // 16-byte x loads per thread per step
-  __shared__ __attribute__((aligned(16))) unsigned short xs[2][XR * DG_LDS_ROW];
+  __shared__ __attribute__((aligned(16))) unsigned short xs[3][XR * DG_LDS_ROW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int split = blockIdx.x / tiles, tile = blockIdx.x - split * tiles;
-  const int ks = K / S, k0 = split * ks, nsteps = ks / 256;
+  constexpr int nsteps = NSTEPS;  // K slice = 256 * NSTEPS, fully unrolled: straight-line
+                                  // code lets hipcc count every vmcnt exactly
+  const int k0 = split * 256 * NSTEPS;
   const int nbase = tile * NW + wave * 16 * RT;
 
   const unsigned short* wr[RT];
@@ -53,8 +57,10 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
 #pragma unroll
     for (int p = 0; p < XPASS; ++p) {
       const int idx = p * NT + tid, row = idx >> 5, col = (idx & 31) * 8;
-      xv[p] = row < M ? *reinterpret_cast<const u16x8*>(x + (long)row * x_stride + k0 + step * 256 + col)
-                      : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      // rows >= M are clamped, not zeroed: they only feed output columns m >= M,
+      // which are never stored, and a per-lane select around a load makes hipcc
+      // branch and drain vmcnt(0) — the whole weight prefetch — every step
+      xv[p] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + k0 + step * 256 + col);
     }
   };
   auto store_x = [&](int buf) {
@@ -71,23 +77,33 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // weights: 3-deep register ring (two 256-k steps in flight while one is consumed);
-  // x: LDS double buffer, one step ahead
-  u16x8 a0[RT][8], a1[RT][8], a2[RT][8];
-  auto load_w = [&](u16x8 (&dst)[RT][8], int step) {
-    if (step < nsteps) {
+  // Both operands run two 256-k steps ahead, issued in the order x(st+2), W(st+2)
+  // every step, so each in-order vmcnt wait (x into LDS one step ahead, W for the
+  // MFMAs) leaves the younger step's loads in flight: weights in a 3-deep VGPR
+  // ring, x through registers into a 3-deep LDS ring.
+  u16x8 ring[3][RT][8];
+  auto load_w = [&](int slot, int step) {
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT; ++r)
 #pragma unroll
-        for (int s = 0; s < 8; ++s) dst[r][s] = *reinterpret_cast<const u16x8*>(wr[r] + step * 256 + 32 * s);
-    }
+      for (int s = 0; s < 8; ++s)
+        ring[slot][r][s] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wr[r] + step * 256 + 32 * s));
   };
-  auto body = [&](u16x8 (&cur)[RT][8], u16x8 (&refill)[RT][8], int st) {
-    const int buf = st & 1;
-    const bool more = st + 1 < nsteps;
-    load_w(refill, st + 2);
-    if (more) load_x(st + 1);
-    const unsigned short* xb = &xs[buf][c * DG_LDS_ROW + 8 * g];
+  // prologue: x(0) -> LDS[0]; x(1) in registers; W(0), W(1) in flight
+  load_x(0);
+  store_x(0);
+  if (nsteps > 1) load_x(1);
+  load_w(0, 0);
+  if (nsteps > 1) load_w(1, 1);
+  __syncthreads();
+#pragma unroll
+  for (int st = 0; st < nsteps; ++st) {
+    if (st + 1 < nsteps) store_x((st + 1) % 3);  // x(st+1), loaded during step st-1
+    if (st + 2 < nsteps) {
+      load_x(st + 2);
+      load_w((st + 2) % 3, st + 2);
+    }
+    const unsigned short* xb = &xs[st % 3][c * DG_LDS_ROW + 8 * g];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
 #pragma unroll
@@ -95,22 +111,11 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
         const u16x8 b = *reinterpret_cast<const u16x8*>(xb + 16 * t * DG_LDS_ROW + 32 * s);
 #pragma unroll
         for (int r = 0; r < RT; ++r)
-          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur[r][s]),
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ring[st % 3][r][s]),
                                                                __builtin_bit_cast(bf16x8, b), acc[r][t], 0, 0, 0);
       }
     }
-    if (more) store_x(buf ^ 1);
-    __syncthreads();
-  };
-  load_w(a0, 0);
-  load_w(a1, 1);
-  load_x(0);
-  store_x(0);
-  __syncthreads();
-  for (int st = 0; st < nsteps; st += 3) {
-    body(a0, a2, st);
-    if (st + 1 < nsteps) body(a1, a0, st + 1);
-    if (st + 2 < nsteps) body(a2, a1, st + 2);
+    if (st + 1 < nsteps) __syncthreads();
   }
 
   // C: col m = 16t + c, rows n = nbase + 16r + 4g + j
@@ -153,12 +158,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(unsigned short* __re
   *reinterpret_cast<u32x4*>(out + (long)m * out_stride + n) = o;
 }
 
-template <int MT, int RT>
+template <int MT, int RT, int NSTEPS>
 static void dg_launch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                       int N, int K, int S, hipStream_t s) {
-  constexpr int NWAVES = 4, NW = 16 * RT * NWAVES;
+  constexpr int NWAVES = RT == 1 ? 8 : 4, NW = 16 * RT * NWAVES;  // 128 weight rows per workgroup
   const int tiles = (N + NW - 1) / NW;
-  decode_gemm_kernel<MT, RT, NWAVES><<<tiles * S, 64 * NWAVES, 0, s>>>(
+  decode_gemm_kernel<MT, RT, NWAVES, NSTEPS><<<tiles * S, 64 * NWAVES, 0, s>>>(
       static_cast<unsigned short*>(out), out_stride, ws, static_cast<const unsigned short*>(x), x_stride,
       static_cast<const unsigned short*>(w), M, N, K, S, tiles);
   if (S > 1) {
@@ -168,16 +173,34 @@ static void dg_launch(void* out, long out_stride, float* ws, const void* x, long
   }
 }
 
+template <int MT, int RT>
+static bool dg_steps(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M, int N,
+                     int K, int S, hipStream_t s) {
+  const int nsteps = K / S / 256;
+  switch (nsteps) {
+    case 1: dg_launch<MT, RT, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 2: dg_launch<MT, RT, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 4: dg_launch<MT, RT, 4>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 8: dg_launch<MT, RT, 8>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 16: dg_launch<MT, RT, 16>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    default: return false;
+  }
+}
+
+// K slice per workgroup = K / S must be 256 * {1, 2, 4, 8, 16}; false otherwise.
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, hipStream_t s) {
-#define HS_DG(MT_)                                                                   \
-  if (rt == 1) { dg_launch<MT_, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true; } \
-  if (rt == 2) { dg_launch<MT_, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true; } \
+  if (M <= 16) {
+    if (rt == 1) return dg_steps<1, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 2) return dg_steps<1, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+  } else if (M <= 32) {
+    if (rt == 1) return dg_steps<2, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 2) return dg_steps<2, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+  } else {
+    if (rt == 1) return dg_steps<4, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 2) return dg_steps<4, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+  }
   return false;
-  if (M <= 16) { HS_DG(1) }
-  if (M <= 32) { HS_DG(2) }
-  HS_DG(4)
-#undef HS_DG
 }
 
 }  // namespace hipserve

@@ -201,6 +201,45 @@ void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, 
                                     ids.data_ptr<int>(), T, logits.size(1), k, cur_stream());
 }
 
+int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes) {
+  return reinterpret_cast<int64_t>(hipserve::car_create((int)rank, (int)world, (size_t)max_bytes));
+}
+
+at::Tensor car_handle(int64_t state) {
+  auto t = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  hipserve::car_get_handle(reinterpret_cast<void*>(state), t.data_ptr());
+  return t;
+}
+
+void car_open(int64_t state, int64_t peer, const at::Tensor& handle) {
+  TORCH_CHECK(handle.device().is_cpu() && handle.numel() == 64 && handle.scalar_type() == at::kByte);
+  auto h = handle.contiguous();
+  hipserve::car_open(reinterpret_cast<void*>(state), (int)peer, h.data_ptr());
+}
+
+void car_all_reduce(int64_t state, const at::Tensor& inp, at::Tensor& out, bool two_shot) {
+  CHECK_DEV(inp); CHECK_BF16(inp); CHECK_BF16(out); CHECK_CONTIG(inp); CHECK_CONTIG(out);
+  TORCH_CHECK(inp.numel() == out.numel(), "car_all_reduce: size mismatch");
+  const size_t bytes = inp.numel() * 2;
+  TORCH_CHECK(bytes % 16 == 0 && bytes <= hipserve::car_max_bytes(reinterpret_cast<void*>(state)),
+              "car_all_reduce: size must be a multiple of 16 B and fit the registered buffer");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+  hipserve::launch_car(reinterpret_cast<void*>(state), inp.data_ptr(), out.data_ptr(), bytes, two_shot, 0,
+                       cur_stream());
+}
+
+bool car_error(int64_t state) { return hipserve::car_error(reinterpret_cast<void*>(state)); }
+
+void car_destroy(int64_t state) { hipserve::car_destroy(reinterpret_cast<void*>(state)); }
+
+void fill_uniform(at::Tensor& out, int64_t row0, int64_t col0, int64_t gcols, int64_t key, double scale) {
+  CHECK_DEV(out); CHECK_BF16(out);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1, "fill_uniform: 2-D row-major view");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  hipserve::launch_fill_uniform(out.data_ptr(), out.stride(0), out.size(0), out.size(1), row0, col0, gcols,
+                                (unsigned int)(key & 0xffffffffu), (float)scale, cur_stream());
+}
+
 void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::Tensor& ws, int64_t rt,
                  int64_t splits) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
@@ -218,7 +257,7 @@ void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::
   TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
                                            splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
                                            w.data_ptr(), M, N, K, rt, splits, cur_stream()),
-              "decode_gemm: unsupported rt");
+              "decode_gemm: unsupported (rt, K/splits): rt in {1,2}, K/splits = 256*{1,2,4,8,16}");
 }
 
 void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,
@@ -279,6 +318,14 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale) -> ()");
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
+  // custom all-reduce control ops carry an opaque state handle: catch-all kernels
+  m.def("car_create(int rank, int world, int max_bytes) -> int", &car_create);
+  m.def("car_handle(int state) -> Tensor", &car_handle);
+  m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);
+  m.def("car_all_reduce(int state, Tensor inp, Tensor(a!) out, bool two_shot) -> ()", &car_all_reduce);
+  m.def("car_error(int state) -> bool", &car_error);
+  m.def("car_destroy(int state) -> ()", &car_destroy);
+  m.def("fill_uniform(Tensor(a!) out, int row0, int col0, int gcols, int key, float scale) -> ()");
   m.def("decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int rt, int splits) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
@@ -295,6 +342,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("gguf_gemm", &gguf_gemm);
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("decode_gemm", &decode_gemm);
+  m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

@@ -74,6 +74,7 @@ class ModelRunner:
         self.block_size = ecfg.block_size
         self.model = LlamaModel(mcfg, tp, self.device, self.dtype, self.ops, max_pos=self.max_model_len)
         self.model.decode_partition = ecfg.decode_partition
+        self.model.block_size_hint = ecfg.block_size
         t0 = time.time()
         self._load_weights()
         self.load_time = time.time() - t0

@@ -96,40 +96,62 @@ class LlamaModel:
         mp = max_pos or cfg.max_position_embeddings
         self.cos_sin = ref.rope_cos_sin(self.D, mp, cfg.rope_theta, cfg.rope_scaling).to(self.device)
         self.decode_partition = 512
+        self.block_size_hint = 16  # KV block size (set by the runner)
         self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
 
     # ---------------------------------------------------------------- weights
     def allocate_random(self, seed: int = 0, std: float = 0.02):
-        """Random-init weights directly on the device (synthetic benchmarks)."""
+        """Synthetic weights generated on the device (K16, csrc/kernels/init.hip):
+        uniform with standard deviation ``std``, keyed by each element's position in
+        the UNSHARDED tensor, so every TP rank holds exactly its shard of the same
+        model and dummy weights are identical for any TP degree."""
         cfg, dev, dt = self.cfg, self.device, self.dtype
-        g = torch.Generator(device=dev)
-        g.manual_seed(seed * 1000 + self.tp.rank)
         H, D = cfg.hidden_size, self.D
+        rank, tp = self.tp.rank, self.tp.world_size
+        scale = std * math.sqrt(3.0)
+        names = {}
 
-        def rnd(*shape):
-            return (torch.randn(*shape, generator=g, device=dev, dtype=torch.float32) * std).to(dt) \
-                if math.prod(shape) < (1 << 26) else _randn_chunked(shape, g, dev, dt, std)
+        def fill(view, key, row0, col0, gcols):
+            k = (seed * 1000003 + names.setdefault(key, len(names) + 1) * 7919) & 0xFFFFFFFF
+            self.ops.fill_uniform(view, row0, col0, gcols, k, scale)
 
-        self.embed = rnd(self.vpad, H)
+        def new(*shape):
+            return torch.empty(*shape, device=dev, dtype=dt)
+
+        self.embed = new(self.vpad, H)
+        fill(self.embed, "embed", rank * self.vpad, 0, H)
         self.norm = torch.ones(H, device=dev, dtype=dt)
-        self.lm_head = self.embed if cfg.tie_word_embeddings else rnd(self.vpad, H)
-        qkv_w = (self.nq + 2 * self.nkv) * D
+        if cfg.tie_word_embeddings:
+            self.lm_head = self.embed
+        else:
+            self.lm_head = new(self.vpad, H)
+            fill(self.lm_head, "lm_head", rank * self.vpad, 0, H)
+        nq, nkv, I = self.nq, self.nkv, self.inter
+        kv_head0 = rank * nkv if cfg.num_kv_heads >= tp else rank // (tp // cfg.num_kv_heads)
         self.layers = []
-        for _ in range(cfg.num_layers):
-            lw = LayerWeights(
-                ln1=torch.ones(H, device=dev, dtype=dt),
-                wqkv=rnd(qkv_w, H),
-                wo=rnd(H, self.nq * D),
-                ln2=torch.ones(H, device=dev, dtype=dt),
-            )
+        for li in range(cfg.num_layers):
+            lw = LayerWeights(ln1=torch.ones(H, device=dev, dtype=dt), wqkv=new((nq + 2 * nkv) * D, H),
+                              wo=new(H, nq * D), ln2=torch.ones(H, device=dev, dtype=dt))
+            fill(lw.wqkv[:nq * D], f"{li}.q", rank * nq * D, 0, H)
+            fill(lw.wqkv[nq * D:(nq + nkv) * D], f"{li}.k", kv_head0 * D, 0, H)
+            fill(lw.wqkv[(nq + nkv) * D:], f"{li}.v", kv_head0 * D, 0, H)
+            fill(lw.wo, f"{li}.o", 0, rank * nq * D, cfg.num_heads * D)
             if cfg.num_experts:
-                E = cfg.num_experts
-                lw.router = rnd(E, H)
-                lw.w13 = rnd(E, 2 * self.inter, H)
-                lw.w2 = rnd(E, H, self.inter)
+                E, Ig = cfg.num_experts, cfg.intermediate_size
+                lw.router = new(E, H)
+                fill(lw.router, f"{li}.router", 0, 0, H)
+                lw.w13 = new(E, 2 * I, H)
+                lw.w2 = new(E, H, I)
+                for e in range(E):
+                    fill(lw.w13[e, :I], f"{li}.w1", e * Ig + rank * I, 0, H)
+                    fill(lw.w13[e, I:], f"{li}.w3", e * Ig + rank * I, 0, H)
+                    fill(lw.w2[e], f"{li}.w2", e * H, rank * I, Ig)
             else:
-                lw.wgu = rnd(2 * self.inter, H)
-                lw.wd = rnd(H, self.inter)
+                lw.wgu = new(2 * I, H)
+                fill(lw.wgu[:I], f"{li}.gate", rank * I, 0, H)
+                fill(lw.wgu[I:], f"{li}.up", rank * I, 0, H)
+                lw.wd = new(H, I)
+                fill(lw.wd, f"{li}.down", 0, rank * I, cfg.intermediate_size)
             self.layers.append(lw)
 
     # ---------------------------------------------------------------- forward
@@ -169,6 +191,8 @@ class LlamaModel:
         residual = torch.empty_like(h)
         xn = torch.empty_like(h)
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
+        if Td:
+            part, tmp_out, tmp_ml = self._decode_split(Td, meta)
         for i, lw in enumerate(self.layers):
             if i == 0:
                 residual.copy_(h)
@@ -184,7 +208,7 @@ class LlamaModel:
                                       meta.ctx_prefill, meta.tiles, nq, nkv, self.scale)
             if Td:
                 ops.paged_decode(attn[Tp:], qkv[Tp:], kc, vc, meta.bt_decode, meta.ctx_decode,
-                                 meta.tmp_out, meta.tmp_ml, nq, nkv, self.decode_partition, self.scale)
+                                 tmp_out, tmp_ml, nq, nkv, part, self.scale)
             o = self.linear(attn, lw.wo)
             self.tp.all_reduce(o)
             ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
@@ -198,6 +222,26 @@ class LlamaModel:
             self.tp.all_reduce(h)
         ops.fused_add_rmsnorm(xn, h, residual, self.norm, eps)
         return xn
+
+    def _decode_split(self, Td: int, meta: AttnMeta):
+        """Context partition size for the decode attention: with >= 512 (sequence,
+        kv-head) workgroups the chip is full without splitting, so contexts up to
+        2048 run as ONE partition (no partial-merge kernel; 6.3 vs 5.3 TB/s at
+        B=64, ctx 1152, profiles/decode_partition_sweep.md); small batches split the
+        context (512) to occupy the CUs. Workspace views are sized to the chosen
+        partition count so the grid carries no dead partitions."""
+        part = self.decode_partition
+        if Td * self.nkv >= 512:
+            part = max(part, 2048)
+        width = meta.bt_decode.shape[1] * self.block_size_hint
+        mp = max(1, -(-width // part))
+        to, tm = meta.tmp_out, meta.tmp_ml
+        if to is None or mp > to.shape[2]:
+            return self.decode_partition, to, tm
+        nq, D = to.shape[1], to.shape[3]
+        to = to.view(-1)[: Td * nq * mp * D].view(Td, nq, mp, D)
+        tm = tm.view(-1)[: Td * nq * mp * 2].view(Td, nq, mp, 2)
+        return part, to, tm
 
     def moe(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Mixtral sparse MoE (top-k of E experts, renormalised softmax weights)."""
@@ -274,13 +318,3 @@ class LlamaModel:
         k = torch.zeros(L, num_blocks, self.nkv, block_size, self.D, device=self.device, dtype=self.dtype)
         v = torch.zeros(L, num_blocks, self.nkv, self.D, block_size, device=self.device, dtype=self.dtype)
         return [(k[i], v[i]) for i in range(L)]
-
-
-def _randn_chunked(shape, g, dev, dt, std):
-    out = torch.empty(*shape, device=dev, dtype=dt)
-    flat = out.view(-1)
-    step = 1 << 26
-    for s in range(0, flat.numel(), step):
-        n = min(step, flat.numel() - s)
-        flat[s:s + n] = (torch.randn(n, generator=g, device=dev, dtype=torch.float32) * std).to(dt)
-    return out

@@ -72,6 +72,10 @@ class KernelOps:
         self._op.silu_and_mul(out, x)
         return out
 
+    def fill_uniform(self, out, row0, col0, gcols, key, scale):
+        self._op.fill_uniform(out, row0, col0, gcols, key, scale)
+        return out
+
     def rope_cache(self, qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode):
         self._op.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
 
@@ -95,6 +99,9 @@ class ReferenceOps:
     """PyTorch reference path (CPU plumbing engine / numerics oracle)."""
 
     name = "reference"
+
+    def fill_uniform(self, out, row0, col0, gcols, key, scale):
+        return ref.fill_uniform(out, row0, col0, gcols, key, scale)
 
     def rmsnorm(self, out, x, w, eps):
         out.copy_(ref.rmsnorm(x, w, eps))

@@ -22,7 +22,7 @@ SKINNY_CONFIGS = [(1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (2, 1), (2, 2), (2, 4
 # split-K MFMA GEMM with an LDS-staged x chunk shared by 64 rows (gguf.hip, qtype 6 = bf16)
 SPLITK_CONFIGS = [1, 2, 4, 8]
 DG_RT = [1, 2]
-DG_SPLITS = [1, 2, 4, 7, 8, 14, 16]
+DG_STEPS = [1, 2, 4, 8, 16]  # 256-k steps per workgroup (compile-time in decode_gemm.hip)
 COLD_BYTES = 1 << 30
 _EMPTY = {}
 TUNE_MS = [1, 2, 4, 8, 16, 24, 32, 48, 64]
@@ -100,12 +100,13 @@ class GemmTuner:
     @staticmethod
     def candidates(M, N, K):
         out = []
+        tiles = -(-N // 128)
         for rt in DG_RT:
-            tiles = -(-N // (64 * rt))
-            for sp in DG_SPLITS:
-                if K % (256 * sp) or (sp > 1 and N % 8) or tiles * sp > 4096:
+            for ns in DG_STEPS:
+                if K % (256 * ns):
                     continue
-                if sp > 1 and tiles * sp // 2 >= 1024:  # plenty of workgroups already
+                sp = K // (256 * ns)
+                if (sp > 1 and N % 8) or tiles * sp > 4096 or tiles * sp < 64:
                     continue
                 out.append(("dg", rt, sp))
         for rt, kw in SKINNY_CONFIGS:

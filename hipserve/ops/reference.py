@@ -212,3 +212,29 @@ def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, steps, bf16_r
         i = int(torch.argmax(g))
         toks[r], lps[r] = i, float(x[i] - lse)
     return toks, lps
+
+
+# ----------------------------------------------------------------------------- K16
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 on int64 tensors holding uint32 values (products wrap mod 2^64,
+    the low 32 bits are exact)."""
+    M = 0xFFFFFFFF
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & M
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & M
+    return x ^ (x >> 16)
+
+
+def fill_uniform(out: torch.Tensor, row0: int, col0: int, gcols: int, key: int, scale: float):
+    """Torch twin of csrc/kernels/init.hip (bit-identical): uniform(-scale, scale)
+    keyed by global element coordinates, written into the 2-D view ``out``."""
+    rows, cols = out.shape
+    r = torch.arange(rows, dtype=torch.int64).unsqueeze(1) + row0
+    c = torch.arange(cols, dtype=torch.int64).unsqueeze(0) + col0
+    idx = (r * gcols + c) & 0xFFFFFFFF
+    h = _mix32(_mix32(idx) ^ (key & 0xFFFFFFFF))
+    u = (h >> 8).to(torch.float32) * 5.9604644775390625e-08
+    v = (u - 0.5) * torch.tensor(2.0 * scale, dtype=torch.float32)
+    out.copy_(v.to(torch.bfloat16).to(out.dtype))
+    return out

@@ -35,6 +35,7 @@ class TPGroup:
         self.device = device
         self._cpu_group = None
         self._ring = None
+        self.custom_ar = None
 
     SHM_SLOT_BYTES = 8 << 20
     SHM_SLOTS = 4
@@ -68,9 +69,44 @@ class TPGroup:
         return self.rank == 0
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over TP ranks: decode-sized bf16 messages through the HIP-IPC
+        custom all-reduce (when set up), everything else through RCCL."""
         if self.world_size > 1:
-            dist.all_reduce(t, group=self.group)
+            car = self.custom_ar
+            if car is not None and car.supports(t):
+                car.all_reduce(t)
+            else:
+                dist.all_reduce(t, group=self.group)
         return t
+
+    def setup_custom_ar(self, max_bytes: int | None = None) -> bool:
+        """Collective: map peer buffers and keep the custom all-reduce only if its
+        self-test against RCCL passes on every rank."""
+        if self.world_size == 1 or self.device is None or self.device.type != "cuda" \
+                or os.environ.get("HIPSERVE_CUSTOM_AR", "1") == "0":
+            return False
+        from .custom_ar import DEFAULT_MAX_BYTES, CustomAllReduce, self_test
+        try:
+            car = CustomAllReduce(self.rank, self.world_size, self._cpu_group, self.device,
+                                  max_bytes or DEFAULT_MAX_BYTES)
+        except Exception as e:
+            car = None
+            err = str(e)
+        else:
+            err = ""
+        oks = [None] * self.world_size
+        dist.all_gather_object(oks, car is not None, group=self._cpu_group)
+        if not all(oks):
+            if car is not None:
+                car.close()
+            import logging
+            logging.getLogger("hipserve.comm").warning("custom all-reduce unavailable (%s); using RCCL", err)
+            return False
+        if not self_test(car, self.group, self._cpu_group):
+            car.close()
+            return False
+        self.custom_ar = car
+        return True
 
     def all_gather_lastdim(self, t: torch.Tensor) -> torch.Tensor:
         """[n, V/TP] on every rank -> [n, V] on every rank."""
@@ -138,6 +174,8 @@ def init_tp(world_size: int | None = None, backend: str | None = None, device_ty
     g = TPGroup(rank, ws, dist.group.WORLD, dev)
     g._cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
     g.setup_shm_ring()
+    if device_type == "cuda":
+        g.setup_custom_ar()
     _TP = g
     return g
 

@@ -77,7 +77,8 @@ def test_rope_cache(ops, mode, bs):
 
 @pytest.mark.parametrize("nq,nkv,D", [(32, 8, 128), (64, 8, 128), (32, 32, 64), (32, 4, 64)])
 @pytest.mark.parametrize("bs", [16, 32])
-def test_paged_decode(ops, nq, nkv, D, bs):
+@pytest.mark.parametrize("part", [512, 2048])
+def test_paged_decode(ops, nq, nkv, D, bs, part):
     torch.manual_seed(2)
     ctx = [1, 17, 100, 600, 1300, 512, 33]
     B = len(ctx)
@@ -88,7 +89,6 @@ def test_paged_decode(ops, nq, nkv, D, bs):
     bt = perm.view(B, max_blocks).contiguous()
     cl = torch.tensor(ctx, device=DEV, dtype=torch.int32)
     q = torch.randn(B, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
-    part = 512
     max_parts = math.ceil(max_blocks * bs / part)
     tmp_out = torch.empty(B, nq, max_parts, D, device=DEV, dtype=torch.float32)
     tmp_ml = torch.empty(B, nq, max_parts, 2, device=DEV, dtype=torch.float32)
@@ -200,12 +200,12 @@ def test_splitk_bf16_gemm(ops, M, splits):
 @pytest.mark.parametrize("M", [1, 7, 16, 23, 32, 50, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 512), (6144, 1792)])
 @pytest.mark.parametrize("rt", [1, 2])
-@pytest.mark.parametrize("splits", [1, 2, 7])
+@pytest.mark.parametrize("splits", [1, 2, 7, 8])
 def test_decode_gemm(ops, M, N, K, rt, splits):
     """Split-K LDS-shared decode GEMM vs fp32 torch (incl. ragged M, N tails, strided x)."""
     from hipserve.ops.gemm import decode_gemm
-    if K % (256 * splits):
-        pytest.skip("K not divisible")
+    if K % (256 * splits) or K // splits // 256 not in (1, 2, 4, 8, 16):
+        pytest.skip("unsupported K slice")
     torch.manual_seed(M * 7 + N)
     xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
     x = xb[:, :K]  # row stride != K
@@ -240,3 +240,15 @@ def test_moe_kernels_match_reference(ops, T, E, k):
     want = m.moe(x, lw).float()
     m.ops = ops
     _close(got, want, atol=3e-2 * want.abs().max().item() + 1e-3, frac=0.995)
+
+
+@pytest.mark.parametrize("rows,cols,row0,col0,gcols", [(64, 96, 0, 0, 96), (300, 1000, 17, 5, 4096),
+                                                       (1, 8192, 1000, 0, 8192)])
+def test_fill_uniform_bit_exact(ops, rows, cols, row0, col0, gcols):
+    """On-device synthetic init == its torch twin, bit for bit (strided view too)."""
+    base = torch.zeros(rows, cols + 8, device=DEV, dtype=torch.bfloat16)
+    view = base[:, 4:4 + cols]
+    ops.fill_uniform(view, row0, col0, gcols, 987654321, 0.0346)
+    want = ref.fill_uniform(torch.empty(rows, cols, dtype=torch.bfloat16), row0, col0, gcols, 987654321, 0.0346)
+    assert torch.equal(view.cpu(), want)
+    assert torch.count_nonzero(base[:, :4]) == 0 and torch.count_nonzero(base[:, 4 + cols:]) == 0

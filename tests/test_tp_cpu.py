@@ -25,7 +25,8 @@ def _port():
 
 
 def _cfg(ckpt, tp):
-    return EngineConfig(model=ckpt, load_format="safetensors", device="cpu", dtype="float32",
+    fmt = "safetensors" if os.path.isdir(ckpt) else "dummy"
+    return EngineConfig(model=ckpt, load_format=fmt, device="cpu", dtype="float32",
                         tensor_parallel_size=tp, num_kv_blocks=128, max_model_len=256,
                         max_num_batched_tokens=32, max_num_seqs=4)
 
@@ -81,3 +82,25 @@ def test_tp_matches_tp1(tmp_path, preset, world):
                                                                 ignore_eos=True))]
     got = _run_tp(ckpt, world)
     assert got == want
+
+
+@pytest.mark.parametrize("preset,world", [("tiny-llama", 2), ("tiny-mixtral", 4)])
+def test_dummy_weights_tp_invariant(preset, world):
+    """On-device synthetic init (K16) is keyed by global coordinates: a TP=N engine
+    with --load-format dummy runs the same model as TP=1."""
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.parallel.comm import TPGroup
+
+    ref = LLMEngine(_cfg(preset, 1), tp=TPGroup())
+    want = [r[0] for r in ref.generate(PROMPTS, SamplingParams(temperature=0.0, max_tokens=8,
+                                                                ignore_eos=True))]
+    assert _run_tp(preset, world) == want
+
+
+def test_fill_uniform_reference_properties():
+    from hipserve.ops import reference as ref
+    full = ref.fill_uniform(torch.empty(64, 96), 0, 0, 96, 1234, 0.5)
+    part = ref.fill_uniform(torch.empty(16, 32), 8, 40, 96, 1234, 0.5)
+    assert torch.equal(part, full[8:24, 40:72])
+    assert full.abs().max() <= 0.5 and abs(full.mean()) < 0.05
+    assert abs(full.std().item() - 0.5 / 3 ** 0.5) < 0.02

@@ -56,8 +56,11 @@ def bench_sample(ops):
 
 
 def bench_decode(ops):
-    D, bs, part = 128, 16, 512
-    for B, ctx, nq, nkv in [(64, 1152, 32, 8), (256, 1152, 32, 8), (1, 4096, 32, 8), (64, 4096, 64, 8)]:
+    import os
+    D, bs = 128, 16
+    parts = [int(x) for x in os.environ.get("DECODE_PARTS", "512").split(",")]
+    for (B, ctx, nq, nkv), part in [(c, p) for c in [(64, 1152, 32, 8), (64, 1280, 32, 8), (256, 1152, 32, 8),
+                                                     (1, 4096, 32, 8), (64, 4096, 64, 8)] for p in parts]:
         mb = math.ceil(ctx / bs) + 1
         nblocks = B * mb
         kc = torch.randn(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
@@ -71,7 +74,8 @@ def bench_decode(ops):
         out = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
         us = timeit(lambda: ops.paged_decode(out, q, kc, vc, bt, cl, to, tm, nq, nkv, part, 1 / math.sqrt(D)))
         byts = 2 * B * ctx * nkv * D * 2
-        emit(op="paged_decode", B=B, ctx=ctx, nq=nq, nkv=nkv, us=round(us, 1), TBps=round(byts / us / 1e6, 2))
+        emit(op="paged_decode", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, us=round(us, 1),
+             TBps=round(byts / us / 1e6, 2))
 
 
 def bench_prefill(ops):
