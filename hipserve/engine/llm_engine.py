@@ -15,6 +15,8 @@ import numpy as np
 from ..config import EngineConfig, ModelConfig, resolve_model_config
 from ..parallel.comm import TPGroup, get_tp
 from ..tokenizer import IncrementalDetokenizer, get_tokenizer
+from ..utils.faults import FaultInjector
+from ..utils.tracing import Tracer, step_kind
 from .block_manager import BlockManager
 from .metrics import EngineMetrics
 from .model_runner import ModelRunner
@@ -46,6 +48,9 @@ class LLMEngine:
         self.last_step_time = time.monotonic()
         self.lookahead = bool(cfg.extra.get("decode_lookahead", True)) and self.runner.use_graphs
         self._inflight = None
+        self.tracer = Tracer.from_env()
+        self.faults = FaultInjector.from_env()
+        self.step_no = 0
 
     # ---------------------------------------------------------------- requests
     def new_request_id(self) -> str:
@@ -94,9 +99,13 @@ class LLMEngine:
         (stop checks, detokenisation, streaming) then overlaps GPU work instead of
         leaving the GPU idle between steps. Anything else (prefill, admissions,
         preemption, penalties, logprobs) runs synchronously."""
+        self.faults.on_step("rank0", self.step_no)
+        self.step_no += 1
+        tr = self.tracer
         if self._inflight is not None:
             return self._step_pipelined()
-        so = self.scheduler.schedule()
+        with tr.phase("schedule"):
+            so = self.scheduler.schedule()
         outputs: list[RequestOutput] = []
         for s in so.preempted:
             if s.status == Status.FINISHED:
@@ -104,18 +113,31 @@ class LLMEngine:
         if so.empty:
             return outputs
         t0 = time.monotonic()
-        inp = self.runner.prepare(so)
+        tr.step_begin()
+        with tr.phase("prepare"):
+            inp = self.runner.prepare(so)
         if self.lookahead and self.runner.graph_eligible(inp):
-            self._inflight = self._launch(so, inp, t0)
+            with tr.phase("launch"):
+                self._inflight = self._launch(so, inp, t0)
             return outputs
         if self.tp.world_size > 1:
             self.tp.broadcast_obj(("step", inp))
         sampled = self._commit(so)
-        toks, lps, top = self.runner.execute(inp)
+        with tr.phase("execute"):
+            toks, lps, top = self.runner.execute(inp)
         now = time.monotonic()
-        self.metrics.on_step(so, now - t0, self.blocks.usage(), self.scheduler)
-        outputs += self._process(so, sampled, toks, lps, top, now)
+        self._step_done(so, now - t0)
+        with tr.phase("process"):
+            outputs += self._process(so, sampled, toks, lps, top, now)
         return outputs
+
+    def _step_done(self, so, dt):
+        self.metrics.on_step(so, dt, self.blocks.usage(), self.scheduler)
+        if self.tracer.enabled:
+            npf = sum(s.num_tokens for s in so.prefill)
+            self.tracer.step_done(step_kind(npf, len(so.decode)), so.num_tokens,
+                                  len(so.prefill) + len(so.decode), dt, self.blocks.usage(),
+                                  self.scheduler.num_running, self.scheduler.num_waiting)
 
     # -- pipelined decode ---------------------------------------------------
     def _launch(self, so, inp, t0, src=None):
@@ -127,17 +149,24 @@ class LLMEngine:
 
     def _step_pipelined(self) -> list[RequestOutput]:
         so, sampled, handle, t0 = self._inflight
-        nxt = self._schedule_lookahead(sampled)
+        tr = self.tracer
+        with tr.phase("schedule"):
+            nxt = self._schedule_lookahead(sampled)
         t1 = time.monotonic()
         self._inflight = None
         if nxt is not None:
             so2, src = nxt
-            inp = self.runner.prepare(so2)
-            self._inflight = self._launch(so2, inp, t1, src)
-        toks, lps = self.runner.wait(handle)
+            tr.step_begin()
+            with tr.phase("prepare"):
+                inp = self.runner.prepare(so2)
+            with tr.phase("launch"):
+                self._inflight = self._launch(so2, inp, t1, src)
+        with tr.phase("wait"):
+            toks, lps = self.runner.wait(handle)
         now = time.monotonic()
-        self.metrics.on_step(so, now - t0, self.blocks.usage(), self.scheduler)
-        return self._process(so, sampled, toks, lps, None, now)
+        self._step_done(so, now - t0)
+        with tr.phase("process"):
+            return self._process(so, sampled, toks, lps, None, now)
 
     def _schedule_lookahead(self, sampled):
         """Next decode-only batch while the previous step is still in flight, or
@@ -271,16 +300,21 @@ class LLMEngine:
         return [tuple(res[rid]) for rid in order]
 
     def shutdown(self):
+        self.tracer.close()
         if self.tp.world_size > 1 and self.tp.is_first:
             self.tp.broadcast_obj(("stop", None))
 
 
-def worker_loop(runner: ModelRunner, tp: TPGroup):
+def worker_loop(runner: ModelRunner, tp: TPGroup, faults: FaultInjector | None = None):
     """TP ranks > 0: execute whatever rank 0 schedules until told to stop."""
+    faults = faults or FaultInjector.from_env()
+    step = 0
     while True:
         kind, inp = tp.broadcast_obj(None)
         if kind == "stop":
             return
+        faults.on_step("worker", step)
+        step += 1
         if runner.graph_eligible(inp):
             runner.launch(inp)  # no host readback on workers: keep the GPU queue fed
         else:

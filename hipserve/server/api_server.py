@@ -23,6 +23,7 @@ from prometheus_client import CONTENT_TYPE_LATEST, generate_latest
 
 from .. import __version__
 from ..engine.request import SamplingParams
+from ..utils.faults import stall_timeout
 from .async_engine import AsyncEngine, EngineDeadError
 
 log = logging.getLogger("hipserve.server")
@@ -48,6 +49,7 @@ class OpenAIServer:
         self.max_model_len = max_model_len
         self.created = int(time.time())
         self.tokenizer = self.engine.tokenizer
+        self.stall_timeout = stall_timeout()
 
     # ------------------------------------------------------------ app
     def app(self) -> web.Application:
@@ -68,7 +70,7 @@ class OpenAIServer:
         if not self.ae.alive:
             return web.Response(status=503, text="engine dead")
         # stuck-loop watchdog: a running engine refreshes its heartbeat every step
-        if self.engine.has_unfinished() and time.monotonic() - self.ae.heartbeat > 120:
+        if self.engine.has_unfinished() and time.monotonic() - self.ae.heartbeat > self.stall_timeout:
             return web.Response(status=503, text="engine stalled")
         return web.Response(status=200, text="OK")
 
@@ -360,10 +362,22 @@ async def _collect(gens):
 
 
 async def serve(engine, host: str, port: int, model_name: str, ready: asyncio.Event | None = None,
-                extra_names: tuple = ()):
+                extra_names: tuple = (), worker_procs=(), death_grace_s: float = 5.0):
+    """Serve until the engine dies. ``worker_procs``: TP worker processes to watch;
+    if one exits the engine is marked dead (/health 503) and this process exits
+    after ``death_grace_s`` so Kubernetes restarts the pod."""
     loop = asyncio.get_running_loop()
     ae = AsyncEngine(engine)
     ae.start(loop)
+    monitor = None
+    if worker_procs:
+        from ..utils.faults import WorkerMonitor
+
+        monitor = WorkerMonitor(
+            worker_procs, exit_after=death_grace_s,
+            on_death=lambda p: ae.mark_dead(EngineDeadError(
+                f"TP worker pid {getattr(p, 'pid', '?')} exited with code {getattr(p, 'exitcode', '?')}")))
+        monitor.start()
     srv = OpenAIServer(ae, model_name, engine.max_model_len, extra_names)
     runner = web.AppRunner(srv.app(), access_log=None)
     await runner.setup()
@@ -379,5 +393,7 @@ async def serve(engine, host: str, port: int, model_name: str, ready: asyncio.Ev
             # keep serving 503 on /health so k8s restarts the pod
             await asyncio.sleep(3600 * 24 * 365)
     finally:
+        if monitor is not None:
+            monitor.stop()
         ae.stop()
         await runner.cleanup()

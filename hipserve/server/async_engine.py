@@ -50,6 +50,16 @@ class AsyncEngine:
     def alive(self) -> bool:
         return self.thread is not None and self.thread.is_alive() and self.error is None
 
+    def mark_dead(self, exc: BaseException):
+        """Declare the engine dead from outside the engine thread (e.g. a TP
+        worker exited: the engine thread may be stuck in a collective forever).
+        ``/health`` turns 503 and every waiting request gets an error."""
+        if self.error is None:
+            self.error = exc
+            log.error("engine marked dead: %s", exc)
+            if self.loop is not None:
+                self.loop.call_soon_threadsafe(self._fail_all, exc)
+
     # ------------------------------------------------------------ engine thread
     def _run(self):
         eng = self.engine

@@ -86,7 +86,9 @@ def _worker(cfg: EngineConfig, rank: int, world: int, port: int):
     from ..engine.llm_engine import worker_loop
     from ..engine.model_runner import ModelRunner
     from ..parallel.comm import init_tp
+    from ..utils.faults import ParentWatch
 
+    ParentWatch().start()  # rank 0 gone -> exit, never hold the GPU as an orphan
     tp = init_tp(world, device_type="cuda" if cfg.device == "cuda" else "cpu")
     mcfg = resolve_model_config(cfg.model, cfg.served_model_name)
     from ..tokenizer import get_tokenizer
@@ -122,7 +124,8 @@ def main(argv=None, prog="hipserve"):
     engine = LLMEngine(cfg, tp=tp)
     names = (cfg.model,) if cfg.served_model_name else ()
     try:
-        asyncio.run(serve(engine, cfg.host, cfg.port, cfg.model_name, extra_names=names))
+        asyncio.run(serve(engine, cfg.host, cfg.port, cfg.model_name, extra_names=names,
+                          worker_procs=procs))
     finally:
         engine.shutdown()
         for p in procs:

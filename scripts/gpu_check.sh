@@ -1,0 +1,64 @@
+#!/bin/bash
+# One gpurun call: GPU tests, smoke, decode-GEMM sweep, 1-GPU bench, rocprofv3 kernel stats.
+# usage (from the build container):
+#   gpurun --timeout 1100 -- 'bash scripts/gpu_check.sh [tests|bench|prof|sweep ...]'
+# Every GPU step has its own time limit and the steps are chained with &&:
+# the first failure / timeout ends the call.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+steps="${*:-tests smoke sweep bench prof}"
+
+run_tests() {
+  timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+  local rc=$?
+  tail -n 15 $OUT/pytest_gpu.log
+  return $rc
+}
+run_smoke() {
+  timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+  local rc=$?; tail -n 3 $OUT/smoke.log; return $rc
+}
+run_sweep() {
+  timeout -k 10 300 python -u tools/bench_ops.py sweep 16,32,64 > $OUT/gemm_sweep.log 2>&1
+  local rc=$?; cat $OUT/gemm_sweep.log; return $rc
+}
+run_ops() {
+  timeout -k 10 300 python -u tools/bench_ops.py ${OPS:-all} > $OUT/bench_ops.log 2>&1
+  local rc=$?; cat $OUT/bench_ops.log; return $rc
+}
+run_bench() {
+  timeout -k 10 480 python -u bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1
+  local rc=$?; tail -n 2 $OUT/bench.log; return $rc
+}
+run_prof() {
+  local here=$PWD
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/prof \
+     -o run -- python3 $here/bench.py --path engine --steps 1 --warmup 1 > $here/$OUT/prof.log 2>&1)
+  local rc=$?; tail -n 3 $OUT/prof.log
+  [ $rc -eq 0 ] || return $rc
+  local db; db=$(find $OUT/prof -name '*results.db' | head -n 1)
+  if [ -n "$db" ]; then
+    (cd tools && python prof_db.py "$here/$db" "$here/$OUT/prof_summary.md" "bench.py --path engine" > /dev/null)
+  fi
+  find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/prof_kernel_stats.csv \;
+  rm -rf $OUT/prof  # raw traces exceed gpurun's 64 MiB copy-back limit
+  return 0
+}
+
+for s in $steps; do
+  echo "=== $s ($(date +%T))"
+  case $s in
+    tests) run_tests ;;
+    smoke) run_smoke ;;
+    sweep) run_sweep ;;
+    ops) run_ops ;;
+    bench) run_bench ;;
+    prof) run_prof ;;
+    *) echo "unknown step $s"; false ;;
+  esac || { echo "step $s failed (rc=$?)"; exit 1; }
+done
+echo "=== done ($(date +%T))"
