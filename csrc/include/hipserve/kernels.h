@@ -75,8 +75,10 @@ void launch_fill_uniform(void* out, long ld, int rows, int cols, long row0, long
 
 // decode_gemm.hip — split-K LDS-shared decode GEMM (M <= 64, K % (256*S) == 0). S > 1 needs
 // ws >= S*M*N fp32 and N % 8 == 0. Returns false for an uncompiled rt.
+// packed = w in the pack_decode_weight layout ([ceil(N/128)][K/256][8][8][64][8] bf16).
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
-                        int N, int K, int rt, int S, hipStream_t s);
+                        int N, int K, int rt, int S, bool packed, hipStream_t s);
+void launch_pack_decode_weight(void* out, const void* w, int N, int K, hipStream_t s);
 }  // namespace hipserve
 
 namespace hipserve {

@@ -21,6 +21,13 @@
 //    cross-XCD fences: the 8 L2s are not coherent with each other mid-kernel).
 //  * blockIdx -> (slice, tile) is slice-major so the 8 XCDs (round-robin dispatch)
 //    each walk disjoint weight rows of one slice.
+//  * kPacked: the weight is pre-shuffled ONCE at load time into the exact order the
+//    waves consume it, [N/128][K/256][8 row groups][8 k-slots][64 lanes][8]
+//    (pack_decode_weight below). Every 16-byte-per-lane load instruction then reads
+//    1 KiB of contiguous memory and a workgroup streams one contiguous region
+//    (64 KiB per 256-k step) — the access pattern of a memcpy, instead of 128
+//    rows x 512 B pieces scattered over 128 DRAM pages per step. Rows past N are
+//    zero padding (N is rounded up to 128 in the packed copy).
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -28,7 +35,7 @@ namespace hipserve {
 
 constexpr int DG_LDS_ROW = 264;  // 256 + 8 bf16 pad -> 528 B row stride
 
-template <int MT, int RT, int NWAVES, int NSTEPS>
+template <int MT, int RT, int NWAVES, int NSTEPS, bool kPacked>
 __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     unsigned short* __restrict__ out, long out_stride, float* __restrict__ ws,
     const unsigned short* __restrict__ x, long x_stride, const unsigned short* __restrict__ w,
@@ -48,8 +55,15 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
   const int nbase = tile * NW + wave * 16 * RT;
 
   const unsigned short* wr[RT];
+  if constexpr (kPacked) {
+    // [tile][kstep][row group = wave*RT + r][slot s][lane][8]
+    const unsigned short* wp = w + ((long)tile * (K >> 8) + (long)split * NSTEPS) * (NW * 256) + lane * 8;
 #pragma unroll
-  for (int r = 0; r < RT; ++r) wr[r] = w + (long)min(nbase + 16 * r + c, N - 1) * K + k0 + 8 * g;
+    for (int r = 0; r < RT; ++r) wr[r] = wp + (long)(wave * RT + r) * (8 * 512);
+  } else {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) wr[r] = w + (long)min(nbase + 16 * r + c, N - 1) * K + k0 + 8 * g;
+  }
 
   // x staging: thread -> (row, 16-byte column chunk)
   u16x8 xv[XPASS];
@@ -87,7 +101,8 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int s = 0; s < 8; ++s)
-        ring[slot][r][s] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wr[r] + step * 256 + 32 * s));
+        ring[slot][r][s] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(
+            kPacked ? wr[r] + (long)step * (NW * 256) + 512 * s : wr[r] + step * 256 + 32 * s));
   };
   // prologue: x(0) -> LDS[0]; x(1) in registers; W(0), W(1) in flight
   load_x(0);
@@ -158,12 +173,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(unsigned short* __re
   *reinterpret_cast<u32x4*>(out + (long)m * out_stride + n) = o;
 }
 
-template <int MT, int RT, int NSTEPS>
+template <int MT, int RT, int NSTEPS, bool kPacked>
 static void dg_launch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                       int N, int K, int S, hipStream_t s) {
   constexpr int NWAVES = RT == 1 ? 8 : 4, NW = 16 * RT * NWAVES;  // 128 weight rows per workgroup
   const int tiles = (N + NW - 1) / NW;
-  decode_gemm_kernel<MT, RT, NWAVES, NSTEPS><<<tiles * S, 64 * NWAVES, 0, s>>>(
+  decode_gemm_kernel<MT, RT, NWAVES, NSTEPS, kPacked><<<tiles * S, 64 * NWAVES, 0, s>>>(
       static_cast<unsigned short*>(out), out_stride, ws, static_cast<const unsigned short*>(x), x_stride,
       static_cast<const unsigned short*>(w), M, N, K, S, tiles);
   if (S > 1) {
@@ -173,34 +188,71 @@ static void dg_launch(void* out, long out_stride, float* ws, const void* x, long
   }
 }
 
-template <int MT, int RT>
+template <int MT, int RT, bool kPacked>
 static bool dg_steps(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M, int N,
                      int K, int S, hipStream_t s) {
   const int nsteps = K / S / 256;
   switch (nsteps) {
-    case 1: dg_launch<MT, RT, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 2: dg_launch<MT, RT, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 4: dg_launch<MT, RT, 4>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 8: dg_launch<MT, RT, 8>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 16: dg_launch<MT, RT, 16>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 1: dg_launch<MT, RT, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 2: dg_launch<MT, RT, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 4: dg_launch<MT, RT, 4, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 7: dg_launch<MT, RT, 7, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 8: dg_launch<MT, RT, 8, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 16: dg_launch<MT, RT, 16, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
     default: return false;
   }
 }
 
-// K slice per workgroup = K / S must be 256 * {1, 2, 4, 8, 16}; false otherwise.
-bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
+template <bool kPacked>
+static bool dg_dispatch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, hipStream_t s) {
   if (M <= 16) {
-    if (rt == 1) return dg_steps<1, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
-    if (rt == 2) return dg_steps<1, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 1) return dg_steps<1, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 2) return dg_steps<1, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
   } else if (M <= 32) {
-    if (rt == 1) return dg_steps<2, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
-    if (rt == 2) return dg_steps<2, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 1) return dg_steps<2, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 2) return dg_steps<2, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
   } else {
-    if (rt == 1) return dg_steps<4, 1>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
-    if (rt == 2) return dg_steps<4, 2>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 1) return dg_steps<4, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 2) return dg_steps<4, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
   }
   return false;
+}
+
+// K slice per workgroup = K / S must be 256 * {1, 2, 4, 7, 8, 16}; false otherwise.
+// packed: w is the pack_decode_weight layout (N rounded up to 128 rows).
+bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
+                        int N, int K, int rt, int S, bool packed, hipStream_t s) {
+  return packed ? dg_dispatch<true>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, s)
+                : dg_dispatch<false>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, s);
+}
+
+// W[N, K] row-major -> packed [ceil(N/128)][K/256][8][8][64][8] (zero rows past N).
+// One thread per packed 16-byte piece: reads 16 B of a weight row, writes 16 B.
+__global__ __launch_bounds__(256) void pack_decode_weight_kernel(unsigned short* __restrict__ out,
+                                                                 const unsigned short* __restrict__ w, int N, int K,
+                                                                 long pieces) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= pieces) return;
+  // piece index = ((((tile * KS + kstep) * 8 + rg) * 8 + s) * 64 + lane)
+  const int lane = i & 63, sl = (i >> 6) & 7, rg = (i >> 9) & 7;
+  const long ts = i >> 12;
+  const int KS = K >> 8;
+  const int kstep = ts % KS;
+  const long tile = ts / KS;
+  const int g = lane >> 4, c = lane & 15;
+  const long n = tile * 128 + rg * 16 + c;
+  const long k = (long)kstep * 256 + 32 * sl + 8 * g;
+  u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (n < N) v = *reinterpret_cast<const u16x8*>(w + n * K + k);
+  *reinterpret_cast<u16x8*>(out + i * 8) = v;
+}
+
+void launch_pack_decode_weight(void* out, const void* w, int N, int K, hipStream_t s) {
+  const long tiles = (N + 127) / 128;
+  const long pieces = tiles * (K / 256) * 8 * 8 * 64;
+  pack_decode_weight_kernel<<<(pieces + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out),
+                                                                 static_cast<const unsigned short*>(w), N, K, pieces);
 }
 
 }  // namespace hipserve

@@ -256,8 +256,39 @@ void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
                                            splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
-                                           w.data_ptr(), M, N, K, rt, splits, cur_stream()),
-              "decode_gemm: unsupported (rt, K/splits): rt in {1,2}, K/splits = 256*{1,2,4,8,16}");
+                                           w.data_ptr(), M, N, K, rt, splits, false, cur_stream()),
+              "decode_gemm: unsupported (rt, K/splits): rt in {1,2}, K/splits = 256*{1,2,4,7,8,16}");
+}
+
+// Packed weights: wp = pack_decode_weight(w[N, K]) (flat, ceil(N/128)*128*K bf16).
+void decode_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, at::Tensor& ws, int64_t N,
+                        int64_t rt, int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  CHECK_CONTIG(wp);
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 256 == 0 && wp.numel() == (N + 127) / 128 * 128 * K, "decode_gemm_packed: packed size mismatch");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "decode_gemm_packed: out shape");
+  TORCH_CHECK(M >= 1 && M <= 64, "decode_gemm_packed: 1 <= M <= 64");
+  TORCH_CHECK(splits >= 1 && K % (256 * splits) == 0, "decode_gemm_packed: K must be a multiple of 256*splits");
+  TORCH_CHECK(N % 4 == 0 && out.stride(0) % 4 == 0 && x.stride(0) % 8 == 0, "decode_gemm_packed: alignment");
+  if (splits > 1) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * N && N % 8 == 0,
+                "decode_gemm_packed: fp32 workspace of S*M*N (N % 8 == 0) required for split-K");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
+                                           splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
+                                           wp.data_ptr(), M, N, K, rt, splits, true, cur_stream()),
+              "decode_gemm_packed: unsupported (rt, K/splits)");
+}
+
+void pack_decode_weight(at::Tensor& out, const at::Tensor& w) {
+  CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_BF16(out); CHECK_CONTIG(out);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) % 256 == 0, "pack_decode_weight: w [N, K], K % 256 == 0");
+  const long N = w.size(0), K = w.size(1);
+  TORCH_CHECK(out.numel() == (N + 127) / 128 * 128 * K, "pack_decode_weight: out must hold ceil(N/128)*128*K");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
+  hipserve::launch_pack_decode_weight(out.data_ptr(), w.data_ptr(), N, K, cur_stream());
 }
 
 void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,
@@ -327,6 +358,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("car_destroy(int state) -> ()", &car_destroy);
   m.def("fill_uniform(Tensor(a!) out, int row0, int col0, int gcols, int key, float scale) -> ()");
   m.def("decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int rt, int splits) -> ()");
+  m.def("decode_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
+  m.def("pack_decode_weight(Tensor(a!) out, Tensor w) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
@@ -342,6 +375,8 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("gguf_gemm", &gguf_gemm);
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("decode_gemm", &decode_gemm);
+  m.impl("decode_gemm_packed", &decode_gemm_packed);
+  m.impl("pack_decode_weight", &pack_decode_weight);
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);

@@ -78,16 +78,28 @@ class ModelRunner:
         t0 = time.time()
         self._load_weights()
         self.load_time = time.time() - t0
+        self.max_bs = min(ecfg.max_num_seqs, max(GRAPH_BUCKETS))
+        self.buckets = [b for b in GRAPH_BUCKETS if b <= max(self.max_bs, 1)]
+        if self.buckets[-1] < self.max_bs:
+            self.buckets.append(self.max_bs)
+        # decode GEMM autotune BEFORE the KV pool takes the memory: its cold-weight
+        # copies need scratch, and weights whose winner is the packed decode GEMM get
+        # their pre-shuffled copy (gemm.PACKED) allocated before the pool is sized
+        self.gemm_report = []
+        if self.device.type == "cuda" and ecfg.extra.get("gemm_autotune", True):
+            from ..ops import gemm
+
+            ms = [b for b in self.buckets if b <= 64]
+            self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms)
+            if ecfg.extra.get("packed_decode", True):
+                self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
+            torch.cuda.empty_cache()
         self.num_blocks = self._num_kv_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.block_size)
         self.pad_block = self.num_blocks - 1          # scratch block for graph padding rows
         self.width = -(-self.max_model_len // self.block_size)
         part = ecfg.decode_partition
         self.max_parts = -(-self.width * self.block_size // part)
-        self.max_bs = min(ecfg.max_num_seqs, max(GRAPH_BUCKETS))
-        self.buckets = [b for b in GRAPH_BUCKETS if b <= max(self.max_bs, 1)]
-        if self.buckets[-1] < self.max_bs:
-            self.buckets.append(self.max_bs)
         nq = self.model.nq
         self.tmp_out = torch.empty(self.max_bs, nq, self.max_parts, mcfg.head_dim,
                                    device=self.device, dtype=torch.float32)
@@ -97,12 +109,6 @@ class ModelRunner:
         self.graph_pool = None
         self._static = None
         self.use_graphs = self.device.type == "cuda" and not ecfg.enforce_eager
-        self.gemm_report = []
-        if self.device.type == "cuda" and ecfg.extra.get("gemm_autotune", True):
-            from ..ops import gemm
-
-            ms = [b for b in self.buckets if b <= 64]
-            self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms)
         if self.use_graphs:
             self._capture_graphs()
 

@@ -171,6 +171,19 @@ class LlamaModel:
             out.add(tuple(self.lm_head.shape))
         return sorted(out)
 
+    def pack_decode_weights(self, shapes) -> int:
+        """Pre-shuffled copies (ops/gemm.py ``PACKED``) of the dense projections whose
+        (N, K) the decode tuner assigned to the packed decode GEMM. Costs one extra
+        copy of those weights in HBM (288 GB per MI355X: bandwidth over capacity)."""
+        n = 0
+        ws = [w for lw in self.layers for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd)]
+        ws.append(self.lm_head)
+        for w in ws:
+            if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
+                gemm.register_packed(w)
+                n += w.numel() * w.element_size()
+        return n
+
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.tp.world_size == 1:
             return F.embedding(ids, self.embed)

@@ -12,6 +12,7 @@ real decode step streams from HBM once per layer.
 from __future__ import annotations
 
 import logging
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -22,7 +23,10 @@ SKINNY_CONFIGS = [(1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (2, 1), (2, 2), (2, 4
 # split-K MFMA GEMM with an LDS-staged x chunk shared by 64 rows (gguf.hip, qtype 6 = bf16)
 SPLITK_CONFIGS = [1, 2, 4, 8]
 DG_RT = [1, 2]
-DG_STEPS = [1, 2, 4, 8, 16]  # 256-k steps per workgroup (compile-time in decode_gemm.hip)
+DG_STEPS = [1, 2, 4, 7, 8, 16]  # 256-k steps per workgroup (compile-time in decode_gemm.hip)
+# decode weights pre-shuffled for the packed decode GEMM, keyed by the plain
+# weight's data_ptr (the plain [N, K] copy stays for prefill / hipBLASLt)
+PACKED: dict[int, tuple] = {}  # data_ptr -> (weakref to the plain weight, packed copy)
 COLD_BYTES = 1 << 30
 _EMPTY = {}
 TUNE_MS = [1, 2, 4, 8, 16, 24, 32, 48, 64]
@@ -32,6 +36,10 @@ class GemmTuner:
     def __init__(self):
         self.table: dict[tuple, object] = {}
         self.report: list[dict] = []
+
+    def packed_shapes(self) -> set:
+        """(N, K) whose tuned choice uses the packed layout at some M."""
+        return {(N, K) for (M, N, K), c in self.table.items() if isinstance(c, tuple) and c[0] == "dgp"}
 
     def choose(self, M: int, N: int, K: int):
         if M > 64:
@@ -80,25 +88,27 @@ class GemmTuner:
         for (N, K) in sorted(set(shapes)):
             ncopy = max(1, min(16, -(-COLD_BYTES // (N * K * 2))))
             ws_ = [torch.randn(N, K, device=device, dtype=torch.bfloat16) for _ in range(ncopy)]
+            wp_ = [pack(w) for w in ws_] if packable(N, K) else None
             n = max(16, ncopy)
             for M in ms:
                 x = torch.randn(M, K, device=device, dtype=torch.bfloat16)
                 out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
                 best, best_t = "blas", self._time(lambda i: F.linear(x, ws_[i % ncopy]), n=n)
                 t_blas = best_t
-                for cfg in self.candidates(M, N, K):
-                    t = self._time(lambda i: run_choice(cfg, out, x, ws_[i % ncopy]), n=n)
+                for cfg in self.candidates(M, N, K, packed=wp_ is not None):
+                    t = self._time(lambda i: run_choice(cfg, out, x, ws_[i % ncopy],
+                                                        wp_[i % ncopy] if wp_ else None), n=n)
                     if t < best_t * 0.97:
                         best, best_t = cfg, t
                 self.table[(M, N, K)] = best
                 self.report.append({"M": M, "N": N, "K": K, "blas_us": round(t_blas, 1),
                                     "best": str(best), "best_us": round(best_t, 1),
                                     "best_TBps": round(N * K * 2 / best_t / 1e6, 2)})
-            del ws_
+            del ws_, wp_
         return self.report
 
     @staticmethod
-    def candidates(M, N, K):
+    def candidates(M, N, K, packed=False):
         out = []
         tiles = -(-N // 128)
         for rt in DG_RT:
@@ -109,6 +119,8 @@ class GemmTuner:
                 if (sp > 1 and N % 8) or tiles * sp > 4096 or tiles * sp < 64:
                     continue
                 out.append(("dg", rt, sp))
+                if packed:
+                    out.append(("dgp", rt, sp))
         for rt, kw in SKINNY_CONFIGS:
             if K % (256 * kw) == 0:
                 out.append(("sk", rt, kw))
@@ -143,7 +155,54 @@ def decode_gemm(out, x, w, rt, splits):
     return out
 
 
-def run_choice(c, out, x, w):
+def packable(N: int, K: int) -> bool:
+    return K % 256 == 0 and N % 8 == 0
+
+
+def pack(w: torch.Tensor) -> torch.Tensor:
+    """Pre-shuffle a [N, K] bf16 weight for ``decode_gemm_packed`` (flat, N padded to 128)."""
+    N, K = w.shape
+    out = torch.empty(-(-N // 128) * 128 * K, dtype=w.dtype, device=w.device)
+    torch.ops.hipserve.pack_decode_weight(out, w.contiguous())
+    return out
+
+
+def packed_of(w: torch.Tensor):
+    """The packed copy of ``w`` — only if registered for this very tensor (a freed
+    weight's address may be reused by another tensor)."""
+    e = PACKED.get(w.data_ptr())
+    if e is None:
+        return None
+    ref, wp = e
+    if ref() is not w:
+        PACKED.pop(w.data_ptr(), None)
+        return None
+    return wp
+
+
+def register_packed(w: torch.Tensor) -> torch.Tensor:
+    wp = packed_of(w)
+    if wp is None:
+        wp = pack(w)
+        PACKED[w.data_ptr()] = (weakref.ref(w), wp)
+    return wp
+
+
+def decode_gemm_packed(out, x, wp, N, rt, splits):
+    M = x.shape[0]
+    ws = (torch.empty(splits * M * N, dtype=torch.float32, device=x.device) if splits > 1
+          else _empty(x.device)[1])
+    torch.ops.hipserve.decode_gemm_packed(out, x, wp, ws, N, rt, splits)
+    return out
+
+
+def run_choice(c, out, x, w, wp=None):
+    if c[0] == "dgp":
+        if wp is None:
+            wp = packed_of(w)
+        if wp is None:  # weight was not packed (e.g. memory): same kernel, plain layout
+            return decode_gemm(out, x, w, c[1], c[2])
+        return decode_gemm_packed(out, x, wp, w.shape[0], c[1], c[2])
     if c[0] == "dg":
         return decode_gemm(out, x, w, c[1], c[2])
     if c[0] == "sk":

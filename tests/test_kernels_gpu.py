@@ -204,7 +204,7 @@ def test_splitk_bf16_gemm(ops, M, splits):
 def test_decode_gemm(ops, M, N, K, rt, splits):
     """Split-K LDS-shared decode GEMM vs fp32 torch (incl. ragged M, N tails, strided x)."""
     from hipserve.ops.gemm import decode_gemm
-    if K % (256 * splits) or K // splits // 256 not in (1, 2, 4, 8, 16):
+    if K % (256 * splits) or K // splits // 256 not in (1, 2, 4, 7, 8, 16):
         pytest.skip("unsupported K slice")
     torch.manual_seed(M * 7 + N)
     xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
@@ -212,6 +212,35 @@ def test_decode_gemm(ops, M, N, K, rt, splits):
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
     out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
     decode_gemm(out, x, w, rt, splits)
+    assert not torch.isnan(out).any(), "unwritten outputs"
+    want = x.float() @ w.float().T
+    _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 16, 23, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 512), (6144, 1792), (4096, 14336)])
+@pytest.mark.parametrize("rt", [1, 2])
+@pytest.mark.parametrize("splits", [1, 2, 8])
+def test_decode_gemm_packed(ops, M, N, K, rt, splits):
+    """Packed-weight decode GEMM (pre-shuffled streaming layout, N padded to 128)
+    vs fp32 torch; also checks the packing kernel against a torch permute."""
+    from hipserve.ops import gemm
+    if K % (256 * splits) or K // splits // 256 not in (1, 2, 4, 7, 8, 16):
+        pytest.skip("unsupported K slice")
+    torch.manual_seed(M * 11 + N + K)
+    xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
+    x = xb[:, :K]
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    wp = gemm.pack(w)
+    Np = -(-N // 128) * 128
+    wpad = torch.zeros(Np, K, device=DEV, dtype=torch.bfloat16)
+    wpad[:N] = w
+    # [tile][kstep][rg][s][g][c][8] from (tile, rg, c, kstep, s, g, 8)
+    want_p = wpad.view(Np // 128, 8, 16, K // 256, 8, 4, 8).permute(0, 3, 1, 4, 5, 2, 6).reshape(-1)
+    assert torch.equal(wp, want_p)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    gemm.decode_gemm_packed(out, x, wp, N, rt, splits)
+    assert not torch.isnan(out).any(), "unwritten outputs"
     want = x.float() @ w.float().T
     _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
 

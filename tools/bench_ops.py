@@ -150,15 +150,16 @@ def bench_gemm_sweep():
     for N, K in shapes:
         ncopy = max(1, min(16, -(-gemm.COLD_BYTES // (N * K * 2))))
         ws_ = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) for _ in range(ncopy)]
+        wp_ = [gemm.pack(w) for w in ws_]
         n = max(16, ncopy)
         for M in ms:
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
             out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
             res = {"blas": T._time(lambda i: F.linear(x, ws_[i % ncopy]), n=n)}
-            for cfg in T.candidates(M, N, K):
-                res[str(cfg)] = T._time(lambda i: gemm.run_choice(cfg, out, x, ws_[i % ncopy]), n=n)
-            emit(op="gemm_sweep", M=M, N=N, K=K, **{k: round(v, 1) for k, v in sorted(res.items(), key=lambda kv: kv[1])[:8]})
-        del ws_
+            for cfg in T.candidates(M, N, K, packed=True):
+                res[str(cfg)] = T._time(lambda i: gemm.run_choice(cfg, out, x, ws_[i % ncopy], wp_[i % ncopy]), n=n)
+            emit(op="gemm_sweep", M=M, N=N, K=K, **{k: round(v, 1) for k, v in sorted(res.items(), key=lambda kv: kv[1])[:10]})
+        del ws_, wp_
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "sweep":
