@@ -79,6 +79,27 @@ HS_DEVICE float block_max(float v, float* scratch) {
 
 HS_HOST_DEVICE int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// SiLU(gate) * up on 8 bf16 lanes, fp32 math, one bf16 rounding (shared by the
+// standalone silu_and_mul kernel and the decode GEMM's fused x staging, so both
+// paths are bit-identical).
+HS_DEVICE unsigned short silu_mul1(unsigned short g, unsigned short u) {
+  const float gf = bf16_to_f32(g);
+  const float s = gf / (1.f + __expf(-gf));
+  return f32_to_bf16(s * bf16_to_f32(u));
+}
+HS_DEVICE u16x8 silu_mul8(const u16x8 g, const u16x8 u) {
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = silu_mul1(g[j], u[j]);
+  return o;
+}
+
+// Row-norm launch policy shared by every RMSNorm-family kernel (norm.hip,
+// decode_fused.hip) so they reduce in the same order and stay bit-identical:
+// 512 threads from 4096 columns up (more loads in flight on the 1-row-per-CU
+// decode shapes), 256 below.
+HS_HOST_DEVICE int norm_threads(int hidden) { return hidden >= 4096 ? 512 : 256; }
+
 // Bijective XCD-aware block remap (MI355X: 8 XCDs, blocks dealt round-robin).
 // Blocks that share operand panels end up on the same XCD's L2.
 HS_DEVICE int xcd_remap(int bid, int nwg) {

@@ -76,9 +76,23 @@ void launch_fill_uniform(void* out, long ld, int rows, int cols, long row0, long
 // decode_gemm.hip — split-K LDS-shared decode GEMM (M <= 64, K % (256*S) == 0). S > 1 needs
 // ws >= S*M*N fp32 and N % 8 == 0. Returns false for an uncompiled rt.
 // packed = w in the pack_decode_weight layout ([ceil(N/128)][K/256][8][8][64][8] bf16).
+// flags: DG_GLU (w packed with glu=true; out = act [M, N/2] = silu(gate) * up; packed only),
+//        DG_PARTIAL (ws != nullptr: write the fp32 partials [S, M, N], no reduce launch).
+// ws == nullptr requires S == 1 (bf16 out written directly).
+constexpr int DG_GLU = 1, DG_PARTIAL = 2;
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
-                        int N, int K, int rt, int S, bool packed, hipStream_t s);
-void launch_pack_decode_weight(void* out, const void* w, int N, int K, hipStream_t s);
+                        int N, int K, int rt, int S, bool packed, int flags, hipStream_t s);
+
+// decode_fused.hip — split-K partial reductions fused with the next op of the layer
+// ws: [S, M, N] fp32 partials. h = bf16(sum_s ws); residual = bf16(h + residual);
+// out = rmsnorm(residual) * w  (bit-identical to splitk_reduce + fused_add_rmsnorm)
+void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
+                               int M, int N, float eps, hipStream_t s);
+// qkv = bf16(sum_s ws) -> RoPE(q, k) -> q into qkv[:, :nq*D], k/v into the paged cache
+void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
+                              const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
+                              int nkv, int D, int block_size, int mode, hipStream_t s);
+void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s);
 }  // namespace hipserve
 
 namespace hipserve {

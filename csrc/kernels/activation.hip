@@ -16,14 +16,7 @@ __global__ __launch_bounds__(256) void silu_and_mul_kernel(
     const int c = (int)(v - r * vpr);
     const u16x8 g = *reinterpret_cast<const u16x8*>(in + r * in_stride + c * 8);
     const u16x8 u = *reinterpret_cast<const u16x8*>(in + r * in_stride + inter + c * 8);
-    u16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gf = bf16_to_f32(g[j]);
-      const float s = gf / (1.f + __expf(-gf));
-      o[j] = f32_to_bf16(s * bf16_to_f32(u[j]));
-    }
-    *reinterpret_cast<u16x8*>(out + r * out_stride + c * 8) = o;
+    *reinterpret_cast<u16x8*>(out + r * out_stride + c * 8) = silu_mul8(g, u);
   }
 }
 

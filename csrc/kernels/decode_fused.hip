@@ -1,0 +1,211 @@
+// Split-K partial reductions fused with the op that follows them in a decode
+// layer (SURVEY §3.F hot loop, K2/K3 fused into K6/K7/K9's epilogue).
+//
+// The decode GEMMs (decode_gemm.hip, DG_PARTIAL) leave fp32 partials
+// ws[S, M, N]; instead of a reduce kernel followed by a separate elementwise
+// kernel (each ~5 us at decode sizes, almost all of it launch + dependent-load
+// latency, profiles/r1_bench_llama3_8b_v3_trace.md), ONE kernel sums the slices
+// and applies the next op:
+//   * splitk_add_rmsnorm: o_proj / down_proj -> residual add -> RMSNorm
+//     (the next layer's input_layernorm, or the final norm);
+//   * splitk_rope_cache:  qkv_proj -> RoPE on q, k -> q back into the qkv buffer,
+//     k / v into the paged cache.
+// Both round exactly where the unfused chain rounds (bf16 after the sum, bf16
+// residual), so the fused and unfused decode paths are bit-identical.
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+// sum over S slices of 8 consecutive fp32 partials, rounded to bf16 like the
+// unfused reduce output, returned as fp32
+HS_DEVICE void sum8_bf16(float (&o)[8], const float* __restrict__ p, long slice, int S) {
+  f32x4 lo = *reinterpret_cast<const f32x4*>(p), hi = *reinterpret_cast<const f32x4*>(p + 4);
+  for (int s = 1; s < S; ++s) {
+    lo += *reinterpret_cast<const f32x4*>(p + s * slice);
+    hi += *reinterpret_cast<const f32x4*>(p + s * slice + 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = bf16_to_f32(f32_to_bf16(lo[j]));
+    o[j + 4] = bf16_to_f32(f32_to_bf16(hi[j]));
+  }
+}
+
+template <int NT, int VPT, bool kWF32>
+__global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* __restrict__ out,
+                                                                 unsigned short* __restrict__ residual,
+                                                                 const float* __restrict__ ws, int S,
+                                                                 const void* __restrict__ weight, int M, int N,
+                                                                 float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = N >> 3;
+  const long slice = (long)M * N;
+  // the norm weight does not depend on the reduction: issue its loads first
+  float w[VPT][8];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      if constexpr (kWF32) {
+        const f32x4* wp = reinterpret_cast<const f32x4*>(weight) + idx * 2;
+        const f32x4 w0 = wp[0], w1 = wp[1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { w[i][j] = w0[j]; w[i][j + 4] = w1[j]; }
+      } else {
+        const u16x8 wv = reinterpret_cast<const u16x8*>(weight)[idx];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[i][j] = bf16_to_f32(wv[j]);
+      }
+    }
+  }
+  u16x8* rr = reinterpret_cast<u16x8*>(residual + (long)row * N);
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      float h[8];
+      sum8_bf16(h, ws + (long)row * N + idx * 8, slice, S);
+      const u16x8 b = rr[idx];
+      u16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        r[j] = f32_to_bf16(h[j] + bf16_to_f32(b[j]));
+        v[i][j] = bf16_to_f32(r[j]);
+        ss += v[i][j] * v[i][j];
+      }
+      rr[idx] = r;
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / N + eps);
+  u16x8* orow = reinterpret_cast<u16x8*>(out + (long)row * N);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv * w[i][j]);
+      orow[idx] = o;
+    }
+  }
+}
+
+template <bool kWF32>
+static void add_rmsnorm_t(void* out, void* residual, const float* ws, int S, const void* w, int M, int N, float eps,
+                          hipStream_t s) {
+  auto* o = static_cast<unsigned short*>(out);
+  auto* r = static_cast<unsigned short*>(residual);
+  const int nvec = N / 8;
+  if (norm_threads(N) == 256) {
+    if (nvec <= 256) splitk_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps);
+    else splitk_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps);
+  } else {
+    if (nvec <= 512) splitk_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps);
+    else if (nvec <= 1024) splitk_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps);
+    else splitk_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps);
+  }
+}
+
+void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
+                               int M, int N, float eps, hipStream_t s) {
+  if (M <= 0) return;
+  if (weight_f32) add_rmsnorm_t<true>(out, residual, ws, S, w, M, N, eps, s);
+  else add_rmsnorm_t<false>(out, residual, ws, S, w, M, N, eps, s);
+}
+
+// The rope_cache kernel (rope_cache.hip) reading its input from the split-K
+// partials instead of a bf16 qkv row. Work item = one 8-wide chunk: (q/k head,
+// chunk) pairs first, then the v chunks; 64-thread workgroups over
+// (token, item block) so a 64-token decode batch spreads over ~450 workgroups
+// instead of 64 (the partial reads are per-CU-bandwidth bound at one WG per token).
+template <int kMode>
+__global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
+    unsigned short* __restrict__ qkv, long qkv_stride, const float* __restrict__ ws, int S,
+    const long* __restrict__ positions, const long* __restrict__ slots, const float* __restrict__ cos_sin,
+    unsigned short* __restrict__ k_cache, unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D,
+    int block_size) {
+  const int t = blockIdx.x;
+  const int it = blockIdx.y * 64 + threadIdx.x;
+  const int half = D / 2;
+  const int qk_chunks = kMode == 0 ? half / 8 : D / 8;  // work items per q/k head
+  const int n_qk = (nq + nkv) * qk_chunks;
+  const int n_v = nkv * (D / 8);
+  if (it >= n_qk + n_v) return;
+  const long pos = positions[t];
+  const long slot = slots[t];
+  const int N = (nq + 2 * nkv) * D;
+  const long slice = (long)T * N;
+  const float* wrow = ws + (long)t * N;
+  const float* cs = cos_sin + pos * D;
+  unsigned short* row = qkv + t * qkv_stride;
+  const long blk = slot >= 0 ? slot / block_size : 0;
+  const int off = slot >= 0 ? (int)(slot % block_size) : 0;
+
+  if (it >= n_qk) {  // V: transposed cache block (tokens contiguous per d)
+    if (slot < 0) return;
+    const int iv = it - n_qk, kh = iv / (D / 8), c = iv % (D / 8);
+    float x[8];
+    sum8_bf16(x, wrow + (nq + nkv) * D + kh * D + c * 8, slice, S);
+    unsigned short* vc = v_cache + (blk * nkv + kh) * (long)D * block_size + off;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vc[(c * 8 + j) * block_size] = f32_to_bf16(x[j]);
+    return;
+  }
+  const int h = it / qk_chunks, c = it % qk_chunks;
+  if (h >= nq && slot < 0) return;
+  if constexpr (kMode == 0) {
+    float x[8], y[8];
+    sum8_bf16(x, wrow + h * D + c * 8, slice, S);
+    sum8_bf16(y, wrow + h * D + half + c * 8, slice, S);
+    u16x8 va, vb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float co = cs[c * 8 + j], si = cs[half + c * 8 + j];
+      va[j] = f32_to_bf16(x[j] * co - y[j] * si);
+      vb[j] = f32_to_bf16(y[j] * co + x[j] * si);
+    }
+    unsigned short* dst = h < nq ? row + h * D
+                                 : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
+    *reinterpret_cast<u16x8*>(dst + c * 8) = va;
+    *reinterpret_cast<u16x8*>(dst + half + c * 8) = vb;
+  } else {
+    float x[8];
+    sum8_bf16(x, wrow + h * D + c * 8, slice, S);
+    u16x8 v;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int i = c * 4 + p;
+      const float co = cs[i], si = cs[half + i];
+      v[2 * p] = f32_to_bf16(x[2 * p] * co - x[2 * p + 1] * si);
+      v[2 * p + 1] = f32_to_bf16(x[2 * p + 1] * co + x[2 * p] * si);
+    }
+    unsigned short* dst = h < nq ? row + h * D
+                                 : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
+    *reinterpret_cast<u16x8*>(dst + c * 8) = v;
+  }
+}
+
+void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
+                              const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
+                              int nkv, int D, int block_size, int mode, hipStream_t s) {
+  if (T <= 0) return;
+  auto* q = static_cast<unsigned short*>(qkv);
+  auto* kc = static_cast<unsigned short*>(k_cache);
+  auto* vc = static_cast<unsigned short*>(v_cache);
+  const int qk_chunks = mode == 0 ? D / 16 : D / 8;
+  const int items = (nq + nkv) * qk_chunks + nkv * (D / 8);
+  const dim3 grid(T, (items + 63) / 64);
+  if (mode == 0)
+    splitk_rope_cache_kernel<0><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc, T, nq,
+                                                     nkv, D, block_size);
+  else
+    splitk_rope_cache_kernel<1><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc, T, nq,
+                                                     nkv, D, block_size);
+}
+
+}  // namespace hipserve

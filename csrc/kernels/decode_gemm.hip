@@ -21,6 +21,14 @@
 //    cross-XCD fences: the 8 L2s are not coherent with each other mid-kernel).
 //  * blockIdx -> (slice, tile) is slice-major so the 8 XCDs (round-robin dispatch)
 //    each walk disjoint weight rows of one slice.
+//  * kGlu (merged gate|up projection, packed with pack_decode_weight(glu=true):
+//    each 128-row tile holds 64 gate rows then the 64 matching up rows): with
+//    S == 1 the epilogue exchanges the up half through LDS and writes
+//    act = silu(gate) * up [M, N/2] directly — no [M, N] gate|up round trip and
+//    no separate silu_and_mul launch. S > 1 partials go to splitk_reduce_glu.
+//  * ws != nullptr: fp32 partials [S, M, N] are written even for S == 1 and no
+//    reduce kernel is launched when DG_PARTIAL is set — the caller's fused
+//    epilogue (decode_fused.hip: residual add + RMSNorm, RoPE + KV write) sums them.
 //  * kPacked: the weight is pre-shuffled ONCE at load time into the exact order the
 //    waves consume it, [N/128][K/256][8 row groups][8 k-slots][64 lanes][8]
 //    (pack_decode_weight below). Every 16-byte-per-lane load instruction then reads
@@ -35,7 +43,7 @@ namespace hipserve {
 
 constexpr int DG_LDS_ROW = 264;  // 256 + 8 bf16 pad -> 528 B row stride
 
-template <int MT, int RT, int NWAVES, int NSTEPS, bool kPacked>
+template <int MT, int RT, int NWAVES, int NSTEPS, bool kPacked, bool kGlu>
 __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     unsigned short* __restrict__ out, long out_stride, float* __restrict__ ws,
     const unsigned short* __restrict__ x, long x_stride, const unsigned short* __restrict__ w,
@@ -74,7 +82,8 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
       // rows >= M are clamped, not zeroed: they only feed output columns m >= M,
       // which are never stored, and a per-lane select around a load makes hipcc
       // branch and drain vmcnt(0) — the whole weight prefetch — every step
-      xv[p] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + k0 + step * 256 + col);
+      const unsigned short* xp = x + (long)min(row, M - 1) * x_stride + k0 + step * 256 + col;
+      xv[p] = *reinterpret_cast<const u16x8*>(xp);
     }
   };
   auto store_x = [&](int buf) {
@@ -133,6 +142,47 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     if (st + 1 < nsteps) __syncthreads();
   }
 
+  if constexpr (kGlu) {
+    if (ws == nullptr) {
+      // row group rg = wave*RT + r: 0-3 gate rows, 4-7 the matching up rows
+      constexpr int EW = 16 * MT;  // exchange row width (fp32)
+      float* ex = reinterpret_cast<float*>(&xs[0][0]);
+      __syncthreads();  // every wave is done reading the x ring
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int rg = wave * RT + r;
+        if (rg < 4) continue;
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ex[((rg - 4) * 16 + 4 * g + j) * EW + 16 * t + c] = bf16_to_f32(f32_to_bf16(acc[r][t][j]));
+      }
+      __syncthreads();
+      const int I = N >> 1;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int rg = wave * RT + r;
+        if (rg >= 4) continue;
+        const int col = tile * 64 + rg * 16 + 4 * g;  // act column of j = 0
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int m = 16 * t + c;
+          if (m >= M) continue;
+          unsigned short o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            o[j] = silu_mul1(f32_to_bf16(acc[r][t][j]),
+                             f32_to_bf16(ex[(rg * 16 + 4 * g + j) * EW + 16 * t + c]));
+          uint2 v;
+          v.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+          v.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+          if (col < I) *reinterpret_cast<uint2*>(out + (long)m * out_stride + col) = v;
+        }
+      }
+      return;
+    }
+  }
   // C: col m = 16t + c, rows n = nbase + 16r + 4g + j
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
@@ -142,7 +192,7 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     for (int t = 0; t < MT; ++t) {
       const int m = 16 * t + c;
       if (m >= M) continue;
-      if (S == 1) {
+      if (ws == nullptr) {
         uint2 v;
         v.x = pack_bf16x2(acc[r][t][0], acc[r][t][1]);
         v.y = pack_bf16x2(acc[r][t][2], acc[r][t][3]);
@@ -173,48 +223,83 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(unsigned short* __re
   *reinterpret_cast<u32x4*>(out + (long)m * out_stride + n) = o;
 }
 
-template <int MT, int RT, int NSTEPS, bool kPacked>
+// GLU split-K reduce: partial columns are in the interleaved packed order
+// (tile t: 64 gate columns then their 64 up columns); act[m, 64t + i] =
+// silu(bf16(sum gate)) * bf16(sum up). 8 act columns per thread.
+__global__ __launch_bounds__(256) void splitk_reduce_glu_kernel(unsigned short* __restrict__ out, long out_stride,
+                                                                const float* __restrict__ ws, int M, int N, int S) {
+  const int I = N >> 1;
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= (long)M * I) return;
+  const int m = i / I, a = i - (long)m * I;
+  const long gc = (long)(a >> 6) * 128 + (a & 63);  // gate column in the partials
+  const float* pg = ws + (long)m * N + gc;
+  f32x4 g0 = *reinterpret_cast<const f32x4*>(pg), g1 = *reinterpret_cast<const f32x4*>(pg + 4);
+  f32x4 u0 = *reinterpret_cast<const f32x4*>(pg + 64), u1 = *reinterpret_cast<const f32x4*>(pg + 68);
+  for (int s = 1; s < S; ++s) {
+    const float* q = pg + (long)s * M * N;
+    g0 += *reinterpret_cast<const f32x4*>(q);
+    g1 += *reinterpret_cast<const f32x4*>(q + 4);
+    u0 += *reinterpret_cast<const f32x4*>(q + 64);
+    u1 += *reinterpret_cast<const f32x4*>(q + 68);
+  }
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = silu_mul1(f32_to_bf16(g0[j]), f32_to_bf16(u0[j]));
+    o[j + 4] = silu_mul1(f32_to_bf16(g1[j]), f32_to_bf16(u1[j]));
+  }
+  *reinterpret_cast<u16x8*>(out + (long)m * out_stride + a) = o;
+}
+
+template <int MT, int RT, int NSTEPS, bool kPacked, bool kGlu>
 static void dg_launch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
-                      int N, int K, int S, hipStream_t s) {
+                      int N, int K, int S, int flags, hipStream_t s) {
   constexpr int NWAVES = RT == 1 ? 8 : 4, NW = 16 * RT * NWAVES;  // 128 weight rows per workgroup
   const int tiles = (N + NW - 1) / NW;
-  decode_gemm_kernel<MT, RT, NWAVES, NSTEPS, kPacked><<<tiles * S, 64 * NWAVES, 0, s>>>(
+  decode_gemm_kernel<MT, RT, NWAVES, NSTEPS, kPacked, kGlu><<<tiles * S, 64 * NWAVES, 0, s>>>(
       static_cast<unsigned short*>(out), out_stride, ws, static_cast<const unsigned short*>(x), x_stride,
       static_cast<const unsigned short*>(w), M, N, K, S, tiles);
-  if (S > 1) {
+  if (ws != nullptr && !(flags & DG_PARTIAL)) {
+    if (kGlu) {
+      const long n8 = (long)M * (N / 2) / 8;
+      splitk_reduce_glu_kernel<<<(n8 + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out), out_stride, ws,
+                                                                 M, N, S);
+      return;
+    }
     const long n8 = (long)M * N / 8;
     splitk_reduce_kernel<<<(n8 + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out), out_stride, ws, M, N,
                                                           S);
   }
 }
 
-template <int MT, int RT, bool kPacked>
+template <int MT, int RT, bool kPacked, bool kGlu>
 static bool dg_steps(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M, int N,
-                     int K, int S, hipStream_t s) {
+                     int K, int S, int flags, hipStream_t s) {
   const int nsteps = K / S / 256;
   switch (nsteps) {
-    case 1: dg_launch<MT, RT, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 2: dg_launch<MT, RT, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 4: dg_launch<MT, RT, 4, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 7: dg_launch<MT, RT, 7, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 8: dg_launch<MT, RT, 8, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
-    case 16: dg_launch<MT, RT, 16, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s); return true;
+    case 1: dg_launch<MT, RT, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    case 2: dg_launch<MT, RT, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    case 4: dg_launch<MT, RT, 4, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    case 7: dg_launch<MT, RT, 7, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    case 8: dg_launch<MT, RT, 8, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    case 16: dg_launch<MT, RT, 16, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
     default: return false;
   }
 }
 
-template <bool kPacked>
+template <bool kPacked, bool kGlu>
 static bool dg_dispatch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
-                        int N, int K, int rt, int S, hipStream_t s) {
+                        int N, int K, int rt, int S, int flags, hipStream_t s) {
   if (M <= 16) {
-    if (rt == 1) return dg_steps<1, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
-    if (rt == 2) return dg_steps<1, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 1) return dg_steps<1, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
+    if (rt == 2) return dg_steps<1, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
   } else if (M <= 32) {
-    if (rt == 1) return dg_steps<2, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
-    if (rt == 2) return dg_steps<2, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 1) return dg_steps<2, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
+    if (rt == 2) return dg_steps<2, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
   } else {
-    if (rt == 1) return dg_steps<4, 1, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
-    if (rt == 2) return dg_steps<4, 2, kPacked>(out, out_stride, ws, x, x_stride, w, M, N, K, S, s);
+    if (rt == 1) return dg_steps<4, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
+    if (rt == 2) return dg_steps<4, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
   }
   return false;
 }
@@ -222,16 +307,21 @@ static bool dg_dispatch(void* out, long out_stride, float* ws, const void* x, lo
 // K slice per workgroup = K / S must be 256 * {1, 2, 4, 7, 8, 16}; false otherwise.
 // packed: w is the pack_decode_weight layout (N rounded up to 128 rows).
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
-                        int N, int K, int rt, int S, bool packed, hipStream_t s) {
-  return packed ? dg_dispatch<true>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, s)
-                : dg_dispatch<false>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, s);
+                        int N, int K, int rt, int S, bool packed, int flags, hipStream_t s) {
+  if (flags & DG_GLU) {  // gate|up interleaved packing -> act = silu(gate) * up
+    return packed && N % 128 == 0 &&
+           dg_dispatch<true, true>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, flags, s);
+  }
+  return packed ? dg_dispatch<true, false>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, flags, s)
+                : dg_dispatch<false, false>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, flags, s);
 }
 
 // W[N, K] row-major -> packed [ceil(N/128)][K/256][8][8][64][8] (zero rows past N).
+// glu: W is a merged [gate; up] weight (N % 128 == 0) packed gate/up-interleaved per tile.
 // One thread per packed 16-byte piece: reads 16 B of a weight row, writes 16 B.
 __global__ __launch_bounds__(256) void pack_decode_weight_kernel(unsigned short* __restrict__ out,
                                                                  const unsigned short* __restrict__ w, int N, int K,
-                                                                 long pieces) {
+                                                                 long pieces, int glu) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= pieces) return;
   // piece index = ((((tile * KS + kstep) * 8 + rg) * 8 + s) * 64 + lane)
@@ -241,18 +331,23 @@ __global__ __launch_bounds__(256) void pack_decode_weight_kernel(unsigned short*
   const int kstep = ts % KS;
   const long tile = ts / KS;
   const int g = lane >> 4, c = lane & 15;
-  const long n = tile * 128 + rg * 16 + c;
+  long n = tile * 128 + rg * 16 + c;
+  if (glu) {  // tile = 64 gate rows [64t, 64t+64) then the up rows N/2 + [64t, 64t+64)
+    const int i = rg * 16 + c;
+    n = i < 64 ? tile * 64 + i : (N >> 1) + tile * 64 + (i - 64);
+  }
   const long k = (long)kstep * 256 + 32 * sl + 8 * g;
   u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   if (n < N) v = *reinterpret_cast<const u16x8*>(w + n * K + k);
   *reinterpret_cast<u16x8*>(out + i * 8) = v;
 }
 
-void launch_pack_decode_weight(void* out, const void* w, int N, int K, hipStream_t s) {
+void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s) {
   const long tiles = (N + 127) / 128;
   const long pieces = tiles * (K / 256) * 8 * 8 * 64;
   pack_decode_weight_kernel<<<(pieces + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out),
-                                                                 static_cast<const unsigned short*>(w), N, K, pieces);
+                                                                 static_cast<const unsigned short*>(w), N, K, pieces,
+                                                                 glu ? 1 : 0);
 }
 
 }  // namespace hipserve

@@ -1,6 +1,6 @@
 // RMSNorm and fused residual-add + RMSNorm.
 //
-// One 256-thread workgroup per token row; each lane owns VPT 16-byte vectors of
+// One 256/512-thread workgroup per token row (norm_threads, common.h); each lane owns VPT 16-byte vectors of
 // the row, held in registers between the sum-of-squares pass and the scale
 // pass, so the row is read from HBM exactly once and written once.
 // fp32 accumulation, bf16 I/O. Weight may be bf16 (HF checkpoints) or fp32
@@ -10,8 +10,8 @@
 
 namespace hipserve {
 
-template <int VPT, bool kAdd, bool kWF32>
-__global__ __launch_bounds__(256) void rmsnorm_kernel(
+template <int NT, int VPT, bool kAdd, bool kWF32>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(
     unsigned short* __restrict__ out, unsigned short* __restrict__ residual,
     const unsigned short* __restrict__ x, const void* __restrict__ weight,
     int hidden, long x_stride, long out_stride, float eps) {
@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int idx = threadIdx.x + i * 256;
+    const int idx = threadIdx.x + i * NT;
     if (idx < nvec) {
       u16x8 a = xr[idx];
       if constexpr (kAdd) {
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   u16x8* orow = reinterpret_cast<u16x8*>(out + row * out_stride);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int idx = threadIdx.x + i * 256;
+    const int idx = threadIdx.x + i * NT;
     if (idx < nvec) {
       float w[8];
       if constexpr (kWF32) {
@@ -77,15 +77,20 @@ static void launch_rmsnorm_t(unsigned short* out, unsigned short* residual,
                              int hidden, long x_stride, long out_stride, float eps,
                              hipStream_t s) {
   const int nvec = hidden / 8;
-  dim3 grid(rows), block(256);
-  if (nvec <= 256)
-    rmsnorm_kernel<1, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
-  else if (nvec <= 512)
-    rmsnorm_kernel<2, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
-  else if (nvec <= 1024)
-    rmsnorm_kernel<4, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
-  else
-    rmsnorm_kernel<8, kAdd, kWF32><<<grid, block, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+  dim3 grid(rows);
+  if (norm_threads(hidden) == 256) {  // hidden < 4096: nvec < 512
+    if (nvec <= 256)
+      rmsnorm_kernel<256, 1, kAdd, kWF32><<<grid, 256, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+    else
+      rmsnorm_kernel<256, 2, kAdd, kWF32><<<grid, 256, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+  } else {
+    if (nvec <= 512)
+      rmsnorm_kernel<512, 1, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+    else if (nvec <= 1024)
+      rmsnorm_kernel<512, 2, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+    else
+      rmsnorm_kernel<512, 4, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+  }
 }
 
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,

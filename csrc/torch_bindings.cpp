@@ -256,7 +256,7 @@ void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
                                            splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
-                                           w.data_ptr(), M, N, K, rt, splits, false, cur_stream()),
+                                           w.data_ptr(), M, N, K, rt, splits, false, 0, cur_stream()),
               "decode_gemm: unsupported (rt, K/splits): rt in {1,2}, K/splits = 256*{1,2,4,7,8,16}");
 }
 
@@ -278,17 +278,96 @@ void decode_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor& 
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
                                            splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
-                                           wp.data_ptr(), M, N, K, rt, splits, true, cur_stream()),
+                                           wp.data_ptr(), M, N, K, rt, splits, true, 0, cur_stream()),
               "decode_gemm_packed: unsupported (rt, K/splits)");
 }
 
-void pack_decode_weight(at::Tensor& out, const at::Tensor& w) {
+// Decode GEMM writing fp32 split-K partials ws[S, M, N] for a fused epilogue
+// (splitk_add_rmsnorm / splitk_rope_cache).
+void decode_gemm_partial(at::Tensor& ws, const at::Tensor& x, const at::Tensor& w, int64_t N, int64_t rt,
+                         int64_t splits, bool packed) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_ROWMAJOR(x); CHECK_CONTIG(w);
+  const int M = x.size(0), K = x.size(1);
+  if (packed) {
+    TORCH_CHECK(w.numel() == (N + 127) / 128 * 128 * K, "decode_gemm_partial: packed size mismatch");
+  } else {
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == N && w.size(1) == K, "decode_gemm_partial: w [N, K]");
+  }
+  TORCH_CHECK(M >= 1 && M <= 64 && K % (256 * splits) == 0 && N % 8 == 0 && x.stride(0) % 8 == 0,
+              "decode_gemm_partial: shape / alignment");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * N,
+              "decode_gemm_partial: ws must hold S*M*N fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_decode_gemm(nullptr, N, ws.data_ptr<float>(), x.data_ptr(), x.stride(0), w.data_ptr(),
+                                           M, N, K, rt, splits, packed, hipserve::DG_PARTIAL, cur_stream()),
+              "decode_gemm_partial: unsupported (rt, K/splits)");
+}
+
+// Merged gate|up decode GEMM with the SiLU-GLU fused: act[M, N/2] = silu(x Wg^T) * (x Wu^T),
+// wp = pack_decode_weight(w, glu=true). splits > 1 needs ws of S*M*N fp32.
+void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp, at::Tensor& ws, int64_t N,
+                     int64_t rt, int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(act); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(act);
+  CHECK_CONTIG(wp);
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(N % 128 == 0 && wp.numel() == N * K && K % (256 * splits) == 0, "decode_gemm_glu: shapes");
+  TORCH_CHECK(act.size(0) == M && act.size(1) == N / 2 && act.stride(0) % 8 == 0, "decode_gemm_glu: act [M, N/2]");
+  TORCH_CHECK(M >= 1 && M <= 64 && x.stride(0) % 8 == 0, "decode_gemm_glu: 1 <= M <= 64");
+  if (splits > 1) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * N,
+                "decode_gemm_glu: ws must hold S*M*N fp32");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_decode_gemm(act.data_ptr(), act.stride(0), splits > 1 ? ws.data_ptr<float>() : nullptr,
+                                           x.data_ptr(), x.stride(0), wp.data_ptr(), M, N, K, rt, splits, true,
+                                           hipserve::DG_GLU, cur_stream()),
+              "decode_gemm_glu: unsupported (rt, K/splits)");
+}
+
+void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
+                        const at::Tensor& weight, double eps) {
+  CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous());
+  const int M = residual.size(0), N = residual.size(1);
+  TORCH_CHECK(out.sizes() == residual.sizes() && ws.numel() >= splits * M * N && N % 8 == 0 && N <= 16384);
+  TORCH_CHECK(weight.numel() == N && weight.is_contiguous() &&
+              (weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  hipserve::launch_splitk_add_rmsnorm(out.data_ptr(), residual.data_ptr(), ws.data_ptr<float>(), splits,
+                                      weight.data_ptr(), weight.scalar_type() == at::kFloat, M, N, (float)eps,
+                                      cur_stream());
+}
+
+void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
+                       const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
+                       int64_t nq, int64_t nkv, int64_t head_dim, int64_t mode) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_ROWMAJOR(qkv);
+  const int T = qkv.size(0);
+  const long N = (nq + 2 * nkv) * head_dim;
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= N);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * T * N);
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong);
+  TORCH_CHECK(positions.numel() >= T && slots.numel() >= T);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim && cos_sin.is_contiguous());
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim, "k_cache [blocks, nkv, bs, D]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == nkv && v_cache.size(2) == head_dim, "v_cache [blocks, nkv, D, bs]");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous());
+  TORCH_CHECK(head_dim % 16 == 0 && (mode == 0 || mode == 1));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  hipserve::launch_splitk_rope_cache(qkv.data_ptr(), qkv.stride(0), ws.data_ptr<float>(), splits,
+                                     positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(),
+                                     cos_sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), T, nq, nkv,
+                                     head_dim, k_cache.size(2), mode, cur_stream());
+}
+
+void pack_decode_weight(at::Tensor& out, const at::Tensor& w, bool glu) {
   CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_BF16(out); CHECK_CONTIG(out);
   TORCH_CHECK(w.dim() == 2 && w.size(1) % 256 == 0, "pack_decode_weight: w [N, K], K % 256 == 0");
   const long N = w.size(0), K = w.size(1);
   TORCH_CHECK(out.numel() == (N + 127) / 128 * 128 * K, "pack_decode_weight: out must hold ceil(N/128)*128*K");
+  TORCH_CHECK(!glu || N % 128 == 0, "pack_decode_weight: glu packing needs N % 128 == 0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
-  hipserve::launch_pack_decode_weight(out.data_ptr(), w.data_ptr(), N, K, cur_stream());
+  hipserve::launch_pack_decode_weight(out.data_ptr(), w.data_ptr(), N, K, glu, cur_stream());
 }
 
 void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,
@@ -359,7 +438,11 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("fill_uniform(Tensor(a!) out, int row0, int col0, int gcols, int key, float scale) -> ()");
   m.def("decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int rt, int splits) -> ()");
   m.def("decode_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
-  m.def("pack_decode_weight(Tensor(a!) out, Tensor w) -> ()");
+  m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");
+  m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
+  m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
+  m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
+  m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
@@ -377,6 +460,10 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm", &decode_gemm);
   m.impl("decode_gemm_packed", &decode_gemm_packed);
   m.impl("pack_decode_weight", &pack_decode_weight);
+  m.impl("decode_gemm_partial", &decode_gemm_partial);
+  m.impl("decode_gemm_glu", &decode_gemm_glu);
+  m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
+  m.impl("splitk_rope_cache", &splitk_rope_cache);
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);

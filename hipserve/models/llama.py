@@ -98,6 +98,7 @@ class LlamaModel:
         self.decode_partition = 512
         self.block_size_hint = 16  # KV block size (set by the runner)
         self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
+        self.fused_decode = True  # decode-only batches: split-K partials -> fused epilogues
 
     # ---------------------------------------------------------------- weights
     def allocate_random(self, seed: int = 0, std: float = 0.02):
@@ -174,15 +175,32 @@ class LlamaModel:
     def pack_decode_weights(self, shapes) -> int:
         """Pre-shuffled copies (ops/gemm.py ``PACKED``) of the dense projections whose
         (N, K) the decode tuner assigned to the packed decode GEMM. Costs one extra
-        copy of those weights in HBM (288 GB per MI355X: bandwidth over capacity)."""
+        copy of those weights in HBM (288 GB per MI355X: bandwidth over capacity).
+        With the fused decode path the merged gate|up weight is packed
+        gate/up-interleaved instead (``PACKED_GLU``: the SiLU-GLU runs in its epilogue)."""
         n = 0
-        ws = [w for lw in self.layers for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd)]
-        ws.append(self.lm_head)
-        for w in ws:
-            if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
-                gemm.register_packed(w)
-                n += w.numel() * w.element_size()
+        glu = self.fused_decode and self.tp.world_size == 1
+        for lw in self.layers:
+            for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
+                if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
+                    gemm.register_packed(w, glu=glu and w is lw.wgu and w.shape[0] % 128 == 0)
+                    n += w.numel() * w.element_size()
+        w = self.lm_head
+        if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
+            gemm.register_packed(w)
+            n += w.numel() * w.element_size()
         return n
+
+    def fused_gemm_shapes(self):
+        """(N, K) of the projections whose decode GEMM output feeds a fused epilogue."""
+        if self.tp.world_size != 1 or not self.layers:
+            return set()
+        lw = self.layers[0]
+        return {tuple(w.shape) for w in (lw.wqkv, lw.wo, lw.wd) if isinstance(w, torch.Tensor)}
+
+    def _fused_ok(self, meta: AttnMeta) -> bool:
+        return (self.fused_decode and meta.num_prefill_tokens == 0 and self.tp.world_size == 1
+                and getattr(self.ops, "name", "") == "hip" and self.cfg.num_experts == 0)
 
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.tp.world_size == 1:
@@ -200,6 +218,8 @@ class LlamaModel:
         H, D, nq, nkv = cfg.hidden_size, self.D, self.nq, self.nkv
         eps = cfg.rms_norm_eps
         Tp, Td = meta.num_prefill_tokens, meta.num_decode
+        if self._fused_ok(meta):
+            return self.forward_decode_fused(ids, meta, kv_caches)
         h = self.embed_tokens(ids)
         residual = torch.empty_like(h)
         xn = torch.empty_like(h)
@@ -234,6 +254,61 @@ class LlamaModel:
                 h = self.linear(act, lw.wd)
             self.tp.all_reduce(h)
         ops.fused_add_rmsnorm(xn, h, residual, self.norm, eps)
+        return xn
+
+    def forward_decode_fused(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Decode-only forward (TP=1) with the decode GEMMs' split-K partials reduced
+        inside the next op: qkv -> RoPE + KV write, o_proj -> residual add + RMSNorm,
+        down -> residual add + the NEXT
+        layer's RMSNorm (final norm after the last layer), SiLU-GLU in the gate|up
+        GEMM's epilogue (gate/up-interleaved packing). Bit-identical to
+        ``forward``; each fusion point falls back to the unfused op when the tuner
+        picked hipBLASLt for that projection."""
+        ops, cfg, op = self.ops, self.cfg, torch.ops.hipserve
+        T = ids.shape[0]
+        D, nq, nkv = self.D, self.nq, self.nkv
+        eps = cfg.rms_norm_eps
+        h = self.embed_tokens(ids)
+        residual = h.clone()
+        xn = torch.empty_like(h)
+        ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
+        attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
+        part, tmp_out, tmp_ml = self._decode_split(T, meta)
+        L = len(self.layers)
+        for i, lw in enumerate(self.layers):
+            kc, vc = kv_caches[i]
+            fc = gemm.fused_choice(T, lw.wqkv)
+            if fc is not None:
+                ws, S = gemm.gemm_partial(xn, lw.wqkv, fc)
+                qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)
+                op.splitk_rope_cache(qkv, ws, S, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
+                                     nq, nkv, D, cfg.rope_mode)
+            else:
+                qkv = self.linear(xn, lw.wqkv)
+                ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
+                               cfg.rope_mode)
+            ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
+                             nq, nkv, part, self.scale)
+            fc = gemm.fused_choice(T, lw.wo)
+            if fc is not None:
+                ws, S = gemm.gemm_partial(attn, lw.wo, fc)
+                op.splitk_add_rmsnorm(xn, residual, ws, S, lw.ln2, eps)
+            else:
+                ops.fused_add_rmsnorm(xn, self.linear(attn, lw.wo), residual, lw.ln2, eps)
+            gc = gemm.glu_choice(T, lw.wgu)
+            if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
+                act = gemm.gemm_glu(xn, lw.wgu, gc)
+            else:
+                gu = self.linear(xn, lw.wgu)
+                act = torch.empty(T, self.inter, device=h.device, dtype=h.dtype)
+                ops.silu_and_mul(act, gu)
+            nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
+            fc = gemm.fused_choice(T, lw.wd)
+            if fc is not None:
+                ws, S = gemm.gemm_partial(act, lw.wd, fc)
+                op.splitk_add_rmsnorm(xn, residual, ws, S, nxt, eps)
+            else:
+                ops.fused_add_rmsnorm(xn, self.linear(act, lw.wd), residual, nxt, eps)
         return xn
 
     def _decode_split(self, Td: int, meta: AttnMeta):

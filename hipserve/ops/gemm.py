@@ -27,7 +27,13 @@ DG_STEPS = [1, 2, 4, 7, 8, 16]  # 256-k steps per workgroup (compile-time in dec
 # decode weights pre-shuffled for the packed decode GEMM, keyed by the plain
 # weight's data_ptr (the plain [N, K] copy stays for prefill / hipBLASLt)
 PACKED: dict[int, tuple] = {}  # data_ptr -> (weakref to the plain weight, packed copy)
+# merged gate|up weights packed gate/up-interleaved for the GLU-fused decode GEMM
+PACKED_GLU: dict[int, tuple] = {}
 COLD_BYTES = 1 << 30
+# A decode GEMM whose fp32 partials feed a fused epilogue (decode_fused.hip) saves
+# the separate elementwise launch that hipBLASLt's output would still need
+# (~5 us each at decode sizes, profiles/r1_bench_llama3_8b_v3_trace.md).
+FUSE_BONUS_US = 4.0
 _EMPTY = {}
 TUNE_MS = [1, 2, 4, 8, 16, 24, 32, 48, 64]
 
@@ -81,7 +87,7 @@ class GemmTuner:
         return v[len(v) // 2] * 1000.0 / n
 
     @torch.inference_mode()
-    def tune(self, shapes, device, ms=None):
+    def tune(self, shapes, device, ms=None, fused=()):
         # inference mode like the engine's graph capture: the generator state tensors a
         # capture registers must not switch between inference and normal tensors
         ms = [m for m in (ms or TUNE_MS) if m <= 64]
@@ -95,6 +101,8 @@ class GemmTuner:
                 out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
                 best, best_t = "blas", self._time(lambda i: F.linear(x, ws_[i % ncopy]), n=n)
                 t_blas = best_t
+                if (N, K) in fused:
+                    best_t += FUSE_BONUS_US  # hipBLASLt output still needs the epilogue launch
                 for cfg in self.candidates(M, N, K, packed=wp_ is not None):
                     t = self._time(lambda i: run_choice(cfg, out, x, ws_[i % ncopy],
                                                         wp_[i % ncopy] if wp_ else None), n=n)
@@ -159,32 +167,41 @@ def packable(N: int, K: int) -> bool:
     return K % 256 == 0 and N % 8 == 0
 
 
-def pack(w: torch.Tensor) -> torch.Tensor:
-    """Pre-shuffle a [N, K] bf16 weight for ``decode_gemm_packed`` (flat, N padded to 128)."""
+def pack(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
+    """Pre-shuffle a [N, K] bf16 weight for ``decode_gemm_packed`` (flat, N padded
+    to 128). glu: [gate; up] weight, tiles interleave 64 gate + 64 up rows."""
     N, K = w.shape
     out = torch.empty(-(-N // 128) * 128 * K, dtype=w.dtype, device=w.device)
-    torch.ops.hipserve.pack_decode_weight(out, w.contiguous())
+    torch.ops.hipserve.pack_decode_weight(out, w.contiguous(), glu)
     return out
 
 
-def packed_of(w: torch.Tensor):
-    """The packed copy of ``w`` — only if registered for this very tensor (a freed
-    weight's address may be reused by another tensor)."""
-    e = PACKED.get(w.data_ptr())
+def _lookup(reg, w):
+    e = reg.get(w.data_ptr())
     if e is None:
         return None
     ref, wp = e
-    if ref() is not w:
-        PACKED.pop(w.data_ptr(), None)
+    if ref() is not w:  # a freed weight's address reused by another tensor
+        reg.pop(w.data_ptr(), None)
         return None
     return wp
 
 
-def register_packed(w: torch.Tensor) -> torch.Tensor:
-    wp = packed_of(w)
+def packed_of(w: torch.Tensor):
+    """The packed copy of ``w`` — only if registered for this very tensor."""
+    return _lookup(PACKED, w)
+
+
+def glu_of(w: torch.Tensor):
+    return _lookup(PACKED_GLU, w)
+
+
+def register_packed(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
+    reg = PACKED_GLU if glu else PACKED
+    wp = _lookup(reg, w)
     if wp is None:
-        wp = pack(w)
-        PACKED[w.data_ptr()] = (weakref.ref(w), wp)
+        wp = pack(w, glu)
+        reg[w.data_ptr()] = (weakref.ref(w), wp)
     return wp
 
 
@@ -194,6 +211,50 @@ def decode_gemm_packed(out, x, wp, N, rt, splits):
           else _empty(x.device)[1])
     torch.ops.hipserve.decode_gemm_packed(out, x, wp, ws, N, rt, splits)
     return out
+
+
+def fused_choice(M: int, w):
+    """(choice, packed weight or None) when the tuned decode GEMM for ``w`` at M can
+    write split-K partials for a fused epilogue; None for hipBLASLt / skinny."""
+    if not isinstance(w, torch.Tensor) or M > 64 or not TUNER.table:
+        return None
+    c = TUNER.choose(M, w.shape[0], w.shape[1])
+    if not isinstance(c, tuple) or c[0] not in ("dg", "dgp"):
+        return None
+    wp = packed_of(w) if c[0] == "dgp" else None
+    return c, wp
+
+
+def gemm_partial(x, w, fc):
+    """Run fused_choice ``fc`` on x writing fp32 partials; returns (ws, S)."""
+    (kind, rt, S), wp = fc
+    M, N = x.shape[0], w.shape[0]
+    ws = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
+    packed = wp is not None
+    torch.ops.hipserve.decode_gemm_partial(ws, x, wp if packed else w, N, rt, S, packed)
+    return ws, S
+
+
+def glu_choice(M: int, w):
+    """(rt, S, glu-packed weight) when the tuned decode GEMM for the merged gate|up
+    weight ``w`` at M is the packed kernel and a GLU-interleaved copy exists."""
+    if not isinstance(w, torch.Tensor) or M > 64 or not TUNER.table:
+        return None
+    c = TUNER.choose(M, w.shape[0], w.shape[1])
+    wp = glu_of(w)
+    if not isinstance(c, tuple) or c[0] != "dgp" or wp is None:
+        return None
+    return c[1], c[2], wp
+
+
+def gemm_glu(x, w, gc):
+    """act[M, N/2] = silu(x Wg^T) * (x Wu^T) in one decode GEMM (+ GLU reduce if S > 1)."""
+    rt, S, wp = gc
+    M, N = x.shape[0], w.shape[0]
+    act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+    ws = (torch.empty(S * M * N, dtype=torch.float32, device=x.device) if S > 1 else _empty(x.device)[1])
+    torch.ops.hipserve.decode_gemm_glu(act, x, wp, ws, N, rt, S)
+    return act
 
 
 def run_choice(c, out, x, w, wp=None):

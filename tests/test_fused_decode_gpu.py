@@ -1,0 +1,143 @@
+"""Fused decode epilogues (csrc/kernels/decode_fused.hip + decode_gemm.hip partial
+/ silu-x modes) must be BIT-identical to the unfused chains they replace, and the
+fused decode forward of the model bit-identical to the unfused forward."""
+import math
+
+import pytest
+import torch
+
+from hipserve.ops import KernelOps, gemm
+from hipserve.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    return KernelOps()
+
+
+def _partials(S, M, N, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randn(S, M, N, device=DEV, generator=g) * 0.5
+
+
+@pytest.mark.parametrize("S,M,N", [(1, 5, 4096), (4, 64, 4096), (8, 17, 2048), (3, 1, 8192)])
+@pytest.mark.parametrize("wf32", [False, True])
+def test_splitk_add_rmsnorm_bit_exact(ops, S, M, N, wf32):
+    ws = _partials(S, M, N, S * 100 + M)
+    res0 = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, device=DEV, dtype=torch.float32 if wf32 else torch.bfloat16)
+    # unfused: reduce -> bf16, fused add + rmsnorm
+    h = ws[0].clone()
+    for s in range(1, S):
+        h = h + ws[s]
+    h = h.to(torch.bfloat16)
+    r1, o1 = res0.clone(), torch.empty_like(res0)
+    ops.fused_add_rmsnorm(o1, h, r1, w, 1e-5)
+    r2, o2 = res0.clone(), torch.empty_like(res0)
+    torch.ops.hipserve.splitk_add_rmsnorm(o2, r2, ws.contiguous(), S, w, 1e-5)
+    assert torch.equal(r1, r2) and torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("S", [1, 4])
+def test_splitk_rope_cache_bit_exact(ops, mode, S):
+    T, nq, nkv, D, bs = 23, 32, 8, 128, 16
+    N = (nq + 2 * nkv) * D
+    ws = _partials(S, T, N, 7 + S)
+    h = ws[0].clone()
+    for s in range(1, S):
+        h = h + ws[s]
+    qkv1 = h.to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    slots = torch.randperm(64 * bs, device=DEV)[:T]
+    slots[3] = -1
+    cs = ref.rope_cos_sin(D, 4096, 500000.0).to(DEV)
+    kc1 = torch.zeros(64, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc1 = torch.zeros(64, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    ops.rope_cache(qkv1, pos, slots, cs, kc1, vc1, nq, nkv, D, mode)
+    qkv2 = torch.zeros(T, N, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.splitk_rope_cache(qkv2, ws.contiguous(), S, pos, slots, cs, kc2, vc2, nq, nkv, D, mode)
+    assert torch.equal(qkv1[:, : nq * D], qkv2[:, : nq * D])
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+
+
+@pytest.mark.parametrize("M", [1, 16, 40, 64])
+@pytest.mark.parametrize("rt,S", [(1, 1), (2, 1), (1, 4), (2, 2)])
+def test_glu_gemm_bit_exact(ops, M, rt, S):
+    """gate|up decode GEMM with the SiLU-GLU epilogue == packed GEMM + silu_and_mul."""
+    I, K = 1792, 4096
+    N = 2 * I
+    torch.manual_seed(M + S)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    gu = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    gemm.decode_gemm_packed(gu, x, gemm.pack(w), N, rt, S)
+    want = torch.empty(M, I, device=DEV, dtype=torch.bfloat16)
+    ops.silu_and_mul(want, gu)
+    act = gemm.gemm_glu(x, w, (rt, S, gemm.pack(w, glu=True)))
+    assert torch.equal(act, want)
+
+
+def _small_model(ops, seed=0):
+    from hipserve.config import PRESETS
+    from hipserve.models.llama import LlamaModel
+    from hipserve.parallel.comm import TPGroup
+
+    cfg = PRESETS["llama-3-8b"].replace(hidden_size=1024, intermediate_size=3584, num_heads=8,
+                                        num_kv_heads=2, num_layers=3, vocab_size=4096,
+                                        max_position_embeddings=2048)
+    m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, ops, max_pos=2048)
+    m.allocate_random(seed=seed, std=0.05)
+    return m, cfg
+
+
+@pytest.mark.parametrize("choices", ["dgp", "dg", "mixed"])
+def test_fused_decode_forward_bit_exact(ops, choices):
+    """Model forward on a decode batch: fused epilogues vs the unfused path."""
+    from hipserve.models.llama import AttnMeta
+
+    m, cfg = _small_model(ops)
+    old = dict(gemm.TUNER.table)
+    try:
+        gemm.TUNER.table.clear()
+        shapes = m.gemm_shapes()
+        for (N, K) in shapes:
+            kind = "dgp" if choices == "dgp" or (choices == "mixed" and N != 1024) else "dg"
+            for mm in gemm.TUNE_MS:
+                S = 2 if K >= 1024 else 1
+                gemm.TUNER.table[(mm, N, K)] = (kind, 1, S)
+        if choices == "mixed":
+            for mm in gemm.TUNE_MS:  # o_proj on hipBLASLt: unfused fallback for that op
+                gemm.TUNER.table[(mm, 1024, 1024)] = "blas"
+        m.pack_decode_weights(set(shapes))
+        B, bs, D = 24, 16, cfg.head_dim
+        ctx = torch.randint(1, 300, (B,), device=DEV, dtype=torch.int32)
+        nblk = 64
+        bt = torch.randperm(B * nblk, device=DEV).int().view(B, nblk)
+        pos = (ctx - 1).long()
+        slots = (bt.gather(1, (pos // bs).view(-1, 1).int()).view(-1).long() * bs + pos % bs)
+        ids = torch.randint(0, cfg.vocab_size, (B,), device=DEV)
+        kv1 = m.allocate_kv_cache(B * nblk, bs)
+        for kc, vc in kv1:
+            kc.normal_()
+            vc.normal_()
+        kv2 = [(k.clone(), v.clone()) for k, v in kv1]
+        parts = math.ceil(nblk * bs / 512)
+        mk = lambda: AttnMeta(num_prefill_tokens=0, num_decode=B, positions=pos, slot_mapping=slots,
+                              bt_decode=bt, ctx_decode=ctx,
+                              tmp_out=torch.empty(B, m.nq, parts, D, device=DEV),
+                              tmp_ml=torch.empty(B, m.nq, parts, 2, device=DEV))
+        m.fused_decode = False
+        out1 = m.forward(ids, mk(), kv1).clone()
+        m.fused_decode = True
+        out2 = m.forward(ids, mk(), kv2).clone()
+        assert torch.equal(out1, out2)
+        for (k1, v1), (k2, v2) in zip(kv1, kv2):
+            assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    finally:
+        gemm.TUNER.table.clear()
+        gemm.TUNER.table.update(old)
