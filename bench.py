@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
     ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0"],
+                    help="GGUF tier: random-init GGUF-quantised weights (BASELINE config: Llama-3-8B Q4_K_M)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
 
@@ -85,7 +87,9 @@ def main():
     cfg = EngineConfig(model=args.model, device="cuda", max_num_seqs=max(args.concurrency, 1),
                        max_num_batched_tokens=args.max_num_batched_tokens,
                        max_model_len=args.input_len + args.output_len + 64,
-                       enforce_eager=args.enforce_eager, seed=rank)
+                       enforce_eager=args.enforce_eager, seed=rank,
+                       load_format="dummy" if args.quantization else "auto",
+                       extra={"quantization": args.quantization} if args.quantization else {})
     t0 = time.time()
     engine = LLMEngine(cfg, tp=TPGroup(0, 1, None, dev))
     init_s = time.time() - t0
@@ -166,12 +170,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16" if not args.quantization else f"bf16 activations, GGUF {args.quantization.upper()} weights",
         "data": "synthetic prompts (random token ids), random-init weights",
         "p50_ttft_ms": round(1000 * float(p50), 2),
         "path": args.path,
         "config": {
-            "model": args.model,
+            "model": args.model + (f" GGUF {args.quantization.upper()}" if args.quantization else ""),
             "tp": 1,
             "global_batch": args.concurrency * world,
             "seq_len": args.input_len + args.output_len,

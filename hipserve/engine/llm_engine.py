@@ -32,6 +32,9 @@ class LLMEngine:
         self.cfg = cfg
         self.tp = tp or get_tp()
         self.model_cfg = model_cfg or resolve_model_config(cfg.model, cfg.served_model_name)
+        if cfg.extra.get("quantization") and cfg.load_format == "dummy":
+            # synthetic GGUF tier: ggml llama weights use interleaved-pair RoPE
+            self.model_cfg = self.model_cfg.replace(rope_mode=1)
         self.tokenizer = get_tokenizer(cfg.model, self.model_cfg, cfg.tokenizer)
         if getattr(self.tokenizer, "model_config_override", None):
             self.model_cfg = self.tokenizer.model_config_override

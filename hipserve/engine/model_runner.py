@@ -128,7 +128,10 @@ class ModelRunner:
                 fmt = "gguf"
             else:
                 fmt = "safetensors"
-        if fmt == "dummy":
+        quant = self.ecfg.extra.get("quantization")
+        if fmt == "dummy" and quant:
+            self.model.allocate_random_quant(quant, seed=self.ecfg.seed)
+        elif fmt == "dummy":
             self.model.allocate_random(seed=self.ecfg.seed)
         elif fmt == "safetensors":
             from ..weights.safetensors_loader import load_hf_weights

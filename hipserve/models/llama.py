@@ -155,6 +155,56 @@ class LlamaModel:
                 fill(lw.wd, f"{li}.down", 0, rank * I, cfg.intermediate_size)
             self.layers.append(lw)
 
+    # synthetic GGUF schemes (GGUF-tier benchmarks): per projection ggml type;
+    # q4_k_m mirrors llama.cpp's Q4_K_M mix (attn_v, ffn_down, output in Q6_K)
+    QUANT_SCHEMES = {
+        "q4_k_m": {"q": 12, "k": 12, "v": 14, "o": 12, "gate": 12, "up": 12, "down": 14, "output": 14},
+        "q8_0": {n: 8 for n in ("q", "k", "v", "o", "gate", "up", "down", "output")},
+        "q4_0": {**{n: 2 for n in ("q", "k", "v", "o", "gate", "up", "down")}, "output": 14},
+    }
+
+    def allocate_random_quant(self, scheme: str, seed: int = 0):
+        """Random-init model with GGUF-quantised projections (``QuantWeight``, the
+        fused dequant-GEMM kernels of csrc/kernels/gguf.hip): random valid ggml
+        blocks of each projection's format. Off the GPU the same blocks are
+        dequantised to dense weights (CPU plumbing / numerics oracle)."""
+        import numpy as np
+
+        from ..ops import quant as Q
+        from ..weights import gguf as G
+
+        if self.tp.world_size != 1:
+            raise NotImplementedError("the GGUF tier runs TP=1 (one device per pod, like llama-server)")
+        types = self.QUANT_SCHEMES[scheme.lower()]
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        H, D, I = cfg.hidden_size, self.D, cfg.intermediate_size
+        nq, nkv, V = cfg.num_heads, cfg.num_kv_heads, cfg.vocab_size
+        rng = np.random.default_rng(seed)
+
+        def qtype(kind, k):  # llama.cpp-style fallback when K is not a multiple of the super-block
+            t = types[kind]
+            return t if k % G.BLOCK[t][0] == 0 else G.Q8_0
+
+        def mat(*specs):  # (kind, N, K) parts stacked along N
+            raws = [(qtype(k, kk), n, kk, Q.random_blocks(rng, qtype(k, kk), n, kk)) for k, n, kk in specs]
+            if dev.type == "cuda":
+                return Q.QuantWeight.from_raw(raws, dev)
+            return torch.cat([torch.from_numpy(G.dequantize(r, t, n * kk).reshape(n, kk)).to(dt)
+                              for t, n, kk, r in raws], 0)
+
+        g = torch.Generator().manual_seed(seed)
+        self.embed = (torch.randn(V, H, generator=g) * 0.02).to(device=dev, dtype=dt)
+        self.norm = torch.ones(H, device=dev, dtype=dt)
+        self.lm_head = mat(("output", V, H))
+        self.layers = []
+        for _ in range(cfg.num_layers):
+            self.layers.append(LayerWeights(
+                ln1=torch.ones(H, device=dev, dtype=dt),
+                wqkv=mat(("q", nq * D, H), ("k", nkv * D, H), ("v", nkv * D, H)),
+                wo=mat(("o", H, nq * D)), ln2=torch.ones(H, device=dev, dtype=dt),
+                wgu=mat(("gate", I, H), ("up", I, H)), wd=mat(("down", H, I))))
+        self.quant_linear = Q.quant_linear
+
     # ---------------------------------------------------------------- forward
     def linear(self, x: torch.Tensor, w, name: str | None = None) -> torch.Tensor:
         if isinstance(w, torch.Tensor):

@@ -96,6 +96,16 @@ class QuantWeight:
         return cls(parts)
 
     @classmethod
+    def from_raw(cls, raws: list, device):
+        """[(qtype, N, K, raw ggml bytes)] -> QuantWeight on ``device``."""
+        parts = []
+        for qtype, N, K, raw in raws:
+            q, d, m, rb = repack(raw, qtype, N, K)
+            to = lambda a, dt: torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)  # noqa: E731
+            parts.append(QuantPart(qtype, N, K, to(q, torch.uint8), to(d, torch.int16), to(m, torch.int16), rb))
+        return cls(parts)
+
+    @classmethod
     def from_float(cls, w: np.ndarray | list, qtype: int, device):
         """Quantise float matrices (tests / synthetic benchmarks)."""
         mats = w if isinstance(w, list) else [w]
@@ -107,6 +117,33 @@ class QuantWeight:
             to = lambda a, dt: torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)  # noqa: E731
             parts.append(QuantPart(qtype, N, K, to(q, torch.uint8), to(d, torch.int16), to(m, torch.int16), rb))
         return cls(parts)
+
+
+# synthetic block scales: |w| ~ 0.02 for every format (random-init benchmarks)
+_SYNTH_D = {G.Q4_K: (8e-5, 6e-4), G.Q5_K: (4e-5, 6e-4), G.Q6_K: (1.5e-5, 0.0), G.Q8_0: (2.5e-4, 0.0),
+            G.Q4_0: (4e-3, 0.0), G.Q4_1: (4e-3, -0.03)}
+
+
+def random_blocks(rng: np.random.Generator, qtype: int, N: int, K: int) -> np.ndarray:
+    """Random GGUF blocks of an [N, K] matrix in ggml's raw layout: random quant
+    bits and sub-block scales, fixed per-block fp16 scale(s) — valid blocks of the
+    real format without quantising float weights (an 8B model in seconds)."""
+    be, bb = G.BLOCK[qtype]
+    nb = K // be
+    b = rng.integers(0, 256, size=(N, nb, bb), dtype=np.uint8)
+    d, dm = _SYNTH_D[qtype]
+    f16 = lambda v: np.frombuffer(np.float16(v).tobytes(), np.uint8)  # noqa: E731
+    if qtype in (G.Q4_K, G.Q5_K):
+        b[:, :, 0:2] = f16(d)
+        b[:, :, 2:4] = f16(dm)
+    elif qtype == G.Q6_K:
+        b[:, :, 208:210] = f16(d)
+    elif qtype in (G.Q8_0, G.Q4_0, G.Q5_0):
+        b[:, :, 0:2] = f16(d)
+    elif qtype in (G.Q4_1, G.Q5_1):
+        b[:, :, 0:2] = f16(d)
+        b[:, :, 2:4] = f16(dm)
+    return b.reshape(-1)
 
 
 _scratch: dict = {}

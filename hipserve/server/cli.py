@@ -37,6 +37,8 @@ def build_parser(prog="hipserve") -> argparse.ArgumentParser:
     ap.add_argument("--trust-remote-code", action="store_true")
     ap.add_argument("--max-model-len", "--ctx-size", "-c", dest="max_model_len", type=int, default=None)
     ap.add_argument("--load-format", default="auto", choices=["auto", "dummy", "safetensors", "gguf"])
+    ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0"],
+                    help="with --load-format dummy: random-init GGUF-quantised weights (GGUF tier benchmarks)")
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
     ap.add_argument("--block-size", type=int, default=16)
@@ -68,7 +70,8 @@ def config_from_args(a) -> EngineConfig:
         max_model_len=a.max_model_len, block_size=a.block_size, max_num_seqs=a.max_num_seqs,
         max_num_batched_tokens=a.max_num_batched_tokens, num_kv_blocks=a.num_kv_blocks,
         enable_prefix_caching=a.enable_prefix_caching, enforce_eager=a.enforce_eager, seed=a.seed,
-        trust_remote_code=a.trust_remote_code, host=a.host, port=a.port)
+        trust_remote_code=a.trust_remote_code, host=a.host, port=a.port,
+        extra={"quantization": a.quantization} if a.quantization else {})
 
 
 def _free_port() -> int:

@@ -34,6 +34,21 @@ run_bench() {
   timeout -k 10 480 python -u bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1
   local rc=$?; tail -n 2 $OUT/bench.log; return $rc
 }
+run_bench_q4() {
+  timeout -k 10 480 python -u bench.py --quantization q4_k_m --out $OUT/bench_q4km.json > $OUT/bench_q4km.log 2>&1
+  local rc=$?; tail -n 2 $OUT/bench_q4km.log; return $rc
+}
+run_prof_q4() {
+  local here=$PWD
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/profq \
+     -o run -- python3 $here/bench.py --path engine --quantization q4_k_m --steps 1 --warmup 1 > $here/$OUT/profq.log 2>&1)
+  local rc=$?; tail -n 3 $OUT/profq.log
+  [ $rc -eq 0 ] || return $rc
+  local db; db=$(find $OUT/profq -name '*results.db' | head -n 1)
+  [ -n "$db" ] && (cd tools && python prof_db.py "$here/$db" "$here/$OUT/profq_summary.md" "bench.py --path engine --quantization q4_k_m" > /dev/null)
+  rm -rf $OUT/profq
+  return 0
+}
 run_prof() {
   local here=$PWD
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/prof \
@@ -57,6 +72,8 @@ for s in $steps; do
     sweep) run_sweep ;;
     ops) run_ops ;;
     bench) run_bench ;;
+    bench_q4) run_bench_q4 ;;
+    prof_q4) run_prof_q4 ;;
     prof) run_prof ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }

@@ -118,3 +118,23 @@ def test_engine_runs_gguf_on_cpu(tmp_path):
         assert r[0] == dense_greedy(eng.runner.model, pr, 6)
     out = eng.generate(["hello"], SamplingParams(temperature=0.0, max_tokens=3, ignore_eos=True))
     assert len(out[0][0]) == 3
+
+
+def test_synthetic_quant_engine_cpu():
+    """--load-format dummy --quantization q4_k_m on the CPU plumbing engine: the
+    random ggml blocks are dequantised to dense weights (same blocks as on GPU)."""
+    import torch
+
+    from hipserve.config import EngineConfig
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.engine.request import SamplingParams
+    from hipserve.parallel.comm import TPGroup
+
+    eng = LLMEngine(EngineConfig(model="tiny-llama", load_format="dummy", device="cpu", dtype="float32",
+                                 num_kv_blocks=128, max_model_len=256, max_num_batched_tokens=64,
+                                 max_num_seqs=4, extra={"quantization": "q4_k_m"}), tp=TPGroup())
+    m = eng.runner.model
+    assert m.cfg.rope_mode == 1 and isinstance(m.layers[0].wqkv, torch.Tensor)
+    assert torch.isfinite(m.layers[0].wd).all()
+    res = eng.generate([[1, 5, 6, 7]], SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
+    assert len(res[0][0]) == 6

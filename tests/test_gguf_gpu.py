@@ -77,3 +77,42 @@ def test_gguf_engine_on_gpu(tmp_path):
                        SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True))
     assert all(len(r[0]) == 10 for r in res)
     assert res[0][0] == res[2][0] == res[4][0]
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K, G.Q8_0, G.Q4_0])
+def test_random_blocks_gemm(qt):
+    """Synthetic GGUF blocks (ops/quant.random_blocks, the GGUF-tier benchmark
+    weights): decode GEMM and prefill path vs x @ numpy-dequantised W."""
+    from hipserve.ops.quant import random_blocks
+    N, K = 320, 1024
+    raw = random_blocks(np.random.default_rng(qt), qt, N, K)
+    dense = G.dequantize(raw, qt, N * K).reshape(N, K)
+    assert np.isfinite(dense).all() and 0.002 < np.abs(dense).mean() < 0.2
+    qw = QuantWeight.from_raw([(qt, N, K, raw)], "cuda")
+    want_w = torch.from_numpy(dense).cuda()
+    for M in (4, 64, 200):
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        y = quant_linear(x, qw).float()
+        want = x.float() @ want_w.T
+        assert (y - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-3
+
+
+def test_synthetic_q4_k_m_engine():
+    """Engine with random-init Q4_K_M weights (bench.py --quantization q4_k_m) on the GPU."""
+    from hipserve.config import PRESETS, EngineConfig
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.engine.request import SamplingParams
+    from hipserve.parallel.comm import TPGroup
+
+    cfg = PRESETS["small-llama"]
+    eng = LLMEngine(EngineConfig(model="small-llama", load_format="dummy", device="cuda", num_kv_blocks=256,
+                                 max_model_len=1024, max_num_batched_tokens=256, max_num_seqs=8,
+                                 extra={"quantization": "q4_k_m"}),
+                    tp=TPGroup(0, 1, None, torch.device("cuda", 0)), model_cfg=cfg)
+    m = eng.runner.model
+    assert isinstance(m.layers[0].wqkv, QuantWeight) and m.cfg.rope_mode == 1
+    assert [p.qtype for p in m.layers[0].wqkv.parts] == [G.Q4_K, G.Q4_K, G.Q6_K]
+    res = eng.generate([[1] + list(range(300, 400)), [1, 5, 6]] * 3,
+                       SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True))
+    assert all(len(r[0]) == 10 for r in res)
+    assert res[0][0] == res[2][0] == res[4][0]

@@ -65,6 +65,23 @@ def summarize(path, title="rocprofv3 kernel trace"):
         sp = [span(s) for s in pre]
         L.append(f"prefill/mixed step: median span {statistics.median(sp):.0f} us, "
                  f"kernel-busy {statistics.median(busy(s) for s in pre):.0f} us")
+        big = [s for s in pre if span(s) >= 0.8 * statistics.median(sp)]
+        per = {}
+        for s in big:
+            acc = {}
+            for f, b, e in s:
+                a = acc.setdefault(f, [0, 0])
+                a[0] += 1
+                a[1] += e - b
+            for f, (n, d) in acc.items():
+                per.setdefault(f, []).append((n, d))
+        agg = sorted(((f, v[0][0], statistics.median(d for _, d in v) / 1e3) for f, v in per.items()),
+                     key=lambda x: -x[2])
+        L += ["", f"### per full prefill step (median over {len(big)} steps)", "",
+              "| kernel | calls/step | us/step | avg us |", "|---|---:|---:|---:|"]
+        for f, n, d in agg[:25]:
+            L.append(f"| `{f}` | {n} | {d:.1f} | {d / n:.2f} |")
+        L.append("")
     if dec:
         sp = [span(s) for s in dec]
         bz = [busy(s) for s in dec]
