@@ -7,7 +7,7 @@ compiled as host C++, and everything is linked into one shared object that
 ``torch.ops.load_library`` loads. The built ``.so`` files live next to the Python
 sources, so they travel with the repo snapshot to the GPU box.
 
-Usage: ``python -m hipserve._build [--force] [-j N]``
+Usage: ``python -m hipserve._build [--force] [-j N] [--sanitize thread|address]``
 """
 from __future__ import annotations
 
@@ -159,6 +159,39 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     return so
 
 
+SANITIZERS = {
+    # ThreadSanitizer: the shm ring's acquire/release protocol between threads
+    "thread": ["-fsanitize=thread"],
+    # AddressSanitizer + UBSan: out-of-bounds slot copies, pool bookkeeping
+    "address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"],
+}
+
+
+def build_sanitizer_test(kind: str, verbose: bool = False) -> str:
+    """Host-only build of csrc/tests/runtime_stress.cpp (native runtime cores, no
+    Python, no GPU) under a sanitizer; returns the binary path. GPU-side
+    sanitizers are not available on the MI355X pool (no xnack+), so the
+    sanitizers cover the host runtime; kernels are checked by the numerics tests."""
+    if kind not in SANITIZERS:
+        raise ValueError(f"sanitizer {kind!r}: one of {sorted(SANITIZERS)}")
+    out_dir = os.path.join(ROOT, "build", "san")
+    os.makedirs(out_dir, exist_ok=True)
+    src = os.path.join(CSRC, "tests", "runtime_stress.cpp")
+    deps = [src] + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.h")))
+    flags = ["-O1", "-g", "-std=c++17", *SANITIZERS[kind], "-pthread"]
+    exe = os.path.join(out_dir, f"runtime_stress_{kind}")
+    want = _stamp(deps, flags)
+    stamp = exe + ".stamp"
+    if os.path.exists(exe) and os.path.exists(stamp) and open(stamp).read() == want:
+        return exe
+    _run(["g++", *flags, src, "-o", exe, "-lrt"])
+    with open(stamp, "w") as f:
+        f.write(want)
+    if verbose:
+        print(f"[hipserve build] {os.path.relpath(exe, ROOT)}", flush=True)
+    return exe
+
+
 def build_all(force: bool = False, jobs: int | None = None, verbose: bool = True):
     jobs = jobs or int(os.environ.get("MAX_JOBS", "8"))
     rt = build_runtime(force=force, verbose=verbose)
@@ -170,7 +203,11 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--sanitize", action="append", choices=sorted(SANITIZERS),
+                    help="also build the native-runtime stress test under this sanitizer")
     a = ap.parse_args(argv)
+    for kind in a.sanitize or []:
+        print(build_sanitizer_test(kind, verbose=True))
     so, rt = build_all(force=a.force, jobs=a.jobs)
     print(so)
     if rt:
