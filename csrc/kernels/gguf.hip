@@ -14,8 +14,9 @@
 // format so that each lane decodes whole contiguous byte runs of ONE block
 // (64 k per lane per 256-k super-block); x fragments follow the same permutation
 // from an LDS-staged x chunk shared by the workgroup's 4 waves (64 rows).
-// Split-K over workgroups (fp32 atomics into a workspace) fills the 256 CUs when
-// N is small.
+// Split-K over workgroups fills the 256 CUs when N is small: each K slice writes
+// its own fp32 slab ws[split, M, N] (plain stores, no pre-zeroing, no atomics:
+// deterministic and hipGraph-safe) and a reduce kernel sums the slabs in order.
 //
 // qdequant (prefill, large M): the same decoders write a bf16 copy that feeds a
 // hipBLASLt GEMM (compute-bound regime, dequant traffic is noise there).
@@ -211,18 +212,22 @@ __global__ __launch_bounds__(256) void qgemm_kernel(
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 4 * g + r;
       if (n >= N) continue;
-      if (ws) atomicAdd(ws + (long)m * N + n, acc[t][r]);
+      if (ws) ws[((long)blockIdx.y * M + m) * N + n] = acc[t][r];
       else out[m * out_stride + n] = f32_to_bf16(acc[t][r]);
     }
   }
 }
 
-__global__ void f32_to_bf16_kernel(unsigned short* __restrict__ out, const float* __restrict__ in,
-                                   int M, int N, long out_stride) {
+// out[m, n] = bf16(sum over the S slabs, in slab order)
+__global__ void splitk_sum_bf16_kernel(unsigned short* __restrict__ out, const float* __restrict__ ws, int M, int N,
+                                       int S, long out_stride) {
   const long i = blockIdx.x * 256L + threadIdx.x;
-  if (i >= (long)M * N) return;
+  const long MN = (long)M * N;
+  if (i >= MN) return;
   const int m = i / N, n = i % N;
-  out[m * out_stride + n] = f32_to_bf16(in[i]);
+  float v = ws[i];
+  for (int s = 1; s < S; ++s) v += ws[s * MN + i];
+  out[m * out_stride + n] = f32_to_bf16(v);
 }
 
 template <int QT>
@@ -260,7 +265,8 @@ void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long o
                       int M, int N, int K, int splits, hipStream_t s) {
   QParams p{static_cast<const unsigned char*>(q), static_cast<const unsigned short*>(d),
             static_cast<const unsigned short*>(m), K, row_bytes};
-  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * M * N, s);
+  const int nsb = K / 256;
+  const int slabs = (nsb + (nsb + splits - 1) / splits - 1) / ((nsb + splits - 1) / splits);  // grid.y
   switch (qtype) {
     case QT_Q4_0: launch_qgemm_t<QT_Q4_0>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
     case QT_Q4_1: launch_qgemm_t<QT_Q4_1>(out, ws, x, x_stride, out_stride, p, M, N, K, splits, s); break;
@@ -272,8 +278,8 @@ void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long o
   }
   if (ws) {
     const long n = (long)M * N;
-    f32_to_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(static_cast<unsigned short*>(out), ws, M, N,
-                                                                   out_stride);
+    splitk_sum_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(static_cast<unsigned short*>(out), ws, M, N,
+                                                                       slabs, out_stride);
   }
 }
 

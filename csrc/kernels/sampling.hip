@@ -165,7 +165,9 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   float rsum = 0.f;
 #pragma unroll
   for (int w = 0; w < kSampWaves; ++w) rsum += red_b[w];
-  const int ramax = am;
+  // an all-NaN row never updates (m, am): emit token 0, never an id past the
+  // vocabulary (the next step would gather an embedding row out of bounds)
+  const int ramax = am < V ? am : 0;
 
   const float temp = temperature[row];
   if (!(temp > 1e-5f)) {

@@ -156,7 +156,10 @@ void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const 
   TORCH_CHECK(qtype >= 0 && qtype <= 6);
   if (qtype <= 2) TORCH_CHECK(d.numel() >= N * (K / 32), "missing SoA scales");
   if (qtype == 1) TORCH_CHECK(mn.numel() >= N * (K / 32), "missing SoA mins");
-  if (splits > 1) TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (long)M * N);
+  if (splits > 1) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= (long)splits * M * N,
+                "gguf_gemm: split-K needs an fp32 workspace of splits*M*N (one slab per K slice)");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::launch_gguf_gemm(out.data_ptr(), splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(),
                              x.stride(0), out.stride(0), q.data_ptr(), d.numel() ? d.data_ptr() : nullptr,

@@ -150,7 +150,7 @@ def splitk_gemm(out, x, w, splits):
     M, K = x.shape
     N = w.shape[0]
     e16, e32 = _empty(x.device)
-    ws = torch.empty(M, N, dtype=torch.float32, device=x.device) if splits > 1 else e32
+    ws = torch.empty(splits, M, N, dtype=torch.float32, device=x.device) if splits > 1 else e32
     torch.ops.hipserve.gguf_gemm(out, x, w.view(torch.uint8), e16, e16, 6, 2 * K, N, K, ws, splits)
     return out
 

@@ -182,7 +182,7 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
         off = 0
         for p in w.parts:
             sp = _splits(p.N, p.K)
-            ws = torch.empty(M, p.N, dtype=torch.float32, device=x.device) if sp > 1 else \
+            ws = torch.empty(sp, M, p.N, dtype=torch.float32, device=x.device) if sp > 1 else \
                 torch.empty(0, dtype=torch.float32, device=x.device)
             torch.ops.hipserve.gguf_gemm(out[:, off:off + p.N], x, p.q, p.d, p.m, p.kqt, p.row_bytes,
                                          p.N, p.K, ws, sp)
