@@ -64,18 +64,65 @@ HS_DEVICE int kbase(int g, int s) {
   }
 }
 
-// Decode the 64 weights lane group g owns in super-chunk sb of `row` into the 8
-// bf16x8 A fragments of the 8 MFMA k-steps.
+// Per-lane raw bytes of one super-chunk (256 k) of one weight row: loaded one
+// super-chunk ahead by the decode GEMM (load_raw), decoded into MFMA A
+// fragments when its turn comes (decode_raw) — the loads stay in flight while
+// the previous super-chunk is decoded and multiplied.
+struct RawQ {
+  u32x4 v[8];            // quant bytes (per format: see load_raw)
+  unsigned short h[4];   // SoA fp16 scales / mins (Q8_0, Q4_0, Q4_1)
+};
+
 template <int QT>
-HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a)[8]) {
+HS_DEVICE void load_raw(const QParams& p, long row, int sb, int g, RawQ& r) {
   if constexpr (QT == QT_BF16) {  // plain bf16 rows: 128 contiguous bytes per lane
     const unsigned char* rp = p.q + row * p.row_bytes + (long)sb * 512 + 128 * g;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) a[s] = __builtin_bit_cast(bf16x8, ld16(rp + 16 * s));
+    for (int s = 0; s < 8; ++s) r.v[s] = ld16(rp + 16 * s);
   } else if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
     constexpr int BB = QT == QT_Q4_K ? 144 : 176;
     const unsigned char* bp = p.q + row * p.row_bytes + (long)sb * BB;
-    const u32x4 hdr = ld16(bp);
+    const int qoff = QT == QT_Q4_K ? 16 : 48;
+    r.v[0] = ld16(bp);                     // d, dmin, 12 B packed scales/mins
+    r.v[1] = ld16(bp + qoff + 32 * g);
+    r.v[2] = ld16(bp + qoff + 32 * g + 16);
+    if constexpr (QT == QT_Q5_K) { r.v[3] = ld16(bp + 16); r.v[4] = ld16(bp + 32); }
+  } else if constexpr (QT == QT_Q6_K) {
+    const unsigned char* bp = p.q + row * p.row_bytes + (long)sb * 224;
+    const int h = g >> 1, odd = g & 1;
+    r.v[0] = ld16(bp + 64 * h + 32 * odd);
+    r.v[1] = ld16(bp + 64 * h + 32 * odd + 16);
+    r.v[2] = ld16(bp + 128 + 32 * h);
+    r.v[3] = ld16(bp + 128 + 32 * h + 16);
+    r.v[4] = ld16(bp + 192);               // 16 int8 sub-block scales
+    r.v[5] = ld16(bp + 208);               // d (+ padding)
+  } else if constexpr (QT == QT_Q8_0) {
+    const unsigned char* qp = p.q + row * (long)p.K + (long)sb * 256 + 64 * g;
+    const unsigned short* dp = p.d + row * (long)(p.K / 32) + sb * 8 + 2 * g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = ld16(qp + 16 * i);
+    r.h[0] = dp[0];
+    r.h[1] = dp[1];
+  } else {  // Q4_0 / Q4_1 SoA
+    const unsigned char* qp = p.q + row * (long)(p.K / 2) + (long)sb * 128 + 32 * g;
+    const long di = row * (long)(p.K / 32) + sb * 8 + 2 * g;
+    r.v[0] = ld16(qp);
+    r.v[1] = ld16(qp + 16);
+    r.h[0] = p.d[di];
+    r.h[1] = p.d[di + 1];
+    if constexpr (QT == QT_Q4_1) { r.h[2] = p.m[di]; r.h[3] = p.m[di + 1]; }
+  }
+}
+
+// Decode the 64 weights lane group g owns in the loaded super-chunk into the 8
+// bf16x8 A fragments of the 8 MFMA k-steps.
+template <int QT>
+HS_DEVICE void decode_raw(const RawQ& r, int g, bf16x8 (&a)[8]) {
+  if constexpr (QT == QT_BF16) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) a[s] = __builtin_bit_cast(bf16x8, r.v[s]);
+  } else if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
+    const u32x4 hdr = r.v[0];
     unsigned char sc12[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) sc12[i] = (hdr[1 + i / 4] >> (8 * (i & 3))) & 0xFF;
@@ -84,10 +131,9 @@ HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a
     scale_min_k4(2 * g, sc12, s1, m1);
     scale_min_k4(2 * g + 1, sc12, s2, m2);
     const float d1 = d * s1, mm1 = dmin * m1, d2 = d * s2, mm2 = dmin * m2;
-    const int qoff = QT == QT_Q4_K ? 16 : 48;
-    u32x4 qs[2] = {ld16(bp + qoff + 32 * g), ld16(bp + qoff + 32 * g + 16)};
+    const u32x4 qs[2] = {r.v[1], r.v[2]};
     u32x4 qh[2];
-    if constexpr (QT == QT_Q5_K) { qh[0] = ld16(bp + 16); qh[1] = ld16(bp + 32); }
+    if constexpr (QT == QT_Q5_K) { qh[0] = r.v[3]; qh[1] = r.v[4]; }
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -102,13 +148,11 @@ HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a
         a[s][j] = static_cast<__bf16>((s < 4) ? d1 * q - mm1 : d2 * q - mm2);
       }
   } else if constexpr (QT == QT_Q6_K) {
-    const unsigned char* bp = p.q + row * p.row_bytes + (long)sb * 224;
+    const u32x4 ql[2] = {r.v[0], r.v[1]};
+    const u32x4 qh[2] = {r.v[2], r.v[3]};
+    const u32x4 scv = r.v[4];
+    const float d = h2f(r.v[5][0] & 0xFFFF);
     const int h = g >> 1, odd = g & 1;
-    u32x4 ql[2] = {ld16(bp + 64 * h + 32 * odd), ld16(bp + 64 * h + 32 * odd + 16)};
-    u32x4 qh[2] = {ld16(bp + 128 + 32 * h), ld16(bp + 128 + 32 * h + 16)};
-    const u32x4 scv = ld16(bp + 192);
-    const u32x4 dv = ld16(bp + 208);
-    const float d = h2f(dv[0] & 0xFFFF);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int q = odd + 2 * (s >> 2);
@@ -125,27 +169,22 @@ HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a
       }
     }
   } else if constexpr (QT == QT_Q8_0) {
-    const unsigned char* qp = p.q + row * (long)p.K + (long)sb * 256 + 64 * g;
-    const unsigned short* dp = p.d + row * (long)(p.K / 32) + sb * 8 + 2 * g;
-    const float dA = h2f(dp[0]), dB = h2f(dp[1]);
-    u32x4 v[4] = {ld16(qp), ld16(qp + 16), ld16(qp + 32), ld16(qp + 48)};
+    const float dA = h2f(r.h[0]), dB = h2f(r.h[1]);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const float dd = (s < 4) ? dA : dB;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = 8 * s + j;  // byte within the lane's 64
-        const signed char c = (signed char)((v[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFF);
+        const signed char c = (signed char)((r.v[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFF);
         a[s][j] = static_cast<__bf16>(dd * (float)c);
       }
     }
-  } else {  // Q4_0 / Q4_1 SoA
-    const unsigned char* qp = p.q + row * (long)(p.K / 2) + (long)sb * 128 + 32 * g;
-    const long di = row * (long)(p.K / 32) + sb * 8 + 2 * g;
-    const float dA = h2f(p.d[di]), dB = h2f(p.d[di + 1]);
+  } else {  // Q4_0 / Q4_1
+    const float dA = h2f(r.h[0]), dB = h2f(r.h[1]);
     float mA = 0.f, mB = 0.f;
-    if constexpr (QT == QT_Q4_1) { mA = h2f(p.m[di]); mB = h2f(p.m[di + 1]); }
-    u32x4 v[2] = {ld16(qp), ld16(qp + 16)};
+    if constexpr (QT == QT_Q4_1) { mA = h2f(r.h[2]); mB = h2f(r.h[3]); }
+    const u32x4 v[2] = {r.v[0], r.v[1]};
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int blk = s >> 2;
@@ -161,10 +200,17 @@ HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a
   }
 }
 
+template <int QT>
+HS_DEVICE void decode_lane(const QParams& p, long row, int sb, int g, bf16x8 (&a)[8]) {
+  RawQ r;
+  load_raw<QT>(p, row, sb, g, r);
+  decode_raw<QT>(r, g, a);
+}
+
 constexpr int kXPad = 8;  // LDS row padding (bf16) for conflict-free b128 reads
 
-template <int QT, int MT>
-__global__ __launch_bounds__(256) void qgemm_kernel(
+template <int QT, int MT, int NWAVES>
+__global__ __launch_bounds__(64 * NWAVES) void qgemm_kernel(
     unsigned short* __restrict__ out, float* __restrict__ ws, const unsigned short* __restrict__ x,
     long x_stride, long out_stride, QParams p, int M, int N, int K, int sb_per_split) {
   constexpr int XR = 16 * MT;            // staged x rows
@@ -172,7 +218,8 @@ __global__ __launch_bounds__(256) void qgemm_kernel(
   __shared__ __attribute__((aligned(16))) unsigned short xs[XR * XS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int n0 = blockIdx.x * 64 + wave * 16;
+  constexpr int NT = 64 * NWAVES;     // threads; the workgroup owns 16 * NWAVES weight rows
+  const int n0 = blockIdx.x * (16 * NWAVES) + wave * 16;
   const int nsb = K / 256;
   const int sb0 = blockIdx.y * sb_per_split;
   const int sb1 = min(nsb, sb0 + sb_per_split);
@@ -181,18 +228,40 @@ __global__ __launch_bounds__(256) void qgemm_kernel(
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Software pipeline over super-chunks: the quant bytes AND the x slice of
+  // super-chunk sb+1 are loaded (into registers) before super-chunk sb is
+  // decoded and multiplied, so HBM / L2 latency overlaps the dequant VALU work
+  // and the MFMAs instead of being exposed once per 256 k.
+  constexpr int XP = (XR * 32 + NT - 1) / NT;  // 16-byte x pieces per thread per super-chunk
+  u16x8 xv[XP];
+  auto load_x = [&](int sb) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int idx = min(i * NT + (int)threadIdx.x, XR * 32 - 1), r = idx >> 5, cc = idx & 31;
+      // rows >= M are clamped, not zeroed: they only feed outputs m >= M (never stored)
+      xv[i] = *reinterpret_cast<const u16x8*>(x + min(r, M - 1) * x_stride + sb * 256 + cc * 8);
+    }
+  };
+  RawQ raw;
+  if (sb0 < sb1) {
+    load_x(sb0);
+    load_raw<QT>(p, row, sb0, g, raw);
+  }
   for (int sb = sb0; sb < sb1; ++sb) {
-    __syncthreads();
-    // stage x[:, sb*256 .. +256] (rows >= M are zero)
-    for (int i = threadIdx.x; i < XR * 32; i += 256) {
-      const int r = i >> 5, cc = i & 31;
-      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (r < M) v = *reinterpret_cast<const u16x8*>(x + r * x_stride + sb * 256 + cc * 8);
-      *reinterpret_cast<u16x8*>(xs + r * XS + cc * 8) = v;
+    __syncthreads();  // previous super-chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int idx = i * NT + threadIdx.x, r = idx >> 5, cc = idx & 31;
+      if (idx < XR * 32) *reinterpret_cast<u16x8*>(xs + r * XS + cc * 8) = xv[i];
+    }
+    const RawQ cur = raw;
+    if (sb + 1 < sb1) {  // prefetch the next super-chunk
+      load_x(sb + 1);
+      load_raw<QT>(p, row, sb + 1, g, raw);
     }
     __syncthreads();
     bf16x8 a[8];
-    decode_lane<QT>(p, row, sb, g, a);
+    decode_raw<QT>(cur, g, a);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int kb = kbase<QT>(g, s);
@@ -250,14 +319,17 @@ __global__ __launch_bounds__(256) void qdequant_kernel(unsigned short* __restric
 template <int QT>
 static void launch_qgemm_t(void* out, float* ws, const void* x, long x_stride, long out_stride,
                            const QParams& p, int M, int N, int K, int splits, hipStream_t s) {
+  // 4 waves = 64 weight rows per workgroup (8-wave 128-row tiles halve the x
+  // staging traffic but measured slower at M = 64: 21.6 vs 18.6 us per Q4_K call)
+  constexpr int NW = 4;
   const int nsb = K / 256;
   const int per = (nsb + splits - 1) / splits;
-  dim3 grid((N + 63) / 64, (nsb + per - 1) / per), block(256);
+  dim3 grid((N + 16 * NW - 1) / (16 * NW), (nsb + per - 1) / per), block(64 * NW);
   auto* o = static_cast<unsigned short*>(out);
   auto* xi = static_cast<const unsigned short*>(x);
-  if (M <= 16) qgemm_kernel<QT, 1><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
-  else if (M <= 32) qgemm_kernel<QT, 2><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
-  else qgemm_kernel<QT, 4><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
+  if (M <= 16) qgemm_kernel<QT, 1, NW><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
+  else if (M <= 32) qgemm_kernel<QT, 2, NW><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
+  else qgemm_kernel<QT, 4, NW><<<grid, block, 0, s>>>(o, ws, xi, x_stride, out_stride, p, M, N, K, per);
 }
 
 void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long out_stride,

@@ -167,10 +167,10 @@ def dequantize(w: QuantWeight) -> torch.Tensor:
 
 
 def _splits(N: int, K: int) -> int:
+    """K slices for the decode dequant-GEMM: ~512 (64-row tile, K slice) workgroups."""
     wgs = (N + 63) // 64
     nsb = K // 256
-    s = max(1, min(nsb, -(-512 // wgs)))
-    return s if s > 1 else 1
+    return max(1, min(nsb, -(-512 // wgs)))
 
 
 def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
