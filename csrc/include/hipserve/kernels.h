@@ -41,10 +41,13 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               int block_size, float scale, hipStream_t s);
 
 // sampling.hip
+// ws: fp32 workspace of sample_workspace_floats(rows, V) for the multi-CU path
+// (vocab >= 8192); nullptr selects the one-workgroup-per-row kernel.
+size_t sample_workspace_floats(int rows, int V);
 void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf16,
                    long stride, int rows, int V, const float* temperature,
                    const int* top_k, const float* top_p, const long* seeds,
-                   const long* steps, hipStream_t s);
+                   const long* steps, float* ws, hipStream_t s);
 
 // gguf.hip — qtype: 0 Q4_0, 1 Q4_1, 2 Q8_0, 3 Q4_K, 4 Q5_K, 5 Q6_K (repacked layouts)
 void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long out_stride,

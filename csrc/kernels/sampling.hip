@@ -21,6 +21,7 @@
 namespace hipserve {
 
 constexpr int kSampThreads = 1024;
+constexpr int kMcMinVocab = 8192;  // multi-CU path from this vocabulary size up
 constexpr int kSampWaves = kSampThreads / 64;
 
 HS_DEVICE unsigned int key16(unsigned short b) {  // order-preserving bf16 key
@@ -291,11 +292,565 @@ static void launch_sample_t(long* out_tok, float* out_lp, const T* logits, long 
   sample_kernel<8, T><<<rows, kSampThreads, lds, s>>>(out_tok, out_lp, logits, stride, V, temperature, top_k, top_p, seeds, steps);
 }
 
+// ============================================================================
+// Multi-CU sampler (large vocabularies). The single-workgroup kernel above is
+// latency-bound per row (~170 us for a 128K-vocab top-p row whether B is 1 or
+// 256: one CU walks the row ~12 times), so a row is split into 16K-element
+// chunks, one 256-thread workgroup each, and the threshold searches become a
+// two-level histogram of the same order-preserving 16-bit key:
+//   coarse: key >> 11 (32 bins), accumulated in per-thread private LDS columns
+//           ([bin][thread]: conflict-free, no atomics — clustered logits made
+//           LDS atomics on 256 exponent bins serialise: 65 us per chunk);
+//   fine:   key & 2047 (2048 bins) of the ONE selected coarse bin, LDS atomics
+//           (lanes spread over 2048 addresses).
+//   mc_stats   (chunk)  max / argmax / sum exp, coarse count + exp-mass
+//   mc_coarse  (row)    combine -> greedy result; coarse bins of the thresholds
+//   mc_fine    (chunk)  fine histograms inside the selected bin(s)
+//   mc_thresh  (row)    exact 16-bit thresholds (a second fine round only when
+//                       top-k and top-p are both active and the nucleus bin moved)
+//   mc_gumbel  (chunk)  Gumbel-max among survivors, same hash as above
+//   mc_final   (row)    argmax over chunks -> token, logprob
+// Same semantics as sample_kernel (bit-identical draws given the thresholds;
+// the threshold masses are summed in a different order).
+constexpr int kMcThreads = 256;
+constexpr int kMcVec = 4;                            // 16-byte pieces per thread
+constexpr int kMcChunk = kMcThreads * kMcVec * 8;    // 8192 elements per workgroup
+constexpr int kMcWaves = kMcThreads / 64;
+constexpr int kCoarseBits = 5, kFineBits = 11;
+constexpr int kCoarse = 1 << kCoarseBits, kFine = 1 << kFineBits;
+
+struct McLayout {  // per-row workspace, in floats
+  int C;
+  HS_HOST_DEVICE long stats() const { return 0; }                          // [C][4] m, s1, massT, argmax
+  HS_HOST_DEVICE long hcnt() const { return 4L * C; }                      // [C][32] uint
+  HS_HOST_DEVICE long hmass() const { return hcnt() + (long)kCoarse * C; } // [C][32]
+  HS_HOST_DEVICE long fcnt() const { return hmass() + (long)kCoarse * C; } // [C][2048] uint
+  HS_HOST_DEVICE long fmassA() const { return fcnt() + (long)kFine * C; }  // [C][2048]
+  HS_HOST_DEVICE long fmassB() const { return fmassA() + (long)kFine * C; }// [C][2048]
+  HS_HOST_DEVICE long best() const { return fmassB() + (long)kFine * C; }  // [C][2] g, idx
+  HS_HOST_DEVICE long state() const { return best() + 2L * C; }            // [32]
+  HS_HOST_DEVICE long cmass() const { return state() + 32; }               // [32] combined coarse mass
+  HS_HOST_DEVICE long size() const { return (cmass() + kCoarse + 3) & ~3L; }  // 16-byte aligned rows
+};
+enum { ST_DONE = 0, ST_M, ST_RSUM, ST_INVT, ST_HK, ST_KREM, ST_HP0, ST_FLOOR, ST_BINA, ST_BINB, ST_NEED2,
+       ST_TARGET };
+
+template <typename T>
+HS_DEVICE void mc_load(const T* __restrict__ row, int chunk, int V, u16x8 (&d)[kMcVec]) {
+#pragma unroll
+  for (int j = 0; j < kMcVec; ++j)
+    RowLoader<T>::load8(row, chunk * kMcChunk + 8 * (threadIdx.x + kMcThreads * j), V, d[j]);
+}
+
+HS_DEVICE int mc_idx(int chunk, int j, int e) { return chunk * kMcChunk + 8 * (threadIdx.x + kMcThreads * j) + e; }
+
+template <typename T>
+__global__ __launch_bounds__(kMcThreads) void mc_stats_kernel(const T* __restrict__ logits, long stride, int V,
+                                                             const float* __restrict__ temperature,
+                                                             const int* __restrict__ top_k,
+                                                             const float* __restrict__ top_p,
+                                                             float* __restrict__ ws, int C) {
+  const int chunk = blockIdx.x, row = blockIdx.y;
+  const McLayout L{C};
+  float* w = ws + (long)row * L.size();
+  __shared__ unsigned int cntp[kCoarse][kMcThreads];  // [bin][thread]: bank = thread
+  __shared__ float massp[kCoarse][kMcThreads];
+  __shared__ float red_a[kMcWaves];
+  __shared__ int red_i[kMcWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  u16x8 d[kMcVec];
+  mc_load(logits + (long)row * stride, chunk, V, d);
+  float m = -INFINITY;
+  int am = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < kMcVec; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = mc_idx(chunk, j, e);
+      const float v = bf16_to_f32(d[j][e]);
+      if (idx < V && (v > m || (v == m && idx < am))) { m = v; am = idx; }
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const int a2 = __shfl_xor(am, o, 64);
+    if (m2 > m || (m2 == m && a2 < am)) { m = m2; am = a2; }
+  }
+  if (lane == 0) { red_a[wid] = m; red_i[wid] = am; }
+  __syncthreads();
+  m = red_a[0]; am = red_i[0];
+#pragma unroll
+  for (int k = 1; k < kMcWaves; ++k)
+    if (red_a[k] > m || (red_a[k] == m && red_i[k] < am)) { m = red_a[k]; am = red_i[k]; }
+  const float temp = temperature[row];
+  const bool sampling = temp > 1e-5f;
+  const int k = top_k[row];
+  const bool hist_k = sampling && k > 0 && k < V, hist_p = sampling && top_p[row] < 1.f;
+  const float inv_t = sampling ? 1.f / temp : 0.f;
+  if (hist_k || hist_p) {
+#pragma unroll
+    for (int b = 0; b < kCoarse; ++b) { cntp[b][tid] = 0u; massp[b][tid] = 0.f; }
+  }
+  float s1 = 0.f, sT = 0.f;
+#pragma unroll
+  for (int j = 0; j < kMcVec; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (mc_idx(chunk, j, e) >= V) continue;
+      const float v = bf16_to_f32(d[j][e]);
+      s1 += __expf(v - m);
+      if (sampling) {
+        const float wt = __expf((v - m) * inv_t);
+        sT += wt;
+        const int b = key16(d[j][e]) >> kFineBits;
+        if (hist_k) cntp[b][tid] += 1u;
+        if (hist_p) massp[b][tid] += wt;
+      }
+    }
+  s1 = wave_sum(s1);
+  sT = wave_sum(sT);
+  __syncthreads();
+  if (lane == 0) red_a[wid] = s1;
+  __syncthreads();
+  float S1 = 0.f;
+#pragma unroll
+  for (int q = 0; q < kMcWaves; ++q) S1 += red_a[q];
+  __syncthreads();
+  if (lane == 0) red_a[wid] = sT;
+  __syncthreads();
+  float ST = 0.f;
+#pragma unroll
+  for (int q = 0; q < kMcWaves; ++q) ST += red_a[q];
+  if (tid == 0) {
+    float* st = w + L.stats() + 4 * chunk;
+    st[0] = m;
+    st[1] = S1;
+    st[2] = ST;
+    st[3] = __int_as_float(am);
+  }
+  if (hist_k || hist_p) {
+    // bin b = tid >> 3 summed by 8 threads over 32 thread columns each
+    const int b = tid >> 3, part = tid & 7;
+    unsigned int c = 0;
+    float ms = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMcThreads / 8; ++i) {
+      const int col = part * (kMcThreads / 8) + i;
+      c += cntp[b][col];
+      ms += massp[b][col];
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      c += __shfl_xor(c, o, 64);
+      ms += __shfl_xor(ms, o, 64);
+    }
+    if (part == 0) {
+      reinterpret_cast<unsigned int*>(w + L.hcnt())[kCoarse * chunk + b] = c;
+      w[L.hmass() + kCoarse * chunk + b] = ms;
+    }
+  }
+}
+
+// One workgroup per row: combine the chunk statistics; greedy rows finish here.
+__global__ __launch_bounds__(64) void mc_coarse_kernel(long* __restrict__ out_tok, float* __restrict__ out_lp,
+                                                       const float* __restrict__ temperature,
+                                                       const int* __restrict__ top_k, const float* __restrict__ top_p,
+                                                       int V, float* __restrict__ ws, int C) {
+  const int row = blockIdx.x;
+  const McLayout L{C};
+  float* w = ws + (long)row * L.size();
+  float* st = w + L.state();
+  __shared__ unsigned int cnt[kCoarse];
+  __shared__ float mass[kCoarse];
+  // lanes 0..C-1 hold the chunk stats; wave reductions for max / argmax / rsum
+  const int lane = threadIdx.x;
+  float m = -INFINITY, s1 = 0.f;
+  int a = 0x7fffffff;
+  if (lane < C) {
+    m = w[L.stats() + 4 * lane];
+    s1 = w[L.stats() + 4 * lane + 1];
+    a = __float_as_int(w[L.stats() + 4 * lane + 3]);
+  }
+  float M = m;
+  int A = a;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(M, o, 64);
+    const int a2 = __shfl_xor(A, o, 64);
+    if (m2 > M || (m2 == M && a2 < A)) { M = m2; A = a2; }
+  }
+  const float R = wave_sum(lane < C ? s1 * __expf(m - M) : 0.f);
+  const float temp = temperature[row];
+  if (!(temp > 1e-5f)) {
+    if (lane == 0) {
+      out_tok[row] = A < V ? A : 0;  // all-NaN row: token 0, never an id past V
+      if (out_lp) out_lp[row] = -__logf(R);
+      st[ST_DONE] = 1.f;
+    }
+    return;
+  }
+  const float inv_t = 1.f / temp;
+  const int k = top_k[row];
+  const float p = top_p[row];
+  const bool use_k = k > 0 && k < V, use_p = p < 1.f;
+  if (lane < kCoarse) {
+    unsigned int c = 0;
+    float ms = 0.f;
+    for (int q = 0; q < C; ++q) {
+      if (use_k) c += reinterpret_cast<const unsigned int*>(w + L.hcnt())[kCoarse * q + lane];
+      if (use_p) ms += w[L.hmass() + kCoarse * q + lane] * __expf((w[L.stats() + 4 * q] - M) * inv_t);
+    }
+    cnt[lane] = c;
+    mass[lane] = ms;
+    w[L.cmass() + lane] = ms;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  int hk = -1, krem = 0;
+  if (use_k) {
+    unsigned int acc = 0;
+    for (int b = kCoarse - 1; b >= 0; --b) {
+      if (acc + cnt[b] >= (unsigned int)k) { hk = b; krem = k - (int)acc; break; }
+      acc += cnt[b];
+    }
+  }
+  int hp0 = -1;
+  if (use_p) {
+    float tot = 0.f;
+    for (int b = kCoarse - 1; b >= max(hk, 0); --b) tot += mass[b];
+    const float target = p * tot;  // exact without top-k, an upper bound with it
+    float acc = 0.f;
+    for (int b = kCoarse - 1; b >= max(hk, 0); --b) {
+      acc += mass[b];
+      if (acc >= target) { hp0 = b; break; }
+    }
+    if (hp0 < 0) hp0 = max(hk, 0);
+  }
+  st[ST_DONE] = 0.f;
+  st[ST_M] = M;
+  st[ST_RSUM] = R;
+  st[ST_INVT] = inv_t;
+  st[ST_HK] = (float)hk;
+  st[ST_KREM] = (float)krem;
+  st[ST_HP0] = (float)hp0;
+  st[ST_BINA] = (float)(use_k ? hk : hp0);
+  st[ST_BINB] = (float)(use_k && use_p && hp0 != hk ? hp0 : -1);
+  st[ST_NEED2] = 0.f;
+  st[ST_FLOOR] = 0.f;
+}
+
+// Fine histograms (key & 2047) of the bins named in the row state: round 0 ->
+// bin A (count + mass) and bin B (mass); round 1 -> bin ST_BINB (mass) for rows
+// that flagged ST_NEED2.
+template <typename T>
+__global__ __launch_bounds__(kMcThreads) void mc_fine_kernel(const T* __restrict__ logits, long stride, int V,
+                                                            float* __restrict__ ws, int C, int round) {
+  const int chunk = blockIdx.x, row = blockIdx.y;
+  const McLayout L{C};
+  float* w = ws + (long)row * L.size();
+  const float* st = w + L.state();
+  if (st[ST_DONE] != 0.f) return;
+  if (round == 1 && st[ST_NEED2] == 0.f) return;
+  const int binA = round == 0 ? (int)st[ST_BINA] : -1;
+  const int binB = (int)st[ST_BINB];
+  if (binA < 0 && binB < 0) return;
+  __shared__ unsigned int fc[kFine];
+  __shared__ float fa[kFine], fb[kFine];
+  for (int i = threadIdx.x; i < kFine; i += kMcThreads) { fc[i] = 0u; fa[i] = 0.f; fb[i] = 0.f; }
+  u16x8 d[kMcVec];
+  mc_load(logits + (long)row * stride, chunk, V, d);
+  const float m = w[L.stats() + 4 * chunk];
+  const float inv_t = st[ST_INVT];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kMcVec; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (mc_idx(chunk, j, e) >= V) continue;
+      const unsigned int key = key16(d[j][e]);
+      const int hi = key >> kFineBits, lo = key & (kFine - 1);
+      if (hi != binA && hi != binB) continue;
+      const float wt = __expf((bf16_to_f32(d[j][e]) - m) * inv_t);
+      if (hi == binA) {
+        atomicAdd(&fc[lo], 1u);
+        atomicAdd(&fa[lo], wt);
+      }
+      if (hi == binB) atomicAdd(&fb[lo], wt);
+    }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kFine; b += kMcThreads) {
+    if (round == 0) {
+      reinterpret_cast<unsigned int*>(w + L.fcnt())[kFine * chunk + b] = fc[b];
+      w[L.fmassA() + kFine * chunk + b] = fa[b];
+    }
+    w[L.fmassB() + kFine * chunk + b] = fb[b];
+  }
+}
+
+// Largest l >= lmin with base + sum_{l' >= l, l' >= lmin} v[l'] >= target over the
+// 2048 fine bins (LDS), block-parallel: 8 bins per thread, suffix scan of the
+// per-thread sums. Returns lmin when the target is never reached (rounding).
+template <typename V>
+HS_DEVICE int suffix_find(const V* v, V base, V target, int lmin, V* scan, int* res) {
+  const int t = threadIdx.x;  // 256 threads, bins [8t, 8t + 8)
+  V seg = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int l = 8 * t + i;
+    if (l >= lmin) seg += v[l];
+  }
+  scan[t] = seg;
+  if (t == 0) *res = lmin;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive suffix scan
+    const V add = t + o < 256 ? scan[t + o] : (V)0;
+    __syncthreads();
+    scan[t] += add;
+    __syncthreads();
+  }
+  const V above = base + (t + 1 < 256 ? scan[t + 1] : (V)0);
+  if (above < target && above + seg >= target) {
+    V acc = above;
+    for (int i = 7; i >= 0; --i) {
+      const int l = 8 * t + i;
+      if (l < lmin) break;
+      acc += v[l];
+      if (acc >= target) { *res = l; break; }
+    }
+  }
+  __syncthreads();
+  const int r = *res;
+  __syncthreads();
+  return r;
+}
+
+// Exact 16-bit thresholds. round 0: top-k, then top-p (flags ST_NEED2 when the
+// nucleus crosses into a coarse bin whose fine histogram was not collected);
+// round 1: finish the flagged rows.
+__global__ __launch_bounds__(256) void mc_thresh_kernel(const int* __restrict__ top_k, const float* __restrict__ top_p,
+                                                        int V, float* __restrict__ ws, int C, int round) {
+  const int row = blockIdx.x;
+  const McLayout L{C};
+  float* w = ws + (long)row * L.size();
+  float* st = w + L.state();
+  if (st[ST_DONE] != 0.f) return;
+  if (round == 1 && st[ST_NEED2] == 0.f) return;
+  const int k = top_k[row];
+  const float p = top_p[row];
+  const bool use_k = k > 0 && k < V, use_p = p < 1.f;
+  if (!use_k && !use_p) {  // plain temperature sampling: no threshold
+    if (threadIdx.x == 0) st[ST_FLOOR] = 0.f;
+    return;
+  }
+  __shared__ unsigned int fc[kFine];
+  __shared__ float fa[kFine], fb[kFine];
+  __shared__ float fscan[256];
+  __shared__ unsigned int uscan[256];
+  __shared__ float scale[64];
+  __shared__ int res;
+  const float M = st[ST_M], inv_t = st[ST_INVT];
+  if (threadIdx.x < C) scale[threadIdx.x] = __expf((w[L.stats() + 4 * threadIdx.x] - M) * inv_t);
+  __syncthreads();
+  const bool needA = round == 0, needB = (int)st[ST_BINB] >= 0;
+  {
+    // thread t combines bins [8t, 8t + 8) over the chunks with 16-byte loads
+    const int b0 = 8 * threadIdx.x;
+    u32x4 c0 = {0u, 0u, 0u, 0u}, c1 = {0u, 0u, 0u, 0u};
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, e0 = a0, e1 = a0;
+#pragma unroll 4
+    for (int q = 0; q < C; ++q) {
+      const float sc = scale[q];
+      if (needA) {
+        if (use_k) {
+          const u32x4* cp = reinterpret_cast<const u32x4*>(w + L.fcnt() + (long)kFine * q + b0);
+          c0 += cp[0];
+          c1 += cp[1];
+        }
+        const f32x4* ap = reinterpret_cast<const f32x4*>(w + L.fmassA() + (long)kFine * q + b0);
+        a0 += ap[0] * sc;
+        a1 += ap[1] * sc;
+      }
+      if (needB) {
+        const f32x4* bp = reinterpret_cast<const f32x4*>(w + L.fmassB() + (long)kFine * q + b0);
+        e0 += bp[0] * sc;
+        e1 += bp[1] * sc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fc[b0 + i] = c0[i]; fc[b0 + 4 + i] = c1[i];
+      fa[b0 + i] = a0[i]; fa[b0 + 4 + i] = a1[i];
+      fb[b0 + i] = e0[i]; fb[b0 + 4 + i] = e1[i];
+    }
+  }
+  __syncthreads();
+  const float* cm = w + L.cmass();
+  const int hk = (int)st[ST_HK];
+  if (round == 1) {  // the nucleus bin ST_BINB, target stored by round 0
+    const int hp = (int)st[ST_BINB];
+    float acc = 0.f;
+    for (int b = kCoarse - 1; b > hp; --b) acc += cm[b];
+    const int lo = suffix_find<float>(fb, acc, st[ST_TARGET], 0, fscan, &res);
+    if (threadIdx.x == 0) st[ST_FLOOR] = (float)((hp << kFineBits) | lo);
+    return;
+  }
+  int floor_k = 0, lo_k = 0;
+  if (use_k) {
+    lo_k = suffix_find<unsigned int>(fc, 0u, (unsigned int)st[ST_KREM], 0, uscan, &res);
+    floor_k = (hk << kFineBits) | lo_k;
+  }
+  int floor = floor_k;
+  if (use_p) {
+    // survivor mass: coarse bins above hb whole, bin hk only from lo_k (top-k)
+    const int hb = use_k ? hk : 0;
+    float in_hk = 0.f;
+    if (use_k) {
+      // survivor mass inside bin hk: sum of fa[l] for l >= lo_k (block reduction)
+      float part = 0.f;
+      for (int l = threadIdx.x; l < kFine; l += 256)
+        if (l >= lo_k) part += fa[l];
+      part = block_sum(part, fscan);
+      in_hk = part;
+    }
+    float tot = in_hk;
+    for (int b = kCoarse - 1; b >= (use_k ? hb + 1 : 0); --b) tot += cm[b];
+    const float target = p * tot;
+    // coarse bin hp of the nucleus threshold; acc = survivor mass above it
+    float acc = 0.f;
+    int hp = hb;
+    for (int b = kCoarse - 1; b > hb; --b) {
+      if (acc + cm[b] >= target) { hp = b; break; }
+      acc += cm[b];
+    }
+    const float* fine = nullptr;
+    int lmin = 0;
+    if (use_k && hp == hk) { fine = fa; lmin = lo_k; }
+    else if (!use_k && hp == (int)st[ST_BINA]) fine = fa;
+    else if (use_k && hp == (int)st[ST_BINB]) fine = fb;
+    if (fine != nullptr) {
+      const int lo = suffix_find<float>(fine, acc, target, lmin, fscan, &res);
+      floor = (hp << kFineBits) | lo;
+    } else if (threadIdx.x == 0) {  // the nucleus bin has no fine histogram yet: second round
+      st[ST_NEED2] = 1.f;
+      st[ST_BINB] = (float)hp;
+      st[ST_TARGET] = target;
+      floor = hp << kFineBits;
+    }
+  }
+  if (threadIdx.x == 0) st[ST_FLOOR] = (float)floor;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kMcThreads) void mc_gumbel_kernel(const T* __restrict__ logits, long stride, int V,
+                                                              const long* __restrict__ seeds,
+                                                              const long* __restrict__ steps, float* __restrict__ ws,
+                                                              int C) {
+  const int chunk = blockIdx.x, row = blockIdx.y;
+  const McLayout L{C};
+  float* w = ws + (long)row * L.size();
+  const float* st = w + L.state();
+  if (st[ST_DONE] != 0.f) return;
+  __shared__ float red_a[kMcWaves];
+  __shared__ int red_i[kMcWaves];
+  u16x8 d[kMcVec];
+  mc_load(logits + (long)row * stride, chunk, V, d);
+  const float M = st[ST_M], inv_t = st[ST_INVT];
+  const unsigned int floor_key = (unsigned int)st[ST_FLOOR];
+  const unsigned int rkey = row_key((unsigned long long)seeds[row], (unsigned long long)steps[row]);
+  constexpr float kNoWin = -20.3f;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < kMcVec; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = mc_idx(chunk, j, e);
+      if (idx >= V || key16(d[j][e]) < floor_key) continue;
+      const float z = (bf16_to_f32(d[j][e]) - M) * inv_t;
+      if (z < kNoWin) continue;
+      const float u = uniform01(rkey, (unsigned int)idx);
+      const float g = z - __logf(-__logf(u));
+      if (g > best || (g == best && idx < bi)) { best = g; bi = idx; }
+    }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float b2 = __shfl_xor(best, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    if (b2 > best || (b2 == best && i2 < bi)) { best = b2; bi = i2; }
+  }
+  if (lane == 0) { red_a[wid] = best; red_i[wid] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < kMcWaves; ++q)
+      if (red_a[q] > best || (red_a[q] == best && red_i[q] < bi)) { best = red_a[q]; bi = red_i[q]; }
+    w[L.best() + 2 * chunk] = best;
+    w[L.best() + 2 * chunk + 1] = __int_as_float(bi);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void mc_final_kernel(long* __restrict__ out_tok, float* __restrict__ out_lp,
+                                                      const T* __restrict__ logits, long stride, int V,
+                                                      const float* __restrict__ ws, int C) {
+  const int row = blockIdx.x;
+  const McLayout L{C};
+  const float* w = ws + (long)row * L.size();
+  const float* st = w + L.state();
+  if (st[ST_DONE] != 0.f || threadIdx.x != 0) return;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = 0; c < C; ++c) {
+    const float g = w[L.best() + 2 * c];
+    const int i = __float_as_int(w[L.best() + 2 * c + 1]);
+    if (g > best || (g == best && i < bi)) { best = g; bi = i; }
+  }
+  if (!(bi >= 0 && bi < V)) bi = 0;  // no survivor (NaN row): token 0
+  out_tok[row] = bi;
+  if (out_lp) {
+    float xv;
+    if constexpr (sizeof(T) == 2) xv = bf16_to_f32(reinterpret_cast<const unsigned short*>(logits + (long)row * stride)[bi]);
+    else xv = bf16_to_f32(f32_to_bf16(reinterpret_cast<const float*>(logits + (long)row * stride)[bi]));
+    out_lp[row] = (xv - st[ST_M]) - __logf(st[ST_RSUM]);
+  }
+}
+
+size_t sample_workspace_floats(int rows, int V) {
+  if (V < kMcMinVocab) return 0;
+  const McLayout L{(V + kMcChunk - 1) / kMcChunk};
+  return (size_t)rows * L.size();
+}
+
+template <typename T>
+static void launch_sample_mc(long* out_tok, float* out_lp, const T* logits, long stride, int rows, int V,
+                             const float* temperature, const int* top_k, const float* top_p, const long* seeds,
+                             const long* steps, float* ws, hipStream_t s) {
+  const int C = (V + kMcChunk - 1) / kMcChunk;
+  const dim3 cg(C, rows);
+  mc_stats_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, temperature, top_k, top_p, ws, C);
+  mc_coarse_kernel<<<rows, 64, 0, s>>>(out_tok, out_lp, temperature, top_k, top_p, V, ws, C);
+  mc_fine_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, ws, C, 0);
+  mc_thresh_kernel<<<rows, 256, 0, s>>>(top_k, top_p, V, ws, C, 0);
+  mc_fine_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, ws, C, 1);
+  mc_thresh_kernel<<<rows, 256, 0, s>>>(top_k, top_p, V, ws, C, 1);
+  mc_gumbel_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, seeds, steps, ws, C);
+  mc_final_kernel<T><<<rows, 64, 0, s>>>(out_tok, out_lp, logits, stride, V, ws, C);
+}
+
 void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf16,
                    long stride, int rows, int V, const float* temperature,
                    const int* top_k, const float* top_p, const long* seeds,
-                   const long* steps, hipStream_t s) {
+                   const long* steps, float* ws, hipStream_t s) {
   if (rows <= 0) return;
+  if (ws != nullptr && V >= kMcMinVocab) {
+    if (is_bf16)
+      launch_sample_mc(out_tok, out_lp, static_cast<const unsigned short*>(logits), stride, rows, V, temperature,
+                       top_k, top_p, seeds, steps, ws, s);
+    else
+      launch_sample_mc(out_tok, out_lp, static_cast<const float*>(logits), stride, rows, V, temperature, top_k,
+                       top_p, seeds, steps, ws, s);
+    return;
+  }
   if (is_bf16)
     launch_sample_t(out_tok, out_lp, static_cast<const unsigned short*>(logits), stride, rows, V, temperature, top_k, top_p, seeds, steps, s);
   else

@@ -136,11 +136,15 @@ void sample(at::Tensor& out_tok, at::Tensor& out_lp, const at::Tensor& logits,
   TORCH_CHECK(out_tok.numel() >= rows && temperature.numel() >= rows && top_k.numel() >= rows &&
               top_p.numel() >= rows && seeds.numel() >= rows && steps.numel() >= rows);
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  // multi-CU sampler workspace (caching allocator: graph-capturable)
+  const size_t wsn = hipserve::sample_workspace_floats(rows, logits.size(1));
+  at::Tensor ws;
+  if (wsn) ws = at::empty({(long)wsn}, logits.options().dtype(at::kFloat));
   hipserve::launch_sample(out_tok.data_ptr<int64_t>(), out_lp.numel() ? out_lp.data_ptr<float>() : nullptr,
                           logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
                           logits.stride(0), rows, logits.size(1), temperature.data_ptr<float>(),
                           top_k.data_ptr<int>(), top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(),
-                          steps.data_ptr<int64_t>(), cur_stream());
+                          steps.data_ptr<int64_t>(), wsn ? ws.data_ptr<float>() : nullptr, cur_stream());
 }
 
 void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const at::Tensor& d,

@@ -150,6 +150,60 @@ def test_sample(ops, dtype):
     assert tok[3].item() == int(logits[3].float().argmax())  # top_k = 1
 
 
+@pytest.mark.parametrize("V,scale", [(128256, 3.0), (128256, 0.05), (32000, 1.0), (9000, 8.0)])
+def test_sample_multicu(ops, V, scale):
+    """Multi-CU sampler (vocab >= 8192) vs the reference: greedy, temperature,
+    top-k, top-p, both (incl. the nucleus moving past the top-k bin), and a
+    clustered row (scale 0.05: nearly flat distribution, heavy key ties)."""
+    torch.manual_seed(V + int(scale * 100))
+    B = 14
+    logits = (torch.randn(B, V, device=DEV) * scale).to(torch.bfloat16)
+    logits[5, 1000:1010] = 30.0   # a very peaked row
+    temp = torch.tensor([0.0, 1.0, 0.7, 1.0, 1.3, 0.9, 1.0, 0.5, 1.0, 2.0, 0.8, 1.0, 0.8, 1.1], device=DEV)
+    top_k = torch.tensor([0, 0, 50, 1, 0, 20, 0, 0, 1000, 5, 0, 7, 40000, 3000], device=DEV, dtype=torch.int32)
+    top_p = torch.tensor([1.0, 1.0, 1.0, 1.0, 0.9, 0.5, 0.1, 0.95, 0.8, 1.0, 0.95, 0.3, 0.95, 0.2], device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.long) * 7919 + 1
+    steps = torch.arange(B, device=DEV, dtype=torch.long) + 3
+    tok = torch.empty(B, device=DEV, dtype=torch.long)
+    lp = torch.empty(B, device=DEV, dtype=torch.float32)
+    ops.sample(tok, lp, logits, temp, top_k, top_p, seeds, steps)
+    rt, rlp = ref.sample(logits.cpu(), temp.cpu(), top_k.cpu(), top_p.cpu(), seeds.cpu(), steps.cpu())
+    assert ((tok.cpu() >= 0) & (tok.cpu() < V)).all()
+    mism = (tok.cpu() != rt).sum().item()
+    assert mism <= 1, (tok.cpu(), rt)
+    ok = tok.cpu() == rt
+    assert torch.allclose(lp.cpu()[ok], rlp[ok], atol=2e-3)
+    assert tok[0].item() == int(logits[0].float().argmax())
+    assert tok[3].item() == int(logits[3].float().argmax())
+    # graph capture + replay gives the same draw
+    g = torch.cuda.CUDAGraph()
+    tok2 = torch.empty_like(tok)
+    lp2 = torch.empty_like(lp)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.sample(tok2, lp2, logits, temp, top_k, top_p, seeds, steps)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        ops.sample(tok2, lp2, logits, temp, top_k, top_p, seeds, steps)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(tok2, tok)
+
+
+def test_sample_nan_row_never_out_of_range(ops):
+    V = 128256
+    logits = torch.full((3, V), float("nan"), device=DEV, dtype=torch.bfloat16)
+    temp = torch.tensor([0.0, 1.0, 0.7], device=DEV)
+    top_k = torch.tensor([0, 0, 10], device=DEV, dtype=torch.int32)
+    top_p = torch.tensor([1.0, 0.9, 0.9], device=DEV)
+    tok = torch.empty(3, device=DEV, dtype=torch.long)
+    lp = torch.empty(3, device=DEV)
+    ops.sample(tok, lp, logits, temp, top_k, top_p, torch.zeros(3, device=DEV, dtype=torch.long),
+               torch.zeros(3, device=DEV, dtype=torch.long))
+    assert ((tok >= 0) & (tok < V)).all()
+
+
 def test_sample_distribution(ops):
     """Empirical frequencies follow softmax(x/T) restricted to top-k."""
     V, N = 16, 4096

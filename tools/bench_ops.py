@@ -39,7 +39,36 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
+def graph_time(fn, n=20, reps=5):
+    """Device time per call with the calls captured in one hipGraph (how the
+    engine's decode step runs them: no host launch cost)."""
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        ts.append((a, b))
+    torch.cuda.synchronize()
+    v = sorted(x.elapsed_time(y) for x, y in ts)
+    return v[len(v) // 2] * 1000.0 / n
+
+
 def bench_sample(ops):
+    timer = graph_time if os.environ.get("BENCH_GRAPH", "1") == "1" else timeit
     for V, B in [(128256, 64), (128256, 256), (32000, 64), (128256, 1)]:
         logits = (torch.randn(B, V, device=DEV) * 3).to(torch.bfloat16)
         tok = torch.empty(B, dtype=torch.long, device=DEV)
@@ -51,8 +80,8 @@ def bench_sample(ops):
             tp = torch.full((B,), p, device=DEV)
             seeds = torch.arange(B, device=DEV)
             steps = torch.zeros(B, dtype=torch.long, device=DEV)
-            us = timeit(lambda: ops.sample(tok, lp, logits, temp, tk, tp, seeds, steps))
-            emit(op="sample", mode=name, V=V, B=B, us=round(us, 1))
+            us = timer(lambda: ops.sample(tok, lp, logits, temp, tk, tp, seeds, steps))
+            emit(op="sample", mode=name, V=V, B=B, us=round(us, 1), graph=timer is graph_time)
 
 
 def bench_decode(ops):
