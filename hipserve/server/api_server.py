@@ -196,17 +196,25 @@ class OpenAIServer:
                                                "Cache-Control": "no-cache", "X-Accel-Buffering": "no"})
             await resp.prepare(request)
             n_out = 0
+            # per-token SSE events are the HTTP side's hot path (it shares the
+            # interpreter with the engine loop): splice pre-serialised constant
+            # parts around the per-token fields instead of json.dumps of a dict
+            head = 'data: {"id":%s,"object":"text_completion","created":%d,"model":%s,"choices":[{"index":' % (
+                _dumps(rid), created, _dumps(model))
             try:
                 async for idx, o in _merge(gens):
                     n_out += len(o.new_token_ids)
-                    ch = {"index": idx, "text": o.new_text, "logprobs": None,
-                          "finish_reason": o.finish_reason if o.finished else None}
                     if params.logprobs is not None and o.logprobs:
-                        ch["logprobs"] = {"tokens": [self.tokenizer.decode(o.new_token_ids)],
-                                          "token_logprobs": [o.logprobs[0]]}
-                    chunk = {"id": rid, "object": "text_completion", "created": created,
-                             "model": model, "choices": [ch]}
-                    await resp.write(("data: " + _dumps(chunk) + "\n\n").encode())
+                        ch = {"index": idx, "text": o.new_text, "finish_reason": o.finish_reason if o.finished else None,
+                              "logprobs": {"tokens": [self.tokenizer.decode(o.new_token_ids)],
+                                           "token_logprobs": [o.logprobs[0]]}}
+                        chunk = {"id": rid, "object": "text_completion", "created": created,
+                                 "model": model, "choices": [ch]}
+                        await resp.write(("data: " + _dumps(chunk) + "\n\n").encode())
+                        continue
+                    fin = _dumps(o.finish_reason) if o.finished else "null"
+                    await resp.write(f'{head}{idx},"text":{_dumps(o.new_text)},"logprobs":null,'
+                                     f'"finish_reason":{fin}}}]}}\n\n'.encode())
                 if include_usage:
                     u = {"id": rid, "object": "text_completion", "created": created, "model": model,
                          "choices": [], "usage": _usage(n_prompt_total, n_out)}
@@ -273,13 +281,15 @@ class OpenAIServer:
                  + "\n\n").encode() for i in range(len(gens)))
             await resp.write(first)
             n_out = 0
+            head = 'data: {"id":%s,"object":"chat.completion.chunk","created":%d,"model":%s,"choices":[{"index":' % (
+                _dumps(rid), created, _dumps(model))
             try:
                 async for idx, o in _merge(gens):
                     n_out += len(o.new_token_ids)
-                    delta = {"content": o.new_text} if (o.new_text or not o.finished) else {}
-                    ch = {"index": idx, "delta": delta, "logprobs": None,
-                          "finish_reason": o.finish_reason if o.finished else None}
-                    await resp.write(("data: " + _dumps({**base, "choices": [ch]}) + "\n\n").encode())
+                    delta = '{"content":%s}' % _dumps(o.new_text) if (o.new_text or not o.finished) else "{}"
+                    fin = _dumps(o.finish_reason) if o.finished else "null"
+                    await resp.write(f'{head}{idx},"delta":{delta},"logprobs":null,'
+                                     f'"finish_reason":{fin}}}]}}\n\n'.encode())
                 if include_usage:
                     await resp.write(("data: " + _dumps({**base, "choices": [],
                                                          "usage": _usage(n_prompt, n_out)}) + "\n\n").encode())

@@ -27,7 +27,7 @@ def steps(rows):
     out, cur = [], []
     for r in rows:
         cur.append(r)
-        if "sample_kernel" in r[0]:
+        if "sample_kernel" in r[0] or "mc_final_kernel" in r[0]:  # the sampler ends every step
             out.append(cur)
             cur = []
     return out
@@ -102,6 +102,19 @@ def summarize(path, title="rocprofv3 kernel trace"):
                      key=lambda x: -x[2])
         for f, n, d in agg:
             L.append(f"| `{f}` | {n} | {d:.1f} | {d / n:.2f} |")
+        # where the idle time sits: gap before each kernel family (median step)
+        gaps = {}
+        for s in dec:
+            acc = {}
+            for (f0, b0, e0), (f1, b1, e1) in zip(s, s[1:]):
+                acc[f1] = acc.get(f1, 0) + max(0, b1 - e0)
+            for f, g in acc.items():
+                gaps.setdefault(f, []).append(g)
+        gl = sorted(((f, statistics.median(v) / 1e3) for f, v in gaps.items()), key=lambda x: -x[1])[:8]
+        L += ["", "### idle gaps inside a decode step, by the kernel that follows (median us/step)", "",
+              "| next kernel | gap us/step |", "|---|---:|"]
+        for f, g in gl:
+            L.append(f"| `{f}` | {g:.1f} |")
     return "\n".join(L) + "\n"
 
 
