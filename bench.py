@@ -197,6 +197,9 @@ def main():
         if args.out:
             with open(args.out, "w") as f:
                 f.write(line + "\n")
+            with open(os.path.splitext(args.out)[0] + "_gemm_tune.jsonl", "w") as f:
+                for r in engine.runner.gemm_report:
+                    f.write(json.dumps(r) + "\n")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -22,14 +22,16 @@
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
+#include <cstdlib>
+
 namespace hipserve {
 
-constexpr int kDecWaves = 4;
+constexpr int kDecWavesMax = 8;
 constexpr int kChunk = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 
-template <int D>
-__global__ __launch_bounds__(256) void paged_decode_kernel(
+template <int D, int kDecWaves>
+__global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const unsigned short* __restrict__ q, long q_stride,
     const unsigned short* __restrict__ k_cache,
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* bt = reinterpret_cast<int*>(smem);                       // <= 256 block ids
   float* red = reinterpret_cast<float*>(smem + 1024);          // m,l per wave/head
-  float* olds = red + 2 * kDecWaves * 16;                      // [4][16][D]
+  float* olds = red + 2 * kDecWaves * 16;                      // [waves][16][D]
 
   const int first_blk = start / block_size;
   const int nbt = (end - 1) / block_size - first_blk + 1;
@@ -225,9 +227,21 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(
   out[(long)b * out_stride + (long)h * D + d] = f32_to_bf16(acc / L);
 }
 
-size_t paged_decode_smem_bytes(int D) {
-  return 1024 + (size_t)2 * kDecWaves * 16 * sizeof(float) +
-         (size_t)kDecWaves * 16 * D * sizeof(float);
+static size_t smem_bytes(int D, int waves) {
+  return 1024 + (size_t)2 * waves * 16 * sizeof(float) + (size_t)waves * 16 * D * sizeof(float);
+}
+
+size_t paged_decode_smem_bytes(int D) { return smem_bytes(D, kDecWavesMax); }
+
+// waves per workgroup (HIPSERVE_DECODE_WAVES = 4 | 8). 8 waves = more concurrent
+// 32-token chunk streams per (sequence, kv head) but measured no faster on
+// MI355X (B=64 ctx 1152: 48.2 vs 47.3 us; profiles/decode_partition_sweep.md).
+static int decode_waves() {
+  static const int env = [] {
+    const char* e = getenv("HIPSERVE_DECODE_WAVES");
+    return e ? atoi(e) : 4;
+  }();
+  return env == 8 ? 8 : 4;
 }
 
 void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
@@ -238,21 +252,29 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
                          int part_size, int max_parts, float scale,
                          hipStream_t s) {
   if (B <= 0) return;
-  dim3 grid(max_parts, nkv, B), block(256);
-  const size_t smem = paged_decode_smem_bytes(D);
+  const int waves = decode_waves();
+  dim3 grid(max_parts, nkv, B), block(64 * waves);
+  const size_t smem = smem_bytes(D, waves);
   auto* o = static_cast<unsigned short*>(out);
   auto* qq = static_cast<const unsigned short*>(q);
   auto* kc = static_cast<const unsigned short*>(k_cache);
   auto* vc = static_cast<const unsigned short*>(v_cache);
+#define HS_DECODE(DD, WW)                                                                                   \
+  paged_decode_kernel<DD, WW><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables,    \
+                                                       bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv,     \
+                                                       block_size, part_size, max_parts, scale)
   if (D == 128) {
-    paged_decode_kernel<128><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, block_size, part_size, max_parts, scale);
+    if (waves == 8) HS_DECODE(128, 8);
+    else HS_DECODE(128, 4);
     if (max_parts > 1)
       paged_decode_reduce_kernel<128><<<dim3(nq, B), dim3(128), 0, s>>>(o, out_stride, tmp_out, tmp_ml, context_lens, nq, part_size, max_parts);
   } else {
-    paged_decode_kernel<64><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, block_size, part_size, max_parts, scale);
+    if (waves == 8) HS_DECODE(64, 8);
+    else HS_DECODE(64, 4);
     if (max_parts > 1)
       paged_decode_reduce_kernel<64><<<dim3(nq, B), dim3(64), 0, s>>>(o, out_stride, tmp_out, tmp_ml, context_lens, nq, part_size, max_parts);
   }
+#undef HS_DECODE
 }
 
 }  // namespace hipserve

@@ -91,7 +91,7 @@ class ModelRunner:
 
             ms = [b for b in self.buckets if b <= 64]
             self.model.fused_decode = bool(ecfg.extra.get("fused_decode", True))
-            fused = self.model.fused_gemm_shapes() if self.model.fused_decode else set()
+            fused = self.model.fused_gemm_shapes() if self.model.fused_decode else {}
             self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms, fused=fused)
             if ecfg.extra.get("packed_decode", True):
                 self.model.pack_decode_weights(gemm.TUNER.packed_shapes())

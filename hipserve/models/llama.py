@@ -241,12 +241,22 @@ class LlamaModel:
             n += w.numel() * w.element_size()
         return n
 
-    def fused_gemm_shapes(self):
-        """(N, K) of the projections whose decode GEMM output feeds a fused epilogue."""
+    def fused_gemm_shapes(self) -> dict:
+        """{(N, K): epilogue spec} of the projections whose decode GEMM output feeds
+        a fused epilogue (ops/gemm.py tunes them as GEMM + epilogue units)."""
         if self.tp.world_size != 1 or not self.layers:
-            return set()
+            return {}
         lw = self.layers[0]
-        return {tuple(w.shape) for w in (lw.wqkv, lw.wo, lw.wd) if isinstance(w, torch.Tensor)}
+        out = {}
+        if isinstance(lw.wo, torch.Tensor):
+            out[tuple(lw.wo.shape)] = ("norm",)
+        if isinstance(lw.wd, torch.Tensor):
+            out[tuple(lw.wd.shape)] = ("norm",)
+        if isinstance(lw.wqkv, torch.Tensor):
+            out[tuple(lw.wqkv.shape)] = ("rope", self.nq, self.nkv, self.D, self.cfg.rope_mode)
+        if isinstance(lw.wgu, torch.Tensor) and lw.wgu.shape[0] % 128 == 0:
+            out[tuple(lw.wgu.shape)] = ("glu",)
+        return out
 
     def _fused_ok(self, meta: AttnMeta) -> bool:
         return (self.fused_decode and meta.num_prefill_tokens == 0 and self.tp.world_size == 1

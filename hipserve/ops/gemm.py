@@ -30,10 +30,10 @@ PACKED: dict[int, tuple] = {}  # data_ptr -> (weakref to the plain weight, packe
 # merged gate|up weights packed gate/up-interleaved for the GLU-fused decode GEMM
 PACKED_GLU: dict[int, tuple] = {}
 COLD_BYTES = 1 << 30
-# A decode GEMM whose fp32 partials feed a fused epilogue (decode_fused.hip) saves
-# the separate elementwise launch that hipBLASLt's output would still need
-# (~5 us each at decode sizes, profiles/r1_bench_llama3_8b_v3_trace.md).
-FUSE_BONUS_US = 4.0
+# Fused decode shapes are tuned as whole units — the GEMM plus the op its output
+# feeds (RMSNorm / RoPE+KV write / SiLU-GLU): hipBLASLt pays a separate epilogue
+# launch, the decode GEMMs pay for reading their split-K partials in the fused
+# epilogue, and only timing both units picks the split count that is really best.
 _EMPTY = {}
 TUNE_MS = [1, 2, 4, 8, 16, 24, 32, 48, 64]
 
@@ -87,30 +87,42 @@ class GemmTuner:
         return v[len(v) // 2] * 1000.0 / n
 
     @torch.inference_mode()
-    def tune(self, shapes, device, ms=None, fused=()):
+    def tune(self, shapes, device, ms=None, fused=None):
+        """fused: {(N, K): spec} for projections whose output feeds a fused
+        epilogue in the decode layer — ("norm",), ("rope", nq, nkv, D, mode) or
+        ("glu",); those are timed as GEMM + epilogue units."""
         # inference mode like the engine's graph capture: the generator state tensors a
         # capture registers must not switch between inference and normal tensors
+        fused = fused or {}
         ms = [m for m in (ms or TUNE_MS) if m <= 64]
         for (N, K) in sorted(set(shapes)):
+            spec = fused.get((N, K))
             ncopy = max(1, min(16, -(-COLD_BYTES // (N * K * 2))))
             ws_ = [torch.randn(N, K, device=device, dtype=torch.bfloat16) for _ in range(ncopy)]
-            wp_ = [pack(w) for w in ws_] if packable(N, K) else None
+            glu = spec is not None and spec[0] == "glu"
+            wp_ = [pack(w, glu=glu) for w in ws_] if packable(N, K) and (not glu or N % 128 == 0) else None
             n = max(16, ncopy)
             for M in ms:
                 x = torch.randn(M, K, device=device, dtype=torch.bfloat16)
                 out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
-                best, best_t = "blas", self._time(lambda i: F.linear(x, ws_[i % ncopy]), n=n)
+                unit = _Unit(spec, M, N, device) if spec else None
+                blas_fn = (lambda i: unit.blas(F.linear(x, ws_[i % ncopy]))) if unit else \
+                    (lambda i: F.linear(x, ws_[i % ncopy]))
+                best, best_t = "blas", self._time(blas_fn, n=n)
                 t_blas = best_t
-                if (N, K) in fused:
-                    best_t += FUSE_BONUS_US  # hipBLASLt output still needs the epilogue launch
                 for cfg in self.candidates(M, N, K, packed=wp_ is not None):
-                    t = self._time(lambda i: run_choice(cfg, out, x, ws_[i % ncopy],
-                                                        wp_[i % ncopy] if wp_ else None), n=n)
+                    if unit is not None:
+                        if cfg[0] == "sk":
+                            continue
+                        fn = (lambda i: unit.fused(cfg, x, ws_[i % ncopy], wp_[i % ncopy] if wp_ else None))
+                    else:
+                        fn = (lambda i: run_choice(cfg, out, x, ws_[i % ncopy], wp_[i % ncopy] if wp_ else None))
+                    t = self._time(fn, n=n)
                     if t < best_t * 0.97:
                         best, best_t = cfg, t
                 self.table[(M, N, K)] = best
-                self.report.append({"M": M, "N": N, "K": K, "blas_us": round(t_blas, 1),
-                                    "best": str(best), "best_us": round(best_t, 1),
+                self.report.append({"M": M, "N": N, "K": K, "unit": spec[0] if spec else "gemm",
+                                    "blas_us": round(t_blas, 1), "best": str(best), "best_us": round(best_t, 1),
                                     "best_TBps": round(N * K * 2 / best_t / 1e6, 2)})
             del ws_, wp_
         return self.report
@@ -133,6 +145,65 @@ class GemmTuner:
             if K % (256 * kw) == 0:
                 out.append(("sk", rt, kw))
         return out
+
+
+class _Unit:
+    """A decode GEMM together with the op its output feeds, for tuning: the
+    hipBLASLt path runs the unfused epilogue kernel, a decode-GEMM config runs
+    the split-K partial GEMM + the fused epilogue it enables (or, for a plain
+    dg config on a GLU shape, the GEMM + silu_and_mul)."""
+
+    def __init__(self, spec, M, N, device):
+        op = torch.ops.hipserve
+        self.op, self.spec, self.M, self.N = op, spec, M, N
+        bf = dict(device=device, dtype=torch.bfloat16)
+        self.kind = spec[0]
+        if self.kind == "norm":
+            self.res = torch.randn(M, N, **bf)
+            self.w = torch.ones(N, **bf)
+            self.y = torch.empty(M, N, **bf)
+        elif self.kind == "rope":
+            _, self.nq, self.nkv, self.D, self.mode = spec
+            nb = -(-M // 16) + 1
+            self.kc = torch.zeros(nb, self.nkv, 16, self.D, **bf)
+            self.vc = torch.zeros(nb, self.nkv, self.D, 16, **bf)
+            self.pos = torch.arange(M, device=device, dtype=torch.long)
+            self.slots = torch.arange(M, device=device, dtype=torch.long)
+            self.cs = torch.rand(4096, self.D, device=device, dtype=torch.float32)
+            self.qkv = torch.empty(M, N, **bf)
+        elif self.kind == "glu":
+            self.act = torch.empty(M, N // 2, **bf)
+
+    def blas(self, y):
+        op = self.op
+        if self.kind == "norm":
+            op.fused_add_rmsnorm(self.y, y, self.res, self.w, 1e-5)
+        elif self.kind == "rope":
+            op.rope_cache(y, self.pos, self.slots, self.cs, self.kc, self.vc, self.nq, self.nkv, self.D, self.mode)
+        else:
+            op.silu_and_mul(self.act, y)
+
+    def fused(self, cfg, x, w, wp):
+        op, M, N = self.op, self.M, self.N
+        kind, rt, S = cfg
+        packed = kind == "dgp" and wp is not None
+        if self.kind == "glu":
+            if packed:  # GLU in the GEMM epilogue (S = 1) or the GLU reduce (S > 1)
+                ws = torch.empty(S * M * N, dtype=torch.float32, device=x.device) if S > 1 else \
+                    _empty(x.device)[1]
+                op.decode_gemm_glu(self.act, x, wp, ws, N, rt, S)
+            else:
+                y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+                decode_gemm(y, x, w, rt, S)
+                op.silu_and_mul(self.act, y)
+            return
+        ws = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
+        op.decode_gemm_partial(ws, x, wp if packed else w, N, rt, S, packed)
+        if self.kind == "norm":
+            op.splitk_add_rmsnorm(self.y, self.res, ws, S, self.w, 1e-5)
+        else:
+            op.splitk_rope_cache(self.qkv, ws, S, self.pos, self.slots, self.cs, self.kc, self.vc,
+                                 self.nq, self.nkv, self.D, self.mode)
 
 
 TUNER = GemmTuner()
