@@ -108,4 +108,11 @@ void launch_moe_gemm(void* out, long out_stride, const void* x, long x_stride, c
                      const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, hipStream_t s);
 void launch_moe_combine(void* out, const void* y, const float* w, const int* pair_slot, int T, int k, int H,
                         hipStream_t s);
+// out[t] = sum_j w[t, j] * bf16(sum_s ws[s, pair_slot[t*k + j], :]) — split-K partials of the w2 GEMM
+void launch_moe_combine_partial(void* out, const float* ws, long slab, int S, const float* w, const int* pair_slot,
+                                int T, int k, int H, hipStream_t s);
+// decode_gemm.hip: expert GEMM on moe_align tiles (see there)
+bool launch_moe_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
+                            long w_estride, const int* slots, const int* tile_expert, int tiles_cap, int tile,
+                            int gather_k, int N, int K, int S, bool packed, bool glu, hipStream_t s);
 }  // namespace hipserve

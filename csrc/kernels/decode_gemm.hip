@@ -36,6 +36,12 @@
 //    (64 KiB per 256-k step) — the access pattern of a memcpy, instead of 128
 //    rows x 512 B pieces scattered over 128 DRAM pages per step. Rows past N are
 //    zero padding (N is rounded up to 128 in the packed copy).
+//  * kMoe (Mixtral decode experts): blockIdx.y is one expert-sorted tile of 16*MT
+//    slots from moe_align (moe.hip); the workgroup streams THAT expert's weight
+//    (w + e * w_estride) and stages the tile's x rows through the slot list
+//    (row = pair / gather_k for the token-indexed w13 input, row = slot for the
+//    slot-indexed w2 input). Padding slots (-1) read row 0 and are never stored;
+//    output rows / partial rows are slot-indexed. Tiles of absent experts exit.
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -43,11 +49,18 @@ namespace hipserve {
 
 constexpr int DG_LDS_ROW = 264;  // 256 + 8 bf16 pad -> 528 B row stride
 
-template <int MT, int RT, int NWAVES, int NSTEPS, bool kPacked, bool kGlu>
+struct MoeTiles {
+  const int* slots;        // [tiles_cap * 16 * MT] pair index per slot, -1 = padding
+  const int* tile_expert;  // [tiles_cap] expert of each tile, -1 = unused tile
+  int gather_k;            // > 0: x row = pair / gather_k; 0: x row = slot
+  long w_estride;          // elements between consecutive experts' weights
+};
+
+template <int MT, int RT, int NWAVES, int NSTEPS, bool kPacked, bool kGlu, bool kMoe = false>
 __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     unsigned short* __restrict__ out, long out_stride, float* __restrict__ ws,
     const unsigned short* __restrict__ x, long x_stride, const unsigned short* __restrict__ w,
-    int M, int N, int K, int S, int tiles) {
+    int M, int N, int K, int S, int tiles, MoeTiles moe = MoeTiles{}) {
   constexpr int NW = 16 * RT * NWAVES;
   constexpr int XR = 16 * MT;                 // x rows staged (padded M)
   constexpr int NT = 64 * NWAVES;             // threads
@@ -61,6 +74,13 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
                                   // code lets hipcc count every vmcnt exactly
   const int k0 = split * 256 * NSTEPS;
   const int nbase = tile * NW + wave * 16 * RT;
+  int mrow0 = 0;  // kMoe: first slot of this expert tile
+  if constexpr (kMoe) {
+    const int e = moe.tile_expert[blockIdx.y];
+    if (e < 0) return;
+    w += (long)e * moe.w_estride;
+    mrow0 = blockIdx.y * XR;
+  }
 
   const unsigned short* wr[RT];
   if constexpr (kPacked) {
@@ -75,7 +95,22 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
 
   // x staging: thread -> (row, 16-byte column chunk)
   u16x8 xv[XPASS];
+  [[maybe_unused]] const unsigned short* xg[XPASS];  // kMoe: gathered row pointers
+  if constexpr (kMoe) {
+#pragma unroll
+    for (int p = 0; p < XPASS; ++p) {
+      const int idx = p * NT + tid, row = idx >> 5, col = (idx & 31) * 8;
+      const int slot = mrow0 + row, pr = moe.slots[slot];
+      const long xrow = pr < 0 ? 0 : (moe.gather_k > 0 ? pr / moe.gather_k : slot);
+      xg[p] = x + xrow * x_stride + k0 + col;
+    }
+  }
   auto load_x = [&](int step) {
+    if constexpr (kMoe) {
+#pragma unroll
+      for (int p = 0; p < XPASS; ++p) xv[p] = *reinterpret_cast<const u16x8*>(xg[p] + step * 256);
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < XPASS; ++p) {
       const int idx = p * NT + tid, row = idx >> 5, col = (idx & 31) * 8;
@@ -142,6 +177,20 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     if (st + 1 < nsteps) __syncthreads();
   }
 
+  // output row of MFMA column m = 16t + c: slot-indexed for kMoe
+  bool mok[MT];
+  int orow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = 16 * t + c;
+    if constexpr (kMoe) {
+      orow[t] = mrow0 + m;
+      mok[t] = moe.slots[orow[t]] >= 0;
+    } else {
+      orow[t] = m;
+      mok[t] = m < M;
+    }
+  }
   if constexpr (kGlu) {
     if (ws == nullptr) {
       // row group rg = wave*RT + r: 0-3 gate rows, 4-7 the matching up rows
@@ -167,8 +216,7 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
         const int col = tile * 64 + rg * 16 + 4 * g;  // act column of j = 0
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
-          const int m = 16 * t + c;
-          if (m >= M) continue;
+          if (!mok[t]) continue;
           unsigned short o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -177,7 +225,7 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
           uint2 v;
           v.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
           v.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-          if (col < I) *reinterpret_cast<uint2*>(out + (long)m * out_stride + col) = v;
+          if (col < I) *reinterpret_cast<uint2*>(out + (long)orow[t] * out_stride + col) = v;
         }
       }
       return;
@@ -190,15 +238,14 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
     if (n >= N) continue;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const int m = 16 * t + c;
-      if (m >= M) continue;
+      if (!mok[t]) continue;
       if (ws == nullptr) {
         uint2 v;
         v.x = pack_bf16x2(acc[r][t][0], acc[r][t][1]);
         v.y = pack_bf16x2(acc[r][t][2], acc[r][t][3]);
-        *reinterpret_cast<uint2*>(out + (long)m * out_stride + n) = v;
+        *reinterpret_cast<uint2*>(out + (long)orow[t] * out_stride + n) = v;
       } else {
-        *reinterpret_cast<f32x4*>(ws + ((long)split * M + m) * N + n) = acc[r][t];
+        *reinterpret_cast<f32x4*>(ws + ((long)split * M + orow[t]) * N + n) = acc[r][t];
       }
     }
   }
@@ -314,6 +361,56 @@ bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, lo
   }
   return packed ? dg_dispatch<true, false>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, flags, s)
                 : dg_dispatch<false, false>(out, out_stride, ws, x, x_stride, w, M, N, K, rt, S, flags, s);
+}
+
+// ---- MoE decode experts (kMoe): one 128-row weight tile x one expert tile per workgroup.
+template <int MT, int NSTEPS, bool kPacked, bool kGlu>
+static void moe_dg_launch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
+                          const MoeTiles& mt, int tiles_cap, int N, int K, int S, hipStream_t s) {
+  const int tiles = (N + 127) / 128;  // RT = 1, 8 waves: 128 weight rows per workgroup
+  dim3 grid(tiles * S, tiles_cap);
+  decode_gemm_kernel<MT, 1, 8, NSTEPS, kPacked, kGlu, true><<<grid, 512, 0, s>>>(
+      static_cast<unsigned short*>(out), out_stride, ws, static_cast<const unsigned short*>(x), x_stride,
+      static_cast<const unsigned short*>(w), tiles_cap * 16 * MT, N, K, S, tiles, mt);
+}
+
+template <int MT, bool kPacked, bool kGlu>
+static bool moe_dg_steps(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
+                         const MoeTiles& mt, int tiles_cap, int N, int K, int S, hipStream_t s) {
+  switch (K / S / 256) {
+    case 1: moe_dg_launch<MT, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    case 2: moe_dg_launch<MT, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    case 4: moe_dg_launch<MT, 4, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    case 7: moe_dg_launch<MT, 7, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    case 8: moe_dg_launch<MT, 8, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    case 16: moe_dg_launch<MT, 16, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    default: return false;
+  }
+}
+
+template <bool kPacked, bool kGlu>
+static bool moe_dg_tile(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
+                        const MoeTiles& mt, int tiles_cap, int tile, int N, int K, int S, hipStream_t s) {
+  if (tile == 16) return moe_dg_steps<1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s);
+  if (tile == 32) return moe_dg_steps<2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s);
+  if (tile == 64) return moe_dg_steps<4, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s);
+  return false;
+}
+
+// Expert GEMM over moe_align tiles. ws == nullptr: bf16 out[slot, N] (glu: act[slot, N/2]
+// from the gate/up-interleaved packing, S must be 1); else fp32 partials
+// ws[S, tiles_cap * tile, N] (summed by moe_combine_partial). w: [E] x (packed or
+// row-major [N, K]) with w_estride elements per expert. K / S = 256 * {1,2,4,7,8,16}.
+bool launch_moe_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
+                            long w_estride, const int* slots, const int* tile_expert, int tiles_cap, int tile,
+                            int gather_k, int N, int K, int S, bool packed, bool glu, hipStream_t s) {
+  const MoeTiles mt{slots, tile_expert, gather_k, w_estride};
+  if (glu) {
+    return packed && ws == nullptr && S == 1 && N % 128 == 0 &&
+           moe_dg_tile<true, true>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, tile, N, K, S, s);
+  }
+  return packed ? moe_dg_tile<true, false>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, tile, N, K, S, s)
+                : moe_dg_tile<false, false>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, tile, N, K, S, s);
 }
 
 // W[N, K] row-major -> packed [ceil(N/128)][K/256][8][8][64][8] (zero rows past N).

@@ -171,6 +171,36 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(unsigned short* __rest
   }
 }
 
+// Split-K w2 partials ws[s][slot][H] (fp32): each pair's y row is bf16(sum over s),
+// exactly what the bf16 expert GEMM output would be, then the weighted sum.
+__global__ __launch_bounds__(256) void moe_combine_partial_kernel(unsigned short* __restrict__ out,
+                                                                  const float* __restrict__ ws, long slab, int S,
+                                                                  const float* __restrict__ w,
+                                                                  const int* __restrict__ pair_slot, int k, int H) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const float wt = w[(long)t * k + j];
+      const float* p = ws + (long)pair_slot[t * k + j] * H + 8 * c;
+      f32x4 lo = *reinterpret_cast<const f32x4*>(p), hi = *reinterpret_cast<const f32x4*>(p + 4);
+      for (int s = 1; s < S; ++s) {
+        lo += *reinterpret_cast<const f32x4*>(p + s * slab);
+        hi += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += wt * bf16_to_f32(f32_to_bf16(lo[e]));
+        acc[e + 4] += wt * bf16_to_f32(f32_to_bf16(hi[e]));
+      }
+    }
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f32_to_bf16(acc[e]);
+    *reinterpret_cast<u16x8*>(out + (long)t * H + 8 * c) = o;
+  }
+}
+
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
                              hipStream_t s) {
   if (T <= 0) return;
@@ -217,6 +247,12 @@ void launch_moe_combine(void* out, const void* y, const float* w, const int* pai
   if (T <= 0) return;
   moe_combine_kernel<<<T, 256, 0, s>>>(static_cast<unsigned short*>(out), static_cast<const unsigned short*>(y), w,
                                        pair_slot, k, H);
+}
+
+void launch_moe_combine_partial(void* out, const float* ws, long slab, int S, const float* w, const int* pair_slot,
+                                int T, int k, int H, hipStream_t s) {
+  if (T <= 0) return;
+  moe_combine_partial_kernel<<<T, 256, 0, s>>>(static_cast<unsigned short*>(out), ws, slab, S, w, pair_slot, k, H);
 }
 
 }  // namespace hipserve

@@ -420,6 +420,56 @@ void moe_combine(at::Tensor& out, const at::Tensor& y, const at::Tensor& w, cons
                                H, cur_stream());
 }
 
+// Expert GEMM over moe_align tiles on the decode GEMM (decode_gemm.hip, kMoe).
+// w: [E, ceil(N/128)*128*K] packed (pack_decode_weight per expert; glu = gate/up
+// interleaved) or row-major [E, N, K]. out bf16: [slots, N] (glu: act [slots, N/2],
+// splits must be 1); out fp32: partials [splits, slots, N] for moe_combine_partial.
+void moe_decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& slots,
+                     const at::Tensor& tile_expert, int64_t tile, int64_t gather_k, int64_t N, int64_t splits,
+                     bool packed, bool glu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_ROWMAJOR(x); CHECK_CONTIG(w);
+  TORCH_CHECK(slots.scalar_type() == at::kInt && tile_expert.scalar_type() == at::kInt && slots.is_contiguous());
+  TORCH_CHECK(tile == 16 || tile == 32 || tile == 64, "moe_decode_gemm: tile in {16, 32, 64}");
+  const long nslots = slots.numel();
+  TORCH_CHECK(nslots % tile == 0 && tile_expert.numel() * tile >= nslots, "moe_decode_gemm: tiles");
+  const int E = w.size(0);
+  const long K = x.size(1);
+  const long estride = packed ? (N + 127) / 128 * 128 * K : N * K;
+  TORCH_CHECK(w.numel() == E * estride, "moe_decode_gemm: weight size != E * (packed) N * K");
+  TORCH_CHECK(K % 256 == 0 && splits >= 1 && K % (256 * splits) == 0 && x.stride(0) % 8 == 0,
+              "moe_decode_gemm: K must be a multiple of 256 * splits");
+  TORCH_CHECK(gather_k > 0 || x.size(0) >= nslots, "moe_decode_gemm: ungathered x needs one row per slot");
+  float* ws = nullptr;
+  if (out.scalar_type() == at::kFloat) {
+    TORCH_CHECK(!glu && out.is_contiguous() && out.numel() >= splits * nslots * N && N % 4 == 0,
+                "moe_decode_gemm: fp32 partials [splits, slots, N]");
+    ws = out.data_ptr<float>();
+  } else {
+    CHECK_BF16(out); CHECK_ROWMAJOR(out);
+    TORCH_CHECK(splits == 1 && out.size(0) >= nslots && out.size(1) >= (glu ? N / 2 : N) && out.stride(0) % 4 == 0,
+                "moe_decode_gemm: bf16 out [slots, N] (glu: [slots, N/2]) needs splits == 1");
+    TORCH_CHECK(!glu || N % 128 == 0, "moe_decode_gemm: glu needs N % 128 == 0");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_moe_decode_gemm(out.data_ptr(), out.dim() == 2 ? out.stride(0) : N, ws, x.data_ptr(),
+                                               x.stride(0), w.data_ptr(), estride, slots.data_ptr<int>(),
+                                               tile_expert.data_ptr<int>(), nslots / tile, tile, gather_k, N, K,
+                                               splits, packed, glu, cur_stream()),
+              "moe_decode_gemm: unsupported K / splits (K / splits / 256 in {1,2,4,7,8,16}) or glu without packing");
+}
+
+void moe_combine_partial(at::Tensor& out, const at::Tensor& ws, const at::Tensor& w, const at::Tensor& pair_slot,
+                         int64_t k) {
+  CHECK_DEV(ws); CHECK_BF16(out); CHECK_CONTIG(out);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.dim() == 3 && ws.is_contiguous(), "ws [S, slots, H] fp32");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && pair_slot.scalar_type() == at::kInt);
+  const int T = out.size(0), H = out.size(1);
+  TORCH_CHECK(ws.size(2) == H && H % 8 == 0 && w.numel() >= T * k && pair_slot.numel() >= T * k);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  hipserve::launch_moe_combine_partial(out.data_ptr(), ws.data_ptr<float>(), ws.stride(0), ws.size(0),
+                                       w.data_ptr<float>(), pair_slot.data_ptr<int>(), T, k, H, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
@@ -427,6 +477,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot) -> ()");
   m.def("moe_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor w, Tensor pair_slot, int k) -> ()");
+  m.def("moe_decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k, int N, int splits, bool packed, bool glu) -> ()");
+  m.def("moe_combine_partial(Tensor(a!) out, Tensor ws, Tensor w, Tensor pair_slot, int k) -> ()");
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
@@ -476,5 +528,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("moe_decode_gemm", &moe_decode_gemm);
+  m.impl("moe_combine_partial", &moe_combine_partial);
   m.impl("gguf_dequant", &gguf_dequant);
 }

@@ -14,7 +14,9 @@ in-house replacement for that engine's model executor.
 """
 from __future__ import annotations
 
+import logging
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -25,6 +27,9 @@ from ..ops import gemm
 from ..ops import reference as ref
 from ..parallel.comm import TPGroup
 
+log = logging.getLogger(__name__)
+
+DG_MOE_STEPS = (1, 2, 4, 7, 8, 16)  # 256-k steps per K slice the expert decode GEMM is built for
 MOE_KERNEL_MAX_PAIRS = 2048  # larger (prefill) batches use per-expert hipBLASLt GEMMs
 
 
@@ -60,6 +65,7 @@ class LayerWeights:
     router: torch.Tensor | None = None       # [E, H]
     w13: torch.Tensor | None = None          # [E, 2*I/TP, H]
     w2: torch.Tensor | None = None           # [E, H, I/TP]
+    moe_packed: tuple | None = None          # (w13 gate/up-interleaved, w2) packed per expert for decode
     quant: dict = field(default_factory=dict)  # GGUF-quantized GEMM weights by name
 
 
@@ -239,7 +245,38 @@ class LlamaModel:
         if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
             gemm.register_packed(w)
             n += w.numel() * w.element_size()
-        return n
+        return n + self.pack_moe_weights()
+
+    def pack_moe_weights(self) -> int:
+        """Per-expert packed copies of the MoE weights for the decode expert GEMM
+        (``moe_hip``): w13 gate/up-interleaved (SiLU-GLU in the GEMM epilogue), w2
+        plain. The row-major originals stay for prefill (per-expert hipBLASLt), so
+        this doubles the expert bytes (Mixtral-8x7B: +90 GB of 288 GB) — skipped
+        when less than 24 GiB of HBM would stay free for the KV cache, or with
+        HIPSERVE_MOE_PACK=0 (the row-major expert GEMM runs instead)."""
+        if (not self.cfg.num_experts or getattr(self.ops, "name", "") != "hip"
+                or os.environ.get("HIPSERVE_MOE_PACK", "1") == "0"):
+            return 0
+        lws = [lw for lw in self.layers if isinstance(lw.w13, torch.Tensor) and self._moe_decode_ok(lw)]
+        if not lws:
+            return 0
+        need = sum(2 * (lw.w13.numel() + lw.w2.numel()) for lw in lws)
+        if self.device.type == "cuda":
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if need + (24 << 30) > free:
+                log.warning("MoE decode weights not packed: %.1f GB needed, %.1f GB free", need / 2**30, free / 2**30)
+                return 0
+        op = torch.ops.hipserve
+        for lw in lws:
+            E, N13, K13 = lw.w13.shape
+            _, N2, K2 = lw.w2.shape
+            p13 = torch.empty(E, N13 * K13, dtype=lw.w13.dtype, device=lw.w13.device)
+            p2 = torch.empty(E, -(-N2 // 128) * 128 * K2, dtype=lw.w2.dtype, device=lw.w2.device)
+            for e in range(E):
+                op.pack_decode_weight(p13[e], lw.w13[e], True)
+                op.pack_decode_weight(p2[e], lw.w2[e], False)
+            lw.moe_packed = (p13, p2)
+        return need
 
     def fused_gemm_shapes(self) -> dict:
         """{(N, K): epilogue spec} of the projections whose decode GEMM output feeds
@@ -422,10 +459,35 @@ class LlamaModel:
             out.index_add_(0, toks, y)
         return out.to(x.dtype)
 
+    def _moe_decode_ok(self, lw: LayerWeights) -> bool:
+        """Shapes the expert decode GEMM (decode_gemm.hip kMoe) takes: K = H for w13
+        (one K slice of 256 * {1,2,4,7,8,16}) and K = I/TP for w2 (split over K)."""
+        H, I = self.cfg.hidden_size, self.inter
+        return ((H // 256) in DG_MOE_STEPS and H % 256 == 0 and I % 256 == 0 and (2 * I) % 128 == 0
+                and self._moe_w2_splits(I, 1, 1) > 0)
+
+    @staticmethod
+    def _moe_w2_splits(K: int, ntiles: int, active: int) -> int:
+        """Split-K factor of the w2 expert GEMM: the fewest K slices (of 256 * one of
+        DG_MOE_STEPS) that give >= 1024 workgroups over the active expert tiles."""
+        ks = K // 256
+        opts = sorted(ks // st for st in DG_MOE_STEPS if ks % st == 0)
+        if not opts:
+            return 0
+        for S in opts:
+            if ntiles * S * active >= 1024:
+                return S
+        return opts[-1]
+
     def moe_hip(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Graph-capturable MoE on the gfx950 kernels (decode-sized batches): top-k
         routing, expert-sorted 16/32/64-row tiles, two gathered MFMA GEMMs with the
-        SiLU*up in between, weighted combine. No host synchronisation."""
+        SiLU*up in between, weighted combine. No host synchronisation.
+
+        The expert GEMMs are the decode GEMM in its MoE mode (weight-streaming:
+        128 weight rows x one expert tile per workgroup, x tile staged in LDS):
+        with packed weights (``pack_moe_weights``) the SiLU-GLU runs in the w13
+        epilogue, and w2 writes split-K fp32 partials that the combine sums."""
         op = torch.ops.hipserve
         cfg = self.cfg
         E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
@@ -442,13 +504,30 @@ class LlamaModel:
         ntiles = torch.empty(1, dtype=torch.int32, device=dev)
         pair_slot = torch.empty(P, dtype=torch.int32, device=dev)
         op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot)
+        out = torch.empty(T, H, dtype=x.dtype, device=dev)
+        if self._moe_decode_ok(lw):
+            packed = lw.moe_packed is not None
+            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+            if packed:
+                op.moe_decode_gemm(act, x, lw.moe_packed[0], slots, tile_expert, tile, k, 2 * self.inter, 1,
+                                   True, True)
+            else:
+                gu = torch.empty(cap, 2 * self.inter, dtype=x.dtype, device=dev)
+                op.moe_decode_gemm(gu, x, lw.w13, slots, tile_expert, tile, k, 2 * self.inter, 1, False, False)
+                self.ops.silu_and_mul(act, gu)
+            active = min(E, cap // tile, P)
+            S = self._moe_w2_splits(self.inter, -(-H // 128), active)
+            ws = torch.empty(S, cap, H, dtype=torch.float32, device=dev)
+            op.moe_decode_gemm(ws, act, lw.moe_packed[1] if packed else lw.w2, slots, tile_expert, tile, 0, H, S,
+                               packed, False)
+            op.moe_combine_partial(out, ws, w, pair_slot, k)
+            return out
         gu = torch.empty(cap, 2 * self.inter, dtype=x.dtype, device=dev)
         op.moe_gemm(gu, x, lw.w13, slots, tile_expert, tile, k)
         act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
         self.ops.silu_and_mul(act, gu)
         y = torch.empty(cap, H, dtype=x.dtype, device=dev)
         op.moe_gemm(y, act, lw.w2, slots, tile_expert, tile, 0)
-        out = torch.empty(T, H, dtype=x.dtype, device=dev)
         op.moe_combine(out, y, w, pair_slot, k)
         return out
 

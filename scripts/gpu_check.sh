@@ -38,30 +38,24 @@ run_bench_q4() {
   timeout -k 10 480 python -u bench.py --quantization q4_k_m --out $OUT/bench_q4km.json > $OUT/bench_q4km.log 2>&1
   local rc=$?; tail -n 2 $OUT/bench_q4km.log; return $rc
 }
-run_prof_q4() {
-  local here=$PWD
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/profq \
-     -o run -- python3 $here/bench.py --path engine --quantization q4_k_m --steps 1 --warmup 1 > $here/$OUT/profq.log 2>&1)
-  local rc=$?; tail -n 3 $OUT/profq.log
+# prof_run <name> <bench args...>: kernel trace of one engine-path bench step,
+# summarised by tools/prof_db.py into $OUT/<name>_summary.md.
+prof_run() {
+  local here=$PWD name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/$name \
+     -o run -- python3 $here/bench.py --path engine --steps 1 --warmup 1 "$@" > $here/$OUT/$name.log 2>&1)
+  local rc=$?; tail -n 3 $OUT/$name.log
   [ $rc -eq 0 ] || return $rc
-  local db; db=$(find $OUT/profq -name '*results.db' | head -n 1)
-  [ -n "$db" ] && (cd tools && python prof_db.py "$here/$db" "$here/$OUT/profq_summary.md" "bench.py --path engine --quantization q4_k_m" > /dev/null)
-  rm -rf $OUT/profq
+  local db; db=$(find $OUT/$name -name '*results.db' | head -n 1)
+  [ -n "$db" ] && (cd tools && python prof_db.py "$here/$db" "$here/$OUT/${name}_summary.md" "bench.py --path engine $*" > /dev/null)
+  find $OUT/$name -name '*kernel_stats.csv' -exec cp {} $OUT/${name}_kernel_stats.csv \;
+  rm -rf $OUT/$name  # raw traces exceed gpurun's 64 MiB copy-back limit
   return 0
 }
-run_prof() {
-  local here=$PWD
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/prof \
-     -o run -- python3 $here/bench.py --path engine --steps 1 --warmup 1 > $here/$OUT/prof.log 2>&1)
-  local rc=$?; tail -n 3 $OUT/prof.log
-  [ $rc -eq 0 ] || return $rc
-  local db; db=$(find $OUT/prof -name '*results.db' | head -n 1)
-  if [ -n "$db" ]; then
-    (cd tools && python prof_db.py "$here/$db" "$here/$OUT/prof_summary.md" "bench.py --path engine" > /dev/null)
-  fi
-  find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/prof_kernel_stats.csv \;
-  rm -rf $OUT/prof  # raw traces exceed gpurun's 64 MiB copy-back limit
-  return 0
+run_bench_mixtral() {
+  timeout -k 10 600 python -u bench.py --model mixtral-8x7b --concurrency 32 --out $OUT/bench_mixtral.json \
+    > $OUT/bench_mixtral.log 2>&1
+  local rc=$?; tail -n 2 $OUT/bench_mixtral.log; return $rc
 }
 
 for s in $steps; do
@@ -73,8 +67,10 @@ for s in $steps; do
     ops) run_ops ;;
     bench) run_bench ;;
     bench_q4) run_bench_q4 ;;
-    prof_q4) run_prof_q4 ;;
-    prof) run_prof ;;
+    bench_mixtral) run_bench_mixtral ;;
+    prof_q4) prof_run profq --quantization q4_k_m ;;
+    prof) prof_run prof ;;
+    prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done

@@ -299,9 +299,12 @@ def test_decode_gemm_packed(ops, M, N, K, rt, splits):
     _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
 
 
+@pytest.mark.parametrize("mode", ["packed", "rowmajor", "legacy"])
 @pytest.mark.parametrize("T,E,k", [(1, 8, 2), (13, 8, 2), (64, 8, 2), (200, 8, 2), (5, 4, 1)])
-def test_moe_kernels_match_reference(ops, T, E, k):
-    """HIP MoE (topk softmax, align, gathered GEMMs, combine) vs the torch path."""
+def test_moe_kernels_match_reference(ops, T, E, k, mode, monkeypatch):
+    """HIP MoE (topk softmax, align, gathered GEMMs, combine) vs the torch path, for
+    the expert decode GEMM on packed (GLU epilogue + split-K partial combine) and
+    row-major weights, and the legacy 16-row gathered GEMM."""
     import types
 
     from hipserve.config import PRESETS
@@ -317,6 +320,12 @@ def test_moe_kernels_match_reference(ops, T, E, k):
                       w13=torch.randn(E, 1536, 512, device=DEV, dtype=torch.bfloat16) * 0.05,
                       w2=torch.randn(E, 512, 768, device=DEV, dtype=torch.bfloat16) * 0.05)
     x = torch.randn(T, 512, device=DEV, dtype=torch.bfloat16)
+    if mode == "packed":
+        assert m.pack_moe_weights() == 0  # no layers registered on the model: nothing packed
+        m.layers = [lw]
+        assert m.pack_moe_weights() > 0 and lw.moe_packed is not None
+    elif mode == "legacy":
+        monkeypatch.setattr(LlamaModel, "_moe_decode_ok", lambda self, lw: False)
     got = m.moe_hip(x, lw).float()
     ref_ops = types.SimpleNamespace(name="reference", silu_and_mul=ops.silu_and_mul)
     m.ops = ref_ops
