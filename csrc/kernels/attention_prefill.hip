@@ -15,6 +15,8 @@
 //    lane movement (accumulator-as-operand, guide §3); the matching A operand is
 //    V^T, which the transposed-per-block V cache serves as two 8-byte loads.
 //  * online softmax in the log2 domain.
+#include <cstdlib>
+
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -151,6 +153,217 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   }
 }
 
+// ---- v2: LDS-shared K/V tiles, GQA heads per workgroup (D = 128, G = nq/nkv >= 2) ----
+//
+//  * workgroup = NWV (4 or 8) waves = HG query heads of ONE kv head x NWV/HG blocks
+//    of 32 query rows (G = 4, NWV = 4: 4 heads x 32 rows); every K/V tile is loaded
+//    once into LDS and read by all waves (v1: every wave re-read it from L2 per
+//    query head). 8 waves (default); 4 (HIPSERVE_PREFILL_ATTN_WAVES=4) measured
+//    2.5-2.8x slower (one 4-wave workgroup per CU resident).
+//  * 64-key tiles, double-buffered in LDS; global loads run two tiles ahead in two
+//    register sets (tile t+2 is issued before tile t's MFMAs, tile t+1 is written
+//    to LDS after them: issue-early / write-late), one barrier per tile.
+//  * S^T = K . Q^T (swapped, so a lane owns 16 keys of one query row) with the K
+//    rows of each 16-key group stored in LDS with key bits 2 and 3 swapped: the S^T
+//    accumulator of a lane then holds 8 CONTIGUOUS keys per MFMA k-slot, so it is
+//    the P^T B operand of O^T = V^T . P^T as is, and the matching V^T A operand is a
+//    single ds_read_b128 from the transposed V tile.
+//  * one online-softmax update per 64 keys; O is rescaled only when some row's
+//    max moved (exact: alpha == 1 otherwise); masks only on diagonal tiles.
+//  * LDS rows padded (K 272 B, V^T 144 B): the 16 lanes of each b128 read phase
+//    hit 16 distinct 16-byte bank groups.
+//  * heaviest query tiles are dispatched first against the causal tail.
+static bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return e != nullptr && *e != 0 && *e != '0';
+}
+
+constexpr int PA2_KT = 64, PA2_KLD = 128 + 8, PA2_VLD = 64 + 8;
+
+template <int HG, int NWV>
+__global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
+    unsigned short* __restrict__ out, long out_stride, const unsigned short* __restrict__ q, long q_stride,
+    const unsigned short* __restrict__ k_cache, const unsigned short* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ cu_q,
+    const int* __restrict__ ctx_lens, const int* __restrict__ tiles, int nq, int nkv, int block_size,
+    float scale) {
+  constexpr int D = 128, KS = 8, NB = 4;
+  constexpr int RB = NWV / HG, QR = 32 * RB, SUB = 128 / QR;
+  constexpr int NT = 64 * NWV, NP = 1024 / NT;  // threads; K (and V^T) 16-byte pieces per thread
+  __shared__ __attribute__((aligned(16))) unsigned short kl[2][PA2_KT * PA2_KLD];
+  __shared__ __attribute__((aligned(16))) unsigned short vl[2][D * PA2_VLD];
+
+  // dispatch order (x fastest) -> (kv-head group fastest, host tile, heavier sub-tile first):
+  // with the host tiles sorted by descending causal work (model_runner) the largest
+  // workgroups go out first (longest-processing-time order against the causal tail)
+  const int L = blockIdx.x + gridDim.x * blockIdx.y, gy = gridDim.y;
+  const int gyi = L % gy, rest = L / gy;
+  const int t = rest / SUB, sub = SUB - 1 - (rest - t * SUB);
+  const int seq = tiles[2 * t], r0 = tiles[2 * t + 1] + sub * QR;
+  const int q0 = cu_q[seq], qlen = cu_q[seq + 1] - q0;
+  if (r0 >= qlen) return;  // whole workgroup: before any barrier
+  const int ctx = ctx_lens[seq];
+  const int G = nq / nkv;
+  const int kh = gyi / (G / HG);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hs = wave % HG, rb = wave / HG;
+  const int h = gyi * HG + hs;
+  const int qi = lane & 31, half = lane >> 5;
+  const int wrow0 = r0 + rb * 32;
+  const bool wactive = wrow0 < qlen;
+  const int row = min(wrow0 + qi, qlen - 1);
+  const int pos = ctx - qlen + row;
+  const int wmax_key = ctx - qlen + min(wrow0 + 31, qlen - 1);
+  const int wmin_pos = ctx - qlen + wrow0;
+  const int nkt = (ctx - qlen + min(r0 + QR - 1, qlen - 1)) / PA2_KT + 1;
+  const int* btab = block_tables + (long)seq * bt_stride;
+  const long hstride = (long)block_size * D;
+
+  // staging: NP K pieces + NP V^T pieces of 16 B per thread per tile
+  // two register sets: tile kt+2 loads while tile kt+1's registers wait for their LDS write
+  u16x8 ska[NP], sva[NP], skb[NP], svb[NP];
+  auto stage_load = [&](u16x8(&sk)[NP], u16x8(&sv)[NP], int kt) {
+    const int kbase = kt * PA2_KT;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int p = tid + NT * i;
+      const int key = min(kbase + (p >> 4), ctx - 1);
+      sk[i] = *reinterpret_cast<const u16x8*>(k_cache + ((long)btab[key / block_size] * nkv + kh) * hstride +
+                                              (long)(key % block_size) * D + (p & 15) * 8);
+      // V^T: 16-key group sc, row d, 8-key half: one block's [D][16] chunk per 256 threads
+      const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
+      int vkey = kbase + 16 * sc + 8 * k8;
+      if (vkey > ctx - 1) vkey = (ctx - 1) & ~7;
+      sv[i] = *reinterpret_cast<const u16x8*>(v_cache + ((long)btab[vkey / block_size] * nkv + kh) * hstride +
+                                              (long)d * block_size + vkey % block_size);
+    }
+  };
+  auto stage_store = [&](const u16x8(&sk)[NP], const u16x8(&sv)[NP], int buf) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int p = tid + NT * i;
+      const int kk = p >> 4;
+      const int krow = (kk & ~12) | ((kk & 4) << 1) | ((kk & 8) >> 1);  // swap key bits 2 and 3
+      *reinterpret_cast<u16x8*>(&kl[buf][krow * PA2_KLD + (p & 15) * 8]) = sk[i];
+      const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
+      *reinterpret_cast<u16x8*>(&vl[buf][d * PA2_VLD + 16 * sc + 8 * k8]) = sv[i];
+    }
+  };
+
+  bf16x8 qf[KS];
+  {
+    const unsigned short* qp = q + (long)(q0 + row) * q_stride + (long)h * D + 8 * half;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks));
+  }
+  const float sl2 = scale * 1.4426950408889634f;
+  f32x16 o[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[nb][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+
+  auto compute = [&](int kt, int buf) {
+    const int kbase = kt * PA2_KT;
+    if (wactive && kbase <= wmax_key) {
+      const unsigned short* kb = &kl[buf][qi * PA2_KLD + 8 * half];
+      f32x16 st[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[h2][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {  // two independent accumulation chains interleaved
+          const u16x8 a = *reinterpret_cast<const u16x8*>(kb + (32 * h2) * PA2_KLD + 16 * ks);
+          st[h2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], st[h2], 0, 0, 0);
+        }
+      if (kbase + PA2_KT - 1 > wmin_pos) {  // diagonal tile: causal mask
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kbase + 32 * h2 + 16 * (r >> 3) + 8 * half + 4 * ((r >> 2) & 1) + (r & 3);
+            if (key > pos) st[h2][r] = -1e30f;
+          }
+      }
+      float mx = -1e30f;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[h2][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx * sl2);
+      if (!__all(m_new == m_run)) {
+        const float alpha = exp2f(m_run - m_new);
+        l_run *= alpha;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[nb][r] *= alpha;
+        m_run = m_new;
+      }
+      float psum = 0.f;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[h2][r], sl2, -m_run));
+          psum += p;
+          pb[r >> 3][r & 7] = static_cast<__bf16>(p);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const unsigned short* vb = &vl[buf][qi * PA2_VLD + 32 * h2 + 16 * s2 + 8 * half];
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const u16x8 a = *reinterpret_cast<const u16x8*>(vb + 32 * nb * PA2_VLD);
+            o[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pb[s2], o[nb], 0, 0, 0);
+          }
+        }
+      }
+      l_run += psum;
+    }
+  };
+
+  stage_load(ska, sva, 0);
+  if (nkt > 1) stage_load(skb, svb, 1);
+  stage_store(ska, sva, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; kt += 2) {
+    // even tile kt in LDS buffer 0; set b holds tile kt+1
+    if (kt + 2 < nkt) stage_load(ska, sva, kt + 2);
+    compute(kt, 0);
+    if (kt + 1 < nkt) stage_store(skb, svb, 1);
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    // odd tile kt+1 in buffer 1; set a holds tile kt+2
+    if (kt + 3 < nkt) stage_load(skb, svb, kt + 3);
+    compute(kt + 1, 1);
+    if (kt + 2 < nkt) stage_store(ska, sva, 0);
+    __syncthreads();
+  }
+  if (!wactive) return;
+  l_run += __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_run;
+  if (wrow0 + qi < qlen) {
+    unsigned short* op = out + (long)(q0 + wrow0 + qi) * out_stride + (long)h * D;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4v w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(o[nb][4 * g + j] * inv);
+        *reinterpret_cast<u16x4v*>(op + 32 * nb + 8 * g + 4 * half) = w;
+      }
+  }
+}
+
 void launch_prefill_attention(void* out, long out_stride, const void* q,
                               long q_stride, const void* k_cache,
                               const void* v_cache, const int* block_tables,
@@ -158,6 +371,31 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               const int* tiles, int ntiles, int nq, int nkv, int D,
                               int block_size, float scale, hipStream_t s) {
   if (ntiles <= 0) return;
+  const int G = nq / nkv;
+  if (D == 128 && block_size % 16 == 0 && G >= 2 && (G & (G - 1)) == 0 && !getenv_flag("HIPSERVE_PREFILL_ATTN_V1")) {
+    const char* ew = getenv("HIPSERVE_PREFILL_ATTN_WAVES");  // 8 (default) or 4 waves per workgroup
+    const int nwv = (ew != nullptr && atoi(ew) == 4) ? 4 : 8;
+    const int HG = G >= nwv ? nwv : G;
+    const int sub = 128 / (32 * (nwv / HG));
+    dim3 g2(ntiles * sub, nkv * (G / HG));
+    auto* o2 = static_cast<unsigned short*>(out);
+    auto* q2 = static_cast<const unsigned short*>(q);
+    auto* k2 = static_cast<const unsigned short*>(k_cache);
+    auto* v2 = static_cast<const unsigned short*>(v_cache);
+#define PA2_LAUNCH(hg, nw)                                                                                  \
+  prefill_attn_v2_kernel<hg, nw><<<g2, 64 * nw, 0, s>>>(o2, out_stride, q2, q_stride, k2, v2, block_tables, \
+                                                        bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale)
+    if (nwv == 8) {
+      if (HG == 8) PA2_LAUNCH(8, 8);
+      else if (HG == 4) PA2_LAUNCH(4, 8);
+      else PA2_LAUNCH(2, 8);
+    } else {
+      if (HG == 4) PA2_LAUNCH(4, 4);
+      else PA2_LAUNCH(2, 4);
+    }
+#undef PA2_LAUNCH
+    return;
+  }
   dim3 grid(ntiles, nq), block(256);
   auto* o = static_cast<unsigned short*>(out);
   auto* qq = static_cast<const unsigned short*>(q);

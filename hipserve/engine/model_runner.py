@@ -220,7 +220,10 @@ class ModelRunner:
             cu[1:] = np.cumsum([s.num_tokens for s in so.prefill])
             cu_q = cu
             ctx_p = np.array([s.end for s in so.prefill], dtype=np.int32)
-            tl = [(i, r) for i, s in enumerate(so.prefill) for r in range(0, s.num_tokens, PREFILL_TILE)]
+            # heaviest (latest absolute position) first: the prefill attention kernel
+            # dispatches tiles in this order (longest-processing-time against the causal tail)
+            tl = sorted(((i, r) for i, s in enumerate(so.prefill) for r in range(0, s.num_tokens, PREFILL_TILE)),
+                        key=lambda t: so.prefill[t[0]].end - so.prefill[t[0]].num_tokens + t[1], reverse=True)
             tiles = np.array(tl, dtype=np.int32).reshape(-1, 2)
             bt_p = bt[:np_]
         bt_d = ctx_d = None

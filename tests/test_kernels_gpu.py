@@ -99,13 +99,20 @@ def test_paged_decode(ops, nq, nkv, D, bs, part):
     _close(out.view(B, nq, D), want, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("nq,nkv,D", [(32, 8, 128), (16, 2, 64)])
-def test_prefill_attention(ops, nq, nkv, D):
+@pytest.mark.parametrize("nq,nkv,D,bs,v1", [(32, 8, 128, 16, False), (32, 8, 128, 16, True), (64, 8, 128, 16, False),
+                                          (8, 1, 128, 32, False), (16, 8, 128, 16, False), (16, 2, 64, 16, False),
+                                          (4, 4, 128, 16, False)])
+@pytest.mark.parametrize("waves", ["4", "8"])
+def test_prefill_attention(ops, nq, nkv, D, bs, v1, waves, monkeypatch):
+    """v2 (LDS-shared K/V, GQA heads per workgroup: G = 2/4/8) and v1 (D = 64, MHA,
+    or HIPSERVE_PREFILL_ATTN_V1) against the fp32 oracle, including long prompts
+    (many 64-key tiles: the lazy rescale) and chunked prefill over a prefix."""
+    monkeypatch.setenv("HIPSERVE_PREFILL_ATTN_V1", "1" if v1 else "0")
+    monkeypatch.setenv("HIPSERVE_PREFILL_ATTN_WAVES", waves)
     torch.manual_seed(3)
-    bs = 16
-    # (ctx_len, q_len): plain prefill, tiny, chunked prefill with prefix context
-    seqs = [(1, 1), (37, 37), (200, 200), (300, 50), (129, 129)]
-    max_blocks = 32
+    # (ctx_len, q_len): plain prefill, tiny, chunked prefill with prefix context, long
+    seqs = [(1, 1), (37, 37), (200, 200), (300, 50), (129, 129), (1100, 1100), (1500, 333)]
+    max_blocks = 1536 // bs
     nblocks = len(seqs) * max_blocks
     kc, vc = _caches(nblocks, nkv, bs, D)
     bt = torch.randperm(nblocks, device=DEV).int().view(len(seqs), max_blocks).contiguous()

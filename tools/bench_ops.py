@@ -109,21 +109,26 @@ def bench_decode(ops):
 
 def bench_prefill(ops):
     D, bs = 128, 16
-    for S, nseq, nq, nkv in [(1024, 8, 32, 8), (4096, 2, 32, 8), (8192, 1, 32, 8)]:
+    for S, nseq, nq, nkv in [(1024, 8, 32, 8), (4096, 2, 32, 8), (8192, 1, 32, 8), (1024, 8, 8, 1)]:
         mb = S // bs
         kc = torch.randn(nseq * mb, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
         vc = torch.randn(nseq * mb, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
         bt = torch.arange(nseq * mb, device=DEV).int().view(nseq, mb)
         cu = torch.arange(0, (nseq + 1) * S, S, device=DEV, dtype=torch.int32)
         ctx = torch.full((nseq,), S, device=DEV, dtype=torch.int32)
-        tiles = torch.tensor([(s, r) for s in range(nseq) for r in range(0, S, 128)], device=DEV,
-                             dtype=torch.int32)
+        tiles = torch.tensor(sorted(((s, r) for s in range(nseq) for r in range(0, S, 128)), key=lambda t: -t[1]),
+                             device=DEV, dtype=torch.int32)
         q = torch.randn(nseq * S, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
         out = torch.empty(nseq * S, nq * D, device=DEV, dtype=torch.bfloat16)
-        us = timeit(lambda: ops.prefill_attention(out, q, kc, vc, bt, cu, ctx, tiles, nq, nkv,
-                                                  1 / math.sqrt(D)), n=10)
         flops = 4 * nseq * (S * S / 2) * D * nq
-        emit(op="prefill_attention", S=S, nseq=nseq, us=round(us, 1), TFLOPs=round(flops / us / 1e6, 1))
+        for ver in ("v2w4", "v2w8", "v1"):  # v1: per-wave L2 K/V reads (HIPSERVE_PREFILL_ATTN_V1=1)
+            os.environ["HIPSERVE_PREFILL_ATTN_V1"] = "1" if ver == "v1" else "0"
+            os.environ["HIPSERVE_PREFILL_ATTN_WAVES"] = "8" if ver == "v2w8" else "4"
+            us = timeit(lambda: ops.prefill_attention(out, q, kc, vc, bt, cu, ctx, tiles, nq, nkv,
+                                                      1 / math.sqrt(D)), n=10)
+            emit(op="prefill_attention", ver=ver, S=S, nseq=nseq, nq=nq, nkv=nkv, us=round(us, 1),
+                 TFLOPs=round(flops / us / 1e6, 1))
+        os.environ.pop("HIPSERVE_PREFILL_ATTN_V1", None)
 
 
 def bench_gemm(ops):
