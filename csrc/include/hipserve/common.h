@@ -94,6 +94,20 @@ HS_DEVICE u16x8 silu_mul8(const u16x8 g, const u16x8 u) {
   return o;
 }
 
+// tanh-GELU(gate) * up (Gemma GeGLU, HF "gelu_pytorch_tanh"):
+// 0.5 x (1 + tanh(y)) = x * sigmoid(2y), y = sqrt(2/pi) (x + 0.044715 x^3).
+HS_DEVICE unsigned short gelu_mul1(unsigned short g, unsigned short u) {
+  const float x = bf16_to_f32(g);
+  const float y2 = 1.5957691216057308f * (x + 0.044715f * x * x * x);
+  return f32_to_bf16(x / (1.f + __expf(-y2)) * bf16_to_f32(u));
+}
+HS_DEVICE u16x8 gelu_mul8(const u16x8 g, const u16x8 u) {
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = gelu_mul1(g[j], u[j]);
+  return o;
+}
+
 // Row-norm launch policy shared by every RMSNorm-family kernel (norm.hip,
 // decode_fused.hip) so they reduce in the same order and stay bit-identical:
 // 512 threads from 4096 columns up (more loads in flight on the 1-row-per-CU

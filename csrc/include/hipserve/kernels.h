@@ -11,9 +11,14 @@ namespace hipserve {
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                     bool weight_f32, int rows, int hidden, long x_stride,
                     long out_stride, float eps, hipStream_t s);
+// per-head q/k RMSNorm inside the qkv rows, in place (fp32 weights [D], D <= 256)
+void launch_qk_rmsnorm(void* qkv, long stride, const float* qw, const float* kw, int T, int nq, int nkv, int D,
+                       float eps, hipStream_t s);
 
 // activation.hip
 void launch_silu_and_mul(void* out, const void* in, long rows, int inter,
+                         long in_stride, long out_stride, hipStream_t s);
+void launch_gelu_and_mul(void* out, const void* in, long rows, int inter,
                          long in_stride, long out_stride, hipStream_t s);
 
 // rope_cache.hip
@@ -29,16 +34,17 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
                          const int* block_tables, int bt_stride,
                          const int* context_lens, float* tmp_out, float* tmp_ml,
                          int B, int nq, int nkv, int D, int block_size,
-                         int part_size, int max_parts, float scale,
+                         int part_size, int max_parts, float scale, int window,
                          hipStream_t s);
 
-// attention_prefill.hip
+// attention_prefill.hip — window > 0: sliding-window attention (keys within
+// window - 1 positions before the query), 0 = full causal
 void launch_prefill_attention(void* out, long out_stride, const void* q,
                               long q_stride, const void* k_cache,
                               const void* v_cache, const int* block_tables,
                               int bt_stride, const int* cu_q, const int* ctx_lens,
                               const int* tiles, int ntiles, int nq, int nkv, int D,
-                              int block_size, float scale, hipStream_t s);
+                              int block_size, float scale, int window, hipStream_t s);
 
 // sampling.hip
 // ws: fp32 workspace of sample_workspace_floats(rows, V) for the multi-CU path
@@ -101,7 +107,7 @@ void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu,
 namespace hipserve {
 // moe.hip — tile in {16, 32, 64}
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
-                             hipStream_t s);
+                             bool renorm, hipStream_t s);
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
                       int tiles_cap, int* num_tiles, int* pair_slot, hipStream_t s);
 void launch_moe_gemm(void* out, long out_stride, const void* x, long x_stride, const void* w, const int* slots,

@@ -39,13 +39,17 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int nq, int nkv, int block_size, int part_size,
-    int max_parts, float scale) {
-  static_assert(D == 128 || D == 64, "head_dim 64 or 128");
+    int max_parts, float scale, int window) {
+  static_assert(D == 128 || D == 96 || D == 64, "head_dim 64, 96 or 128");
   constexpr int KS = D / 32;  // k-steps of the QK MFMA
   constexpr int NB = D / 16;  // 16-column blocks of the PV output
   const int part = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
   const int ctx = context_lens[b];
-  const int start = part * part_size;
+  // sliding window: keys [lo, ctx); partitions start at lo rounded down to a
+  // 32-token chunk (aligned V loads), the keys below lo are masked
+  const int lo = window > 0 ? max(0, ctx - window) : 0;
+  const int lo_al = lo & ~(kChunk - 1);
+  const int start = lo_al + part * part_size;
   if (start >= ctx) return;
   const int end = min(start + part_size, ctx);
   const int G = nq / nkv;
@@ -130,8 +134,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int t0 = cs + 8 * grp + r;
-      s[r] = (t0 <= last_tok) ? sa[r] * sl2 : -1e30f;
-      s[r + 4] = (t0 + 4 <= last_tok) ? sb[r] * sl2 : -1e30f;
+      s[r] = (t0 >= lo && t0 <= last_tok) ? sa[r] * sl2 : -1e30f;
+      s[r + 4] = (t0 + 4 >= lo && t0 + 4 <= last_tok) ? sb[r] * sl2 : -1e30f;
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) mx = fmaxf(mx, s[r]);
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
     }
   __syncthreads();
 
-  const int nparts_seq = (ctx + part_size - 1) / part_size;
+  const int nparts_seq = (ctx - lo_al + part_size - 1) / part_size;
   for (int it = threadIdx.x; it < G * D; it += blockDim.x) {
     const int h = it / D, d = it % D;
     float M = -1e30f;
@@ -210,10 +214,11 @@ template <int D>
 __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
-    const int* __restrict__ context_lens, int nq, int part_size, int max_parts) {
+    const int* __restrict__ context_lens, int nq, int part_size, int max_parts, int window) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int ctx = context_lens[b];
-  const int np = (ctx + part_size - 1) / part_size;
+  const int lo_al = (window > 0 ? max(0, ctx - window) : 0) & ~(kChunk - 1);
+  const int np = (ctx - lo_al + part_size - 1) / part_size;
   if (np <= 1) return;
   const long base = ((long)b * nq + h) * max_parts;
   float M = -1e30f;
@@ -249,7 +254,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
                          const int* block_tables, int bt_stride,
                          const int* context_lens, float* tmp_out, float* tmp_ml,
                          int B, int nq, int nkv, int D, int block_size,
-                         int part_size, int max_parts, float scale,
+                         int part_size, int max_parts, float scale, int window,
                          hipStream_t s) {
   if (B <= 0) return;
   const int waves = decode_waves();
@@ -262,18 +267,20 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
 #define HS_DECODE(DD, WW)                                                                                   \
   paged_decode_kernel<DD, WW><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables,    \
                                                        bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv,     \
-                                                       block_size, part_size, max_parts, scale)
-  if (D == 128) {
-    if (waves == 8) HS_DECODE(128, 8);
-    else HS_DECODE(128, 4);
-    if (max_parts > 1)
-      paged_decode_reduce_kernel<128><<<dim3(nq, B), dim3(128), 0, s>>>(o, out_stride, tmp_out, tmp_ml, context_lens, nq, part_size, max_parts);
-  } else {
-    if (waves == 8) HS_DECODE(64, 8);
-    else HS_DECODE(64, 4);
-    if (max_parts > 1)
-      paged_decode_reduce_kernel<64><<<dim3(nq, B), dim3(64), 0, s>>>(o, out_stride, tmp_out, tmp_ml, context_lens, nq, part_size, max_parts);
-  }
+                                                       block_size, part_size, max_parts, scale, window)
+#define HS_DECODE_D(DD)                                                                                      \
+  do {                                                                                                      \
+    if (waves == 8) HS_DECODE(DD, 8);                                                                       \
+    else HS_DECODE(DD, 4);                                                                                  \
+    if (max_parts > 1)                                                                                      \
+      paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,        \
+                                                                       context_lens, nq, part_size, max_parts, \
+                                                                       window);                             \
+  } while (0)
+  if (D == 128) HS_DECODE_D(128);
+  else if (D == 96) HS_DECODE_D(96);
+  else HS_DECODE_D(64);
+#undef HS_DECODE_D
 #undef HS_DECODE
 }
 

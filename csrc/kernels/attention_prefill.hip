@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ tiles, int nq, int nkv, int block_size,
-    float scale) {
+    float scale, int window) {
   constexpr int KS = D / 16;   // k-steps of QK (K = 16 per MFMA)
   constexpr int NB = D / 32;   // 32-row d blocks of O^T
   const int seq = tiles[2 * blockIdx.x], r0 = tiles[2 * blockIdx.x + 1];
@@ -68,7 +68,9 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   float m_run = -1e30f, l_run = 0.f;
 
   const int nkt = max_key / 32 + 1;
-  for (int kt = 0; kt < nkt; ++kt) {
+  // sliding window: the wave's first row sees keys >= its pos - window + 1
+  const int kt0 = window > 0 ? max(0, ctx - qlen + wrow0 - window + 1) / 32 : 0;
+  for (int kt = kt0; kt < nkt; ++kt) {
     const int kbase = kt * 32;
     // K fragment rows: key kbase + qi (clamped into the valid context)
     const int key = min(kbase + qi, ctx - 1);
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int kk = kbase + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const float v = (kk <= pos) ? st[r] * sl2 : -1e30f;
+      const float v = (kk <= pos && (window <= 0 || kk > pos - window)) ? st[r] * sl2 : -INFINITY;
       st[r] = v;
       mx = fmaxf(mx, v);
     }
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     const unsigned short* __restrict__ k_cache, const unsigned short* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ cu_q,
     const int* __restrict__ ctx_lens, const int* __restrict__ tiles, int nq, int nkv, int block_size,
-    float scale) {
+    float scale, int window) {
   constexpr int D = 128, KS = 8, NB = 4;
   constexpr int RB = NWV / HG, QR = 32 * RB, SUB = 128 / QR;
   constexpr int NT = 64 * NWV, NP = 1024 / NT;  // threads; K (and V^T) 16-byte pieces per thread
@@ -216,6 +218,9 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
   const int wmax_key = ctx - qlen + min(wrow0 + 31, qlen - 1);
   const int wmin_pos = ctx - qlen + wrow0;
   const int nkt = (ctx - qlen + min(r0 + QR - 1, qlen - 1)) / PA2_KT + 1;
+  // sliding window: rows see keys [pos - window + 1, pos]; the workgroup starts at
+  // the tile holding its first row's lowest key
+  const int kt0 = window > 0 ? max(0, ctx - qlen + r0 - window + 1) / PA2_KT : 0;
   const int* btab = block_tables + (long)seq * bt_stride;
   const long hstride = (long)block_size * D;
 
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
 
   auto compute = [&](int kt, int buf) {
     const int kbase = kt * PA2_KT;
-    if (wactive && kbase <= wmax_key) {
+    if (wactive && kbase <= wmax_key && (window <= 0 || kbase + PA2_KT - 1 > wmin_pos - window)) {
       const unsigned short* kb = &kl[buf][qi * PA2_KLD + 8 * half];
       f32x16 st[2];
 #pragma unroll
@@ -281,13 +286,14 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
           const u16x8 a = *reinterpret_cast<const u16x8*>(kb + (32 * h2) * PA2_KLD + 16 * ks);
           st[h2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], st[h2], 0, 0, 0);
         }
-      if (kbase + PA2_KT - 1 > wmin_pos) {  // diagonal tile: causal mask
+      // diagonal tile (causal mask) or a tile crossing some row's window start
+      if (kbase + PA2_KT - 1 > wmin_pos || (window > 0 && kbase <= wmax_key - window)) {
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = kbase + 32 * h2 + 16 * (r >> 3) + 8 * half + 4 * ((r >> 2) & 1) + (r & 3);
-            if (key > pos) st[h2][r] = -1e30f;
+            if (key > pos || (window > 0 && key <= pos - window)) st[h2][r] = -INFINITY;
           }
       }
       float mx = -1e30f;
@@ -330,18 +336,18 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     }
   };
 
-  stage_load(ska, sva, 0);
-  if (nkt > 1) stage_load(skb, svb, 1);
+  stage_load(ska, sva, kt0);
+  if (kt0 + 1 < nkt) stage_load(skb, svb, kt0 + 1);
   stage_store(ska, sva, 0);
   __syncthreads();
-  for (int kt = 0; kt < nkt; kt += 2) {
-    // even tile kt in LDS buffer 0; set b holds tile kt+1
+  for (int kt = kt0; kt < nkt; kt += 2) {
+    // tile kt in LDS buffer 0; set b holds tile kt+1
     if (kt + 2 < nkt) stage_load(ska, sva, kt + 2);
     compute(kt, 0);
     if (kt + 1 < nkt) stage_store(skb, svb, 1);
     __syncthreads();
     if (kt + 1 >= nkt) break;
-    // odd tile kt+1 in buffer 1; set a holds tile kt+2
+    // tile kt+1 in buffer 1; set a holds tile kt+2
     if (kt + 3 < nkt) stage_load(skb, svb, kt + 3);
     compute(kt + 1, 1);
     if (kt + 2 < nkt) stage_store(ska, sva, 0);
@@ -369,7 +375,7 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               const void* v_cache, const int* block_tables,
                               int bt_stride, const int* cu_q, const int* ctx_lens,
                               const int* tiles, int ntiles, int nq, int nkv, int D,
-                              int block_size, float scale, hipStream_t s) {
+                              int block_size, float scale, int window, hipStream_t s) {
   if (ntiles <= 0) return;
   const int G = nq / nkv;
   if (D == 128 && block_size % 16 == 0 && G >= 2 && (G & (G - 1)) == 0 && !getenv_flag("HIPSERVE_PREFILL_ATTN_V1")) {
@@ -384,7 +390,8 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
     auto* v2 = static_cast<const unsigned short*>(v_cache);
 #define PA2_LAUNCH(hg, nw)                                                                                  \
   prefill_attn_v2_kernel<hg, nw><<<g2, 64 * nw, 0, s>>>(o2, out_stride, q2, q_stride, k2, v2, block_tables, \
-                                                        bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale)
+                                                        bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale, \
+                                                        window)
     if (nwv == 8) {
       if (HG == 8) PA2_LAUNCH(8, 8);
       else if (HG == 4) PA2_LAUNCH(4, 8);
@@ -401,10 +408,13 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
   auto* qq = static_cast<const unsigned short*>(q);
   auto* kc = static_cast<const unsigned short*>(k_cache);
   auto* vc = static_cast<const unsigned short*>(v_cache);
-  if (D == 128)
-    prefill_attn_kernel<128><<<grid, block, 0, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale);
-  else
-    prefill_attn_kernel<64><<<grid, block, 0, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale);
+#define PA1_LAUNCH(dd)                                                                                          \
+  prefill_attn_kernel<dd><<<grid, block, 0, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, cu_q, \
+                                                 ctx_lens, tiles, nq, nkv, block_size, scale, window)
+  if (D == 128) PA1_LAUNCH(128);
+  else if (D == 96) PA1_LAUNCH(96);
+  else PA1_LAUNCH(64);
+#undef PA1_LAUNCH
 }
 
 }  // namespace hipserve

@@ -22,36 +22,57 @@ HS_DEVICE float ld_f<unsigned short>(const unsigned short* p, long i) { return b
 template <>
 HS_DEVICE float ld_f<float>(const float* p, long i) { return p[i]; }
 
+// One wave per token, expert e on lane e % 64, slot e / 64 (E <= 128). renorm:
+// weights / sum over the selected k (Mixtral, Qwen3-MoE norm_topk_prob); else the
+// plain softmax probabilities of the selected experts.
 template <typename T>
 __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restrict__ logits, float* __restrict__ w,
-                                                               int* __restrict__ ids, int Tn, int E, int k) {
+                                                               int* __restrict__ ids, int Tn, int E, int k,
+                                                               int renorm) {
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= Tn) return;
-  float v = lane < E ? ld_f<T>(logits, (long)t * E + lane) : -INFINITY;
-  const float mx = wave_max(v);
-  const float e = lane < E ? __expf(v - mx) : 0.f;
-  const float s = wave_sum(e);
-  float p = e / s;
+  float v[2], p[2];
+  int rank[2] = {-1, -1};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int e = lane + 64 * s;
+    v[s] = e < E ? ld_f<T>(logits, (long)t * E + e) : -INFINITY;
+  }
+  const float mx = wave_max(fmaxf(v[0], v[1]));
+  float ex[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) ex[s] = (lane + 64 * s) < E ? __expf(v[s] - mx) : 0.f;
+  const float sum = wave_sum(ex[0] + ex[1]);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) p[s] = ex[s] / sum;
   float sel_sum = 0.f;
-  float mine = 0.f;
-  int rank = -1;
   for (int j = 0; j < k; ++j) {
-    // argmax over lanes (ties -> lower expert id)
-    float bv = (rank < 0 && lane < E) ? p : -1.f;
-    int bi = lane;
+    // argmax over (lane, slot) (ties -> lower expert id)
+    float bv = -1.f;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int e = lane + 64 * s;
+      if (rank[s] < 0 && e < E && (p[s] > bv || (p[s] == bv && e < bi))) { bv = p[s]; bi = e; }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const float v2 = __shfl_xor(bv, o, 64);
       const int i2 = __shfl_xor(bi, o, 64);
       if (v2 > bv || (v2 == bv && i2 < bi)) { bv = v2; bi = i2; }
     }
-    if (lane == bi) { rank = j; mine = p; }
+    if (bi == lane) rank[0] = j;
+    if (bi == lane + 64) rank[1] = j;
     sel_sum += bv;
   }
-  if (rank >= 0) {
-    w[(long)t * k + rank] = mine / sel_sum;
-    ids[(long)t * k + rank] = lane;
+  const float norm = renorm ? 1.f / sel_sum : 1.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (rank[s] >= 0) {
+      w[(long)t * k + rank[s]] = p[s] * norm;
+      ids[(long)t * k + rank[s]] = lane + 64 * s;
+    }
   }
 }
 
@@ -59,9 +80,9 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
                                                          int* __restrict__ slots, int slots_cap,
                                                          int* __restrict__ tile_expert, int tiles_cap,
                                                          int* __restrict__ num_tiles, int* __restrict__ pair_slot) {
-  __shared__ int cnt[64], off[65], cur[64];
+  __shared__ int cnt[128], off[129], cur[128];
   const int tid = threadIdx.x;
-  if (tid < 64) { cnt[tid] = 0; cur[tid] = 0; }
+  if (tid < 128) { cnt[tid] = 0; cur[tid] = 0; }
   __syncthreads();
   for (int p = tid; p < npairs; p += 1024) atomicAdd(&cnt[ids[p]], 1);
   __syncthreads();
@@ -202,14 +223,15 @@ __global__ __launch_bounds__(256) void moe_combine_partial_kernel(unsigned short
 }
 
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
-                             hipStream_t s) {
+                             bool renorm, hipStream_t s) {
   if (T <= 0) return;
   dim3 grid((T + 3) / 4), block(256);
   if (logits_f32)
-    moe_topk_softmax_kernel<float><<<grid, block, 0, s>>>(static_cast<const float*>(logits), w, ids, T, E, k);
+    moe_topk_softmax_kernel<float><<<grid, block, 0, s>>>(static_cast<const float*>(logits), w, ids, T, E, k,
+                                                          renorm ? 1 : 0);
   else
     moe_topk_softmax_kernel<unsigned short><<<grid, block, 0, s>>>(static_cast<const unsigned short*>(logits), w, ids,
-                                                                   T, E, k);
+                                                                   T, E, k, renorm ? 1 : 0);
 }
 
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,

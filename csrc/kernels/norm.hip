@@ -93,6 +93,46 @@ static void launch_rmsnorm_t(unsigned short* out, unsigned short* residual,
   }
 }
 
+// Per-head RMSNorm of the q and k heads inside the merged qkv rows, in place
+// (Qwen3 / Gemma-3 q_norm, k_norm; applied before RoPE). One wave per
+// (token, head), D <= 256 on 4 elements per lane; fp32 weights [D] (Gemma's
+// 1 + w folded in at load).
+__global__ __launch_bounds__(256) void qk_rmsnorm_kernel(unsigned short* __restrict__ qkv, long stride,
+                                                         const float* __restrict__ qw,
+                                                         const float* __restrict__ kw, int T, int nq, int nkv,
+                                                         int D, float eps) {
+  const int nh = nq + nkv;
+  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= (long)T * nh) return;
+  const int t = (int)(item / nh), h = (int)(item % nh);
+  const int lane = threadIdx.x & 63;
+  unsigned short* p = qkv + (long)t * stride + (long)h * D;
+  const float* w = h < nq ? qw : kw;
+  float v[4];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = lane + 64 * i;
+    v[i] = d < D ? bf16_to_f32(p[d]) : 0.f;
+    ss += v[i] * v[i];
+  }
+  ss = wave_sum(ss);
+  const float inv = rsqrtf(ss / D + eps);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = lane + 64 * i;
+    if (d < D) p[d] = f32_to_bf16(v[i] * inv * w[d]);
+  }
+}
+
+void launch_qk_rmsnorm(void* qkv, long stride, const float* qw, const float* kw, int T, int nq, int nkv, int D,
+                       float eps, hipStream_t s) {
+  const long items = (long)T * (nq + nkv);
+  if (items <= 0) return;
+  qk_rmsnorm_kernel<<<dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s>>>(static_cast<unsigned short*>(qkv), stride,
+                                                                           qw, kw, T, nq, nkv, D, eps);
+}
+
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                     bool weight_f32, int rows, int hidden, long x_stride,
                     long out_stride, float eps, hipStream_t s) {

@@ -78,10 +78,11 @@ void rope_cache(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& 
 void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
                   const at::Tensor& v_cache, const at::Tensor& block_tables,
                   const at::Tensor& context_lens, at::Tensor& tmp_out, at::Tensor& tmp_ml,
-                  int64_t nq, int64_t nkv, int64_t part_size, double scale) {
+                  int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_ROWMAJOR(q); CHECK_ROWMAJOR(out);
   const int D = k_cache.size(3), bs = k_cache.size(2);
-  TORCH_CHECK(D == 64 || D == 128, "paged_decode: head_dim 64/128");
+  TORCH_CHECK(D == 64 || D == 96 || D == 128, "paged_decode: head_dim 64/96/128");
+  TORCH_CHECK(window >= 0, "paged_decode: window >= 0");
   TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "paged_decode: GQA group <= 16");
   TORCH_CHECK(bs % 16 == 0, "block_size multiple of 16");
   TORCH_CHECK(part_size % 128 == 0 && part_size / bs < 255);
@@ -100,16 +101,17 @@ void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cach
                                 block_tables.data_ptr<int>(), block_tables.stride(0),
                                 context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
                                 tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size,
-                                max_parts, (float)scale, cur_stream());
+                                max_parts, (float)scale, (int)window, cur_stream());
 }
 
 void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
                        const at::Tensor& v_cache, const at::Tensor& block_tables,
                        const at::Tensor& cu_q, const at::Tensor& ctx_lens,
-                       const at::Tensor& tiles, int64_t nq, int64_t nkv, double scale) {
+                       const at::Tensor& tiles, int64_t nq, int64_t nkv, double scale, int64_t window) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_ROWMAJOR(q); CHECK_ROWMAJOR(out);
   const int D = k_cache.size(3), bs = k_cache.size(2);
-  TORCH_CHECK(D == 64 || D == 128, "prefill_attention: head_dim 64/128");
+  TORCH_CHECK(D == 64 || D == 96 || D == 128, "prefill_attention: head_dim 64/96/128");
+  TORCH_CHECK(window >= 0, "prefill_attention: window >= 0");
   TORCH_CHECK(bs % 16 == 0 && nq % nkv == 0);
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && cu_q.scalar_type() == at::kInt &&
               ctx_lens.scalar_type() == at::kInt && tiles.scalar_type() == at::kInt);
@@ -120,7 +122,29 @@ void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k
                                      block_tables.data_ptr<int>(), block_tables.stride(0),
                                      cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(),
                                      tiles.data_ptr<int>(), tiles.size(0), nq, nkv, D, bs,
-                                     (float)scale, cur_stream());
+                                     (float)scale, (int)window, cur_stream());
+}
+
+// Per-head RMSNorm of q and k inside the merged qkv rows, in place (Qwen3 / Gemma-3).
+void qk_rmsnorm(at::Tensor& qkv, const at::Tensor& q_w, const at::Tensor& k_w, int64_t nq, int64_t nkv,
+                int64_t head_dim, double eps) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_ROWMAJOR(qkv);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= (nq + nkv) * head_dim && head_dim <= 256);
+  TORCH_CHECK(q_w.scalar_type() == at::kFloat && k_w.scalar_type() == at::kFloat && q_w.is_contiguous() &&
+              k_w.is_contiguous() && q_w.numel() == head_dim && k_w.numel() == head_dim,
+              "qk_rmsnorm: fp32 [head_dim] weights");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  hipserve::launch_qk_rmsnorm(qkv.data_ptr(), qkv.stride(0), q_w.data_ptr<float>(), k_w.data_ptr<float>(),
+                              qkv.size(0), nq, nkv, head_dim, (float)eps, cur_stream());
+}
+
+void gelu_and_mul(at::Tensor& out, const at::Tensor& x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0));
+  TORCH_CHECK(out.size(1) % 8 == 0);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_gelu_and_mul(out.data_ptr(), x.data_ptr(), x.size(0), out.size(1), x.stride(0), out.stride(0),
+                                cur_stream());
 }
 
 void sample(at::Tensor& out_tok, at::Tensor& out_lp, const at::Tensor& logits,
@@ -196,16 +220,16 @@ void skinny_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int6
               "skinny_gemm: unsupported (rt, kw)");
 }
 
-void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, int64_t k) {
+void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, int64_t k, bool renorm) {
   CHECK_DEV(logits); CHECK_CONTIG(logits); CHECK_CONTIG(w); CHECK_CONTIG(ids);
-  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 64, "moe: <= 64 experts");
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 128, "moe: <= 128 experts");
   TORCH_CHECK(w.scalar_type() == at::kFloat && ids.scalar_type() == at::kInt);
   TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16);
   const int T = logits.size(0);
   TORCH_CHECK(w.numel() >= T * k && ids.numel() >= T * k && k >= 1 && k <= logits.size(1));
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   hipserve::launch_moe_topk_softmax(logits.data_ptr(), logits.scalar_type() == at::kFloat, w.data_ptr<float>(),
-                                    ids.data_ptr<int>(), T, logits.size(1), k, cur_stream());
+                                    ids.data_ptr<int>(), T, logits.size(1), k, renorm, cur_stream());
 }
 
 int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes) {
@@ -382,7 +406,7 @@ void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots
   CHECK_DEV(ids);
   TORCH_CHECK(ids.scalar_type() == at::kInt && slots.scalar_type() == at::kInt &&
               tile_expert.scalar_type() == at::kInt && pair_slot.scalar_type() == at::kInt);
-  TORCH_CHECK(E <= 64 && (tile == 16 || tile == 32 || tile == 64));
+  TORCH_CHECK(E <= 128 && (tile == 16 || tile == 32 || tile == 64));
   const int npairs = ids.numel();
   TORCH_CHECK(slots.numel() >= npairs + E * (tile - 1) && slots.numel() % tile == 0,
               "slots capacity must cover padding and be a multiple of the tile");
@@ -473,7 +497,7 @@ void moe_combine_partial(at::Tensor& out, const at::Tensor& ws, const at::Tensor
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
-  m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k) -> ()");
+  m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k, bool renorm=True) -> ()");
   m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot) -> ()");
   m.def("moe_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor w, Tensor pair_slot, int k) -> ()");
@@ -483,8 +507,10 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
-  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale) -> ()");
-  m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale) -> ()");
+  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale, int window=0) -> ()");
+  m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale, int window=0) -> ()");
+  m.def("qk_rmsnorm(Tensor(a!) qkv, Tensor q_w, Tensor k_w, int nq, int nkv, int head_dim, float eps) -> ()");
+  m.def("gelu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
   // custom all-reduce control ops carry an opaque state handle: catch-all kernels
@@ -510,6 +536,8 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("rmsnorm", &rmsnorm);
   m.impl("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.impl("silu_and_mul", &silu_and_mul);
+  m.impl("gelu_and_mul", &gelu_and_mul);
+  m.impl("qk_rmsnorm", &qk_rmsnorm);
   m.impl("rope_cache", &rope_cache);
   m.impl("paged_decode", &paged_decode);
   m.impl("prefill_attention", &prefill_attention);

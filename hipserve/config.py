@@ -38,6 +38,28 @@ class ModelConfig:
     num_experts_per_tok: int = 0
     bos_token_id: int | None = 128000
     eos_token_id: tuple = (128001, 128009)
+    # ---- family options (Qwen2/Qwen3/Qwen3-MoE/Gemma-3/Phi-3; defaults = Llama/Mixtral)
+    family: str = "llama"                 # llama | mixtral | qwen2 | qwen3 | qwen3_moe | gemma3 | phi3
+    qkv_bias: bool = False                # Qwen2: q/k/v projections carry a bias
+    qk_norm: bool = False                 # Qwen3 / Gemma-3: per-head RMSNorm of q and k before RoPE
+    moe_intermediate_size: int = 0        # expert width when it differs from intermediate_size (Qwen3-MoE)
+    norm_topk_prob: bool = True           # renormalise the top-k routing weights (Mixtral: always)
+    hidden_act: str = "silu"              # silu | gelu_tanh (Gemma GeGLU)
+    sandwich_norm: bool = False           # Gemma-3: RMSNorm on the attention / MLP outputs too
+    norm_offset: bool = False             # Gemma RMSNorm: x * (1 + w)
+    embed_scale: float = 1.0              # Gemma: embeddings * sqrt(hidden)
+    attn_scale: float = 0.0               # softmax scale (0 = 1/sqrt(head_dim)); Gemma: query_pre_attn_scalar^-0.5
+    sliding_window: int = 0               # window of the sliding-attention layers (0 = none)
+    layer_windows: tuple = ()             # per-layer window (0 = full attention); empty = all full
+    rope_local_theta: float = 0.0         # RoPE base of the sliding layers (Gemma-3: 10000; 0 = rope_theta)
+    partial_rotary_factor: float = 1.0
+
+    @property
+    def expert_size(self):
+        return self.moe_intermediate_size or self.intermediate_size
+
+    def window_of(self, layer: int) -> int:
+        return self.layer_windows[layer] if self.layer_windows else 0
 
     @property
     def q_size(self):
@@ -50,41 +72,139 @@ class ModelConfig:
     def num_params(self) -> int:
         H, I, V, L = self.hidden_size, self.intermediate_size, self.vocab_size, self.num_layers
         attn = H * (self.q_size + 2 * self.kv_size) + self.q_size * H
-        mlp = 3 * H * I * max(1, self.num_experts) + (H * self.num_experts if self.num_experts else 0)
+        if self.num_experts:
+            mlp = 3 * H * self.expert_size * self.num_experts + H * self.num_experts
+        else:
+            mlp = 3 * H * I
         emb = V * H * (1 if self.tie_word_embeddings else 2)
         return L * (attn + mlp + 2 * H) + emb + H
 
     @staticmethod
     def from_hf_dict(d: dict, name: str = "model") -> "ModelConfig":
+        """HF ``config.json`` -> ModelConfig for the served families. Multimodal
+        wrappers (Gemma3ForConditionalGeneration, Qwen3-VL-MoE) contribute their
+        ``text_config`` (the language model; vision towers are not served). Both the
+        Hub's ``rope_theta``/``rope_scaling`` keys and the newer ``rope_parameters``
+        form (per layer type for Gemma-3) are read."""
         arch = (d.get("architectures") or ["LlamaForCausalLM"])[0]
-        family = "mixtral" if "Mixtral" in arch or d.get("num_local_experts") else "llama"
+        mtype = d.get("model_type", "")
+        if isinstance(d.get("text_config"), dict):  # multimodal wrapper: serve the text model
+            td = dict(d["text_config"])
+            for k in ("eos_token_id", "bos_token_id", "tie_word_embeddings"):
+                if k not in td and k in d:
+                    td[k] = d[k]
+            d = td
+            mtype = d.get("model_type", mtype)
+        family = _family_of(arch, mtype, d)
         nh = d["num_attention_heads"]
         H = d["hidden_size"]
+        D = d.get("head_dim") or H // nh
         eos = d.get("eos_token_id", 2)
         eos = tuple(eos) if isinstance(eos, (list, tuple)) else (eos,)
-        return ModelConfig(
+        L = d["num_hidden_layers"]
+        theta, scaling = _rope_params(d, "full_attention" if family == "gemma3" else None)
+        kw = dict(
             name=name,
-            architecture=family,
+            architecture="mixtral" if family in ("mixtral", "qwen3_moe") else "llama",
+            family=family,
             hidden_size=H,
-            num_layers=d["num_hidden_layers"],
+            num_layers=L,
             num_heads=nh,
-            num_kv_heads=d.get("num_key_value_heads", nh),
-            head_dim=d.get("head_dim") or H // nh,
+            num_kv_heads=d.get("num_key_value_heads") or nh,
+            head_dim=D,
             intermediate_size=d["intermediate_size"],
             vocab_size=d["vocab_size"],
             rms_norm_eps=d.get("rms_norm_eps", 1e-5),
-            rope_theta=d.get("rope_theta", 10000.0),
-            rope_scaling=d.get("rope_scaling"),
+            rope_theta=theta,
+            rope_scaling=scaling,
             max_position_embeddings=d.get("max_position_embeddings", 4096),
-            tie_word_embeddings=d.get("tie_word_embeddings", False),
-            num_experts=d.get("num_local_experts", 0) or 0,
-            num_experts_per_tok=d.get("num_experts_per_tok", 0) or 0,
+            tie_word_embeddings=d.get("tie_word_embeddings", family == "gemma3"),
             bos_token_id=d.get("bos_token_id"),
             eos_token_id=eos,
+            partial_rotary_factor=float(d.get("partial_rotary_factor", 1.0) or 1.0),
         )
+        if kw["partial_rotary_factor"] != 1.0:
+            raise NotImplementedError("partial rotary embeddings are not supported")
+        if family == "mixtral":
+            kw.update(num_experts=d.get("num_local_experts", 0) or 0,
+                      num_experts_per_tok=d.get("num_experts_per_tok", 0) or 0)
+        elif family == "qwen2":
+            kw.update(qkv_bias=True)
+        elif family == "qwen3":
+            kw.update(qk_norm=True, qkv_bias=bool(d.get("attention_bias", False)))
+        elif family == "qwen3_moe":
+            if d.get("decoder_sparse_step", 1) != 1 or d.get("mlp_only_layers"):
+                raise NotImplementedError("Qwen3-MoE with dense layers (decoder_sparse_step / mlp_only_layers)")
+            kw.update(qk_norm=True, qkv_bias=bool(d.get("attention_bias", False)),
+                      num_experts=d.get("num_experts") or d["num_local_experts"],
+                      num_experts_per_tok=d["num_experts_per_tok"],
+                      moe_intermediate_size=d["moe_intermediate_size"],
+                      norm_topk_prob=bool(d.get("norm_topk_prob", False)))
+        elif family == "gemma3":
+            if d.get("final_logit_softcapping") or d.get("attn_logit_softcapping"):
+                raise NotImplementedError("logit soft-capping (Gemma-2) is not supported")
+            types = d.get("layer_types")
+            if not types:
+                pat = d.get("sliding_window_pattern", 6)
+                types = ["sliding_attention" if (i + 1) % pat else "full_attention" for i in range(L)]
+            win = int(d.get("sliding_window") or 0)
+            local_theta, _ = _rope_params(d, "sliding_attention")
+            kw.update(qk_norm=True, hidden_act="gelu_tanh", sandwich_norm=True, norm_offset=True,
+                      embed_scale=float(H) ** 0.5,
+                      attn_scale=float(d.get("query_pre_attn_scalar") or D) ** -0.5,
+                      sliding_window=win,
+                      layer_windows=tuple(win if t == "sliding_attention" else 0 for t in types),
+                      rope_local_theta=local_theta)
+        return ModelConfig(**kw)
 
     def replace(self, **kw) -> "ModelConfig":
         return dataclasses.replace(self, **kw)
+
+
+def _family_of(arch: str, mtype: str, d: dict) -> str:
+    a, t = arch.lower(), (mtype or "").lower()
+    if t.startswith("qwen3_moe") or t.startswith("qwen3_vl_moe") or "qwen3moe" in a or "qwen3vlmoe" in a:
+        return "qwen3_moe"
+    if t.startswith("qwen3") or a.startswith("qwen3"):
+        return "qwen3"
+    if t.startswith("qwen2") or a.startswith("qwen2"):
+        return "qwen2"
+    if t.startswith("gemma3") or a.startswith("gemma3"):
+        return "gemma3"
+    if t == "phi3" or a.startswith("phi3"):
+        return "phi3"
+    if t == "mixtral" or "mixtral" in a or d.get("num_local_experts"):
+        return "mixtral"
+    if t in ("llama", "mistral", "") or "llama" in a or "mistral" in a:
+        return "llama"
+    raise NotImplementedError(f"unsupported architecture {arch!r} (model_type {mtype!r})")
+
+
+_ROPE_TYPES = (None, "default", "llama3", "linear")
+
+
+def _rope_params(d: dict, layer_type: str | None) -> tuple[float, dict | None]:
+    """(theta, scaling) from the Hub keys (``rope_theta``, ``rope_scaling``,
+    Gemma-3 ``rope_local_base_freq``) or the ``rope_parameters`` form (one dict,
+    or one per layer type)."""
+    rp = d.get("rope_parameters")
+    if isinstance(rp, dict) and ("full_attention" in rp or "sliding_attention" in rp):
+        rp = rp.get(layer_type or "full_attention")
+    local = layer_type == "sliding_attention"
+    if isinstance(rp, dict) and "rope_theta" in rp:
+        theta = float(rp["rope_theta"])
+        scaling = {k: v for k, v in rp.items() if k != "rope_theta"}
+    elif local:  # Hub Gemma-3: local layers run plain RoPE on rope_local_base_freq
+        theta, scaling = float(d.get("rope_local_base_freq", 10000.0)), None
+    else:
+        theta, scaling = float(d.get("rope_theta", 10000.0)), d.get("rope_scaling")
+    if scaling is not None:
+        typ = scaling.get("rope_type", scaling.get("type"))
+        if typ not in _ROPE_TYPES:
+            raise NotImplementedError(f"RoPE scaling {typ!r} is not supported ({', '.join(map(str, _ROPE_TYPES[1:]))})")
+        if typ in (None, "default"):
+            scaling = None
+    return theta, scaling
 
 
 _LLAMA3_SCALING = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
@@ -112,6 +232,32 @@ PRESETS: dict[str, ModelConfig] = {
                                   num_heads=32, num_kv_heads=4, head_dim=64,
                                   intermediate_size=5632, vocab_size=32000, rope_theta=10000.0,
                                   max_position_embeddings=2048, bos_token_id=1, eos_token_id=(2,)),
+    # the reference chart's default model families (vllm-models/helm-chart/values.yaml:1-19,
+    # ramalama-models/helm-chart/values.yaml:3-19), text models, public hyper-parameters
+    "qwen3-0.6b": ModelConfig(name="qwen3-0.6b", family="qwen3", hidden_size=1024, num_layers=28,
+                              num_heads=16, num_kv_heads=8, head_dim=128, intermediate_size=3072,
+                              vocab_size=151936, rms_norm_eps=1e-6, rope_theta=1e6,
+                              max_position_embeddings=40960, tie_word_embeddings=True, qk_norm=True,
+                              bos_token_id=None, eos_token_id=(151643, 151645)),
+    "qwen3-30b-a3b": ModelConfig(name="qwen3-30b-a3b", architecture="mixtral", family="qwen3_moe",
+                                 hidden_size=2048, num_layers=48, num_heads=32, num_kv_heads=4, head_dim=128,
+                                 intermediate_size=6144, moe_intermediate_size=768, num_experts=128,
+                                 num_experts_per_tok=8, norm_topk_prob=True, vocab_size=151936,
+                                 rms_norm_eps=1e-6, rope_theta=1e6, max_position_embeddings=40960,
+                                 qk_norm=True, bos_token_id=None, eos_token_id=(151643, 151645)),
+    "gemma-3-27b": ModelConfig(name="gemma-3-27b", family="gemma3", hidden_size=5376, num_layers=62,
+                               num_heads=32, num_kv_heads=16, head_dim=128, intermediate_size=21504,
+                               vocab_size=262208, rms_norm_eps=1e-6, rope_theta=1e6,
+                               rope_scaling={"rope_type": "linear", "factor": 8.0},
+                               max_position_embeddings=131072, tie_word_embeddings=True, qk_norm=True,
+                               hidden_act="gelu_tanh", sandwich_norm=True, norm_offset=True,
+                               embed_scale=5376 ** 0.5, attn_scale=168 ** -0.5, sliding_window=1024,
+                               layer_windows=tuple(1024 if (i + 1) % 6 else 0 for i in range(62)),
+                               rope_local_theta=1e4, bos_token_id=2, eos_token_id=(1, 106)),
+    "phi-3-mini": ModelConfig(name="phi-3-mini", family="phi3", hidden_size=3072, num_layers=32,
+                              num_heads=32, num_kv_heads=32, head_dim=96, intermediate_size=8192,
+                              vocab_size=32064, rope_theta=10000.0, max_position_embeddings=4096,
+                              bos_token_id=1, eos_token_id=(32000, 32007)),
     # tiny shapes for CPU plumbing tests
     "tiny-llama": ModelConfig(name="tiny-llama", hidden_size=128, num_layers=2, num_heads=4,
                               num_kv_heads=2, head_dim=32, intermediate_size=256, vocab_size=512,

@@ -1,5 +1,10 @@
-"""Llama-family decoder (Llama-2/3, TinyLlama, Mistral-style GQA) and Mixtral MoE,
-written against the hipserve op set (SURVEY §3.F hot loop).
+"""Decoder-only transformer families on the hipserve op set (SURVEY §3.F hot loop):
+Llama-2/3, TinyLlama, Mistral-style GQA, Mixtral MoE, Qwen2 (qkv bias), Qwen3
+(per-head q/k RMSNorm), Qwen3-MoE (128 experts, top-8), Gemma-3 text (GeGLU,
+sandwich norms, embedding scale, interleaved sliding-window / global layers with
+their own RoPE bases) and Phi-3 — one parameterised model, the family switches
+are ``ModelConfig`` fields (the reference's chart defaults are Gemma-3, Qwen3-VL-MoE
+and Qwen3: vllm-models/helm-chart/values.yaml:1-19).
 
 Per layer: fused add+RMSNorm -> merged QKV GEMM (hipBLASLt) -> fused RoPE +
 paged-cache write -> paged attention (prefill and/or decode kernels) -> o_proj GEMM
@@ -67,6 +72,12 @@ class LayerWeights:
     w2: torch.Tensor | None = None           # [E, H, I/TP]
     moe_packed: tuple | None = None          # (w13 gate/up-interleaved, w2) packed per expert for decode
     quant: dict = field(default_factory=dict)  # GGUF-quantized GEMM weights by name
+    # family extras (Qwen2 bias, Qwen3/Gemma-3 per-head q/k norms, Gemma-3 sandwich norms)
+    bqkv: torch.Tensor | None = None         # [(nq + 2 nkv) * D / TP]
+    q_norm: torch.Tensor | None = None       # [D] fp32
+    k_norm: torch.Tensor | None = None       # [D] fp32
+    post_attn_norm: torch.Tensor | None = None
+    post_ff_norm: torch.Tensor | None = None
 
 
 def shard_sizes(cfg: ModelConfig, tp: int):
@@ -78,8 +89,9 @@ def shard_sizes(cfg: ModelConfig, tp: int):
     else:
         assert tp % cfg.num_kv_heads == 0
         nkv = 1  # kv heads replicated across ranks
-    assert cfg.intermediate_size % tp == 0
-    inter = cfg.intermediate_size // tp
+    I = cfg.expert_size if cfg.num_experts else cfg.intermediate_size
+    assert I % tp == 0
+    inter = I // tp
     vpad = (cfg.vocab_size + tp - 1) // tp
     return nq, nkv, inter, vpad
 
@@ -94,13 +106,19 @@ class LlamaModel:
         self.ops = ops
         self.nq, self.nkv, self.inter, self.vpad = shard_sizes(cfg, tp.world_size)
         self.D = cfg.head_dim
-        self.scale = 1.0 / math.sqrt(self.D)
+        self.scale = cfg.attn_scale or 1.0 / math.sqrt(self.D)
         self.layers: list[LayerWeights] = []
         self.embed: torch.Tensor | None = None
         self.norm: torch.Tensor | None = None
         self.lm_head: torch.Tensor | None = None
         mp = max_pos or cfg.max_position_embeddings
         self.cos_sin = ref.rope_cos_sin(self.D, mp, cfg.rope_theta, cfg.rope_scaling).to(self.device)
+        # sliding-window layers with their own RoPE base (Gemma-3 local layers: plain RoPE)
+        self.cos_sin_local = self.cos_sin
+        if cfg.rope_local_theta and any(cfg.layer_windows):
+            self.cos_sin_local = ref.rope_cos_sin(self.D, mp, cfg.rope_local_theta, None).to(self.device)
+        self.vanilla = not (cfg.qkv_bias or cfg.qk_norm or cfg.sandwich_norm or cfg.hidden_act != "silu"
+                            or any(cfg.layer_windows) or cfg.embed_scale != 1.0)
         self.decode_partition = 512
         self.block_size_hint = 16  # KV block size (set by the runner)
         self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
@@ -125,9 +143,14 @@ class LlamaModel:
         def new(*shape):
             return torch.empty(*shape, device=dev, dtype=dt)
 
+        nd = torch.float32 if cfg.norm_offset else dt  # Gemma norms are fp32 (1 + w)
+
+        def ones(n, dtype=None):
+            return torch.ones(n, device=dev, dtype=dtype or nd)
+
         self.embed = new(self.vpad, H)
         fill(self.embed, "embed", rank * self.vpad, 0, H)
-        self.norm = torch.ones(H, device=dev, dtype=dt)
+        self.norm = ones(H)
         if cfg.tie_word_embeddings:
             self.lm_head = self.embed
         else:
@@ -137,14 +160,19 @@ class LlamaModel:
         kv_head0 = rank * nkv if cfg.num_kv_heads >= tp else rank // (tp // cfg.num_kv_heads)
         self.layers = []
         for li in range(cfg.num_layers):
-            lw = LayerWeights(ln1=torch.ones(H, device=dev, dtype=dt), wqkv=new((nq + 2 * nkv) * D, H),
-                              wo=new(H, nq * D), ln2=torch.ones(H, device=dev, dtype=dt))
+            lw = LayerWeights(ln1=ones(H), wqkv=new((nq + 2 * nkv) * D, H), wo=new(H, nq * D), ln2=ones(H))
             fill(lw.wqkv[:nq * D], f"{li}.q", rank * nq * D, 0, H)
             fill(lw.wqkv[nq * D:(nq + nkv) * D], f"{li}.k", kv_head0 * D, 0, H)
             fill(lw.wqkv[(nq + nkv) * D:], f"{li}.v", kv_head0 * D, 0, H)
             fill(lw.wo, f"{li}.o", 0, rank * nq * D, cfg.num_heads * D)
+            if cfg.qkv_bias:
+                lw.bqkv = torch.zeros((nq + 2 * nkv) * D, device=dev, dtype=dt)
+            if cfg.qk_norm:
+                lw.q_norm, lw.k_norm = ones(D, torch.float32), ones(D, torch.float32)
+            if cfg.sandwich_norm:
+                lw.post_attn_norm, lw.post_ff_norm = ones(H), ones(H)
             if cfg.num_experts:
-                E, Ig = cfg.num_experts, cfg.intermediate_size
+                E, Ig = cfg.num_experts, cfg.expert_size
                 lw.router = new(E, H)
                 fill(lw.router, f"{li}.router", 0, 0, H)
                 lw.w13 = new(E, 2 * I, H)
@@ -235,7 +263,7 @@ class LlamaModel:
         With the fused decode path the merged gate|up weight is packed
         gate/up-interleaved instead (``PACKED_GLU``: the SiLU-GLU runs in its epilogue)."""
         n = 0
-        glu = self.fused_decode and self.tp.world_size == 1
+        glu = self.fused_decode and self.tp.world_size == 1 and self.vanilla
         for lw in self.layers:
             for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
                 if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
@@ -281,7 +309,7 @@ class LlamaModel:
     def fused_gemm_shapes(self) -> dict:
         """{(N, K): epilogue spec} of the projections whose decode GEMM output feeds
         a fused epilogue (ops/gemm.py tunes them as GEMM + epilogue units)."""
-        if self.tp.world_size != 1 or not self.layers:
+        if self.tp.world_size != 1 or not self.layers or not self.vanilla:
             return {}
         lw = self.layers[0]
         out = {}
@@ -297,7 +325,7 @@ class LlamaModel:
 
     def _fused_ok(self, meta: AttnMeta) -> bool:
         return (self.fused_decode and meta.num_prefill_tokens == 0 and self.tp.world_size == 1
-                and getattr(self.ops, "name", "") == "hip" and self.cfg.num_experts == 0)
+                and getattr(self.ops, "name", "") == "hip" and self.cfg.num_experts == 0 and self.vanilla)
 
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.tp.world_size == 1:
@@ -318,6 +346,8 @@ class LlamaModel:
         if self._fused_ok(meta):
             return self.forward_decode_fused(ids, meta, kv_caches)
         h = self.embed_tokens(ids)
+        if cfg.embed_scale != 1.0:  # Gemma: embeddings * sqrt(hidden), the scale rounded to the dtype
+            h = h * float(torch.tensor(cfg.embed_scale, dtype=h.dtype))
         residual = torch.empty_like(h)
         xn = torch.empty_like(h)
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
@@ -330,28 +360,44 @@ class LlamaModel:
             else:
                 ops.fused_add_rmsnorm(xn, h, residual, lw.ln1, eps)
             qkv = self.linear(xn, lw.wqkv)
+            if lw.bqkv is not None:
+                qkv += lw.bqkv
+            if lw.q_norm is not None:  # per-head RMSNorm of q and k, before RoPE
+                ops.qk_rmsnorm(qkv, lw.q_norm, lw.k_norm, nq, nkv, D, eps)
             kc, vc = kv_caches[i]
-            ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
-                           cfg.rope_mode)
+            win = cfg.window_of(i)
+            ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin_local if win else self.cos_sin,
+                           kc, vc, nq, nkv, D, cfg.rope_mode)
             if Tp:
                 ops.prefill_attention(attn[:Tp], qkv[:Tp], kc, vc, meta.bt_prefill, meta.cu_q,
-                                      meta.ctx_prefill, meta.tiles, nq, nkv, self.scale)
+                                      meta.ctx_prefill, meta.tiles, nq, nkv, self.scale, win)
             if Td:
                 ops.paged_decode(attn[Tp:], qkv[Tp:], kc, vc, meta.bt_decode, meta.ctx_decode,
-                                 tmp_out, tmp_ml, nq, nkv, part, self.scale)
+                                 tmp_out, tmp_ml, nq, nkv, part, self.scale, win)
             o = self.linear(attn, lw.wo)
             self.tp.all_reduce(o)
+            if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)
+                ops.rmsnorm(o, o, lw.post_attn_norm, eps)
             ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
             if lw.router is not None:
                 h = self.moe(xn, lw)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=h.device, dtype=h.dtype)
-                ops.silu_and_mul(act, gu)
+                self.act_and_mul(act, gu)
                 h = self.linear(act, lw.wd)
             self.tp.all_reduce(h)
+            if lw.post_ff_norm is not None:
+                ops.rmsnorm(h, h, lw.post_ff_norm, eps)
         ops.fused_add_rmsnorm(xn, h, residual, self.norm, eps)
         return xn
+
+    def act_and_mul(self, out: torch.Tensor, gu: torch.Tensor):
+        """GLU activation of the merged [gate | up] output: SiLU (Llama/Qwen/Mixtral)
+        or tanh-GELU (Gemma GeGLU)."""
+        if self.cfg.hidden_act == "gelu_tanh":
+            return self.ops.gelu_and_mul(out, gu)
+        return self.ops.silu_and_mul(out, gu)
 
     def forward_decode_fused(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """Decode-only forward (TP=1) with the decode GEMMs' split-K partials reduced
@@ -429,16 +475,18 @@ class LlamaModel:
         return part, to, tm
 
     def moe(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
-        """Mixtral sparse MoE (top-k of E experts, renormalised softmax weights)."""
+        """Sparse MoE: softmax over the E router logits, top-k experts, weights
+        renormalised over the k (Mixtral; Qwen3-MoE when ``norm_topk_prob``)."""
         cfg = self.cfg
         k = cfg.num_experts_per_tok
         T = x.shape[0]
-        if (self.ops.name == "hip" and T * k <= MOE_KERNEL_MAX_PAIRS and cfg.num_experts <= 64
+        if (self.ops.name == "hip" and T * k <= MOE_KERNEL_MAX_PAIRS and cfg.num_experts <= 128
                 and cfg.hidden_size % 256 == 0 and self.inter % 256 == 0):
             return self.moe_hip(x, lw)
         logits = F.linear(x, lw.router).float()
         w, idx = torch.topk(torch.softmax(logits, dim=-1), k, dim=-1)
-        w = w / w.sum(-1, keepdim=True)
+        if cfg.norm_topk_prob:
+            w = w / w.sum(-1, keepdim=True)
         out = torch.zeros(T, cfg.hidden_size, device=x.device, dtype=torch.float32)
         flat_idx = idx.reshape(-1)
         flat_tok = torch.arange(T, device=x.device).repeat_interleave(k)
@@ -498,7 +546,7 @@ class LlamaModel:
         logits = gemm.linear(x, lw.router)
         w = torch.empty(T, k, dtype=torch.float32, device=dev)
         ids = torch.empty(T, k, dtype=torch.int32, device=dev)
-        op.moe_topk_softmax(w, ids, logits, k)
+        op.moe_topk_softmax(w, ids, logits, k, cfg.norm_topk_prob)
         slots = torch.empty(cap, dtype=torch.int32, device=dev)
         tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
         ntiles = torch.empty(1, dtype=torch.int32, device=dev)

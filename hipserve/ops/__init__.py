@@ -72,6 +72,13 @@ class KernelOps:
         self._op.silu_and_mul(out, x)
         return out
 
+    def gelu_and_mul(self, out, x):
+        self._op.gelu_and_mul(out, x)
+        return out
+
+    def qk_rmsnorm(self, qkv, q_w, k_w, nq, nkv, D, eps):
+        self._op.qk_rmsnorm(qkv, q_w, k_w, nq, nkv, D, eps)
+
     def fill_uniform(self, out, row0, col0, gcols, key, scale):
         self._op.fill_uniform(out, row0, col0, gcols, key, scale)
         return out
@@ -80,15 +87,15 @@ class KernelOps:
         self._op.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
 
     def paged_decode(self, out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
-                     nq, nkv, part_size, scale):
+                     nq, nkv, part_size, scale, window=0):
         self._op.paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
-                              nq, nkv, part_size, scale)
+                              nq, nkv, part_size, scale, window)
         return out
 
     def prefill_attention(self, out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
-                          nq, nkv, scale):
+                          nq, nkv, scale, window=0):
         self._op.prefill_attention(out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
-                                   nq, nkv, scale)
+                                   nq, nkv, scale, window)
         return out
 
     def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
@@ -117,23 +124,30 @@ class ReferenceOps:
         out.copy_(ref.silu_and_mul(x))
         return out
 
+    def gelu_and_mul(self, out, x):
+        out.copy_(ref.gelu_and_mul(x))
+        return out
+
+    def qk_rmsnorm(self, qkv, q_w, k_w, nq, nkv, D, eps):
+        ref.qk_rmsnorm(qkv, q_w, k_w, nq, nkv, D, eps)
+
     def rope_cache(self, qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode):
         ref.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
 
     def paged_decode(self, out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
-                     nq, nkv, part_size, scale):
+                     nq, nkv, part_size, scale, window=0):
         B = context_lens.shape[0]
         D = k_cache.shape[3]
         out[:B, : nq * D].copy_(ref.paged_decode(q, k_cache, v_cache, block_tables, context_lens,
-                                                 nq, nkv, scale).view(B, nq * D))
+                                                 nq, nkv, scale, window).view(B, nq * D))
         return out
 
     def prefill_attention(self, out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
-                          nq, nkv, scale):
+                          nq, nkv, scale, window=0):
         D = k_cache.shape[3]
         T = int(cu_q[-1])
         out[:T, : nq * D].copy_(ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q,
-                                                      ctx_lens, nq, nkv, scale).view(T, nq * D))
+                                                      ctx_lens, nq, nkv, scale, window).view(T, nq * D))
         return out
 
     def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):

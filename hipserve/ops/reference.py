@@ -34,6 +34,24 @@ def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
     return (torch.nn.functional.silu(g) * u).to(x.dtype)
 
 
+def gelu_and_mul(x: torch.Tensor) -> torch.Tensor:
+    """tanh-GELU(gate) * up (Gemma GeGLU, HF gelu_pytorch_tanh)."""
+    inter = x.shape[-1] // 2
+    g, u = x[..., :inter].float(), x[..., inter:].float()
+    return (torch.nn.functional.gelu(g, approximate="tanh") * u).to(x.dtype)
+
+
+def qk_rmsnorm(qkv: torch.Tensor, q_w: torch.Tensor, k_w: torch.Tensor, nq: int, nkv: int, D: int, eps: float):
+    """In place: RMSNorm over head_dim of every q head (weight q_w) and k head (k_w)."""
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    q = qkv[:, : nq * D].view(T, nq, D)
+    k = qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
+    q.copy_(rmsnorm(q, q_w, eps))
+    k.copy_(rmsnorm(k, k_w, eps))
+
+
 def rope_cos_sin(head_dim: int, max_pos: int, theta: float, scaling: dict | None = None,
                  rotary_dim: int | None = None) -> torch.Tensor:
     """fp32 [max_pos, D] table = [cos | sin] with optional Llama-3 frequency scaling."""
@@ -103,8 +121,9 @@ def _gather_kv(k_cache, v_cache, block_table, n):
     return k, v
 
 
-def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nq, nkv, scale):
-    """q [B, nq*D (+extra)] -> out [B, nq, D] (fp32 math)."""
+def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nq, nkv, scale, window=0):
+    """q [B, nq*D (+extra)] -> out [B, nq, D] (fp32 math). window > 0: only the
+    last ``window`` keys (sliding-window layers)."""
     D = k_cache.shape[3]
     B = context_lens.shape[0]
     G = nq // nkv
@@ -112,6 +131,8 @@ def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nq, nkv, scale
     for b in range(B):
         n = int(context_lens[b])
         k, v = _gather_kv(k_cache, v_cache, block_tables[b], n)
+        if window > 0 and n > window:
+            k, v = k[n - window:], v[n - window:]
         qb = q[b, : nq * D].view(nq, D).float()
         kf = k.float().repeat_interleave(G, dim=1)  # [n, nq, D]
         vf = v.float().repeat_interleave(G, dim=1)
@@ -121,8 +142,9 @@ def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nq, nkv, scale
     return out
 
 
-def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nq, nkv, scale):
-    """q [T, nq*D (+extra)] -> out [T, nq, D]; causal over absolute positions."""
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nq, nkv, scale, window=0):
+    """q [T, nq*D (+extra)] -> out [T, nq, D]; causal over absolute positions;
+    window > 0: keys within ``window - 1`` positions before the query."""
     D = k_cache.shape[3]
     G = nq // nkv
     T = int(cu_q[-1])
@@ -139,7 +161,10 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nq, nkv
         s = torch.einsum("qhd,nhd->hqn", qs, kf) * scale
         qpos = torch.arange(ctx - ql, ctx, device=q.device)[:, None]
         kpos = torch.arange(ctx, device=q.device)[None, :]
-        s = s.masked_fill((kpos > qpos)[None], float("-inf"))
+        mask = kpos > qpos
+        if window > 0:
+            mask = mask | (kpos <= qpos - window)
+        s = s.masked_fill(mask[None], float("-inf"))
         p = torch.softmax(s, dim=-1)
         out[q0:q1] = torch.einsum("hqn,nhd->qhd", p, vf).to(q.dtype)
     return out

@@ -53,17 +53,55 @@ class _Ckpt:
     def has(self, name):
         return name in self.where
 
+    def find(self, suffix) -> str | None:
+        for k in self.where:
+            if k.endswith(suffix):
+                return k
+        return None
+
     def full(self, name) -> torch.Tensor:
-        return self.where[name].get_tensor(name)
+        t = self.where[name].get_tensor(name)
+        return self._dequant(name, t) if t.dtype in _FP8 else t
 
     def rows(self, name, start, stop) -> torch.Tensor:
+        if self._is_fp8(name):
+            return self.full(name)[start:stop]
         return self.where[name].get_slice(name)[start:stop]
 
     def cols(self, name, start, stop) -> torch.Tensor:
+        if self._is_fp8(name):
+            return self.full(name)[:, start:stop]
         return self.where[name].get_slice(name)[:, start:stop]
+
+    def _is_fp8(self, name) -> bool:
+        return self.where[name].get_slice(name).get_dtype() in ("F8_E4M3", "F8_E5M2")
+
+    def _dequant(self, name, t) -> torch.Tensor:
+        """FP8 checkpoints (compressed-tensors "FP8-Dynamic" / block-FP8): weights
+        are dequantised to the compute dtype at load with their ``weight_scale``
+        (per tensor or per output channel) or ``weight_scale_inv`` (128x128 blocks)."""
+        base = name[: -len("weight")] if name.endswith("weight") else name + "_"
+        for sname in (base + "weight_scale", base + "weight_scale_inv"):
+            if sname in self.where:
+                s = self.where[sname].get_tensor(sname).float()
+                w = t.float()
+                if s.numel() == 1 or (s.dim() >= 1 and s.shape[0] == w.shape[0] and s.numel() == w.shape[0]):
+                    return w * s.reshape(-1, *([1] * (w.dim() - 1))) if s.numel() > 1 else w * s.reshape(())
+                bn, bk = -(-w.shape[0] // s.shape[0]), -(-w.shape[1] // s.shape[1])
+                s = s.repeat_interleave(bn, 0)[: w.shape[0]].repeat_interleave(bk, 1)[:, : w.shape[1]]
+                return w * s
+        raise ValueError(f"FP8 tensor {name} without weight_scale / weight_scale_inv")
+
+
+_FP8 = tuple(getattr(torch, n) for n in ("float8_e4m3fn", "float8_e5m2") if hasattr(torch, n))
 
 
 def load_hf_weights(model: LlamaModel, model_path: str):
+    """Load a HF-format checkpoint of any served family into ``model`` (this rank's
+    TP shard): Llama / Mistral, Mixtral, Qwen2 (q/k/v bias), Qwen3 (q/k norms),
+    Qwen3-MoE (incl. the fused, transposed expert tensors of Qwen3-VL-MoE), Gemma-3
+    text (sandwich norms stored as fp32 ``1 + w``), Phi-3 (fused qkv / gate_up).
+    Multimodal wrappers are read through their language-model prefix."""
     ck = _Ckpt(resolve_checkpoint_dir(model_path))
     cfg, tp = model.cfg, model.tp
     r, W = tp.rank, tp.world_size
@@ -74,9 +112,24 @@ def load_hf_weights(model: LlamaModel, model_path: str):
         kv0 = r * nkv
     else:  # replicated kv heads: rank r uses kv head r // (W / nkv_total)
         kv0 = r // (W // cfg.num_kv_heads)
+    emb_name = ck.find("embed_tokens.weight")
+    if emb_name is None:
+        raise KeyError("no embed_tokens.weight in the checkpoint")
+    pre = emb_name[: -len("embed_tokens.weight")]  # "model." | "model.language_model." | ...
 
     def to(t):
         return t.to(device=dev, dtype=dt).contiguous()
+
+    def normw(name):
+        """RMSNorm weight: Gemma's x * (1 + w) kept exactly as fp32 (1 + w)."""
+        t = ck.full(name)
+        if cfg.norm_offset:
+            return (1.0 + t.float()).to(device=dev).contiguous()
+        return to(t)
+
+    def headnorm(name):  # q/k norms: fp32 weights for the per-head RMSNorm op
+        t = ck.full(name).float()
+        return ((1.0 + t) if cfg.norm_offset else t).to(device=dev).contiguous()
 
     def vocab_shard(name):
         t = ck.rows(name, r * vpad, min((r + 1) * vpad, cfg.vocab_size))
@@ -84,43 +137,89 @@ def load_hf_weights(model: LlamaModel, model_path: str):
             t = torch.cat([t, torch.zeros(vpad - t.shape[0], H, dtype=t.dtype)])
         return to(t)
 
-    model.embed = vocab_shard("model.embed_tokens.weight")
-    model.norm = to(ck.full("model.norm.weight"))
-    if cfg.tie_word_embeddings or not ck.has("lm_head.weight"):
+    model.embed = vocab_shard(emb_name)
+    model.norm = normw(pre + "norm.weight")
+    head = "lm_head.weight" if ck.has("lm_head.weight") else ck.find("lm_head.weight")
+    if cfg.tie_word_embeddings or head is None:
         model.lm_head = model.embed
     else:
-        model.lm_head = vocab_shard("lm_head.weight")
+        model.lm_head = vocab_shard(head)
+    qs, ks = (slice(r * nq * D, (r + 1) * nq * D), slice(kv0 * D, (kv0 + nkv) * D))
     model.layers = []
     for i in range(cfg.num_layers):
-        p = f"model.layers.{i}."
-        q = ck.rows(p + "self_attn.q_proj.weight", r * nq * D, (r + 1) * nq * D)
-        k = ck.rows(p + "self_attn.k_proj.weight", kv0 * D, (kv0 + nkv) * D)
-        v = ck.rows(p + "self_attn.v_proj.weight", kv0 * D, (kv0 + nkv) * D)
+        p = f"{pre}layers.{i}."
+        a = p + "self_attn."
+        if ck.has(a + "qkv_proj.weight"):  # Phi-3: fused [q; k; v]
+            f = ck.full(a + "qkv_proj.weight")
+            q, k, v = torch.split(f, [cfg.num_heads * D, cfg.num_kv_heads * D, cfg.num_kv_heads * D], 0)
+            q, k, v = q[qs], k[ks], v[ks]
+        else:
+            q = ck.rows(a + "q_proj.weight", qs.start, qs.stop)
+            k = ck.rows(a + "k_proj.weight", ks.start, ks.stop)
+            v = ck.rows(a + "v_proj.weight", ks.start, ks.stop)
         lw = LayerWeights(
-            ln1=to(ck.full(p + "input_layernorm.weight")),
+            ln1=normw(p + "input_layernorm.weight"),
             wqkv=to(torch.cat([q, k, v], 0)),
-            wo=to(ck.cols(p + "self_attn.o_proj.weight", r * nq * D, (r + 1) * nq * D)),
-            ln2=to(ck.full(p + "post_attention_layernorm.weight")),
+            wo=to(ck.cols(a + "o_proj.weight", qs.start, qs.stop)),
+            ln2=normw(p + ("pre_feedforward_layernorm.weight" if cfg.sandwich_norm
+                           else "post_attention_layernorm.weight")),
         )
+        if cfg.qkv_bias:
+            lw.bqkv = to(torch.cat([ck.full(a + "q_proj.bias")[qs], ck.full(a + "k_proj.bias")[ks],
+                                    ck.full(a + "v_proj.bias")[ks]], 0))
+        if cfg.qk_norm:
+            lw.q_norm = headnorm(a + "q_norm.weight")
+            lw.k_norm = headnorm(a + "k_norm.weight")
+        if cfg.sandwich_norm:
+            lw.post_attn_norm = normw(p + "post_attention_layernorm.weight")
+            lw.post_ff_norm = normw(p + "post_feedforward_layernorm.weight")
         if cfg.num_experts:
-            E = cfg.num_experts
-            m = p + "block_sparse_moe."
-            lw.router = to(ck.full(m + "gate.weight"))
-            w13, w2 = [], []
-            for e in range(E):
-                ep = f"{m}experts.{e}."
-                g = ck.rows(ep + "w1.weight", r * inter, (r + 1) * inter)
-                u = ck.rows(ep + "w3.weight", r * inter, (r + 1) * inter)
-                w13.append(torch.cat([g, u], 0))
-                w2.append(ck.cols(ep + "w2.weight", r * inter, (r + 1) * inter))
-            lw.w13 = to(torch.stack(w13))
-            lw.w2 = to(torch.stack(w2))
+            lw.router, lw.w13, lw.w2 = _load_experts(ck, p, cfg, r, inter, to)
+        elif ck.has(p + "mlp.gate_up_proj.weight"):  # Phi-3: fused [gate; up]
+            f = ck.full(p + "mlp.gate_up_proj.weight")
+            I = cfg.intermediate_size
+            lw.wgu = to(torch.cat([f[r * inter:(r + 1) * inter], f[I + r * inter:I + (r + 1) * inter]], 0))
+            lw.wd = to(ck.cols(p + "mlp.down_proj.weight", r * inter, (r + 1) * inter))
         else:
             g = ck.rows(p + "mlp.gate_proj.weight", r * inter, (r + 1) * inter)
             u = ck.rows(p + "mlp.up_proj.weight", r * inter, (r + 1) * inter)
             lw.wgu = to(torch.cat([g, u], 0))
             lw.wd = to(ck.cols(p + "mlp.down_proj.weight", r * inter, (r + 1) * inter))
         model.layers.append(lw)
+
+
+def _load_experts(ck, p, cfg, r, inter, to):
+    """(router [E, H], w13 [E, 2*I/TP, H] as [gate; up], w2 [E, H, I/TP]) from
+    Mixtral (block_sparse_moe.experts.e.w1/w3/w2), Qwen3-MoE
+    (mlp.experts.e.gate_proj/up_proj/down_proj) or fused expert tensors
+    (mlp.experts.gate_up_proj [E, 2I, H] / Qwen3-VL-MoE's transposed [E, H, 2I])."""
+    E, H, I = cfg.num_experts, cfg.hidden_size, cfg.expert_size
+    sl = slice(r * inter, (r + 1) * inter)
+    if ck.has(p + "block_sparse_moe.gate.weight"):
+        m = p + "block_sparse_moe."
+        names = ("w1", "w3", "w2")
+    else:
+        m = p + "mlp."
+        names = ("gate_proj", "up_proj", "down_proj")
+    router = to(ck.full(m + "gate.weight"))
+    if ck.has(m + "experts.gate_up_proj"):
+        gu = ck.full(m + "experts.gate_up_proj")
+        dn = ck.full(m + "experts.down_proj")
+        if tuple(gu.shape) == (E, H, 2 * I) and (H != 2 * I or cfg.family == "qwen3_moe"):
+            gu = gu.transpose(1, 2)
+        if tuple(dn.shape) == (E, I, H) and (H != I or cfg.family == "qwen3_moe"):
+            dn = dn.transpose(1, 2)
+        w13 = torch.cat([gu[:, sl], gu[:, I + sl.start:I + sl.stop]], 1)
+        w2 = dn[:, :, sl]
+        return router, to(w13), to(w2)
+    w13, w2 = [], []
+    for e in range(E):
+        ep = f"{m}experts.{e}."
+        g = ck.rows(ep + names[0] + ".weight", sl.start, sl.stop)
+        u = ck.rows(ep + names[1] + ".weight", sl.start, sl.stop)
+        w13.append(torch.cat([g, u], 0))
+        w2.append(ck.cols(ep + names[2] + ".weight", sl.start, sl.stop))
+    return router, to(torch.stack(w13)), to(torch.stack(w2))
 
 
 def save_hf_checkpoint(path: str, cfg, tensors: dict[str, torch.Tensor]):

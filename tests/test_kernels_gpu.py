@@ -75,10 +75,13 @@ def test_rope_cache(ops, mode, bs):
     _close(vc, vc_r, atol=0)
 
 
-@pytest.mark.parametrize("nq,nkv,D", [(32, 8, 128), (64, 8, 128), (32, 32, 64), (32, 4, 64)])
+@pytest.mark.parametrize("nq,nkv,D", [(32, 8, 128), (64, 8, 128), (32, 32, 64), (32, 4, 64), (32, 32, 96)])
 @pytest.mark.parametrize("bs", [16, 32])
 @pytest.mark.parametrize("part", [512, 2048])
-def test_paged_decode(ops, nq, nkv, D, bs, part):
+@pytest.mark.parametrize("window", [0, 100])
+def test_paged_decode(ops, nq, nkv, D, bs, part, window):
+    """Split-K paged decode (incl. head_dim 96 and sliding-window layers: keys
+    [ctx - window, ctx)) vs the fp32 oracle."""
     torch.manual_seed(2)
     ctx = [1, 17, 100, 600, 1300, 512, 33]
     B = len(ctx)
@@ -94,16 +97,17 @@ def test_paged_decode(ops, nq, nkv, D, bs, part):
     tmp_ml = torch.empty(B, nq, max_parts, 2, device=DEV, dtype=torch.float32)
     out = torch.zeros(B, nq * D, device=DEV, dtype=torch.bfloat16)
     scale = 1.0 / math.sqrt(D)
-    ops.paged_decode(out, q, kc, vc, bt, cl, tmp_out, tmp_ml, nq, nkv, part, scale)
-    want = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), nq, nkv, scale)
+    ops.paged_decode(out, q, kc, vc, bt, cl, tmp_out, tmp_ml, nq, nkv, part, scale, window)
+    want = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), nq, nkv, scale, window)
     _close(out.view(B, nq, D), want, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("nq,nkv,D,bs,v1", [(32, 8, 128, 16, False), (32, 8, 128, 16, True), (64, 8, 128, 16, False),
                                           (8, 1, 128, 32, False), (16, 8, 128, 16, False), (16, 2, 64, 16, False),
-                                          (4, 4, 128, 16, False)])
+                                          (4, 4, 128, 16, False), (8, 8, 96, 16, False)])
 @pytest.mark.parametrize("waves", ["4", "8"])
-def test_prefill_attention(ops, nq, nkv, D, bs, v1, waves, monkeypatch):
+@pytest.mark.parametrize("window", [0, 200])
+def test_prefill_attention(ops, nq, nkv, D, bs, v1, waves, window, monkeypatch):
     """v2 (LDS-shared K/V, GQA heads per workgroup: G = 2/4/8) and v1 (D = 64, MHA,
     or HIPSERVE_PREFILL_ATTN_V1) against the fp32 oracle, including long prompts
     (many 64-key tiles: the lazy rescale) and chunked prefill over a prefix."""
@@ -129,9 +133,33 @@ def test_prefill_attention(ops, nq, nkv, D, bs, v1, waves, monkeypatch):
     tiles_t = torch.tensor(tiles, device=DEV, dtype=torch.int32)
     out = torch.zeros(T, nq * D, device=DEV, dtype=torch.bfloat16)
     scale = 1.0 / math.sqrt(D)
-    ops.prefill_attention(out, q, kc, vc, bt, cu_t, ctx_t, tiles_t, nq, nkv, scale)
-    want = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(), nq, nkv, scale)
+    ops.prefill_attention(out, q, kc, vc, bt, cu_t, ctx_t, tiles_t, nq, nkv, scale, window)
+    want = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cu_t.cpu(), ctx_t.cpu(), nq, nkv, scale,
+                                 window)
     _close(out.view(T, nq, D), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("T,nq,nkv,D", [(37, 16, 8, 128), (5, 32, 4, 64), (64, 8, 8, 96), (3, 8, 2, 256)])
+def test_qk_rmsnorm(ops, T, nq, nkv, D):
+    """Per-head q/k RMSNorm in place inside the qkv rows; v untouched."""
+    torch.manual_seed(11)
+    W = (nq + 2 * nkv) * D
+    qkv = torch.randn(T, W + 32, device=DEV, dtype=torch.bfloat16)[:, :W]
+    qw = torch.rand(D, device=DEV) + 0.5
+    kw = torch.rand(D, device=DEV) + 0.5
+    want = qkv.cpu().clone()
+    ref.qk_rmsnorm(want, qw.cpu(), kw.cpu(), nq, nkv, D, 1e-6)
+    ops.qk_rmsnorm(qkv, qw, kw, nq, nkv, D, 1e-6)
+    _close(qkv[:, : (nq + nkv) * D], want[:, : (nq + nkv) * D], atol=2e-2, rtol=1e-2)
+    assert torch.equal(qkv[:, (nq + nkv) * D:].cpu(), want[:, (nq + nkv) * D:])
+
+
+@pytest.mark.parametrize("rows,inter", [(5, 21504), (64, 1792), (1, 8)])
+def test_gelu_and_mul(ops, rows, inter):
+    x = torch.randn(rows, 2 * inter, device=DEV, dtype=torch.bfloat16) * 2
+    out = torch.empty(rows, inter, device=DEV, dtype=torch.bfloat16)
+    ops.gelu_and_mul(out, x)
+    _close(out, ref.gelu_and_mul(x.cpu()), atol=2e-2, rtol=1e-2)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -307,8 +335,9 @@ def test_decode_gemm_packed(ops, M, N, K, rt, splits):
 
 
 @pytest.mark.parametrize("mode", ["packed", "rowmajor", "legacy"])
-@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (13, 8, 2), (64, 8, 2), (200, 8, 2), (5, 4, 1)])
-def test_moe_kernels_match_reference(ops, T, E, k, mode, monkeypatch):
+@pytest.mark.parametrize("T,E,k,norm", [(1, 8, 2, True), (13, 8, 2, True), (64, 8, 2, True), (200, 8, 2, True),
+                                        (5, 4, 1, True), (3, 128, 8, True), (40, 128, 8, False), (9, 64, 4, False)])
+def test_moe_kernels_match_reference(ops, T, E, k, norm, mode, monkeypatch):
     """HIP MoE (topk softmax, align, gathered GEMMs, combine) vs the torch path, for
     the expert decode GEMM on packed (GLU epilogue + split-K partial combine) and
     row-major weights, and the legacy 16-row gathered GEMM."""
@@ -319,11 +348,12 @@ def test_moe_kernels_match_reference(ops, T, E, k, mode, monkeypatch):
     from hipserve.parallel.comm import TPGroup
 
     cfg = PRESETS["tiny-mixtral"].replace(hidden_size=512, intermediate_size=768, num_experts=E,
-                                          num_experts_per_tok=k)
+                                          num_experts_per_tok=k, norm_topk_prob=norm)
     m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, ops)
     torch.manual_seed(T)
     lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None,
-                      router=torch.randn(E, 512, device=DEV, dtype=torch.bfloat16) * 0.2,
+                      # many experts: wider logits so the k-th / (k+1)-th choice never ties in bf16
+                      router=torch.randn(E, 512, device=DEV, dtype=torch.bfloat16) * (0.2 if E <= 8 else 0.6),
                       w13=torch.randn(E, 1536, 512, device=DEV, dtype=torch.bfloat16) * 0.05,
                       w2=torch.randn(E, 512, 768, device=DEV, dtype=torch.bfloat16) * 0.05)
     x = torch.randn(T, 512, device=DEV, dtype=torch.bfloat16)
