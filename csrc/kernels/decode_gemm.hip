@@ -384,6 +384,9 @@ static bool moe_dg_steps(void* out, long out_stride, float* ws, const void* x, l
     case 7: moe_dg_launch<MT, 7, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
     case 8: moe_dg_launch<MT, 8, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
     case 16: moe_dg_launch<MT, 16, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    // small-expert MoE (Qwen3-MoE: expert width 768 / 1536 -> w2 K in one slice)
+    case 3: moe_dg_launch<MT, 3, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
+    case 6: moe_dg_launch<MT, 6, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, mt, tiles_cap, N, K, S, s); return true;
     default: return false;
   }
 }
@@ -400,7 +403,7 @@ static bool moe_dg_tile(void* out, long out_stride, float* ws, const void* x, lo
 // Expert GEMM over moe_align tiles. ws == nullptr: bf16 out[slot, N] (glu: act[slot, N/2]
 // from the gate/up-interleaved packing, S must be 1); else fp32 partials
 // ws[S, tiles_cap * tile, N] (summed by moe_combine_partial). w: [E] x (packed or
-// row-major [N, K]) with w_estride elements per expert. K / S = 256 * {1,2,4,7,8,16}.
+// row-major [N, K]) with w_estride elements per expert. K / S = 256 * {1,2,3,4,6,7,8,16}.
 bool launch_moe_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
                             long w_estride, const int* slots, const int* tile_expert, int tiles_cap, int tile,
                             int gather_k, int N, int K, int S, bool packed, bool glu, hipStream_t s) {

@@ -479,7 +479,7 @@ void moe_decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, 
                                                x.stride(0), w.data_ptr(), estride, slots.data_ptr<int>(),
                                                tile_expert.data_ptr<int>(), nslots / tile, tile, gather_k, N, K,
                                                splits, packed, glu, cur_stream()),
-              "moe_decode_gemm: unsupported K / splits (K / splits / 256 in {1,2,4,7,8,16}) or glu without packing");
+              "moe_decode_gemm: unsupported K / splits (K / splits / 256 in {1,2,3,4,6,7,8,16}) or glu without packing");
 }
 
 void moe_combine_partial(at::Tensor& out, const at::Tensor& ws, const at::Tensor& w, const at::Tensor& pair_slot,

@@ -34,8 +34,9 @@ from ..parallel.comm import TPGroup
 
 log = logging.getLogger(__name__)
 
-DG_MOE_STEPS = (1, 2, 4, 7, 8, 16)  # 256-k steps per K slice the expert decode GEMM is built for
-MOE_KERNEL_MAX_PAIRS = 2048  # larger (prefill) batches use per-expert hipBLASLt GEMMs
+DG_MOE_STEPS = (1, 2, 3, 4, 6, 7, 8, 16)  # 256-k steps per K slice the expert decode GEMM is built for
+MOE_KERNEL_MAX_PAIRS = 2048  # larger (prefill) batches use per-expert hipBLASLt GEMMs ...
+MOE_KERNEL_MAX_ROWS_PER_EXPERT = 1024  # ... unless the experts are many and small (Qwen3-MoE: 128 x 768)
 
 
 @dataclass
@@ -480,8 +481,11 @@ class LlamaModel:
         cfg = self.cfg
         k = cfg.num_experts_per_tok
         T = x.shape[0]
-        if (self.ops.name == "hip" and T * k <= MOE_KERNEL_MAX_PAIRS and cfg.num_experts <= 128
-                and cfg.hidden_size % 256 == 0 and self.inter % 256 == 0):
+        P = T * k
+        if (self.ops.name == "hip" and cfg.num_experts <= 128 and cfg.hidden_size % 256 == 0
+                and self.inter % 256 == 0
+                and (P <= MOE_KERNEL_MAX_PAIRS
+                     or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts and self._moe_decode_ok(lw)))):
             return self.moe_hip(x, lw)
         logits = F.linear(x, lw.router).float()
         w, idx = torch.topk(torch.softmax(logits, dim=-1), k, dim=-1)
@@ -565,9 +569,14 @@ class LlamaModel:
                 self.ops.silu_and_mul(act, gu)
             active = min(E, cap // tile, P)
             S = self._moe_w2_splits(self.inter, -(-H // 128), active)
+            w2 = lw.moe_packed[1] if packed else lw.w2
+            if S == 1:  # one K slice: bf16 expert outputs, no fp32 partial slab
+                y = torch.empty(cap, H, dtype=x.dtype, device=dev)
+                op.moe_decode_gemm(y, act, w2, slots, tile_expert, tile, 0, H, 1, packed, False)
+                op.moe_combine(out, y, w, pair_slot, k)
+                return out
             ws = torch.empty(S, cap, H, dtype=torch.float32, device=dev)
-            op.moe_decode_gemm(ws, act, lw.moe_packed[1] if packed else lw.w2, slots, tile_expert, tile, 0, H, S,
-                               packed, False)
+            op.moe_decode_gemm(ws, act, w2, slots, tile_expert, tile, 0, H, S, packed, False)
             op.moe_combine_partial(out, ws, w, pair_slot, k)
             return out
         gu = torch.empty(cap, 2 * self.inter, dtype=x.dtype, device=dev)

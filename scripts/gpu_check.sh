@@ -71,6 +71,8 @@ for s in $steps; do
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
+    prof_qwen3moe) prof_run profqm --model qwen3-30b-a3b ;;
+    prof_gemma3) prof_run profg3 --model gemma-3-27b ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done
