@@ -81,26 +81,36 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
                                                          int* __restrict__ tile_expert, int tiles_cap,
                                                          int* __restrict__ num_tiles, int* __restrict__ pair_slot) {
   __shared__ int cnt[128], off[129], cur[128];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 128) { cnt[tid] = 0; cur[tid] = 0; }
   __syncthreads();
   for (int p = tid; p < npairs; p += 1024) atomicAdd(&cnt[ids[p]], 1);
   __syncthreads();
-  if (tid == 0) {
-    off[0] = 0;
-    for (int e = 0; e < E; ++e) off[e + 1] = off[e] + (cnt[e] + tile - 1) / tile * tile;
-    *num_tiles = off[E] / tile;
+  if (tid < 64) {  // exclusive scan of the tile-padded counts, 2 experts per lane (E <= 128)
+    const int e0 = 2 * lane, e1 = 2 * lane + 1;
+    const int a = e0 < E ? (cnt[e0] + tile - 1) / tile * tile : 0;
+    const int b = e1 < E ? (cnt[e1] + tile - 1) / tile * tile : 0;
+    int incl = a + b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - a - b;
+    off[e0] = excl;
+    off[e1] = excl + a;
+    if (lane == 63) {
+      off[128] = incl;
+      *num_tiles = incl / tile;
+    }
   }
   __syncthreads();
+  const int total = off[128];
   for (int s = tid; s < slots_cap; s += 1024) slots[s] = -1;
-  for (int t = tid; t < tiles_cap; t += 1024) {
-    int e = -1;
-    if (t * tile < off[E]) {
-      for (int q = 0; q < E; ++q)
-        if (t * tile >= off[q] && t * tile < off[q + 1]) e = q;
-    }
-    tile_expert[t] = e;
-  }
+  // each expert labels its own tiles; tiles past the used range are -1
+  if (tid < E)
+    for (int t = off[tid] / tile; t < (off[tid] + (cnt[tid] + tile - 1) / tile * tile) / tile; ++t) tile_expert[t] = tid;
+  for (int t = total / tile + tid; t < tiles_cap; t += 1024) tile_expert[t] = -1;
   __syncthreads();
   for (int p = tid; p < npairs; p += 1024) {
     const int e = ids[p];

@@ -125,12 +125,60 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_kernel(unsigned short* __restr
   }
 }
 
+// Vector form for D = 8 * LPH (64 / 128 / 256): LPH lanes per head, one 16-byte
+// load per lane, 64 / LPH heads per wave, the sum of squares reduced over the
+// head's lane group with xor shuffles.
+template <int LPH>
+__global__ __launch_bounds__(256) void qk_rmsnorm_vec_kernel(unsigned short* __restrict__ qkv, long stride,
+                                                             const float* __restrict__ qw,
+                                                             const float* __restrict__ kw, int T, int nq, int nkv,
+                                                             float eps) {
+  constexpr int D = 8 * LPH, HPW = 64 / LPH;
+  const int nh = nq + nkv;
+  const int lane = threadIdx.x & 63;
+  const long item = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * HPW + lane / LPH;
+  const bool valid = item < (long)T * nh;
+  const long it = valid ? item : 0;
+  const int t = (int)(it / nh), h = (int)(it % nh);
+  const int c = lane % LPH;
+  u16x8* p = reinterpret_cast<u16x8*>(qkv + (long)t * stride + (long)h * D) + c;
+  const u16x8 v = *p;
+  float f[8], ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f[j] = bf16_to_f32(v[j]);
+    ss += f[j] * f[j];
+  }
+#pragma unroll
+  for (int o = LPH / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float inv = rsqrtf(ss / D + eps);
+  const f32x4* wp = reinterpret_cast<const f32x4*>(h < nq ? qw : kw) + 2 * c;
+  const f32x4 w0 = wp[0], w1 = wp[1];
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = f32_to_bf16(f[j] * inv * w0[j]);
+    o[j + 4] = f32_to_bf16(f[j + 4] * inv * w1[j]);
+  }
+  if (valid) *p = o;
+}
+
 void launch_qk_rmsnorm(void* qkv, long stride, const float* qw, const float* kw, int T, int nq, int nkv, int D,
                        float eps, hipStream_t s) {
   const long items = (long)T * (nq + nkv);
   if (items <= 0) return;
-  qk_rmsnorm_kernel<<<dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s>>>(static_cast<unsigned short*>(qkv), stride,
-                                                                           qw, kw, T, nq, nkv, D, eps);
+  auto* q = static_cast<unsigned short*>(qkv);
+  const bool vec = stride % 8 == 0 && (D == 64 || D == 128 || D == 256);
+  if (vec) {
+    const int hpw = 64 / (D / 8);  // heads per wave
+    const long waves = (items + hpw - 1) / hpw;
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    if (D == 64) qk_rmsnorm_vec_kernel<8><<<grid, 256, 0, s>>>(q, stride, qw, kw, T, nq, nkv, eps);
+    else if (D == 128) qk_rmsnorm_vec_kernel<16><<<grid, 256, 0, s>>>(q, stride, qw, kw, T, nq, nkv, eps);
+    else qk_rmsnorm_vec_kernel<32><<<grid, 256, 0, s>>>(q, stride, qw, kw, T, nq, nkv, eps);
+    return;
+  }
+  qk_rmsnorm_kernel<<<dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s>>>(q, stride, qw, kw, T, nq, nkv, D, eps);
 }
 
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
