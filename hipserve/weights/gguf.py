@@ -167,17 +167,24 @@ class GGUFFile:
         if md.get("tokenizer.ggml.eot_token_id") is not None:
             eos_ids.add(int(md["tokenizer.ggml.eot_token_id"]))
         n_exp = int(g("expert_count", 0) or 0)
+        if a not in GGUF_ARCHS:
+            raise NotImplementedError(f"GGUF architecture {a!r} (supported: {', '.join(GGUF_ARCHS)})")
+        if int(g("rope.dimension_count", head_dim) or head_dim) != head_dim:
+            raise NotImplementedError("partial rotary embeddings are not supported")
+        fam = {"llama": "mixtral" if n_exp else "llama"}.get(a, a)
         return ModelConfig(
             name=name or md.get("general.name", os.path.basename(self.path)),
-            architecture="mixtral" if n_exp else "llama",
+            architecture="mixtral" if n_exp else "llama", family=fam,
             hidden_size=H, num_layers=int(g("block_count")), num_heads=nh,
             num_kv_heads=int(g("attention.head_count_kv", nh)), head_dim=head_dim,
             intermediate_size=int(g("feed_forward_length")), vocab_size=V,
             rms_norm_eps=float(g("attention.layer_norm_rms_epsilon", 1e-5)),
-            rope_theta=float(g("rope.freq_base", 10000.0)), rope_mode=1,
+            # llama.cpp permutes llama q/k rows for interleaved RoPE; phi3 / qwen run NeoX RoPE
+            rope_theta=float(g("rope.freq_base", 10000.0)), rope_mode=1 if a == "llama" else 0,
             max_position_embeddings=int(g("context_length", 4096)),
             tie_word_embeddings="output.weight" not in self.tensors,
             num_experts=n_exp, num_experts_per_tok=int(g("expert_used_count", 0) or 0),
+            qkv_bias=a == "qwen2", qk_norm=a == "qwen3",
             bos_token_id=int(md.get("tokenizer.ggml.bos_token_id", 1)),
             eos_token_id=tuple(sorted(eos_ids)))
 
@@ -626,6 +633,11 @@ class GGUFTokenizer:
 
 
 # ------------------------------------------------------------------ loading
+# llama.cpp architectures the GGUF tier serves (the reference's GGUF chart runs
+# TinyLlama (llama) and Phi-3-mini (phi3): ramalama-models/helm-chart/values.yaml:3-19)
+GGUF_ARCHS = ("llama", "phi3", "qwen2", "qwen3")
+
+
 def gguf_name_map(layer: int) -> dict:
     p = f"blk.{layer}."
     return {"attn_norm": p + "attn_norm.weight", "q": p + "attn_q.weight", "k": p + "attn_k.weight",
@@ -666,9 +678,18 @@ def load_gguf_weights(model, path: str):
     model.layers = []
     for i in range(cfg.num_layers):
         n = gguf_name_map(i)
-        lw = LayerWeights(ln1=norm(n["attn_norm"]), wqkv=matrix(n["q"], n["k"], n["v"]),
-                          wo=matrix(n["o"]), ln2=norm(n["ffn_norm"]),
-                          wgu=matrix(n["gate"], n["up"]), wd=matrix(n["down"]))
+        p = f"blk.{i}."
+        # phi3: fused attn_qkv [q; k; v] and ffn_up holding [gate; up] (no ffn_gate)
+        qkv = matrix(p + "attn_qkv.weight") if p + "attn_qkv.weight" in gf.tensors else \
+            matrix(n["q"], n["k"], n["v"])
+        gu = matrix(n["gate"], n["up"]) if n["gate"] in gf.tensors else matrix(n["up"])
+        lw = LayerWeights(ln1=norm(n["attn_norm"]), wqkv=qkv, wo=matrix(n["o"]), ln2=norm(n["ffn_norm"]),
+                          wgu=gu, wd=matrix(n["down"]))
+        if cfg.qkv_bias:  # qwen2
+            lw.bqkv = torch.cat([dense(p + f"attn_{x}.bias") for x in ("q", "k", "v")]).contiguous()
+        if cfg.qk_norm:  # qwen3
+            lw.q_norm = torch.from_numpy(gf.tensor_f32(p + "attn_q_norm.weight").astype(np.float32)).to(dev)
+            lw.k_norm = torch.from_numpy(gf.tensor_f32(p + "attn_k_norm.weight").astype(np.float32)).to(dev)
         model.layers.append(lw)
     from ..ops.quant import quant_linear
 

@@ -88,6 +88,74 @@ def test_greedy_matches_transformers(tmp_path, family):
             assert row[t] >= row.max() - 1e-4, (family, i, t, int(row.argmax()), float(row.max() - row[t]))
 
 
+def _hf_to_gguf(m, family, path):
+    """Write the HF model's tensors as an F32 GGUF of llama.cpp's layout for
+    ``family`` (phi3: fused attn_qkv and ffn_up = [gate; up]; qwen2: q/k/v biases;
+    qwen3: attn_q_norm / attn_k_norm)."""
+    import numpy as np
+
+    from hipserve.weights import gguf as G
+
+    c = m.config
+    sd = {k: v.detach().float().numpy() for k, v in m.state_dict().items()}
+    H, V, L = c.hidden_size, c.vocab_size, c.num_hidden_layers
+    D = getattr(c, "head_dim", None) or H // c.num_attention_heads
+    a = family
+    toks = ["<unk>", "<s>", "</s>"] + [f"<0x{b:02X}>" for b in range(256)] + [f"▁w{i}" for i in range(V - 259)]
+    md = {"general.architecture": a, "general.name": f"tiny-{a}", f"{a}.context_length": 512,
+          f"{a}.embedding_length": H, f"{a}.block_count": L, f"{a}.feed_forward_length": c.intermediate_size,
+          f"{a}.attention.head_count": c.num_attention_heads,
+          f"{a}.attention.head_count_kv": c.num_key_value_heads, f"{a}.attention.key_length": D,
+          f"{a}.rope.freq_base": float(c.rope_parameters["rope_theta"]), f"{a}.rope.dimension_count": D,
+          f"{a}.attention.layer_norm_rms_epsilon": float(c.rms_norm_eps),
+          "tokenizer.ggml.model": "llama", "tokenizer.ggml.tokens": toks,
+          "tokenizer.ggml.scores": [float(-i) for i in range(len(toks))],
+          "tokenizer.ggml.token_type": [3 if i < 3 else (6 if i < 259 else 1) for i in range(len(toks))],
+          "tokenizer.ggml.bos_token_id": 1, "tokenizer.ggml.eos_token_id": 2}
+    t = [("token_embd.weight", sd["model.embed_tokens.weight"], G.F32),
+         ("output_norm.weight", sd["model.norm.weight"], G.F32), ("output.weight", sd["lm_head.weight"], G.F32)]
+    for i in range(L):
+        p, b = f"model.layers.{i}.", f"blk.{i}."
+        t += [(b + "attn_norm.weight", sd[p + "input_layernorm.weight"], G.F32),
+              (b + "ffn_norm.weight", sd[p + "post_attention_layernorm.weight"], G.F32),
+              (b + "attn_output.weight", sd[p + "self_attn.o_proj.weight"], G.F32),
+              (b + "ffn_down.weight", sd[p + "mlp.down_proj.weight"], G.F32)]
+        if a == "phi3":
+            t += [(b + "attn_qkv.weight", sd[p + "self_attn.qkv_proj.weight"], G.F32),
+                  (b + "ffn_up.weight", sd[p + "mlp.gate_up_proj.weight"], G.F32)]
+        else:
+            t += [(b + f"attn_{x}.weight", sd[p + f"self_attn.{x}_proj.weight"], G.F32) for x in "qkv"]
+            t += [(b + "ffn_gate.weight", sd[p + "mlp.gate_proj.weight"], G.F32),
+                  (b + "ffn_up.weight", sd[p + "mlp.up_proj.weight"], G.F32)]
+        if a == "qwen2":
+            t += [(b + f"attn_{x}.bias", sd[p + f"self_attn.{x}_proj.bias"], G.F32) for x in "qkv"]
+        if a == "qwen3":
+            t += [(b + "attn_q_norm.weight", sd[p + "self_attn.q_norm.weight"], G.F32),
+                  (b + "attn_k_norm.weight", sd[p + "self_attn.k_norm.weight"], G.F32)]
+    G.write_gguf(path, md, [(n, np.ascontiguousarray(x), q) for n, x, q in t])
+    return path
+
+
+@pytest.mark.parametrize("family", ["phi3", "qwen2", "qwen3"])
+def test_gguf_family_matches_transformers(tmp_path, family):
+    """GGUF tier (llama-server role) for the non-llama llama.cpp architectures,
+    incl. the reference's Phi-3-mini (ramalama-models/helm-chart/values.yaml:13-19):
+    an F32 GGUF of the same weights greedy-decodes like transformers."""
+    m, _ = _build(tmp_path, family)
+    p = _hf_to_gguf(m, family, str(tmp_path / f"{family}.gguf"))
+    eng = LLMEngine(EngineConfig(model=p, device="cpu", dtype="float32", load_format="gguf", max_num_seqs=4,
+                                 max_num_batched_tokens=24, num_kv_blocks=128, max_model_len=256), tp=TPGroup())
+    assert eng.runner.model.cfg.family == family and eng.runner.model.cfg.rope_mode == 0
+    prompts = [[1, 5, 9, 33, 70, 100], list(range(3, 40))]
+    res = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
+    for pr, (toks, _, _) in zip(prompts, res):
+        with torch.no_grad():
+            lg = m(torch.tensor([list(pr) + list(toks)])).logits[0].float()
+        for i, t in enumerate(toks):
+            row = lg[len(pr) - 1 + i]
+            assert row[t] >= row.max() - 1e-3, (family, i, t, int(row.argmax()))
+
+
 def test_gemma3_hub_config_keys():
     """Hub-style Gemma-3 config.json (rope_theta / rope_local_base_freq / rope_scaling /
     sliding_window_pattern, multimodal text_config wrapper) maps to the same layout."""
