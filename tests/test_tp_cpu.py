@@ -84,6 +84,23 @@ def test_tp_matches_tp1(tmp_path, preset, world):
     assert got == want
 
 
+@pytest.mark.parametrize("family", ["qwen2", "qwen3_moe", "gemma3", "phi3"])
+def test_tp_families_match_tp1(tmp_path, family):
+    """TP=2 sharding of the family extras: Qwen2 q/k/v biases, Qwen3 q/k norms +
+    MoE experts split along the expert width, Gemma-3 sandwich norms after the TP
+    reduction + sliding-window layers, Phi-3 fused qkv / gate_up split per rank."""
+    pytest.importorskip("transformers")
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.parallel.comm import TPGroup
+    from tests.test_hf_parity import _build
+
+    _, ckpt = _build(tmp_path, family)
+    ref = LLMEngine(_cfg(ckpt, 1), tp=TPGroup())
+    want = [r[0] for r in ref.generate(PROMPTS, SamplingParams(temperature=0.0, max_tokens=8,
+                                                                ignore_eos=True))]
+    assert _run_tp(ckpt, 2) == want
+
+
 @pytest.mark.parametrize("preset,world", [("tiny-llama", 2), ("tiny-mixtral", 4)])
 def test_dummy_weights_tp_invariant(preset, world):
     """On-device synthetic init (K16) is keyed by global coordinates: a TP=N engine
