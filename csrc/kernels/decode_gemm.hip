@@ -331,6 +331,9 @@ static bool dg_steps(void* out, long out_stride, float* ws, const void* x, long 
     case 7: dg_launch<MT, RT, 7, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
     case 8: dg_launch<MT, RT, 8, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
     case 16: dg_launch<MT, RT, 16, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    // K = 3072 (Phi-3, Llama-3.2-3B) and K = 5376 (Gemma-3-27B) in one K slice
+    case 12: dg_launch<MT, RT, 12, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    case 21: dg_launch<MT, RT, 21, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
     default: return false;
   }
 }
@@ -351,7 +354,7 @@ static bool dg_dispatch(void* out, long out_stride, float* ws, const void* x, lo
   return false;
 }
 
-// K slice per workgroup = K / S must be 256 * {1, 2, 4, 7, 8, 16}; false otherwise.
+// K slice per workgroup = K / S must be 256 * {1, 2, 4, 7, 8, 12, 16, 21}; false otherwise.
 // packed: w is the pack_decode_weight layout (N rounded up to 128 rows).
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, bool packed, int flags, hipStream_t s) {

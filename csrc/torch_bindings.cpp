@@ -288,7 +288,7 @@ void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::
   TORCH_CHECK(hipserve::launch_decode_gemm(out.data_ptr(), out.stride(0),
                                            splits > 1 ? ws.data_ptr<float>() : nullptr, x.data_ptr(), x.stride(0),
                                            w.data_ptr(), M, N, K, rt, splits, false, 0, cur_stream()),
-              "decode_gemm: unsupported (rt, K/splits): rt in {1,2}, K/splits = 256*{1,2,4,7,8,16}");
+              "decode_gemm: unsupported (rt, K/splits): rt in {1,2}, K/splits = 256*{1,2,4,7,8,12,16,21}");
 }
 
 // Packed weights: wp = pack_decode_weight(w[N, K]) (flat, ceil(N/128)*128*K bf16).

@@ -23,7 +23,7 @@ SKINNY_CONFIGS = [(1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (2, 1), (2, 2), (2, 4
 # split-K MFMA GEMM with an LDS-staged x chunk shared by 64 rows (gguf.hip, qtype 6 = bf16)
 SPLITK_CONFIGS = [1, 2, 4, 8]
 DG_RT = [1, 2]
-DG_STEPS = [1, 2, 4, 7, 8, 16]  # 256-k steps per workgroup (compile-time in decode_gemm.hip)
+DG_STEPS = [1, 2, 4, 7, 8, 12, 16, 21]  # 256-k steps per workgroup (compile-time in decode_gemm.hip)
 # decode weights pre-shuffled for the packed decode GEMM, keyed by the plain
 # weight's data_ptr (the plain [N, K] copy stays for prefill / hipBLASLt)
 PACKED: dict[int, tuple] = {}  # data_ptr -> (weakref to the plain weight, packed copy)
