@@ -96,6 +96,16 @@ class ModelRunner:
             if ecfg.extra.get("packed_decode", True):
                 self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
             torch.cuda.empty_cache()
+        # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
+        # budget (measured no faster than the heuristic on sustained prefill chains,
+        # profiles/r1_prefill_gemm_tunableop.md)
+        self.prefill_gemm_report = []
+        if self.device.type == "cuda" and ecfg.extra.get("prefill_gemm_tune", False):
+            from ..ops import prefill_tune
+
+            shapes = [s for s in self.model.gemm_shapes() if s != tuple(getattr(self.model.lm_head, "shape", ()))]
+            self.prefill_gemm_report = prefill_tune.tune(shapes, [ecfg.max_num_batched_tokens], self.device)
+            torch.cuda.empty_cache()
         self.num_blocks = self._num_kv_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.block_size)
         self.pad_block = self.num_blocks - 1          # scratch block for graph padding rows

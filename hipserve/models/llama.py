@@ -265,13 +265,27 @@ class LlamaModel:
         gate/up-interleaved instead (``PACKED_GLU``: the SiLU-GLU runs in its epilogue)."""
         n = 0
         glu = self.fused_decode and self.tp.world_size == 1 and self.vanilla
+        # HBM budget: a packed copy is only made while >= 24 GiB + a quarter of the
+        # device stay free for the KV cache (a 70B model on ONE 288 GB MI355X keeps
+        # most weights unpacked; the tuner's packed choice then runs on the plain layout)
+        reserve = 24 << 30
+        if self.device.type == "cuda":
+            reserve += torch.cuda.get_device_properties(self.device).total_memory // 4
+
+        def fits(w):
+            if self.device.type != "cuda":
+                return True
+            free, _ = torch.cuda.mem_get_info(self.device)
+            return free - w.numel() * w.element_size() >= reserve
+
         for lw in self.layers:
             for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
-                if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
+                if (isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes
+                        and fits(w)):
                     gemm.register_packed(w, glu=glu and w is lw.wgu and w.shape[0] % 128 == 0)
                     n += w.numel() * w.element_size()
         w = self.lm_head
-        if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes:
+        if isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes and fits(w):
             gemm.register_packed(w)
             n += w.numel() * w.element_size()
         return n + self.pack_moe_weights()
