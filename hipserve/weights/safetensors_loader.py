@@ -49,17 +49,30 @@ class _Ckpt:
         for h in self.handles:
             for k in h.keys():
                 self.where[k] = h
+        # integer weight-only checkpoints (weights/int_quant.py): "<x>.weight" is a
+        # virtual tensor dequantised from "<x>.weight_packed" / "<x>.qweight"
+        self.bits = _quant_bits(path)
+        self.virtual = {}
+        for k in list(self.where):
+            for suf, kind in ((".weight_packed", "ct"), (".qweight", "awq")):
+                if k.endswith(suf) and k[: -len(suf)] + ".weight" not in self.where:
+                    self.virtual[k[: -len(suf)] + ".weight"] = (kind, k[: -len(suf)])
 
     def has(self, name):
-        return name in self.where
+        return name in self.where or name in self.virtual
 
     def find(self, suffix) -> str | None:
-        for k in self.where:
+        for k in list(self.where) + list(self.virtual):
             if k.endswith(suffix):
                 return k
         return None
 
+    def _get(self, name):
+        return self.where[name].get_tensor(name) if name in self.where else None
+
     def full(self, name) -> torch.Tensor:
+        if name in self.virtual:
+            return self._dequant_int(name)
         t = self.where[name].get_tensor(name)
         return self._dequant(name, t) if t.dtype in _FP8 else t
 
@@ -74,7 +87,21 @@ class _Ckpt:
         return self.where[name].get_slice(name)[:, start:stop]
 
     def _is_fp8(self, name) -> bool:
+        """True for every tensor that must be dequantised whole before slicing."""
+        if name in self.virtual:
+            return True
         return self.where[name].get_slice(name).get_dtype() in ("F8_E4M3", "F8_E5M2")
+
+    def _dequant_int(self, name) -> torch.Tensor:
+        from . import int_quant
+
+        kind, base = self.virtual[name]
+        if kind == "awq":
+            return int_quant.dequant_awq(self._get(base + ".qweight"), self._get(base + ".qzeros"),
+                                         self._get(base + ".scales"))
+        return int_quant.dequant_pack_quantized(
+            self._get(base + ".weight_packed"), self._get(base + ".weight_scale"),
+            self._get(base + ".weight_zero_point"), self._get(base + ".weight_shape"), self.bits)
 
     def _dequant(self, name, t) -> torch.Tensor:
         """FP8 checkpoints (compressed-tensors "FP8-Dynamic" / block-FP8): weights
@@ -91,6 +118,21 @@ class _Ckpt:
                 s = s.repeat_interleave(bn, 0)[: w.shape[0]].repeat_interleave(bk, 1)[:, : w.shape[1]]
                 return w * s
         raise ValueError(f"FP8 tensor {name} without weight_scale / weight_scale_inv")
+
+
+def _quant_bits(path: str) -> int | None:
+    """Weight bit width from config.json's quantization_config (compressed-tensors
+    ``config_groups.*.weights.num_bits`` or AWQ ``bits``); None if absent."""
+    try:
+        with open(os.path.join(path, "config.json")) as f:
+            q = json.load(f).get("quantization_config") or {}
+    except (OSError, ValueError):
+        return None
+    for grp in (q.get("config_groups") or {}).values():
+        w = grp.get("weights") or {}
+        if w.get("num_bits"):
+            return int(w["num_bits"])
+    return int(q["bits"]) if q.get("bits") else None
 
 
 _FP8 = tuple(getattr(torch, n) for n in ("float8_e4m3fn", "float8_e5m2") if hasattr(torch, n))
