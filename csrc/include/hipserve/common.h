@@ -125,4 +125,38 @@ HS_DEVICE int xcd_remap(int bid, int nwg) {
   return base + bid / kXcd;
 }
 
+// Sum of S split-K slices of 8 consecutive fp32 partials (p, p + slice, ...),
+// accumulated in slice order 0, 1, 2, ... into (lo, hi). Loads go out in batches
+// of 8 slices with no branch or use between them: a plain load-add loop over a
+// runtime S compiles to one s_waitcnt per slice — S serial HBM round trips
+// (~0.7 us each), which is what made the decode split-K epilogues ~5.7 us at
+// S = 8. Slices past S re-read slice S-1 (a cache hit, discarded).
+constexpr int kSliceBatch = 8;
+
+HS_DEVICE void sum_slices8(f32x4& lo, f32x4& hi, const float* __restrict__ p, long slice, int S) {
+  for (int s0 = 0; s0 < S; s0 += kSliceBatch) {
+    f32x4 a[kSliceBatch], b[kSliceBatch];
+#pragma unroll
+    for (int j = 0; j < kSliceBatch; ++j) {
+      const float* q = p + min(s0 + j, S - 1) * slice;
+      a[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q));
+      b[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q + 4));
+    }
+    if (s0 == 0) {
+      lo = a[0];
+      hi = b[0];
+    } else {
+      lo += a[0];
+      hi += b[0];
+    }
+#pragma unroll
+    for (int j = 1; j < kSliceBatch; ++j) {
+      if (s0 + j < S) {
+        lo += a[j];
+        hi += b[j];
+      }
+    }
+  }
+}
+
 }  // namespace hipserve

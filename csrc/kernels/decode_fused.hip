@@ -17,14 +17,11 @@
 
 namespace hipserve {
 
-// sum over S slices of 8 consecutive fp32 partials, rounded to bf16 like the
-// unfused reduce output, returned as fp32
+// sum over S slices of 8 consecutive fp32 partials (batched loads, common.h),
+// rounded to bf16 like the unfused reduce output, returned as fp32
 HS_DEVICE void sum8_bf16(float (&o)[8], const float* __restrict__ p, long slice, int S) {
-  f32x4 lo = *reinterpret_cast<const f32x4*>(p), hi = *reinterpret_cast<const f32x4*>(p + 4);
-  for (int s = 1; s < S; ++s) {
-    lo += *reinterpret_cast<const f32x4*>(p + s * slice);
-    hi += *reinterpret_cast<const f32x4*>(p + s * slice + 4);
-  }
+  f32x4 lo, hi;
+  sum_slices8(lo, hi, p, slice, S);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     o[j] = bf16_to_f32(f32_to_bf16(lo[j]));
@@ -42,25 +39,25 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
   const int row = blockIdx.x;
   const int nvec = N >> 3;
   const long slice = (long)M * N;
-  // the norm weight does not depend on the reduction: issue its loads first
-  float w[VPT][8];
+  // the norm weight and the residual do not depend on the reduction: issue their
+  // loads first and keep them raw, so no s_waitcnt sits in front of the partials
+  f32x4 wf[VPT][2];
+  u16x8 wb[VPT], res[VPT];
+  u16x8* rr = reinterpret_cast<u16x8*>(residual + (long)row * N);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * NT;
     if (idx < nvec) {
       if constexpr (kWF32) {
         const f32x4* wp = reinterpret_cast<const f32x4*>(weight) + idx * 2;
-        const f32x4 w0 = wp[0], w1 = wp[1];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { w[i][j] = w0[j]; w[i][j + 4] = w1[j]; }
+        wf[i][0] = wp[0];
+        wf[i][1] = wp[1];
       } else {
-        const u16x8 wv = reinterpret_cast<const u16x8*>(weight)[idx];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w[i][j] = bf16_to_f32(wv[j]);
+        wb[i] = reinterpret_cast<const u16x8*>(weight)[idx];
       }
+      res[i] = rr[idx];
     }
   }
-  u16x8* rr = reinterpret_cast<u16x8*>(residual + (long)row * N);
   float v[VPT][8];
   float ss = 0.f;
 #pragma unroll
@@ -69,11 +66,10 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
     if (idx < nvec) {
       float h[8];
       sum8_bf16(h, ws + (long)row * N + idx * 8, slice, S);
-      const u16x8 b = rr[idx];
       u16x8 r;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        r[j] = f32_to_bf16(h[j] + bf16_to_f32(b[j]));
+        r[j] = f32_to_bf16(h[j] + bf16_to_f32(res[i][j]));
         v[i][j] = bf16_to_f32(r[j]);
         ss += v[i][j] * v[i][j];
       }
@@ -89,7 +85,12 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
     if (idx < nvec) {
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv * w[i][j]);
+      for (int j = 0; j < 8; ++j) {
+        float wj;
+        if constexpr (kWF32) wj = wf[i][j >> 2][j & 3];
+        else wj = bf16_to_f32(wb[i][j]);
+        o[j] = f32_to_bf16(v[i][j] * inv * wj);
+      }
       orow[idx] = o;
     }
   }

@@ -259,11 +259,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(unsigned short* __re
   const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
   if (i >= (long)M * N) return;
   const int m = i / N, n = i - (long)m * N;
-  f32x4 lo = *reinterpret_cast<const f32x4*>(ws + i), hi = *reinterpret_cast<const f32x4*>(ws + i + 4);
-  for (int s = 1; s < S; ++s) {
-    lo += *reinterpret_cast<const f32x4*>(ws + (long)s * M * N + i);
-    hi += *reinterpret_cast<const f32x4*>(ws + (long)s * M * N + i + 4);
-  }
+  f32x4 lo, hi;
+  sum_slices8(lo, hi, ws + i, (long)M * N, S);
   u32x4 o;
   o[0] = pack_bf16x2(lo[0], lo[1]);
   o[1] = pack_bf16x2(lo[2], lo[3]);

@@ -214,11 +214,8 @@ __global__ __launch_bounds__(256) void moe_combine_partial_kernel(unsigned short
     for (int j = 0; j < k; ++j) {
       const float wt = w[(long)t * k + j];
       const float* p = ws + (long)pair_slot[t * k + j] * H + 8 * c;
-      f32x4 lo = *reinterpret_cast<const f32x4*>(p), hi = *reinterpret_cast<const f32x4*>(p + 4);
-      for (int s = 1; s < S; ++s) {
-        lo += *reinterpret_cast<const f32x4*>(p + s * slab);
-        hi += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
-      }
+      f32x4 lo, hi;
+      sum_slices8(lo, hi, p, slab, S);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         acc[e] += wt * bf16_to_f32(f32_to_bf16(lo[e]));
