@@ -15,6 +15,12 @@ OpenAI server with SSE streaming.
 
 Rank 0 prints ONE JSON line; value = total output tokens/s over all ranks
 (time = max over ranks of the K timed waves, barrier + device sync on both sides).
+
+``--tp T`` (T = the torchrun world size) instead serves ONE model sharded over the
+T ranks — BASELINE.json's "Llama-3-70B TP=8 over xGMI" config:
+``torchrun --nproc-per-node 8 bench.py --model llama-3-70b --tp 8``. Rank 0 runs
+the engine, the HTTP stack and the load generator; ranks 1..T-1 run the TP worker
+loop (hipserve/server/cli.py ``_worker``), exactly as a TP pod does.
 """
 from __future__ import annotations
 
@@ -62,8 +68,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
+    if args.tp > 1 and args.tp != world:
+        raise SystemExit(f"--tp {args.tp} needs a torchrun world size of {args.tp} (got {world})")
+    tp_mode = args.tp > 1
+    leader = not tp_mode or rank == 0
     stack = lg = None
-    if args.path == "gateway":
+    if args.path == "gateway" and leader:
         # client-side processes start BEFORE this process touches the GPU
         from hipserve.bench.local_stack import GatewayStack, LoadgenProc, free_port, wait_http
 
@@ -71,34 +81,50 @@ def main():
         stack = GatewayStack({args.model: [eport]}).start()
         lg = LoadgenProc()
 
-    if world > 1:
+    from hipserve.config import EngineConfig
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.engine.request import SamplingParams
+    from hipserve.parallel.comm import TPGroup, init_tp
+
+    tpg = None
+    if tp_mode:
+        tpg = init_tp(world)  # RCCL group + shm step ring + custom all-reduce
+    elif world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
     dev = torch.device("cuda", local)
-
-    from hipserve.config import EngineConfig
-    from hipserve.engine.llm_engine import LLMEngine
-    from hipserve.engine.request import SamplingParams
-    from hipserve.parallel.comm import TPGroup
-
-    if args.tp != 1:
-        raise SystemExit("bench.py measures TP=1 replicas; TP>1 runs via `python -m hipserve.server`")
     cfg = EngineConfig(model=args.model, device="cuda", max_num_seqs=max(args.concurrency, 1),
+                       tensor_parallel_size=args.tp,
                        max_num_batched_tokens=args.max_num_batched_tokens,
                        max_model_len=args.input_len + args.output_len + 64,
-                       enforce_eager=args.enforce_eager, seed=rank,
+                       enforce_eager=args.enforce_eager, seed=0 if tp_mode else rank,
                        load_format="dummy" if args.quantization else "auto",
                        extra={"quantization": args.quantization} if args.quantization else {})
+    if tp_mode and not leader:
+        from hipserve.config import resolve_model_config
+        from hipserve.engine.llm_engine import worker_loop
+        from hipserve.engine.model_runner import ModelRunner
+
+        from hipserve.tokenizer import get_tokenizer
+
+        mcfg = resolve_model_config(cfg.model, cfg.served_model_name)
+        tk = get_tokenizer(cfg.model, mcfg, cfg.tokenizer)  # GGUF: the file's own hyper-parameters
+        mcfg = getattr(tk, "model_config_override", None) or mcfg
+        worker_loop(ModelRunner(cfg, mcfg, tpg), tpg)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     t0 = time.time()
-    engine = LLMEngine(cfg, tp=TPGroup(0, 1, None, dev))
+    engine = LLMEngine(cfg, tp=tpg if tp_mode else TPGroup(0, 1, None, dev))
     init_s = time.time() - t0
+    dp = world > 1 and not tp_mode  # independent replicas: cross-rank barriers and sums
     rng = np.random.default_rng(1234 + rank)
     V = engine.model_cfg.vocab_size
 
     def barrier():
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if dp:  # TP workers sit in their step loop: the engine's own collectives sync them
             dist.barrier()
         torch.cuda.synchronize(dev)
 
@@ -147,7 +173,7 @@ def main():
 
     stats = torch.tensor([elapsed, float(tok_total)], dtype=torch.float64, device=dev)
     p50 = torch.tensor([statistics.median(ttfts)], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dp:
         el = stats[:1].clone()
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         tk = stats[1:].clone()
@@ -176,13 +202,13 @@ def main():
         "path": args.path,
         "config": {
             "model": args.model + (f" GGUF {args.quantization.upper()}" if args.quantization else ""),
-            "tp": 1,
-            "global_batch": args.concurrency * world,
+            "tp": args.tp,
+            "global_batch": args.concurrency * (world // args.tp),
             "seq_len": args.input_len + args.output_len,
             "input_len": args.input_len,
             "output_len": args.output_len,
             "concurrency_per_gpu": args.concurrency,
-            "parallelism": f"dp{world}" if world > 1 else "tp1",
+            "parallelism": f"tp{args.tp}" if tp_mode else (f"dp{world}" if world > 1 else "tp1"),
             "sampling": {"temperature": args.temperature, "top_p": args.top_p},
         },
         "engine_init_s": round(init_s, 1),
@@ -191,6 +217,8 @@ def main():
     if lg is not None:
         lg.close()
         stack.stop()
+    if tp_mode:
+        engine.shutdown()  # releases the workers from worker_loop
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
