@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0"],
                     help="GGUF tier: random-init GGUF-quantised weights (BASELINE config: Llama-3-8B Q4_K_M)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: fp32 on the host with gloo collectives (tests of the DP / TP paths)")
+    ap.add_argument("--num-kv-blocks", type=int, default=None, help="KV pool size (default: from HBM)")
     return ap.parse_args()
 
 
@@ -86,15 +89,18 @@ def main():
     from hipserve.engine.request import SamplingParams
     from hipserve.parallel.comm import TPGroup, init_tp
 
+    cuda = args.device == "cuda"
     tpg = None
     if tp_mode:
-        tpg = init_tp(world)  # RCCL group + shm step ring + custom all-reduce
+        tpg = init_tp(world, device_type=args.device)  # RCCL group + shm step ring + custom all-reduce
     elif world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    dev = torch.device("cuda", local)
-    cfg = EngineConfig(model=args.model, device="cuda", max_num_seqs=max(args.concurrency, 1),
+        if cuda:
+            torch.cuda.set_device(local)
+        dist.init_process_group("nccl" if cuda else "gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", local) if cuda else torch.device("cpu")
+    cfg = EngineConfig(model=args.model, device=args.device, max_num_seqs=max(args.concurrency, 1),
+                       dtype="bfloat16" if cuda else "float32", num_kv_blocks=args.num_kv_blocks,
                        tensor_parallel_size=args.tp,
                        max_num_batched_tokens=args.max_num_batched_tokens,
                        max_model_len=args.input_len + args.output_len + 64,
@@ -122,11 +128,15 @@ def main():
     rng = np.random.default_rng(1234 + rank)
     V = engine.model_cfg.vocab_size
 
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
     def barrier():
-        torch.cuda.synchronize(dev)
+        sync()
         if dp:  # TP workers sit in their step loop: the engine's own collectives sync them
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
 
     if args.path == "gateway":
         import asyncio
@@ -194,9 +204,9 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if tp_mode else "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if not args.quantization else f"bf16 activations, GGUF {args.quantization.upper()} weights",
+        "dtype": ("bf16" if cuda else "fp32") if not args.quantization else f"bf16 activations, GGUF {args.quantization.upper()} weights",
         "data": "synthetic prompts (random token ids), random-init weights",
         "p50_ttft_ms": round(1000 * float(p50), 2),
         "path": args.path,

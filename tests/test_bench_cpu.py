@@ -1,0 +1,52 @@
+"""bench.py's launch contract on CPU: the single-process run, the
+driver's multi-rank form (``torch.distributed.run --nproc-per-node N``: one DP
+replica per rank, barriers + max-over-ranks timing, summed tokens) and ``--tp``
+(one model sharded over the ranks: rank 0 engine + HTTP stack, ranks > 0 in the TP
+worker loop), over gloo with a tiny random-init Llama. The GPU form is the same
+code with RCCL; the driver runs it on MI355X."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--device", "cpu", "--model", "tiny-llama", "--concurrency", "2", "--input-len", "16",
+        "--output-len", "4", "--steps", "1", "--warmup", "1", "--num-kv-blocks", "256"]
+
+
+def _run(cmd):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints exactly one line
+    return lines[0]
+
+
+def _torchrun(n, port, extra):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(n)] + extra
+
+
+def test_bench_single_process_gateway():
+    out = _run([sys.executable, "bench.py"] + ARGS)
+    assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "tp1" and out["path"] == "gateway"
+    assert out["value"] > 0 and out["p50_ttft_ms"] > 0 and out["steps"] == 1 and out["warmup"] == 1
+    assert abs(out["value"] - 2 * 4 / (out["ms_per_step"] / 1000)) / out["value"] < 0.01
+
+
+@pytest.mark.parametrize("tp", [1, 2])
+def test_bench_two_ranks(tp):
+    out = _run(_torchrun(2, 29650 + tp, ARGS + ["--tp", str(tp)]))
+    assert out["n_gpus"] == 2
+    if tp == 1:  # weak scaling: two replicas, tokens summed over ranks
+        assert out["config"]["parallelism"] == "dp2" and out["scaling"] == "weak"
+        assert out["config"]["global_batch"] == 4
+        tokens = 2 * 2 * 4
+    else:  # one replica sharded over both ranks
+        assert out["config"]["parallelism"] == "tp2" and out["scaling"] == "strong"
+        assert out["config"]["tp"] == 2 and out["config"]["global_batch"] == 2
+        tokens = 2 * 4
+    assert abs(out["value"] - tokens / (out["ms_per_step"] / 1000)) / out["value"] < 0.01
