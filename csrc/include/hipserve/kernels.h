@@ -122,3 +122,19 @@ bool launch_moe_decode_gemm(void* out, long out_stride, float* ws, const void* x
                             long w_estride, const int* slots, const int* tile_expert, int tiles_cap, int tile,
                             int gather_k, int N, int K, int S, bool packed, bool glu, hipStream_t s);
 }  // namespace hipserve
+
+namespace hipserve {
+
+// stage_copy.hip — up to 8 word-aligned copies in one dispatch; host_mask bit 2i / 2i+1
+// marks copy i's src / dst as pinned host memory (device-mapped pointers).
+constexpr int kMaxStageCopies = 8;
+struct StageCopyArgs {
+  void* dst[kMaxStageCopies];
+  const void* src[kMaxStageCopies];
+  long words[kMaxStageCopies];
+  int n;
+  unsigned int host_mask;
+};
+void launch_stage_copy(const StageCopyArgs& a, hipStream_t s);
+
+}  // namespace hipserve

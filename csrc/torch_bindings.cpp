@@ -271,6 +271,38 @@ void fill_uniform(at::Tensor& out, int64_t row0, int64_t col0, int64_t gcols, in
                                 (unsigned int)(key & 0xffffffffu), (float)scale, cur_stream());
 }
 
+// Pinned host tensors are addressed through their device mapping; every pair must
+// match in byte size (a multiple of 4) and be contiguous. Runs on `device`'s
+// current stream.
+void stage_copy(const std::vector<at::Tensor>& dst, const std::vector<at::Tensor>& src, int64_t device) {
+  TORCH_CHECK(dst.size() == src.size() && dst.size() <= (size_t)hipserve::kMaxStageCopies,
+              "stage_copy: matching lists of at most 8 tensors");
+  hipserve::StageCopyArgs a{};
+  a.n = (int)dst.size();
+  auto addr = [](const at::Tensor& t, bool& host) -> void* {
+    TORCH_CHECK(t.is_contiguous(), "stage_copy: tensors must be contiguous");
+    if (t.is_cuda()) { host = false; return t.data_ptr(); }
+    TORCH_CHECK(t.is_pinned(), "stage_copy: host tensors must be pinned");
+    host = true;
+    void* d = nullptr;
+    TORCH_CHECK(hipHostGetDevicePointer(&d, t.data_ptr(), 0) == hipSuccess && d,
+                "stage_copy: pinned tensor has no device mapping");
+    return d;
+  };
+  for (int i = 0; i < a.n; ++i) {
+    const size_t nb = dst[i].nbytes();
+    TORCH_CHECK(nb == src[i].nbytes() && nb % 4 == 0, "stage_copy: pair ", i, " byte sizes differ or not 4-aligned");
+    bool hd = false, hs = false;
+    a.dst[i] = addr(dst[i], hd);
+    a.src[i] = addr(src[i], hs);
+    a.words[i] = (long)(nb / 4);
+    a.host_mask |= (hs ? 1u : 0u) << (2 * i);
+    a.host_mask |= (hd ? 1u : 0u) << (2 * i + 1);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)device);
+  hipserve::launch_stage_copy(a, cur_stream());
+}
+
 void decode_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, at::Tensor& ws, int64_t rt,
                  int64_t splits) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
@@ -521,6 +553,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("car_error(int state) -> bool", &car_error);
   m.def("car_destroy(int state) -> ()", &car_destroy);
   m.def("fill_uniform(Tensor(a!) out, int row0, int col0, int gcols, int key, float scale) -> ()");
+  m.def("stage_copy(Tensor(a!)[] dst, Tensor[] src, int device) -> ()", &stage_copy);
   m.def("decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int rt, int splits) -> ()");
   m.def("decode_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");

@@ -12,6 +12,7 @@ SURVEY §3.B step 4); prefill / mixed batches run eagerly.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -349,6 +350,19 @@ class ModelRunner:
         self.ops.sample(st["tok"][:b], st["lp"][:b], logits, st["temp"][:b], st["topk"][:b],
                         st["topp"][:b], st["seeds"][:b], st["steps"][:b])
 
+    def _stage_in(self, b: int, sg):
+        """Pinned staging set -> device static inputs, one zero-copy dispatch
+        (csrc/kernels/stage_copy.hip); captured at the head of a parity graph."""
+        st, mb, W = self._static, self.buckets[-1], self.width
+        torch.ops.hipserve.stage_copy([st["d64"], st["d32"][: b * W], st["d32"][mb * W:], st["df"]],
+                                      [sg["h64"], sg["h32"][: b * W], sg["h32"][mb * W:], sg["hf"]],
+                                      self.device.index or 0)
+
+    def _stage_out(self, b: int, sg):
+        st = self._static
+        torch.ops.hipserve.stage_copy([sg["tok"][:b], sg["lp"][:b]], [st["tok"][:b], st["lp"][:b]],
+                                      self.device.index or 0)
+
     @torch.inference_mode()
     def _capture_graphs(self):
         mb, W, dev = self.buckets[-1], self.width, self.device
@@ -365,6 +379,8 @@ class ModelRunner:
                 "done": None,
             })
         self._launches = 0
+        # HIPSERVE_STAGE_COPY=blit: per-buffer hipMemcpyAsync instead of the staging kernel
+        self._stage_kernel = os.environ.get("HIPSERVE_STAGE_COPY", "kernel") != "blit"
         d64 = torch.zeros(6 * mb, dtype=torch.long, device=dev)
         d32 = torch.zeros(mb * W + 2 * mb, dtype=torch.int32, device=dev)
         df = torch.zeros(2 * mb, dtype=torch.float32, device=dev)
@@ -394,10 +410,18 @@ class ModelRunner:
         torch.cuda.synchronize(dev)
         self.graph_pool = torch.cuda.graph_pool_handle()
         for b in reversed(self.buckets):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
-                self._graph_forward(b)
-            self.graphs[b] = g
+            # staging kernel: one graph per staging-set parity with the H2D and D2H
+            # copies captured inside, so consecutive steps are back-to-back graphs
+            # (a standalone dispatch after a graph waits ~0.2 ms for the graph's end)
+            for par in ((0, 1) if self._stage_kernel else (None,)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool):
+                    if par is not None:
+                        self._stage_in(b, self._stage[par])
+                    self._graph_forward(b)
+                    if par is not None:
+                        self._stage_out(b, self._stage[par])
+                self.graphs[b if par is None else (b, par)] = g
         torch.cuda.synchronize(dev)
         self.graph_capture_time = time.time() - t0
 
@@ -441,13 +465,16 @@ class ModelRunner:
         af[n:b] = 0.0
         af[mb:mb + n] = inp.top_p
         st = self._static
-        st["d64"].copy_(h64, non_blocking=True)
-        st["d32"][: b * W].copy_(h32[: b * W], non_blocking=True)
-        st["d32"][mb * W:].copy_(h32[mb * W:], non_blocking=True)
-        st["df"].copy_(hf, non_blocking=True)
-        self.graphs[b].replay()
-        sg["tok"][:n].copy_(st["tok"][:n], non_blocking=True)
-        sg["lp"][:n].copy_(st["lp"][:n], non_blocking=True)
+        if self._stage_kernel:  # the graph of this parity stages in/out itself
+            self.graphs[(b, (self._launches - 1) & 1)].replay()
+        else:
+            st["d64"].copy_(h64, non_blocking=True)
+            st["d32"][: b * W].copy_(h32[: b * W], non_blocking=True)
+            st["d32"][mb * W:].copy_(h32[mb * W:], non_blocking=True)
+            st["df"].copy_(hf, non_blocking=True)
+            self.graphs[b].replay()
+            sg["tok"][:n].copy_(st["tok"][:n], non_blocking=True)
+            sg["lp"][:n].copy_(st["lp"][:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         sg["done"] = ev

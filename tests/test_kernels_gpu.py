@@ -258,12 +258,24 @@ def test_sample_distribution(ops):
     assert (cnt[8:] - p).abs().max() < 0.03
 
 
+def _skinny_cases():
+    """(N, K, rt, kw) with K divisible by the kernel's 256*kw K chunk."""
+    return [(n, k, rt, kw)
+            for n, k in [(4096, 4096), (200, 1024), (6144, 4096), (4096, 14336)]
+            for rt, kw in [(1, 1), (1, 4), (1, 8), (2, 2), (2, 8)]
+            if k % (256 * kw) == 0]
+
+
+def _dg_cases(shapes, splits):
+    """(N, K, splits) whose K slice is one of the compiled step counts (DG_STEPS)."""
+    from hipserve.ops.gemm import DG_STEPS
+    return [(n, k, s) for n, k in shapes for s in splits
+            if k % (256 * s) == 0 and k // s // 256 in DG_STEPS]
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (200, 1024), (6144, 4096), (4096, 14336)])
-@pytest.mark.parametrize("rt,kw", [(1, 1), (1, 4), (1, 8), (2, 2), (2, 8)])
+@pytest.mark.parametrize("N,K,rt,kw", _skinny_cases())
 def test_skinny_gemm(ops, M, N, K, rt, kw):
-    if K % (256 * kw):
-        pytest.skip("K not divisible")
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
@@ -287,14 +299,13 @@ def test_splitk_bf16_gemm(ops, M, splits):
 
 
 @pytest.mark.parametrize("M", [1, 7, 16, 23, 32, 50, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 512), (6144, 1792)])
+@pytest.mark.parametrize("N,K,splits", _dg_cases([(4096, 4096), (1000, 512), (6144, 1792),
+                                                  (4096, 3072), (4096, 5376)], [1, 2, 7, 8]))
 @pytest.mark.parametrize("rt", [1, 2])
-@pytest.mark.parametrize("splits", [1, 2, 7, 8])
 def test_decode_gemm(ops, M, N, K, rt, splits):
-    """Split-K LDS-shared decode GEMM vs fp32 torch (incl. ragged M, N tails, strided x)."""
+    """Split-K LDS-shared decode GEMM vs fp32 torch (incl. ragged M, N tails, strided x,
+    and the 12/21-step K slices of Gemma-3's K = 3072 / 5376)."""
     from hipserve.ops.gemm import decode_gemm
-    if K % (256 * splits) or K // splits // 256 not in (1, 2, 4, 7, 8, 16):
-        pytest.skip("unsupported K slice")
     torch.manual_seed(M * 7 + N)
     xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
     x = xb[:, :K]  # row stride != K
@@ -307,15 +318,13 @@ def test_decode_gemm(ops, M, N, K, rt, splits):
 
 
 @pytest.mark.parametrize("M", [1, 16, 23, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 512), (6144, 1792), (4096, 14336)])
+@pytest.mark.parametrize("N,K,splits", _dg_cases([(4096, 4096), (1000, 512), (6144, 1792),
+                                                  (4096, 14336), (4096, 5376)], [1, 2, 8]))
 @pytest.mark.parametrize("rt", [1, 2])
-@pytest.mark.parametrize("splits", [1, 2, 8])
 def test_decode_gemm_packed(ops, M, N, K, rt, splits):
     """Packed-weight decode GEMM (pre-shuffled streaming layout, N padded to 128)
     vs fp32 torch; also checks the packing kernel against a torch permute."""
     from hipserve.ops import gemm
-    if K % (256 * splits) or K // splits // 256 not in (1, 2, 4, 7, 8, 16):
-        pytest.skip("unsupported K slice")
     torch.manual_seed(M * 11 + N + K)
     xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
     x = xb[:, :K]
@@ -381,3 +390,29 @@ def test_fill_uniform_bit_exact(ops, rows, cols, row0, col0, gcols):
     want = ref.fill_uniform(torch.empty(rows, cols, dtype=torch.bfloat16), row0, col0, gcols, 987654321, 0.0346)
     assert torch.equal(view.cpu(), want)
     assert torch.count_nonzero(base[:, :4]) == 0 and torch.count_nonzero(base[:, 4 + cols:]) == 0
+
+
+def test_stage_copy_host_device_roundtrip(ops):
+    """Zero-copy staging kernel: pinned host -> device and device -> pinned host in one
+    dispatch each, with mixed dtypes and sizes, matches torch copies; rewriting the host
+    buffer between launches is seen by the next launch (no stale cached lines)."""
+    h64 = torch.arange(300, dtype=torch.long).pin_memory()
+    h32 = (torch.arange(5000, dtype=torch.int32) * 3).pin_memory()
+    hf = torch.linspace(-1, 1, 17).pin_memory()
+    d64 = torch.zeros(300, dtype=torch.long, device=DEV)
+    d32 = torch.zeros(5000, dtype=torch.int32, device=DEV)
+    df = torch.zeros(17, device=DEV)
+    for it in range(3):
+        h64.add_(7)
+        h32[:4000].mul_(-1)
+        torch.ops.hipserve.stage_copy([d64, d32[:4000], d32[4000:], df], [h64, h32[:4000], h32[4000:], hf], 0)
+        torch.cuda.synchronize()
+        assert torch.equal(d64.cpu(), h64) and torch.equal(d32.cpu(), h32) and torch.equal(df.cpu(), hf)
+    out64 = torch.zeros(300, dtype=torch.long).pin_memory()
+    outf = torch.zeros(17).pin_memory()
+    d64.mul_(3)
+    torch.ops.hipserve.stage_copy([out64, outf], [d64, df], 0)
+    ev = torch.cuda.Event()
+    ev.record()
+    ev.synchronize()
+    assert torch.equal(out64, h64 * 3) and torch.equal(outf, hf)
