@@ -24,7 +24,33 @@ import yaml
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+_next_port = [0]
+
+
+def _bindable(p: int) -> bool:
+    s = socket.socket()
+    try:
+        s.bind(("127.0.0.1", p))
+        return True
+    except OSError:
+        return False
+    finally:
+        s.close()
+
+
 def free_port() -> int:
+    """A free localhost port. Under torchrun (WORLD_SIZE > 1) every local rank scans
+    its own disjoint range, so the N replicas of a DP bench starting at the same
+    moment never pick the same port between probe and bind (the kernel's bind(0)
+    can hand the port one rank just released to the next)."""
+    world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    if world > 1:
+        base = 30000 + 200 * int(os.environ.get("LOCAL_RANK", "0") or 0)
+        while _next_port[0] < 200:
+            p = base + _next_port[0]
+            _next_port[0] += 1
+            if _bindable(p):
+                return p
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
