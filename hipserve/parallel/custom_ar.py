@@ -15,14 +15,17 @@ RCCL path instead of producing wrong sums.
 from __future__ import annotations
 
 import logging
+import os
 
 import torch
 import torch.distributed as dist
 
 log = logging.getLogger("hipserve.custom_ar")
 
-ONE_SHOT_MAX = 256 << 10
-DEFAULT_MAX_BYTES = 8 << 20
+# crossovers (tools/bench_allreduce.py prints the measured ones for a node):
+# one-shot -> two-shot, and custom kernel -> RCCL ring (messages above max_bytes)
+ONE_SHOT_MAX = int(os.environ.get("HIPSERVE_CAR_ONE_SHOT_MAX", 256 << 10))
+DEFAULT_MAX_BYTES = int(os.environ.get("HIPSERVE_CAR_MAX_BYTES", 8 << 20))
 
 
 class CustomAllReduce:
