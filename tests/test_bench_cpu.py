@@ -50,3 +50,20 @@ def test_bench_two_ranks(tp):
         assert out["config"]["tp"] == 2 and out["config"]["global_batch"] == 2
         tokens = 2 * 4
     assert abs(out["value"] - tokens / (out["ms_per_step"] / 1000)) / out["value"] < 0.01
+
+
+def test_free_port_disjoint_per_local_rank(monkeypatch):
+    """DP replicas under torchrun draw gateway/router/engine ports from disjoint
+    per-LOCAL_RANK ranges, distinct within a process."""
+    from hipserve.bench import local_stack
+
+    got = {}
+    for r in range(8):
+        monkeypatch.setenv("WORLD_SIZE", "8")
+        monkeypatch.setenv("LOCAL_RANK", str(r))
+        monkeypatch.setattr(local_stack, "_next_port", [0])
+        got[r] = [local_stack.free_port() for _ in range(3)]
+        assert len(set(got[r])) == 3
+    allp = [p for ps in got.values() for p in ps]
+    assert len(set(allp)) == len(allp)
+    assert all(30000 + 200 * r <= p < 30200 + 200 * r for r, ps in got.items() for p in ps)
