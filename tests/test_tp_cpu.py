@@ -53,6 +53,11 @@ def _worker(rank, world, port, ckpt, q):
             worker_loop(runner, tp)
     finally:
         dist.destroy_process_group()
+    # skip interpreter teardown: a gloo/c10d helper thread still joinable at static
+    # destruction can abort() the process after the results are already delivered
+    q.close()
+    q.join_thread()
+    os._exit(0)
 
 
 def _run_tp(ckpt, world):
