@@ -77,6 +77,15 @@ bool car_error(void* state);
 void car_destroy(void* state);
 size_t car_max_bytes(void* state);
 void launch_car(void* state, const void* inp, void* out, size_t bytes, bool two_shot, int blocks, hipStream_t s);
+// [rows, row_bytes] shard of every rank -> out [rows, world * row_bytes] (rank-major within a row)
+void launch_car_all_gather(void* state, const void* inp, void* out, size_t shard_bytes, size_t row_bytes,
+                           hipStream_t s);
+// Row-parallel projection epilogue: h = bf16(sum over ranks of (sum_s x[s])); residual = bf16(h + residual);
+// out = rmsnorm(residual) * w. x: fp32 split-K partials [S, M, N] (x_f32) or bf16 [M, N] (S = 1).
+// exch_f32: exchange fp32 partial sums (TP = N within fp32 rounding of TP = 1) or bf16 (half the bytes).
+bool car_norm_fits(void* state, int M, int N, bool exch_f32);
+void launch_car_add_rmsnorm(void* state, void* out, void* residual, const void* x, bool x_f32, int S,
+                            const void* w, bool weight_f32, int M, int N, float eps, bool exch_f32, hipStream_t s);
 
 // init.hip — on-device synthetic weights keyed by global coordinates (TP-invariant)
 void launch_fill_uniform(void* out, long ld, int rows, int cols, long row0, long col0, long gcols,

@@ -259,6 +259,44 @@ void car_all_reduce(int64_t state, const at::Tensor& inp, at::Tensor& out, bool 
                        cur_stream());
 }
 
+void car_all_gather(int64_t state, const at::Tensor& inp, at::Tensor& out) {
+  CHECK_DEV(inp); CHECK_DEV(out); CHECK_CONTIG(inp); CHECK_CONTIG(out);
+  TORCH_CHECK(inp.dim() == 2 && out.dim() == 2 && inp.size(0) == out.size(0) && inp.dtype() == out.dtype(),
+              "car_all_gather: [rows, cols] -> [rows, world * cols]");
+  TORCH_CHECK(out.size(1) % inp.size(1) == 0, "car_all_gather: out columns must be world * in columns");
+  const size_t row = inp.size(1) * inp.element_size();
+  const size_t bytes = row * inp.size(0);
+  TORCH_CHECK(bytes <= hipserve::car_max_bytes(reinterpret_cast<void*>(state)), "car_all_gather: shard too large");
+  if (bytes == 0) return;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+  hipserve::launch_car_all_gather(reinterpret_cast<void*>(state), inp.data_ptr(), out.data_ptr(), bytes, row,
+                                  cur_stream());
+}
+
+bool car_norm_fits(int64_t state, int64_t M, int64_t N, bool exch_f32) {
+  return hipserve::car_norm_fits(reinterpret_cast<void*>(state), (int)M, (int)N, exch_f32);
+}
+
+void car_add_rmsnorm(int64_t state, at::Tensor& out, at::Tensor& residual, const at::Tensor& x, int64_t splits,
+                     const at::Tensor& weight, double eps, bool exch_f32) {
+  CHECK_DEV(x); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual); CHECK_CONTIG(x);
+  TORCH_CHECK(residual.dim() == 2 && out.sizes() == residual.sizes(), "car_add_rmsnorm: out/residual [M, N]");
+  const int M = residual.size(0), N = residual.size(1);
+  const bool xf = x.scalar_type() == at::kFloat;
+  TORCH_CHECK(xf || x.scalar_type() == at::kBFloat16, "car_add_rmsnorm: x fp32 partials or bf16");
+  TORCH_CHECK(splits >= 1 && (xf || splits == 1), "car_add_rmsnorm: bf16 input has one slice");
+  TORCH_CHECK(x.numel() == splits * (int64_t)M * N, "car_add_rmsnorm: x must hold splits * M * N values");
+  TORCH_CHECK(weight.numel() == N && weight.is_contiguous() &&
+              (weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat));
+  TORCH_CHECK(hipserve::car_norm_fits(reinterpret_cast<void*>(state), M, N, exch_f32),
+              "car_add_rmsnorm: N must divide into 8-wide chunks per rank and the message fit the buffer");
+  if (M == 0) return;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_car_add_rmsnorm(reinterpret_cast<void*>(state), out.data_ptr(), residual.data_ptr(),
+                                   x.data_ptr(), xf, (int)splits, weight.data_ptr(),
+                                   weight.scalar_type() == at::kFloat, M, N, (float)eps, exch_f32, cur_stream());
+}
+
 bool car_error(int64_t state) { return hipserve::car_error(reinterpret_cast<void*>(state)); }
 
 void car_destroy(int64_t state) { hipserve::car_destroy(reinterpret_cast<void*>(state)); }
@@ -550,6 +588,9 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("car_handle(int state) -> Tensor", &car_handle);
   m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);
   m.def("car_all_reduce(int state, Tensor inp, Tensor(a!) out, bool two_shot) -> ()", &car_all_reduce);
+  m.def("car_all_gather(int state, Tensor inp, Tensor(a!) out) -> ()", &car_all_gather);
+  m.def("car_norm_fits(int state, int M, int N, bool exch_f32) -> bool", &car_norm_fits);
+  m.def("car_add_rmsnorm(int state, Tensor(a!) out, Tensor(b!) residual, Tensor x, int splits, Tensor weight, float eps, bool exch_f32) -> ()", &car_add_rmsnorm);
   m.def("car_error(int state) -> bool", &car_error);
   m.def("car_destroy(int state) -> ()", &car_destroy);
   m.def("fill_uniform(Tensor(a!) out, int row0, int col0, int gcols, int key, float scale) -> ()");

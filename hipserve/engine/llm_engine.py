@@ -103,6 +103,7 @@ class LLMEngine:
         leaving the GPU idle between steps. Anything else (prefill, admissions,
         preemption, penalties, logprobs) runs synchronously."""
         self.faults.on_step("rank0", self.step_no)
+        self.tp.check()  # a timed-out TP collective on any rank: raise -> engine dead
         self.step_no += 1
         tr = self.tracer
         if self._inflight is not None:
@@ -317,6 +318,7 @@ def worker_loop(runner: ModelRunner, tp: TPGroup, faults: FaultInjector | None =
         if kind == "stop":
             return
         faults.on_step("worker", step)
+        tp.check()
         step += 1
         if runner.graph_eligible(inp):
             runner.launch(inp)  # no host readback on workers: keep the GPU queue fed

@@ -79,6 +79,16 @@ class ModelRunner:
         t0 = time.time()
         self._load_weights()
         self.load_time = time.time() - t0
+        if tp.world_size > 1:
+            if "tp_exact_reduce" in ecfg.extra:
+                tp.exact_reduce = bool(ecfg.extra["tp_exact_reduce"])
+            if self.device.type == "cuda":
+                # in-house TP collectives sized for the largest message of a step:
+                # a prefill chunk's [tokens, hidden] bf16 and the logits shard
+                H = mcfg.hidden_size
+                msg = max(ecfg.max_num_batched_tokens * H * 2,
+                          ecfg.max_num_seqs * self.model.vpad * 2, 8 << 20)
+                tp.ensure_custom_ar(msg)
         self.max_bs = min(ecfg.max_num_seqs, max(GRAPH_BUCKETS))
         self.buckets = [b for b in GRAPH_BUCKETS if b <= max(self.max_bs, 1)]
         if self.buckets[-1] < self.max_bs:
@@ -179,11 +189,7 @@ class ModelRunner:
         if n < 16:
             raise RuntimeError(f"not enough GPU memory for the KV cache (budget {budget / 2**30:.1f} GiB)")
         # all TP ranks must agree on the pool size
-        if self.tp.world_size > 1:
-            t = torch.tensor([n], device=self.device)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN, group=self.tp.group)
-            n = int(t.item())
-        return n
+        return self.tp.min_int(n)
 
     @property
     def usable_blocks(self) -> int:
@@ -401,6 +407,10 @@ class ModelRunner:
         st["topp"].fill_(1.0)
         st["src"].fill_(-1)
         t0 = time.time()
+        # TP ranks enter the captured collectives together (the tuner and the
+        # weight packing take different times per rank; a custom-collective
+        # barrier must not spin through a peer's whole setup)
+        self.tp.barrier()
         stream = torch.cuda.Stream(device=dev)
         stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(stream):

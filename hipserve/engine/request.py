@@ -3,7 +3,42 @@ from __future__ import annotations
 
 import enum
 import time
+import math
 from dataclasses import dataclass, field
+
+INT32_MAX = (1 << 31) - 1
+MAX_LOGPROBS = 20   # OpenAI's top_logprobs limit; also the sampler kernel's top-n capacity
+MAX_N = 128
+MAX_STOP = 64
+
+
+def _int(name: str, v, lo: int, hi: int) -> int:
+    if isinstance(v, bool) or not isinstance(v, (int, float, str)):
+        raise ValueError(f"{name} must be an integer")
+    try:
+        if isinstance(v, float):
+            if not v.is_integer():
+                raise ValueError
+            v = int(v)
+        else:
+            v = int(v)
+    except (ValueError, OverflowError):
+        raise ValueError(f"{name} must be an integer") from None
+    if not lo <= v <= hi:
+        raise ValueError(f"{name} must be in [{lo}, {hi}]")
+    return v
+
+
+def _float(name: str, v, lo: float, hi: float) -> float:
+    if isinstance(v, bool) or not isinstance(v, (int, float, str)):
+        raise ValueError(f"{name} must be a number")
+    try:
+        v = float(v)
+    except ValueError:
+        raise ValueError(f"{name} must be a number") from None
+    if not math.isfinite(v) or not lo <= v <= hi:
+        raise ValueError(f"{name} must be in [{lo}, {hi}]")
+    return v
 
 
 @dataclass
@@ -24,17 +59,37 @@ class SamplingParams:
     n: int = 1
 
     def __post_init__(self):
+        """Coerce and range-check every field: a value that reaches the engine
+        thread unchecked (a 2**64 seed in the int64 seed array, a string logprobs
+        count) would raise inside ``step()`` and kill the engine for every
+        request, so bad requests fail here with ValueError (HTTP 400)."""
         if isinstance(self.stop, str):
             self.stop = [self.stop]
-        self.stop = list(self.stop or [])
-        if self.temperature < 0:
-            raise ValueError("temperature must be >= 0")
-        if not 0.0 < self.top_p <= 1.0:
+        if not isinstance(self.stop, (list, tuple)) or not all(isinstance(s, str) for s in self.stop):
+            raise ValueError("stop must be a string or a list of strings")
+        self.stop = [s for s in self.stop if s]
+        if len(self.stop) > MAX_STOP:
+            raise ValueError(f"at most {MAX_STOP} stop strings")
+        self.temperature = _float("temperature", self.temperature, 0.0, 1e4)
+        self.top_p = _float("top_p", self.top_p, 0.0, 1.0)
+        if self.top_p <= 0.0:
             raise ValueError("top_p must be in (0, 1]")
-        if self.max_tokens is not None and self.max_tokens < 1:
-            raise ValueError("max_tokens must be >= 1")
+        self.top_k = _int("top_k", self.top_k, -1, INT32_MAX)
         if self.top_k < 0:
             self.top_k = 0
+        if self.max_tokens is not None:
+            self.max_tokens = _int("max_tokens", self.max_tokens, 1, INT32_MAX)
+        self.min_tokens = _int("min_tokens", self.min_tokens, 0, INT32_MAX)
+        self.stop_token_ids = [_int("stop_token_ids", t, 0, INT32_MAX) for t in (self.stop_token_ids or [])]
+        self.ignore_eos = bool(self.ignore_eos)
+        if self.seed is not None:
+            self.seed = _int("seed", self.seed, -(1 << 63), (1 << 63) - 1)
+        self.presence_penalty = _float("presence_penalty", self.presence_penalty, -2.0, 2.0)
+        self.frequency_penalty = _float("frequency_penalty", self.frequency_penalty, -2.0, 2.0)
+        self.repetition_penalty = _float("repetition_penalty", self.repetition_penalty, 1e-3, 100.0)
+        if self.logprobs is not None:
+            self.logprobs = _int("logprobs", self.logprobs, 0, MAX_LOGPROBS)
+        self.n = _int("n", self.n, 1, MAX_N)
 
     @property
     def greedy(self) -> bool:

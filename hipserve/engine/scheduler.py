@@ -126,7 +126,11 @@ class Scheduler:
                     self.blocks.match_prefix(seq)
                 n = min(seq.num_uncomputed, budget)
                 target = seq.num_computed_tokens + n
-                if not self.blocks.can_grow(seq, target, watermark=True):
+                # the watermark protects RUNNING sequences' growth: with nothing running
+                # (and nothing admitted yet this step) it would only block admission
+                # forever for a chunk that fits the free pool exactly
+                idle = not self.running and not out.prefill
+                if not self.blocks.can_grow(seq, target, watermark=not idle):
                     if not self.running and not out.prefill:
                         # nothing else can free memory: the request can never fit
                         if not self.blocks.can_grow(seq, target):

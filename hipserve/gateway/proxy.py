@@ -22,6 +22,7 @@ import time
 from dataclasses import dataclass, field
 
 log = logging.getLogger("hipserve.gateway")
+access_log = logging.getLogger("hipserve.access")  # one INFO line per proxied request
 
 _HOP = {b"connection", b"keep-alive", b"proxy-connection", b"te", b"trailer", b"upgrade"}
 
@@ -239,14 +240,18 @@ class HTTPProxy:
             client_ka = ka and delimited
             out.append(b"Connection: keep-alive" if client_ka else b"Connection: close")
             writer.write(b"\r\n".join(out) + b"\r\n\r\n")
-            # relay the body as it arrives (SSE chunks are forwarded immediately)
+            # relay the body as it arrives (SSE chunks are forwarded immediately);
+            # drain after every chunk so a client that went away is noticed at once
+            # (asyncio drops writes to a closed transport silently): the upstream
+            # connection is then closed, which aborts the generation in the engine
             while True:
                 data = await ur.read(1 << 16)
                 if not data:
                     break
+                if writer.transport.is_closing():
+                    raise ConnectionResetError("client disconnected")
                 writer.write(data)
-                if writer.transport.get_write_buffer_size() > (1 << 20):
-                    await writer.drain()
+                await writer.drain()
             await writer.drain()
             self.on_done(req, dest, time.monotonic() - t0, status_line)
             return client_ka
@@ -261,7 +266,7 @@ class HTTPProxy:
                 pass
 
     def on_done(self, req, dest, dt, status_line):
-        log.debug("%s %s %s -> %s:%s %s %.1fms", self.name, req.method, req.target, dest[0], dest[1],
+        access_log.info("%s %s %s %s -> %s:%s %s %.1fms", self.name, req.peer, req.method, req.target, dest[0], dest[1],
                   status_line.decode("latin-1"), 1000 * dt)
 
     async def start(self, host: str, port: int, reuse_port: bool = True):

@@ -264,7 +264,7 @@ class LlamaModel:
         With the fused decode path the merged gate|up weight is packed
         gate/up-interleaved instead (``PACKED_GLU``: the SiLU-GLU runs in its epilogue)."""
         n = 0
-        glu = self.fused_decode and self.tp.world_size == 1 and self.vanilla
+        glu = self.fused_decode and self.vanilla
         # HBM budget: a packed copy is only made while >= 24 GiB + a quarter of the
         # device stay free for the KV cache (a 70B model on ONE 288 GB MI355X keeps
         # most weights unpacked; the tuner's packed choice then runs on the plain layout)
@@ -324,7 +324,7 @@ class LlamaModel:
     def fused_gemm_shapes(self) -> dict:
         """{(N, K): epilogue spec} of the projections whose decode GEMM output feeds
         a fused epilogue (ops/gemm.py tunes them as GEMM + epilogue units)."""
-        if self.tp.world_size != 1 or not self.layers or not self.vanilla:
+        if not self.layers or not self.vanilla:
             return {}
         lw = self.layers[0]
         out = {}
@@ -339,8 +339,36 @@ class LlamaModel:
         return out
 
     def _fused_ok(self, meta: AttnMeta) -> bool:
-        return (self.fused_decode and meta.num_prefill_tokens == 0 and self.tp.world_size == 1
+        return (self.fused_decode and meta.num_prefill_tokens == 0
                 and getattr(self.ops, "name", "") == "hip" and self.cfg.num_experts == 0 and self.vanilla)
+
+    def add_rmsnorm(self, out, residual, x, splits, w):
+        """residual += x summed over the TP ranks; out = RMSNorm(residual) * w.
+        ``x`` is this rank's partial output of a row-parallel projection: fp32
+        split-K partials [S, M, N] of a decode GEMM, or the plain projection output
+        (bf16; fp32 under exact TP reduction). TP=1 runs the single-GPU fused
+        kernels; TP>1 the in-house cross-rank epilogue (parallel/comm.py)."""
+        eps = self.cfg.rms_norm_eps
+        if self.tp.world_size > 1:
+            return self.tp.add_rmsnorm(out, residual, x, splits, w, eps, ops=self.ops)
+        if x.dtype == torch.float32 and residual.dtype != torch.float32:
+            torch.ops.hipserve.splitk_add_rmsnorm(out, residual, x, splits, w, eps)
+        else:
+            self.ops.fused_add_rmsnorm(out, x, residual, w, eps)
+        return out
+
+    def linear_rowpar(self, x: torch.Tensor, w) -> torch.Tensor:
+        """Row-parallel projection (o_proj / down_proj). Under exact TP reduction
+        the GEMM writes fp32, so the cross-rank sum rounds once, like TP=1's GEMM."""
+        if (self.tp.world_size > 1 and self.tp.exact_reduce and x.is_cuda and isinstance(w, torch.Tensor)):
+            return torch.mm(x, w.t(), out_dtype=torch.float32)
+        return self.linear(x, w)
+
+    def _tp_sum(self, x: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+        """Plain all-reduce of a row-parallel output (the sandwich-norm families,
+        whose post-norm needs the full sum before the residual add)."""
+        self.tp.all_reduce(x)
+        return x if x.dtype == like.dtype else x.to(like.dtype)
 
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.tp.world_size == 1:
@@ -363,17 +391,14 @@ class LlamaModel:
         h = self.embed_tokens(ids)
         if cfg.embed_scale != 1.0:  # Gemma: embeddings * sqrt(hidden), the scale rounded to the dtype
             h = h * float(torch.tensor(cfg.embed_scale, dtype=h.dtype))
-        residual = torch.empty_like(h)
+        residual = h.clone()
         xn = torch.empty_like(h)
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
         if Td:
             part, tmp_out, tmp_ml = self._decode_split(Td, meta)
+        ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
+        L = len(self.layers)
         for i, lw in enumerate(self.layers):
-            if i == 0:
-                residual.copy_(h)
-                ops.rmsnorm(xn, h, lw.ln1, eps)
-            else:
-                ops.fused_add_rmsnorm(xn, h, residual, lw.ln1, eps)
             qkv = self.linear(xn, lw.wqkv)
             if lw.bqkv is not None:
                 qkv += lw.bqkv
@@ -389,22 +414,27 @@ class LlamaModel:
             if Td:
                 ops.paged_decode(attn[Tp:], qkv[Tp:], kc, vc, meta.bt_decode, meta.ctx_decode,
                                  tmp_out, tmp_ml, nq, nkv, part, self.scale, win)
-            o = self.linear(attn, lw.wo)
-            self.tp.all_reduce(o)
+            o = self.linear_rowpar(attn, lw.wo)
             if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)
+                o = self._tp_sum(o, xn)
                 ops.rmsnorm(o, o, lw.post_attn_norm, eps)
-            ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
+                ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
+            else:
+                self.add_rmsnorm(xn, residual, o, 1, lw.ln2)
             if lw.router is not None:
                 h = self.moe(xn, lw)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=h.device, dtype=h.dtype)
                 self.act_and_mul(act, gu)
-                h = self.linear(act, lw.wd)
-            self.tp.all_reduce(h)
+                h = self.linear_rowpar(act, lw.wd)
+            nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             if lw.post_ff_norm is not None:
+                h = self._tp_sum(h, xn)
                 ops.rmsnorm(h, h, lw.post_ff_norm, eps)
-        ops.fused_add_rmsnorm(xn, h, residual, self.norm, eps)
+                ops.fused_add_rmsnorm(xn, h, residual, nxt, eps)
+            else:
+                self.add_rmsnorm(xn, residual, h, 1, nxt)
         return xn
 
     def act_and_mul(self, out: torch.Tensor, gu: torch.Tensor):
@@ -415,8 +445,9 @@ class LlamaModel:
         return self.ops.silu_and_mul(out, gu)
 
     def forward_decode_fused(self, ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
-        """Decode-only forward (TP=1) with the decode GEMMs' split-K partials reduced
-        inside the next op: qkv -> RoPE + KV write, o_proj -> residual add + RMSNorm,
+        """Decode-only forward with the decode GEMMs' split-K partials reduced
+        inside the next op (at TP>1 the o_proj / down epilogues are the in-house
+        cross-rank reduce + residual + RMSNorm kernel, ``add_rmsnorm``): qkv -> RoPE + KV write, o_proj -> residual add + RMSNorm,
         down -> residual add + the NEXT
         layer's RMSNorm (final norm after the last layer), SiLU-GLU in the gate|up
         GEMM's epilogue (gate/up-interleaved packing). Bit-identical to
@@ -450,9 +481,9 @@ class LlamaModel:
             fc = gemm.fused_choice(T, lw.wo)
             if fc is not None:
                 ws, S = gemm.gemm_partial(attn, lw.wo, fc)
-                op.splitk_add_rmsnorm(xn, residual, ws, S, lw.ln2, eps)
+                self.add_rmsnorm(xn, residual, ws, S, lw.ln2)
             else:
-                ops.fused_add_rmsnorm(xn, self.linear(attn, lw.wo), residual, lw.ln2, eps)
+                self.add_rmsnorm(xn, residual, self.linear_rowpar(attn, lw.wo), 1, lw.ln2)
             gc = gemm.glu_choice(T, lw.wgu)
             if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
@@ -464,9 +495,9 @@ class LlamaModel:
             fc = gemm.fused_choice(T, lw.wd)
             if fc is not None:
                 ws, S = gemm.gemm_partial(act, lw.wd, fc)
-                op.splitk_add_rmsnorm(xn, residual, ws, S, nxt, eps)
+                self.add_rmsnorm(xn, residual, ws, S, nxt)
             else:
-                ops.fused_add_rmsnorm(xn, self.linear(act, lw.wd), residual, nxt, eps)
+                self.add_rmsnorm(xn, residual, self.linear_rowpar(act, lw.wd), 1, nxt)
         return xn
 
     def _decode_split(self, Td: int, meta: AttnMeta):

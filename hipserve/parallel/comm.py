@@ -36,6 +36,12 @@ class TPGroup:
         self._cpu_group = None
         self._ring = None
         self.custom_ar = None
+        self.backend = dist.get_backend(group) if group is not None else None
+        # row-parallel epilogues exchange fp32 partial sums up to this many rows (all
+        # decode batches), bf16 above (prefill chunks: half the xGMI bytes);
+        # exact_reduce forces fp32 everywhere (prefill GEMMs then write fp32 too)
+        self.fp32_exchange_rows = int(os.environ.get("HIPSERVE_TP_FP32_ROWS", 512))
+        self.exact_reduce = os.environ.get("HIPSERVE_TP_EXACT", "0") == "1"
 
     SHM_SLOT_BYTES = 8 << 20
     SHM_SLOTS = 4
@@ -68,20 +74,75 @@ class TPGroup:
     def is_first(self):
         return self.rank == 0
 
+    def _uncapturable(self, what: str):
+        """A process-group collective inside a hipGraph capture is only legal on
+        RCCL; with a gloo device group (the shared-GPU TP tests) every captured
+        collective must be an in-house kernel."""
+        if self.backend == "gloo" and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"{what} is not covered by the custom collectives and cannot be "
+                               "captured on a gloo process group (register a larger custom buffer)")
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum over TP ranks: decode-sized bf16 messages through the HIP-IPC
-        custom all-reduce (when set up), everything else through RCCL."""
+        """In-place sum over TP ranks: bf16 messages that fit the registered buffer
+        through the HIP-IPC custom all-reduce (when set up), everything else
+        through the process group (RCCL)."""
         if self.world_size > 1:
             car = self.custom_ar
             if car is not None and car.supports(t):
                 car.all_reduce(t)
             else:
+                self._uncapturable("all_reduce")
                 dist.all_reduce(t, group=self.group)
         return t
 
+    def add_rmsnorm(self, out, residual, x, splits, weight, eps, ops=None, exch_f32: bool | None = None):
+        """Row-parallel projection epilogue (o_proj / down_proj / MoE combine):
+        h = sum over ranks of this rank's partial output ``x`` (fp32 split-K partials
+        [S, M, N] or bf16 [M, N]), residual += bf16(h), out = RMSNorm(residual).
+        One in-house kernel when the custom collectives are up; otherwise a local
+        reduce + all-reduce + fused_add_rmsnorm (same rounding points)."""
+        M, N = residual.shape
+        car = self.custom_ar
+        if exch_f32 is None:
+            exch_f32 = self.exact_reduce or M <= self.fp32_exchange_rows
+        if car is not None and x.is_cuda:
+            if not car.norm_fits(M, N, exch_f32) and exch_f32 and not self.exact_reduce:
+                exch_f32 = False
+            if car.norm_fits(M, N, exch_f32):
+                car.add_rmsnorm(out, residual, x, splits, weight, eps, exch_f32)
+                return out
+        if x.dtype == torch.float32 and x.numel() == splits * M * N and residual.dtype != torch.float32:
+            h = x.view(splits, M, N).sum(0)
+            if not (exch_f32 and self.world_size > 1):
+                h = h.to(residual.dtype)
+        else:
+            h = x.view(M, N)
+        if self.world_size > 1:
+            self._uncapturable("add_rmsnorm")
+            dist.all_reduce(h, group=self.group)
+        (ops or _default_ops(residual.device)).fused_add_rmsnorm(out, h.to(residual.dtype), residual, weight, eps)
+        return out
+
+    def check(self):
+        """Raise if a custom collective timed out on any rank (sticky, host-visible)."""
+        if self.custom_ar is not None:
+            self.custom_ar.check()
+
+    def ensure_custom_ar(self, max_bytes: int) -> bool:
+        """Collective (every rank, same argument): (re)create the custom collectives
+        with at least ``max_bytes`` per message."""
+        car = self.custom_ar
+        if car is not None and car.max_bytes >= max_bytes:
+            return True
+        if car is not None:
+            self.barrier()
+            car.close()
+            self.custom_ar = None
+        return self.setup_custom_ar(max_bytes)
+
     def setup_custom_ar(self, max_bytes: int | None = None) -> bool:
         """Collective: map peer buffers and keep the custom all-reduce only if its
-        self-test against RCCL passes on every rank."""
+        self-test against the process group passes on every rank."""
         if self.world_size == 1 or self.device is None or self.device.type != "cuda" \
                 or os.environ.get("HIPSERVE_CUSTOM_AR", "1") == "0":
             return False
@@ -109,11 +170,16 @@ class TPGroup:
         return True
 
     def all_gather_lastdim(self, t: torch.Tensor) -> torch.Tensor:
-        """[n, V/TP] on every rank -> [n, V] on every rank."""
+        """[n, V/TP] on every rank -> [n, V] on every rank (in-house IPC gather when
+        it fits, else the process group)."""
         if self.world_size == 1:
             return t
         t = t.contiguous()
-        if t.device.type == "cpu":  # gloo: list form
+        car = self.custom_ar
+        if car is not None and car.supports_gather(t):
+            return car.all_gather(t)
+        self._uncapturable("all_gather")
+        if t.device.type == "cpu" or self.backend == "gloo":  # gloo: list form
             parts = [torch.empty_like(t) for _ in range(self.world_size)]
             dist.all_gather(parts, t, group=self.group)
             return torch.cat(parts, dim=-1)
@@ -145,6 +211,20 @@ class TPGroup:
         if self.world_size > 1:
             dist.barrier(group=self._cpu_group)
 
+    def min_int(self, n: int) -> int:
+        """Minimum of a host integer over ranks (CPU group: no device collective)."""
+        if self.world_size == 1:
+            return n
+        t = torch.tensor([n], dtype=torch.long)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._cpu_group)
+        return int(t.item())
+
+
+def _default_ops(device):
+    from ..ops import get_ops
+
+    return get_ops(device)
+
 
 _TP: TPGroup | None = None
 
@@ -174,8 +254,8 @@ def init_tp(world_size: int | None = None, backend: str | None = None, device_ty
     g = TPGroup(rank, ws, dist.group.WORLD, dev)
     g._cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
     g.setup_shm_ring()
-    if device_type == "cuda":
-        g.setup_custom_ar()
+    # the custom collectives are created by the ModelRunner once the message sizes
+    # (hidden size x token budget, logits shard) are known: ensure_custom_ar()
     _TP = g
     return g
 

@@ -1,16 +1,24 @@
-"""In-house all-reduce for decode-sized TP messages: a thin owner
-of the HIP-IPC peer buffers behind ``csrc/kernels/allreduce.hip``.
+"""In-house TP collectives: a thin owner of the HIP-IPC peer
+buffers behind ``csrc/kernels/allreduce.hip``.
 
 Every rank allocates one uncached buffer, exports its IPC handle, gathers the
-peers' handles over the CPU (gloo) group and maps them; from then on
-``all_reduce(t)`` is a single graph-capturable kernel launch that reads the peers'
-staged copies directly over xGMI (one-shot up to ``ONE_SHOT_MAX`` bytes,
-reduce-scatter + all-gather above). Messages larger than the registered buffer
-(prefill chunks) stay on RCCL, whose ring is bandwidth-optimal there.
+peers' handles over the CPU (gloo) group and maps them; from then on each
+collective is a single graph-capturable kernel launch that reads the peers'
+staged copies directly over xGMI:
 
-Enabled only after a self-test against RCCL passes on every rank (the decision
-is collective), so a node whose IPC / peer mapping misbehaves silently keeps the
-RCCL path instead of producing wrong sums.
+* ``all_reduce(t)``  bf16 sum, one-shot up to ``ONE_SHOT_MAX`` bytes, reduce-
+  scatter + all-gather above;
+* ``all_gather(t, out)``  [rows, cols] -> [rows, world * cols] (LM-head logits);
+* ``add_rmsnorm(...)`` the row-parallel projection epilogue of a decoder layer —
+  cross-rank sum of the local (split-K) partials, residual add and RMSNorm in one
+  kernel, exchanging fp32 (TP=N within fp32 rounding of TP=1) or bf16.
+
+Messages larger than the registered buffer stay on RCCL. Enabled only after a
+self-test against the process-group all-reduce passes on every rank (the
+decision is collective), so a node whose IPC / peer mapping misbehaves keeps the
+RCCL path instead of producing wrong sums. A barrier timeout anywhere sets a
+sticky error that every rank sees (``failed()``, a pinned host word: no device
+sync) and the engine turns into a dead pod.
 """
 from __future__ import annotations
 
@@ -22,10 +30,14 @@ import torch.distributed as dist
 
 log = logging.getLogger("hipserve.custom_ar")
 
-# crossovers (tools/bench_allreduce.py prints the measured ones for a node):
-# one-shot -> two-shot, and custom kernel -> RCCL ring (messages above max_bytes)
+# one-shot -> two-shot crossover (tools/bench_allreduce.py prints the measured one
+# for a node) and the default registered message size
 ONE_SHOT_MAX = int(os.environ.get("HIPSERVE_CAR_ONE_SHOT_MAX", 256 << 10))
 DEFAULT_MAX_BYTES = int(os.environ.get("HIPSERVE_CAR_MAX_BYTES", 8 << 20))
+
+
+class CollectiveError(RuntimeError):
+    """A custom collective timed out on some rank (a peer died or hung)."""
 
 
 class CustomAllReduce:
@@ -35,9 +47,9 @@ class CustomAllReduce:
         load_library()
         self.op = torch.ops.hipserve
         self.rank, self.world, self.device = rank, world, device
-        self.max_bytes = max_bytes
         with torch.cuda.device(device):
             self.state = int(self.op.car_create(rank, world, max_bytes))
+            self.max_bytes = max_bytes
             mine = self.op.car_handle(self.state)
         handles = [None] * world
         dist.all_gather_object(handles, bytes(mine.numpy().tobytes()), group=cpu_group)
@@ -59,8 +71,29 @@ class CustomAllReduce:
         self.op.car_all_reduce(self.state, t, out, two_shot)
         return out
 
+    def supports_gather(self, t: torch.Tensor) -> bool:
+        n = t.numel() * t.element_size()
+        return (t.is_cuda and t.dim() == 2 and t.is_contiguous() and n <= self.max_bytes
+                and (t.shape[1] * t.element_size()) % 2 == 0)
+
+    def all_gather(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(t.shape[0], self.world * t.shape[1], dtype=t.dtype, device=t.device)
+        self.op.car_all_gather(self.state, t, out)
+        return out
+
+    def norm_fits(self, M: int, N: int, exch_f32: bool) -> bool:
+        return bool(self.op.car_norm_fits(self.state, M, N, exch_f32))
+
+    def add_rmsnorm(self, out, residual, x, splits, weight, eps, exch_f32):
+        self.op.car_add_rmsnorm(self.state, out, residual, x, splits, weight, eps, exch_f32)
+
     def failed(self) -> bool:
         return bool(self.op.car_error(self.state))
+
+    def check(self):
+        if self.failed():
+            raise CollectiveError("a TP collective timed out (a peer rank died or hung); the engine is dead")
 
     def close(self):
         if self.state:
@@ -69,20 +102,26 @@ class CustomAllReduce:
 
 
 def self_test(car: CustomAllReduce, group, cpu_group) -> bool:
-    """Compare against the process-group all-reduce on a few message sizes;
-    collective agreement (all ranks must pass)."""
+    """Compare against the process-group all-reduce on a few message sizes (one-shot
+    and two-shot) plus the all-gather; collective agreement (all ranks must pass)."""
     ok = True
     try:
         for numel in (8, 4096, 64 * 8192, min(car.max_bytes // 2, 2 << 20)):
             g = torch.Generator(device=car.device).manual_seed(1234 + 17 * car.rank + numel)
             x = torch.randn(numel, device=car.device, dtype=torch.float32, generator=g).to(torch.bfloat16)
-            want = x.float().clone()
-            dist.all_reduce(want, group=group)
+            want = x.float().cpu()
+            dist.all_reduce(want, group=cpu_group)
             got = car.all_reduce(x.clone())
             torch.cuda.synchronize(car.device)
-            if car.failed() or not torch.allclose(got.float(), want, atol=0.05, rtol=0.02):
+            if car.failed() or not torch.allclose(got.float().cpu(), want, atol=0.05, rtol=0.02):
                 ok = False
                 break
+        if ok:
+            x = torch.full((3, 64), float(car.rank + 1), device=car.device, dtype=torch.bfloat16)
+            got = car.all_gather(x)
+            torch.cuda.synchronize(car.device)
+            want = torch.cat([torch.full((3, 64), float(r + 1)) for r in range(car.world)], 1)
+            ok = not car.failed() and torch.equal(got.float().cpu(), want)
     except Exception as e:  # a broken IPC mapping must not take the engine down
         log.warning("custom all-reduce self-test raised: %s", e)
         ok = False

@@ -13,6 +13,7 @@ Replaces the engines the reference launches: ``vllm/vllm-openai:v0.11.0``
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import logging
 import time
@@ -113,26 +114,37 @@ class OpenAIServer:
         if mt is None:
             mt = self.max_model_len if chat else 16
         lp = body.get("logprobs")
-        if chat:
-            lp = body.get("top_logprobs", 1) if lp else None
-        elif lp is not None:
-            lp = int(lp)
+        if chat:  # chat: logprobs is a bool, top_logprobs the count (>= 1 reported)
+            if lp is not None and not isinstance(lp, bool):
+                raise ValueError("logprobs must be a boolean for chat completions")
+            tl = body.get("top_logprobs")
+            lp = (1 if tl is None else tl) if lp else None
+        stop_ids = body.get("stop_token_ids") or []
+        if not isinstance(stop_ids, list):
+            raise ValueError("stop_token_ids must be a list of integers")
+
+        def opt(key, default):
+            v = body.get(key)
+            return default if v is None else v
+
+        # SamplingParams coerces and range-checks every field (ValueError -> 400)
         return SamplingParams(
-            temperature=float(body.get("temperature", 1.0) if body.get("temperature") is not None else 1.0),
-            top_p=float(body.get("top_p", 1.0) if body.get("top_p") is not None else 1.0),
-            top_k=int(body.get("top_k", 0) or 0),
-            max_tokens=int(mt),
-            min_tokens=int(body.get("min_tokens", 0) or 0),
-            stop=body.get("stop") or [],
-            stop_token_ids=list(body.get("stop_token_ids") or []),
-            ignore_eos=bool(body.get("ignore_eos", False)),
-            seed=body.get("seed"),
-            presence_penalty=float(body.get("presence_penalty", 0.0) or 0.0),
-            frequency_penalty=float(body.get("frequency_penalty", 0.0) or 0.0),
-            repetition_penalty=float(body.get("repetition_penalty", 1.0) or 1.0),
-            logprobs=lp,
-            n=int(body.get("n", 1) or 1),
-        )
+            temperature=opt("temperature", 1.0), top_p=opt("top_p", 1.0), top_k=opt("top_k", 0),
+            max_tokens=mt, min_tokens=opt("min_tokens", 0), stop=opt("stop", []),
+            stop_token_ids=stop_ids, ignore_eos=bool(body.get("ignore_eos", False)),
+            seed=body.get("seed"), presence_penalty=opt("presence_penalty", 0.0),
+            frequency_penalty=opt("frequency_penalty", 0.0),
+            repetition_penalty=opt("repetition_penalty", 1.0), logprobs=lp, n=opt("n", 1))
+
+    def _check_prompt(self, ids):
+        """The engine's add_request checks, run in the handler so that a bad prompt
+        is a 400 before any SSE header goes out (not a truncated stream)."""
+        if not ids:
+            raise ValueError("empty prompt")
+        V = self.engine.model_cfg.vocab_size
+        for t in ids:
+            if isinstance(t, bool) or not isinstance(t, int) or not 0 <= t < V:
+                raise ValueError(f"prompt token id out of range [0, {V})")
 
     def _clip_max_tokens(self, params: SamplingParams, n_prompt: int):
         room = self.max_model_len - n_prompt
@@ -149,8 +161,8 @@ class OpenAIServer:
             for j in range(params.n):
                 sp = params
                 if params.n > 1:
-                    sp = SamplingParams(**{**params.__dict__, "n": 1,
-                                           "seed": None if params.seed is None else params.seed + j})
+                    seed = None if params.seed is None else ((params.seed + j + (1 << 63)) % (1 << 64)) - (1 << 63)
+                    sp = SamplingParams(**{**params.__dict__, "n": 1, "seed": seed})
                 gens.append((idx, self.ae.generate(f"{base_id}-{idx}", p, sp)))
                 idx += 1
         return gens
@@ -178,9 +190,10 @@ class OpenAIServer:
             return bad
         try:
             params = self._params(body, chat=False)
-            prompts = [self.tokenizer.encode(p) if isinstance(p, str) else [int(t) for t in p]
+            prompts = [self.tokenizer.encode(p) if isinstance(p, str) else list(p)
                        for p in self._prompts(body)]
             for p in prompts:
+                self._check_prompt(p)
                 self._clip_max_tokens(params, len(p))
         except (ValueError, TypeError) as e:
             return _err(400, str(e))
@@ -202,24 +215,25 @@ class OpenAIServer:
             head = 'data: {"id":%s,"object":"text_completion","created":%d,"model":%s,"choices":[{"index":' % (
                 _dumps(rid), created, _dumps(model))
             try:
-                async for idx, o in _merge(gens):
-                    n_out += len(o.new_token_ids)
-                    if params.logprobs is not None and o.logprobs:
-                        ch = {"index": idx, "text": o.new_text, "finish_reason": o.finish_reason if o.finished else None,
-                              "logprobs": {"tokens": [self.tokenizer.decode(o.new_token_ids)],
-                                           "token_logprobs": [o.logprobs[0]]}}
-                        chunk = {"id": rid, "object": "text_completion", "created": created,
-                                 "model": model, "choices": [ch]}
-                        await resp.write(("data: " + _dumps(chunk) + "\n\n").encode())
-                        continue
-                    fin = _dumps(o.finish_reason) if o.finished else "null"
-                    await resp.write(f'{head}{idx},"text":{_dumps(o.new_text)},"logprobs":null,'
-                                     f'"finish_reason":{fin}}}]}}\n\n'.encode())
+                async with contextlib.aclosing(_merge(gens)) as merged:
+                    async for idx, o in merged:
+                        n_out += len(o.new_token_ids)
+                        if params.logprobs is not None and o.logprobs:
+                            ch = {"index": idx, "text": o.new_text, "finish_reason": o.finish_reason if o.finished else None,
+                                  "logprobs": {"tokens": [self.tokenizer.decode(o.new_token_ids)],
+                                               "token_logprobs": [o.logprobs[0]]}}
+                            chunk = {"id": rid, "object": "text_completion", "created": created,
+                                     "model": model, "choices": [ch]}
+                            await resp.write(("data: " + _dumps(chunk) + "\n\n").encode())
+                            continue
+                        fin = _dumps(o.finish_reason) if o.finished else "null"
+                        await resp.write(f'{head}{idx},"text":{_dumps(o.new_text)},"logprobs":null,'
+                                         f'"finish_reason":{fin}}}]}}\n\n'.encode())
                 if include_usage:
                     u = {"id": rid, "object": "text_completion", "created": created, "model": model,
                          "choices": [], "usage": _usage(n_prompt_total, n_out)}
                     await resp.write(("data: " + _dumps(u) + "\n\n").encode())
-            except EngineDeadError as e:
+            except (EngineDeadError, ValueError) as e:
                 await resp.write(("data: " + _dumps({"error": {"message": str(e)}}) + "\n\n").encode())
             await resp.write(b"data: [DONE]\n\n")
             await resp.write_eof()
@@ -258,6 +272,7 @@ class OpenAIServer:
         try:
             params = self._params(body, chat=True)
             ids = self.tokenizer.encode_chat(msgs, add_generation_prompt=True)
+            self._check_prompt(ids)
             self._clip_max_tokens(params, len(ids))
         except (ValueError, TypeError) as e:
             return _err(400, str(e))
@@ -284,16 +299,17 @@ class OpenAIServer:
             head = 'data: {"id":%s,"object":"chat.completion.chunk","created":%d,"model":%s,"choices":[{"index":' % (
                 _dumps(rid), created, _dumps(model))
             try:
-                async for idx, o in _merge(gens):
-                    n_out += len(o.new_token_ids)
-                    delta = '{"content":%s}' % _dumps(o.new_text) if (o.new_text or not o.finished) else "{}"
-                    fin = _dumps(o.finish_reason) if o.finished else "null"
-                    await resp.write(f'{head}{idx},"delta":{delta},"logprobs":null,'
-                                     f'"finish_reason":{fin}}}]}}\n\n'.encode())
+                async with contextlib.aclosing(_merge(gens)) as merged:
+                    async for idx, o in merged:
+                        n_out += len(o.new_token_ids)
+                        delta = '{"content":%s}' % _dumps(o.new_text) if (o.new_text or not o.finished) else "{}"
+                        fin = _dumps(o.finish_reason) if o.finished else "null"
+                        await resp.write(f'{head}{idx},"delta":{delta},"logprobs":null,'
+                                         f'"finish_reason":{fin}}}]}}\n\n'.encode())
                 if include_usage:
                     await resp.write(("data: " + _dumps({**base, "choices": [],
                                                          "usage": _usage(n_prompt, n_out)}) + "\n\n").encode())
-            except EngineDeadError as e:
+            except (EngineDeadError, ValueError) as e:
                 await resp.write(("data: " + _dumps({"error": {"message": str(e)}}) + "\n\n").encode())
             await resp.write(b"data: [DONE]\n\n")
             await resp.write_eof()
@@ -327,8 +343,11 @@ async def _merge(gens):
     """Interleave several async generators, yielding (index, output)."""
     if len(gens) == 1:
         idx, g = gens[0]
-        async for o in g:
-            yield idx, o
+        try:
+            async for o in g:
+                yield idx, o
+        finally:  # client gone / handler failed: AsyncEngine.generate aborts the request
+            await g.aclose()
         return
     q: asyncio.Queue = asyncio.Queue()
     done = object()
@@ -356,6 +375,9 @@ async def _merge(gens):
     finally:
         for t in tasks:
             t.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
+        for _, g in gens:
+            await g.aclose()
 
 
 async def _collect(gens):

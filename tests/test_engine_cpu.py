@@ -155,7 +155,7 @@ def test_seeded_sampling_reproducible():
 
 def test_penalties_and_logprobs():
     eng = make_engine()
-    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True, frequency_penalty=5.0,
+    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True, frequency_penalty=2.0, presence_penalty=2.0,
                         logprobs=3)
     toks = eng.generate([[1, 2, 3]], sp)[0][0]
     # a strong frequency penalty makes greedy avoid immediate repeats
