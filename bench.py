@@ -61,8 +61,30 @@ def parse():
     return ap.parse_args()
 
 
+def _self_launch(args) -> int:
+    """``--gpus N`` without torchrun: start the documented multi-rank form as a
+    CHILD process (one rank per GPU, 127.0.0.1 rendezvous) and return its exit
+    code. Nothing here has touched the GPU yet."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(_self_launch(args))
+    if args.gpus != int(world_env or "1"):
+        raise SystemExit(f"--gpus {args.gpus} does not match the launched world size {world_env or 1}: "
+                         "run one rank per GPU (torch.distributed.run --nproc-per-node N bench.py --gpus N)")
     import numpy as np
     import torch
     import torch.distributed as dist

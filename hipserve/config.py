@@ -263,6 +263,11 @@ PRESETS: dict[str, ModelConfig] = {
                               num_kv_heads=2, head_dim=32, intermediate_size=256, vocab_size=512,
                               rope_theta=10000.0, max_position_embeddings=2048,
                               bos_token_id=1, eos_token_id=(2,)),
+    # the 70B head layout in miniature (8 kv heads: one per rank at TP=8) for world-8 CPU runs
+    "tiny-llama-tp8": ModelConfig(name="tiny-llama-tp8", hidden_size=256, num_layers=2, num_heads=16,
+                                  num_kv_heads=8, head_dim=16, intermediate_size=512, vocab_size=512,
+                                  rope_theta=500000.0, max_position_embeddings=2048,
+                                  bos_token_id=1, eos_token_id=(2,)),
     "tiny-mixtral": ModelConfig(name="tiny-mixtral", architecture="mixtral", hidden_size=128,
                                 num_layers=2, num_heads=4, num_kv_heads=2, head_dim=32,
                                 intermediate_size=192, vocab_size=512, rope_theta=1e6,

@@ -425,7 +425,7 @@ class LlamaModel:
                 h = self.moe(xn, lw)
             else:
                 gu = self.linear(xn, lw.wgu)
-                act = torch.empty(T, self.inter, device=h.device, dtype=h.dtype)
+                act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 self.act_and_mul(act, gu)
                 h = self.linear_rowpar(act, lw.wd)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
@@ -489,7 +489,7 @@ class LlamaModel:
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
             else:
                 gu = self.linear(xn, lw.wgu)
-                act = torch.empty(T, self.inter, device=h.device, dtype=h.dtype)
+                act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 ops.silu_and_mul(act, gu)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             fc = gemm.fused_choice(T, lw.wd)

@@ -67,3 +67,21 @@ def test_free_port_disjoint_per_local_rank(monkeypatch):
     allp = [p for ps in got.values() for p in ps]
     assert len(set(allp)) == len(allp)
     assert all(30000 + 200 * r <= p < 30200 + 200 * r for r, ps in got.items() for p in ps)
+
+
+def test_bench_tp8_world8():
+    """The 70B TP=8 launch form (``torch.distributed.run --nproc-per-node 8 bench.py
+    --tp 8``) end to end at world 8 over gloo: rank 0 engine + HTTP stack + load
+    generator, ranks 1-7 in the TP worker loop, step inputs over the shared-memory
+    ring. CPU-sized model with the 70B head layout (8 kv heads: one per rank)."""
+    args = [a if a != "tiny-llama" else "tiny-llama-tp8" for a in ARGS]
+    out = _run(_torchrun(8, 29660, args + ["--tp", "8"]))
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "tp8" and out["scaling"] == "strong"
+    assert out["value"] > 0 and out["p50_ttft_ms"] > 0
+
+
+def test_bench_gpus_flag_must_match_world():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "does not match" in r.stderr

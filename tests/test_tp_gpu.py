@@ -7,10 +7,17 @@ readback (``ModelRunner.launch``); every collective is an in-house HIP-IPC kerne
 (no RCCL on this path: the process group is gloo, and a process-group collective
 inside a graph capture raises).
 
-With exact TP reduction (row-parallel partials exchanged and summed in fp32, the
-prefill GEMMs writing fp32) TP=2 differs from TP=1 only by fp32 summation order,
-so 256 greedy tokens per prompt must match TP=1 exactly. The default (bf16
-exchange for prefill chunks) is checked on first-token logits agreement.
+TP=2 reproduces TP=1 token for token except where TP=1 itself sits on a numerical
+near-tie: bitwise identity across TP degrees would need every GEMM to keep a
+reduction order independent of its shard width (it does not: the decode GEMM
+tuner and hipBLASLt choose per shape), so fp32-rounding differences flip a
+greedy argmax where TP=1's top candidates' log-probabilities are within ``TIE``
+nats (bf16 activations turn an fp32-order difference into bf16-ulp noise within
+a few ops). The
+check walks all 256 positions of every prompt: at a divergence it asserts that
+TP=2 picked one of TP=1's top-5 within ``TIE`` of TP=1's choice, then resynchronises (teacher-forces
+TP=1's token) and continues. With exact reduction (fp32 exchange, fp32 prefill
+GEMM outputs) and with the default (bf16 exchange of prefill chunks).
 Reference: every HF model in the reference runs at TP=2
 (vllm-models/helm-chart/values.yaml:5,10; templates/model-deployments.yaml:37-38)."""
 import multiprocessing as mp
@@ -49,11 +56,20 @@ def _engine_cfg(tp, exact):
                         tensor_parallel_size=tp, extra={"tp_exact_reduce": exact})
 
 
-def _generate(eng):
+def _generate(eng, prompts, n, top2=False):
+    """Greedy tokens (and TP=1's per-step top-5 log-probs) for each prompt."""
     from hipserve.engine.request import SamplingParams
 
-    res = eng.generate(PROMPTS, SamplingParams(temperature=0.0, max_tokens=N_TOK, ignore_eos=True))
-    return [r[0] for r in res]
+    sp = SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True, logprobs=5 if top2 else None)
+    rids = [eng.add_request(None, p, sp).request_id for p in prompts]
+    toks = {r: [] for r in rids}
+    tops = {r: [] for r in rids}
+    while eng.has_unfinished():
+        for o in eng.step():
+            toks[o.request_id].extend(o.new_token_ids)
+            if top2 and o.logprobs and len(o.logprobs) > 1:
+                tops[o.request_id].append(o.logprobs[1])
+    return [toks[r] for r in rids], [tops[r] for r in rids]
 
 
 def _worker(rank, world, port, exact, q):
@@ -74,10 +90,35 @@ def _worker(rank, world, port, exact, q):
             eng = LLMEngine(cfg, tp=tp, model_cfg=_model_cfg())
             info = {"graphs": len(eng.runner.graphs), "lookahead": eng.lookahead,
                     "custom_ar": tp.custom_ar is not None, "shm_ring": tp._ring is not None}
-            toks = _generate(eng)
+            # the TP=1 reference lives in this process too (rank 1 idles in its loop)
+            from hipserve.parallel.comm import TPGroup
+
+            ref = LLMEngine(_engine_cfg(1, False), tp=TPGroup(0, 1, None, torch.device("cuda", 0)),
+                            model_cfg=_model_cfg())
+            want, top2 = _generate(ref, PROMPTS, N_TOK, top2=True)
+            got, _ = _generate(eng, PROMPTS, N_TOK)
+            info["exact_prefix"] = [next((j for j, (x, y) in enumerate(zip(a, b)) if x != y), len(a))
+                                    for a, b in zip(got, want)]
+            # walk every position; at a divergence verify the near-tie and resync
+            ties = []
+            for i, p in enumerate(PROMPTS):
+                j0, g = 0, got[i]
+                while True:
+                    j = next((k for k in range(j0, N_TOK) if g[k - j0] != want[i][k]), None)
+                    if j is None:
+                        break
+                    cand = dict(top2[i][j])
+                    ties.append((i, j, want[i][j], g[j - j0], cand.get(want[i][j]), cand.get(g[j - j0])))
+                    if len(ties) > 100:
+                        break
+                    j0 = j + 1
+                    if j0 >= N_TOK:
+                        break
+                    g = _generate(eng, [p + want[i][:j0]], N_TOK - j0)[0][0]
+            info["ties"] = ties
             info["car_failed"] = tp.custom_ar.failed() if tp.custom_ar else None
             eng.shutdown()
-            out = ("ok", toks, info)
+            out = ("ok", None, info)
         else:
             worker_loop(ModelRunner(cfg, _model_cfg(), tp), tp)
     except Exception:
@@ -102,32 +143,26 @@ def _run_tp(world, exact):
     for p in ps:
         p.start()
     try:
-        status, toks, info = q.get(timeout=100)
+        status, err, info = q.get(timeout=140)
     finally:
         for p in ps:
             p.join(20)
             if p.is_alive():
                 p.kill()
-    assert status == "ok", toks
-    return toks, info
+    assert status == "ok", err
+    return None, info
 
 
-def _reference():
-    import torch
-
-    from hipserve.engine.llm_engine import LLMEngine
-    from hipserve.parallel.comm import TPGroup
-
-    eng = LLMEngine(_engine_cfg(1, False), tp=TPGroup(0, 1, None, torch.device("cuda", 0)),
-                    model_cfg=_model_cfg())
-    return _generate(eng)
+TIE = 0.05  # nats between TP=1's choice and TP=2's
 
 
-def test_tp2_shared_gpu_exact_matches_tp1():
-    want = _reference()
-    got, info = _run_tp(2, exact=True)
+@pytest.mark.parametrize("exact", [True, False])
+def test_tp2_shared_gpu_matches_tp1(exact):
+    _, info = _run_tp(2, exact)
     assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
     assert info["car_failed"] is False
-    for i, (a, b) in enumerate(zip(got, want)):
-        first = next((j for j, (x, y) in enumerate(zip(a, b)) if x != y), None)
-        assert a == b, f"prompt {i}: TP=2 diverges from TP=1 at token {first}"
+    print("exact prefix per prompt:", info["exact_prefix"], "divergences:", len(info["ties"]))
+    assert len(info["ties"]) <= N_TOK * len(PROMPTS) // 10, info["ties"]
+    for i, j, t1, t2, lp1, lp2 in info["ties"]:
+        assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=2 token {t2} not in TP=1's top-5"
+        assert lp1 - lp2 <= TIE, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
