@@ -130,16 +130,11 @@ def main():
                        load_format="dummy" if args.quantization else "auto",
                        extra={"quantization": args.quantization} if args.quantization else {})
     if tp_mode and not leader:
-        from hipserve.config import resolve_model_config
-        from hipserve.engine.llm_engine import worker_loop
+        from hipserve.engine.llm_engine import prepare_model, worker_loop
         from hipserve.engine.model_runner import ModelRunner
 
-        from hipserve.tokenizer import get_tokenizer
-
-        mcfg = resolve_model_config(cfg.model, cfg.served_model_name)
-        tk = get_tokenizer(cfg.model, mcfg, cfg.tokenizer)  # GGUF: the file's own hyper-parameters
-        mcfg = getattr(tk, "model_config_override", None) or mcfg
-        worker_loop(ModelRunner(cfg, mcfg, tpg), tpg)
+        wcfg, mcfg, _ = prepare_model(cfg, tpg)  # GGUF: the file's own hyper-parameters
+        worker_loop(ModelRunner(wcfg, mcfg, tpg), tpg)
         dist.barrier()
         dist.destroy_process_group()
         return

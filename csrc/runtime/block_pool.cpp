@@ -82,6 +82,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def("block_hash", &BlockPool::block_hash)
       .def("match_prefix", &match_prefix_py)
       .def("register_full_blocks", &BlockPool::register_full_blocks)
+      .def("register_blocks", &BlockPool::register_blocks)
       .def("reset_prefix_cache", &BlockPool::reset_prefix_cache)
       .def("refcount", &BlockPool::refcount);
   m.def("build_batch", &build_batch, py::arg("tables"), py::arg("starts"), py::arg("ends"),

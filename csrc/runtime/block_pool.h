@@ -134,6 +134,29 @@ class BlockPool {
     }
   }
 
+  // Incremental form: `tokens` holds ONLY blocks [first, last) and `parent` is the
+  // chained hash of block first-1 (0 for the first block); returns the hash of
+  // block last-1, for the next call. O(new tokens) instead of O(context).
+  uint64_t register_blocks(const std::vector<int>& block_ids, const std::vector<int>& tokens, int first,
+                           int last, uint64_t parent) {
+    std::vector<int> blk(block_size_);
+    for (int i = first; i < last && i < (int)block_ids.size(); ++i) {
+      const size_t off = (size_t)(i - first) * block_size_;
+      if (off + block_size_ > tokens.size()) break;
+      std::memcpy(blk.data(), tokens.data() + off, block_size_ * sizeof(int));
+      const uint64_t h = block_hash(parent, blk);
+      parent = h;
+      if (!prefix_) continue;
+      const int b = block_ids[i];
+      if (has_hash_[b] || cache_.count(h)) continue;
+      cache_[h] = b;
+      hash_[b] = h;
+      has_hash_[b] = 1;
+      std::memcpy(&tokens_[(size_t)b * block_size_], blk.data(), block_size_ * sizeof(int));
+    }
+    return parent;
+  }
+
   void reset_prefix_cache() {
     for (int b : lru_) { drop_hash(b); free_.push_back(b); }
     lru_.clear();

@@ -286,12 +286,24 @@ PRESETS: dict[str, ModelConfig] = {
 }
 
 
-def resolve_model_config(model: str, name: str | None = None) -> ModelConfig:
-    """Preset name, HF model directory (config.json), HF cache id, or a .gguf file."""
+def preset_key(model: str) -> str | None:
+    """Built-in preset a model name / Hub id maps to (``meta-llama/Meta-Llama-3-8B``
+    -> ``llama-3-8b``), or None. Local paths never map to a preset."""
+    if os.path.exists(model):
+        return None
     key = model.lower().split("/")[-1]
-    for k, cfg in PRESETS.items():
+    for k in PRESETS:
         if key == k or key.replace("meta-", "").replace("-instruct", "") == k:
-            return cfg
+            return k
+    return None
+
+
+def resolve_model_config(model: str, name: str | None = None) -> ModelConfig:
+    """Preset name, HF model directory (config.json), HF cache id, or a .gguf file.
+    (A Hub id is first materialised into the cache by ``weights.hub.materialize``.)"""
+    k = preset_key(model)
+    if k is not None and not _hf_cache_dir(model):
+        return PRESETS[k]
     if os.path.isdir(model) and os.path.exists(os.path.join(model, "config.json")):
         with open(os.path.join(model, "config.json")) as f:
             return ModelConfig.from_hf_dict(json.load(f), name=name or os.path.basename(model))

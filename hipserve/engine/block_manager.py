@@ -48,11 +48,17 @@ class BlockManager:
         """Publish the sequence's completely filled blocks to the prefix cache."""
         if not self.prefix_caching:
             return
-        full = seq.num_computed_tokens // self.block_size
+        bs = self.block_size
+        full = seq.num_computed_tokens // bs
         first = getattr(seq, "_registered_blocks", 0)
         if full > first:
-            toks = seq.all_token_ids()[: full * self.block_size]
-            self.pool.register_full_blocks(seq.block_ids, toks, first, full)
+            # only the newly filled blocks' tokens, hash chained from the last call
+            # (O(new tokens) per step, not O(context))
+            a, b, npr = first * bs, full * bs, seq.num_prompt_tokens
+            toks = seq.prompt_token_ids[a:b] if b <= npr else (
+                seq.prompt_token_ids[a:] + seq.output_token_ids[max(0, a - npr):b - npr])
+            seq._reg_hash = self.pool.register_blocks(seq.block_ids, toks, first, full,
+                                                       getattr(seq, "_reg_hash", 0) if first else 0)
             seq._registered_blocks = full
 
     def free(self, seq: Sequence):

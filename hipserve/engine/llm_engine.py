@@ -26,18 +26,33 @@ from .scheduler import ScheduledSeq, Scheduler, SchedulerOutput
 PLACEHOLDER = -1  # output token whose value is still on the GPU (decode lookahead)
 
 
+def prepare_model(cfg: EngineConfig, tp: TPGroup, model_cfg: ModelConfig | None = None):
+    """(cfg, model config, tokenizer) of a pod's model, in the order a first start
+    needs: the Hub id is materialised into the (PVC-backed) HF cache first — rank 0
+    downloads, the other TP ranks wait — and only then are the config and the
+    tokenizer read from it. Collective: every TP rank calls it."""
+    from ..weights.hub import materialize
+
+    path = materialize(cfg.model, cfg.load_format, tp)
+    if path != cfg.model:
+        cfg = cfg.replace(model=path, served_model_name=cfg.served_model_name or cfg.model,
+                          tokenizer=cfg.tokenizer if cfg.tokenizer and cfg.tokenizer != cfg.model else None)
+    mcfg = model_cfg or resolve_model_config(cfg.model, cfg.served_model_name)
+    if cfg.extra.get("quantization") and cfg.load_format == "dummy":
+        # synthetic GGUF tier: ggml llama weights use interleaved-pair RoPE
+        mcfg = mcfg.replace(rope_mode=1)
+    tokenizer = get_tokenizer(cfg.model, mcfg, cfg.tokenizer)
+    if getattr(tokenizer, "model_config_override", None):
+        mcfg = tokenizer.model_config_override
+    return cfg, mcfg, tokenizer
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, tp: TPGroup | None = None,
                  model_cfg: ModelConfig | None = None):
-        self.cfg = cfg
         self.tp = tp or get_tp()
-        self.model_cfg = model_cfg or resolve_model_config(cfg.model, cfg.served_model_name)
-        if cfg.extra.get("quantization") and cfg.load_format == "dummy":
-            # synthetic GGUF tier: ggml llama weights use interleaved-pair RoPE
-            self.model_cfg = self.model_cfg.replace(rope_mode=1)
-        self.tokenizer = get_tokenizer(cfg.model, self.model_cfg, cfg.tokenizer)
-        if getattr(self.tokenizer, "model_config_override", None):
-            self.model_cfg = self.tokenizer.model_config_override
+        self.cfg, self.model_cfg, self.tokenizer = prepare_model(cfg, self.tp, model_cfg)
+        cfg = self.cfg
         self.runner = ModelRunner(cfg, self.model_cfg, self.tp)
         self.max_model_len = self.runner.max_model_len
         self.blocks = BlockManager(self.runner.usable_blocks, cfg.block_size, cfg.enable_prefix_caching)
@@ -46,7 +61,7 @@ class LLMEngine:
         self.seqs: dict[str, Sequence] = {}
         self.detok: dict[str, IncrementalDetokenizer] = {}
         self._ids = itertools.count()
-        self.metrics = EngineMetrics()
+        self.metrics = EngineMetrics(model_name=cfg.model_name)
         self.eos_ids = tuple(self.tokenizer.eos_token_ids or self.model_cfg.eos_token_id or ())
         self.last_step_time = time.monotonic()
         self.lookahead = bool(cfg.extra.get("decode_lookahead", True)) and self.runner.use_graphs

@@ -3,11 +3,15 @@ none — no scrape annotations in any template)."""
 from __future__ import annotations
 
 import time
+from collections import deque
 
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram
 
 _LAT_BUCKETS = (0.001, 0.005, 0.01, 0.02, 0.04, 0.06, 0.08, 0.1, 0.25, 0.5, 0.75, 1.0, 2.5, 5.0,
                 7.5, 10.0, 20.0, 40.0, 80.0)
+
+
+TTFT_WINDOW = 10000
 
 
 class EngineMetrics:
@@ -43,7 +47,8 @@ class EngineMetrics:
         self.num_steps = 0
         self.total_gen = 0
         self.total_prompt = 0
-        self.ttfts: list[float] = []
+        # recent TTFTs for in-process summaries; bounded (a serving pod runs for weeks)
+        self.ttfts: deque[float] = deque(maxlen=TTFT_WINDOW)
 
     def _l(self):
         return {"model_name": self.model_name}

@@ -85,20 +85,14 @@ def _free_port() -> int:
 def _worker(cfg: EngineConfig, rank: int, world: int, port: int):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    from ..config import resolve_model_config
-    from ..engine.llm_engine import worker_loop
+    from ..engine.llm_engine import prepare_model, worker_loop
     from ..engine.model_runner import ModelRunner
     from ..parallel.comm import init_tp
     from ..utils.faults import ParentWatch
 
     ParentWatch().start()  # rank 0 gone -> exit, never hold the GPU as an orphan
     tp = init_tp(world, device_type="cuda" if cfg.device == "cuda" else "cpu")
-    mcfg = resolve_model_config(cfg.model, cfg.served_model_name)
-    from ..tokenizer import get_tokenizer
-
-    tk = get_tokenizer(cfg.model, mcfg, cfg.tokenizer)
-    if getattr(tk, "model_config_override", None):
-        mcfg = tk.model_config_override
+    cfg, mcfg, _ = prepare_model(cfg, tp)  # waits for rank 0's first-start download
     runner = ModelRunner(cfg, mcfg, tp)
     worker_loop(runner, tp)
 

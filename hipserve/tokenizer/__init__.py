@@ -12,6 +12,10 @@ _DEFAULT_CHAT_TEMPLATE = (
     "{% if add_generation_prompt %}<|start_header_id|>assistant<|end_header_id|>\n\n{% endif %}")
 
 
+class UnsupportedContentError(ValueError):
+    """An OpenAI content part the served model cannot consume (HTTP 400)."""
+
+
 def render_chat(template: str, messages: list[dict], bos_token: str = "", eos_token: str = "",
                 add_generation_prompt: bool = True) -> str:
     import jinja2
@@ -24,9 +28,21 @@ def render_chat(template: str, messages: list[dict], bos_token: str = "", eos_to
     env.globals["raise_exception"] = raise_exception
     msgs = []
     for m in messages:
+        if not isinstance(m, dict):
+            raise ValueError("each message must be an object with 'role' and 'content'")
         c = m.get("content", "")
-        if isinstance(c, list):  # OpenAI content parts
-            c = "".join(p.get("text", "") for p in c if isinstance(p, dict))
+        if c is None:
+            c = ""
+        if isinstance(c, list):  # OpenAI content parts: text only (no vision tower is served)
+            for p in c:
+                if not isinstance(p, dict) or p.get("type", "text") != "text":
+                    kind = p.get("type") if isinstance(p, dict) else type(p).__name__
+                    raise UnsupportedContentError(
+                        f"content part of type {kind!r} is not supported: this deployment serves the "
+                        "model's text path only (image / audio inputs are rejected, not dropped)")
+            c = "".join(p.get("text", "") for p in c)
+        elif not isinstance(c, str):
+            raise ValueError("message content must be a string or a list of content parts")
         msgs.append({**m, "content": c})
     return env.from_string(template).render(messages=msgs, bos_token=bos_token, eos_token=eos_token,
                                             add_generation_prompt=add_generation_prompt)

@@ -97,3 +97,34 @@ def test_scheduler_invariants(program, seed):
         _step(sch, bm, live, rng, limits)
     assert not sch.has_unfinished() and not live
     assert bm.num_free() == NUM_BLOCKS
+
+
+def test_idle_admission_ignores_watermark():
+    """with nothing running, a first chunk that fits the free pool only
+    WITHOUT the watermark used to be neither finished nor admitted — retried
+    every step forever, blocking the FCFS queue. It must be admitted."""
+    bm = BlockManager(NUM_BLOCKS, BS, prefix_caching=False)
+    sch = Scheduler(bm, MAX_SEQS, 1000, 1000)
+    # exactly the whole pool: fits without the watermark, not with it
+    seq = Sequence("r0", list(range(NUM_BLOCKS * BS - 1)), SamplingParams(max_tokens=1))
+    sch.add(seq)
+    so = sch.schedule()
+    assert [s.seq.request_id for s in so.prefill] == ["r0"]
+    assert not so.preempted
+
+
+def test_incremental_prefix_registration_matches():
+    """BlockManager.register hashes only the newly filled blocks (chained from the
+    last call); a later sequence with the same prefix must still hit every block."""
+    bm = BlockManager(16, 4, prefix_caching=True)
+    a = Sequence("a", list(range(10, 20)), SamplingParams(max_tokens=8))
+    bm.grow(a, 10)
+    a.num_computed_tokens = 10
+    bm.register(a)                      # blocks 0-1 (8 tokens)
+    a.output_token_ids += [7, 8, 9]
+    bm.grow(a, 13)
+    a.num_computed_tokens = 13
+    bm.register(a)                      # block 2 (prompt tail + outputs)
+    b = Sequence("b", list(range(10, 20)) + [7, 8, 9, 5], SamplingParams(max_tokens=1))
+    bm.match_prefix(b)
+    assert b.num_computed_tokens == 12 and b.block_ids == a.block_ids[:3]

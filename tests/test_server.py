@@ -134,3 +134,70 @@ def test_full_path_ingress_router_two_models():
             await rr.cleanup()
 
     asyncio.run(main())
+
+
+def test_bad_request_fields_are_400_and_engine_survives():
+    """out-of-range / mistyped sampling fields used to reach the
+    engine thread and kill it. Each must be a 400; the engine stays healthy."""
+    async def main():
+        ae, runner, port = await start_engine_server()
+        base = f"http://127.0.0.1:{port}"
+        bad_completions = [{"seed": 2 ** 64}, {"seed": "x"}, {"top_k": 2 ** 40}, {"logprobs": 10 ** 6},
+                           {"temperature": "hot"}, {"stop": 5}, {"n": 0}, {"max_tokens": -3},
+                           {"presence_penalty": float("inf")}, {"stop_token_ids": "1,2"},
+                           {"prompt": [1, 5, 10 ** 9], "stream": True}, {"prompt": [], "stream": True}]
+        bad_chat = [{"logprobs": True, "top_logprobs": "abc"}, {"logprobs": 3},
+                    {"messages": [{"role": "user", "content": [
+                        {"type": "text", "text": "what is this?"},
+                        {"type": "image_url", "image_url": {"url": "data:image/png;base64,AAAA"}}]}]},
+                    {"messages": [{"role": "user", "content": 7}], "stream": True}]
+        async with aiohttp.ClientSession() as s:
+            for extra in bad_completions:
+                body = {"model": "tiny", "prompt": [1, 5, 6], "max_tokens": 3, **extra}
+                r = await s.post(base + "/v1/completions", json=body)
+                assert r.status == 400, (extra, r.status, await r.text())
+            for extra in bad_chat:
+                body = {"model": "tiny", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3, **extra}
+                r = await s.post(base + "/v1/chat/completions", json=body)
+                assert r.status == 400, (extra, r.status, await r.text())
+            assert (await s.get(base + "/health")).status == 200
+            r = await s.post(base + "/v1/completions", json={"model": "tiny", "prompt": [1, 5, 6], "max_tokens": 3,
+                                                              "seed": 2 ** 63 - 1, "n": 2, "logprobs": 2})
+            assert r.status == 200, await r.text()
+            assert ae.alive
+        ae.stop()
+        await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_client_disconnect_aborts_generation():
+    """a client that goes away mid-stream (through the router) must
+    abort the generation in the engine, not run on to max_tokens."""
+    async def main():
+        ae, r1, p1 = await start_engine_server("llama", "tiny-llama")
+        router = ModelRouter([("llama", [f"127.0.0.1:{p1}"])])
+        await router.start("127.0.0.1", 0)
+        eng = ae.engine
+        reader, writer = await asyncio.open_connection("127.0.0.1", router.port)
+        body = json.dumps({"model": "llama", "prompt": [1, 5, 6], "max_tokens": 480, "stream": True,
+                           "ignore_eos": True}).encode()
+        writer.write(b"POST /v1/completions HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                     b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+        await writer.drain()
+        got = b""
+        while got.count(b"data: ") < 3:
+            got += await reader.read(4096)
+        assert eng.has_unfinished()
+        writer.transport.abort()  # RST: the client is gone
+        for _ in range(200):
+            await asyncio.sleep(0.05)
+            if not eng.has_unfinished():
+                break
+        assert not eng.has_unfinished(), "generation kept running after the client disconnected"
+        assert eng.metrics.total_gen < 480
+        await router.stop()
+        ae.stop()
+        await r1.cleanup()
+
+    asyncio.run(main())
