@@ -18,57 +18,83 @@ import time
 import aiohttp
 
 
-async def one_request(session, url, model, prompt, output_len, temperature, top_p, seed=None):
+def request_body(model, prompt, output_len, temperature, top_p, seed=None) -> bytes:
     body = {"model": model, "prompt": prompt, "max_tokens": output_len, "stream": True,
             "ignore_eos": True, "temperature": temperature, "top_p": top_p,
             "stream_options": {"include_usage": True}}
     if seed is not None:
         body["seed"] = seed
+    return json.dumps(body, separators=(",", ":")).encode()
+
+
+_JSON = {"Content-Type": "application/json"}
+
+
+async def one_request(session, url, model, prompt, output_len, temperature, top_p, seed=None, body=None):
+    """One streaming completion; ``body`` = the pre-encoded request (a client
+    has its request ready before the clock starts). Token events are counted
+    without decoding their JSON; only the final usage event is parsed."""
+    if body is None:
+        body = request_body(model, prompt, output_len, temperature, top_p, seed)
     t0 = time.perf_counter()
     ttft = None
     last = t0
     itls = []
     ntok = 0
     usage = None
-    async with session.post(url + "/v1/completions", json=body) as r:
+    async with session.post(url + "/v1/completions", data=body, headers=_JSON) as r:
         if r.status != 200:
             raise RuntimeError(f"HTTP {r.status}: {(await r.text())[:300]}")
         buf = b""
         async for chunk in r.content.iter_any():
             buf += chunk
-            while b"\n\n" in buf:
-                ev, buf = buf.split(b"\n\n", 1)
-                if not ev.startswith(b"data: "):
+            if b"\n\n" not in buf:
+                continue
+            *events, buf = buf.split(b"\n\n")
+            now = time.perf_counter()
+            for ev in events:
+                if not ev.startswith(b"data: ") or ev == b"data: [DONE]":
                     continue
-                data = ev[6:]
-                if data == b"[DONE]":
+                if b'"usage"' in ev:
+                    j = json.loads(ev[6:])
+                    if j.get("usage"):
+                        usage = j["usage"]
+                    if not j.get("choices"):
+                        continue
+                elif b'"choices":[]' in ev:
                     continue
-                j = json.loads(data)
-                if j.get("usage"):
-                    usage = j["usage"]
-                if j.get("choices"):
-                    now = time.perf_counter()
-                    if ttft is None:
-                        ttft = now - t0
-                    else:
-                        itls.append(now - last)
-                    last = now
-                    ntok += 1
+                if ttft is None:
+                    ttft = now - t0
+                else:
+                    itls.append(now - last)
+                last = now
+                ntok += 1
     n = usage["completion_tokens"] if usage else ntok
     return {"ttft": ttft, "tokens": n, "latency": time.perf_counter() - t0, "itl": itls}
 
 
+def make_prompts(rng: random.Random, concurrency: int, input_len: int, vocab: int) -> list[list[int]]:
+    """Synthetic prompts: uniform random token ids in [10, vocab)."""
+    import numpy as np
+
+    g = np.random.default_rng(rng.getrandbits(63))
+    return g.integers(10, vocab, size=(concurrency, input_len)).tolist()
+
+
 async def wave(url, model, concurrency, input_len, output_len, vocab, temperature=0.8, top_p=0.95,
-               rng=None, session=None):
+               rng=None, session=None, prompts=None, bodies=None):
     rng = rng or random.Random(0)
-    prompts = [[rng.randrange(10, vocab) for _ in range(input_len)] for _ in range(concurrency)]
+    if prompts is None and bodies is None:
+        prompts = make_prompts(rng, concurrency, input_len, vocab)
+    if bodies is None:
+        bodies = [request_body(model, p, output_len, temperature, top_p) for p in prompts]
     own = session is None
     if own:
         session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
                                         connector=aiohttp.TCPConnector(limit=0))
     try:
-        res = await asyncio.gather(*[one_request(session, url, model, p, output_len, temperature, top_p)
-                                     for p in prompts])
+        res = await asyncio.gather(*[one_request(session, url, model, None, output_len, temperature, top_p,
+                                                 body=b) for b in bodies])
     finally:
         if own:
             await session.close()
@@ -126,6 +152,11 @@ def main(argv=None):
 
 
 
+def _bodies(rng, key):
+    model, conc, inp, out, vocab, temp, top_p = key
+    return [request_body(model, p, out, temp, top_p) for p in make_prompts(rng, conc, inp, vocab)]
+
+
 def serve_stdio():
     """Line-oriented JSON command loop (used by bench.py so the client runs in its
     own process and never competes with the engine for the GIL)."""
@@ -134,6 +165,8 @@ def serve_stdio():
     loop = asyncio.new_event_loop()
     session = None
     rng = random.Random(1234)
+    pending = None  # (shape key, prompts) of the NEXT wave, generated while idle:
+    # a client has its prompts ready; building them is not part of the timed wave
     for line in sys.stdin:
         cmd = json.loads(line)
         if cmd["op"] == "quit":
@@ -144,17 +177,21 @@ def serve_stdio():
                                              connector=aiohttp.TCPConnector(limit=0))
             session = loop.run_until_complete(mk())
         if cmd["op"] == "wave":
+            key = (cmd["model"], cmd["concurrency"], cmd["input_len"], cmd["output_len"], cmd["vocab"],
+                   cmd.get("temperature", 0.8), cmd.get("top_p", 0.95))
+            bodies = pending[1] if pending is not None and pending[0] == key else _bodies(rng, key)
             t0 = time.perf_counter()
             try:
                 res = loop.run_until_complete(wave(cmd["url"], cmd["model"], cmd["concurrency"],
                                                    cmd["input_len"], cmd["output_len"], cmd["vocab"],
                                                    cmd.get("temperature", 0.8), cmd.get("top_p", 0.95),
-                                                   rng=rng, session=session))
+                                                   rng=rng, session=session, bodies=bodies))
                 out = {"ok": True, "results": res, "elapsed": time.perf_counter() - t0}
             except Exception as e:
                 out = {"ok": False, "error": repr(e)}
             sys.stdout.write(json.dumps(out) + "\n")
             sys.stdout.flush()
+            pending = (key, _bodies(rng, key))
     if session is not None:
         loop.run_until_complete(session.close())
 
