@@ -55,6 +55,18 @@ void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf1
                    const int* top_k, const float* top_p, const long* seeds,
                    const long* steps, float* ws, hipStream_t s);
 
+// penalties.hip — device-side OpenAI penalties + top-n logprobs (graph-capturable).
+// counts int32 [slots, V], seen bits [slots, ceil(V/32)]; slot < 0: row untouched.
+void launch_penalty_apply(void* logits, bool is_bf16, long stride, int rows, int V, const int* slot,
+                          const float* pres, const float* freq, const float* rep, const int* counts,
+                          const unsigned int* seen, hipStream_t s);
+void launch_penalty_update(const long* tok, const int* slot, int n, int* counts, unsigned int* seen, int V,
+                           hipStream_t s);
+void launch_penalty_init(int* counts, unsigned int* seen, int V, const int* slots, const int* off,
+                         const int* n_prompt, const int* toks, int ninit, hipStream_t s);
+void launch_top_logprobs(const void* logits, bool is_bf16, long stride, int rows, int V, const int* nreq,
+                         int* out_ids, float* out_lp, int K, hipStream_t s);
+
 // gguf.hip — qtype: 0 Q4_0, 1 Q4_1, 2 Q8_0, 3 Q4_K, 4 Q5_K, 5 Q6_K (repacked layouts)
 void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long out_stride,
                       const void* q, const void* d, const void* m, int qtype, long row_bytes,

@@ -297,6 +297,68 @@ void car_add_rmsnorm(int64_t state, at::Tensor& out, at::Tensor& residual, const
                                    weight.scalar_type() == at::kFloat, M, N, (float)eps, exch_f32, cur_stream());
 }
 
+static void check_pen_state(const at::Tensor& counts, const at::Tensor& seen, int V) {
+  CHECK_DEV(counts); CHECK_CONTIG(counts); CHECK_CONTIG(seen);
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.dim() == 2 && counts.size(1) == V,
+              "penalty counts: int32 [slots, V]");
+  TORCH_CHECK(seen.scalar_type() == at::kInt && seen.dim() == 2 && seen.size(0) == counts.size(0) &&
+              seen.size(1) == (V + 31) / 32, "penalty seen: int32 [slots, ceil(V/32)]");
+}
+
+void penalty_apply(at::Tensor& logits, const at::Tensor& slot, const at::Tensor& pres, const at::Tensor& freq,
+                   const at::Tensor& rep, const at::Tensor& counts, const at::Tensor& seen) {
+  CHECK_DEV(logits); CHECK_ROWMAJOR(logits);
+  TORCH_CHECK(logits.dim() == 2 && (logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat));
+  const int rows = logits.size(0), V = logits.size(1);
+  check_pen_state(counts, seen, V);
+  TORCH_CHECK(slot.scalar_type() == at::kInt && slot.numel() >= rows);
+  TORCH_CHECK(pres.scalar_type() == at::kFloat && freq.scalar_type() == at::kFloat && rep.scalar_type() == at::kFloat);
+  TORCH_CHECK(pres.numel() >= rows && freq.numel() >= rows && rep.numel() >= rows);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  hipserve::launch_penalty_apply(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), rows, V,
+                                 slot.data_ptr<int>(), pres.data_ptr<float>(), freq.data_ptr<float>(),
+                                 rep.data_ptr<float>(), counts.data_ptr<int>(),
+                                 reinterpret_cast<const unsigned int*>(seen.data_ptr<int>()), cur_stream());
+}
+
+void penalty_update(const at::Tensor& tok, const at::Tensor& slot, at::Tensor& counts, at::Tensor& seen) {
+  CHECK_DEV(tok);
+  TORCH_CHECK(tok.scalar_type() == at::kLong && slot.scalar_type() == at::kInt && slot.numel() >= tok.numel());
+  const int V = counts.size(1);
+  check_pen_state(counts, seen, V);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(tok.device());
+  hipserve::launch_penalty_update(tok.data_ptr<int64_t>(), slot.data_ptr<int>(), tok.numel(), counts.data_ptr<int>(),
+                                  reinterpret_cast<unsigned int*>(seen.data_ptr<int>()), V, cur_stream());
+}
+
+void penalty_init(at::Tensor& counts, at::Tensor& seen, const at::Tensor& slots, const at::Tensor& off,
+                  const at::Tensor& n_prompt, const at::Tensor& toks) {
+  const int V = counts.size(1);
+  check_pen_state(counts, seen, V);
+  TORCH_CHECK(slots.scalar_type() == at::kInt && off.scalar_type() == at::kInt && n_prompt.scalar_type() == at::kInt &&
+              toks.scalar_type() == at::kInt);
+  const int n = slots.numel();
+  TORCH_CHECK(off.numel() == n + 1 && n_prompt.numel() == n);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(counts.device());
+  hipserve::launch_penalty_init(counts.data_ptr<int>(), reinterpret_cast<unsigned int*>(seen.data_ptr<int>()), V,
+                                slots.data_ptr<int>(), off.data_ptr<int>(), n_prompt.data_ptr<int>(),
+                                toks.data_ptr<int>(), n, cur_stream());
+}
+
+void top_logprobs(const at::Tensor& logits, const at::Tensor& nreq, at::Tensor& out_ids, at::Tensor& out_lp) {
+  CHECK_DEV(logits); CHECK_ROWMAJOR(logits);
+  TORCH_CHECK(logits.dim() == 2 && (logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat));
+  const int rows = logits.size(0);
+  TORCH_CHECK(nreq.scalar_type() == at::kInt && nreq.numel() >= rows);
+  TORCH_CHECK(out_ids.scalar_type() == at::kInt && out_lp.scalar_type() == at::kFloat && out_ids.dim() == 2 &&
+              out_ids.sizes() == out_lp.sizes() && out_ids.size(0) >= rows && out_ids.is_contiguous() &&
+              out_lp.is_contiguous() && out_ids.size(1) <= 64);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  hipserve::launch_top_logprobs(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), rows,
+                                logits.size(1), nreq.data_ptr<int>(), out_ids.data_ptr<int>(),
+                                out_lp.data_ptr<float>(), out_ids.size(1), cur_stream());
+}
+
 bool car_error(int64_t state) { return hipserve::car_error(reinterpret_cast<void*>(state)); }
 
 void car_destroy(int64_t state) { hipserve::car_destroy(reinterpret_cast<void*>(state)); }
@@ -603,6 +665,10 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
+  m.def("penalty_apply(Tensor(a!) logits, Tensor slot, Tensor pres, Tensor freq, Tensor rep, Tensor counts, Tensor seen) -> ()");
+  m.def("penalty_update(Tensor tok, Tensor slot, Tensor(a!) counts, Tensor(b!) seen) -> ()");
+  m.def("penalty_init(Tensor(a!) counts, Tensor(b!) seen, Tensor slots, Tensor off, Tensor n_prompt, Tensor toks) -> ()");
+  m.def("top_logprobs(Tensor logits, Tensor nreq, Tensor(a!) out_ids, Tensor(b!) out_lp) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
 
@@ -616,6 +682,10 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
+  m.impl("penalty_apply", &penalty_apply);
+  m.impl("penalty_update", &penalty_update);
+  m.impl("penalty_init", &penalty_init);
+  m.impl("top_logprobs", &top_logprobs);
   m.impl("gguf_gemm", &gguf_gemm);
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("decode_gemm", &decode_gemm);

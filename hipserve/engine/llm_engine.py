@@ -100,6 +100,8 @@ class LLMEngine:
 
     def abort(self, request_id: str):
         seq = self.scheduler.abort(request_id)
+        if seq is not None:
+            self.runner.release(seq)
         self.seqs.pop(request_id, None)
         self.detok.pop(request_id, None)
         return seq
@@ -181,11 +183,11 @@ class LLMEngine:
             with tr.phase("launch"):
                 self._inflight = self._launch(so2, inp, t1, src)
         with tr.phase("wait"):
-            toks, lps = self.runner.wait(handle)
+            toks, lps, top = self.runner.wait(handle)
         now = time.monotonic()
         self._step_done(so, now - t0)
         with tr.phase("process"):
-            return self._process(so, sampled, toks, lps, None, now)
+            return self._process(so, sampled, toks, lps, top, now)
 
     def _schedule_lookahead(self, sampled):
         """Next decode-only batch while the previous step is still in flight, or
@@ -201,8 +203,6 @@ class LLMEngine:
             if j is None or seq.is_prefill:
                 return None
             p = seq.params
-            if p.has_penalties or p.logprobs:
-                return None
             n_out = len(seq.output_token_ids)
             if (p.max_tokens is not None and n_out >= p.max_tokens) or seq.num_tokens >= self.max_model_len:
                 continue  # finishes with the in-flight token: not scheduled again
@@ -289,12 +289,14 @@ class LLMEngine:
             del seq.output_token_ids[n_out:]  # drop a look-ahead placeholder
             del seq.output_logprobs[n_out:]
             self.scheduler.finish(seq, reason)
+            self.runner.release(seq)
             self.metrics.on_finish(seq, now)
             self.seqs.pop(seq.request_id, None)
             self.detok.pop(seq.request_id, None)
         return out
 
     def _finish_output(self, seq: Sequence) -> RequestOutput:
+        self.runner.release(seq)
         self.seqs.pop(seq.request_id, None)
         self.detok.pop(seq.request_id, None)
         return RequestOutput(seq.request_id, [], "", True, seq.finish_reason or "length",

@@ -27,6 +27,7 @@ from ..runtime import native
 from .scheduler import SchedulerOutput
 
 PREFILL_TILE = 128
+TOP_LOGPROBS = 20   # per-row capacity of the device top-logprobs output (OpenAI max)
 GRAPH_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 448, 512]
 
 
@@ -49,8 +50,12 @@ class StepInputs:
     top_p: np.ndarray
     seeds: np.ndarray
     steps: np.ndarray
-    penalties: list | None = None         # per logits row: None | (presence, freq, rep, ids)
-    top_logprobs: int = 0
+    # OpenAI penalties / logprobs, applied on the device (csrc/kernels/penalties.hip)
+    pen_slot: np.ndarray | None = None    # int32 [n]: penalty-state slot per sampled row (-1: none)
+    pen_vals: np.ndarray | None = None    # float32 [3, n]: presence, frequency, repetition
+    nlogprobs: np.ndarray | None = None   # int32 [n]: top-n logprobs wanted per row (0: none)
+    pen_init: tuple | None = None         # (slots, off, n_prompt, toks) int32: slots (re)built this step
+    top_logprobs: int = 0                 # max n over the rows
     # decode lookahead: per decode row, the row of the PREVIOUS graph step's sampled
     # tokens that is this row's input id (-1: use ids[row]); consumed on the device
     src: np.ndarray | None = None
@@ -117,6 +122,12 @@ class ModelRunner:
             shapes = [s for s in self.model.gemm_shapes() if s != tuple(getattr(self.model.lm_head, "shape", ()))]
             self.prefill_gemm_report = prefill_tune.tune(shapes, [ecfg.max_num_batched_tokens], self.device)
             torch.cuda.empty_cache()
+        # device penalty state: one slot per concurrently running penalised sequence
+        V = mcfg.vocab_size
+        nslots = max(1, min(ecfg.max_num_seqs, int(ecfg.extra.get("penalty_slots", 256))))
+        self.pen_counts = torch.zeros(nslots, V, dtype=torch.int32, device=self.device)
+        self.pen_seen = torch.zeros(nslots, (V + 31) // 32, dtype=torch.int32, device=self.device)
+        self._free_pen = list(range(nslots - 1, -1, -1))
         self.num_blocks = self._num_kv_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.block_size)
         self.pad_block = self.num_blocks - 1          # scratch block for graph padding rows
@@ -128,6 +139,7 @@ class ModelRunner:
                                    device=self.device, dtype=torch.float32)
         self.tmp_ml = torch.empty(self.max_bs, nq, self.max_parts, 2, device=self.device,
                                   dtype=torch.float32)
+        self.stats = {"graph_steps": 0, "eager_steps": 0}  # which path each step took
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self._static = None
@@ -248,13 +260,15 @@ class ModelRunner:
             bt_d = bt[np_:]
             ctx_d = np.array([s.end for s in so.decode], dtype=np.int32)
         n = len(sample_seqs)
+        n_pf = len(sample_seqs) - len(so.decode)  # rows sampling after a (last) prefill chunk
         temp = np.empty(n, np.float32)
         topk = np.empty(n, np.int32)
         topp = np.empty(n, np.float32)
         seeds = np.empty(n, np.int64)
         steps = np.empty(n, np.int64)
-        pen = None
+        pen_slot = pen_vals = nlp = pen_init = None
         topn = 0
+        init = []
         for i, q in enumerate(sample_seqs):
             p = q.params
             temp[i] = p.temperature
@@ -263,14 +277,37 @@ class ModelRunner:
             seeds[i] = q.seed
             steps[i] = len(q.output_token_ids)
             if p.has_penalties:
-                if pen is None:
-                    pen = [None] * n
-                pen[i] = (p.presence_penalty, p.frequency_penalty, p.repetition_penalty,
-                          q.prompt_token_ids, list(q.output_token_ids))
+                if pen_slot is None:
+                    pen_slot = np.full(n, -1, np.int32)
+                    pen_vals = np.zeros((3, n), np.float32)
+                    pen_vals[2] = 1.0
+                if q.pen_slot is None:
+                    q.pen_slot = self._free_pen.pop()
+                pen_slot[i] = q.pen_slot
+                pen_vals[:, i] = (p.presence_penalty, p.frequency_penalty, p.repetition_penalty)
+                if i < n_pf:  # first sample (or a recompute): rebuild the slot from the ids so far
+                    init.append(q)
             if p.logprobs:
-                topn = max(topn, p.logprobs)
+                if nlp is None:
+                    nlp = np.zeros(n, np.int32)
+                nlp[i] = min(p.logprobs, TOP_LOGPROBS)
+                topn = max(topn, int(nlp[i]))
+        if init:
+            ids_l = [q.prompt_token_ids + [t for t in q.output_token_ids if t >= 0] for q in init]
+            off = np.zeros(len(init) + 1, np.int32)
+            off[1:] = np.cumsum([len(x) for x in ids_l])
+            pen_init = (np.array([q.pen_slot for q in init], np.int32), off,
+                        np.array([q.num_prompt_tokens for q in init], np.int32),
+                        np.fromiter((t for x in ids_l for t in x), np.int32, int(off[-1])))
         return StepInputs(ids, pos, slots, Tp, len(so.decode), bt_p, cu_q, ctx_p, tiles, bt_d, ctx_d,
-                          np.array(rows, dtype=np.int64), temp, topk, topp, seeds, steps, pen, topn)
+                          np.array(rows, dtype=np.int64), temp, topk, topp, seeds, steps,
+                          pen_slot, pen_vals, nlp, pen_init, topn)
+
+    def release(self, seq):
+        """A finished / aborted sequence gives its penalty slot back."""
+        if seq.pen_slot is not None:
+            self._free_pen.append(seq.pen_slot)
+            seq.pen_slot = None
 
     # ------------------------------------------------------------ execution
     def _t(self, a, dtype=None):
@@ -286,18 +323,19 @@ class ModelRunner:
         return self.buckets[-1] if self.use_graphs else 0
 
     def graph_eligible(self, inp: StepInputs) -> bool:
-        return (self.use_graphs and inp.num_prefill_tokens == 0 and inp.penalties is None
-                and inp.top_logprobs == 0 and 0 < inp.num_decode <= self.buckets[-1])
+        # penalties and logprobs run inside the graph (device state + per-row inputs)
+        return (self.use_graphs and inp.num_prefill_tokens == 0 and inp.pen_init is None
+                and 0 < inp.num_decode <= self.buckets[-1])
 
     @torch.inference_mode()
     def execute(self, inp: StepInputs):
         """Returns (tokens np.int64 [n], logprobs np.float32 [n], top_logprobs or None)."""
         n = len(inp.logits_rows)
         if self.graph_eligible(inp):
-            tok, lp = self.wait(self.launch(inp))
-            return tok, lp, None
+            return self.wait(self.launch(inp))
         if inp.src is not None:
             raise RuntimeError("device-side input ids (lookahead) need the hipGraph decode path")
+        self.stats["eager_steps"] += 1
         ids = self._t(inp.ids)
         meta = AttnMeta(
             num_prefill_tokens=inp.num_prefill_tokens, num_decode=inp.num_decode,
@@ -314,34 +352,26 @@ class ModelRunner:
             return np.zeros(0, np.int64), np.zeros(0, np.float32), None
         rows = self._t(inp.logits_rows)
         logits = self.model.compute_logits(hidden.index_select(0, rows))
-        if inp.penalties is not None:
-            logits = self._apply_penalties(logits, inp.penalties)
+        pslot = None
+        if inp.pen_slot is not None:
+            if inp.pen_init is not None:
+                self.ops.penalty_init(self.pen_counts, self.pen_seen, *[self._t(a) for a in inp.pen_init])
+            pslot = self._t(inp.pen_slot)
+            pv = self._t(inp.pen_vals)
+            self.ops.penalty_apply(logits, pslot, pv[0], pv[1], pv[2], self.pen_counts, self.pen_seen)
         tok = torch.empty(n, dtype=torch.long, device=self.device)
         lp = torch.empty(n, dtype=torch.float32, device=self.device)
         self.ops.sample(tok, lp, logits, self._t(inp.temperature), self._t(inp.top_k),
                         self._t(inp.top_p), self._t(inp.seeds), self._t(inp.steps))
+        if pslot is not None:
+            self.ops.penalty_update(tok, pslot, self.pen_counts, self.pen_seen)
         top = None
         if inp.top_logprobs:
-            ls = torch.log_softmax(logits.float(), dim=-1)
-            v, i = ls.topk(inp.top_logprobs, dim=-1)
-            top = (i.cpu().numpy(), v.cpu().numpy())
+            ti = torch.empty(n, TOP_LOGPROBS, dtype=torch.int32, device=self.device)
+            tl = torch.empty(n, TOP_LOGPROBS, dtype=torch.float32, device=self.device)
+            self.ops.top_logprobs(logits, self._t(inp.nlogprobs), ti, tl)
+            top = (ti.cpu().numpy(), tl.cpu().numpy())
         return tok.cpu().numpy(), lp.cpu().numpy(), top
-
-    def _apply_penalties(self, logits, pens):
-        logits = logits.float().clone()
-        V = logits.shape[1]
-        for i, p in enumerate(pens):
-            if p is None:
-                continue
-            pres, freq, rep, prompt, out = p
-            if out and (pres or freq):
-                cnt = torch.bincount(torch.tensor(out, device=logits.device), minlength=V)[:V].float()
-                logits[i] -= freq * cnt + pres * (cnt > 0).float()
-            if rep != 1.0:
-                seen = torch.tensor(sorted(set(prompt) | set(out)), device=logits.device, dtype=torch.long)
-                v = logits[i, seen]
-                logits[i, seen] = torch.where(v > 0, v / rep, v * rep)
-        return logits
 
     # ------------------------------------------------------------ hipGraphs
     def _graph_forward(self, b: int):
@@ -353,8 +383,13 @@ class ModelRunner:
         ids = torch.where(src >= 0, st["tok"].index_select(0, src.clamp(min=0)), st["ids"][:b])
         hidden = self.model.forward(ids, meta, self.kv)
         logits = self.model.compute_logits(hidden)
+        # penalties / top-n logprobs: early-exit kernels for rows that want none
+        self.ops.penalty_apply(logits, st["pslot"][:b], st["pres"][:b], st["freq"][:b], st["rep"][:b],
+                               self.pen_counts, self.pen_seen)
         self.ops.sample(st["tok"][:b], st["lp"][:b], logits, st["temp"][:b], st["topk"][:b],
                         st["topp"][:b], st["seeds"][:b], st["steps"][:b])
+        self.ops.penalty_update(st["tok"][:b], st["pslot"][:b], self.pen_counts, self.pen_seen)
+        self.ops.top_logprobs(logits, st["nlp"][:b], st["top_ids"][:b], st["top_lp"][:b])
 
     def _stage_in(self, b: int, sg):
         """Pinned staging set -> device static inputs, one zero-copy dispatch
@@ -366,7 +401,8 @@ class ModelRunner:
 
     def _stage_out(self, b: int, sg):
         st = self._static
-        torch.ops.hipserve.stage_copy([sg["tok"][:b], sg["lp"][:b]], [st["tok"][:b], st["lp"][:b]],
+        torch.ops.hipserve.stage_copy([sg["tok"][:b], sg["lp"][:b], sg["top_ids"][:b], sg["top_lp"][:b]],
+                                      [st["tok"][:b], st["lp"][:b], st["top_ids"][:b], st["top_lp"][:b]],
                                       self.device.index or 0)
 
     @torch.inference_mode()
@@ -378,27 +414,33 @@ class ModelRunner:
         for _ in range(2):
             self._stage.append({
                 "h64": torch.zeros(6 * mb, dtype=torch.long).pin_memory(),
-                "h32": torch.zeros(mb * W + 2 * mb, dtype=torch.int32).pin_memory(),
-                "hf": torch.zeros(2 * mb, dtype=torch.float32).pin_memory(),
+                "h32": torch.zeros(mb * W + 4 * mb, dtype=torch.int32).pin_memory(),
+                "hf": torch.zeros(5 * mb, dtype=torch.float32).pin_memory(),
                 "tok": torch.zeros(mb, dtype=torch.long).pin_memory(),
                 "lp": torch.zeros(mb, dtype=torch.float32).pin_memory(),
+                "top_ids": torch.zeros(mb, TOP_LOGPROBS, dtype=torch.int32).pin_memory(),
+                "top_lp": torch.zeros(mb, TOP_LOGPROBS, dtype=torch.float32).pin_memory(),
                 "done": None,
             })
         self._launches = 0
         # HIPSERVE_STAGE_COPY=blit: per-buffer hipMemcpyAsync instead of the staging kernel
         self._stage_kernel = os.environ.get("HIPSERVE_STAGE_COPY", "kernel") != "blit"
         d64 = torch.zeros(6 * mb, dtype=torch.long, device=dev)
-        d32 = torch.zeros(mb * W + 2 * mb, dtype=torch.int32, device=dev)
-        df = torch.zeros(2 * mb, dtype=torch.float32, device=dev)
+        d32 = torch.zeros(mb * W + 4 * mb, dtype=torch.int32, device=dev)
+        df = torch.zeros(5 * mb, dtype=torch.float32, device=dev)
         st = {
             "d64": d64, "d32": d32, "df": df,
             "ids": d64[0:mb], "pos": d64[mb:2 * mb], "slots": d64[2 * mb:3 * mb],
             "seeds": d64[3 * mb:4 * mb], "steps": d64[4 * mb:5 * mb], "src": d64[5 * mb:6 * mb],
             "bt": d32[: mb * W].view(mb, W), "ctx": d32[mb * W: mb * W + mb],
             "topk": d32[mb * W + mb: mb * W + 2 * mb],
+            "pslot": d32[mb * W + 2 * mb: mb * W + 3 * mb], "nlp": d32[mb * W + 3 * mb: mb * W + 4 * mb],
             "temp": df[0:mb], "topp": df[mb:2 * mb],
+            "pres": df[2 * mb:3 * mb], "freq": df[3 * mb:4 * mb], "rep": df[4 * mb:5 * mb],
             "tok": torch.zeros(mb, dtype=torch.long, device=dev),
             "lp": torch.zeros(mb, dtype=torch.float32, device=dev),
+            "top_ids": torch.zeros(mb, TOP_LOGPROBS, dtype=torch.int32, device=dev),
+            "top_lp": torch.zeros(mb, TOP_LOGPROBS, dtype=torch.float32, device=dev),
         }
         self._static = st
         st["bt"].fill_(self.pad_block)
@@ -406,6 +448,8 @@ class ModelRunner:
         st["slots"].fill_(self.pad_block * self.block_size)
         st["topp"].fill_(1.0)
         st["src"].fill_(-1)
+        st["pslot"].fill_(-1)
+        st["rep"].fill_(1.0)
         t0 = time.time()
         # TP ranks enter the captured collectives together (the tuner and the
         # weight packing take different times per rank; a custom-collective
@@ -443,6 +487,7 @@ class ModelRunner:
         n = inp.num_decode
         b = next(x for x in self.buckets if x >= n)
         mb, W = self.buckets[-1], self.width
+        self.stats["graph_steps"] += 1
         sg = self._stage[self._launches & 1]
         self._launches += 1
         if sg["done"] is not None:
@@ -470,10 +515,23 @@ class ModelRunner:
         a32[mb * W: mb * W + n] = inp.ctx_decode
         a32[mb * W + n: mb * W + b] = 1
         a32[mb * W + mb: mb * W + mb + n] = inp.top_k
+        o = mb * W + 2 * mb  # penalty slots, then top-n logprobs counts
+        a32[o:o + n] = inp.pen_slot if inp.pen_slot is not None else -1
+        a32[o + n:o + b] = -1
+        a32[o + mb:o + mb + n] = inp.nlogprobs if inp.nlogprobs is not None else 0
+        a32[o + mb + n:o + mb + b] = 0
         af = hf.numpy()
         af[0:n] = inp.temperature
         af[n:b] = 0.0
         af[mb:mb + n] = inp.top_p
+        if inp.pen_vals is not None:
+            af[2 * mb:2 * mb + n] = inp.pen_vals[0]
+            af[3 * mb:3 * mb + n] = inp.pen_vals[1]
+            af[4 * mb:4 * mb + n] = inp.pen_vals[2]
+        else:
+            af[2 * mb:2 * mb + n] = 0.0
+            af[3 * mb:3 * mb + n] = 0.0
+            af[4 * mb:4 * mb + n] = 1.0
         st = self._static
         if self._stage_kernel:  # the graph of this parity stages in/out itself
             self.graphs[(b, (self._launches - 1) & 1)].replay()
@@ -483,14 +541,16 @@ class ModelRunner:
             st["d32"][mb * W:].copy_(h32[mb * W:], non_blocking=True)
             st["df"].copy_(hf, non_blocking=True)
             self.graphs[b].replay()
-            sg["tok"][:n].copy_(st["tok"][:n], non_blocking=True)
-            sg["lp"][:n].copy_(st["lp"][:n], non_blocking=True)
+            for k in ("tok", "lp", "top_ids", "top_lp"):
+                sg[k][:n].copy_(st[k][:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         sg["done"] = ev
-        return (sg, n, ev)
+        return (sg, n, ev, inp.top_logprobs)
 
     def wait(self, handle):
-        sg, n, ev = handle
+        """(tokens, logprobs, top-n (ids, logprobs) or None) of a launched step."""
+        sg, n, ev, topn = handle
         ev.synchronize()
-        return sg["tok"][:n].numpy().copy(), sg["lp"][:n].numpy().copy()
+        top = (sg["top_ids"][:n].numpy().copy(), sg["top_lp"][:n].numpy().copy()) if topn else None
+        return sg["tok"][:n].numpy().copy(), sg["lp"][:n].numpy().copy(), top

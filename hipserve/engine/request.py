@@ -126,6 +126,7 @@ class Sequence:
     first_token_time: float | None = None
     last_token_time: float | None = None
     seed: int = 0
+    pen_slot: int | None = None         # device penalty-state slot (ModelRunner), while it has penalties
     # detokenizer state
     output_text: str = ""
     _decoded_upto: int = 0

@@ -101,6 +101,18 @@ class KernelOps:
     def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
         self._op.sample(out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps)
 
+    def penalty_apply(self, logits, slot, pres, freq, rep, counts, seen):
+        self._op.penalty_apply(logits, slot, pres, freq, rep, counts, seen)
+
+    def penalty_update(self, tok, slot, counts, seen):
+        self._op.penalty_update(tok, slot, counts, seen)
+
+    def penalty_init(self, counts, seen, slots, off, n_prompt, toks):
+        self._op.penalty_init(counts, seen, slots, off, n_prompt, toks)
+
+    def top_logprobs(self, logits, nreq, out_ids, out_lp):
+        self._op.top_logprobs(logits, nreq, out_ids, out_lp)
+
 
 class ReferenceOps:
     """PyTorch reference path (CPU plumbing engine / numerics oracle)."""
@@ -149,6 +161,18 @@ class ReferenceOps:
         out[:T, : nq * D].copy_(ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q,
                                                       ctx_lens, nq, nkv, scale, window).view(T, nq * D))
         return out
+
+    def penalty_apply(self, logits, slot, pres, freq, rep, counts, seen):
+        ref.penalty_apply(logits, slot, pres, freq, rep, counts, seen)
+
+    def penalty_update(self, tok, slot, counts, seen):
+        ref.penalty_update(tok, slot, counts, seen)
+
+    def penalty_init(self, counts, seen, slots, off, n_prompt, toks):
+        ref.penalty_init(counts, seen, slots, off, n_prompt, toks)
+
+    def top_logprobs(self, logits, nreq, out_ids, out_lp):
+        ref.top_logprobs(logits, nreq, out_ids, out_lp)
 
     def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
         t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, bf16_row=False)

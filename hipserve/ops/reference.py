@@ -263,3 +263,79 @@ def fill_uniform(out: torch.Tensor, row0: int, col0: int, gcols: int, key: int, 
     v = (u - 0.5) * torch.tensor(2.0 * scale, dtype=torch.float32)
     out.copy_(v.to(torch.bfloat16).to(out.dtype))
     return out
+
+
+# ---------------------------------------------------------------- penalties / logprobs
+# Oracle of csrc/kernels/penalties.hip. State per slot: counts int32 [slots, V]
+# (generated-token occurrences), seen int32 [slots, ceil(V/32)] bitmask (prompt or
+# generated). vLLM / OpenAI order: repetition first, then frequency + presence.
+def _seen_mask(seen: torch.Tensor, V: int) -> torch.Tensor:
+    v = torch.arange(V, device=seen.device)
+    return ((seen[:, v // 32] >> (v % 32)) & 1).bool()
+
+
+def penalty_apply(logits, slot, pres, freq, rep, counts, seen):
+    rows, V = logits.shape
+    for r in range(rows):
+        s = int(slot[r])
+        p, f, q = float(pres[r]), float(freq[r]), float(rep[r])
+        if s < 0 or (p == 0.0 and f == 0.0 and q == 1.0):
+            continue
+        l = logits[r].float()
+        m = _seen_mask(seen[s:s + 1], V)[0]
+        l = torch.where(m, torch.where(l > 0, l / q, l * q), l)
+        c = counts[s].float()
+        l = l - f * c - p * (c > 0).float()
+        logits[r].copy_(l.to(logits.dtype))
+    return logits
+
+
+def penalty_update(tok, slot, counts, seen):
+    V = counts.shape[1]
+    for r in range(tok.shape[0]):
+        s, t = int(slot[r]), int(tok[r])
+        if s < 0 or not 0 <= t < V:
+            continue
+        counts[s, t] += 1
+        seen[s, t // 32] |= _bit(t)
+
+
+def _bit(t: int) -> int:
+    b = 1 << (t % 32)
+    return b - (1 << 32) if b >= (1 << 31) else b  # int32 two's complement
+
+
+def penalty_init(counts, seen, slots, off, n_prompt, toks):
+    V = counts.shape[1]
+    for j in range(slots.shape[0]):
+        s = int(slots[j])
+        counts[s].zero_()
+        seen[s].zero_()
+        a, b, npr = int(off[j]), int(off[j + 1]), int(n_prompt[j])
+        for i in range(a, b):
+            t = int(toks[i])
+            if not 0 <= t < V:
+                continue
+            seen[s, t // 32] |= _bit(t)
+            if i - a >= npr:
+                counts[s, t] += 1
+
+
+def top_logprobs(logits, nreq, out_ids, out_lp):
+    """n largest log-softmax entries per row (ties -> lowest id), K = out width."""
+    K = out_ids.shape[1]
+    out_ids.fill_(-1)
+    out_lp.fill_(float("-inf"))
+    for r in range(logits.shape[0]):
+        n = min(int(nreq[r]), K)
+        if n <= 0:
+            continue
+        l = logits[r].float()
+        ls = l - torch.logsumexp(l, 0)
+        # order by (bf16-rounded value desc, id asc) like the kernel's 16-bit keys
+        key = l.to(torch.bfloat16).float()
+        order = sorted(range(l.shape[0]), key=lambda i: (-key[i].item(), i))[:n] if l.shape[0] <= 4096 else \
+            torch.argsort(-key, stable=True)[:n].tolist()
+        for i, v in enumerate(order):
+            out_ids[r, i] = v
+            out_lp[r, i] = ls[v]

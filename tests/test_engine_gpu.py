@@ -25,17 +25,84 @@ PROMPTS = [[1] + list(range(10, 300)), [1, 7, 8, 9], [1] + [42] * 40, list(range
 
 
 def test_graph_matches_eager():
-    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    """hipGraph decode vs eager decode, batch = a graph bucket (no padding rows):
+    every greedy token must match exactly (same kernels, same GEMM choices)."""
+    sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
     g = _engine(False)
     assert g.runner.use_graphs and g.runner.graphs
     e = _engine(True)
-    rg = g.generate(PROMPTS, sp)
+    rg = g.generate(PROMPTS, sp)  # 4 sequences: bucket 4
     re_ = e.generate(PROMPTS, sp)
+    assert g.runner.stats["graph_steps"] >= 20 and e.runner.stats["graph_steps"] == 0
     for a, b in zip(rg, re_):
-        assert len(a[0]) == 12
-        assert a[0][:3] == b[0][:3]
-        agree = sum(x == y for x, y in zip(a[0], b[0])) / 12
-        assert agree >= 0.5
+        assert len(a[0]) == 24
+        assert a[0] == b[0]
+
+
+def test_penalties_and_logprobs_stay_on_graph():
+    """One penalised + logprobs request in a batch of 8 keeps the whole batch on
+    the hipGraph + lookahead path (device-side penalty state, in-graph top-n
+    logprobs), and matches the eager engine token for token and logprob for
+    logprob."""
+    prompts = PROMPTS * 2
+    sps = [SamplingParams(temperature=0.0, max_tokens=20, ignore_eos=True) for _ in prompts]
+    sps[1] = SamplingParams(temperature=0.0, max_tokens=20, ignore_eos=True, frequency_penalty=1.5,
+                            presence_penalty=0.5, repetition_penalty=1.3, logprobs=5)
+
+    def run(eng):
+        rids = [eng.add_request(None, p, sp).request_id for p, sp in zip(prompts, sps)]
+        toks, lps = {r: [] for r in rids}, {r: [] for r in rids}
+        while eng.has_unfinished():
+            for o in eng.step():
+                toks[o.request_id] += o.new_token_ids
+                if o.logprobs and len(o.logprobs) > 1:
+                    lps[o.request_id].append(o.logprobs[1])
+        return [toks[r] for r in rids], lps[rids[1]]
+
+    g, e = _engine(False), _engine(True)
+    assert g.lookahead
+    tg, lg = run(g)
+    te, le = run(e)
+    assert tg == te
+    assert g.runner.stats["graph_steps"] >= 18, g.runner.stats  # decode stayed on the graph path
+    assert len(lg) == len(le) == 20
+    for a, b in zip(lg, le):
+        assert [i for i, _ in a] == [i for i, _ in b]
+        assert all(abs(x - y) < 1e-3 for (_, x), (_, y) in zip(a, b))
+    # the penalty really acted: the penalised greedy sequence differs from the plain one
+    assert tg[1] != tg[5]
+    assert len(g.runner._free_pen) == g.runner.pen_counts.shape[0]  # slot returned
+
+
+def test_full_model_logits_vs_fp32_reference():
+    """Prefill logits of the GPU engine (HIP kernels, bf16) vs the CPU fp32 engine
+    with identical weights: max |error| <= 0.05 (logit std ~0.45) and the argmax
+    agrees on >= 90% of positions."""
+    g = _engine(True)
+    c = _engine(True, device="cpu", dtype="float32")
+    gm, cm = g.runner.model, c.runner.model
+    cm.embed, cm.lm_head, cm.norm = gm.embed.float().cpu(), gm.lm_head.float().cpu(), gm.norm.float().cpu()
+    for lg, lc in zip(gm.layers, cm.layers):
+        for f in ("ln1", "wqkv", "wo", "ln2", "wgu", "wd"):
+            setattr(lc, f, getattr(lg, f).float().cpu())
+    got = {}
+    for name, m in (("gpu", gm), ("cpu", cm)):
+        orig = m.compute_logits
+
+        def cap(h, orig=orig, name=name):
+            out = orig(h)
+            got.setdefault(name, []).append(out.float().cpu().clone())
+            return out
+
+        m.compute_logits = cap
+    sp = SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True)
+    g.generate(PROMPTS, sp)
+    c.generate(PROMPTS, sp)
+    a, b = torch.cat(got["gpu"]), torch.cat(got["cpu"])
+    assert a.shape == b.shape
+    err = (a - b).abs()
+    assert err.max().item() <= 0.05, (err.max().item(), b.std().item())
+    assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.9
 
 
 def test_sampled_generation_runs():

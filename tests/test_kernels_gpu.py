@@ -416,3 +416,62 @@ def test_stage_copy_host_device_roundtrip(ops):
     ev.record()
     ev.synchronize()
     assert torch.equal(out64, h64 * 3) and torch.equal(outf, hf)
+
+
+@pytest.mark.parametrize("V,dt", [(32000, torch.bfloat16), (128256, torch.bfloat16), (1000, torch.float32)])
+def test_penalty_and_top_logprobs_kernels(V, dt):
+    """csrc/kernels/penalties.hip vs the torch reference (hipserve/ops/reference.py):
+    slot init from prompt + generated ids, in-graph updates, penalty application
+    (rows without a slot untouched) and top-n logprobs with lowest-id tie breaks."""
+    from hipserve.ops import reference as R
+
+    op = torch.ops.hipserve
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(V)
+    rows, slots = 6, 4
+    words = (V + 31) // 32
+    counts = torch.zeros(slots, V, dtype=torch.int32)
+    seen = torch.zeros(slots, words, dtype=torch.int32)
+    # init slots 0, 2, 3 from (prompt, generated) histories
+    hist = [(torch.randint(0, V, (50,), generator=g), torch.randint(0, 200, (30,), generator=g))
+            for _ in range(3)]
+    sl = torch.tensor([0, 2, 3], dtype=torch.int32)
+    toks = torch.cat([torch.cat([p, o]) for p, o in hist]).int()
+    off = torch.tensor([0, 80, 160, 240], dtype=torch.int32)
+    npr = torch.tensor([50, 50, 50], dtype=torch.int32)
+    cd, sd = counts.to(dev), seen.to(dev)
+    op.penalty_init(cd, sd, sl.to(dev), off.to(dev), npr.to(dev), toks.to(dev))
+    R.penalty_init(counts, seen, sl, off, npr, toks)
+    assert torch.equal(cd.cpu(), counts) and torch.equal(sd.cpu(), seen)
+    # a sampled step updates the slots
+    tok = torch.randint(0, V, (rows,), generator=g).long()
+    slot = torch.tensor([0, -1, 2, 3, -1, -1], dtype=torch.int32)
+    op.penalty_update(tok.to(dev), slot.to(dev), cd, sd)
+    R.penalty_update(tok, slot, counts, seen)
+    assert torch.equal(cd.cpu(), counts) and torch.equal(sd.cpu(), seen)
+    # apply: row 3 has a slot but no active penalty (untouched), rows 1/4/5 no slot
+    logits = (torch.randn(rows, V, generator=g) * 3).to(dt)
+    pres = torch.tensor([0.5, 1.0, -0.7, 0.0, 0.0, 0.0])
+    freq = torch.tensor([1.5, 1.0, 0.3, 0.0, 0.0, 0.0])
+    rep = torch.tensor([1.3, 1.0, 0.8, 1.0, 1.0, 1.0])
+    got = logits.to(dev)
+    op.penalty_apply(got, slot.to(dev), pres.to(dev), freq.to(dev), rep.to(dev), cd, sd)
+    want = logits.clone()
+    R.penalty_apply(want, slot, pres, freq, rep, counts, seen)
+    assert torch.equal(got.cpu()[[1, 3, 4, 5]], logits[[1, 3, 4, 5]])
+    rel = 1e-5 if dt == torch.float32 else 2.0 ** -7  # one bf16 ulp
+    assert ((got.cpu().float() - want.float()).abs() <= want.float().abs() * rel + 1e-5).all()
+    # top-n logprobs (with forced ties in row 2)
+    want[2, 100:110] = want[2].max() + 1
+    got = want.to(dev)
+    nreq = torch.tensor([5, 0, 20, 1, 3, 7], dtype=torch.int32)
+    ids = torch.empty(rows, 20, dtype=torch.int32, device=dev)
+    lps = torch.empty(rows, 20, dtype=torch.float32, device=dev)
+    op.top_logprobs(got, nreq.to(dev), ids, lps)
+    rid = torch.empty(rows, 20, dtype=torch.int32)
+    rlp = torch.empty(rows, 20)
+    R.top_logprobs(want, nreq, rid, rlp)
+    assert torch.equal(ids.cpu(), rid)
+    fin = torch.isfinite(rlp)
+    assert torch.equal(torch.isfinite(lps.cpu()), fin)
+    assert (lps.cpu()[fin] - rlp[fin]).abs().max().item() < 1e-3

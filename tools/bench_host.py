@@ -46,6 +46,7 @@ def make_fake_runner(decode_ms: float, prefill_ms: float, vocab: int, max_num_se
             self.device_free_at = time.perf_counter()
             self.busy = 0.0
             self.rng = np.random.default_rng(0)
+            self._free_pen = list(range(max_num_seqs))
 
         def _occupy(self, ms):
             now = time.perf_counter()
@@ -62,13 +63,12 @@ def make_fake_runner(decode_ms: float, prefill_ms: float, vocab: int, max_num_se
             d = t - time.perf_counter()
             if d > 0:
                 time.sleep(d)
-            return self.rng.integers(10, vocab, n), np.zeros(n, np.float32)
+            return self.rng.integers(10, vocab, n), np.zeros(n, np.float32), None
 
         def execute(self, inp):
             n = len(inp.logits_rows)
             if self.graph_eligible(inp):
-                tok, lp = self.wait(self.launch(inp))
-                return tok, lp, None
+                return self.wait(self.launch(inp))
             t = self._occupy(prefill_ms if inp.num_prefill_tokens else decode_ms)
             d = t - time.perf_counter()
             if d > 0:
