@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: fp32 on the host with gloo collectives (tests of the DP / TP paths)")
     ap.add_argument("--num-kv-blocks", type=int, default=None, help="KV pool size (default: from HBM)")
+    ap.add_argument("--request-rate", type=float, default=None,
+                    help="gateway path: open-loop Poisson arrivals at this rate (req/s) for the timed "
+                         "region (steps x concurrency requests) instead of closed-loop waves")
     return ap.parse_args()
 
 
@@ -191,10 +194,17 @@ def main():
     barrier()
     t0 = time.perf_counter()
     tok_total, ttfts = 0, []
-    for _ in range(args.steps):
-        n, tt = wave()
-        tok_total += n
-        ttfts += tt
+    if args.request_rate and args.path == "gateway":
+        res, _ = lg.open_loop(url=stack.url, model=args.model, rate=args.request_rate,
+                              num_requests=args.steps * args.concurrency, input_len=args.input_len,
+                              output_len=args.output_len, vocab=min(V, 100000), temperature=args.temperature,
+                              top_p=args.top_p)
+        tok_total, ttfts = sum(r["tokens"] for r in res), [r["ttft"] for r in res]
+    else:
+        for _ in range(args.steps):
+            n, tt = wave()
+            tok_total += n
+            ttfts += tt
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -226,6 +236,7 @@ def main():
         "dtype": ("bf16" if cuda else "fp32") if not args.quantization else f"bf16 activations, GGUF {args.quantization.upper()} weights",
         "data": "synthetic prompts (random token ids), random-init weights",
         "p50_ttft_ms": round(1000 * float(p50), 2),
+        "load": f"open-loop Poisson {args.request_rate} req/s" if args.request_rate else "closed-loop waves",
         "path": args.path,
         "config": {
             "model": args.model + (f" GGUF {args.quantization.upper()}" if args.quantization else ""),

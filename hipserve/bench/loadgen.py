@@ -101,6 +101,41 @@ async def wave(url, model, concurrency, input_len, output_len, vocab, temperatur
     return res
 
 
+async def open_loop(url, model, rate, num_requests, input_len, output_len, vocab, temperature=0.8, top_p=0.95,
+                    rng=None, session=None, burstiness=1.0):
+    """Open-loop arrivals: ``num_requests`` requests with gamma-distributed
+    inter-arrival gaps of mean 1/``rate`` seconds (burstiness 1.0 = Poisson), each
+    sent at its arrival time whether or not earlier ones finished — TTFT then
+    reflects queueing under a realistic load instead of one synchronised wave."""
+    import numpy as np
+
+    rng = rng or random.Random(0)
+    g = np.random.default_rng(rng.getrandbits(63))
+    bodies = [request_body(model, p, output_len, temperature, top_p)
+              for p in make_prompts(rng, num_requests, input_len, vocab)]
+    shape = 1.0 / burstiness
+    gaps = g.gamma(shape, 1.0 / (rate * shape), size=num_requests) if rate > 0 else np.zeros(num_requests)
+    own = session is None
+    if own:
+        session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
+                                        connector=aiohttp.TCPConnector(limit=0))
+    try:
+        t0 = time.perf_counter()
+        at = np.cumsum(gaps)
+
+        async def fire(i):
+            d = t0 + at[i] - time.perf_counter()
+            if d > 0:
+                await asyncio.sleep(d)
+            return await one_request(session, url, model, None, output_len, temperature, top_p, body=bodies[i])
+
+        res = await asyncio.gather(*[fire(i) for i in range(num_requests)])
+        return res, time.perf_counter() - t0
+    finally:
+        if own:
+            await session.close()
+
+
 def summarize(results, elapsed):
     toks = sum(r["tokens"] for r in results)
     ttfts = sorted(r["ttft"] for r in results if r["ttft"] is not None)
@@ -137,6 +172,10 @@ def main(argv=None):
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--waves", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--request-rate", type=float, default=None,
+                    help="open loop: mean arrivals per second (Poisson; --burstiness for gamma) instead of waves")
+    ap.add_argument("--num-requests", type=int, default=256, help="open loop: requests to send")
+    ap.add_argument("--burstiness", type=float, default=1.0)
     a = ap.parse_args(argv)
 
     async def go():
@@ -145,6 +184,10 @@ def main(argv=None):
             async with aiohttp.ClientSession() as s:
                 j = await (await s.get(a.url + "/v1/models")).json()
                 model = j["data"][0]["id"]
+        if a.request_rate is not None:
+            res, el = await open_loop(a.url, model, a.request_rate, a.num_requests, a.input_len, a.output_len,
+                                      a.vocab, burstiness=a.burstiness)
+            return {**summarize(res, el), "mode": "open-loop", "request_rate": a.request_rate}
         return await run(a.url, model, a.concurrency, a.input_len, a.output_len, a.vocab, a.waves, a.warmup)
 
     print(json.dumps(asyncio.run(go())))
@@ -176,6 +219,18 @@ def serve_stdio():
                 return aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
                                              connector=aiohttp.TCPConnector(limit=0))
             session = loop.run_until_complete(mk())
+        if cmd["op"] == "open":
+            try:
+                res, el = loop.run_until_complete(open_loop(
+                    cmd["url"], cmd["model"], cmd["rate"], cmd["num_requests"], cmd["input_len"],
+                    cmd["output_len"], cmd["vocab"], cmd.get("temperature", 0.8), cmd.get("top_p", 0.95),
+                    rng=rng, session=session, burstiness=cmd.get("burstiness", 1.0)))
+                out = {"ok": True, "results": res, "elapsed": el}
+            except Exception as e:
+                out = {"ok": False, "error": repr(e)}
+            sys.stdout.write(json.dumps(out) + "\n")
+            sys.stdout.flush()
+            continue
         if cmd["op"] == "wave":
             key = (cmd["model"], cmd["concurrency"], cmd["input_len"], cmd["output_len"], cmd["vocab"],
                    cmd.get("temperature", 0.8), cmd.get("top_p", 0.95))

@@ -159,6 +159,17 @@ class LoadgenProc:
             raise RuntimeError(out["error"])
         return out["results"]
 
+    def open_loop(self, **kw):
+        """Open-loop arrivals (loadgen.open_loop); returns (results, elapsed_s)."""
+        import json
+
+        self.p.stdin.write(json.dumps({"op": "open", **kw}) + "\n")
+        self.p.stdin.flush()
+        out = json.loads(self.p.stdout.readline() or '{"ok": false, "error": "load generator died"}')
+        if not out["ok"]:
+            raise RuntimeError(out["error"])
+        return out["results"], out["elapsed"]
+
     def close(self):
         try:
             self.p.stdin.write('{"op": "quit"}\n')

@@ -85,3 +85,9 @@ def test_bench_gpus_flag_must_match_world():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS, cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "does not match" in r.stderr
+
+
+def test_bench_open_loop_request_rate():
+    """--request-rate: open-loop Poisson arrivals through the gateway path."""
+    out = _run([sys.executable, "bench.py"] + ARGS + ["--request-rate", "20", "--steps", "2"])
+    assert out["load"].startswith("open-loop") and out["value"] > 0 and out["p50_ttft_ms"] > 0
