@@ -118,7 +118,13 @@ __global__ __launch_bounds__(kTopT) void top_logprobs_kernel(const T* __restrict
   __shared__ unsigned int c_n;
   const int r = blockIdx.x, t = threadIdx.x;
   const int n = min(nreq[r], K);
-  if (n <= 0) return;
+  if (n <= 0) {
+    if (t < K) {
+      out_ids[(long)r * K + t] = -1;
+      out_lp[(long)r * K + t] = -INFINITY;
+    }
+    return;
+  }
   const T* row = logits + (long)r * stride;
   // 1. log-sum-exp
   float m = -INFINITY;

@@ -423,8 +423,10 @@ def test_penalty_and_top_logprobs_kernels(V, dt):
     """csrc/kernels/penalties.hip vs the torch reference (hipserve/ops/reference.py):
     slot init from prompt + generated ids, in-graph updates, penalty application
     (rows without a slot untouched) and top-n logprobs with lowest-id tie breaks."""
+    from hipserve.ops import load_library
     from hipserve.ops import reference as R
 
+    load_library()
     op = torch.ops.hipserve
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(V)
