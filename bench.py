@@ -264,7 +264,7 @@ def main():
             with open(args.out, "w") as f:
                 f.write(line + "\n")
             with open(os.path.splitext(args.out)[0] + "_gemm_tune.jsonl", "w") as f:
-                for r in engine.runner.gemm_report:
+                for r in engine.runner.gemm_report + getattr(engine.runner, "gguf_split_report", []):
                     f.write(json.dumps(r) + "\n")
     if world > 1:
         dist.barrier()

@@ -73,6 +73,19 @@ void launch_gguf_gemm(void* out, float* ws, const void* x, long x_stride, long o
                       int M, int N, int K, int splits, hipStream_t s);
 void launch_gguf_dequant(void* out, const void* q, const void* d, const void* m, int qtype,
                          long row_bytes, int N, int K, hipStream_t s);
+// gguf_mfma.hip — decode GEMM v2 over the parts of a merged projection, weights in
+// the tiled layout ([N/16][K/256][chunk]): out[:, col + n] (bf16, S == 1) or
+// ws[S, M, Ntot] fp32 partials. M <= 64, parts' rows % 16 == 0.
+struct GgufPart {
+  const void* q;
+  int qtype;
+  int rows;
+  int col;
+};
+int gguf_tiled_chunk_bytes(int qtype);
+void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
+                            const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s);
+void launch_gguf_dequant_tiled(void* out, const void* q, int qtype, int N, int K, hipStream_t s);
 
 }  // namespace hipserve
 
@@ -119,6 +132,8 @@ bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, lo
 void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
                                int M, int N, float eps, hipStream_t s);
 // qkv = bf16(sum_s ws) -> RoPE(q, k) -> q into qkv[:, :nq*D], k/v into the paged cache
+// act[M, I] = GLU of the plain [gate | up] partials ws[S, M, 2I] (decode_fused.hip)
+void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s);
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
                               const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
                               int nkv, int D, int block_size, int mode, hipStream_t s);

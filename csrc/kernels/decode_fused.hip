@@ -209,4 +209,35 @@ void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S
                                                      nkv, D, block_size);
 }
 
+// GLU over the split-K partials of a merged [gate | up] projection in the plain
+// (non-interleaved) layout — the GGUF decode GEMM's output (gguf_mfma.hip):
+// act[m, j] = act(bf16(sum_s gate)) * bf16(sum_s up), bit-identical to the reduce
+// followed by silu_and_mul / gelu_and_mul. grid (M, ceil(I / 2048)), 8 per thread.
+template <bool kGelu>
+__global__ __launch_bounds__(256) void splitk_glu_kernel(unsigned short* __restrict__ act, long act_stride,
+                                                         const float* __restrict__ ws, int S, int M, int I) {
+  const int m = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c * 8 >= I) return;
+  const long N = 2L * I, slice = (long)M * N;
+  float g[8], u[8];
+  sum8_bf16(g, ws + m * N + c * 8, slice, S);
+  sum8_bf16(u, ws + m * N + I + c * 8, slice, S);
+  u16x8 gb, ub;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gb[j] = f32_to_bf16(g[j]);
+    ub[j] = f32_to_bf16(u[j]);
+  }
+  *reinterpret_cast<u16x8*>(act + m * act_stride + c * 8) = kGelu ? gelu_mul8(gb, ub) : silu_mul8(gb, ub);
+}
+
+void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s) {
+  if (M <= 0) return;
+  const dim3 grid(M, (I / 8 + 255) / 256);
+  auto* a = static_cast<unsigned short*>(act);
+  if (gelu) splitk_glu_kernel<true><<<grid, 256, 0, s>>>(a, act_stride, ws, S, M, I);
+  else splitk_glu_kernel<false><<<grid, 256, 0, s>>>(a, act_stride, ws, S, M, I);
+}
+
 }  // namespace hipserve

@@ -1,0 +1,553 @@
+// GGUF decode GEMM v2 — dequant in registers at ~2 VALU ops per
+// weight, f16 MFMA, weights in a tiled layout built once at load.
+//
+// Why v1 (gguf.hip qgemm) ran at 0.7-2 TB/s of quantised bytes:
+//  * a 64-row workgroup re-read the whole x K-slice for 64 rows of ~4.5-bit
+//    weights (x traffic 3.6x the weight traffic at M = 64);
+//  * split-K workgroups read 144-210 B pieces of rows 2-8 KB apart: partial cache
+//    lines, fetched again by the neighbouring K slice on another XCD;
+//  * dequant cost ~4 VALU ops per weight (byte extract, int->float, FMA, ->bf16).
+// v2:
+//  * tiled layout [N/16][K/256][chunk]: the 16 rows x 256 k one wave multiplies
+//    are one contiguous chunk, lane-interleaved so every lane-specific 16-byte load
+//    is one coalesced 1 KiB wave access; a K slice of a row group is contiguous;
+//  * workgroup = 4 waves x 2 row groups = 128 weight rows sharing one x staging
+//    (f16, LDS, double-buffered), split over K to fill the chip; 4-wave steps keep
+//    occupancy granular (a 150-VGPR body still runs 12 waves per CU);
+//  * nibbles become f16 by bit assembly: (w & 0x000F000F) | 0x6400_6400 is the
+//    f16 pair (1024 + q_a, 1024 + q_b) for bytes 0 and 2 of a word (exact); one
+//    v_pk_add_f16 removes the 1024 (exact), one v_pk_fma_f16 applies the block
+//    scale and min with a single f16 rounding (11-bit mantissa: finer than the
+//    bf16 weights of v1). Q6_K ORs its two high bits into bit 4-5 first, Q8_0
+//    flips the sign bit (int8 + 128 in [0, 255]) before the OR;
+//  * the MFMA k order inside each 8-element fragment is therefore the pair order
+//    {0, 2, 1, 3, 4, 6, 5, 7}: x is converted to f16 ONCE per workgroup while
+//    staging into LDS, already in that order, so A and B agree on every k;
+//  * v_mfma_f32_16x16x32_f16 (same rate as bf16), fp32 accumulation; x is
+//    clamped to the f16 range on staging;
+//  * all parts of a merged projection are one launch (part table: format, column
+//    offset, rows; two formats per launch for the Q4_K/Q5_K + Q6_K mixes); split-K
+//    writes fp32 partials [S, M, N_total] that the decode layer's fused epilogues
+//    consume (RoPE + KV write, residual + RMSNorm, SiLU-GLU) — no reduce kernel.
+// Measured (tools/bench_gguf.py, profiles/r2_gguf_v2.md): Llama-3-8B Q4_K_M at
+// M = 1, gate|up 3.5-3.8 TB/s, lm_head (Q6_K) 4.5 TB/s, vs 1.5 / 2.9 for v1.
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+namespace {
+
+enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5 };
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr unsigned kMagic = 0x64006400u;  // f16 pair (1024, 1024)
+constexpr int kXS = 256 + 8;              // LDS row stride (f16 elements): conflict-free b128 reads
+
+HS_DEVICE h2 as_h2(unsigned u) { return __builtin_bit_cast(h2, u); }
+HS_DEVICE unsigned as_u(h2 h) { return __builtin_bit_cast(unsigned, h); }
+HS_DEVICE float h2f(unsigned short h) { return static_cast<float>(__builtin_bit_cast(_Float16, h)); }
+HS_DEVICE h2 splat(float f) {
+  const _Float16 v = static_cast<_Float16>(f);
+  return h2{v, v};
+}
+HS_DEVICE u32x4 ld16(const unsigned char* p) { return *reinterpret_cast<const u32x4*>(p); }
+
+// the 16-byte fragment of 8 f16 values from 4 packed pairs
+HS_DEVICE f16x8 frag(h2 a, h2 b, h2 c, h2 d) {
+  return __builtin_bit_cast(f16x8, u32x4{as_u(a), as_u(b), as_u(c), as_u(d)});
+}
+
+// nibbles at bit offset sh of bytes (0, 2) and (1, 3) of w -> 1024 + q pairs
+HS_DEVICE void nib_pairs(unsigned w, int sh, unsigned& p02, unsigned& p13) {
+  p02 = ((w >> sh) & 0x000F000Fu) | kMagic;
+  p13 = ((w >> (sh + 8)) & 0x000F000Fu) | kMagic;
+}
+
+struct Raw {
+  u32x4 v[5];
+  unsigned s2[2];  // Q6_K: the lane's 4 int8 sub-block scales (2 words, 2 bytes used each)
+  unsigned short h[4];
+};
+
+// Tiled weight layout (hipserve/ops/quant.py repack_tiled): a part is
+// [N/16 row groups][K/256 super-chunks][CB bytes]; one chunk = the 16 rows x 256 k a
+// wave multiplies, arranged so every lane-specific 16-byte load of the wave is one
+// fully coalesced 1 KiB access (lane = 16 g + c: row c, k quarter g):
+//   Q4_K  [16 hdr x 16][2 x 64 lanes x 16 qs]                       2304 B
+//   Q5_K  Q4_K + [16 rows x 32 qh]                                  2816 B
+//   Q6_K  [2 x 64 lanes x 16 ql][16 rows x 64 qh][16 x 16 scales][16 x 2 d]  3360 B
+//   Q8_0  [4 x 64 lanes x 16 q][16 rows x 8 d]                      4352 B
+//   Q4_0  [2 x 64 lanes x 16 q][16 rows x 8 d]                      2304 B
+//   Q4_1  Q4_0 + [16 rows x 8 m]                                    2560 B
+template <int QT>
+constexpr int chunk_bytes() {
+  return QT == Q4_K ? 2304 : QT == Q5_K ? 2816 : QT == Q6_K ? 3360 : QT == Q8_0 ? 4352 : QT == Q4_0 ? 2304 : 2560;
+}
+
+struct Part {
+  const unsigned char* q;
+  int qt;       // format of the part
+  int rows;     // N of the part (multiple of 16)
+  int col;      // first output column
+  int tile0;    // first tile index of the part in the launch
+};
+constexpr int kMaxParts = 4;
+// 4-wave workgroups of 2 row groups per wave (128 rows): occupancy then comes in
+// 4-wave steps, so a 150-VGPR body still runs 3 workgroups (12 waves) per CU
+constexpr int kWaves = 4;
+struct Parts {
+  Part p[kMaxParts];
+  int n;
+};
+
+template <int QT>
+HS_DEVICE void load_raw(const unsigned char* ch, int g, int c, int lane, Raw& r) {
+  if constexpr (QT == Q4_K || QT == Q5_K) {
+    r.v[0] = ld16(ch + 16 * c);  // d, dmin, 12 B of 6-bit scales / mins
+    r.v[1] = ld16(ch + 256 + 16 * lane);
+    r.v[2] = ld16(ch + 1280 + 16 * lane);
+    if constexpr (QT == Q5_K) {
+      r.v[3] = ld16(ch + 2304 + 32 * c);
+      r.v[4] = ld16(ch + 2320 + 32 * c);
+    }
+  } else if constexpr (QT == Q6_K) {
+    r.v[0] = ld16(ch + 16 * lane);
+    r.v[1] = ld16(ch + 1024 + 16 * lane);
+    r.v[2] = ld16(ch + 2048 + 64 * c + 32 * (g >> 1));
+    r.v[3] = ld16(ch + 2064 + 64 * c + 32 * (g >> 1));
+    const uint2 sc = *reinterpret_cast<const uint2*>(ch + 3072 + 16 * c + 8 * (g >> 1));  // scales 8h..8h+7
+    r.s2[0] = sc.x;
+    r.s2[1] = sc.y;
+    r.h[0] = *reinterpret_cast<const unsigned short*>(ch + 3328 + 2 * c);
+  } else if constexpr (QT == Q8_0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = ld16(ch + 1024 * i + 16 * lane);
+    const unsigned dd = *reinterpret_cast<const unsigned*>(ch + 4096 + 16 * c + 4 * g);
+    r.h[0] = dd & 0xFFFF;
+    r.h[1] = dd >> 16;
+  } else {  // Q4_0 / Q4_1
+    r.v[0] = ld16(ch + 16 * lane);
+    r.v[1] = ld16(ch + 1024 + 16 * lane);
+    const unsigned dd = *reinterpret_cast<const unsigned*>(ch + 2048 + 16 * c + 4 * g);
+    r.h[0] = dd & 0xFFFF;
+    r.h[1] = dd >> 16;
+    if constexpr (QT == Q4_1) {
+      const unsigned mm = *reinterpret_cast<const unsigned*>(ch + 2304 + 16 * c + 4 * g);
+      r.h[2] = mm & 0xFFFF;
+      r.h[3] = mm >> 16;
+    }
+  }
+}
+
+HS_DEVICE unsigned word(const u32x4 (&v)[2], int i) { return v[i >> 2][i & 3]; }  // i in [0, 8)
+
+// 6-bit scale / min j of a K-quant super-block from its 12 packed bytes (words
+// w1 w2 w3 = bytes 0-3, 4-7, 8-11). j is lane-dependent: bytes are picked with
+// shifts by 8 (j & 3) (every byte used sits at j, j +- 4), never by indexing a
+// register array (that becomes compare/select chains).
+HS_DEVICE void scale_min_k4(int j, unsigned w1, unsigned w2, unsigned w3, float& sc, float& mn) {
+  const int sh = 8 * (j & 3);
+  const unsigned lo = (w1 >> sh) & 0xFF, mid = (w2 >> sh) & 0xFF, hi = (w3 >> sh) & 0xFF;
+  const unsigned s_hi = (hi & 0xF) | ((lo >> 6) << 4), m_hi = (hi >> 4) | ((mid >> 6) << 4);
+  sc = (float)(j < 4 ? (lo & 63) : s_hi);
+  mn = (float)(j < 4 ? (mid & 63) : m_hi);
+}
+
+// k of element j (fragment order) of step s, lane group g: contiguous 8-runs whose
+// base matches v1's kbase; inside a run the pair order {0, 2, 1, 3, 4, 6, 5, 7}
+template <int QT>
+HS_DEVICE int kbase(int g, int s) {
+  if constexpr (QT == Q6_K) {
+    const int q = (g & 1) + 2 * (s >> 2);
+    return 128 * (g >> 1) + 32 * q + 8 * (s & 3);
+  } else {
+    return 64 * g + 32 * (s >> 2) + 8 * (s & 3);
+  }
+}
+
+// Decode step s (8 weights) of the lane's super-chunk. ints(): the 8 quantised
+// integers (minus the format's zero point) as exact f16, pair order; step(): the
+// weights in f16 (one v_pk_fma per pair with the block scale / min); scale():
+// the same scale / min in fp32 for the exact bf16 dequant of the prefill path.
+template <int QT>
+struct Dec {
+  h2 dA, cA, dB, cB;        // per-step-group scale / offset pairs (K-quants: sub-blocks; SoA: blocks)
+  float fdA, fcA, fdB, fcB;  // the same in fp32
+  float d6;                  // Q6_K super-block scale
+
+  HS_DEVICE void setup(const Raw& r, int g) {
+    fcA = fcB = 0.f;
+    if constexpr (QT == Q4_K || QT == Q5_K) {
+      const u32x4 hdr = r.v[0];
+      const float d = h2f(hdr[0] & 0xFFFF), dmin = h2f(hdr[0] >> 16);
+      float s1, m1, s2, m2;
+      scale_min_k4(2 * g, hdr[1], hdr[2], hdr[3], s1, m1);
+      scale_min_k4(2 * g + 1, hdr[1], hdr[2], hdr[3], s2, m2);
+      fdA = d * s1;
+      fcA = -dmin * m1;
+      fdB = d * s2;
+      fcB = -dmin * m2;
+    } else if constexpr (QT == Q6_K) {
+      d6 = h2f(r.h[0]);
+    } else {
+      fdA = h2f(r.h[0]);
+      fdB = h2f(r.h[1]);
+      if constexpr (QT == Q4_1) {
+        fcA = h2f(r.h[2]);
+        fcB = h2f(r.h[3]);
+      }
+    }
+    dA = splat(fdA);
+    dB = splat(fdB);
+    cA = splat(fcA);
+    cB = splat(fcB);
+  }
+
+  HS_DEVICE void scale(const Raw& r, int g, int s, float& d, float& c) const {
+    if constexpr (QT == Q6_K) {
+      // sub-block 8h + 2q + ((s & 3) >> 1), q = (g & 1) + 2 (s >> 2): byte 2 (g & 1) + ((s & 3) >> 1)
+      // of the lane's scale word (s >> 2)
+      d = d6 * (float)(signed char)((r.s2[s >> 2] >> (8 * (2 * (g & 1) + ((s & 3) >> 1)))) & 0xFF);
+      c = 0.f;
+    } else if constexpr (QT == Q4_K || QT == Q5_K || QT == Q8_0) {
+      d = s < 4 ? fdA : fdB;
+      c = s < 4 ? fcA : fcB;
+    } else {
+      d = (s >> 2) ? fdB : fdA;
+      c = (s >> 2) ? fcB : fcA;
+    }
+  }
+
+  HS_DEVICE f16x8 ints(const Raw& r, int g, int s) const {
+    unsigned p[4];
+    _Float16 z;  // 1024 + zero point
+    if constexpr (QT == Q4_K || QT == Q5_K) {
+      const u32x4 qs[2] = {r.v[1], r.v[2]};
+      const int sh = s < 4 ? 0 : 4;
+      const unsigned wa = word(qs, 2 * (s & 3)), wb = word(qs, 2 * (s & 3) + 1);
+      nib_pairs(wa, sh, p[0], p[1]);
+      nib_pairs(wb, sh, p[2], p[3]);
+      if constexpr (QT == Q5_K) {  // + 16 where the high bit of the element is set
+        const u32x4 qh[2] = {r.v[3], r.v[4]};
+        const int bit = 2 * g + (s >> 2);
+        const unsigned ha = word(qh, 2 * (s & 3)), hb = word(qh, 2 * (s & 3) + 1);
+        p[0] |= ((ha >> bit) & 0x00010001u) << 4;
+        p[1] |= ((ha >> (bit + 8)) & 0x00010001u) << 4;
+        p[2] |= ((hb >> bit) & 0x00010001u) << 4;
+        p[3] |= ((hb >> (bit + 8)) & 0x00010001u) << 4;
+      }
+      z = (_Float16)1024.f;
+    } else if constexpr (QT == Q6_K) {
+      const u32x4 ql[2] = {r.v[0], r.v[1]};
+      const u32x4 qh[2] = {r.v[2], r.v[3]};
+      const int q = (g & 1) + 2 * (s >> 2);
+      const int sh = s < 4 ? 0 : 4;
+      const unsigned la = word(ql, 2 * (s & 3)), lb = word(ql, 2 * (s & 3) + 1);
+      const unsigned ha = word(qh, 2 * (s & 3)) >> (2 * q), hb = word(qh, 2 * (s & 3) + 1) >> (2 * q);
+      nib_pairs(la, sh, p[0], p[1]);
+      nib_pairs(lb, sh, p[2], p[3]);
+      p[0] |= (ha & 0x00030003u) << 4;
+      p[1] |= ((ha >> 8) & 0x00030003u) << 4;
+      p[2] |= (hb & 0x00030003u) << 4;
+      p[3] |= ((hb >> 8) & 0x00030003u) << 4;
+      z = (_Float16)1056.f;  // q6 - 32
+    } else if constexpr (QT == Q8_0) {
+      const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+      const unsigned wa = qv[s >> 1][2 * (s & 1)] ^ 0x80808080u, wb = qv[s >> 1][2 * (s & 1) + 1] ^ 0x80808080u;
+      p[0] = (wa & 0x00FF00FFu) | kMagic;
+      p[1] = ((wa >> 8) & 0x00FF00FFu) | kMagic;
+      p[2] = (wb & 0x00FF00FFu) | kMagic;
+      p[3] = ((wb >> 8) & 0x00FF00FFu) | kMagic;
+      z = (_Float16)1152.f;  // int8 value
+    } else {  // Q4_0 / Q4_1: block (s >> 2); elements 0-15 low nibbles, 16-31 high
+      const u32x4 v[2] = {r.v[0], r.v[1]};
+      const int blk = s >> 2, e = s & 3;
+      const int sh = e < 2 ? 0 : 4;
+      const unsigned wa = word(v, 4 * blk + 2 * (e & 1)), wb = word(v, 4 * blk + 2 * (e & 1) + 1);
+      nib_pairs(wa, sh, p[0], p[1]);
+      nib_pairs(wb, sh, p[2], p[3]);
+      z = (_Float16)(QT == Q4_0 ? 1032.f : 1024.f);  // q - 8 / q
+    }
+    const h2 off = h2{-z, -z};
+    return frag(as_h2(p[0]) + off, as_h2(p[1]) + off, as_h2(p[2]) + off, as_h2(p[3]) + off);
+  }
+
+  HS_DEVICE f16x8 step(const Raw& r, int g, int s) const {
+    const f16x8 q = ints(r, g, s);
+    h2 dd, cc;
+    if constexpr (QT == Q6_K) {
+      float d, c;
+      scale(r, g, s, d, c);
+      dd = splat(d);
+      cc = h2{(_Float16)0.f, (_Float16)0.f};
+    } else if constexpr (QT == Q4_0 || QT == Q4_1) {
+      dd = (s >> 2) ? dB : dA;
+      cc = (s >> 2) ? cB : cA;
+    } else {
+      dd = s < 4 ? dA : dB;
+      cc = s < 4 ? cA : cB;
+    }
+    const u32x4 qu = __builtin_bit_cast(u32x4, q);
+    if constexpr (QT == Q6_K || QT == Q8_0 || QT == Q4_0)  // no min term
+      return frag(as_h2(qu[0]) * dd, as_h2(qu[1]) * dd, as_h2(qu[2]) * dd, as_h2(qu[3]) * dd);
+    else
+      return frag(as_h2(qu[0]) * dd + cc, as_h2(qu[1]) * dd + cc, as_h2(qu[2]) * dd + cc, as_h2(qu[3]) * dd + cc);
+  }
+};
+
+HS_DEVICE _Float16 to_f16_sat(unsigned short b) {
+  const float f = fminf(fmaxf(bf16_to_f32(b), -65504.f), 65504.f);
+  return static_cast<_Float16>(f);
+}
+
+// One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
+// x staging. Body per format; the kernel picks it per part (two formats per launch).
+template <int QT, int MT, int RT, int NWAVES>
+HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][16 * MT * kXS], unsigned short* __restrict__ out, long out_stride,
+                           float* __restrict__ ws, const unsigned short* __restrict__ x, long x_stride,
+                           const Part& P, int M, int Ntot, int K, int sb_per_split) {
+  constexpr int XR = 16 * MT;           // staged x rows (M padded)
+  constexpr int NT = 64 * NWAVES;
+  constexpr int CB = chunk_bytes<QT>();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int gi0 = (blockIdx.x - P.tile0) * (NWAVES * RT) + wave * RT;  // first row group of this wave
+  const int ngroups = P.rows >> 4;
+  const int nsb = K >> 8;
+  const int sb0 = blockIdx.y * sb_per_split, sb1 = min(nsb, sb0 + sb_per_split);
+  const unsigned char* base[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) base[r] = P.q + (long)min(gi0 + r, ngroups - 1) * nsb * CB;
+
+  // x staging: 32 fragments (g, s) of 8 per row and super-chunk; thread -> (row, fragment)
+  constexpr int XP = (XR * 32 + NT - 1) / NT;
+  u16x8 xv[XP];
+  auto load_x = [&](int sb) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int idx = min(i * NT + tid, XR * 32 - 1), row = idx >> 5, fr = idx & 31;
+      const int kb = kbase<QT>(fr >> 3, fr & 7);
+      // rows >= M are clamped, never stored
+      xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + sb * 256 + kb);
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
+      if (idx >= XR * 32) break;
+      const u16x8 b = xv[i];
+      f16x8 h;
+      h[0] = to_f16_sat(b[0]); h[1] = to_f16_sat(b[2]); h[2] = to_f16_sat(b[1]); h[3] = to_f16_sat(b[3]);
+      h[4] = to_f16_sat(b[4]); h[5] = to_f16_sat(b[6]); h[6] = to_f16_sat(b[5]); h[7] = to_f16_sat(b[7]);
+      *reinterpret_cast<f16x8*>(&xs[buf][row * kXS + fr * 8]) = h;
+    }
+  };
+
+  f32x4 acc[RT][MT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Raw raw[RT];
+  if (sb0 < sb1) {
+    load_x(sb0);
+#pragma unroll
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sb0 * CB, g, c, lane, raw[r]);
+    store_x(0);
+  }
+  __syncthreads();
+  for (int sb = sb0; sb < sb1; ++sb) {
+    const int buf = (sb - sb0) & 1;
+    Raw cur[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) cur[r] = raw[r];
+    if (sb + 1 < sb1) {  // next super-chunk in flight while this one is decoded and multiplied
+      load_x(sb + 1);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)(sb + 1) * CB, g, c, lane, raw[r]);
+    }
+    const _Float16* xb = &xs[buf][c * kXS + 64 * g];  // fragment (g, s) of row 16t + c at + 8s
+    Dec<QT> dec[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      f16x8 a[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {  // one LDS read of x per (s, t), shared by the RT row groups
+        const f16x8 b = *reinterpret_cast<const f16x8*>(xb + 16 * t * kXS + 8 * s);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b, acc[r][t], 0, 0, 0);
+      }
+    }
+    if (sb + 1 < sb1) store_x(buf ^ 1);
+    __syncthreads();
+  }
+  // C: col m = 16t + c, rows n = 16 gi + 4g + j
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    if (gi0 + r >= ngroups) continue;
+    const int col = P.col + 16 * (gi0 + r) + 4 * g;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = 16 * t + c;
+      if (m >= M) continue;
+      if (ws != nullptr) {
+        *reinterpret_cast<f32x4*>(ws + ((long)blockIdx.y * M + m) * Ntot + col) = acc[r][t];
+      } else {
+        uint2 v;
+        v.x = pack_bf16x2(acc[r][t][0], acc[r][t][1]);
+        v.y = pack_bf16x2(acc[r][t][2], acc[r][t][3]);
+        *reinterpret_cast<uint2*>(out + (long)m * out_stride + col) = v;
+      }
+    }
+  }
+}
+
+template <int QA, int QB, int MT, int RT, int NWAVES>
+__global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __restrict__ out, long out_stride,
+                                                            float* __restrict__ ws, const unsigned short* __restrict__ x,
+                                                            long x_stride, Parts parts, int M, int Ntot, int K,
+                                                            int sb_per_split) {
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2][16 * MT * kXS];
+  const int tile = blockIdx.x;
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxParts; ++i)
+    if (i < parts.n && tile >= parts.p[i].tile0) pi = i;
+  const Part& P = parts.p[pi];
+  if (QA == QB || P.qt == QA)
+    qgemm2_body<QA, MT, RT, NWAVES>(xs, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+  else
+    qgemm2_body<QB, MT, RT, NWAVES>(xs, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+}
+
+template <int QA, int QB>
+void launch_t(void* out, long out_stride, float* ws, const void* x, long x_stride, const Parts& P, int tiles,
+              int M, int Ntot, int K, int S, hipStream_t s) {
+  constexpr int RT = 2, NW = kWaves;
+  const int nsb = K / 256;
+  const int per = (nsb + S - 1) / S;
+  const dim3 grid(tiles, (nsb + per - 1) / per), block(64 * NW);
+  auto* o = static_cast<unsigned short*>(out);
+  auto* xi = static_cast<const unsigned short*>(x);
+  if (M <= 16)
+    qgemm2_kernel<QA, QB, 1, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+  else if (M <= 32)
+    qgemm2_kernel<QA, QB, 2, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+  else
+    qgemm2_kernel<QA, QB, 4, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+}
+
+// ---------------------------------------------------------------- tiled -> bf16
+// Prefill: one wave per (row group, super-chunk) chunk, out[N, K] row-major bf16.
+template <int QT>
+__global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __restrict__ out,
+                                                            const unsigned char* __restrict__ q, int ngroups, int K) {
+  constexpr int CB = chunk_bytes<QT>();
+  const int nsb = K >> 8;
+  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= (long)ngroups * nsb) return;
+  const int gi = (int)(item / nsb), sb = (int)(item % nsb);
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  Raw r;
+  load_raw<QT>(q + item * CB, g, c, lane, r);
+  Dec<QT> dec;
+  dec.setup(r, g);
+  unsigned short* row = out + (long)(16 * gi + c) * K + sb * 256;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const f16x8 q = dec.ints(r, g, s);  // exact integers, pair order {0, 2, 1, 3, 4, 6, 5, 7}
+    float d, m;
+    dec.scale(r, g, s, d, m);           // fp32 scale: one rounding, to bf16, like the v1 dequant
+    constexpr int src[8] = {0, 2, 1, 3, 4, 6, 5, 7};
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16((float)q[src[j]] * d + m);
+    *reinterpret_cast<u16x8*>(row + kbase<QT>(g, s)) = o;
+  }
+}
+
+}  // namespace
+
+int gguf_tiled_chunk_bytes(int qtype) {
+  switch (qtype) {
+    case Q4_0: return chunk_bytes<Q4_0>();
+    case Q4_1: return chunk_bytes<Q4_1>();
+    case Q8_0: return chunk_bytes<Q8_0>();
+    case Q4_K: return chunk_bytes<Q4_K>();
+    case Q5_K: return chunk_bytes<Q5_K>();
+    case Q6_K: return chunk_bytes<Q6_K>();
+  }
+  return 0;
+}
+
+// Parts in the tiled layout. ws != nullptr: fp32 partials [S, M, Ntot]; else bf16
+// out (S must be 1). Parts of one format, or of the pairs Q4_K+Q6_K / Q5_K+Q6_K
+// (the K-quant mixes), share one launch; any other mix launches per format.
+void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
+                            const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s) {
+  constexpr int ROWS = 16 * 2 * kWaves;
+  int fmts[kMaxParts], nf = 0;
+  for (int i = 0; i < nparts; ++i) {
+    bool seen = false;
+    for (int j = 0; j < nf; ++j) seen |= fmts[j] == parts[i].qtype;
+    if (!seen) fmts[nf++] = parts[i].qtype;
+  }
+  auto table = [&](int fa, int fb, int& tiles) {
+    Parts P{};
+    tiles = 0;
+    for (int i = 0; i < nparts; ++i) {
+      if (parts[i].qtype != fa && parts[i].qtype != fb) continue;
+      P.p[P.n++] = Part{static_cast<const unsigned char*>(parts[i].q), parts[i].qtype, parts[i].rows, parts[i].col,
+                        tiles};
+      tiles += (parts[i].rows + ROWS - 1) / ROWS;
+    }
+    return P;
+  };
+  int tiles = 0;
+  if (nf == 2) {
+    const int a = fmts[0] < fmts[1] ? fmts[0] : fmts[1], b = fmts[0] < fmts[1] ? fmts[1] : fmts[0];
+    if ((a == Q4_K || a == Q5_K) && b == Q6_K) {
+      const Parts P = table(a, b, tiles);
+      if (a == Q4_K) launch_t<Q4_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s);
+      else launch_t<Q5_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s);
+      return;
+    }
+  }
+  for (int f = 0; f < nf; ++f) {
+    const Parts P = table(fmts[f], fmts[f], tiles);
+    switch (fmts[f]) {
+      case Q4_0: launch_t<Q4_0, Q4_0>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case Q4_1: launch_t<Q4_1, Q4_1>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case Q8_0: launch_t<Q8_0, Q8_0>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case Q4_K: launch_t<Q4_K, Q4_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case Q5_K: launch_t<Q5_K, Q5_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case Q6_K: launch_t<Q6_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+    }
+  }
+}
+
+void launch_gguf_dequant_tiled(void* out, const void* q, int qtype, int N, int K, hipStream_t s) {
+  const long items = (long)(N / 16) * (K / 256);
+  const dim3 grid((unsigned)((items + 3) / 4)), block(256);
+  auto* o = static_cast<unsigned short*>(out);
+  auto* qq = static_cast<const unsigned char*>(q);
+  switch (qtype) {
+    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+  }
+}
+
+}  // namespace hipserve

@@ -195,6 +195,59 @@ void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const 
                              splits, cur_stream());
 }
 
+// parts in the tiled layout (one uint8 tensor [N/16, K/256, chunk] each), their
+// formats / rows / output columns. ws.numel() > 0: fp32 partials [S_actual, M, Ntot]
+// (returned S_actual = ceil(nsb / ceil(nsb / S))); else bf16 out [M, >= Ntot], S == 1.
+int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const std::vector<at::Tensor>& qs,
+                        const std::vector<int64_t>& qtypes, const std::vector<int64_t>& rows,
+                        const std::vector<int64_t>& cols, int64_t Ntot, int64_t K, int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x);
+  const int np = qs.size();
+  TORCH_CHECK(np >= 1 && np <= 4 && (int)qtypes.size() == np && (int)rows.size() == np && (int)cols.size() == np,
+              "gguf_gemm_parts: 1-4 parts");
+  TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && splits >= 1);
+  const int M = x.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64, "gguf_gemm_parts handles 1 <= M <= 64");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
+  const int nsb = K / 256;
+  const int per = (nsb + splits - 1) / splits;
+  const int S = (nsb + per - 1) / per;
+  hipserve::GgufPart P[4];
+  for (int i = 0; i < np; ++i) {
+    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 5, "gguf_gemm_parts: kernel qtype 0-5");
+    TORCH_CHECK(qs[i].scalar_type() == at::kByte && qs[i].is_contiguous() && qs[i].device() == x.device());
+    TORCH_CHECK(cols[i] % 4 == 0 && rows[i] % 16 == 0 && rows[i] > 0 && cols[i] + rows[i] <= Ntot,
+                "parts: 16-row multiples at 4-aligned columns inside Ntot");
+    TORCH_CHECK(qs[i].numel() == rows[i] / 16 * nsb * hipserve::gguf_tiled_chunk_bytes(qtypes[i]),
+                "part q is not a tiled [N/16, K/256, chunk] tensor of its format");
+    P[i] = hipserve::GgufPart{qs[i].data_ptr(), (int)qtypes[i], (int)rows[i], (int)cols[i]};
+  }
+  float* wp = nullptr;
+  if (ws.numel() > 0) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= (long)S * M * Ntot,
+                "gguf_gemm_parts: ws must hold S * M * Ntot fp32");
+    TORCH_CHECK(ws.device() == x.device());
+    wp = ws.data_ptr<float>();
+  } else {
+    TORCH_CHECK(S == 1, "gguf_gemm_parts: split-K needs a partial workspace");
+    CHECK_BF16(out); CHECK_ROWMAJOR(out);
+    TORCH_CHECK(out.size(0) == M && out.size(1) >= Ntot && out.stride(0) % 4 == 0 && out.device() == x.device());
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_gguf_gemm_parts(wp ? nullptr : out.data_ptr(), wp ? 0 : out.stride(0), wp, x.data_ptr(),
+                                   x.stride(0), P, np, M, Ntot, K, splits, cur_stream());
+  return S;
+}
+
+void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, int64_t qtype, int64_t N, int64_t K) {
+  CHECK_DEV(q); CHECK_BF16(out);
+  TORCH_CHECK(out.is_contiguous() && out.numel() >= N * K && N % 16 == 0 && K % 256 == 0);
+  TORCH_CHECK(qtype >= 0 && qtype <= 5 && q.scalar_type() == at::kByte && q.is_contiguous());
+  TORCH_CHECK(q.numel() == N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype), "not a tiled tensor");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), qtype, N, K, cur_stream());
+}
+
 void gguf_dequant(at::Tensor& out, const at::Tensor& q, const at::Tensor& d, const at::Tensor& mn,
                   int64_t qtype, int64_t row_bytes, int64_t N, int64_t K) {
   CHECK_DEV(q); CHECK_BF16(out); TORCH_CHECK(out.is_contiguous() && out.numel() >= N * K);
@@ -523,6 +576,16 @@ void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, co
                                      head_dim, k_cache.size(2), mode, cur_stream());
 }
 
+void splitk_glu(at::Tensor& act, const at::Tensor& ws, int64_t splits, bool gelu) {
+  CHECK_DEV(act); CHECK_BF16(act); CHECK_ROWMAJOR(act);
+  const int M = act.size(0), I = act.size(1);
+  TORCH_CHECK(I % 8 == 0 && act.stride(0) % 8 == 0, "splitk_glu: I % 8 == 0");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * 2L * I);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(act.device());
+  hipserve::launch_splitk_glu(act.data_ptr(), act.stride(0), ws.data_ptr<float>(), splits, M, I, gelu,
+                              cur_stream());
+}
+
 void pack_decode_weight(at::Tensor& out, const at::Tensor& w, bool glu) {
   CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_BF16(out); CHECK_CONTIG(out);
   TORCH_CHECK(w.dim() == 2 && w.size(1) % 256 == 0, "pack_decode_weight: w [N, K], K % 256 == 0");
@@ -646,6 +709,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
   // custom all-reduce control ops carry an opaque state handle: catch-all kernels
+  m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits) -> int", &gguf_gemm_parts);
+  m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
   m.def("car_create(int rank, int world, int max_bytes) -> int", &car_create);
   m.def("car_handle(int state) -> Tensor", &car_handle);
   m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);
@@ -663,6 +728,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
+  m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("penalty_apply(Tensor(a!) logits, Tensor slot, Tensor pres, Tensor freq, Tensor rep, Tensor counts, Tensor seen) -> ()");
@@ -695,6 +761,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm_glu", &decode_gemm_glu);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.impl("splitk_rope_cache", &splitk_rope_cache);
+  m.impl("splitk_glu", &splitk_glu);
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);

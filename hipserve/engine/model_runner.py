@@ -111,6 +111,11 @@ class ModelRunner:
             self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms, fused=fused)
             if ecfg.extra.get("packed_decode", True):
                 self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
+            qws = self.model.quant_weights() if hasattr(self.model, "quant_weights") else []
+            if qws:  # GGUF: split-K of the dequant-MFMA decode GEMM per shape and batch
+                from ..ops import quant as Q
+
+                self.gguf_split_report = Q.tune_splits(qws, self.device, [m for m in Q.M_BUCKETS if m <= 64])
             torch.cuda.empty_cache()
         # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
         # budget (measured no faster than the heuristic on sustained prefill chains,

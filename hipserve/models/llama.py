@@ -466,9 +466,9 @@ class LlamaModel:
         L = len(self.layers)
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
-            fc = gemm.fused_choice(T, lw.wqkv)
-            if fc is not None:
-                ws, S = gemm.gemm_partial(xn, lw.wqkv, fc)
+            pt = self._partial(xn, lw.wqkv)
+            if pt is not None:
+                ws, S = pt
                 qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)
                 op.splitk_rope_cache(qkv, ws, S, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
                                      nq, nkv, D, cfg.rope_mode)
@@ -478,27 +478,47 @@ class LlamaModel:
                                cfg.rope_mode)
             ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
                              nq, nkv, part, self.scale)
-            fc = gemm.fused_choice(T, lw.wo)
-            if fc is not None:
-                ws, S = gemm.gemm_partial(attn, lw.wo, fc)
-                self.add_rmsnorm(xn, residual, ws, S, lw.ln2)
+            pt = self._partial(attn, lw.wo)
+            if pt is not None:
+                self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2)
             else:
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(attn, lw.wo), 1, lw.ln2)
             gc = gemm.glu_choice(T, lw.wgu)
+            pt = None if gc is not None or isinstance(lw.wgu, torch.Tensor) else self._partial(xn, lw.wgu)
             if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
+            elif pt is not None:   # quantised gate|up: GLU over the plain-layout partials
+                act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
+                op.splitk_glu(act, pt[0], pt[1], False)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 ops.silu_and_mul(act, gu)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
-            fc = gemm.fused_choice(T, lw.wd)
-            if fc is not None:
-                ws, S = gemm.gemm_partial(act, lw.wd, fc)
-                self.add_rmsnorm(xn, residual, ws, S, nxt)
+            pt = self._partial(act, lw.wd)
+            if pt is not None:
+                self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt)
             else:
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(act, lw.wd), 1, nxt)
         return xn
+
+    def quant_weights(self) -> list:
+        """Every GGUF-quantised projection (QuantWeight), lm_head included."""
+        from ..ops import quant as Q
+        ws = [self.lm_head] + [getattr(lw, n) for lw in self.layers for n in ("wqkv", "wo", "wgu", "wd")]
+        return [w for w in ws if isinstance(w, Q.QuantWeight)]
+
+    def _partial(self, x: torch.Tensor, w):
+        """(fp32 split-K partials [S, M, N], S) of ``x @ w.T`` for a fused decode
+        epilogue: the tuned bf16 decode GEMM, or the GGUF MFMA GEMM for a
+        ``QuantWeight``; None when the projection runs unfused (hipBLASLt choice)."""
+        if isinstance(w, torch.Tensor):
+            fc = gemm.fused_choice(x.shape[0], w)
+            return gemm.gemm_partial(x, w, fc) if fc is not None else None
+        from ..ops import quant as Q
+        if getattr(w, "v2", False) and x.shape[0] <= Q.MAX_FUSED_M and x.is_cuda:
+            return Q.quant_partial(x, w)
+        return None
 
     def _decode_split(self, Td: int, meta: AttnMeta):
         """Context partition size for the decode attention: with >= 512 (sequence,

@@ -7,8 +7,12 @@ structure-of-arrays) and keeps merged projections (q|k|v, gate|up) as parts that
 may use different formats (Q4_K_M puts attn_v/ffn_down in Q6_K).
 
 ``quant_linear(x, w)``: decode batches (M <= 64) run the fused dequant-in-register
-MFMA GEMM; larger M (prefill) dequantises one part at a time into a reusable bf16
-scratch and runs hipBLASLt.
+f16-MFMA GEMM of ``csrc/kernels/gguf_mfma.hip`` — ONE launch per format over all
+parts of a merged projection (256 weight rows per workgroup, split-K for
+occupancy); ``quant_partial`` hands its fp32 split-K partials to the fused decode
+epilogues (RoPE + KV write, residual + RMSNorm, GLU). Larger M (prefill)
+dequantises every part into one contiguous bf16 scratch and runs ONE hipBLASLt
+GEMM.
 """
 from __future__ import annotations
 
@@ -50,11 +54,73 @@ def repack(raw: np.ndarray, qtype: int, N: int, K: int):
     raise NotImplementedError(G.TYPE_NAMES.get(qtype, qtype))
 
 
+CHUNK_BYTES = {G.Q4_K: 2304, G.Q5_K: 2816, G.Q6_K: 3360, G.Q8_0: 4352, G.Q4_0: 2304, G.Q4_1: 2560}
+
+
+def _lanes(a: np.ndarray, n_ld: int) -> np.ndarray:
+    """[R, nsb, 16 rows, 4 g, n_ld, 16 B] -> [R, nsb, n_ld * 64 lanes * 16 B]: load j of
+    lane 16 g + c at j * 1024 + 16 * lane (one coalesced 1 KiB access per load)."""
+    R, nsb = a.shape[:2]
+    return a.transpose(0, 1, 4, 3, 2, 5).reshape(R, nsb, n_ld * 1024)
+
+
+def repack_tiled(raw: np.ndarray, qtype: int, N: int, K: int) -> np.ndarray:
+    """GGUF raw bytes of an [N, K] matrix (N % 16 == 0, K % 256 == 0) -> the v2
+    decode kernel's tiled layout uint8 [N/16, K/256, chunk] (csrc/kernels/gguf_mfma.hip):
+    each chunk holds the 16 rows x 256 k one wave multiplies, lane-interleaved."""
+    be, bb = G.BLOCK[qtype]
+    R, nsb = N // 16, K // 256
+    per = 256 // be                      # ggml blocks per 256-k super-chunk
+    b = np.asarray(raw, np.uint8).reshape(R, 16, nsb, per * bb).transpose(0, 2, 1, 3)  # [R, nsb, 16, bytes]
+    if qtype in (G.Q4_K, G.Q5_K):
+        qo = 16 if qtype == G.Q4_K else 48
+        parts = [b[..., 0:16].reshape(R, nsb, 256),
+                 _lanes(b[..., qo:qo + 128].reshape(R, nsb, 16, 4, 2, 16), 2)]
+        if qtype == G.Q5_K:
+            parts.append(b[..., 16:48].reshape(R, nsb, 512))
+    elif qtype == G.Q6_K:
+        parts = [_lanes(b[..., 0:128].reshape(R, nsb, 16, 4, 2, 16), 2),
+                 b[..., 128:192].reshape(R, nsb, 1024), b[..., 192:208].reshape(R, nsb, 256),
+                 b[..., 208:210].reshape(R, nsb, 32)]
+    else:
+        blk = b.reshape(R, nsb, 16, per, bb)
+        if qtype == G.Q8_0:
+            q = blk[..., 2:34].reshape(R, nsb, 16, 4, 4, 16)       # lane g: bytes 64 g + 16 i
+            parts = [_lanes(q, 4), blk[..., 0:2].reshape(R, nsb, 256)]
+        else:
+            qo = 2 if qtype == G.Q4_0 else 4
+            q = blk[..., qo:qo + 16].reshape(R, nsb, 16, 4, 2, 16)  # lane g: blocks 2g, 2g+1
+            parts = [_lanes(q, 2), blk[..., 0:2].reshape(R, nsb, 256)]
+            if qtype == G.Q4_1:
+                parts.append(blk[..., 2:4].reshape(R, nsb, 256))
+    out = np.concatenate(parts, axis=2)
+    assert out.shape[2] == CHUNK_BYTES[qtype]
+    return np.ascontiguousarray(out)
+
+
+def tileable(N: int, K: int) -> bool:
+    return N % 16 == 0 and K % 256 == 0
+
+
 class QuantPart:
-    def __init__(self, qtype, N, K, q, d, m, row_bytes):
+    """One GGUF matrix on the device: ``tiled`` parts (N % 16 == 0) hold the v2
+    layout in ``q`` [N/16, K/256, chunk]; others the v1 row layout + SoA scales."""
+
+    def __init__(self, qtype, N, K, q, d, m, row_bytes, tiled=False):
         self.qtype, self.N, self.K = qtype, N, K
         self.kqt = KERNEL_QT[qtype]
         self.q, self.d, self.m, self.row_bytes = q, d, m, row_bytes
+        self.tiled = tiled
+
+    @classmethod
+    def build(cls, raw, qtype: int, N: int, K: int, device):
+        def to(a, dt):
+            return torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)
+        if tileable(N, K):
+            e = torch.empty(0, dtype=torch.int16, device=device)
+            return cls(qtype, N, K, to(repack_tiled(raw, qtype, N, K), torch.uint8), e, e, 0, tiled=True)
+        q, d, m, rb = repack(raw, qtype, N, K)
+        return cls(qtype, N, K, to(q, torch.uint8), to(d, torch.int16), to(m, torch.int16), rb)
 
     @property
     def nbytes(self):
@@ -67,6 +133,37 @@ class QuantWeight:
         self.N = sum(p.N for p in parts)
         self.K = parts[0].K
         assert all(p.K == self.K for p in parts)
+        self._gkey = None
+
+    @property
+    def groups(self):
+        """One decode-GEMM launch per format: [(kernel qtype, parts, output column of
+        each part)] (recomputed if ``parts`` is edited)."""
+        key = tuple(map(id, self.parts))
+        if key != self._gkey:
+            groups: dict[int, tuple[list, list]] = {}
+            off = 0
+            for p in self.parts:
+                ps, cols = groups.setdefault(p.kqt, ([], []))
+                ps.append(p)
+                cols.append(off)
+                off += p.N
+            self._groups = [(kqt, ps, cols) for kqt, (ps, cols) in groups.items()]
+            self._v2 = all(p.tiled for p in self.parts)
+            cols = np.cumsum([0] + [p.N for p in self.parts])[:-1].tolist()
+            self.v2_args = ([p.q for p in self.parts], [p.kqt for p in self.parts], [p.N for p in self.parts], cols)
+            self._gkey = key
+        return self._groups
+
+    @property
+    def v2(self) -> bool:
+        """The v2 MFMA kernel applies (every part tiled), unless disabled."""
+        self.groups
+        return self._v2 and not getattr(self, "_v2_off", False)
+
+    @v2.setter
+    def v2(self, on: bool):
+        self._v2_off = not on
 
     @property
     def shape(self):
@@ -89,21 +186,13 @@ class QuantWeight:
             if not cls.supported(t.type, K):
                 return torch.cat([torch.from_numpy(gf.tensor_f32(x)).to(device, torch.bfloat16)
                                   for x in names], 0)
-            q, d, m, rb = repack(gf.raw(n), t.type, N, K)
-            to = lambda a, dt: torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)  # noqa: E731
-            parts.append(QuantPart(t.type, N, K, to(q, torch.uint8), to(d, torch.int16),
-                                   to(m, torch.int16), rb))
+            parts.append(QuantPart.build(gf.raw(n), t.type, N, K, device))
         return cls(parts)
 
     @classmethod
     def from_raw(cls, raws: list, device):
         """[(qtype, N, K, raw ggml bytes)] -> QuantWeight on ``device``."""
-        parts = []
-        for qtype, N, K, raw in raws:
-            q, d, m, rb = repack(raw, qtype, N, K)
-            to = lambda a, dt: torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)  # noqa: E731
-            parts.append(QuantPart(qtype, N, K, to(q, torch.uint8), to(d, torch.int16), to(m, torch.int16), rb))
-        return cls(parts)
+        return cls([QuantPart.build(raw, qtype, N, K, device) for qtype, N, K, raw in raws])
 
     @classmethod
     def from_float(cls, w: np.ndarray | list, qtype: int, device):
@@ -113,9 +202,7 @@ class QuantWeight:
         for mat in mats:
             mat = np.asarray(mat, np.float32)
             N, K = mat.shape
-            q, d, m, rb = repack(G.quantize(mat, qtype), qtype, N, K)
-            to = lambda a, dt: torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)  # noqa: E731
-            parts.append(QuantPart(qtype, N, K, to(q, torch.uint8), to(d, torch.int16), to(m, torch.int16), rb))
+            parts.append(QuantPart.build(G.quantize(mat, qtype), qtype, N, K, device))
         return cls(parts)
 
 
@@ -157,20 +244,149 @@ def _dequant_scratch(device, numel):
     return buf
 
 
+def _dequant_into(buf: torch.Tensor, p: QuantPart):
+    if p.tiled:
+        torch.ops.hipserve.gguf_dequant_tiled(buf, p.q, p.kqt, p.N, p.K)
+    else:
+        torch.ops.hipserve.gguf_dequant(buf, p.q, p.d, p.m, p.kqt, p.row_bytes, p.N, p.K)
+
+
 def dequantize(w: QuantWeight) -> torch.Tensor:
-    outs = []
+    out = torch.empty(w.N, w.K, dtype=torch.bfloat16, device=w.parts[0].q.device)
+    off = 0
     for p in w.parts:
-        o = torch.empty(p.N, p.K, dtype=torch.bfloat16, device=p.q.device)
-        torch.ops.hipserve.gguf_dequant(o, p.q, p.d, p.m, p.kqt, p.row_bytes, p.N, p.K)
-        outs.append(o)
-    return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+        _dequant_into(out[off:off + p.N], p)
+        off += p.N
+    return out
 
 
 def _splits(N: int, K: int) -> int:
-    """K slices for the decode dequant-GEMM: ~512 (64-row tile, K slice) workgroups."""
+    """K slices for the v1 decode dequant-GEMM: ~512 (64-row tile, K slice) workgroups."""
     wgs = (N + 63) // 64
     nsb = K // 256
     return max(1, min(nsb, -(-512 // wgs)))
+
+
+ROWS_PER_WG = 128      # gguf_mfma.hip: 4 waves x 2 row groups of 16
+TARGET_WGS = 1024      # ~4 four-wave workgroups per CU
+
+
+def _actual_splits(nsb: int, S: int) -> int:
+    per = -(-nsb // S)
+    return -(-nsb // per)
+
+
+# (weight signature, M bucket) -> S, measured by tune_splits at engine start
+SPLIT_TABLE: dict = {}
+M_BUCKETS = (1, 8, 16, 32, 48, 64)
+PARTIAL_READ_BPS = 5e12   # the fused epilogue re-reads the fp32 partials at ~HBM rate
+
+
+def _sig(w: QuantWeight):
+    return (w.K, tuple((p.kqt, p.N) for p in w.parts))
+
+
+def _bucket(M: int) -> int:
+    for b in M_BUCKETS:
+        if M <= b:
+            return b
+    return M_BUCKETS[-1]
+
+
+def v2_splits(w: QuantWeight, M: int) -> int:
+    """K slices for the v2 kernel: the tuned choice for (weight shape, M bucket) if
+    any, else enough (row tile, K slice) workgroups to fill the chip, capped so the
+    fp32 partials (S*M*N*4 B) stay below the weight bytes."""
+    S = SPLIT_TABLE.get((_sig(w), _bucket(M)))
+    if S is not None:
+        return S
+    tiles = sum(-(-p.N // ROWS_PER_WG) for _, ps, _ in w.groups for p in ps)
+    nsb = w.K // 256
+    if tiles >= 512:
+        return 1
+    S = min(nsb, -(-TARGET_WGS // tiles))
+    cap = max(1, w.nbytes // max(1, 4 * M * w.N))
+    return _actual_splits(nsb, max(1, min(S, cap)))
+
+
+_EMPTY: dict = {}
+
+
+def _empty(device, dtype):
+    key = (device, dtype)
+    t = _EMPTY.get(key)
+    if t is None:
+        t = _EMPTY[key] = torch.empty(0, dtype=dtype, device=device)
+    return t
+
+
+def _launch_v2(out, ws, x, w: QuantWeight, S: int):
+    a = w.v2_args
+    torch.ops.hipserve.gguf_gemm_parts(out, ws, x, a[0], a[1], a[2], a[3], w.N, w.K, S)
+
+
+def _graph_time_us(fn, reps: int = 10, rounds: int = 3) -> float:
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    best = float("inf")
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        best = min(best, 1000 * e0.elapsed_time(e1) / reps)
+    del g
+    return best
+
+
+def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) -> list:
+    """Measure the v2 decode GEMM per distinct QuantWeight shape and M bucket for
+    S in {1, 2, 4, ...} and keep the S minimising kernel time + the epilogue's
+    re-read of the partials (S*M*N*4 B at PARTIAL_READ_BPS). Timed inside a
+    hipGraph (the decode step's launch mode). Returns report rows."""
+    seen, report = {}, []
+    for w in weights:
+        if isinstance(w, QuantWeight) and w.v2:
+            seen.setdefault(_sig(w), w)
+    nbuf = max((4 * w.N * max(ms) * 32 for w in seen.values()), default=0)
+    ws = torch.empty(min(nbuf, max_ws_bytes) // 4, dtype=torch.float32, device=device)
+    empty = _empty(device, torch.bfloat16)
+    for sig, w in seen.items():
+        nsb = w.K // 256
+        for M in ms:
+            x = torch.randn(M, w.K, device=device, dtype=torch.bfloat16)
+            cands = sorted({_actual_splits(nsb, s) for s in (1, 2, 4, 8, 16, 32, 64) if s <= nsb})
+            cost = {}
+            for S in cands:
+                if S * M * w.N > ws.numel():
+                    continue
+                t = _graph_time_us(lambda S=S: _launch_v2(empty, ws, x, w, S))
+                cost[S] = t + 1e6 * S * M * w.N * 4 / PARTIAL_READ_BPS
+            best = min(cost, key=cost.get)
+            SPLIT_TABLE[(sig, _bucket(M))] = best
+            report.append({"K": w.K, "N": w.N, "M": M, "S": best,
+                           "us": {k: round(v, 2) for k, v in sorted(cost.items())}})
+    del ws
+    return report
+
+
+def quant_partial(x: torch.Tensor, w: QuantWeight):
+    """Decode GEMM writing fp32 split-K partials ws[S, M, N] for a fused epilogue
+    (splitk_rope_cache / splitk_add_rmsnorm / splitk_glu); returns (ws, S)."""
+    M = x.shape[0]
+    S = v2_splits(w, M)
+    ws = torch.empty(S * M * w.N, dtype=torch.float32, device=x.device)
+    _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S)
+    return ws, S
 
 
 def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
@@ -178,9 +394,23 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
     out = torch.empty(M, w.N, dtype=torch.bfloat16, device=x.device)
     if M == 0:
         return out
-    if M <= MAX_FUSED_M:
+    if M <= MAX_FUSED_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+        if w.v2 and x.is_cuda:
+            S = v2_splits(w, M)
+            if S == 1:
+                _launch_v2(out, _empty(x.device, torch.float32), x, w, 1)
+                return out
+            ws = torch.empty(S, M, w.N, dtype=torch.float32, device=x.device)
+            _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S)
+            return ws.sum(0).to(torch.bfloat16)
         off = 0
-        for p in w.parts:
+        for p in w.parts:  # v1: row-layout parts only
+            if p.tiled:
+                buf = _dequant_scratch(x.device, p.N * p.K)[: p.N * p.K].view(p.N, p.K)
+                _dequant_into(buf, p)
+                out[:, off:off + p.N] = torch.nn.functional.linear(x, buf)
+                off += p.N
+                continue
             sp = _splits(p.N, p.K)
             ws = torch.empty(sp, M, p.N, dtype=torch.float32, device=x.device) if sp > 1 else \
                 torch.empty(0, dtype=torch.float32, device=x.device)
@@ -188,10 +418,11 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
                                          p.N, p.K, ws, sp)
             off += p.N
         return out
+    # prefill: every part dequantised into one contiguous [N, K] scratch, one GEMM
+    buf = _dequant_scratch(x.device, w.N * w.K)[: w.N * w.K].view(w.N, w.K)
     off = 0
     for p in w.parts:
-        buf = _dequant_scratch(x.device, p.N * p.K)[: p.N * p.K].view(p.N, p.K)
-        torch.ops.hipserve.gguf_dequant(buf, p.q, p.d, p.m, p.kqt, p.row_bytes, p.N, p.K)
-        out[:, off:off + p.N] = torch.nn.functional.linear(x, buf)
+        _dequant_into(buf[off:off + p.N], p)
         off += p.N
-    return out
+    return torch.nn.functional.linear(x, buf)
+

@@ -70,12 +70,15 @@ def test_gguf_engine_on_gpu(tmp_path):
     p = str(tmp_path / "small.gguf")
     G.write_synthetic_llama_gguf(p, cfg, G.Q4_K, mixed_k=True)
     eng = LLMEngine(EngineConfig(model=p, device="cuda", num_kv_blocks=256, max_model_len=1024,
-                                 max_num_batched_tokens=256, max_num_seqs=8),
+                                 max_num_batched_tokens=512, max_num_seqs=8),
                     tp=TPGroup(0, 1, None, torch.device("cuda", 0)))
     assert isinstance(eng.runner.model.layers[0].wqkv, QuantWeight)
     res = eng.generate([[1] + list(range(300, 400)), [1, 5, 6]] * 3,
                        SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True))
     assert all(len(r[0]) == 10 for r in res)
+    # one prefill batch (the decode MFMA kernel computes in f16, the prefill GEMM on
+    # bf16-dequantised weights: a prompt chunked across both paths may legitimately
+    # flip a near-tie), then identical decode rows
     assert res[0][0] == res[2][0] == res[4][0]
 
 
@@ -115,4 +118,76 @@ def test_synthetic_q4_k_m_engine():
     res = eng.generate([[1] + list(range(300, 400)), [1, 5, 6]] * 3,
                        SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True))
     assert all(len(r[0]) == 10 for r in res)
+    # one prefill batch (the decode MFMA kernel computes in f16, the prefill GEMM on
+    # bf16-dequantised weights: a prompt chunked across both paths may legitimately
+    # flip a near-tie), then identical decode rows
     assert res[0][0] == res[2][0] == res[4][0]
+
+
+def _rand_qw(specs, seed=0):
+    """QuantWeight of random valid ggml blocks: specs = [(qtype, N, K)]."""
+    from hipserve.ops.quant import random_blocks
+    rng = np.random.default_rng(seed)
+    raws = [(t, n, k, random_blocks(rng, t, n, k)) for t, n, k in specs]
+    return QuantWeight.from_raw(raws, "cuda"), raws
+
+
+def _dense(raws):
+    return torch.cat([torch.from_numpy(G.dequantize(r, t, n * k).reshape(n, k)) for t, n, k, r in raws]).cuda()
+
+
+@pytest.mark.parametrize("qt", QTYPES + [G.Q4_1])
+@pytest.mark.parametrize("M", [1, 16, 33, 64])
+def test_mfma_v2_formats(qt, M):
+    """gguf_mfma.hip (one launch over all parts, split-K partials) vs an fp32
+    matmul of the numpy-decoded weights, for every format, including a part whose
+    rows are not a multiple of the 256-row workgroup."""
+    from hipserve.ops.quant import quant_partial, v2_splits
+    K = 2048
+    qw, raws = _rand_qw([(qt, 512, K), (qt, 80, K), (qt, 272, K)], seed=M)
+    assert qw.v2 and len(qw.groups) == 1
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense(raws).T
+    tol = 1e-2 * want.abs().max().item() + 1e-3
+    y = quant_linear(x, qw).float()
+    assert (y - want).abs().max().item() < tol
+    ws, S = quant_partial(x, qw)
+    assert S == v2_splits(qw, M) and ws.numel() == S * M * qw.N
+    part = ws.view(S, M, qw.N).sum(0)
+    assert (part - want).abs().max().item() < tol
+
+
+def test_mfma_v2_mixed_formats_one_weight():
+    """Q4_K_M-style merged q|k|v: Q4_K parts and a Q6_K part = two launches into
+    one output; direct bf16 (S == 1) and partial paths agree with the v1 kernel."""
+    from hipserve.ops import quant as Q
+    K = 4096
+    qw, raws = _rand_qw([(G.Q4_K, 1024, K), (G.Q4_K, 256, K), (G.Q6_K, 256, K)], seed=7)
+    assert len(qw.groups) == 2
+    x = torch.randn(8, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense(raws).T
+    y2 = quant_linear(x, qw).float()
+    qw.v2 = False
+    y1 = quant_linear(x, qw).float()
+    tol = 1e-2 * want.abs().max().item() + 1e-3
+    assert (y2 - want).abs().max().item() < tol and (y1 - want).abs().max().item() < tol
+    qw.v2 = True
+    old = Q.TARGET_WGS
+    try:
+        Q.TARGET_WGS = 1  # forces S == 1: bf16 written by the kernel itself
+        assert Q.v2_splits(qw, 8) == 1
+        y3 = quant_linear(x, qw).float()
+    finally:
+        Q.TARGET_WGS = old
+    assert (y3 - want).abs().max().item() < tol
+
+
+def test_splitk_glu_matches_reduce_then_silu():
+    M, I, S = 5, 1536, 3
+    ws = torch.randn(S, M, 2 * I, device="cuda") * 2
+    act = torch.empty(M, I, device="cuda", dtype=torch.bfloat16)
+    torch.ops.hipserve.splitk_glu(act, ws, S, False)
+    gu = ws.sum(0).to(torch.bfloat16).float()
+    g, u = gu[:, :I], gu[:, I:]
+    want = (g * torch.sigmoid(g)) * u
+    assert torch.allclose(act.float(), want, rtol=1e-2, atol=1e-2)

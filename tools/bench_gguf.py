@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""GGUF decode-GEMM microbenchmark on one MI355X: the v1 per-part kernel
+(csrc/kernels/gguf.hip) vs the v2 f16-MFMA kernel (csrc/kernels/gguf_mfma.hip)
+on the Llama-3-8B Q4_K_M projection shapes, random valid ggml blocks.
+
+    python tools/bench_gguf.py --m 1 16 64
+
+One JSON line per (projection, M, kernel): µs per call and the weight-byte
+bandwidth (TB/s) — decode GEMMs are bound by streaming the quantised weights.
+``--splits`` sweeps the v2 split-K factor instead of the heuristic.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from hipserve.ops import load_library  # noqa: E402
+from hipserve.ops import quant as Q  # noqa: E402
+from hipserve.weights import gguf as G  # noqa: E402
+
+H, I, NQ, NKV, D, V = 4096, 14336, 32, 8, 128, 128256
+SHAPES = {  # Q4_K_M: attn_v / ffn_down / output in Q6_K
+    "qkv": [(G.Q4_K, NQ * D, H), (G.Q4_K, NKV * D, H), (G.Q6_K, NKV * D, H)],
+    "o": [(G.Q4_K, H, NQ * D)],
+    "gate_up": [(G.Q4_K, I, H), (G.Q4_K, I, H)],
+    "down": [(G.Q6_K, H, I)],
+    "lm_head": [(G.Q6_K, V, H)],
+}
+
+
+def _time(fn, reps=20, graph_reps=10):
+    """Device µs per call: ``reps`` calls captured in one hipGraph (no host launch
+    cost, like the engine's decode step), replayed ``graph_reps`` times."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(graph_reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return 1000 * e0.elapsed_time(e1) / (reps * graph_reps)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, nargs="+", default=[1, 16, 64])
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--splits", type=int, nargs="*", default=None)
+    a = ap.parse_args()
+    load_library()
+    rng = np.random.default_rng(0)
+    for name, specs in SHAPES.items():
+        if a.only and name not in a.only:
+            continue
+        raws = [(t, n, k, Q.random_blocks(rng, t, n, k)) for t, n, k in specs]
+        qw = Q.QuantWeight.from_raw(raws, "cuda")
+        del raws
+        for M in a.m:
+            x = torch.randn(M, qw.K, device="cuda", dtype=torch.bfloat16)
+            rows = []
+            qw.v2 = False
+            rows.append(("v1", None, _time(lambda: Q.quant_linear(x, qw))))
+            qw.v2 = True
+            rows.append(("v2", Q.v2_splits(qw, M), _time(lambda: Q.quant_linear(x, qw))))
+            rows.append(("v2_partial", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw))))
+            for S in a.splits or []:
+                def run(S=S):
+                    ws = torch.empty(S * M * qw.N, dtype=torch.float32, device="cuda")
+                    Q._launch_v2(Q._empty(x.device, torch.bfloat16), ws, x, qw, S)
+                rows.append((f"v2_S{S}", S, _time(run)))
+            for kern, S, us in rows:
+                print(json.dumps({"proj": name, "M": M, "kernel": kern, "splits": S, "us": round(us, 2),
+                                  "weight_MB": round(qw.nbytes / 1e6, 2),
+                                  "TBps": round(qw.nbytes / us / 1e6, 3)}), flush=True)
+        del qw
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,7 @@ def family(name: str) -> str:
     if name.startswith(("Cijk", "Custom_Cijk")):
         m = re.search(r"MT(\d+x\d+x\d+)", name)
         return f"hipBLASLt GEMM MT{m.group(1) if m else '?'}"
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
     name = re.sub(r"^void ", "", name)
     if name.startswith("at::native"):
