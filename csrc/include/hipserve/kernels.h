@@ -78,6 +78,7 @@ void launch_gguf_dequant(void* out, const void* q, const void* d, const void* m,
 // ws[S, M, Ntot] fp32 partials. M <= 64, parts' rows % 16 == 0.
 struct GgufPart {
   const void* q;
+  const float* rs;  // FP8 formats: per-row output scale
   int qtype;
   int rows;
   int col;
@@ -85,7 +86,7 @@ struct GgufPart {
 int gguf_tiled_chunk_bytes(int qtype);
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s);
-void launch_gguf_dequant_tiled(void* out, const void* q, int qtype, int N, int K, hipStream_t s);
+void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s);
 
 }  // namespace hipserve
 
@@ -132,6 +133,8 @@ bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, lo
 void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
                                int M, int N, float eps, hipStream_t s);
 // qkv = bf16(sum_s ws) -> RoPE(q, k) -> q into qkv[:, :nq*D], k/v into the paged cache
+// out[M, N] (bf16, row stride out_stride) = sum of the fp32 partials ws[S, M, N] (decode_gemm.hip)
+void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, int N, int S, hipStream_t s);
 // act[M, I] = GLU of the plain [gate | up] partials ws[S, M, 2I] (decode_fused.hip)
 void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s);
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,

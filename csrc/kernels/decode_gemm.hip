@@ -298,6 +298,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_glu_kernel(unsigned short* 
   *reinterpret_cast<u16x8*>(out + (long)m * out_stride + a) = o;
 }
 
+void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, int N, int S, hipStream_t s) {
+  const long n8 = (long)M * N / 8;
+  if (n8 <= 0) return;
+  splitk_reduce_kernel<<<(n8 + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out), out_stride, ws, M, N, S);
+}
+
 template <int MT, int RT, int NSTEPS, bool kPacked, bool kGlu>
 static void dg_launch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                       int N, int K, int S, int flags, hipStream_t s) {

@@ -38,13 +38,21 @@ namespace hipserve {
 
 namespace {
 
-enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5 };
+// GGUF block formats + FP8 e4m3 weights (per-row scale; FP8B adds 128 x 128 block
+// scales, the block-FP8 checkpoints)
+enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5, FP8 = 6, FP8B = 7 };
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr unsigned kMagic = 0x64006400u;  // f16 pair (1024, 1024)
-constexpr int kXS = 256 + 8;              // LDS row stride (f16 elements): conflict-free b128 reads
+// x in LDS: 4 planes (lane group g) of [row][8 fragments of 8 f16 + 8 pad]: a row is
+// 36 words (36 / 4 = 9, odd) and a plane a multiple of 64 words, so the 16 lanes of
+// each ds_read_b128 lane group (rows c, planes g) land on 16 distinct 4-bank slots
+// (slot = 9 c + s mod 16): conflict-free (the plain [row][256 + 8] image was 2-way)
+constexpr int kXR = 72;  // row stride in f16 (8 fragments x 8 + 8 pad)
+template <int MT>
+constexpr int x_plane() { return 16 * MT * kXR; }
 
 HS_DEVICE h2 as_h2(unsigned u) { return __builtin_bit_cast(h2, u); }
 HS_DEVICE unsigned as_u(h2 h) { return __builtin_bit_cast(unsigned, h); }
@@ -82,13 +90,17 @@ struct Raw {
 //   Q8_0  [4 x 64 lanes x 16 q][16 rows x 8 d]                      4352 B
 //   Q4_0  [2 x 64 lanes x 16 q][16 rows x 8 d]                      2304 B
 //   Q4_1  Q4_0 + [16 rows x 8 m]                                    2560 B
+//   FP8   [4 x 64 lanes x 16 q]                                     4096 B
+//   FP8B  FP8 + [16 rows x 2 f32 block scales]                      4224 B
 template <int QT>
 constexpr int chunk_bytes() {
-  return QT == Q4_K ? 2304 : QT == Q5_K ? 2816 : QT == Q6_K ? 3360 : QT == Q8_0 ? 4352 : QT == Q4_0 ? 2304 : 2560;
+  return QT == Q4_K ? 2304 : QT == Q5_K ? 2816 : QT == Q6_K ? 3360 : QT == Q8_0 ? 4352 : QT == Q4_0 ? 2304
+       : QT == Q4_1 ? 2560 : QT == FP8 ? 4096 : 4224;
 }
 
 struct Part {
   const unsigned char* q;
+  const float* rs;  // per-row output scale (FP8), nullptr for GGUF formats
   int qt;       // format of the part
   int rows;     // N of the part (multiple of 16)
   int col;      // first output column
@@ -122,6 +134,11 @@ HS_DEVICE void load_raw(const unsigned char* ch, int g, int c, int lane, Raw& r)
     r.s2[0] = sc.x;
     r.s2[1] = sc.y;
     r.h[0] = *reinterpret_cast<const unsigned short*>(ch + 3328 + 2 * c);
+  } else if constexpr (QT == FP8 || QT == FP8B) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = ld16(ch + 1024 * i + 16 * lane);
+    if constexpr (QT == FP8B)  // the lane's 64 k sit in 128-block (g >> 1) of this super-chunk
+      r.s2[0] = *reinterpret_cast<const unsigned*>(ch + 4096 + 8 * c + 4 * (g >> 1));
   } else if constexpr (QT == Q8_0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.v[i] = ld16(ch + 1024 * i + 16 * lane);
@@ -192,6 +209,8 @@ struct Dec {
       fcB = -dmin * m2;
     } else if constexpr (QT == Q6_K) {
       d6 = h2f(r.h[0]);
+    } else if constexpr (QT == FP8 || QT == FP8B) {
+      fdA = fdB = QT == FP8B ? __builtin_bit_cast(float, r.s2[0]) : 1.f;
     } else {
       fdA = h2f(r.h[0]);
       fdB = h2f(r.h[1]);
@@ -222,6 +241,18 @@ struct Dec {
   }
 
   HS_DEVICE f16x8 ints(const Raw& r, int g, int s) const {
+    if constexpr (QT == FP8 || QT == FP8B) {
+      // e4m3 -> f16 by moving bits: sign to bit 15, exponent + mantissa to bits 7-13
+      // gives the value / 256 exactly (normals and subnormals; the 256 is folded into
+      // the row scale). Bytes (0, 2) and (1, 3) of a word pair up as in the GGUF paths.
+      const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+      const unsigned wa = qv[s >> 1][2 * (s & 1)], wb = qv[s >> 1][2 * (s & 1) + 1];
+      const unsigned p0 = ((wa << 7) & 0x3F803F80u) | ((wa << 8) & 0x80008000u);
+      const unsigned p1 = ((wa >> 1) & 0x3F803F80u) | (wa & 0x80008000u);
+      const unsigned p2 = ((wb << 7) & 0x3F803F80u) | ((wb << 8) & 0x80008000u);
+      const unsigned p3 = ((wb >> 1) & 0x3F803F80u) | (wb & 0x80008000u);
+      return frag(as_h2(p0), as_h2(p1), as_h2(p2), as_h2(p3));
+    }
     unsigned p[4];
     _Float16 z;  // 1024 + zero point
     if constexpr (QT == Q4_K || QT == Q5_K) {
@@ -277,6 +308,11 @@ struct Dec {
 
   HS_DEVICE f16x8 step(const Raw& r, int g, int s) const {
     const f16x8 q = ints(r, g, s);
+    if constexpr (QT == FP8) return q;  // row scale in the epilogue
+    if constexpr (QT == FP8B) {
+      const u32x4 qu = __builtin_bit_cast(u32x4, q);
+      return frag(as_h2(qu[0]) * dA, as_h2(qu[1]) * dA, as_h2(qu[2]) * dA, as_h2(qu[3]) * dA);
+    }
     h2 dd, cc;
     if constexpr (QT == Q6_K) {
       float d, c;
@@ -306,7 +342,7 @@ HS_DEVICE _Float16 to_f16_sat(unsigned short b) {
 // One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
 // x staging. Body per format; the kernel picks it per part (two formats per launch).
 template <int QT, int MT, int RT, int NWAVES>
-HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][16 * MT * kXS], unsigned short* __restrict__ out, long out_stride,
+HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short* __restrict__ out, long out_stride,
                            float* __restrict__ ws, const unsigned short* __restrict__ x, long x_stride,
                            const Part& P, int M, int Ntot, int K, int sb_per_split) {
   constexpr int XR = 16 * MT;           // staged x rows (M padded)
@@ -323,12 +359,13 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][16 * MT * kXS], unsigned short* __r
   for (int r = 0; r < RT; ++r) base[r] = P.q + (long)min(gi0 + r, ngroups - 1) * nsb * CB;
 
   // x staging: 32 fragments (g, s) of 8 per row and super-chunk; thread -> (row, fragment)
-  constexpr int XP = (XR * 32 + NT - 1) / NT;
+  constexpr int XP = XR * 32 / NT;
+  static_assert(XP * NT == XR * 32, "x staging must divide evenly (no guarded, sinkable loads)");
   u16x8 xv[XP];
   auto load_x = [&](int sb) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
-      const int idx = min(i * NT + tid, XR * 32 - 1), row = idx >> 5, fr = idx & 31;
+      const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
       const int kb = kbase<QT>(fr >> 3, fr & 7);
       // rows >= M are clamped, never stored
       xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + sb * 256 + kb);
@@ -338,12 +375,11 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][16 * MT * kXS], unsigned short* __r
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
-      if (idx >= XR * 32) break;
       const u16x8 b = xv[i];
       f16x8 h;
       h[0] = to_f16_sat(b[0]); h[1] = to_f16_sat(b[2]); h[2] = to_f16_sat(b[1]); h[3] = to_f16_sat(b[3]);
       h[4] = to_f16_sat(b[4]); h[5] = to_f16_sat(b[6]); h[6] = to_f16_sat(b[5]); h[7] = to_f16_sat(b[7]);
-      *reinterpret_cast<f16x8*>(&xs[buf][row * kXS + fr * 8]) = h;
+      *reinterpret_cast<f16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = h;
     }
   };
 
@@ -353,25 +389,30 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][16 * MT * kXS], unsigned short* __r
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Raw raw[RT];
+  // Two register sets for the weights, used alternately (loop unrolled by 2): no
+  // copies between iterations, so the only wait for a super-chunk's weights is at
+  // their first use. Per iteration the x loads of the next super-chunk go out before
+  // its weight loads: store_x's in-order vmcnt wait then leaves the weights in flight.
+  Raw rawA[RT], rawB[RT];
   if (sb0 < sb1) {
     load_x(sb0);
 #pragma unroll
-    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sb0 * CB, g, c, lane, raw[r]);
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sb0 * CB, g, c, lane, rawA[r]);
     store_x(0);
   }
   __syncthreads();
-  for (int sb = sb0; sb < sb1; ++sb) {
+  auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
     const int buf = (sb - sb0) & 1;
-    Raw cur[RT];
+    // next super-chunk in flight while this one is decoded and multiplied; issued
+    // unconditionally (the last iteration re-reads its own chunk) so no branch splits
+    // the loads from their uses and the vmcnt waits stay counted, not drained
+    const int sn = min(sb + 1, sb1 - 1);
+    load_x(sn);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < RT; ++r) cur[r] = raw[r];
-    if (sb + 1 < sb1) {  // next super-chunk in flight while this one is decoded and multiplied
-      load_x(sb + 1);
-#pragma unroll
-      for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)(sb + 1) * CB, g, c, lane, raw[r]);
-    }
-    const _Float16* xb = &xs[buf][c * kXS + 64 * g];  // fragment (g, s) of row 16t + c at + 8s
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
+    __builtin_amdgcn_sched_barrier(0);  // the scheduler would sink them below the MFMAs
+    const _Float16* xb = &xs[buf][g * x_plane<MT>() + c * kXR];  // fragment (g, s) of row 16t + c at + 8s
     Dec<QT> dec[RT];
 #pragma unroll
     for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
@@ -382,19 +423,30 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][16 * MT * kXS], unsigned short* __r
       for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {  // one LDS read of x per (s, t), shared by the RT row groups
-        const f16x8 b = *reinterpret_cast<const f16x8*>(xb + 16 * t * kXS + 8 * s);
+        const f16x8 b = *reinterpret_cast<const f16x8*>(xb + 16 * t * kXR + 8 * s);
 #pragma unroll
         for (int r = 0; r < RT; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b, acc[r][t], 0, 0, 0);
       }
     }
-    if (sb + 1 < sb1) store_x(buf ^ 1);
+    store_x(buf ^ 1);
     __syncthreads();
+  };
+  int sb = sb0;
+  for (; sb + 1 < sb1; sb += 2) {  // no exit inside the pair: the loop-carried vmcnt state stays exact
+    iter(sb, rawA, rawB);
+    iter(sb + 1, rawB, rawA);
   }
+  if (sb < sb1) iter(sb, rawA, rawB);
   // C: col m = 16t + c, rows n = 16 gi + 4g + j
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
     if (gi0 + r >= ngroups) continue;
     const int col = P.col + 16 * (gi0 + r) + 4 * g;
+    if constexpr (QT == FP8 || QT == FP8B) {
+      const f32x4 rs = *reinterpret_cast<const f32x4*>(P.rs + 16 * (gi0 + r) + 4 * g);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[r][t] *= rs;
+    }
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int m = 16 * t + c;
@@ -416,7 +468,7 @@ __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __r
                                                             float* __restrict__ ws, const unsigned short* __restrict__ x,
                                                             long x_stride, Parts parts, int M, int Ntot, int K,
                                                             int sb_per_split) {
-  __shared__ __attribute__((aligned(16))) _Float16 xs[2][16 * MT * kXS];
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<MT>()];
   const int tile = blockIdx.x;
   int pi = 0;
 #pragma unroll
@@ -427,6 +479,17 @@ __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __r
     qgemm2_body<QA, MT, RT, NWAVES>(xs, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
   else
     qgemm2_body<QB, MT, RT, NWAVES>(xs, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+}
+
+// 33 <= M <= 64 body shape (HIPSERVE_QGEMM_M64, for A/B measurement): 0 = 8 waves x 1
+// row group (default: measured 3-8 % faster at M = 64), 1 = 4 waves x 2 (both 128
+// weight rows per workgroup)
+int m64_variant() {
+  static const int v = [] {
+    const char* e = getenv("HIPSERVE_QGEMM_M64");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <int QA, int QB>
@@ -442,15 +505,18 @@ void launch_t(void* out, long out_stride, float* ws, const void* x, long x_strid
     qgemm2_kernel<QA, QB, 1, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
   else if (M <= 32)
     qgemm2_kernel<QA, QB, 2, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
-  else
+  else if (m64_variant() == 1)  // 4 waves x 2 row groups
     qgemm2_kernel<QA, QB, 4, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+  else  // 8 waves x 1 row group: half the accumulators and weight registers per wave
+    qgemm2_kernel<QA, QB, 4, 1, 8><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
 }
 
 // ---------------------------------------------------------------- tiled -> bf16
 // Prefill: one wave per (row group, super-chunk) chunk, out[N, K] row-major bf16.
 template <int QT>
 __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __restrict__ out,
-                                                            const unsigned char* __restrict__ q, int ngroups, int K) {
+                                                            const unsigned char* __restrict__ q,
+                                                            const float* __restrict__ rs, int ngroups, int K) {
   constexpr int CB = chunk_bytes<QT>();
   const int nsb = K >> 8;
   const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -467,6 +533,7 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
     const f16x8 q = dec.ints(r, g, s);  // exact integers, pair order {0, 2, 1, 3, 4, 6, 5, 7}
     float d, m;
     dec.scale(r, g, s, d, m);           // fp32 scale: one rounding, to bf16, like the v1 dequant
+    if constexpr (QT == FP8 || QT == FP8B) d *= rs[16 * gi + c];
     constexpr int src[8] = {0, 2, 1, 3, 4, 6, 5, 7};
     u16x8 o;
 #pragma unroll
@@ -485,6 +552,8 @@ int gguf_tiled_chunk_bytes(int qtype) {
     case Q4_K: return chunk_bytes<Q4_K>();
     case Q5_K: return chunk_bytes<Q5_K>();
     case Q6_K: return chunk_bytes<Q6_K>();
+    case FP8: return chunk_bytes<FP8>();
+    case FP8B: return chunk_bytes<FP8B>();
   }
   return 0;
 }
@@ -506,8 +575,8 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
     tiles = 0;
     for (int i = 0; i < nparts; ++i) {
       if (parts[i].qtype != fa && parts[i].qtype != fb) continue;
-      P.p[P.n++] = Part{static_cast<const unsigned char*>(parts[i].q), parts[i].qtype, parts[i].rows, parts[i].col,
-                        tiles};
+      P.p[P.n++] = Part{static_cast<const unsigned char*>(parts[i].q), parts[i].rs, parts[i].qtype, parts[i].rows,
+                        parts[i].col, tiles};
       tiles += (parts[i].rows + ROWS - 1) / ROWS;
     }
     return P;
@@ -531,22 +600,26 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
       case Q4_K: launch_t<Q4_K, Q4_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
       case Q5_K: launch_t<Q5_K, Q5_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
       case Q6_K: launch_t<Q6_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case FP8: launch_t<FP8, FP8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case FP8B: launch_t<FP8B, FP8B>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
     }
   }
 }
 
-void launch_gguf_dequant_tiled(void* out, const void* q, int qtype, int N, int K, hipStream_t s) {
+void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s) {
   const long items = (long)(N / 16) * (K / 256);
   const dim3 grid((unsigned)((items + 3) / 4)), block(256);
   auto* o = static_cast<unsigned short*>(out);
   auto* qq = static_cast<const unsigned char*>(q);
   switch (qtype) {
-    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
-    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
-    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
-    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
-    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
-    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, N / 16, K); break;
+    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
   }
 }
 

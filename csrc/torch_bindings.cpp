@@ -199,11 +199,11 @@ void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const 
 // formats / rows / output columns. ws.numel() > 0: fp32 partials [S_actual, M, Ntot]
 // (returned S_actual = ceil(nsb / ceil(nsb / S))); else bf16 out [M, >= Ntot], S == 1.
 int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const std::vector<at::Tensor>& qs,
-                        const std::vector<int64_t>& qtypes, const std::vector<int64_t>& rows,
+                        const std::vector<at::Tensor>& rss, const std::vector<int64_t>& qtypes, const std::vector<int64_t>& rows,
                         const std::vector<int64_t>& cols, int64_t Ntot, int64_t K, int64_t splits) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x);
   const int np = qs.size();
-  TORCH_CHECK(np >= 1 && np <= 4 && (int)qtypes.size() == np && (int)rows.size() == np && (int)cols.size() == np,
+  TORCH_CHECK(np >= 1 && np <= 4 && (int)qtypes.size() == np && (int)rss.size() == np && (int)rows.size() == np && (int)cols.size() == np,
               "gguf_gemm_parts: 1-4 parts");
   TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && splits >= 1);
   const int M = x.size(0);
@@ -214,13 +214,17 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   const int S = (nsb + per - 1) / per;
   hipserve::GgufPart P[4];
   for (int i = 0; i < np; ++i) {
-    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 5, "gguf_gemm_parts: kernel qtype 0-5");
+    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 7, "gguf_gemm_parts: kernel qtype 0-7");
+    const bool fp8 = qtypes[i] >= 6;
+    TORCH_CHECK(!fp8 || (rss[i].scalar_type() == at::kFloat && rss[i].is_contiguous() && rss[i].numel() == rows[i] &&
+                         rss[i].device() == x.device()), "FP8 parts need an fp32 row scale per row");
     TORCH_CHECK(qs[i].scalar_type() == at::kByte && qs[i].is_contiguous() && qs[i].device() == x.device());
     TORCH_CHECK(cols[i] % 4 == 0 && rows[i] % 16 == 0 && rows[i] > 0 && cols[i] + rows[i] <= Ntot,
                 "parts: 16-row multiples at 4-aligned columns inside Ntot");
     TORCH_CHECK(qs[i].numel() == rows[i] / 16 * nsb * hipserve::gguf_tiled_chunk_bytes(qtypes[i]),
                 "part q is not a tiled [N/16, K/256, chunk] tensor of its format");
-    P[i] = hipserve::GgufPart{qs[i].data_ptr(), (int)qtypes[i], (int)rows[i], (int)cols[i]};
+    P[i] = hipserve::GgufPart{qs[i].data_ptr(), fp8 ? rss[i].data_ptr<float>() : nullptr, (int)qtypes[i],
+                              (int)rows[i], (int)cols[i]};
   }
   float* wp = nullptr;
   if (ws.numel() > 0) {
@@ -239,13 +243,16 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   return S;
 }
 
-void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, int64_t qtype, int64_t N, int64_t K) {
+void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& rs, int64_t qtype, int64_t N,
+                        int64_t K) {
   CHECK_DEV(q); CHECK_BF16(out);
   TORCH_CHECK(out.is_contiguous() && out.numel() >= N * K && N % 16 == 0 && K % 256 == 0);
-  TORCH_CHECK(qtype >= 0 && qtype <= 5 && q.scalar_type() == at::kByte && q.is_contiguous());
+  TORCH_CHECK(qtype >= 0 && qtype <= 7 && q.scalar_type() == at::kByte && q.is_contiguous());
   TORCH_CHECK(q.numel() == N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype), "not a tiled tensor");
+  TORCH_CHECK(qtype < 6 || (rs.scalar_type() == at::kFloat && rs.numel() == N), "FP8 needs an fp32 row scale");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
-  hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), qtype, N, K, cur_stream());
+  hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), qtype >= 6 ? rs.data_ptr<float>() : nullptr,
+                                      qtype, N, K, cur_stream());
 }
 
 void gguf_dequant(at::Tensor& out, const at::Tensor& q, const at::Tensor& d, const at::Tensor& mn,
@@ -576,6 +583,15 @@ void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, co
                                      head_dim, k_cache.size(2), mode, cur_stream());
 }
 
+void splitk_reduce(at::Tensor& out, const at::Tensor& ws, int64_t splits) {
+  CHECK_DEV(out); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  const int M = out.size(0), N = out.size(1);
+  TORCH_CHECK(N % 8 == 0 && out.stride(0) % 8 == 0, "splitk_reduce: N % 8 == 0");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * (long)N);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  hipserve::launch_splitk_reduce(out.data_ptr(), out.stride(0), ws.data_ptr<float>(), M, N, splits, cur_stream());
+}
+
 void splitk_glu(at::Tensor& act, const at::Tensor& ws, int64_t splits, bool gelu) {
   CHECK_DEV(act); CHECK_BF16(act); CHECK_ROWMAJOR(act);
   const int M = act.size(0), I = act.size(1);
@@ -709,8 +725,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
   // custom all-reduce control ops carry an opaque state handle: catch-all kernels
-  m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits) -> int", &gguf_gemm_parts);
-  m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
+  m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits) -> int", &gguf_gemm_parts);
+  m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
   m.def("car_create(int rank, int world, int max_bytes) -> int", &car_create);
   m.def("car_handle(int state) -> Tensor", &car_handle);
   m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);
@@ -729,6 +745,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu) -> ()");
+  m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("penalty_apply(Tensor(a!) logits, Tensor slot, Tensor pres, Tensor freq, Tensor rep, Tensor counts, Tensor seen) -> ()");
@@ -762,6 +779,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.impl("splitk_rope_cache", &splitk_rope_cache);
   m.impl("splitk_glu", &splitk_glu);
+  m.impl("splitk_reduce", &splitk_reduce);
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);

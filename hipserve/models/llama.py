@@ -98,6 +98,10 @@ def shard_sizes(cfg: ModelConfig, tp: int):
 
 
 class LlamaModel:
+    # load FP8 checkpoints natively (e4m3 + scales, ops/quant.py) instead of
+    # dequantising them to bf16 at load (weights/safetensors_loader.py)
+    native_fp8 = True
+
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,
                  max_pos: int | None = None):
         self.cfg = cfg
@@ -208,6 +212,8 @@ class LlamaModel:
         from ..ops import quant as Q
         from ..weights import gguf as G
 
+        if scheme.lower() == "fp8":
+            return self.allocate_random_fp8(seed)
         if self.tp.world_size != 1:
             raise NotImplementedError("the GGUF tier runs TP=1 (one device per pod, like llama-server)")
         types = self.QUANT_SCHEMES[scheme.lower()]
@@ -238,6 +244,43 @@ class LlamaModel:
                 wqkv=mat(("q", nq * D, H), ("k", nkv * D, H), ("v", nkv * D, H)),
                 wo=mat(("o", H, nq * D)), ln2=torch.ones(H, device=dev, dtype=dt),
                 wgu=mat(("gate", I, H), ("up", I, H)), wd=mat(("down", H, I))))
+        self.quant_linear = Q.quant_linear
+
+    def allocate_random_fp8(self, seed: int = 0):
+        """Random-init model whose projections are FP8 e4m3 with per-output-channel
+        scales (the layout of the reference's "FP8-Dynamic" checkpoints, kept native:
+        ops/quant.py QuantWeight, FP8 format). Embeddings, norms and lm_head stay bf16
+        (the checkpoints' ``ignore`` list). Off the GPU the same e4m3 values are
+        dequantised to dense weights."""
+        from ..ops import quant as Q
+
+        self.allocate_random(seed=seed)  # norms, embeddings, lm_head, bf16 projections (replaced below)
+        dev = self.device
+        g = torch.Generator(device=dev).manual_seed(seed + 1)
+
+        def fp8(w):
+            s = w.float().abs().amax(1, keepdim=True).clamp_min(1e-12) / 448.0
+            q = (w.float() / s).to(torch.float8_e4m3fn)
+            if dev.type == "cuda" and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0:
+                return Q.QuantPart.from_fp8(q, s, dev)
+            return (q.float() * s).to(self.dtype)
+
+        def quant(w, splits):
+            parts = [fp8(t) for t in torch.split(w, splits, 0)]
+            if all(isinstance(p, Q.QuantPart) for p in parts):
+                return Q.QuantWeight(parts)
+            return torch.cat([p if isinstance(p, torch.Tensor) else Q.dequantize(Q.QuantWeight([p])) for p in parts])
+
+        D = self.D
+        for lw in self.layers:
+            lw.wqkv = quant(lw.wqkv, [self.nq * D, self.nkv * D, self.nkv * D])
+            lw.wo = quant(lw.wo, [lw.wo.shape[0]])
+            if lw.wgu is not None:
+                lw.wgu = quant(lw.wgu, [self.inter, self.inter])
+                lw.wd = quant(lw.wd, [lw.wd.shape[0]])
+        del g
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         self.quant_linear = Q.quant_linear
 
     # ---------------------------------------------------------------- forward

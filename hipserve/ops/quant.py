@@ -21,7 +21,10 @@ import torch
 
 from ..weights import gguf as G
 
-KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5}
+# FP8 e4m3 weights (compressed-tensors "FP8-Dynamic" per-channel / per-tensor scales,
+# and 128 x 128 block-scaled FP8) share the v2 kernel: pseudo type ids beside ggml's
+FP8, FP8B = 1000, 1001
+KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7}
 MAX_FUSED_M = 64
 
 
@@ -54,7 +57,8 @@ def repack(raw: np.ndarray, qtype: int, N: int, K: int):
     raise NotImplementedError(G.TYPE_NAMES.get(qtype, qtype))
 
 
-CHUNK_BYTES = {G.Q4_K: 2304, G.Q5_K: 2816, G.Q6_K: 3360, G.Q8_0: 4352, G.Q4_0: 2304, G.Q4_1: 2560}
+CHUNK_BYTES = {G.Q4_K: 2304, G.Q5_K: 2816, G.Q6_K: 3360, G.Q8_0: 4352, G.Q4_0: 2304, G.Q4_1: 2560,
+               FP8: 4096, FP8B: 4224}
 
 
 def _lanes(a: np.ndarray, n_ld: int) -> np.ndarray:
@@ -103,14 +107,40 @@ def tileable(N: int, K: int) -> bool:
 
 
 class QuantPart:
-    """One GGUF matrix on the device: ``tiled`` parts (N % 16 == 0) hold the v2
-    layout in ``q`` [N/16, K/256, chunk]; others the v1 row layout + SoA scales."""
+    """One quantised matrix on the device: ``tiled`` parts (N % 16 == 0) hold the v2
+    layout in ``q`` [N/16, K/256, chunk]; others (GGUF only) the v1 row layout + SoA
+    scales. FP8 parts carry ``rs``, the fp32 per-row output scale (256 x the
+    channel scale: the kernel's e4m3 -> f16 bit move yields value / 256)."""
 
-    def __init__(self, qtype, N, K, q, d, m, row_bytes, tiled=False):
+    def __init__(self, qtype, N, K, q, d, m, row_bytes, tiled=False, rs=None):
         self.qtype, self.N, self.K = qtype, N, K
         self.kqt = KERNEL_QT[qtype]
         self.q, self.d, self.m, self.row_bytes = q, d, m, row_bytes
         self.tiled = tiled
+        self.rs = rs if rs is not None else torch.empty(0, dtype=torch.float32, device=q.device)
+
+    @classmethod
+    def from_fp8(cls, q: torch.Tensor, scale: torch.Tensor, device):
+        """FP8 e4m3 weight [N, K] (float8_e4m3fn or its uint8 bits) and its scale:
+        one value (per tensor), [N] / [N, 1] (per output channel) or
+        [ceil(N/128), ceil(K/128)] (128 x 128 blocks). N % 16 == 0, K % 256 == 0."""
+        N, K = q.shape
+        q = q.to(device)
+        q8 = q.view(torch.uint8) if q.dtype != torch.uint8 else q
+        s = scale.to(device=device, dtype=torch.float32)
+        R, nsb = N // 16, K // 256
+        lanes = q8.reshape(R, 16, nsb, 4, 4, 16).permute(0, 2, 4, 3, 1, 5).reshape(R, nsb, 4096)
+        if s.numel() == 1 or (s.numel() == N and (s.dim() == 1 or s.shape[-1] == 1)):
+            rs = (256.0 * s.reshape(-1).expand(N)).contiguous()
+            return cls(FP8, N, K, lanes.contiguous(), _E16(device), _E16(device), 0, tiled=True, rs=rs)
+        bn, bk = s.shape
+        if bn * 128 < N or bk * 128 < K:
+            raise ValueError(f"block scale {tuple(s.shape)} does not cover a {N}x{K} weight in 128-blocks")
+        rows = s[torch.arange(N, device=device) // 128][:, : K // 128]          # [N, K/128]
+        blk = rows.reshape(R, 16, nsb, 2).permute(0, 2, 1, 3).contiguous().view(torch.uint8).reshape(R, nsb, 128)
+        chunk = torch.cat([lanes, blk], 2).contiguous()
+        rs = torch.full((N,), 256.0, dtype=torch.float32, device=device)
+        return cls(FP8B, N, K, chunk, _E16(device), _E16(device), 0, tiled=True, rs=rs)
 
     @classmethod
     def build(cls, raw, qtype: int, N: int, K: int, device):
@@ -124,7 +154,7 @@ class QuantPart:
 
     @property
     def nbytes(self):
-        return self.q.numel() + 2 * (self.d.numel() + self.m.numel())
+        return self.q.numel() + 2 * (self.d.numel() + self.m.numel()) + 4 * self.rs.numel()
 
 
 class QuantWeight:
@@ -151,7 +181,8 @@ class QuantWeight:
             self._groups = [(kqt, ps, cols) for kqt, (ps, cols) in groups.items()]
             self._v2 = all(p.tiled for p in self.parts)
             cols = np.cumsum([0] + [p.N for p in self.parts])[:-1].tolist()
-            self.v2_args = ([p.q for p in self.parts], [p.kqt for p in self.parts], [p.N for p in self.parts], cols)
+            self.v2_args = ([p.q for p in self.parts], [p.rs for p in self.parts], [p.kqt for p in self.parts],
+                            [p.N for p in self.parts], cols)
             self._gkey = key
         return self._groups
 
@@ -246,7 +277,7 @@ def _dequant_scratch(device, numel):
 
 def _dequant_into(buf: torch.Tensor, p: QuantPart):
     if p.tiled:
-        torch.ops.hipserve.gguf_dequant_tiled(buf, p.q, p.kqt, p.N, p.K)
+        torch.ops.hipserve.gguf_dequant_tiled(buf, p.q, p.rs, p.kqt, p.N, p.K)
     else:
         torch.ops.hipserve.gguf_dequant(buf, p.q, p.d, p.m, p.kqt, p.row_bytes, p.N, p.K)
 
@@ -312,6 +343,10 @@ def v2_splits(w: QuantWeight, M: int) -> int:
 _EMPTY: dict = {}
 
 
+def _E16(device):
+    return torch.empty(0, dtype=torch.int16, device=device)
+
+
 def _empty(device, dtype):
     key = (device, dtype)
     t = _EMPTY.get(key)
@@ -322,7 +357,7 @@ def _empty(device, dtype):
 
 def _launch_v2(out, ws, x, w: QuantWeight, S: int):
     a = w.v2_args
-    torch.ops.hipserve.gguf_gemm_parts(out, ws, x, a[0], a[1], a[2], a[3], w.N, w.K, S)
+    torch.ops.hipserve.gguf_gemm_parts(out, ws, x, a[0], a[1], a[2], a[3], a[4], w.N, w.K, S)
 
 
 def _graph_time_us(fn, reps: int = 10, rounds: int = 3) -> float:
@@ -402,7 +437,8 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
                 return out
             ws = torch.empty(S, M, w.N, dtype=torch.float32, device=x.device)
             _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S)
-            return ws.sum(0).to(torch.bfloat16)
+            torch.ops.hipserve.splitk_reduce(out, ws, S)
+            return out
         off = 0
         for p in w.parts:  # v1: row-layout parts only
             if p.tiled:

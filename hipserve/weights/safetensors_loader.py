@@ -86,6 +86,34 @@ class _Ckpt:
             return self.full(name)[:, start:stop]
         return self.where[name].get_slice(name)[:, start:stop]
 
+    # ---- native FP8: e4m3 bits + scale, sliced per TP rank, never dequantised
+    def fp8_scale_name(self, name) -> str | None:
+        base = name[: -len("weight")] if name.endswith("weight") else name + "_"
+        for sname in (base + "weight_scale", base + "weight_scale_inv"):
+            if sname in self.where:
+                return sname
+        return None
+
+    def is_fp8_e4m3(self, name) -> bool:
+        return (name in self.where and self.where[name].get_slice(name).get_dtype() == "F8_E4M3"
+                and self.fp8_scale_name(name) is not None)
+
+    def fp8_part(self, name, axis: int, start: int, stop: int):
+        """(e4m3 weight slice, matching scale) — rows (axis 0, output channels) or
+        columns (axis 1, input features) [start, stop). None when a 128-block scale
+        would need a split block."""
+        sname = self.fp8_scale_name(name)
+        sc = self.where[sname].get_tensor(sname).float()
+        sl = self.where[name].get_slice(name)
+        q = sl[start:stop] if axis == 0 else sl[:, start:stop]
+        per_row = sc.numel() == 1 or (sc.dim() >= 1 and sc.shape[0] == sl.get_shape()[0] and sc.numel() == sc.shape[0])
+        if per_row:
+            return q, (sc.reshape(-1)[start:stop] if axis == 0 and sc.numel() > 1 else sc.reshape(-1))
+        if start % 128:
+            return None
+        b0, b1 = start // 128, -(-stop // 128)
+        return q, (sc[b0:b1] if axis == 0 else sc[:, b0:b1])
+
     def _is_fp8(self, name) -> bool:
         """True for every tensor that must be dequantised whole before slicing."""
         if name in self.virtual:
@@ -162,6 +190,25 @@ def load_hf_weights(model: LlamaModel, model_path: str):
     def to(t):
         return t.to(device=dev, dtype=dt).contiguous()
 
+    # native FP8 projections (the FP8-Dynamic / block-FP8 checkpoints): kept as e4m3
+    # in HBM and multiplied by the v2 dequant-MFMA kernel (ops/quant.py), half the
+    # bytes of the bf16 weights
+    native_fp8 = dev.type == "cuda" and getattr(model, "native_fp8", True)
+    n_fp8 = [0]
+
+    def proj(specs):
+        """specs: [(name, axis, start, stop)] stacked along the output rows."""
+        if native_fp8 and all(ck.is_fp8_e4m3(n) for n, *_ in specs):
+            from ..ops import quant as Q
+
+            parts = [ck.fp8_part(n, ax, a, b) for n, ax, a, b in specs]
+            if all(pp is not None for pp in parts) and all(
+                    pp[0].shape[0] % 16 == 0 and pp[0].shape[1] % 256 == 0 for pp in parts):
+                n_fp8[0] += 1
+                return Q.QuantWeight([Q.QuantPart.from_fp8(qq, sc, dev) for qq, sc in parts])
+        ts = [ck.rows(n, a, b) if ax == 0 else ck.cols(n, a, b) for n, ax, a, b in specs]
+        return to(torch.cat(ts, 0) if len(ts) > 1 else ts[0])
+
     def normw(name):
         """RMSNorm weight: Gemma's x * (1 + w) kept exactly as fp32 (1 + w)."""
         t = ck.full(name)
@@ -195,14 +242,14 @@ def load_hf_weights(model: LlamaModel, model_path: str):
             f = ck.full(a + "qkv_proj.weight")
             q, k, v = torch.split(f, [cfg.num_heads * D, cfg.num_kv_heads * D, cfg.num_kv_heads * D], 0)
             q, k, v = q[qs], k[ks], v[ks]
+            wqkv = to(torch.cat([q, k, v], 0))
         else:
-            q = ck.rows(a + "q_proj.weight", qs.start, qs.stop)
-            k = ck.rows(a + "k_proj.weight", ks.start, ks.stop)
-            v = ck.rows(a + "v_proj.weight", ks.start, ks.stop)
+            wqkv = proj([(a + "q_proj.weight", 0, qs.start, qs.stop), (a + "k_proj.weight", 0, ks.start, ks.stop),
+                         (a + "v_proj.weight", 0, ks.start, ks.stop)])
         lw = LayerWeights(
             ln1=normw(p + "input_layernorm.weight"),
-            wqkv=to(torch.cat([q, k, v], 0)),
-            wo=to(ck.cols(a + "o_proj.weight", qs.start, qs.stop)),
+            wqkv=wqkv,
+            wo=proj([(a + "o_proj.weight", 1, qs.start, qs.stop)]),
             ln2=normw(p + ("pre_feedforward_layernorm.weight" if cfg.sandwich_norm
                            else "post_attention_layernorm.weight")),
         )
@@ -223,11 +270,14 @@ def load_hf_weights(model: LlamaModel, model_path: str):
             lw.wgu = to(torch.cat([f[r * inter:(r + 1) * inter], f[I + r * inter:I + (r + 1) * inter]], 0))
             lw.wd = to(ck.cols(p + "mlp.down_proj.weight", r * inter, (r + 1) * inter))
         else:
-            g = ck.rows(p + "mlp.gate_proj.weight", r * inter, (r + 1) * inter)
-            u = ck.rows(p + "mlp.up_proj.weight", r * inter, (r + 1) * inter)
-            lw.wgu = to(torch.cat([g, u], 0))
-            lw.wd = to(ck.cols(p + "mlp.down_proj.weight", r * inter, (r + 1) * inter))
+            lw.wgu = proj([(p + "mlp.gate_proj.weight", 0, r * inter, (r + 1) * inter),
+                           (p + "mlp.up_proj.weight", 0, r * inter, (r + 1) * inter)])
+            lw.wd = proj([(p + "mlp.down_proj.weight", 1, r * inter, (r + 1) * inter)])
         model.layers.append(lw)
+    if n_fp8[0]:
+        from ..ops import quant as Q
+
+        model.quant_linear = Q.quant_linear
 
 
 def _load_experts(ck, p, cfg, r, inter, to):

@@ -191,3 +191,113 @@ def test_splitk_glu_matches_reduce_then_silu():
     g, u = gu[:, :I], gu[:, I:]
     want = (g * torch.sigmoid(g)) * u
     assert torch.allclose(act.float(), want, rtol=1e-2, atol=1e-2)
+
+
+# ---------------------------------------------------------------- FP8 weights
+def _fp8_ref(q, s, N, K):
+    """fp32 dequantised weight of e4m3 bits q and scale s (per tensor / row / 128-block)."""
+    w = q.float()
+    if s.numel() == 1 or s.numel() == N:
+        return w * s.reshape(-1, 1).float()
+    rows = s.float()[torch.arange(N) // 128][:, torch.arange(K) // 128]
+    return w * rows
+
+
+@pytest.mark.parametrize("mode", ["tensor", "channel", "block"])
+@pytest.mark.parametrize("M", [1, 16, 40, 64])
+def test_fp8_linear_matches_fp32(mode, M):
+    """FP8 e4m3 weights in the v2 kernel (bit-moved e4m3 -> f16, row / block scales)
+    vs an fp32 matmul of the dequantised weights; decode (M <= 64, direct and split-K
+    partials) and the prefill path (tiled dequant + hipBLASLt)."""
+    from hipserve.ops import quant as Q
+    torch.manual_seed(M)
+    N1, N2, K = 512, 144, 1536
+    qs, ss = [], []
+    for N in (N1, N2):
+        w = torch.randn(N, K) * 0.03
+        if mode == "tensor":
+            s = w.abs().amax() / 448.0
+        elif mode == "channel":
+            s = w.abs().amax(1, keepdim=True) / 448.0
+        else:
+            s = torch.rand(-(-N // 128), K // 128) * 1e-4 + 5e-5
+        full = s if mode != "block" else s[torch.arange(N) // 128][:, torch.arange(K) // 128]
+        q = (w / full).clamp(-448, 448).to(torch.float8_e4m3fn)
+        qs.append(q)
+        ss.append(s)
+    qw = Q.QuantWeight([Q.QuantPart.from_fp8(q, s, "cuda") for q, s in zip(qs, ss)])
+    assert qw.v2 and qw.parts[0].kqt == (7 if mode == "block" else 6)
+    wref = torch.cat([_fp8_ref(q, s, q.shape[0], K) for q, s in zip(qs, ss)]).cuda()
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ wref.T
+    tol = 1e-2 * want.abs().max().item() + 1e-4
+    assert (Q.quant_linear(x, qw).float() - want).abs().max().item() < tol
+    ws, S = Q.quant_partial(x, qw)
+    assert (ws.view(S, M, qw.N).sum(0) - want).abs().max().item() < tol
+    deq = Q.dequantize(qw).float()
+    assert torch.allclose(deq, wref.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-6)
+    xp = torch.randn(100, K, device="cuda", dtype=torch.bfloat16)  # prefill path
+    wantp = xp.float() @ wref.T
+    assert (Q.quant_linear(xp, qw).float() - wantp).abs().max().item() < 1e-2 * wantp.abs().max().item() + 1e-4
+
+
+def test_fp8_checkpoint_native_vs_dequant(tmp_path):
+    """A compressed-tensors FP8 checkpoint (e4m3 weights + per-channel weight_scale)
+    loads natively (QuantWeight, ~half the bytes) and its logits match the same
+    checkpoint dequantised to bf16 at load."""
+    from safetensors.torch import save_file
+    import json
+
+    from hipserve.config import PRESETS, EngineConfig
+    from hipserve.ops import quant as Q
+    from hipserve.parallel.comm import TPGroup
+    from hipserve.weights.safetensors_loader import random_hf_tensors, save_hf_checkpoint
+
+    cfg = PRESETS["small-llama"]
+    t = random_hf_tensors(cfg, seed=3)
+    out = {}
+    for k, v in t.items():
+        if k.endswith("proj.weight") and "layers" in k:
+            s = v.abs().amax(1, keepdim=True) / 448.0
+            out[k] = (v / s).to(torch.float8_e4m3fn)
+            out[k[: -len("weight")] + "weight_scale"] = s.float()
+        else:
+            out[k] = v.to(torch.bfloat16)
+    d = str(tmp_path / "ckpt")
+    save_hf_checkpoint(d, cfg, {k: v for k, v in out.items()})
+    conf = json.load(open(d + "/config.json"))
+    conf["quantization_config"] = {"quant_method": "compressed-tensors", "config_groups": {"group_0": {
+        "weights": {"num_bits": 8, "type": "float", "strategy": "channel"},
+        "input_activations": {"num_bits": 8, "type": "float", "strategy": "token", "dynamic": True}}},
+        "ignore": ["lm_head"]}
+    json.dump(conf, open(d + "/config.json", "w"))
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.engine.request import SamplingParams
+    import hipserve.models.llama as L
+
+    got, qtypes = {}, {}
+    prompts = [[1, 5, 9, 200, 31, 7, 2], [1] + list(range(40, 90))]
+    for native in (True, False):
+        L.LlamaModel.native_fp8 = native
+        try:
+            eng = LLMEngine(EngineConfig(model=d, device="cuda", num_kv_blocks=64, max_model_len=256,
+                                         max_num_seqs=4, max_num_batched_tokens=256),
+                            tp=TPGroup(0, 1, None, torch.device("cuda", 0)))
+        finally:
+            L.LlamaModel.native_fp8 = True
+        m = eng.runner.model
+        qtypes[native] = isinstance(m.layers[0].wqkv, Q.QuantWeight)
+        orig = m.compute_logits
+
+        def cap(h, orig=orig, native=native):
+            out = orig(h)
+            got.setdefault(native, []).append(out.float().cpu().clone())
+            return out
+
+        m.compute_logits = cap
+        eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True))
+        eng.shutdown()
+    assert qtypes == {True: True, False: False}
+    a, b = torch.cat(got[True]), torch.cat(got[False])
+    assert (a - b).abs().max().item() < 5e-2 * b.abs().max().item() + 1e-3
+    assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.85

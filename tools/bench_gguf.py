@@ -64,22 +64,28 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[1, 16, 64])
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--splits", type=int, nargs="*", default=None)
+    ap.add_argument("--fp8", action="store_true", help="FP8 e4m3 per-channel weights of the same shapes")
     a = ap.parse_args()
     load_library()
     rng = np.random.default_rng(0)
     for name, specs in SHAPES.items():
         if a.only and name not in a.only:
             continue
-        raws = [(t, n, k, Q.random_blocks(rng, t, n, k)) for t, n, k in specs]
-        qw = Q.QuantWeight.from_raw(raws, "cuda")
-        del raws
+        if a.fp8:
+            parts = []
+            for _, n, k in specs:
+                w = torch.randn(n, k, device="cuda") * 0.02
+                sc = w.abs().amax(1, keepdim=True) / 448.0
+                parts.append(Q.QuantPart.from_fp8((w / sc).to(torch.float8_e4m3fn), sc, "cuda"))
+                del w
+            qw = Q.QuantWeight(parts)
+        else:
+            raws = [(t, n, k, Q.random_blocks(rng, t, n, k)) for t, n, k in specs]
+            qw = Q.QuantWeight.from_raw(raws, "cuda")
+            del raws
         for M in a.m:
             x = torch.randn(M, qw.K, device="cuda", dtype=torch.bfloat16)
             rows = []
-            qw.v2 = False
-            rows.append(("v1", None, _time(lambda: Q.quant_linear(x, qw))))
-            qw.v2 = True
-            rows.append(("v2", Q.v2_splits(qw, M), _time(lambda: Q.quant_linear(x, qw))))
             rows.append(("v2_partial", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw))))
             for S in a.splits or []:
                 def run(S=S):
