@@ -148,7 +148,10 @@ namespace hipserve {
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
                              bool renorm, hipStream_t s);
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
-                      int tiles_cap, int* num_tiles, int* pair_slot, hipStream_t s);
+                      int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s);
+// xs[slot, H] = x[slots[slot] / k] (zeros for padding slots): grouped-GEMM input rows
+void launch_moe_gather(void* out, const void* x, long x_stride, const int* slots, int nslots, int k, int H,
+                       hipStream_t s);
 void launch_moe_gemm(void* out, long out_stride, const void* x, long x_stride, const void* w, const int* slots,
                      const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, hipStream_t s);
 void launch_moe_combine(void* out, const void* y, const float* w, const int* pair_slot, int T, int k, int H,

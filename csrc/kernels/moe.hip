@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restri
 __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ ids, int npairs, int E, int tile,
                                                          int* __restrict__ slots, int slots_cap,
                                                          int* __restrict__ tile_expert, int tiles_cap,
-                                                         int* __restrict__ num_tiles, int* __restrict__ pair_slot) {
+                                                         int* __restrict__ num_tiles, int* __restrict__ pair_slot,
+                                                         int* __restrict__ group_end) {
   __shared__ int cnt[128], off[129], cur[128];
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 128) { cnt[tid] = 0; cur[tid] = 0; }
@@ -99,6 +100,10 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
     const int excl = incl - a - b;
     off[e0] = excl;
     off[e1] = excl + a;
+    if (group_end != nullptr) {  // per-expert end row of the padded expert-sorted slots (grouped GEMM offsets)
+      if (e0 < E) group_end[e0] = excl + a;
+      if (e1 < E) group_end[e1] = incl;
+    }
     if (lane == 63) {
       off[128] = incl;
       *num_tiles = incl / tile;
@@ -242,9 +247,36 @@ void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int*
 }
 
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
-                      int tiles_cap, int* num_tiles, int* pair_slot, hipStream_t s) {
+                      int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s) {
   moe_align_kernel<<<1, 1024, 0, s>>>(ids, npairs, E, tile, slots, slots_cap, tile_expert, tiles_cap, num_tiles,
-                                      pair_slot);
+                                      pair_slot, group_end);
+}
+
+// Prefill MoE input: xs[slot] = x[slots[slot] / k] (the token of the pair in that
+// slot), zero rows for padding slots — the A operand of the grouped expert GEMM.
+// One workgroup per 8 slots, 16-byte vectors.
+__global__ __launch_bounds__(256) void moe_gather_kernel(unsigned short* __restrict__ out,
+                                                         const unsigned short* __restrict__ x, long x_stride,
+                                                         const int* __restrict__ slots, int nslots, int k, int H) {
+  const int vpr = H >> 3;  // 16-byte vectors per row
+  const int slot = blockIdx.x * 8 + threadIdx.x / 32;
+  if (slot >= nslots) return;
+  const int p = slots[slot];
+  u16x8* dst = reinterpret_cast<u16x8*>(out + (long)slot * H);
+  if (p < 0) {
+    for (int v = threadIdx.x & 31; v < vpr; v += 32) dst[v] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    return;
+  }
+  const u16x8* src = reinterpret_cast<const u16x8*>(x + (long)(p / k) * x_stride);
+  for (int v = threadIdx.x & 31; v < vpr; v += 32) dst[v] = src[v];
+}
+
+void launch_moe_gather(void* out, const void* x, long x_stride, const int* slots, int nslots, int k, int H,
+                       hipStream_t s) {
+  if (nslots <= 0) return;
+  moe_gather_kernel<<<(nslots + 7) / 8, 256, 0, s>>>(static_cast<unsigned short*>(out),
+                                                     static_cast<const unsigned short*>(x), x_stride, slots, nslots,
+                                                     k, H);
 }
 
 template <int MT>

@@ -613,7 +613,7 @@ void pack_decode_weight(at::Tensor& out, const at::Tensor& w, bool glu) {
 }
 
 void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,
-               at::Tensor& num_tiles, at::Tensor& pair_slot) {
+               at::Tensor& num_tiles, at::Tensor& pair_slot, const c10::optional<at::Tensor>& group_end) {
   CHECK_DEV(ids);
   TORCH_CHECK(ids.scalar_type() == at::kInt && slots.scalar_type() == at::kInt &&
               tile_expert.scalar_type() == at::kInt && pair_slot.scalar_type() == at::kInt);
@@ -622,10 +622,25 @@ void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots
   TORCH_CHECK(slots.numel() >= npairs + E * (tile - 1) && slots.numel() % tile == 0,
               "slots capacity must cover padding and be a multiple of the tile");
   TORCH_CHECK(tile_expert.numel() * tile >= slots.numel() && pair_slot.numel() >= npairs);
+  int* ge = nullptr;
+  if (group_end.has_value() && group_end->numel() > 0) {
+    TORCH_CHECK(group_end->scalar_type() == at::kInt && group_end->numel() >= E && group_end->is_contiguous());
+    ge = group_end->data_ptr<int>();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(ids.device());
   hipserve::launch_moe_align(ids.data_ptr<int>(), npairs, E, tile, slots.data_ptr<int>(), slots.numel(),
                              tile_expert.data_ptr<int>(), tile_expert.numel(), num_tiles.data_ptr<int>(),
-                             pair_slot.data_ptr<int>(), cur_stream());
+                             pair_slot.data_ptr<int>(), ge, cur_stream());
+}
+
+void moe_gather(at::Tensor& out, const at::Tensor& x, const at::Tensor& slots, int64_t k) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_CONTIG(out);
+  TORCH_CHECK(slots.scalar_type() == at::kInt && slots.is_contiguous() && out.size(0) >= slots.numel());
+  const int H = out.size(1);
+  TORCH_CHECK(H % 8 == 0 && x.size(1) == H && x.stride(0) % 8 == 0, "moe_gather: H % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_moe_gather(out.data_ptr(), x.data_ptr(), x.stride(0), slots.data_ptr<int>(), slots.numel(), k, H,
+                              cur_stream());
 }
 
 void moe_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& slots,
@@ -709,7 +724,8 @@ void moe_combine_partial(at::Tensor& out, const at::Tensor& ws, const at::Tensor
 
 TORCH_LIBRARY(hipserve, m) {
   m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k, bool renorm=True) -> ()");
-  m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot) -> ()");
+  m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot, Tensor(e!)? group_end=None) -> ()");
+  m.def("moe_gather(Tensor(a!) out, Tensor x, Tensor slots, int k) -> ()");
   m.def("moe_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor w, Tensor pair_slot, int k) -> ()");
   m.def("moe_decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k, int N, int splits, bool packed, bool glu) -> ()");
@@ -783,6 +799,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
   m.impl("moe_align", &moe_align);
+  m.impl("moe_gather", &moe_gather);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
   m.impl("moe_decode_gemm", &moe_decode_gemm);

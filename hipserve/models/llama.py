@@ -595,6 +595,9 @@ class LlamaModel:
                 and (P <= MOE_KERNEL_MAX_PAIRS
                      or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts and self._moe_decode_ok(lw)))):
             return self.moe_hip(x, lw)
+        if self.ops.name == "hip" and hasattr(torch, "_grouped_mm") and cfg.num_experts <= 128 \
+                and cfg.hidden_size % 8 == 0 and self.inter % 8 == 0 and isinstance(lw.w13, torch.Tensor):
+            return self.moe_grouped(x, lw)
         logits = F.linear(x, lw.router).float()
         w, idx = torch.topk(torch.softmax(logits, dim=-1), k, dim=-1)
         if cfg.norm_topk_prob:
@@ -638,6 +641,44 @@ class LlamaModel:
             if ntiles * S * active >= 1024:
                 return S
         return opts[-1]
+
+    def moe_grouped(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
+        """Prefill-sized MoE without a host synchronisation: routing (top-k kernel),
+        expert-sorted 16-row-padded slots with per-expert end offsets (moe_align),
+        the token rows gathered into that order (moe_gather), the two expert GEMMs
+        as hipBLASLt grouped GEMMs over the device-side offsets (``torch._grouped_mm``
+        — one launch per projection for all experts, no per-expert launch loop), the
+        SiLU-GLU between them and the weighted combine (moe_combine). Replaces the
+        argsort / bincount(.tolist()) / index_add torch loop of round 1 (Mixtral
+        prefill step 234 -> 191 ms, profiles/r2_mixtral_grouped_moe_trace.md). The one
+        host round trip left is inside torch._grouped_mm, which reads the group
+        offsets on the host on this ROCm build (not graph-capturable; prefill runs
+        eager, decode uses moe_hip)."""
+        op = torch.ops.hipserve
+        cfg = self.cfg
+        E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
+        T, dev = x.shape[0], x.device
+        P, tile = T * k, 16
+        cap = -(-(P + E * (tile - 1)) // tile) * tile
+        logits = gemm.linear(x, lw.router)
+        w = torch.empty(T, k, dtype=torch.float32, device=dev)
+        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
+        op.moe_topk_softmax(w, ids, logits, k, cfg.norm_topk_prob)
+        slots = torch.empty(cap, dtype=torch.int32, device=dev)
+        tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
+        ntiles = torch.empty(1, dtype=torch.int32, device=dev)
+        pair_slot = torch.empty(P, dtype=torch.int32, device=dev)
+        ends = torch.empty(E, dtype=torch.int32, device=dev)
+        op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
+        xs = torch.empty(cap, H, dtype=x.dtype, device=dev)
+        op.moe_gather(xs, x, slots, k)
+        gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
+        act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+        self.ops.silu_and_mul(act, gu)
+        y = torch._grouped_mm(act, lw.w2.transpose(1, 2), offs=ends)
+        out = torch.empty(T, H, dtype=x.dtype, device=dev)
+        op.moe_combine(out, y, w, pair_slot, k)
+        return out
 
     def moe_hip(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Graph-capturable MoE on the gfx950 kernels (decode-sized batches): top-k
