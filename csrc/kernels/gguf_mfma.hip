@@ -40,7 +40,9 @@ namespace {
 
 // GGUF block formats + FP8 e4m3 weights (per-row scale; FP8B adds 128 x 128 block
 // scales, the block-FP8 checkpoints)
-enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5, FP8 = 6, FP8B = 7 };
+// INT8: unsigned 8-bit weights (compressed-tensors pack-quantized / AWQ 8-bit) with
+// a group scale and zero point per half lane-quarter (32 k): w = (u - 128 - zp) * s
+enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5, FP8 = 6, FP8B = 7, INT8 = 8 };
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -92,10 +94,11 @@ struct Raw {
 //   Q4_1  Q4_0 + [16 rows x 8 m]                                    2560 B
 //   FP8   [4 x 64 lanes x 16 q]                                     4096 B
 //   FP8B  FP8 + [16 rows x 2 f32 block scales]                      4224 B
+//   INT8  [4 x 64 lanes x 16 u8][16 rows x 4 g x 2 halves x (f16 scale, f16 offset)]  4608 B
 template <int QT>
 constexpr int chunk_bytes() {
   return QT == Q4_K ? 2304 : QT == Q5_K ? 2816 : QT == Q6_K ? 3360 : QT == Q8_0 ? 4352 : QT == Q4_0 ? 2304
-       : QT == Q4_1 ? 2560 : QT == FP8 ? 4096 : 4224;
+       : QT == Q4_1 ? 2560 : QT == FP8 ? 4096 : QT == FP8B ? 4224 : 4608;
 }
 
 struct Part {
@@ -134,6 +137,12 @@ HS_DEVICE void load_raw(const unsigned char* ch, int g, int c, int lane, Raw& r)
     r.s2[0] = sc.x;
     r.s2[1] = sc.y;
     r.h[0] = *reinterpret_cast<const unsigned short*>(ch + 3328 + 2 * c);
+  } else if constexpr (QT == INT8) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = ld16(ch + 1024 * i + 16 * lane);
+    const uint2 so = *reinterpret_cast<const uint2*>(ch + 4096 + 32 * c + 8 * g);  // (sA, oA), (sB, oB)
+    r.s2[0] = so.x;
+    r.s2[1] = so.y;
   } else if constexpr (QT == FP8 || QT == FP8B) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.v[i] = ld16(ch + 1024 * i + 16 * lane);
@@ -211,6 +220,11 @@ struct Dec {
       d6 = h2f(r.h[0]);
     } else if constexpr (QT == FP8 || QT == FP8B) {
       fdA = fdB = QT == FP8B ? __builtin_bit_cast(float, r.s2[0]) : 1.f;
+    } else if constexpr (QT == INT8) {  // c = offset (-1024 - 128 - zp), applied before the scale
+      fdA = h2f(r.s2[0] & 0xFFFF);
+      fcA = h2f(r.s2[0] >> 16);
+      fdB = h2f(r.s2[1] & 0xFFFF);
+      fcB = h2f(r.s2[1] >> 16);
     } else {
       fdA = h2f(r.h[0]);
       fdB = h2f(r.h[1]);
@@ -231,6 +245,9 @@ struct Dec {
       // of the lane's scale word (s >> 2)
       d = d6 * (float)(signed char)((r.s2[s >> 2] >> (8 * (2 * (g & 1) + ((s & 3) >> 1)))) & 0xFF);
       c = 0.f;
+    } else if constexpr (QT == INT8) {
+      d = s < 4 ? fdA : fdB;
+      c = 0.f;
     } else if constexpr (QT == Q4_K || QT == Q5_K || QT == Q8_0) {
       d = s < 4 ? fdA : fdB;
       c = s < 4 ? fcA : fcB;
@@ -241,6 +258,14 @@ struct Dec {
   }
 
   HS_DEVICE f16x8 ints(const Raw& r, int g, int s) const {
+    if constexpr (QT == INT8) {  // u - 128 - zp, exact
+      const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+      const unsigned wa = qv[s >> 1][2 * (s & 1)], wb = qv[s >> 1][2 * (s & 1) + 1];
+      const h2 cc = s < 4 ? cA : cB;
+      const unsigned p0 = (wa & 0x00FF00FFu) | kMagic, p1 = ((wa >> 8) & 0x00FF00FFu) | kMagic;
+      const unsigned p2 = (wb & 0x00FF00FFu) | kMagic, p3 = ((wb >> 8) & 0x00FF00FFu) | kMagic;
+      return frag(as_h2(p0) + cc, as_h2(p1) + cc, as_h2(p2) + cc, as_h2(p3) + cc);
+    }
     if constexpr (QT == FP8 || QT == FP8B) {
       // e4m3 -> f16 by moving bits: sign to bit 15, exponent + mantissa to bits 7-13
       // gives the value / 256 exactly (normals and subnormals; the 256 is folded into
@@ -307,6 +332,14 @@ struct Dec {
   }
 
   HS_DEVICE f16x8 step(const Raw& r, int g, int s) const {
+    if constexpr (QT == INT8) {  // (1024 + u + off) * s: exact integer, one rounding
+      const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+      const unsigned wa = qv[s >> 1][2 * (s & 1)], wb = qv[s >> 1][2 * (s & 1) + 1];
+      const h2 dd = s < 4 ? dA : dB, cc = s < 4 ? cA : cB;
+      const unsigned p0 = (wa & 0x00FF00FFu) | kMagic, p1 = ((wa >> 8) & 0x00FF00FFu) | kMagic;
+      const unsigned p2 = (wb & 0x00FF00FFu) | kMagic, p3 = ((wb >> 8) & 0x00FF00FFu) | kMagic;
+      return frag((as_h2(p0) + cc) * dd, (as_h2(p1) + cc) * dd, (as_h2(p2) + cc) * dd, (as_h2(p3) + cc) * dd);
+    }
     const f16x8 q = ints(r, g, s);
     if constexpr (QT == FP8) return q;  // row scale in the epilogue
     if constexpr (QT == FP8B) {
@@ -554,6 +587,7 @@ int gguf_tiled_chunk_bytes(int qtype) {
     case Q6_K: return chunk_bytes<Q6_K>();
     case FP8: return chunk_bytes<FP8>();
     case FP8B: return chunk_bytes<FP8B>();
+    case INT8: return chunk_bytes<INT8>();
   }
   return 0;
 }
@@ -602,6 +636,7 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
       case Q6_K: launch_t<Q6_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
       case FP8: launch_t<FP8, FP8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
       case FP8B: launch_t<FP8B, FP8B>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case INT8: launch_t<INT8, INT8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
     }
   }
 }
@@ -620,6 +655,7 @@ void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qt
     case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
     case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
     case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case INT8: dequant_tiled_kernel<INT8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
   }
 }
 

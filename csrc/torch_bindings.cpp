@@ -214,8 +214,8 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   const int S = (nsb + per - 1) / per;
   hipserve::GgufPart P[4];
   for (int i = 0; i < np; ++i) {
-    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 7, "gguf_gemm_parts: kernel qtype 0-7");
-    const bool fp8 = qtypes[i] >= 6;
+    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 8, "gguf_gemm_parts: kernel qtype 0-8");
+    const bool fp8 = qtypes[i] == 6 || qtypes[i] == 7;
     TORCH_CHECK(!fp8 || (rss[i].scalar_type() == at::kFloat && rss[i].is_contiguous() && rss[i].numel() == rows[i] &&
                          rss[i].device() == x.device()), "FP8 parts need an fp32 row scale per row");
     TORCH_CHECK(qs[i].scalar_type() == at::kByte && qs[i].is_contiguous() && qs[i].device() == x.device());
@@ -247,11 +247,12 @@ void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& 
                         int64_t K) {
   CHECK_DEV(q); CHECK_BF16(out);
   TORCH_CHECK(out.is_contiguous() && out.numel() >= N * K && N % 16 == 0 && K % 256 == 0);
-  TORCH_CHECK(qtype >= 0 && qtype <= 7 && q.scalar_type() == at::kByte && q.is_contiguous());
+  TORCH_CHECK(qtype >= 0 && qtype <= 8 && q.scalar_type() == at::kByte && q.is_contiguous());
   TORCH_CHECK(q.numel() == N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype), "not a tiled tensor");
-  TORCH_CHECK(qtype < 6 || (rs.scalar_type() == at::kFloat && rs.numel() == N), "FP8 needs an fp32 row scale");
+  const bool fp8 = qtype == 6 || qtype == 7;
+  TORCH_CHECK(!fp8 || (rs.scalar_type() == at::kFloat && rs.numel() == N), "FP8 needs an fp32 row scale");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
-  hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), qtype >= 6 ? rs.data_ptr<float>() : nullptr,
+  hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), fp8 ? rs.data_ptr<float>() : nullptr,
                                       qtype, N, K, cur_stream());
 }
 

@@ -24,7 +24,10 @@ from ..weights import gguf as G
 # FP8 e4m3 weights (compressed-tensors "FP8-Dynamic" per-channel / per-tensor scales,
 # and 128 x 128 block-scaled FP8) share the v2 kernel: pseudo type ids beside ggml's
 FP8, FP8B = 1000, 1001
-KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7}
+# 8-bit integer weight-only (compressed-tensors pack-quantized 8-bit / AWQ 8-bit):
+# unsigned bytes u = q + 128, per-group scale and zero point
+INT8 = 1002
+KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7, INT8: 8}
 MAX_FUSED_M = 64
 
 
@@ -58,7 +61,7 @@ def repack(raw: np.ndarray, qtype: int, N: int, K: int):
 
 
 CHUNK_BYTES = {G.Q4_K: 2304, G.Q5_K: 2816, G.Q6_K: 3360, G.Q8_0: 4352, G.Q4_0: 2304, G.Q4_1: 2560,
-               FP8: 4096, FP8B: 4224}
+               FP8: 4096, FP8B: 4224, INT8: 4608}
 
 
 def _lanes(a: np.ndarray, n_ld: int) -> np.ndarray:
@@ -118,6 +121,32 @@ class QuantPart:
         self.q, self.d, self.m, self.row_bytes = q, d, m, row_bytes
         self.tiled = tiled
         self.rs = rs if rs is not None else torch.empty(0, dtype=torch.float32, device=q.device)
+
+    @classmethod
+    def from_int8(cls, u: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor | None, device):
+        """8-bit weight-only matrix: ``u`` [N, K] unsigned bytes holding q + 128 (the
+        compressed-tensors pack-quantized convention), ``scale`` [N, K / group] or
+        [N, 1] (per channel), optional signed ``zero_point`` of the same shape:
+        w = (u - 128 - zp) * scale. Groups of >= 32 k; N % 16 == 0, K % 256 == 0."""
+        N, K = u.shape
+        u = u.to(device=device, dtype=torch.uint8)
+        sc = scale.to(device=device, dtype=torch.float32).reshape(N, -1)
+        ng = sc.shape[1]
+        G = K // ng
+        if G * ng != K or G < 32 or G % 32:
+            raise ValueError(f"int8 group size {K}/{ng} not supported (needs a multiple of 32)")
+        zp = (zero_point.to(device=device, dtype=torch.float32).reshape(N, -1) if zero_point is not None
+              else torch.zeros_like(sc))
+        R, nsb = N // 16, K // 256
+        lanes = u.reshape(R, 16, nsb, 4, 4, 16).permute(0, 2, 4, 3, 1, 5).reshape(R, nsb, 4096)
+        # (scale, offset = -(1024 + 128 + zp)) per (row, super-chunk, lane quarter g, half h): k0 = 256 sb + 64 g + 32 h
+        k0 = torch.arange(nsb * 8, device=device) * 32                 # [nsb * 4 * 2] in (sb, g, h) order
+        gi = k0 // G
+        s16 = sc[:, gi].to(torch.float16)                              # [N, nsb*8]
+        o16 = (-(1152.0 + zp[:, gi])).to(torch.float16)
+        meta = torch.stack([s16, o16], -1).reshape(R, 16, nsb, 8, 2).permute(0, 2, 1, 3, 4).contiguous()
+        chunk = torch.cat([lanes, meta.view(torch.uint8).reshape(R, nsb, 512)], 2).contiguous()
+        return cls(INT8, N, K, chunk, _E16(device), _E16(device), 0, tiled=True)
 
     @classmethod
     def from_fp8(cls, q: torch.Tensor, scale: torch.Tensor, device):

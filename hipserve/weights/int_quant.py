@@ -17,10 +17,12 @@ compressed-tensors ``pack-quantized`` format. Two on-disk layouts are read:
   [K / group, N]; eight nibbles per int32 in AWQ's interleaved column order
   (0, 2, 4, 6, 1, 3, 5, 7). w^T = (q - z) * s.
 
-On MI355X the dequantised bf16 weights stream through the same packed decode GEMM
-as native bf16 checkpoints; 288 GB of HBM per GPU holds a 30B-A3B model in bf16
-several times over, so the int8 storage buys nothing at serve time — the format is
-a download/storage format here. (GGUF is the in-kernel quantised path: gguf.hip.)
+On the GPU, 8-bit pack-quantized dense projections are NOT dequantised: the loader
+(safetensors_loader.py ``int8_part``) keeps the bytes, group scales and zero points
+and the v2 quantised decode GEMM (csrc/kernels/gguf_mfma.hip, INT8 format) dequantises
+in registers — half the bf16 bytes per decode step. 4-bit layouts, AutoAWQ and MoE
+expert weights are dequantised here to bf16 at load (288 GB of HBM holds a 30B-A3B
+model in bf16 several times over).
 """
 from __future__ import annotations
 

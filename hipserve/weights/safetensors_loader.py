@@ -114,6 +114,37 @@ class _Ckpt:
         b0, b1 = start // 128, -(-stop // 128)
         return q, (sc[b0:b1] if axis == 0 else sc[:, b0:b1])
 
+    # ---- native 8-bit integer weight-only (compressed-tensors pack-quantized, 8 bits)
+    def is_int8_ct(self, name) -> bool:
+        return self.bits == 8 and self.virtual.get(name, (None,))[0] == "ct"
+
+    def int8_part(self, name, axis: int, start: int, stop: int):
+        """(unsigned bytes q + 128 [rows, cols], scale, zero point or None) of rows /
+        columns [start, stop); None when a column slice would split a group."""
+        from . import int_quant
+
+        base = self.virtual[name][1]
+        packed = self._get(base + ".weight_packed")
+        scale = self._get(base + ".weight_scale").float()
+        zp = self._get(base + ".weight_zero_point")
+        shp = self._get(base + ".weight_shape")
+        N = packed.shape[0]
+        K = int(shp.reshape(-1)[1]) if shp is not None else packed.shape[1] * 4
+        u = int_quant._unpack_rows(packed, 8, K).to(torch.uint8)
+        if scale.dim() == 1:
+            scale = scale.reshape(-1, 1)
+        if zp is not None:
+            if zp.dtype == torch.int32 and zp.shape[0] != N:  # packed along N
+                zp = (int_quant._unpack_rows(zp.t().contiguous(), 8, N) - 128).t()
+            zp = zp.float().reshape(N, -1)
+        if axis == 0:
+            return u[start:stop], scale[start:stop], (zp[start:stop] if zp is not None else None)
+        G = K // scale.shape[1]
+        if scale.shape[1] > 1 and (start % G or stop % G):
+            return None
+        cs = slice(start // G, stop // G) if scale.shape[1] > 1 else slice(0, 1)
+        return u[:, start:stop], scale[:, cs], (zp[:, cs] if zp is not None else None)
+
     def _is_fp8(self, name) -> bool:
         """True for every tensor that must be dequantised whole before slicing."""
         if name in self.virtual:
@@ -190,9 +221,10 @@ def load_hf_weights(model: LlamaModel, model_path: str):
     def to(t):
         return t.to(device=dev, dtype=dt).contiguous()
 
-    # native FP8 projections (the FP8-Dynamic / block-FP8 checkpoints): kept as e4m3
-    # in HBM and multiplied by the v2 dequant-MFMA kernel (ops/quant.py), half the
-    # bytes of the bf16 weights
+    # native FP8 projections (the FP8-Dynamic / block-FP8 checkpoints, e4m3 + scales)
+    # and 8-bit integer weight-only projections (compressed-tensors pack-quantized,
+    # the reference's AWQ-8bit export) stay quantised in HBM and are multiplied by
+    # the v2 dequant-MFMA kernel (ops/quant.py): half the bytes of bf16 weights
     native_fp8 = dev.type == "cuda" and getattr(model, "native_fp8", True)
     n_fp8 = [0]
 
@@ -206,6 +238,15 @@ def load_hf_weights(model: LlamaModel, model_path: str):
                     pp[0].shape[0] % 16 == 0 and pp[0].shape[1] % 256 == 0 for pp in parts):
                 n_fp8[0] += 1
                 return Q.QuantWeight([Q.QuantPart.from_fp8(qq, sc, dev) for qq, sc in parts])
+        if native_fp8 and all(ck.is_int8_ct(n) for n, *_ in specs):
+            from ..ops import quant as Q
+
+            parts = [ck.int8_part(n, ax, a, b) for n, ax, a, b in specs]
+            if all(pp is not None for pp in parts) and all(
+                    pp[0].shape[0] % 16 == 0 and pp[0].shape[1] % 256 == 0
+                    and (pp[0].shape[1] // pp[1].shape[1]) % 32 == 0 for pp in parts):
+                n_fp8[0] += 1
+                return Q.QuantWeight([Q.QuantPart.from_int8(u, sc, zp, dev) for u, sc, zp in parts])
         ts = [ck.rows(n, a, b) if ax == 0 else ck.cols(n, a, b) for n, ax, a, b in specs]
         return to(torch.cat(ts, 0) if len(ts) > 1 else ts[0])
 

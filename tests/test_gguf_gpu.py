@@ -301,3 +301,80 @@ def test_fp8_checkpoint_native_vs_dequant(tmp_path):
     a, b = torch.cat(got[True]), torch.cat(got[False])
     assert (a - b).abs().max().item() < 5e-2 * b.abs().max().item() + 1e-3
     assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.85
+
+
+# ---------------------------------------------------------------- INT8 weight-only
+@pytest.mark.parametrize("group", [32, 128, 0])
+@pytest.mark.parametrize("asym", [False, True])
+@pytest.mark.parametrize("M", [1, 24, 64])
+def test_int8_linear_matches_fp32(group, asym, M):
+    """8-bit weight-only (pack-quantized convention: bytes q + 128, group scale, zero
+    point) in the v2 kernel vs an fp32 matmul of (q - zp) * s; group 0 = per channel."""
+    from hipserve.ops import quant as Q
+    torch.manual_seed(M + group)
+    N, K = 272, 1024
+    G = group or K
+    q = torch.randint(-128, 128, (N, K))
+    scale = torch.rand(N, K // G) * 2e-3 + 1e-4
+    zp = torch.randint(-8, 8, (N, K // G)) if asym else None
+    qw = Q.QuantWeight([Q.QuantPart.from_int8((q + 128).to(torch.uint8), scale, zp, "cuda")])
+    assert qw.v2 and qw.parts[0].kqt == 8
+    wref = ((q - (zp.repeat_interleave(G, 1) if asym else 0)).float() * scale.repeat_interleave(G, 1)).cuda()
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ wref.T
+    tol = 1e-2 * want.abs().max().item() + 1e-4
+    assert (Q.quant_linear(x, qw).float() - want).abs().max().item() < tol
+    deq = Q.dequantize(qw).float()
+    assert torch.allclose(deq, wref.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-6)
+
+
+def test_int8_pack_quantized_checkpoint_native(tmp_path):
+    """A compressed-tensors pack-quantized 8-bit checkpoint loads natively (INT8
+    QuantWeights, in-register dequant) and its logits match the same checkpoint
+    dequantised to bf16 at load."""
+    transformers = pytest.importorskip("transformers")
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("tiq", os.path.join(os.path.dirname(__file__), "test_int_quant.py"))
+    tiq = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tiq)
+    from hipserve.config import EngineConfig
+    from hipserve.engine.llm_engine import LLMEngine
+    from hipserve.engine.request import SamplingParams
+    from hipserve.ops import quant as Q
+    from hipserve.parallel.comm import TPGroup
+    import hipserve.models.llama as L
+
+    cfg = transformers.LlamaConfig(hidden_size=256, num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
+                                   head_dim=64, intermediate_size=512, vocab_size=320, max_position_embeddings=512,
+                                   rms_norm_eps=1e-6, tie_word_embeddings=False)
+    torch.manual_seed(11)
+    m = transformers.AutoModelForCausalLM.from_config(cfg, dtype=torch.float32).eval()
+    path = tmp_path / "llama-int8"
+    tiq._quantise_ckpt(m, path, "ct", bits=8, group=32)
+    got = {}
+    prompts = [[1, 5, 9, 33, 70, 100], list(range(3, 60))]
+    for native in (True, False):
+        L.LlamaModel.native_fp8 = native
+        try:
+            eng = LLMEngine(EngineConfig(model=str(path), device="cuda", max_num_seqs=2, max_num_batched_tokens=128,
+                                         num_kv_blocks=64, max_model_len=256),
+                            tp=TPGroup(0, 1, None, torch.device("cuda", 0)))
+        finally:
+            L.LlamaModel.native_fp8 = True
+        mm = eng.runner.model
+        assert isinstance(mm.layers[0].wqkv, Q.QuantWeight) == native
+        if native:
+            assert mm.layers[0].wqkv.parts[0].kqt == 8
+        orig = mm.compute_logits
+
+        def cap(h, orig=orig, native=native):
+            out = orig(h)
+            got.setdefault(native, []).append(out.float().cpu().clone())
+            return out
+
+        mm.compute_logits = cap
+        eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True))
+        eng.shutdown()
+    a, b = torch.cat(got[True]), torch.cat(got[False])
+    assert (a - b).abs().max().item() < 5e-2 * b.abs().max().item() + 1e-3

@@ -519,6 +519,7 @@ def test_moe_grouped_prefill_vs_fp32(ops, T, E, k, norm):
     calls = []
     orig = m.moe_grouped
     m.moe_grouped = lambda *a_: calls.append(1) or orig(*a_)
-    x_big = torch.randn(4096, H, device=DEV, dtype=torch.bfloat16)
+    from hipserve.models.llama import MOE_KERNEL_MAX_ROWS_PER_EXPERT
+    x_big = torch.randn(MOE_KERNEL_MAX_ROWS_PER_EXPERT * E // k + 64, H, device=DEV, dtype=torch.bfloat16)
     m.moe(x_big, lw)
     assert calls, "prefill-sized MoE did not take the grouped path"
