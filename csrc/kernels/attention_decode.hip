@@ -30,8 +30,10 @@ constexpr int kDecWavesMax = 8;
 constexpr int kChunk = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 
+// two register sets for the chunk pipeline: keep VGPR + AGPR <= 256 so two waves fit
+// per SIMD (two 4-wave workgroups per CU — B = 64 x 8 kv heads is 2 per CU)
 template <int D, int kDecWaves>
-__global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
+__global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(2, 8))) void paged_decode_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const unsigned short* __restrict__ q, long q_stride,
     const unsigned short* __restrict__ k_cache,
@@ -90,9 +92,17 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
   const int last_tok = ctx - 1;
   const int bt_base_tok = first_blk * block_size;
 
-  for (int c = wave; c < nchunks; c += kDecWaves) {
-    const int cs = start + c * kChunk;
-    // ---- K loads: tile a row m -> token 8*(m>>2) + (m&3); tile b -> +4
+  // Software pipeline over this wave's chunks (wave, wave + W, ...): the K / V
+  // loads of the next chunk are issued before the current chunk's MFMAs, from two
+  // register sets used alternately (loop unrolled by 2, no exit inside a pair, loads
+  // unconditional with the chunk index clamped), so each chunk's HBM latency hides
+  // behind the previous chunk's math instead of being exposed once per chunk.
+  struct Chunk {
+    u16x8 ka[KS], kb[KS], vv[NB];
+  };
+  auto load_chunk = [&](int c, Chunk& ch) {
+    const int cs = start + min(c, nchunks - 1) * kChunk;
+    // K: tile a row m -> token 8*(m>>2) + (m&3); tile b -> +4
     const int m = col;
     int ta = cs + 8 * (m >> 2) + (m & 3);
     int tb = ta + 4;
@@ -104,41 +114,40 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
     const unsigned short* kb = k_cache +
         ((long)bt[(tb - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
         (long)(tb % block_size) * D + 8 * grp;
-    u16x8 kav[KS], kbv[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      kav[ks] = *reinterpret_cast<const u16x8*>(ka + 32 * ks);
-      kbv[ks] = *reinterpret_cast<const u16x8*>(kb + 32 * ks);
+      ch.ka[ks] = *reinterpret_cast<const u16x8*>(ka + 32 * ks);
+      ch.kb[ks] = *reinterpret_cast<const u16x8*>(kb + 32 * ks);
     }
-    // ---- V loads: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
+    // V: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
     int tv = cs + 8 * grp;
     if (tv > last_tok) tv = last_tok & ~7;
     const unsigned short* vb = v_cache +
         ((long)bt[(tv - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
         (tv % block_size) + (long)col * block_size;
-    u16x8 vv[NB];
 #pragma unroll
-    for (int n = 0; n < NB; ++n)
-      vv[n] = *reinterpret_cast<const u16x8*>(vb + (long)16 * n * block_size);
-
+    for (int n = 0; n < NB; ++n) ch.vv[n] = *reinterpret_cast<const u16x8*>(vb + (long)16 * n * block_size);
+  };
+  auto compute_chunk = [&](int c, const Chunk& ch) {
+    const int cs = start + c * kChunk;
     // ---- S^T = K . Q^T
     f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kav[ks]), qf[ks], sa, 0, 0, 0);
-      sb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kbv[ks]), qf[ks], sb, 0, 0, 0);
+      sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ch.ka[ks]), qf[ks], sa, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ch.kb[ks]), qf[ks], sb, 0, 0, 0);
     }
     // lane holds scores of tokens cs + 8*grp + r (sa) and + 4 + r (sb) for head col
-    float s[8];
+    float sc[8];
     float mx = -1e30f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int t0 = cs + 8 * grp + r;
-      s[r] = (t0 >= lo && t0 <= last_tok) ? sa[r] * sl2 : -1e30f;
-      s[r + 4] = (t0 + 4 >= lo && t0 + 4 <= last_tok) ? sb[r] * sl2 : -1e30f;
+      sc[r] = (t0 >= lo && t0 <= last_tok) ? sa[r] * sl2 : -1e30f;
+      sc[r + 4] = (t0 + 4 >= lo && t0 + 4 <= last_tok) ? sb[r] * sl2 : -1e30f;
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) mx = fmaxf(mx, s[r]);
+    for (int r = 0; r < 8; ++r) mx = fmaxf(mx, sc[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
@@ -148,9 +157,9 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
     bf16x8 pf;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const float p = exp2f(s[r] - m_new);
-      psum += p;
-      pf[r] = static_cast<__bf16>(p);
+      const float pr = exp2f(sc[r] - m_new);
+      psum += pr;
+      pf[r] = static_cast<__bf16>(pr);
     }
     l_run = l_run * alpha + psum;
     // rescale O: rows of the PV output are heads 4*grp + r
@@ -163,7 +172,22 @@ __global__ __launch_bounds__(64 * kDecWaves) void paged_decode_kernel(
     // ---- O += P . V
 #pragma unroll
     for (int n = 0; n < NB; ++n)
-      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vv[n]), o[n], 0, 0, 0);
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, ch.vv[n]), o[n], 0, 0, 0);
+  };
+  constexpr int W = kDecWaves;
+  int c = wave;
+  if (c < nchunks) {
+    Chunk A, B;
+    load_chunk(c, A);
+    for (; c + W < nchunks; c += 2 * W) {
+      load_chunk(c + W, B);
+      __builtin_amdgcn_sched_barrier(0);
+      compute_chunk(c, A);
+      load_chunk(c + 2 * W, A);
+      __builtin_amdgcn_sched_barrier(0);
+      compute_chunk(c + W, B);
+    }
+    if (c < nchunks) compute_chunk(c, A);
   }
 
   // ---- per-wave row sums, then merge the 4 waves through LDS

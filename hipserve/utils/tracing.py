@@ -13,6 +13,10 @@ chosen once from the environment at engine construction (zero cost when off):
 ``HIPSERVE_PROFILE=torch:<dir>[:<first>-<last>]``
     ``torch.profiler`` (CPU + HIP activities) over engine steps first..last
     (default 20-40), exported as a Chrome trace ``<dir>/hipserve_steps_<pid>.json``.
+``HIPSERVE_PROFILE=timing``
+    host wall time per engine phase accumulated in ``Tracer.times`` (name ->
+    [calls, seconds]); ``tools/decode_gap.py`` uses it to split a decode step into
+    host phases vs device time.
 ``HIPSERVE_STEP_LOG=<path>``
     one JSON line per engine step: step index, kind (prefill / mixed / decode),
     scheduled tokens and sequences, wall milliseconds, KV-pool usage, queue depths.
@@ -56,6 +60,23 @@ class _Range:
         return False
 
 
+class _Timed:
+    __slots__ = ("acc", "name", "t0")
+
+    def __init__(self, acc, name):
+        self.acc, self.name = acc, name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        a = self.acc.setdefault(self.name, [0, 0.0])
+        a[0] += 1
+        a[1] += time.perf_counter() - self.t0
+        return False
+
+
 class Tracer:
     """Per-engine tracer. ``phase(name)`` is a context manager; ``step_done``
     is called once per engine step with its scheduling summary."""
@@ -69,6 +90,7 @@ class Tracer:
         self.step = 0
         self._log = None
         self._lock = threading.Lock()
+        self.times: dict | None = {} if self.mode == "timing" else None
         if self.mode == "ranges":
             self.ranges = _roctx()
         elif self.mode.startswith("torch:"):
@@ -91,6 +113,8 @@ class Tracer:
         return bool(self.ranges or self.prof_dir or self._log)
 
     def phase(self, name: str):
+        if self.times is not None:
+            return _Timed(self.times, name)
         if self.ranges is None:
             return _NULL
         return _Range(self.ranges[0], self.ranges[1], name)
