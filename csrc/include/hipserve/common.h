@@ -133,6 +133,14 @@ HS_DEVICE int xcd_remap(int bid, int nwg) {
 // S = 8. Slices past S re-read slice S-1 (a cache hit, discarded).
 constexpr int kSliceBatch = 8;
 
+// RoPE rotation of the pair (a, b) by (c, s) with a FIXED rounding sequence (one
+// explicit FMA each, never left to -ffp-contract): every kernel that rotates q / k
+// (rope_cache, splitk_rope_cache, the fused decode attention) agrees bit for bit.
+HS_DEVICE void rope_rot(float a, float b, float c, float s, float& ra, float& rb) {
+  ra = __builtin_fmaf(a, c, -(b * s));
+  rb = __builtin_fmaf(b, c, a * s);
+}
+
 HS_DEVICE void sum_slices8(f32x4& lo, f32x4& hi, const float* __restrict__ p, long slice, int S) {
   for (int s0 = 0; s0 < S; s0 += kSliceBatch) {
     f32x4 a[kSliceBatch], b[kSliceBatch];

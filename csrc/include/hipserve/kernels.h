@@ -29,6 +29,12 @@ void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
 
 // attention_decode.hip
 size_t paged_decode_smem_bytes(int D);
+// fused decode: qkv split-K partials [S, B, N] -> RoPE(q, k) + KV write + attention
+void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S, int N, const long* positions,
+                             const long* slots, const float* cos_sin, int mode, void* k_cache, void* v_cache,
+                             const int* block_tables, int bt_stride, const int* context_lens, float* tmp_out,
+                             float* tmp_ml, int B, int nq, int nkv, int D, int block_size, int part_size,
+                             int max_parts, float scale, int window, hipStream_t s);
 void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
                          const void* k_cache, const void* v_cache,
                          const int* block_tables, int bt_stride,

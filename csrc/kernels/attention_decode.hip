@@ -30,9 +30,37 @@ constexpr int kDecWavesMax = 8;
 constexpr int kChunk = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 
+// Fused decode input (kQKV): the qkv projection's fp32 split-K partials instead of a
+// bf16 q row. The kernel sums them, applies RoPE to q (and to the new token's k),
+// writes the new token's k / v into the paged cache and attends — replacing the
+// separate splitk_rope_cache launch of the fused decode layer. Rounding matches that
+// kernel exactly (bf16 after the sum, bf16 after RoPE).
+struct QkvIn {
+  const float* ws;        // partials [S, B, N], N = (nq + 2 nkv) * D
+  long slice;             // B * N
+  int S, N;
+  const long* positions;  // [B]
+  const long* slots;      // [B], -1 = padding row (no cache write)
+  const float* cos_sin;   // [max_pos, D]: cos in [0, D/2), sin in [D/2, D)
+  unsigned short* k_cache;
+  unsigned short* v_cache;
+  int mode;               // 0 = rotate-half (HF), 1 = interleaved pairs (GGUF llama)
+};
+
+// 8 consecutive partial sums over the S slices, rounded to bf16 (as splitk_rope_cache)
+HS_DEVICE void qkv_sum8(float (&o)[8], const float* p, long slice, int S) {
+  f32x4 lo, hi;
+  sum_slices8(lo, hi, p, slice, S);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = bf16_to_f32(f32_to_bf16(lo[j]));
+    o[j + 4] = bf16_to_f32(f32_to_bf16(hi[j]));
+  }
+}
+
 // two register sets for the chunk pipeline: keep VGPR + AGPR <= 256 so two waves fit
 // per SIMD (two 4-wave workgroups per CU — B = 64 x 8 kv heads is 2 per CU)
-template <int D, int kDecWaves>
+template <int D, int kDecWaves, bool kQKV = false>
 __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(2, 8))) void paged_decode_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const unsigned short* __restrict__ q, long q_stride,
@@ -41,7 +69,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int nq, int nkv, int block_size, int part_size,
-    int max_parts, float scale, int window) {
+    int max_parts, float scale, int window, QkvIn qi = QkvIn{}) {
   static_assert(D == 128 || D == 96 || D == 64, "head_dim 64, 96 or 128");
   constexpr int KS = D / 32;  // k-steps of the QK MFMA
   constexpr int NB = D / 16;  // 16-column blocks of the PV output
@@ -71,7 +99,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
 
   // Q fragment: B[k = d][n = head]; lane holds head `col`, d = 8*grp + 32*ks + j
   bf16x8 qf[KS];
-  {
+  if constexpr (!kQKV) {
     const int h = kh * G + col;
     const unsigned short* qrow = q + (long)b * q_stride + (long)h * D;
 #pragma unroll
@@ -80,6 +108,113 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
                           : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       qf[ks] = __builtin_bit_cast(bf16x8, v);
     }
+  } else {
+    static_assert(!kQKV || KS % 2 == 0, "fused qkv decode: head_dim 64 or 128");
+    constexpr int half = D / 2;
+    const long pos = qi.positions[b];
+    const float* cs = qi.cos_sin + pos * D;
+    const float* wrow = qi.ws + (long)b * qi.N;
+    // --- the new token's k (RoPE) and v into the paged cache, by the ONE wave of the
+    //     workgroup whose partition holds the last position that will stream the last
+    //     chunk (chunk c belongs to wave c % W): no workgroup barrier, the other waves
+    //     start streaming at once and never read the new token
+    const long slot = qi.slots[b];
+    const int nch = (end - start + kChunk - 1) / kChunk;
+    if (end == ctx && slot >= 0 && wave == (nch - 1) % kDecWaves) {
+      const long blk = slot / block_size;
+      const int off = (int)(slot % block_size);
+      const int nk_items = qi.mode == 0 ? half / 8 : D / 8;
+      const int it = lane;
+      if (it < nk_items + D / 8) {
+        if (it >= nk_items) {  // v: transposed cache block (tokens contiguous per d)
+          const int c8 = it - nk_items;
+          float x[8];
+          qkv_sum8(x, wrow + (long)(nq + nkv) * D + (long)kh * D + c8 * 8, qi.slice, qi.S);
+          unsigned short* vc = qi.v_cache + (blk * nkv + kh) * (long)D * block_size + off;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vc[(c8 * 8 + j) * block_size] = f32_to_bf16(x[j]);
+        } else {
+          const float* kr = wrow + (long)nq * D + (long)kh * D;
+          unsigned short* kc = qi.k_cache + ((blk * nkv + kh) * block_size + off) * (long)D;
+          if (qi.mode == 0) {
+            float x[8], y[8];
+            qkv_sum8(x, kr + it * 8, qi.slice, qi.S);
+            qkv_sum8(y, kr + half + it * 8, qi.slice, qi.S);
+            u16x8 va, vb;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float co = cs[it * 8 + j], si = cs[half + it * 8 + j];
+              float ra, rb;
+              rope_rot(x[j], y[j], co, si, ra, rb);
+              va[j] = f32_to_bf16(ra);
+              vb[j] = f32_to_bf16(rb);
+            }
+            *reinterpret_cast<u16x8*>(kc + it * 8) = va;
+            *reinterpret_cast<u16x8*>(kc + half + it * 8) = vb;
+          } else {
+            float x[8];
+            qkv_sum8(x, kr + it * 8, qi.slice, qi.S);
+            u16x8 v;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              const int i = it * 4 + p;
+              const float co = cs[i], si = cs[half + i];
+              float ra, rb;
+              rope_rot(x[2 * p], x[2 * p + 1], co, si, ra, rb);
+              v[2 * p] = f32_to_bf16(ra);
+              v[2 * p + 1] = f32_to_bf16(rb);
+            }
+            *reinterpret_cast<u16x8*>(kc + it * 8) = v;
+          }
+        }
+      }
+    }
+    // --- q: sum, round, RoPE in-lane (partner d +- D/2 is fragment ks +- KS/2;
+    //     interleaved pairs sit inside each 8-run), round
+    float qv[KS][8];
+    const int h = kh * G + col;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (col < G) {
+        qkv_sum8(qv[ks], wrow + (long)h * D + 8 * grp + 32 * ks, qi.slice, qi.S);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qv[ks][j] = 0.f;
+      }
+    }
+    if (qi.mode == 0) {
+#pragma unroll
+      for (int ks = 0; ks < KS / 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * grp + 32 * ks + j;
+          const float co = cs[i], si = cs[half + i];
+          const float x = qv[ks][j], y = qv[ks + KS / 2][j];
+          rope_rot(x, y, co, si, qv[ks][j], qv[ks + KS / 2][j]);
+        }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int i = (8 * grp + 32 * ks) / 2 + p;
+          const float co = cs[i], si = cs[half + i];
+          const float x = qv[ks][2 * p], y = qv[ks][2 * p + 1];
+          rope_rot(x, y, co, si, qv[ks][2 * p], qv[ks][2 * p + 1]);
+        }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      u16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = col < G ? f32_to_bf16(qv[ks][j]) : 0;
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+    // the writing wave's own later loads of the last chunk (other lanes) must see its
+    // stores: workgroup-scope release / acquire = wait for the stores to complete (an
+    // agent-scope fence would write back the whole L2 from every workgroup)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   const float sl2 = scale * kLog2e;
   f32x4 o[NB];
@@ -306,6 +441,39 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
   else HS_DECODE_D(64);
 #undef HS_DECODE_D
 #undef HS_DECODE
+}
+
+// Fused decode: qkv partials -> RoPE + KV write + attention (see QkvIn). D in {64, 128}.
+void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S, int N, const long* positions,
+                             const long* slots, const float* cos_sin, int mode, void* k_cache, void* v_cache,
+                             const int* block_tables, int bt_stride, const int* context_lens, float* tmp_out,
+                             float* tmp_ml, int B, int nq, int nkv, int D, int block_size, int part_size,
+                             int max_parts, float scale, int window, hipStream_t s) {
+  if (B <= 0) return;
+  const int waves = decode_waves();
+  dim3 grid(max_parts, nkv, B), block(64 * waves);
+  const size_t smem = smem_bytes(D, waves);
+  auto* o = static_cast<unsigned short*>(out);
+  auto* kc = static_cast<unsigned short*>(k_cache);
+  auto* vc = static_cast<unsigned short*>(v_cache);
+  const QkvIn qi{ws, (long)B * N, S, N, positions, slots, cos_sin, kc, vc, mode};
+#define HS_DECODE_QKV(DD, WW)                                                                                  \
+  paged_decode_kernel<DD, WW, true><<<grid, block, smem, s>>>(o, out_stride, nullptr, 0, kc, vc, block_tables,  \
+                                                             bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv,  \
+                                                             block_size, part_size, max_parts, scale, window, qi)
+#define HS_DECODE_QKV_D(DD)                                                                                   \
+  do {                                                                                                        \
+    if (waves == 8) HS_DECODE_QKV(DD, 8);                                                                     \
+    else HS_DECODE_QKV(DD, 4);                                                                                \
+    if (max_parts > 1)                                                                                        \
+      paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,          \
+                                                                       context_lens, nq, part_size, max_parts,   \
+                                                                       window);                               \
+  } while (0)
+  if (D == 128) HS_DECODE_QKV_D(128);
+  else HS_DECODE_QKV_D(64);
+#undef HS_DECODE_QKV_D
+#undef HS_DECODE_QKV
 }
 
 }  // namespace hipserve

@@ -167,8 +167,10 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float co = cs[c * 8 + j], si = cs[half + c * 8 + j];
-      va[j] = f32_to_bf16(x[j] * co - y[j] * si);
-      vb[j] = f32_to_bf16(y[j] * co + x[j] * si);
+      float ra, rb;
+      rope_rot(x[j], y[j], co, si, ra, rb);
+      va[j] = f32_to_bf16(ra);
+      vb[j] = f32_to_bf16(rb);
     }
     unsigned short* dst = h < nq ? row + h * D
                                  : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
@@ -182,8 +184,10 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
     for (int p = 0; p < 4; ++p) {
       const int i = c * 4 + p;
       const float co = cs[i], si = cs[half + i];
-      v[2 * p] = f32_to_bf16(x[2 * p] * co - x[2 * p + 1] * si);
-      v[2 * p + 1] = f32_to_bf16(x[2 * p + 1] * co + x[2 * p] * si);
+      float ra, rb;
+      rope_rot(x[2 * p], x[2 * p + 1], co, si, ra, rb);
+      v[2 * p] = f32_to_bf16(ra);
+      v[2 * p + 1] = f32_to_bf16(rb);
     }
     unsigned short* dst = h < nq ? row + h * D
                                  : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;

@@ -23,8 +23,7 @@ HS_DEVICE void rotate8(float (&x)[8], float (&y)[8], const float* cs, int i0,
   for (int j = 0; j < 8; ++j) {
     const float c = cs[i0 + j], s = cs[half + i0 + j];
     const float a = x[j], b = y[j];
-    x[j] = a * c - b * s;
-    y[j] = b * c + a * s;
+    rope_rot(a, b, c, s, x[j], y[j]);
   }
 }
 
@@ -83,8 +82,10 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
         const int i = c * 4 + p;  // pair index
         const float co = cs[i], si = cs[half + i];
         const float a = bf16_to_f32(v[2 * p]), b = bf16_to_f32(v[2 * p + 1]);
-        v[2 * p] = f32_to_bf16(a * co - b * si);
-        v[2 * p + 1] = f32_to_bf16(b * co + a * si);
+        float ra, rb;
+        rope_rot(a, b, co, si, ra, rb);
+        v[2 * p] = f32_to_bf16(ra);
+        v[2 * p + 1] = f32_to_bf16(rb);
       }
       if (h < nq) {
         *reinterpret_cast<u16x8*>(base + c * 8) = v;

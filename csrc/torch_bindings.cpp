@@ -104,6 +104,43 @@ void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cach
                                 max_parts, (float)scale, (int)window, cur_stream());
 }
 
+void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
+                      const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
+                      const at::Tensor& block_tables, const at::Tensor& context_lens, at::Tensor& tmp_out,
+                      at::Tensor& tmp_ml, int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window,
+                      int64_t mode) {
+  CHECK_DEV(ws); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  const int D = k_cache.size(3), bs = k_cache.size(2);
+  TORCH_CHECK(D == 64 || D == 128, "paged_decode_qkv: head_dim 64/128");
+  TORCH_CHECK(window >= 0 && (mode == 0 || mode == 1));
+  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "paged_decode_qkv: GQA group <= 16");
+  TORCH_CHECK(bs % 16 == 0 && part_size % 128 == 0 && part_size / bs < 255);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && context_lens.scalar_type() == at::kInt);
+  TORCH_CHECK(block_tables.stride(1) == 1);
+  const int B = out.size(0);
+  const long N = (nq + 2 * nkv) * D;
+  TORCH_CHECK(out.size(1) >= nq * D);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * B * N);
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong);
+  TORCH_CHECK(positions.numel() >= B && slots.numel() >= B);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == D && cos_sin.is_contiguous());
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && v_cache.dim() == 4 && v_cache.size(2) == D);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous());
+  const int max_parts = tmp_ml.size(2);
+  TORCH_CHECK(tmp_out.is_contiguous() && tmp_ml.is_contiguous());
+  TORCH_CHECK(tmp_ml.dim() == 4 && tmp_ml.size(0) >= B && tmp_ml.size(1) == nq && tmp_ml.size(3) == 2);
+  TORCH_CHECK(tmp_out.dim() == 4 && tmp_out.size(2) == max_parts && tmp_out.size(3) == D);
+  TORCH_CHECK((long)max_parts * part_size >= (long)block_tables.size(1) * bs,
+              "workspace partitions must cover block_tables capacity");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  hipserve::launch_paged_decode_qkv(out.data_ptr(), out.stride(0), ws.data_ptr<float>(), splits, N,
+                                    positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                                    mode, k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                    block_tables.stride(0), context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
+                                    tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size, max_parts, (float)scale,
+                                    (int)window, cur_stream());
+}
+
 void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
                        const at::Tensor& v_cache, const at::Tensor& block_tables,
                        const at::Tensor& cu_q, const at::Tensor& ctx_lens,
@@ -762,6 +799,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu) -> ()");
+  m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
@@ -796,6 +834,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.impl("splitk_rope_cache", &splitk_rope_cache);
   m.impl("splitk_glu", &splitk_glu);
+  m.impl("paged_decode_qkv", &paged_decode_qkv);
   m.impl("splitk_reduce", &splitk_reduce);
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);

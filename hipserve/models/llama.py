@@ -101,6 +101,12 @@ class LlamaModel:
     # load FP8 checkpoints natively (e4m3 + scales, ops/quant.py) instead of
     # dequantising them to bf16 at load (weights/safetensors_loader.py)
     native_fp8 = True
+    # fused decode: qkv partials -> RoPE + KV write + attention in one kernel
+    # (attention_decode.hip QkvIn), opt-in with HIPSERVE_FUSED_QKV_ATTN=1. Bit-exact,
+    # but measured SLOWER on Llama-3-8B B=64 (5.57 vs 5.49 ms per decode step,
+    # tools/decode_gap.py): every wave re-reads the fp32 partials for q before it can
+    # stream K/V, which costs more than the separate splitk_rope_cache launch saves
+    fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "0") == "1"
 
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,
                  max_pos: int | None = None):
@@ -510,7 +516,12 @@ class LlamaModel:
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
             pt = self._partial(xn, lw.wqkv)
-            if pt is not None:
+            if pt is not None and self.fused_qkv_attention and D in (64, 128):
+                # RoPE + KV write + attention in one kernel, straight from the partials
+                op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
+                                    meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part, self.scale,
+                                    0, cfg.rope_mode)
+            elif pt is not None:
                 ws, S = pt
                 qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)
                 op.splitk_rope_cache(qkv, ws, S, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
@@ -519,8 +530,9 @@ class LlamaModel:
                 qkv = self.linear(xn, lw.wqkv)
                 ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
                                cfg.rope_mode)
-            ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
-                             nq, nkv, part, self.scale)
+            if pt is None or not (self.fused_qkv_attention and D in (64, 128)):
+                ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
+                                 nq, nkv, part, self.scale)
             pt = self._partial(attn, lw.wo)
             if pt is not None:
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2)

@@ -141,3 +141,41 @@ def test_fused_decode_forward_bit_exact(ops, choices):
     finally:
         gemm.TUNER.table.clear()
         gemm.TUNER.table.update(old)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("S,part", [(1, 512), (4, 128), (3, 256)])
+@pytest.mark.parametrize("D", [128, 64])
+def test_paged_decode_qkv_bit_exact(ops, mode, S, part, D):
+    """Fused qkv partials -> RoPE + KV write + attention == splitk_rope_cache followed
+    by paged_decode, bit for bit (output and both caches), with split contexts
+    (several partitions + reduce) and a padding row (slot -1)."""
+    B, nq, nkv, bs = 9, 16, 4, 16
+    N = (nq + 2 * nkv) * D
+    ws = _partials(S, B, N, 31 + S + D)
+    nblk = 40
+    ctx = torch.randint(1, nblk * bs, (B,), device=DEV, dtype=torch.int32)
+    ctx[0] = 1
+    ctx[1] = nblk * bs
+    bt = torch.randperm(B * nblk, device=DEV).int().view(B, nblk)
+    pos = (ctx - 1).long()
+    slots = bt.gather(1, (pos // bs).view(-1, 1).int()).view(-1).long() * bs + pos % bs
+    slots[4] = -1
+    cs = ref.rope_cos_sin(D, 4096, 500000.0).to(DEV)
+    kc1 = torch.randn(B * nblk, nkv, bs, D, device=DEV).to(torch.bfloat16)
+    vc1 = torch.randn(B * nblk, nkv, D, bs, device=DEV).to(torch.bfloat16)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    parts = math.ceil(nblk * bs / part)
+    mk = lambda: (torch.empty(B, nq, parts, D, device=DEV), torch.empty(B, nq, parts, 2, device=DEV))
+    scale = D ** -0.5
+    qkv = torch.zeros(B, N, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.splitk_rope_cache(qkv, ws.contiguous(), S, pos, slots, cs, kc1, vc1, nq, nkv, D, mode)
+    out1 = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
+    t1, m1 = mk()
+    ops.paged_decode(out1, qkv, kc1, vc1, bt, ctx, t1, m1, nq, nkv, part, scale)
+    out2 = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
+    t2, m2 = mk()
+    torch.ops.hipserve.paged_decode_qkv(out2, ws.contiguous(), S, pos, slots, cs, kc2, vc2, bt, ctx, t2, m2,
+                                        nq, nkv, part, scale, 0, mode)
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    assert torch.equal(out1, out2)
