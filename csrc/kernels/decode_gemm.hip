@@ -67,7 +67,10 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
   constexpr int XR = 16 * MT;                 // x rows staged (padded M)
   constexpr int NT = 64 * NWAVES;             // threads
   constexpr int XPASS = XR * 32 / NT;         // 16-byte x loads per thread per step
-  __shared__ __attribute__((aligned(16))) unsigned short xs[3][XR * DG_LDS_ROW];
+  // x ring in LDS: 2 slots suffice (x(st+1) is stored at the start of step st into the
+  // slot x(st-1) used, after the barrier that ended step st-1); at M = 64 that is
+  // 68 KB instead of 101 KB, so two workgroups fit per CU
+  __shared__ __attribute__((aligned(16))) unsigned short xs[2][XR * DG_LDS_ROW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -159,12 +162,12 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
   __syncthreads();
 #pragma unroll
   for (int st = 0; st < nsteps; ++st) {
-    if (st + 1 < nsteps) store_x((st + 1) % 3);  // x(st+1), loaded during step st-1
+    if (st + 1 < nsteps) store_x((st + 1) % 2);  // x(st+1), loaded during step st-1
     if (st + 2 < nsteps) {
       load_x(st + 2);
       load_w((st + 2) % 3, st + 2);
     }
-    const unsigned short* xb = &xs[st % 3][c * DG_LDS_ROW + 8 * g];
+    const unsigned short* xb = &xs[st % 2][c * DG_LDS_ROW + 8 * g];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
 #pragma unroll
