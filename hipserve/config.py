@@ -18,6 +18,58 @@ from dataclasses import dataclass, field
 
 
 @dataclass(frozen=True)
+class VisionConfig:
+    """Qwen3-VL vision tower (HF ``vision_config``): a ViT over 16x16x2 (HxWxT)
+    patches with a learned, bilinearly resampled position table, 2D RoPE, a 2x2
+    spatial merger into the language model's hidden size and DeepStack features
+    (merged outputs of intermediate blocks added to the first decoder layers)."""
+    depth: int = 27
+    hidden_size: int = 1152
+    intermediate_size: int = 4304
+    num_heads: int = 16
+    patch_size: int = 16
+    temporal_patch_size: int = 2
+    in_channels: int = 3
+    spatial_merge_size: int = 2
+    out_hidden_size: int = 2048
+    num_position_embeddings: int = 2304
+    deepstack_visual_indexes: tuple = (8, 16, 24)
+    hidden_act: str = "gelu_pytorch_tanh"
+    # special tokens of the language model
+    image_token_id: int = 151655
+    video_token_id: int = 151656
+    vision_start_token_id: int = 151652
+    vision_end_token_id: int = 151653
+    # image preprocessing (preprocessor_config.json)
+    min_pixels: int = 65536
+    max_pixels: int = 16777216
+    image_mean: tuple = (0.5, 0.5, 0.5)
+    image_std: tuple = (0.5, 0.5, 0.5)
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_heads
+
+    @property
+    def patch_dim(self) -> int:
+        return self.in_channels * self.temporal_patch_size * self.patch_size ** 2
+
+    @staticmethod
+    def from_hf_dict(d: dict) -> "VisionConfig | None":
+        v = d.get("vision_config")
+        if not isinstance(v, dict) or "depth" not in v:
+            return None
+        kw = {k: v[k] for k in ("depth", "hidden_size", "intermediate_size", "num_heads", "patch_size",
+                                "temporal_patch_size", "in_channels", "spatial_merge_size", "out_hidden_size",
+                                "num_position_embeddings", "hidden_act") if k in v}
+        kw["deepstack_visual_indexes"] = tuple(v.get("deepstack_visual_indexes") or ())
+        for k in ("image_token_id", "video_token_id", "vision_start_token_id", "vision_end_token_id"):
+            if d.get(k) is not None:
+                kw[k] = int(d[k])
+        return VisionConfig(**kw)
+
+
+@dataclass(frozen=True)
 class ModelConfig:
     name: str = "llama"
     architecture: str = "llama"          # llama | mixtral
@@ -53,6 +105,10 @@ class ModelConfig:
     layer_windows: tuple = ()             # per-layer window (0 = full attention); empty = all full
     rope_local_theta: float = 0.0         # RoPE base of the sliding layers (Gemma-3: 10000; 0 = rope_theta)
     partial_rotary_factor: float = 1.0
+    # Qwen3-VL: interleaved multimodal RoPE (rotary pairs split T/H/W by this
+    # section table; text tokens have t = h = w so it reduces to plain RoPE)
+    mrope_section: tuple = ()
+    vision: VisionConfig | None = None
 
     @property
     def expert_size(self):
@@ -88,7 +144,8 @@ class ModelConfig:
         form (per layer type for Gemma-3) are read."""
         arch = (d.get("architectures") or ["LlamaForCausalLM"])[0]
         mtype = d.get("model_type", "")
-        if isinstance(d.get("text_config"), dict):  # multimodal wrapper: serve the text model
+        vision = VisionConfig.from_hf_dict(d) if mtype.startswith("qwen3_vl") or "qwen3vl" in arch.lower() else None
+        if isinstance(d.get("text_config"), dict):  # multimodal wrapper: the language model
             td = dict(d["text_config"])
             for k in ("eos_token_id", "bos_token_id", "tie_word_embeddings"):
                 if k not in td and k in d:
@@ -125,6 +182,12 @@ class ModelConfig:
         )
         if kw["partial_rotary_factor"] != 1.0:
             raise NotImplementedError("partial rotary embeddings are not supported")
+        if vision is not None:
+            rp = d.get("rope_parameters") or d.get("rope_scaling") or {}
+            sec = tuple(int(x) for x in (rp.get("mrope_section") or (24, 20, 20)))
+            if rp.get("mrope_interleaved") is False:
+                raise NotImplementedError("non-interleaved MRoPE (Qwen2-VL layout) is not supported")
+            kw.update(vision=vision, mrope_section=sec)
         if family == "mixtral":
             kw.update(num_experts=d.get("num_local_experts", 0) or 0,
                       num_experts_per_tok=d.get("num_experts_per_tok", 0) or 0)
@@ -306,7 +369,8 @@ def resolve_model_config(model: str, name: str | None = None) -> ModelConfig:
         return PRESETS[k]
     if os.path.isdir(model) and os.path.exists(os.path.join(model, "config.json")):
         with open(os.path.join(model, "config.json")) as f:
-            return ModelConfig.from_hf_dict(json.load(f), name=name or os.path.basename(model))
+            return _with_preprocessor(ModelConfig.from_hf_dict(json.load(f), name=name or os.path.basename(model)),
+                                      model)
     if model.endswith(".gguf") and os.path.exists(model):
         from .weights.gguf import GGUFFile
 
@@ -314,9 +378,34 @@ def resolve_model_config(model: str, name: str | None = None) -> ModelConfig:
     hub = _hf_cache_dir(model)
     if hub:
         with open(os.path.join(hub, "config.json")) as f:
-            return ModelConfig.from_hf_dict(json.load(f), name=name or model)
+            return _with_preprocessor(ModelConfig.from_hf_dict(json.load(f), name=name or model), hub)
     raise ValueError(f"unknown model {model!r}: not a preset ({', '.join(PRESETS)}), "
                      "a directory with config.json, a cached HF id or a .gguf file")
+
+
+def _with_preprocessor(cfg: ModelConfig, path: str) -> ModelConfig:
+    """Image preprocessing limits of a vision model from its preprocessor_config.json
+    (``size.shortest_edge`` / ``longest_edge`` or ``min_pixels`` / ``max_pixels``,
+    ``image_mean`` / ``image_std``)."""
+    p = os.path.join(path, "preprocessor_config.json")
+    if cfg.vision is None or not os.path.exists(p):
+        return cfg
+    with open(p) as f:
+        d = json.load(f)
+    size = d.get("size") or {}
+    kw = {}
+    lo = d.get("min_pixels") or size.get("shortest_edge") or size.get("min_pixels")
+    hi = d.get("max_pixels") or size.get("longest_edge") or size.get("max_pixels")
+    if lo:
+        kw["min_pixels"] = int(lo)
+    if hi:
+        kw["max_pixels"] = int(hi)
+    for k in ("image_mean", "image_std"):
+        if d.get(k):
+            kw[k] = tuple(float(x) for x in d[k])
+    if d.get("patch_size") and int(d["patch_size"]) != cfg.vision.patch_size:
+        raise ValueError("preprocessor patch_size differs from the vision tower's")
+    return cfg.replace(vision=dataclasses.replace(cfg.vision, **kw))
 
 
 def _hf_cache_dir(repo_id: str) -> str | None:

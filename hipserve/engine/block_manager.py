@@ -5,6 +5,12 @@ from ..runtime import native
 from .request import Sequence
 
 
+def _hash_prompt(seq: Sequence) -> list[int]:
+    """Prompt ids as prefix-cache keys: image placeholder tokens are keyed by their
+    image's content (two prompts with different images never share KV blocks)."""
+    return seq.mm.hash_ids if seq.mm is not None else seq.prompt_token_ids
+
+
 class BlockManager:
     def __init__(self, num_blocks: int, block_size: int, prefix_caching: bool = True,
                  watermark: float = 0.01):
@@ -37,7 +43,7 @@ class BlockManager:
     def match_prefix(self, seq: Sequence):
         if not self.prefix_caching:
             return
-        ids, ntok = self.pool.match_prefix(seq.all_token_ids())
+        ids, ntok = self.pool.match_prefix(_hash_prompt(seq) + seq.output_token_ids)
         seq.block_ids = list(ids)
         seq.num_computed_tokens = ntok
         seq.num_cached_prefix = ntok
@@ -55,8 +61,8 @@ class BlockManager:
             # only the newly filled blocks' tokens, hash chained from the last call
             # (O(new tokens) per step, not O(context))
             a, b, npr = first * bs, full * bs, seq.num_prompt_tokens
-            toks = seq.prompt_token_ids[a:b] if b <= npr else (
-                seq.prompt_token_ids[a:] + seq.output_token_ids[max(0, a - npr):b - npr])
+            prompt = _hash_prompt(seq)
+            toks = prompt[a:b] if b <= npr else (prompt[a:] + seq.output_token_ids[max(0, a - npr):b - npr])
             seq._reg_hash = self.pool.register_blocks(seq.block_ids, toks, first, full,
                                                        getattr(seq, "_reg_hash", 0) if first else 0)
             seq._registered_blocks = full

@@ -76,7 +76,13 @@ class LLMEngine:
 
     def add_request(self, request_id: str | None, prompt, params: SamplingParams,
                     arrival_time: float | None = None) -> Sequence:
+        from ..multimodal import MultiModalPrompt, mm_state
+
         request_id = request_id or self.new_request_id()
+        images = None
+        if isinstance(prompt, MultiModalPrompt):
+            images = prompt.images or None
+            prompt = prompt.ids
         if isinstance(prompt, str):
             ids = self.tokenizer.encode(prompt)
         else:
@@ -89,6 +95,13 @@ class LLMEngine:
         if len(ids) >= self.max_model_len:
             raise ValueError(f"prompt has {len(ids)} tokens; max_model_len is {self.max_model_len}")
         seq = Sequence(request_id, ids, params, eos_token_ids=self.eos_ids)
+        vcfg = self.model_cfg.vision
+        if images:
+            if vcfg is None or self.runner.model.visual is None:
+                raise ValueError("this model has no vision encoder: image inputs are not supported")
+            seq.mm = mm_state(ids, images, vcfg)
+        elif vcfg is not None and vcfg.image_token_id in ids:
+            raise ValueError("image placeholder tokens in a prompt without images")
         if arrival_time is not None:
             seq.arrival_time = arrival_time
         seq.seed = params.seed if params.seed is not None else random.getrandbits(62)

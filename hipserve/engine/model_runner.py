@@ -304,9 +304,49 @@ class ModelRunner:
             pen_init = (np.array([q.pen_slot for q in init], np.int32), off,
                         np.array([q.num_prompt_tokens for q in init], np.int32),
                         np.fromiter((t for x in ids_l for t in x), np.int32, int(off[-1])))
-        return StepInputs(ids, pos, slots, Tp, len(so.decode), bt_p, cu_q, ctx_p, tiles, bt_d, ctx_d,
-                          np.array(rows, dtype=np.int64), temp, topk, topp, seeds, steps,
-                          pen_slot, pen_vals, nlp, pen_init, topn)
+        inp = StepInputs(ids, pos, slots, Tp, len(so.decode), bt_p, cu_q, ctx_p, tiles, bt_d, ctx_d,
+                         np.array(rows, dtype=np.int64), temp, topk, topp, seeds, steps,
+                         pen_slot, pen_vals, nlp, pen_init, topn)
+        if any(s.seq.mm is not None for s in seqs):
+            self._prepare_mm(seqs, inp)
+        return inp
+
+    def _prepare_mm(self, seqs, inp: StepInputs):
+        """Multimodal rows of a batch: rotary positions of the sequences' tokens from
+        their MRoPE tables (prompt) or index + delta (generated tokens); the image
+        tokens, whose three axes differ, get their own table rows; each image whose
+        token span intersects a prefill chunk is listed with the chunk's slice of it
+        (every TP rank runs the replicated vision tower on the same pixels)."""
+        pos = np.array(inp.positions, dtype=np.int64, copy=True)
+        rope_rows, rope_pos, images = [], [], []
+        t = 0
+        for s in seqs:
+            mm = s.seq.mm
+            n = s.num_tokens
+            if mm is not None:
+                npr = s.seq.num_prompt_tokens
+                a, b = s.start, min(s.end, npr)
+                if a < b:
+                    p3 = mm.pos3[:, a:b]
+                    pos[t:t + b - a] = p3[0]
+                    odd = np.nonzero((p3[0] != p3[1]) | (p3[0] != p3[2]))[0]
+                    if odd.size:
+                        rope_rows.append(odd + t)
+                        rope_pos.append(p3[:, odd])
+                    for (ia, ib), im in zip(mm.spans, mm.images):
+                        lo, hi = max(ia, a), min(ib, b)
+                        if lo < hi:
+                            images.append((t + lo - a, lo - ia, hi - ia, im.pixels, tuple(im.grid), im.digest))
+                if s.end > npr:
+                    k0 = max(s.start, npr)
+                    pos[t + k0 - s.start:t + n] = np.arange(k0, s.end) + mm.delta
+            t += n
+        inp.positions = pos
+        if rope_rows or images:
+            inp.extra["mm"] = {
+                "rope_rows": np.concatenate(rope_rows) if rope_rows else np.zeros(0, np.int64),
+                "rope_pos": np.concatenate(rope_pos, 1) if rope_pos else np.zeros((3, 0), np.int64),
+                "images": images}
 
     def release(self, seq):
         """A finished / aborted sequence gives its penalty slot back."""
@@ -352,6 +392,8 @@ class ModelRunner:
         if inp.num_decode > self.max_bs:
             meta.tmp_out = torch.empty(inp.num_decode, *self.tmp_out.shape[1:], device=self.device)
             meta.tmp_ml = torch.empty(inp.num_decode, *self.tmp_ml.shape[1:], device=self.device)
+        if "mm" in inp.extra:
+            self._attach_mm(inp.extra["mm"], meta, len(inp.ids))
         hidden = self.model.forward(ids, meta, self.kv)
         if n == 0:
             return np.zeros(0, np.int64), np.zeros(0, np.float32), None
@@ -377,6 +419,40 @@ class ModelRunner:
             self.ops.top_logprobs(logits, self._t(inp.nlogprobs), ti, tl)
             top = (ti.cpu().numpy(), tl.cpu().numpy())
         return tok.cpu().numpy(), lp.cpu().numpy(), top
+
+    def _attach_mm(self, mm: dict, meta: AttnMeta, T: int):
+        """Vision-tower outputs and MRoPE rows of a multimodal prefill batch into the
+        attention metadata: a per-row rotary table (the model's table gathered at the
+        rows' positions, image rows replaced by their 3D MRoPE rows) with
+        positions = row index, and the image embeddings / DeepStack features with the
+        batch rows they belong to."""
+        from ..models.vision import image_geometry
+        from ..multimodal import mrope_cos_sin
+
+        cfg = self.mcfg
+        if len(mm["rope_rows"]):
+            cs = self.model.cos_sin.index_select(0, meta.positions)
+            rows = self._t(mm["rope_rows"])
+            vals = mrope_cos_sin(mm["rope_pos"], cfg.head_dim, cfg.rope_theta, cfg.mrope_section)
+            cs.index_copy_(0, rows, self._t(vals))
+            meta.cos_sin = cs
+            meta.positions = torch.arange(T, device=self.device)
+        if not mm["images"]:
+            return
+        vis = self.model.visual
+        cache = {}
+        rows, embs, dss = [], [], []
+        for row0, lo, hi, pixels, grid, digest in mm["images"]:
+            if digest not in cache:
+                geo = image_geometry([grid], vis.cfg)
+                cache[digest] = vis.forward(torch.from_numpy(pixels), geo)
+            e, ds = cache[digest]
+            rows.append(torch.arange(row0, row0 + hi - lo))
+            embs.append(e[lo:hi])
+            dss.append([d[lo:hi] for d in ds])
+        meta.mm_rows = torch.cat(rows).to(self.device)
+        meta.mm_embeds = torch.cat(embs).to(self.model.dtype)
+        meta.mm_deepstack = [torch.cat([d[j] for d in dss]).to(self.model.dtype) for j in range(len(dss[0]))]
 
     # ------------------------------------------------------------ hipGraphs
     def _graph_forward(self, b: int):

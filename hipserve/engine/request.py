@@ -127,6 +127,7 @@ class Sequence:
     last_token_time: float | None = None
     seed: int = 0
     pen_slot: int | None = None         # device penalty-state slot (ModelRunner), while it has penalties
+    mm: object = None                   # multimodal.MMState of a prompt with images
     # detokenizer state
     output_text: str = ""
     _decoded_upto: int = 0

@@ -56,6 +56,12 @@ class AttnMeta:
     ctx_decode: torch.Tensor | None = None   # int32 [nd]
     tmp_out: torch.Tensor | None = None
     tmp_ml: torch.Tensor | None = None
+    # multimodal prefill (Qwen3-VL): per-row rotary table (positions = row index),
+    # image embeddings for rows mm_rows and DeepStack features added after layers 0..n-1
+    cos_sin: torch.Tensor | None = None
+    mm_rows: torch.Tensor | None = None
+    mm_embeds: torch.Tensor | None = None
+    mm_deepstack: list | None = None
 
 
 @dataclass
@@ -134,6 +140,11 @@ class LlamaModel:
         self.block_size_hint = 16  # KV block size (set by the runner)
         self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
         self.fused_decode = True  # decode-only batches: split-K partials -> fused epilogues
+        self.visual = None        # models.vision.VisionTower (Qwen3-VL), replicated on every TP rank
+        if cfg.vision is not None:
+            from .vision import VisionTower
+
+            self.visual = VisionTower(cfg.vision, self.device, dtype, ops)
 
     # ---------------------------------------------------------------- weights
     def allocate_random(self, seed: int = 0, std: float = 0.02):
@@ -199,6 +210,8 @@ class LlamaModel:
                 lw.wd = new(H, I)
                 fill(lw.wd, f"{li}.down", 0, rank * I, cfg.intermediate_size)
             self.layers.append(lw)
+        if self.visual is not None:
+            self.visual.allocate_random(seed)
 
     # synthetic GGUF schemes (GGUF-tier benchmarks): per projection ggml type;
     # q4_k_m mirrors llama.cpp's Q4_K_M mix (attn_v, ffn_down, output in Q6_K)
@@ -440,6 +453,11 @@ class LlamaModel:
         h = self.embed_tokens(ids)
         if cfg.embed_scale != 1.0:  # Gemma: embeddings * sqrt(hidden), the scale rounded to the dtype
             h = h * float(torch.tensor(cfg.embed_scale, dtype=h.dtype))
+        ds = None
+        if meta.mm_rows is not None:  # image placeholders take the vision tower's embeddings
+            h.index_copy_(0, meta.mm_rows, meta.mm_embeds.to(h.dtype))
+            ds = meta.mm_deepstack
+        cos_sin = self.cos_sin if meta.cos_sin is None else meta.cos_sin
         residual = h.clone()
         xn = torch.empty_like(h)
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
@@ -455,7 +473,7 @@ class LlamaModel:
                 ops.qk_rmsnorm(qkv, lw.q_norm, lw.k_norm, nq, nkv, D, eps)
             kc, vc = kv_caches[i]
             win = cfg.window_of(i)
-            ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin_local if win else self.cos_sin,
+            ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin_local if win else cos_sin,
                            kc, vc, nq, nkv, D, cfg.rope_mode)
             if Tp:
                 ops.prefill_attention(attn[:Tp], qkv[:Tp], kc, vc, meta.bt_prefill, meta.cu_q,
@@ -478,6 +496,10 @@ class LlamaModel:
                 self.act_and_mul(act, gu)
                 h = self.linear_rowpar(act, lw.wd)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
+            if ds is not None and i < len(ds) and self.tp.rank == 0:
+                # DeepStack: visual features join the residual stream after layer i
+                # (rank 0 only: the row-parallel partials are summed across ranks next)
+                h = h.index_add(0, meta.mm_rows, ds[i].to(h.dtype))
             if lw.post_ff_norm is not None:
                 h = self._tp_sum(h, xn)
                 ops.rmsnorm(h, h, lw.post_ff_norm, eps)

@@ -174,6 +174,25 @@ class ReferenceOps:
     def top_logprobs(self, logits, nreq, out_ids, out_lp):
         ref.top_logprobs(logits, nreq, out_ids, out_lp)
 
+    # ---- vision tower (Qwen3-VL ViT)
+    def layernorm(self, out, x, w, b, eps, residual=None):
+        if residual is None:
+            out.copy_(ref.layernorm(x, w, b, eps))
+        else:
+            y, r = ref.add_layernorm(x, residual, w, b, eps)
+            residual.copy_(r)
+            out.copy_(y)
+        return out
+
+    def gelu_(self, x, tanh):
+        x.copy_(ref.gelu(x, tanh))
+        return x
+
+    def vision_attention(self, out, qkv, cos_sin, cu_seqlens, nh, D, scale, meta=None):
+        ref.vision_rope(qkv, cos_sin, nh, D)
+        out.copy_(ref.vision_attention(qkv, cu_seqlens, nh, D, scale))
+        return out
+
     def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
         t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, bf16_row=False)
         n = t.shape[0]

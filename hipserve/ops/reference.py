@@ -41,6 +41,48 @@ def gelu_and_mul(x: torch.Tensor) -> torch.Tensor:
     return (torch.nn.functional.gelu(g, approximate="tanh") * u).to(x.dtype)
 
 
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    """LayerNorm over the last dim (fp32 statistics, x.dtype out)."""
+    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def add_layernorm(x: torch.Tensor, residual: torch.Tensor, w, b, eps: float):
+    """(LayerNorm(r), r) with r = residual + x rounded to x.dtype first."""
+    r = (x.float() + residual.float()).to(x.dtype)
+    return layernorm(r, w, b, eps), r
+
+
+def gelu(x: torch.Tensor, tanh: bool) -> torch.Tensor:
+    return torch.nn.functional.gelu(x.float(), approximate="tanh" if tanh else "none").to(x.dtype)
+
+
+def vision_rope(qkv: torch.Tensor, cos_sin: torch.Tensor, nh: int, D: int):
+    """In place: rotate-half RoPE of the q and k heads of a ViT qkv [T, 3*nh*D] with one
+    fp32 table row per token ([cos(D/2) | sin(D/2)], the 2D row/column angles)."""
+    T = qkv.shape[0]
+    half = D // 2
+    c, s = cos_sin[:T, None, :half].float(), cos_sin[:T, None, half:].float()
+    for j in range(2):
+        x = qkv[:, j * nh * D:(j + 1) * nh * D].view(T, nh, D)
+        a, b = x[..., :half].float(), x[..., half:].float()
+        x.copy_(torch.cat([a * c - b * s, b * c + a * s], -1).to(x.dtype))
+
+
+def vision_attention(qkv: torch.Tensor, cu_seqlens, nh: int, D: int, scale: float) -> torch.Tensor:
+    """Bidirectional attention within each segment [cu[i], cu[i+1]) of a ViT qkv
+    [T, 3*nh*D] (fp32 math) -> [T, nh*D]."""
+    T = qkv.shape[0]
+    q = qkv[:, : nh * D].view(T, nh, D).float()
+    k = qkv[:, nh * D:2 * nh * D].view(T, nh, D).float()
+    v = qkv[:, 2 * nh * D:].view(T, nh, D).float()
+    out = torch.empty(T, nh, D, dtype=torch.float32, device=qkv.device)
+    cu = [int(x) for x in cu_seqlens]
+    for a, b in zip(cu[:-1], cu[1:]):
+        s = torch.einsum("qhd,khd->hqk", q[a:b], k[a:b]) * scale
+        out[a:b] = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), v[a:b])
+    return out.view(T, nh * D).to(qkv.dtype)
+
+
 def qk_rmsnorm(qkv: torch.Tensor, q_w: torch.Tensor, k_w: torch.Tensor, nq: int, nkv: int, D: int, eps: float):
     """In place: RMSNorm over head_dim of every q head (weight q_w) and k head (k_w)."""
     T = qkv.shape[0]

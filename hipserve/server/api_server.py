@@ -40,6 +40,12 @@ def _dumps(o) -> str:
     return json.dumps(o, separators=(",", ":"), ensure_ascii=False)
 
 
+def _has_images(msgs) -> bool:
+    return any(isinstance(m, dict) and isinstance(m.get("content"), list)
+               and any(isinstance(p, dict) and p.get("type") in ("image_url", "image") for p in m["content"])
+               for m in msgs)
+
+
 class OpenAIServer:
     def __init__(self, aengine: AsyncEngine, model_name: str, max_model_len: int,
                  extra_names: tuple = ()):
@@ -145,6 +151,22 @@ class OpenAIServer:
         for t in ids:
             if isinstance(t, bool) or not isinstance(t, int) or not 0 <= t < V:
                 raise ValueError(f"prompt token id out of range [0, {V})")
+
+    async def _encode_images(self, msgs, vcfg):
+        """Chat messages with image parts -> MultiModalPrompt: the template with one
+        image marker per part, the images fetched / decoded / patchified off the event
+        loop (worker thread), each marker's pad token expanded to the image's merged
+        patch count."""
+        from ..multimodal import MultiModalPrompt, expand_image_tokens, load_image, preprocess_image
+
+        ids, urls = self.tokenizer.encode_chat_mm(msgs, vcfg)
+        allow_local = bool(self.engine.cfg.extra.get("allow_local_media", False))
+
+        def work():
+            return [preprocess_image(load_image(u, allow_local=allow_local), vcfg) for u in urls]
+
+        images = await asyncio.get_running_loop().run_in_executor(None, work)
+        return MultiModalPrompt(expand_image_tokens(ids, images, vcfg), images)
 
     def _clip_max_tokens(self, params: SamplingParams, n_prompt: int):
         room = self.max_model_len - n_prompt
@@ -271,7 +293,12 @@ class OpenAIServer:
             return _err(400, "messages must be a non-empty list")
         try:
             params = self._params(body, chat=True)
-            ids = self.tokenizer.encode_chat(msgs, add_generation_prompt=True)
+            vcfg = self.engine.model_cfg.vision
+            if vcfg is not None and _has_images(msgs):
+                prompt = await self._encode_images(msgs, vcfg)
+                ids = prompt.ids
+            else:
+                ids = prompt = self.tokenizer.encode_chat(msgs, add_generation_prompt=True)
             self._check_prompt(ids)
             self._clip_max_tokens(params, len(ids))
         except (ValueError, TypeError) as e:
@@ -283,7 +310,7 @@ class OpenAIServer:
         model = body.get("model") or self.model_name
         stream = bool(body.get("stream", False))
         include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
-        gens = await self._run_many([ids], params, rid)
+        gens = await self._run_many([prompt], params, rid)
         n_prompt = len(ids) * params.n
         if stream:
             resp = web.StreamResponse(headers={"Content-Type": "text/event-stream",

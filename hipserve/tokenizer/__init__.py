@@ -56,6 +56,7 @@ class BaseTokenizer:
     chat_template: str = _DEFAULT_CHAT_TEMPLATE
     vocab_size: int = 0
     add_bos: bool = True
+    chat_adds_bos: bool = True
 
     def encode(self, text: str, add_special_tokens: bool = True) -> list[int]:
         raise NotImplementedError
@@ -74,6 +75,48 @@ class BaseTokenizer:
                 and not self.bos_token:
             ids = [self.bos_token_id] + ids
         return ids
+
+    def encode_chat_mm(self, messages, vision) -> tuple[list[int], list[str]]:
+        """Chat prompt of a vision model: every image part (OpenAI ``image_url`` or
+        ``image``) becomes ``<|vision_start|><|image_pad|><|vision_end|>`` — what the
+        Qwen3-VL chat template emits for it — and its URL is returned, in prompt order.
+        The single ``<|image_pad|>`` per image is expanded by the caller once the
+        image's patch grid is known. Text segments are tokenised separately around the
+        image markers, so tokenizers without these special tokens work too."""
+        urls: list[str] = []
+        flat = []
+        for m in messages:
+            if isinstance(m, dict) and isinstance(m.get("content"), list):
+                parts = []
+                for p in m["content"]:
+                    kind = p.get("type", "text") if isinstance(p, dict) else None
+                    if kind == "text":
+                        parts.append(p.get("text", ""))
+                    elif kind in ("image_url", "image"):
+                        u = p.get("image_url", p.get("image"))
+                        u = u.get("url") if isinstance(u, dict) else u
+                        urls.append(u)
+                        parts.append(_IMAGE_MARK)
+                    else:
+                        raise UnsupportedContentError(f"content part of type {kind!r} is not supported "
+                                                      "(text and image_url parts are)")
+                m = {**m, "content": "".join(parts)}
+            flat.append(m)
+        text = self.apply_chat_template(flat, True)
+        pieces = text.split(_IMAGE_MARK)
+        ids = []
+        for i, piece in enumerate(pieces):
+            if i:
+                ids += [vision.vision_start_token_id, vision.image_token_id, vision.vision_end_token_id]
+            if piece:
+                ids += self.encode(piece, add_special_tokens=False)
+        if self.chat_adds_bos and self.bos_token_id is not None and self.add_bos \
+                and (not ids or ids[0] != self.bos_token_id) and not self.bos_token:
+            ids = [self.bos_token_id] + ids
+        return ids, urls
+
+
+_IMAGE_MARK = "<|vision_start|><|image_pad|><|vision_end|>"
 
 
 class SyntheticTokenizer(BaseTokenizer):
@@ -151,6 +194,8 @@ class HFTokenizer(BaseTokenizer):
     def encode_chat(self, messages, add_generation_prompt=True):
         text = self.apply_chat_template(messages, add_generation_prompt)
         return self.tk.encode(text, add_special_tokens=False).ids
+
+    chat_adds_bos = False  # HF chat templates carry any BOS themselves
 
 
 def get_tokenizer(model: str, model_cfg, tokenizer: str | None = None) -> BaseTokenizer:

@@ -319,6 +319,11 @@ def load_hf_weights(model: LlamaModel, model_path: str):
         from ..ops import quant as Q
 
         model.quant_linear = Q.quant_linear
+    if model.visual is not None:  # Qwen3-VL vision tower (bf16 in every checkpoint, replicated)
+        vname = ck.find("patch_embed.proj.weight")
+        if vname is None:
+            raise KeyError("vision config present but no visual.patch_embed.proj.weight in the checkpoint")
+        model.visual.load(ck.full, vname[: -len("patch_embed.proj.weight")])
 
 
 def _load_experts(ck, p, cfg, r, inter, to):
