@@ -186,3 +186,16 @@ struct StageCopyArgs {
 void launch_stage_copy(const StageCopyArgs& a, hipStream_t s);
 
 }  // namespace hipserve
+
+namespace hipserve {
+// vision.hip — Qwen3-VL vision tower. residual != nullptr: residual = bf16(residual + x),
+// out = LayerNorm(residual) (else LayerNorm(x)); bf16 weight / bias [C], C % 8 == 0.
+void launch_layernorm(void* out, void* residual, const void* x, const void* w, const void* b, int rows, int C,
+                      float eps, hipStream_t s);
+void launch_gelu(void* x, long n, bool tanh_approx, hipStream_t s);
+// qkv [T, 3 nh D]: 2D RoPE of q, k in place (fp32 table [T, D]), then bidirectional attention
+// within each segment [cu[i], cu[i+1]) -> out [T, nh D]; tiles [ntiles, 2] = (segment, first row)
+// in steps of 128 rows.
+void launch_vision_attention(void* out, void* qkv, const float* cos_sin, const int* cu, const int* tiles,
+                             int ntiles, int T, int nh, int D, float scale, hipStream_t s);
+}  // namespace hipserve

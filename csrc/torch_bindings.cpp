@@ -758,6 +758,51 @@ void moe_combine_partial(at::Tensor& out, const at::Tensor& ws, const at::Tensor
                                        w.data_ptr<float>(), pair_slot.data_ptr<int>(), T, k, H, cur_stream());
 }
 
+// ---- vision tower (vision.hip)
+void layernorm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+               const c10::optional<at::Tensor>& residual, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_CONTIG(x); CHECK_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && out.sizes() == x.sizes(), "layernorm: x, out [rows, C]");
+  const int C = x.size(1);
+  TORCH_CHECK(C % 8 == 0 && C <= 8192, "layernorm: C must be a multiple of 8, <= 8192");
+  TORCH_CHECK(w.numel() == C && b.numel() == C && w.scalar_type() == at::kBFloat16 &&
+              b.scalar_type() == at::kBFloat16 && w.is_contiguous() && b.is_contiguous(),
+              "layernorm: bf16 weight and bias [C]");
+  void* r = nullptr;
+  if (residual.has_value()) {
+    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->sizes() == x.sizes(), "layernorm: residual [rows, C]");
+    r = residual->data_ptr();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_layernorm(out.data_ptr(), r, x.data_ptr(), w.data_ptr(), b.data_ptr(), x.size(0), C, (float)eps,
+                             cur_stream());
+}
+
+void gelu_(at::Tensor& x, bool tanh_approx) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.numel() % 8 == 0, "gelu_: numel must be a multiple of 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_gelu(x.data_ptr(), x.numel(), tanh_approx, cur_stream());
+}
+
+void vision_attention(at::Tensor& out, at::Tensor& qkv, const at::Tensor& cos_sin, const at::Tensor& cu,
+                      const at::Tensor& tiles, int64_t nh, int64_t D, double scale) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_BF16(out); CHECK_CONTIG(qkv); CHECK_CONTIG(out);
+  TORCH_CHECK(D % 8 == 0 && D >= 16 && D <= 128, "vision_attention: head_dim must be a multiple of 8 in [16, 128]");
+  const int T = qkv.size(0);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 3 * nh * D, "vision_attention: qkv [T, 3 * nh * D]");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == T && out.size(1) == nh * D, "vision_attention: out [T, nh * D]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.dim() == 2 &&
+              cos_sin.size(0) >= T && cos_sin.size(1) == D, "vision_attention: fp32 cos_sin [T, D]");
+  TORCH_CHECK(cu.scalar_type() == at::kInt && tiles.scalar_type() == at::kInt && tiles.dim() == 2 &&
+              tiles.size(1) == 2 && cu.is_contiguous() && tiles.is_contiguous(),
+              "vision_attention: int32 cu_seqlens and tiles [n, 2]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  hipserve::launch_vision_attention(out.data_ptr(), qkv.data_ptr(), cos_sin.data_ptr<float>(), cu.data_ptr<int>(),
+                                    tiles.data_ptr<int>(), tiles.size(0), T, nh, D, (float)scale, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
@@ -807,11 +852,17 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("penalty_update(Tensor tok, Tensor slot, Tensor(a!) counts, Tensor(b!) seen) -> ()");
   m.def("penalty_init(Tensor(a!) counts, Tensor(b!) seen, Tensor slots, Tensor off, Tensor n_prompt, Tensor toks) -> ()");
   m.def("top_logprobs(Tensor logits, Tensor nreq, Tensor(a!) out_ids, Tensor(b!) out_lp) -> ()");
+  m.def("layernorm(Tensor(a!) out, Tensor x, Tensor w, Tensor b, Tensor(b!)? residual, float eps) -> ()");
+  m.def("gelu_(Tensor(a!) x, bool tanh_approx) -> ()");
+  m.def("vision_attention(Tensor(a!) out, Tensor(b!) qkv, Tensor cos_sin, Tensor cu, Tensor tiles, int nh, int D, float scale) -> ()");
   m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("rmsnorm", &rmsnorm);
+  m.impl("layernorm", &layernorm);
+  m.impl("gelu_", &gelu_);
+  m.impl("vision_attention", &vision_attention);
   m.impl("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.impl("silu_and_mul", &silu_and_mul);
   m.impl("gelu_and_mul", &gelu_and_mul);

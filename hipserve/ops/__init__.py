@@ -113,6 +113,32 @@ class KernelOps:
     def top_logprobs(self, logits, nreq, out_ids, out_lp):
         self._op.top_logprobs(logits, nreq, out_ids, out_lp)
 
+    # ---- vision tower (csrc/kernels/vision.hip)
+    def layernorm(self, out, x, w, b, eps, residual=None):
+        self._op.layernorm(out, x, w, b, residual, eps)
+        return out
+
+    def gelu_(self, x, tanh):
+        self._op.gelu_(x, tanh)
+        return x
+
+    VISION_TILE = 128  # query rows per attention workgroup (4 waves x 32)
+
+    def vision_meta(self, geo, nh, D):
+        """(cu_seqlens, tiles) device tensors of an image batch for vision_attention."""
+        import numpy as np
+
+        cu = geo.cu_seqlens
+        tiles = np.array([(s, r) for s in range(len(cu) - 1) for r in range(0, int(cu[s + 1] - cu[s]),
+                                                                          self.VISION_TILE)], np.int32)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        return (torch.from_numpy(cu.astype(np.int32)).to(dev), torch.from_numpy(tiles.reshape(-1, 2)).to(dev))
+
+    def vision_attention(self, out, qkv, cos_sin, cu_seqlens, nh, D, scale, meta=None):
+        cu, tiles = meta
+        self._op.vision_attention(out, qkv, cos_sin, cu, tiles, nh, D, scale)
+        return out
+
 
 class ReferenceOps:
     """PyTorch reference path (CPU plumbing engine / numerics oracle)."""
