@@ -14,7 +14,11 @@
 //    exchange). K rows of each 16-key group sit in LDS with key bits 2 and 3 swapped,
 //    so the S^T accumulator holds 8 consecutive keys per MFMA k-slot and feeds
 //    O^T = V^T . P^T as the B operand without lane movement; V^T is transposed into
-//    LDS by the staging stores (b16 writes), read back as one ds_read_b128 per slot.
+//    LDS by the staging stores (each thread packs one d of two keys into a dword: a
+//    wave's stores cover all 64 banks), read back as one ds_read_b128 per slot.
+//  * at most 256 VGPRs (amdgpu_waves_per_eu 2): two waves per SIMD hide the
+//    dependent-MFMA and softmax latency (278 registers gave one wave per SIMD and
+//    4.4x less throughput).
 //  * d is zero-padded to a multiple of 16 for QK (KS k-steps) and of 32 for PV (NB
 //    row blocks); the padding rows of V^T are zeroed once, Q/K padding is loaded as 0.
 //  * online softmax in the log2 domain; only the segment's last tile is masked.
@@ -168,7 +172,7 @@ typedef unsigned short u16x4v __attribute__((ext_vector_type(4)));
 constexpr int VA_KT = 64, VA_NWV = 4, VA_NT = 64 * VA_NWV;
 
 template <int KS, int NB>
-__global__ __launch_bounds__(VA_NT) void vision_attn_kernel(unsigned short* __restrict__ out,
+__global__ __launch_bounds__(VA_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) void vision_attn_kernel(unsigned short* __restrict__ out,
                                                             const unsigned short* __restrict__ qkv,
                                                             const int* __restrict__ cu,
                                                             const int* __restrict__ tiles, int nh, int D,
@@ -177,7 +181,9 @@ __global__ __launch_bounds__(VA_NT) void vision_attn_kernel(unsigned short* __re
   constexpr int KLD = DK + 8, VLD = VA_KT + 8;
   constexpr int KPR = DK / 8;                          // 16-byte K pieces per key row
   constexpr int NPK = (VA_KT * KPR + VA_NT - 1) / VA_NT;
-  constexpr int NPV = (VA_KT * (DV / 8) + VA_NT - 1) / VA_NT;
+  // V staging items: (key pair, 8-d piece); a thread loads the piece of both keys and
+  // writes 8 dwords of V^T (d, key pair) — a wave's 32 key pairs x 2 pieces hit 64 banks
+  constexpr int NPV = (VA_KT / 2 * (DV / 8) + VA_NT - 1) / VA_NT;
   __shared__ __attribute__((aligned(16))) unsigned short kl[2][VA_KT * KLD];
   __shared__ __attribute__((aligned(16))) unsigned short vl[2][DV * VLD];
 
@@ -201,8 +207,8 @@ __global__ __launch_bounds__(VA_NT) void vision_attn_kernel(unsigned short* __re
     vl[bsel][D * VLD + rem] = 0;
   }
 
-  u16x8 ska[NPK], sva[NPV], skb[NPK], svb[NPV];
-  auto stage_load = [&](u16x8(&sk)[NPK], u16x8(&sv)[NPV], int kt) {
+  u16x8 ska[NPK], sva[NPV][2], skb[NPK], svb[NPV][2];
+  auto stage_load = [&](u16x8(&sk)[NPK], u16x8(&sv)[NPV][2], int kt) {
     const int kb = kt * VA_KT;
 #pragma unroll
     for (int i = 0; i < NPK; ++i) {
@@ -216,14 +222,17 @@ __global__ __launch_bounds__(VA_NT) void vision_attn_kernel(unsigned short* __re
 #pragma unroll
     for (int i = 0; i < NPV; ++i) {
       const int p = tid + VA_NT * i;
-      const int key = p / (DV / 8), pc = p - key * (DV / 8);
-      const int kk = min(kb + key, len - 1);
-      u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (p < VA_KT * (DV / 8) && pc < nvp) z = *reinterpret_cast<const u16x8*>(vbase_p + (long)kk * rs + 8 * pc);
-      sv[i] = z;
+      const int kp = p & 31, pc = p >> 5;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int kk = min(kb + 2 * kp + e, len - 1);
+        u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (pc < nvp) z = *reinterpret_cast<const u16x8*>(vbase_p + (long)kk * rs + 8 * pc);
+        sv[i][e] = z;
+      }
     }
   };
-  auto stage_store = [&](const u16x8(&sk)[NPK], const u16x8(&sv)[NPV], int buf) {
+  auto stage_store = [&](const u16x8(&sk)[NPK], const u16x8(&sv)[NPV][2], int buf) {
 #pragma unroll
     for (int i = 0; i < NPK; ++i) {
       const int p = tid + VA_NT * i;
@@ -236,10 +245,12 @@ __global__ __launch_bounds__(VA_NT) void vision_attn_kernel(unsigned short* __re
 #pragma unroll
     for (int i = 0; i < NPV; ++i) {
       const int p = tid + VA_NT * i;
-      const int key = p / (DV / 8), pc = p - key * (DV / 8);
-      if (p < VA_KT * (DV / 8) && pc < nvp) {
+      const int kp = p & 31, pc = p >> 5;
+      if (pc < nvp) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) vl[buf][(8 * pc + j) * VLD + key] = sv[i][j];
+        for (int j = 0; j < 8; ++j)
+          *reinterpret_cast<unsigned int*>(&vl[buf][(8 * pc + j) * VLD + 2 * kp]) =
+              (unsigned int)sv[i][0][j] | ((unsigned int)sv[i][1][j] << 16);
       }
     }
   };
