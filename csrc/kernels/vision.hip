@@ -148,23 +148,34 @@ void launch_gelu(void* x, long n, bool tanh_approx, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- 2D RoPE (q, k in place)
-// one thread per (token, q|k head, rotary pair); table row t = [cos(D/2) | sin(D/2)]
+// one thread per (token, q|k head): the head's D values in registers (16-byte loads),
+// rotate-half pairs (j, j + D/2) against the token's table row [cos(D/2) | sin(D/2)]
+template <int D>
 __global__ __launch_bounds__(256) void vision_rope_kernel(unsigned short* __restrict__ qkv,
-                                                          const float* __restrict__ cos_sin, int T, int nh,
-                                                          int D) {
-  const int half = D >> 1;
+                                                          const float* __restrict__ cos_sin, int T, int nh) {
+  constexpr int NV = D / 8, H = D / 2;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const long per_tok = 2L * nh * half;
-  if (i >= (long)T * per_tok) return;
-  const int t = (int)(i / per_tok);
-  const int rem = (int)(i - (long)t * per_tok);
-  const int head = rem / half, j = rem - head * half;  // head in [0, 2 nh): q heads then k heads
-  unsigned short* p = qkv + (long)t * 3 * nh * D + (long)head * D;
-  const float c = cos_sin[(long)t * D + j], sn = cos_sin[(long)t * D + half + j];
-  float ra, rb;
-  rope_rot(bf16_to_f32(p[j]), bf16_to_f32(p[j + half]), c, sn, ra, rb);
-  p[j] = f32_to_bf16(ra);
-  p[j + half] = f32_to_bf16(rb);
+  if (i >= 2L * T * nh) return;
+  const int t = (int)(i / (2 * nh)), head = (int)(i - (long)t * 2 * nh);  // q heads then k heads
+  u16x8* p = reinterpret_cast<u16x8*>(qkv + (long)t * 3 * nh * D + (long)head * D);
+  const float* cs = cos_sin + (long)t * D;
+  float x[D];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const u16x8 a = p[v];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[8 * v + j] = bf16_to_f32(a[j]);
+  }
+  float y[D];
+#pragma unroll
+  for (int j = 0; j < H; ++j) rope_rot(x[j], x[j + H], cs[j], cs[H + j], y[j], y[j + H]);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(y[8 * v + j]);
+    p[v] = o;
+  }
 }
 
 // ---------------------------------------------------------------- attention
@@ -377,8 +388,15 @@ void launch_vision_attention(void* out, void* qkv, const float* cos_sin, const i
                              int ntiles, int T, int nh, int D, float scale, hipStream_t s) {
   if (T <= 0 || ntiles <= 0) return;
   auto* q = static_cast<unsigned short*>(qkv);
-  const long nrot = (long)T * nh * D;  // 2 * nh * (D/2) rotary pairs per token
-  vision_rope_kernel<<<(unsigned)((nrot + 255) / 256), 256, 0, s>>>(q, cos_sin, T, nh, D);
+  const unsigned rg = (unsigned)((2L * T * nh + 255) / 256);
+  switch (D) {
+    case 64: vision_rope_kernel<64><<<rg, 256, 0, s>>>(q, cos_sin, T, nh); break;
+    case 72: vision_rope_kernel<72><<<rg, 256, 0, s>>>(q, cos_sin, T, nh); break;
+    case 80: vision_rope_kernel<80><<<rg, 256, 0, s>>>(q, cos_sin, T, nh); break;
+    case 96: vision_rope_kernel<96><<<rg, 256, 0, s>>>(q, cos_sin, T, nh); break;
+    case 128: vision_rope_kernel<128><<<rg, 256, 0, s>>>(q, cos_sin, T, nh); break;
+    default: vision_rope_kernel<16><<<rg, 256, 0, s>>>(q, cos_sin, T, nh); break;
+  }
   dim3 grid(ntiles, nh);
   auto* o = static_cast<unsigned short*>(out);
 #define VA_LAUNCH(ks, nb) vision_attn_kernel<ks, nb><<<grid, VA_NT, 0, s>>>(o, q, cu, tiles, nh, D, scale)

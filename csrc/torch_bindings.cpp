@@ -789,7 +789,8 @@ void gelu_(at::Tensor& x, bool tanh_approx) {
 void vision_attention(at::Tensor& out, at::Tensor& qkv, const at::Tensor& cos_sin, const at::Tensor& cu,
                       const at::Tensor& tiles, int64_t nh, int64_t D, double scale) {
   CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_BF16(out); CHECK_CONTIG(qkv); CHECK_CONTIG(out);
-  TORCH_CHECK(D % 8 == 0 && D >= 16 && D <= 128, "vision_attention: head_dim must be a multiple of 8 in [16, 128]");
+  TORCH_CHECK(D == 16 || D == 64 || D == 72 || D == 80 || D == 96 || D == 128,
+              "vision_attention: head_dim must be one of 16, 64, 72, 80, 96, 128");
   const int T = qkv.size(0);
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 3 * nh * D, "vision_attention: qkv [T, 3 * nh * D]");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == T && out.size(1) == nh * D, "vision_attention: out [T, nh * D]");

@@ -308,6 +308,15 @@ PRESETS: dict[str, ModelConfig] = {
                                  num_experts_per_tok=8, norm_topk_prob=True, vocab_size=151936,
                                  rms_norm_eps=1e-6, rope_theta=1e6, max_position_embeddings=40960,
                                  qk_norm=True, bos_token_id=None, eos_token_id=(151643, 151645)),
+    # the reference's default HF model (vllm-models/helm-chart/values.yaml:8-12) with its
+    # vision tower: Qwen3-VL-30B-A3B (text = Qwen3-30B-A3B with interleaved MRoPE)
+    "qwen3-vl-30b-a3b": ModelConfig(name="qwen3-vl-30b-a3b", architecture="mixtral", family="qwen3_moe",
+                                    hidden_size=2048, num_layers=48, num_heads=32, num_kv_heads=4, head_dim=128,
+                                    intermediate_size=6144, moe_intermediate_size=768, num_experts=128,
+                                    num_experts_per_tok=8, norm_topk_prob=True, vocab_size=151936,
+                                    rms_norm_eps=1e-6, rope_theta=5e6, max_position_embeddings=262144,
+                                    qk_norm=True, bos_token_id=None, eos_token_id=(151643, 151645),
+                                    mrope_section=(24, 20, 20), vision=VisionConfig()),
     "gemma-3-27b": ModelConfig(name="gemma-3-27b", family="gemma3", hidden_size=5376, num_layers=62,
                                num_heads=32, num_kv_heads=16, head_dim=128, intermediate_size=21504,
                                vocab_size=262208, rms_norm_eps=1e-6, rope_theta=1e6,
