@@ -258,3 +258,71 @@ def test_chat_endpoint_with_image(tmp_path):
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+def _tp_worker(rank, world, port, ckpt, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from hipserve.config import resolve_model_config
+    from hipserve.engine.llm_engine import worker_loop
+    from hipserve.engine.model_runner import ModelRunner
+    from hipserve.parallel.comm import init_tp
+
+    tp = init_tp(world, backend="gloo", device_type="cpu")
+    cfg = _tp_cfg(ckpt, world)
+    try:
+        if rank == 0:
+            eng = LLMEngine(cfg, tp=tp)
+            q.put(_tp_generate(eng))
+            eng.shutdown()
+        else:
+            worker_loop(ModelRunner(cfg, resolve_model_config(ckpt), tp), tp)
+    finally:
+        dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def _tp_cfg(ckpt, tp):
+    return EngineConfig(model=ckpt, device="cpu", dtype="float32", tensor_parallel_size=tp, num_kv_blocks=128,
+                        max_model_len=256, max_num_batched_tokens=20, max_num_seqs=4)
+
+
+def _tp_generate(eng):
+    vc = _vcfg(eng.model_cfg)
+    ims = [preprocess_image(_image(20, 96, 64), vc), preprocess_image(_image(21, 64, 64), vc)]
+    sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    res = eng.generate([MultiModalPrompt(_prompt(ims, vc), ims), [1, 2, 3, 4, 5]], sp)
+    return [r[0] for r in res]
+
+
+def test_tp2_with_images_matches_tp1(tmp_path):
+    """TP=2 over gloo (rank 0 schedules; pixels travel in the step broadcast; every
+    rank runs the replicated vision tower; DeepStack features enter the row-parallel
+    partial sum on rank 0 only) generates exactly the TP=1 tokens."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    _, ckpt = _hf_model(tmp_path)
+    want = _tp_generate(LLMEngine(_tp_cfg(ckpt, 1), tp=TPGroup()))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, ckpt, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want
