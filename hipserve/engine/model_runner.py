@@ -116,6 +116,9 @@ class ModelRunner:
                 from ..ops import quant as Q
 
                 self.gguf_split_report = Q.tune_splits(qws, self.device, [m for m in Q.M_BUCKETS if m <= 64])
+                if ecfg.extra.get("quant_dense_shadow", True):
+                    total = torch.cuda.get_device_properties(self.device).total_memory
+                    self.quant_shadow_bytes = Q.make_dense_shadows(qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()
         # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
         # budget (measured no faster than the heuristic on sustained prefill chains,

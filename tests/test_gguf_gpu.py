@@ -378,3 +378,18 @@ def test_int8_pack_quantized_checkpoint_native(tmp_path):
         eng.shutdown()
     a, b = torch.cat(got[True]), torch.cat(got[False])
     assert (a - b).abs().max().item() < 5e-2 * b.abs().max().item() + 1e-3
+
+
+def test_dense_shadow_prefill_matches_dequant_path():
+    """Prefill on the resident bf16 shadow (make_dense_shadows) is bit-identical to the
+    per-call dequant-into-scratch path; decode-sized batches keep the quantised kernel."""
+    from hipserve.ops.quant import make_dense_shadows
+    qw, raws = _rand_qw([(G.Q4_K, 512, 2048), (G.Q6_K, 256, 2048)], seed=5)
+    x = torch.randn(300, 2048, device="cuda", dtype=torch.bfloat16)
+    want = quant_linear(x, qw)
+    xs = x[:16].contiguous()
+    want_small = quant_linear(xs, qw)
+    assert make_dense_shadows([qw], "cuda", 0) == qw.N * qw.K * 2 and qw.dense is not None
+    assert torch.equal(quant_linear(x, qw), want)
+    assert torch.equal(quant_linear(xs, qw), want_small)
+    assert torch.equal(qw.dense, dequantize(qw))
