@@ -113,7 +113,7 @@ def test_hf_virtualservice_order_and_ingress_emulation():
 
 
 def test_hf_nginx_router_fixed_config():
-    docs = render(HF)
+    docs = render(HF, {"apiGateway": {"kind": "nginx"}})
     cm = by_kind(docs, "ConfigMap")["hipserve-api-gateway-config"]
     conf = cm["data"]["nginx.conf"]
     for needle in ("proxy_buffering off;", "proxy_http_version 1.1;", "client_max_body_size 0;",
@@ -124,8 +124,8 @@ def test_hf_nginx_router_fixed_config():
     assert conf.count("{") == conf.count("}")
 
 
-def test_hf_hipserve_router_variant():
-    docs = render(HF, {"apiGateway": {"kind": "hipserve"}}, ns="prod")
+def test_hf_hipserve_router_default():
+    docs = render(HF, {}, ns="prod")
     cm = by_kind(docs, "ConfigMap")["hipserve-api-gateway-config"]
     backends = json.loads(cm["data"]["backends.json"])
     assert [b["name"] for b in backends] == ["llama-3-8b", "mixtral-8x7b"]
