@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
     ap.add_argument("--enforce-eager", action="store_true")
-    ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0", "fp8"],
+    ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0", "fp8", "int8"],
                     help="GGUF tier: random-init GGUF-quantised weights (BASELINE config: Llama-3-8B Q4_K_M)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -235,13 +235,15 @@ def main():
         "vs_baseline": None,
         "dtype": ("bf16" if cuda else "fp32") if not args.quantization else (
             "bf16 activations, FP8 e4m3 weights (per-channel scales)" if args.quantization == "fp8"
+            else "bf16 activations, INT8 weight-only (per-channel scales)" if args.quantization == "int8"
             else f"bf16 activations, GGUF {args.quantization.upper()} weights"),
         "data": "synthetic prompts (random token ids), random-init weights",
         "p50_ttft_ms": round(1000 * float(p50), 2),
         "load": f"open-loop Poisson {args.request_rate} req/s" if args.request_rate else "closed-loop waves",
         "path": args.path,
         "config": {
-            "model": args.model + ((" FP8" if args.quantization == "fp8" else f" GGUF {args.quantization.upper()}")
+            "model": args.model + ((" FP8" if args.quantization == "fp8" else " INT8" if args.quantization == "int8"
+                                    else f" GGUF {args.quantization.upper()}")
                                    if args.quantization else ""),
             "tp": args.tp,
             "global_batch": args.concurrency * (world // args.tp),

@@ -93,6 +93,14 @@ int gguf_tiled_chunk_bytes(int qtype);
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s);
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s);
+// quantised MoE experts (tiled layout per expert, stacked [E][N/16][K/256][chunk]) over
+// moe_align tiles of 16/32/64 slots: out[slot, N] bf16 (S == 1) or ws[S, nslots, N] fp32.
+// qtype: FP8 (rs [E, N]) or INT8 (the checkpoint expert formats). Returns false for an
+// unsupported tile / qtype.
+bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* q,
+                      const float* rs, int qtype, long w_estride, long rs_estride, const int* slots,
+                      const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, int S,
+                      hipStream_t s);
 
 }  // namespace hipserve
 

@@ -117,6 +117,17 @@ struct Parts {
   Part p[kMaxParts];
   int n;
 };
+// MoE expert tiles (moe_align, moe.hip): the workgroup's blockIdx.z is one tile of
+// 16 * MT expert-sorted pair slots; its x rows are gathered (token = pair / gather_k,
+// or the slot itself for w2 over the activations) and its outputs land on slot rows
+struct MoeQ {
+  const int* slots;        // [nslots] pair index (token * k + j) or -1 (padding)
+  const int* tile_expert;  // [tiles_cap] expert of each tile, -1 past the last tile
+  long w_estride;          // bytes of one expert's tiled weight
+  long rs_estride;         // floats of one expert's row scales (FP8), 0 otherwise
+  int gather_k;            // > 0: x row = pair / gather_k; 0: x row = slot
+  int nslots;              // slot rows of out / of each ws split
+};
 
 template <int QT>
 HS_DEVICE void load_raw(const unsigned char* ch, int g, int c, int lane, Raw& r) {
@@ -374,10 +385,10 @@ HS_DEVICE _Float16 to_f16_sat(unsigned short b) {
 
 // One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
 // x staging. Body per format; the kernel picks it per part (two formats per launch).
-template <int QT, int MT, int RT, int NWAVES>
+template <int QT, int MT, int RT, int NWAVES, bool kMoe = false>
 HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short* __restrict__ out, long out_stride,
                            float* __restrict__ ws, const unsigned short* __restrict__ x, long x_stride,
-                           const Part& P, int M, int Ntot, int K, int sb_per_split) {
+                           const Part& P, int M, int Ntot, int K, int sb_per_split, const MoeQ& moe = MoeQ{}) {
   constexpr int XR = 16 * MT;           // staged x rows (M padded)
   constexpr int NT = 64 * NWAVES;
   constexpr int CB = chunk_bytes<QT>();
@@ -395,13 +406,25 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
   constexpr int XP = XR * 32 / NT;
   static_assert(XP * NT == XR * 32, "x staging must divide evenly (no guarded, sinkable loads)");
   u16x8 xv[XP];
+  const int mrow0 = kMoe ? (int)blockIdx.z * XR : 0;  // kMoe: first slot of the expert tile
+  [[maybe_unused]] const unsigned short* xg[kMoe ? XP : 1];  // kMoe: gathered row of each staging item
+  if constexpr (kMoe) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int slot = mrow0 + ((i * NT + tid) >> 5), pr = moe.slots[slot];
+      xg[i] = x + (pr < 0 ? 0L : (long)(moe.gather_k > 0 ? pr / moe.gather_k : slot)) * x_stride;
+    }
+  }
   auto load_x = [&](int sb) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
       const int kb = kbase<QT>(fr >> 3, fr & 7);
-      // rows >= M are clamped, never stored
-      xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + sb * 256 + kb);
+      // rows >= M are clamped, never stored (kMoe: padding slots read row 0, never stored)
+      if constexpr (kMoe)
+        xv[i] = *reinterpret_cast<const u16x8*>(xg[i] + sb * 256 + kb);
+      else
+        xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + sb * 256 + kb);
     }
   };
   auto store_x = [&](int buf) {
@@ -482,10 +505,17 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
     }
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const int m = 16 * t + c;
-      if (m >= M) continue;
+      int m = 16 * t + c;
+      long wrow = (long)blockIdx.y * M + m;
+      if constexpr (kMoe) {
+        m += mrow0;  // output row = slot
+        if (moe.slots[m] < 0) continue;
+        wrow = (long)blockIdx.y * moe.nslots + m;
+      } else if (m >= M) {
+        continue;
+      }
       if (ws != nullptr) {
-        *reinterpret_cast<f32x4*>(ws + ((long)blockIdx.y * M + m) * Ntot + col) = acc[r][t];
+        *reinterpret_cast<f32x4*>(ws + wrow * Ntot + col) = acc[r][t];
       } else {
         uint2 v;
         v.x = pack_bf16x2(acc[r][t][0], acc[r][t][1]);
@@ -542,6 +572,42 @@ void launch_t(void* out, long out_stride, float* ws, const void* x, long x_strid
     qgemm2_kernel<QA, QB, 4, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
   else  // 8 waves x 1 row group: half the accumulators and weight registers per wave
     qgemm2_kernel<QA, QB, 4, 1, 8><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+}
+
+// MoE experts: grid (row tiles of N, K splits, expert tiles); workgroups of tiles past
+// the last one (tile_expert -1) exit before any barrier
+template <int QT, int MT, int RT, int NWAVES>
+__global__ __launch_bounds__(64 * NWAVES) void qmoe_kernel(unsigned short* __restrict__ out, long out_stride,
+                                                          float* __restrict__ ws, const unsigned short* __restrict__ x,
+                                                          long x_stride, const unsigned char* __restrict__ q,
+                                                          const float* __restrict__ rs, MoeQ moe, int N, int K,
+                                                          int sb_per_split) {
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<MT>()];
+  const int e = moe.tile_expert[blockIdx.z];
+  if (e < 0) return;
+  const Part P{q + (long)e * moe.w_estride, rs != nullptr ? rs + (long)e * moe.rs_estride : nullptr, QT, N, 0, 0};
+  qgemm2_body<QT, MT, RT, NWAVES, true>(xs, out, out_stride, ws, x, x_stride, P, 16 * MT, N, K, sb_per_split, moe);
+}
+
+template <int QT>
+void moe_launch_t(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* q, const float* rs,
+                  const MoeQ& moe, int tiles_cap, int tile, int N, int K, int S, hipStream_t s) {
+  const int nsb = K / 256;
+  const int per = (nsb + S - 1) / S;
+  auto* o = static_cast<unsigned short*>(out);
+  auto* xi = static_cast<const unsigned short*>(x);
+  auto* qq = static_cast<const unsigned char*>(q);
+  const int ysplit = (nsb + per - 1) / per;
+  if (tile == 16) {
+    const dim3 grid((N + 127) / 128, ysplit, tiles_cap);
+    qmoe_kernel<QT, 1, 2, kWaves><<<grid, 64 * kWaves, 0, s>>>(o, out_stride, ws, xi, x_stride, qq, rs, moe, N, K, per);
+  } else if (tile == 32) {
+    const dim3 grid((N + 127) / 128, ysplit, tiles_cap);
+    qmoe_kernel<QT, 2, 2, kWaves><<<grid, 64 * kWaves, 0, s>>>(o, out_stride, ws, xi, x_stride, qq, rs, moe, N, K, per);
+  } else {
+    const dim3 grid((N + 127) / 128, ysplit, tiles_cap);
+    qmoe_kernel<QT, 4, 1, 8><<<grid, 512, 0, s>>>(o, out_stride, ws, xi, x_stride, qq, rs, moe, N, K, per);
+  }
 }
 
 // ---------------------------------------------------------------- tiled -> bf16
@@ -639,6 +705,19 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
       case INT8: launch_t<INT8, INT8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
     }
   }
+}
+
+bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* q,
+                      const float* rs, int qtype, long w_estride, long rs_estride, const int* slots,
+                      const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, int S,
+                      hipStream_t s) {
+  if (tile != 16 && tile != 32 && tile != 64) return false;
+  const MoeQ moe{slots, tile_expert, w_estride, rs_estride, gather_k, tiles_cap * tile};
+  switch (qtype) {
+    case FP8: moe_launch_t<FP8>(out, out_stride, ws, x, x_stride, q, rs, moe, tiles_cap, tile, N, K, S, s); return true;
+    case INT8: moe_launch_t<INT8>(out, out_stride, ws, x, x_stride, q, rs, moe, tiles_cap, tile, N, K, S, s); return true;
+  }
+  return false;
 }
 
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s) {

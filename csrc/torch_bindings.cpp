@@ -280,6 +280,47 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   return S;
 }
 
+int64_t qmoe_gemm(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const at::Tensor& q, const at::Tensor& rs,
+                  int64_t qtype, int64_t N, int64_t K, const at::Tensor& slots, const at::Tensor& tile_expert,
+                  int64_t tile, int64_t gather_k, int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x);
+  TORCH_CHECK(qtype == 6 || qtype == 8, "qmoe_gemm: expert formats FP8 (per-row scale) and INT8");
+  TORCH_CHECK(tile == 16 || tile == 32 || tile == 64, "qmoe_gemm: tile 16/32/64");
+  TORCH_CHECK(N % 16 == 0 && K % 256 == 0 && x.size(1) >= K && x.stride(0) % 8 == 0, "qmoe_gemm: shapes");
+  TORCH_CHECK(slots.scalar_type() == at::kInt && tile_expert.scalar_type() == at::kInt && slots.is_contiguous() &&
+              tile_expert.is_contiguous() && slots.numel() == tile_expert.numel() * tile,
+              "qmoe_gemm: int32 slots [tiles * tile] and tile_expert [tiles]");
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.is_contiguous() && q.dim() == 2 && q.device() == x.device(),
+              "qmoe_gemm: q uint8 [E, expert bytes]");
+  const long per_e = N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype);
+  TORCH_CHECK(q.size(1) == per_e, "qmoe_gemm: q rows are not tiled [N/16, K/256, chunk] experts");
+  const bool fp8 = qtype == 6;
+  TORCH_CHECK(!fp8 || (rs.scalar_type() == at::kFloat && rs.is_contiguous() && rs.dim() == 2 &&
+                       rs.size(0) == q.size(0) && rs.size(1) == N), "qmoe_gemm: FP8 experts need rs [E, N] fp32");
+  TORCH_CHECK(gather_k > 0 || x.size(0) >= slots.numel(), "qmoe_gemm: slot-indexed x needs a row per slot");
+  const int nsb = K / 256;
+  const int per = (nsb + splits - 1) / splits;
+  const int S = (nsb + per - 1) / per;
+  const long nslots = slots.numel();
+  float* wp = nullptr;
+  if (ws.numel() > 0) {
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= S * nslots * N &&
+                ws.device() == x.device(), "qmoe_gemm: ws must hold S * slots * N fp32");
+    wp = ws.data_ptr<float>();
+  } else {
+    TORCH_CHECK(S == 1, "qmoe_gemm: split-K needs a partial workspace");
+    CHECK_BF16(out); CHECK_ROWMAJOR(out);
+    TORCH_CHECK(out.size(0) == nslots && out.size(1) >= N && out.stride(0) % 4 == 0 && out.device() == x.device());
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_qmoe_gemm(wp ? nullptr : out.data_ptr(), wp ? 0 : out.stride(0), wp, x.data_ptr(),
+                                         x.stride(0), q.data_ptr(), fp8 ? rs.data_ptr<float>() : nullptr, qtype,
+                                         per_e, fp8 ? N : 0, slots.data_ptr<int>(), tile_expert.data_ptr<int>(),
+                                         tile_expert.numel(), tile, gather_k, N, K, splits, cur_stream()),
+              "qmoe_gemm: unsupported configuration");
+  return S;
+}
+
 void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& rs, int64_t qtype, int64_t N,
                         int64_t K) {
   CHECK_DEV(q); CHECK_BF16(out);
@@ -827,6 +868,7 @@ TORCH_LIBRARY(hipserve, m) {
   // custom all-reduce control ops carry an opaque state handle: catch-all kernels
   m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits) -> int", &gguf_gemm_parts);
   m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
+  m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits) -> int", &qmoe_gemm);
   m.def("car_create(int rank, int world, int max_bytes) -> int", &car_create);
   m.def("car_handle(int state) -> Tensor", &car_handle);
   m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);

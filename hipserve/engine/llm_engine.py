@@ -38,7 +38,7 @@ def prepare_model(cfg: EngineConfig, tp: TPGroup, model_cfg: ModelConfig | None 
         cfg = cfg.replace(model=path, served_model_name=cfg.served_model_name or cfg.model,
                           tokenizer=cfg.tokenizer if cfg.tokenizer and cfg.tokenizer != cfg.model else None)
     mcfg = model_cfg or resolve_model_config(cfg.model, cfg.served_model_name)
-    if cfg.extra.get("quantization") and cfg.extra["quantization"] != "fp8" and cfg.load_format == "dummy":
+    if cfg.extra.get("quantization") and cfg.extra["quantization"] not in ("fp8", "int8") and cfg.load_format == "dummy":
         # synthetic GGUF tier: ggml llama weights use interleaved-pair RoPE
         mcfg = mcfg.replace(rope_mode=1)
     tokenizer = get_tokenizer(cfg.model, mcfg, cfg.tokenizer)

@@ -111,6 +111,12 @@ class ModelRunner:
             self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms, fused=fused)
             if ecfg.extra.get("packed_decode", True):
                 self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
+            moes = self.model.quant_moes() if hasattr(self.model, "quant_moes") else []
+            if moes and ecfg.extra.get("quant_dense_shadow", True):  # bf16 experts for prefill
+                from ..ops import quant as Q
+
+                total = torch.cuda.get_device_properties(self.device).total_memory
+                self.quant_shadow_bytes = Q.make_moe_shadows(moes, self.device, (24 << 30) + total // 4)
             qws = self.model.quant_weights() if hasattr(self.model, "quant_weights") else []
             if qws:  # GGUF: split-K of the dequant-MFMA decode GEMM per shape and batch
                 from ..ops import quant as Q
@@ -118,7 +124,8 @@ class ModelRunner:
                 self.gguf_split_report = Q.tune_splits(qws, self.device, [m for m in Q.M_BUCKETS if m <= 64])
                 if ecfg.extra.get("quant_dense_shadow", True):
                     total = torch.cuda.get_device_properties(self.device).total_memory
-                    self.quant_shadow_bytes = Q.make_dense_shadows(qws, self.device, (24 << 30) + total // 4)
+                    self.quant_shadow_bytes = getattr(self, "quant_shadow_bytes", 0) + Q.make_dense_shadows(
+                        qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()
         # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
         # budget (measured no faster than the heuristic on sustained prefill chains,

@@ -231,8 +231,8 @@ class LlamaModel:
         from ..ops import quant as Q
         from ..weights import gguf as G
 
-        if scheme.lower() == "fp8":
-            return self.allocate_random_fp8(seed)
+        if scheme.lower() in ("fp8", "int8"):
+            return self.allocate_random_fp8(seed, scheme.lower())
         if self.tp.world_size != 1:
             raise NotImplementedError("the GGUF tier runs TP=1 (one device per pod, like llama-server)")
         types = self.QUANT_SCHEMES[scheme.lower()]
@@ -265,30 +265,43 @@ class LlamaModel:
                 wgu=mat(("gate", I, H), ("up", I, H)), wd=mat(("down", H, I))))
         self.quant_linear = Q.quant_linear
 
-    def allocate_random_fp8(self, seed: int = 0):
-        """Random-init model whose projections are FP8 e4m3 with per-output-channel
-        scales (the layout of the reference's "FP8-Dynamic" checkpoints, kept native:
-        ops/quant.py QuantWeight, FP8 format). Embeddings, norms and lm_head stay bf16
-        (the checkpoints' ``ignore`` list). Off the GPU the same e4m3 values are
+    def allocate_random_fp8(self, seed: int = 0, kind: str = "fp8"):
+        """Random-init model whose projections are 8-bit weights with per-output-channel
+        scales, kept native in HBM (ops/quant.py): ``fp8`` = e4m3 (the layout of the
+        reference's "FP8-Dynamic" checkpoints), ``int8`` = symmetric int8 weight-only
+        (the reference's AWQ-8bit export). MoE experts become ``QuantMoE`` stacks for
+        the quantised expert GEMM. Embeddings, norms, router and lm_head stay bf16 (the
+        checkpoints' ``ignore`` list). Off the GPU the same 8-bit values are
         dequantised to dense weights."""
         from ..ops import quant as Q
 
         self.allocate_random(seed=seed)  # norms, embeddings, lm_head, bf16 projections (replaced below)
         dev = self.device
-        g = torch.Generator(device=dev).manual_seed(seed + 1)
 
-        def fp8(w):
-            s = w.float().abs().amax(1, keepdim=True).clamp_min(1e-12) / 448.0
-            q = (w.float() / s).to(torch.float8_e4m3fn)
-            if dev.type == "cuda" and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0:
-                return Q.QuantPart.from_fp8(q, s, dev)
-            return (q.float() * s).to(self.dtype)
+        def q8(w):  # -> (QuantPart or None, dequantised dense)
+            wf = w.float()
+            if kind == "int8":
+                s = wf.abs().amax(1, keepdim=True).clamp_min(1e-12) / 127.0
+                qi = torch.round(wf / s).clamp(-127, 127)
+                dense = (qi * s).to(self.dtype)
+                ok = dev.type == "cuda" and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0
+                return (Q.QuantPart.from_int8((qi + 128).to(torch.uint8), s, None, dev) if ok else None), dense
+            s = wf.abs().amax(1, keepdim=True).clamp_min(1e-12) / 448.0
+            q = (wf / s).to(torch.float8_e4m3fn)
+            ok = dev.type == "cuda" and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0
+            return (Q.QuantPart.from_fp8(q, s, dev) if ok else None), (q.float() * s).to(self.dtype)
 
         def quant(w, splits):
-            parts = [fp8(t) for t in torch.split(w, splits, 0)]
-            if all(isinstance(p, Q.QuantPart) for p in parts):
-                return Q.QuantWeight(parts)
-            return torch.cat([p if isinstance(p, torch.Tensor) else Q.dequantize(Q.QuantWeight([p])) for p in parts])
+            parts = [q8(t) for t in torch.split(w, splits, 0)]
+            if all(p is not None for p, _ in parts):
+                return Q.QuantWeight([p for p, _ in parts])
+            return torch.cat([d for _, d in parts])
+
+        def experts(w):
+            parts = [q8(w[e]) for e in range(w.shape[0])]
+            if all(p is not None for p, _ in parts) and Q.QuantMoE.supported(parts[0][0].kqt, *w.shape[1:]):
+                return Q.QuantMoE([p for p, _ in parts])
+            return torch.stack([d for _, d in parts])
 
         D = self.D
         for lw in self.layers:
@@ -297,10 +310,16 @@ class LlamaModel:
             if lw.wgu is not None:
                 lw.wgu = quant(lw.wgu, [self.inter, self.inter])
                 lw.wd = quant(lw.wd, [lw.wd.shape[0]])
-        del g
+            if lw.w13 is not None:
+                lw.w13, lw.w2 = experts(lw.w13), experts(lw.w2)
         if dev.type == "cuda":
             torch.cuda.empty_cache()
         self.quant_linear = Q.quant_linear
+
+    def quant_moes(self) -> list:
+        """Every quantised expert stack (QuantMoE)."""
+        from ..ops import quant as Q
+        return [w for lw in self.layers for w in (lw.w13, lw.w2) if isinstance(w, Q.QuantMoE)]
 
     # ---------------------------------------------------------------- forward
     def linear(self, x: torch.Tensor, w, name: str | None = None) -> torch.Tensor:
@@ -624,6 +643,13 @@ class LlamaModel:
         k = cfg.num_experts_per_tok
         T = x.shape[0]
         P = T * k
+        if not isinstance(lw.w13, torch.Tensor):  # quantised experts (ops/quant.py QuantMoE)
+            if P <= MOE_KERNEL_MAX_PAIRS:
+                return self.moe_quant(x, lw)
+            from ..ops import quant as Q
+
+            lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router,
+                              w13=Q.moe_dense(lw.w13, 0), w2=Q.moe_dense(lw.w2, 1))
         if (self.ops.name == "hip" and cfg.num_experts <= 128 and cfg.hidden_size % 256 == 0
                 and self.inter % 256 == 0
                 and (P <= MOE_KERNEL_MAX_PAIRS
@@ -769,6 +795,47 @@ class LlamaModel:
         y = torch.empty(cap, H, dtype=x.dtype, device=dev)
         op.moe_gemm(y, act, lw.w2, slots, tile_expert, tile, 0)
         op.moe_combine(out, y, w, pair_slot, k)
+        return out
+
+    def moe_quant(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
+        """Decode-sized MoE on quantised experts (INT8 / FP8, ``QuantMoE``): routing and
+        expert-sorted tiles as ``moe_hip``, then the dequant-MFMA expert GEMM in its
+        MoE mode (gathered token rows, one expert's weight stream per workgroup) for
+        w13, SiLU-GLU, and w2 (split over K into fp32 partials summed by the
+        weighted combine). No host synchronisation (graph-capturable)."""
+        op = torch.ops.hipserve
+        cfg = self.cfg
+        E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
+        T, dev = x.shape[0], x.device
+        P = T * k
+        tile = 16 if P <= 8 * E else (32 if P <= 32 * E else 64)
+        cap = -(-(P + E * (tile - 1)) // tile) * tile
+        logits = gemm.linear(x, lw.router)
+        w = torch.empty(T, k, dtype=torch.float32, device=dev)
+        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
+        op.moe_topk_softmax(w, ids, logits, k, cfg.norm_topk_prob)
+        slots = torch.empty(cap, dtype=torch.int32, device=dev)
+        tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
+        ntiles = torch.empty(1, dtype=torch.int32, device=dev)
+        pair_slot = torch.empty(P, dtype=torch.int32, device=dev)
+        op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot)
+        w13, w2 = lw.w13, lw.w2
+        f32 = torch.empty(0, dtype=torch.float32, device=dev)
+        gu = torch.empty(cap, w13.N, dtype=x.dtype, device=dev)
+        op.qmoe_gemm(gu, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1)
+        act = torch.empty(cap, w13.N // 2, dtype=x.dtype, device=dev)
+        self.act_and_mul(act, gu)
+        out = torch.empty(T, H, dtype=x.dtype, device=dev)
+        active = min(E, cap // tile, P)
+        S = self._moe_w2_splits(w2.K, -(-H // 128), active)
+        if S <= 1:
+            y = torch.empty(cap, H, dtype=x.dtype, device=dev)
+            op.qmoe_gemm(y, f32, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, 1)
+            op.moe_combine(out, y, w, pair_slot, k)
+            return out
+        ws = torch.empty(S, cap, H, dtype=torch.float32, device=dev)
+        S = op.qmoe_gemm(out, ws, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, S)
+        op.moe_combine_partial(out, ws[:S], w, pair_slot, k)
         return out
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

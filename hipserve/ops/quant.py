@@ -519,3 +519,71 @@ def make_dense_shadows(weights, device, reserve_bytes: int) -> int:
         w.dense = dequantize(w)
         added += need
     return added
+
+
+class QuantMoE:
+    """The quantised experts of one MoE projection, stacked for the expert GEMM
+    (``qmoe_gemm``, gguf_mfma.hip MoE mode): ``q`` uint8 [E, N/16 * K/256 * chunk]
+    (each expert in the v2 tiled layout), FP8 row scales ``rs`` [E, N]. INT8
+    (compressed-tensors 8-bit, the reference's AWQ-8bit export) and per-channel FP8
+    experts; prefill runs bf16 expert GEMMs on ``dense`` (a resident shadow when HBM
+    allows, else a per-call dequantised scratch)."""
+
+    KERNEL_QTS = (6, 8)  # FP8 (per-row scale), INT8
+
+    def __init__(self, parts: list):
+        p0 = parts[0]
+        assert all(p.kqt == p0.kqt and p.N == p0.N and p.K == p0.K and p.tiled for p in parts)
+        self.E, self.N, self.K, self.kqt = len(parts), p0.N, p0.K, p0.kqt
+        self.q = torch.stack([p.q.reshape(-1) for p in parts]).contiguous()
+        self.rs = (torch.stack([p.rs for p in parts]).contiguous() if p0.kqt == 6
+                   else torch.empty(0, 0, dtype=torch.float32, device=p0.q.device))
+        self.dense = None
+
+    @property
+    def shape(self):
+        return (self.E, self.N, self.K)
+
+    def dequantize(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        out = out if out is not None else torch.empty(self.E, self.N, self.K, dtype=torch.bfloat16,
+                                                      device=self.q.device)
+        for e in range(self.E):
+            torch.ops.hipserve.gguf_dequant_tiled(out[e], self.q[e], self.rs[e] if self.rs.numel() else self.rs,
+                                                  self.kqt, self.N, self.K)
+        return out
+
+    @staticmethod
+    def supported(kqt: int, N: int, K: int) -> bool:
+        return kqt in QuantMoE.KERNEL_QTS and N % 16 == 0 and K % 256 == 0
+
+
+_MOE_SCRATCH: dict = {}
+
+
+def moe_dense(w: QuantMoE, slot: int) -> torch.Tensor:
+    """bf16 [E, N, K] experts for a prefill-sized MoE: the resident shadow, or one of two
+    per-device scratch buffers (w13 / w2 of the current layer) dequantised now."""
+    if w.dense is not None:
+        return w.dense
+    key = (w.q.device, slot)
+    buf = _MOE_SCRATCH.get(key)
+    n = w.E * w.N * w.K
+    if buf is None or buf.numel() < n:
+        buf = _MOE_SCRATCH[key] = torch.empty(n, dtype=torch.bfloat16, device=w.q.device)
+    return w.dequantize(buf[:n].view(w.E, w.N, w.K))
+
+
+def make_moe_shadows(moes, device, reserve_bytes: int) -> int:
+    """bf16 shadows of quantised experts for prefill while ``reserve_bytes`` stay free."""
+    import os
+
+    if os.environ.get("HIPSERVE_QUANT_SHADOW", "1") == "0" or torch.device(device).type != "cuda":
+        return 0
+    added = 0
+    for w in moes:
+        need = w.E * w.N * w.K * 2
+        free, _ = torch.cuda.mem_get_info(device)
+        if w.dense is None and free - need >= reserve_bytes:
+            w.dense = w.dequantize()
+            added += need
+    return added

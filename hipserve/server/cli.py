@@ -37,7 +37,7 @@ def build_parser(prog="hipserve") -> argparse.ArgumentParser:
     ap.add_argument("--trust-remote-code", action="store_true")
     ap.add_argument("--max-model-len", "--ctx-size", "-c", dest="max_model_len", type=int, default=None)
     ap.add_argument("--load-format", default="auto", choices=["auto", "dummy", "safetensors", "gguf"])
-    ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0", "fp8"],
+    ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0", "fp8", "int8"],
                     help="with --load-format dummy: random-init GGUF-quantised weights (GGUF tier benchmarks)")
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")

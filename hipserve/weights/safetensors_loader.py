@@ -304,7 +304,7 @@ def load_hf_weights(model: LlamaModel, model_path: str):
             lw.post_attn_norm = normw(p + "post_attention_layernorm.weight")
             lw.post_ff_norm = normw(p + "post_feedforward_layernorm.weight")
         if cfg.num_experts:
-            lw.router, lw.w13, lw.w2 = _load_experts(ck, p, cfg, r, inter, to)
+            lw.router, lw.w13, lw.w2 = _load_experts(ck, p, cfg, r, inter, to, dev if native_fp8 else None)
         elif ck.has(p + "mlp.gate_up_proj.weight"):  # Phi-3: fused [gate; up]
             f = ck.full(p + "mlp.gate_up_proj.weight")
             I = cfg.intermediate_size
@@ -326,11 +326,14 @@ def load_hf_weights(model: LlamaModel, model_path: str):
         model.visual.load(ck.full, vname[: -len("patch_embed.proj.weight")])
 
 
-def _load_experts(ck, p, cfg, r, inter, to):
+def _load_experts(ck, p, cfg, r, inter, to, native_dev=None):
     """(router [E, H], w13 [E, 2*I/TP, H] as [gate; up], w2 [E, H, I/TP]) from
     Mixtral (block_sparse_moe.experts.e.w1/w3/w2), Qwen3-MoE
     (mlp.experts.e.gate_proj/up_proj/down_proj) or fused expert tensors
-    (mlp.experts.gate_up_proj [E, 2I, H] / Qwen3-VL-MoE's transposed [E, H, 2I])."""
+    (mlp.experts.gate_up_proj [E, 2I, H] / Qwen3-VL-MoE's transposed [E, H, 2I]).
+    With ``native_dev`` (a GPU), per-expert INT8 (compressed-tensors 8-bit, the
+    reference's AWQ-8bit export) or per-channel FP8 experts stay quantised
+    (``QuantMoE`` stacks for the quantised expert GEMM) instead of becoming bf16."""
     E, H, I = cfg.num_experts, cfg.hidden_size, cfg.expert_size
     sl = slice(r * inter, (r + 1) * inter)
     if ck.has(p + "block_sparse_moe.gate.weight"):
@@ -340,6 +343,10 @@ def _load_experts(ck, p, cfg, r, inter, to):
         m = p + "mlp."
         names = ("gate_proj", "up_proj", "down_proj")
     router = to(ck.full(m + "gate.weight"))
+    if native_dev is not None and not ck.has(m + "experts.gate_up_proj"):
+        q = _native_experts(ck, m, names, E, sl, native_dev)
+        if q is not None:
+            return router, q[0], q[1]
     if ck.has(m + "experts.gate_up_proj"):
         gu = ck.full(m + "experts.gate_up_proj")
         dn = ck.full(m + "experts.down_proj")
@@ -358,6 +365,46 @@ def _load_experts(ck, p, cfg, r, inter, to):
         w13.append(torch.cat([g, u], 0))
         w2.append(ck.cols(ep + names[2] + ".weight", sl.start, sl.stop))
     return router, to(torch.stack(w13)), to(torch.stack(w2))
+
+
+def _native_experts(ck, m, names, E, sl, dev):
+    """(QuantMoE w13, QuantMoE w2) of per-expert INT8 / per-channel FP8 tensors, or None
+    when the experts are another format or a slice would split a scale group."""
+    from ..ops import quant as Q
+
+    first = f"{m}experts.0.{names[0]}.weight"
+    int8 = ck.is_int8_ct(first)
+    if not int8 and not ck.is_fp8_e4m3(first):
+        return None
+
+    def part(name, axis):
+        pp = ck.int8_part(name, axis, sl.start, sl.stop) if int8 else ck.fp8_part(name, axis, sl.start, sl.stop)
+        if pp is None or (not int8 and pp[1].numel() not in (1, pp[0].shape[0])):
+            raise ValueError("unsupported expert slice")  # a split group / 128-block scales
+        return pp
+
+    def build(pps):  # row-stacked pieces of one expert -> QuantPart
+        if int8:
+            zps = [z for _, _, z in pps]
+            zp = None if all(z is None for z in zps) else torch.cat(
+                [z if z is not None else torch.zeros_like(sc) for (_, sc, _), z in zip(pps, zps)])
+            return Q.QuantPart.from_int8(torch.cat([u for u, _, _ in pps]), torch.cat([sc for _, sc, _ in pps]),
+                                         zp, dev)
+        qs = torch.cat([q for q, _ in pps])
+        sc = torch.cat([s.reshape(-1).expand(q.shape[0]) if s.numel() == 1 else s.reshape(-1) for q, s in pps])
+        return Q.QuantPart.from_fp8(qs, sc, dev)
+
+    try:
+        p13, p2 = [], []
+        for e in range(E):
+            ep = f"{m}experts.{e}."
+            p13.append(build([part(ep + names[0] + ".weight", 0), part(ep + names[1] + ".weight", 0)]))
+            p2.append(build([part(ep + names[2] + ".weight", 1)]))
+    except ValueError:
+        return None
+    if not (Q.QuantMoE.supported(p13[0].kqt, p13[0].N, p13[0].K) and Q.QuantMoE.supported(p2[0].kqt, p2[0].N, p2[0].K)):
+        return None
+    return Q.QuantMoE(p13), Q.QuantMoE(p2)
 
 
 def save_hf_checkpoint(path: str, cfg, tensors: dict[str, torch.Tensor]):
