@@ -151,9 +151,12 @@ void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S
 void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, int N, int S, hipStream_t s);
 // act[M, I] = GLU of the plain [gate | up] partials ws[S, M, 2I] (decode_fused.hip)
 void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s);
+// bias (bf16 [N]) and per-head q/k RMSNorm (fp32 weights [D], mode 0, D/16 a power of two)
+// optional: nullptr skips them (Qwen2 / Qwen3 families)
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
                               const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
-                              int nkv, int D, int block_size, int mode, hipStream_t s);
+                              int nkv, int D, int block_size, int mode, hipStream_t s, const void* bias = nullptr,
+                              const float* qw = nullptr, const float* kw = nullptr, float eps = 1e-6f);
 void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s);
 }  // namespace hipserve
 

@@ -19,6 +19,13 @@ namespace hipserve {
 
 // sum over S slices of 8 consecutive fp32 partials (batched loads, common.h),
 // rounded to bf16 like the unfused reduce output, returned as fp32
+// x = bf16(x + b) for 8 bf16 bias values (torch's bf16 add of the bias vector)
+HS_DEVICE void add_bias8(float (&x)[8], const unsigned short* __restrict__ b) {
+  const u16x8 v = *reinterpret_cast<const u16x8*>(b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = bf16_to_f32(f32_to_bf16(x[j] + bf16_to_f32(v[j])));
+}
+
 HS_DEVICE void sum8_bf16(float (&o)[8], const float* __restrict__ p, long slice, int S) {
   f32x4 lo, hi;
   sum_slices8(lo, hi, p, slice, S);
@@ -124,12 +131,19 @@ void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S
 // chunk) pairs first, then the v chunks; 64-thread workgroups over
 // (token, item block) so a 64-token decode batch spreads over ~450 workgroups
 // instead of 64 (the partial reads are per-CU-bandwidth bound at one WG per token).
-template <int kMode>
+//
+// Family extras, bit-identical to the unfused chain (GEMM -> bias add -> qk_rmsnorm ->
+// rope_cache): bias (Qwen2: bf16 [N], added to the bf16-rounded sum and rounded
+// again) and per-head q/k RMSNorm (Qwen3: fp32 weights [D]; a head's lanes are
+// consecutive, its sum of squares is reduced in qk_rmsnorm_vec_kernel's order: each
+// lane's two chunks (d and d + D/2) are the kernel's first xor pair, then xor 4, 2, 1).
+template <int kMode, bool kNorm>
 __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
     unsigned short* __restrict__ qkv, long qkv_stride, const float* __restrict__ ws, int S,
     const long* __restrict__ positions, const long* __restrict__ slots, const float* __restrict__ cos_sin,
     unsigned short* __restrict__ k_cache, unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D,
-    int block_size) {
+    int block_size, const unsigned short* __restrict__ bias, const float* __restrict__ qw,
+    const float* __restrict__ kw, float eps) {
   const int t = blockIdx.x;
   const int it = blockIdx.y * 64 + threadIdx.x;
   const int half = D / 2;
@@ -152,6 +166,7 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
     const int iv = it - n_qk, kh = iv / (D / 8), c = iv % (D / 8);
     float x[8];
     sum8_bf16(x, wrow + (nq + nkv) * D + kh * D + c * 8, slice, S);
+    if (bias != nullptr) add_bias8(x, bias + (nq + nkv) * D + kh * D + c * 8);
     unsigned short* vc = v_cache + (blk * nkv + kh) * (long)D * block_size + off;
 #pragma unroll
     for (int j = 0; j < 8; ++j) vc[(c * 8 + j) * block_size] = f32_to_bf16(x[j]);
@@ -163,6 +178,26 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
     float x[8], y[8];
     sum8_bf16(x, wrow + h * D + c * 8, slice, S);
     sum8_bf16(y, wrow + h * D + half + c * 8, slice, S);
+    if (bias != nullptr) {
+      add_bias8(x, bias + h * D + c * 8);
+      add_bias8(y, bias + h * D + half + c * 8);
+    }
+    if constexpr (kNorm) {
+      float ss = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s2 += y[j] * y[j];
+      ss += s2;
+      for (int o = qk_chunks / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      const float inv = rsqrtf(ss / D + eps);
+      const float* nw = h < nq ? qw : kw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        x[j] = bf16_to_f32(f32_to_bf16(x[j] * inv * nw[c * 8 + j]));
+        y[j] = bf16_to_f32(f32_to_bf16(y[j] * inv * nw[half + c * 8 + j]));
+      }
+    }
     u16x8 va, vb;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -179,6 +214,7 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
   } else {
     float x[8];
     sum8_bf16(x, wrow + h * D + c * 8, slice, S);
+    if (bias != nullptr) add_bias8(x, bias + h * D + c * 8);
     u16x8 v;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -197,20 +233,25 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
 
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
                               const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
-                              int nkv, int D, int block_size, int mode, hipStream_t s) {
+                              int nkv, int D, int block_size, int mode, hipStream_t s, const void* bias,
+                              const float* qw, const float* kw, float eps) {
   if (T <= 0) return;
   auto* q = static_cast<unsigned short*>(qkv);
   auto* kc = static_cast<unsigned short*>(k_cache);
   auto* vc = static_cast<unsigned short*>(v_cache);
+  auto* b = static_cast<const unsigned short*>(bias);
   const int qk_chunks = mode == 0 ? D / 16 : D / 8;
   const int items = (nq + nkv) * qk_chunks + nkv * (D / 8);
   const dim3 grid(T, (items + 63) / 64);
-  if (mode == 0)
-    splitk_rope_cache_kernel<0><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc, T, nq,
-                                                     nkv, D, block_size);
+  if (mode == 0 && qw != nullptr)
+    splitk_rope_cache_kernel<0, true><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc, T,
+                                                           nq, nkv, D, block_size, b, qw, kw, eps);
+  else if (mode == 0)
+    splitk_rope_cache_kernel<0, false><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc,
+                                                            T, nq, nkv, D, block_size, b, nullptr, nullptr, eps);
   else
-    splitk_rope_cache_kernel<1><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc, T, nq,
-                                                     nkv, D, block_size);
+    splitk_rope_cache_kernel<1, false><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc,
+                                                            T, nq, nkv, D, block_size, b, nullptr, nullptr, eps);
 }
 
 // GLU over the split-K partials of a merged [gate | up] projection in the plain

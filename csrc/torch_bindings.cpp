@@ -642,10 +642,28 @@ void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor&
 
 void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
                        const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
-                       int64_t nq, int64_t nkv, int64_t head_dim, int64_t mode) {
+                       int64_t nq, int64_t nkv, int64_t head_dim, int64_t mode,
+                       const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& q_w,
+                       const c10::optional<at::Tensor>& k_w, double eps) {
   CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_ROWMAJOR(qkv);
   const int T = qkv.size(0);
   const long N = (nq + 2 * nkv) * head_dim;
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                "splitk_rope_cache: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  const float *qwp = nullptr, *kwp = nullptr;
+  if (q_w.has_value()) {
+    TORCH_CHECK(k_w.has_value() && q_w->scalar_type() == at::kFloat && k_w->scalar_type() == at::kFloat &&
+                q_w->numel() == head_dim && k_w->numel() == head_dim && q_w->is_contiguous() && k_w->is_contiguous(),
+                "splitk_rope_cache: fp32 q/k norm weights [head_dim]");
+    const int lanes = (int)head_dim / 16;
+    TORCH_CHECK(mode == 0 && (lanes == 4 || lanes == 8 || lanes == 16), "splitk_rope_cache: q/k norm needs mode 0, head_dim 64/128/256");
+    qwp = q_w->data_ptr<float>();
+    kwp = k_w->data_ptr<float>();
+  }
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= N);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * T * N);
   TORCH_CHECK(positions.scalar_type() == at::kLong && slots.scalar_type() == at::kLong);
@@ -659,7 +677,7 @@ void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, co
   hipserve::launch_splitk_rope_cache(qkv.data_ptr(), qkv.stride(0), ws.data_ptr<float>(), splits,
                                      positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(),
                                      cos_sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), T, nq, nkv,
-                                     head_dim, k_cache.size(2), mode, cur_stream());
+                                     head_dim, k_cache.size(2), mode, cur_stream(), bp, qwp, kwp, (float)eps);
 }
 
 void splitk_reduce(at::Tensor& out, const at::Tensor& ws, int64_t splits) {
@@ -889,7 +907,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu) -> ()");
   m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
-  m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
+  m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode, Tensor? bias=None, Tensor? q_w=None, Tensor? k_w=None, float eps=1e-6) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");
   m.def("penalty_apply(Tensor(a!) logits, Tensor slot, Tensor pres, Tensor freq, Tensor rep, Tensor counts, Tensor seen) -> ()");
   m.def("penalty_update(Tensor tok, Tensor slot, Tensor(a!) counts, Tensor(b!) seen) -> ()");

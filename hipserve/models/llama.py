@@ -136,6 +136,13 @@ class LlamaModel:
             self.cos_sin_local = ref.rope_cos_sin(self.D, mp, cfg.rope_local_theta, None).to(self.device)
         self.vanilla = not (cfg.qkv_bias or cfg.qk_norm or cfg.sandwich_norm or cfg.hidden_act != "silu"
                             or any(cfg.layer_windows) or cfg.embed_scale != 1.0)
+        # families the fused decode layer covers: Llama-style plus q/k/v bias (Qwen2),
+        # per-head q/k RMSNorm (Qwen3; folded into the split-K RoPE epilogue) and MoE
+        # MLPs (Mixtral, Qwen3-MoE / Qwen3-VL-MoE); Gemma-3 (sandwich norms, GeGLU,
+        # sliding windows, embedding scale) keeps the unfused layer
+        self.fused_family = not (cfg.sandwich_norm or cfg.hidden_act != "silu" or any(cfg.layer_windows)
+                                 or cfg.embed_scale != 1.0) and (
+            not cfg.qk_norm or (cfg.rope_mode == 0 and self.D in (64, 128, 256)))
         self.decode_partition = 512
         self.block_size_hint = 16  # KV block size (set by the runner)
         self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
@@ -345,7 +352,7 @@ class LlamaModel:
         With the fused decode path the merged gate|up weight is packed
         gate/up-interleaved instead (``PACKED_GLU``: the SiLU-GLU runs in its epilogue)."""
         n = 0
-        glu = self.fused_decode and self.vanilla
+        glu = self.fused_decode and self.fused_family
         # HBM budget: a packed copy is only made while >= 24 GiB + a quarter of the
         # device stay free for the KV cache (a 70B model on ONE 288 GB MI355X keeps
         # most weights unpacked; the tuner's packed choice then runs on the plain layout)
@@ -405,7 +412,7 @@ class LlamaModel:
     def fused_gemm_shapes(self) -> dict:
         """{(N, K): epilogue spec} of the projections whose decode GEMM output feeds
         a fused epilogue (ops/gemm.py tunes them as GEMM + epilogue units)."""
-        if not self.layers or not self.vanilla:
+        if not self.layers or not self.fused_family:
             return {}
         lw = self.layers[0]
         out = {}
@@ -421,7 +428,7 @@ class LlamaModel:
 
     def _fused_ok(self, meta: AttnMeta) -> bool:
         return (self.fused_decode and meta.num_prefill_tokens == 0
-                and getattr(self.ops, "name", "") == "hip" and self.cfg.num_experts == 0 and self.vanilla)
+                and getattr(self.ops, "name", "") == "hip" and self.fused_family)
 
     def add_rmsnorm(self, out, residual, x, splits, w):
         """residual += x summed over the TP ranks; out = RMSNorm(residual) * w.
@@ -554,24 +561,30 @@ class LlamaModel:
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
         part, tmp_out, tmp_ml = self._decode_split(T, meta)
         L = len(self.layers)
+        lw0 = self.layers[0]
+        extras = lw0.bqkv is not None or lw0.q_norm is not None
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
             pt = self._partial(xn, lw.wqkv)
-            if pt is not None and self.fused_qkv_attention and D in (64, 128):
+            if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
                                     meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part, self.scale,
                                     0, cfg.rope_mode)
-            elif pt is not None:
+            elif pt is not None:  # + q/k/v bias and per-head q/k RMSNorm of the family, if any
                 ws, S = pt
                 qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)
                 op.splitk_rope_cache(qkv, ws, S, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
-                                     nq, nkv, D, cfg.rope_mode)
+                                     nq, nkv, D, cfg.rope_mode, lw.bqkv, lw.q_norm, lw.k_norm, eps)
             else:
                 qkv = self.linear(xn, lw.wqkv)
+                if lw.bqkv is not None:
+                    qkv += lw.bqkv
+                if lw.q_norm is not None:
+                    ops.qk_rmsnorm(qkv, lw.q_norm, lw.k_norm, nq, nkv, D, eps)
                 ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
                                cfg.rope_mode)
-            if pt is None or not (self.fused_qkv_attention and D in (64, 128)):
+            if pt is None or not (self.fused_qkv_attention and D in (64, 128) and not extras):
                 ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
                                  nq, nkv, part, self.scale)
             pt = self._partial(attn, lw.wo)
@@ -579,6 +592,10 @@ class LlamaModel:
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2)
             else:
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(attn, lw.wo), 1, lw.ln2)
+            nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
+            if lw.router is not None:  # MoE MLP: routed expert GEMMs, then residual + next norm
+                self.add_rmsnorm(xn, residual, self.moe(xn, lw), 1, nxt)
+                continue
             gc = gemm.glu_choice(T, lw.wgu)
             pt = None if gc is not None or isinstance(lw.wgu, torch.Tensor) else self._partial(xn, lw.wgu)
             if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
@@ -590,7 +607,6 @@ class LlamaModel:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 ops.silu_and_mul(act, gu)
-            nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             pt = self._partial(act, lw.wd)
             if pt is not None:
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt)

@@ -82,7 +82,7 @@ def test_glu_gemm_bit_exact(ops, M, rt, S):
     assert torch.equal(act, want)
 
 
-def _small_model(ops, seed=0):
+def _small_model(ops, seed=0, family="llama"):
     from hipserve.config import PRESETS
     from hipserve.models.llama import LlamaModel
     from hipserve.parallel.comm import TPGroup
@@ -90,17 +90,72 @@ def _small_model(ops, seed=0):
     cfg = PRESETS["llama-3-8b"].replace(hidden_size=1024, intermediate_size=3584, num_heads=8,
                                         num_kv_heads=2, num_layers=3, vocab_size=4096,
                                         max_position_embeddings=2048)
+    if family == "qwen2":
+        cfg = cfg.replace(family="qwen2", qkv_bias=True)
+    elif family == "qwen3":
+        cfg = cfg.replace(family="qwen3", qk_norm=True)
+    elif family == "qwen3_moe":
+        cfg = cfg.replace(family="qwen3_moe", architecture="mixtral", qk_norm=True, num_experts=8,
+                          num_experts_per_tok=2, moe_intermediate_size=512)
     m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, ops, max_pos=2048)
     m.allocate_random(seed=seed, std=0.05)
+    g = torch.Generator(device=DEV).manual_seed(seed + 1)
+    for lw in m.layers:  # non-trivial family extras
+        if lw.bqkv is not None:
+            lw.bqkv = (torch.randn(lw.bqkv.shape, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+        if lw.q_norm is not None:
+            lw.q_norm = 1 + 0.2 * torch.randn(lw.q_norm.shape, device=DEV, generator=g)
+            lw.k_norm = 1 + 0.2 * torch.randn(lw.k_norm.shape, device=DEV, generator=g)
     return m, cfg
 
 
+@pytest.mark.parametrize("bias,norm,D", [(True, False, 128), (False, True, 128), (True, True, 64),
+                                         (False, True, 64)])
+@pytest.mark.parametrize("S", [1, 3])
+def test_splitk_rope_cache_extras_bit_exact(ops, bias, norm, D, S):
+    """split-K RoPE epilogue with the Qwen2 bias and / or Qwen3 per-head q/k RMSNorm ==
+    bf16 reduce -> bias add -> qk_rmsnorm -> rope_cache."""
+    T, nq, nkv, bs = 29, 16, 4, 16
+    N = (nq + 2 * nkv) * D
+    ws = _partials(S, T, N, 11 + S + D)
+    h = ws[0].clone()
+    for s in range(1, S):
+        h = h + ws[s]
+    qkv1 = h.to(torch.bfloat16)
+    b = (torch.randn(N, device=DEV) * 0.3).to(torch.bfloat16) if bias else None
+    qw = 1 + 0.2 * torch.randn(D, device=DEV) if norm else None
+    kw = 1 + 0.2 * torch.randn(D, device=DEV) if norm else None
+    if bias:
+        qkv1 += b
+    if norm:
+        ops.qk_rmsnorm(qkv1, qw, kw, nq, nkv, D, 1e-6)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    slots = torch.randperm(64 * bs, device=DEV)[:T]
+    slots[5] = -1
+    cs = ref.rope_cos_sin(D, 4096, 1e6).to(DEV)
+    kc1 = torch.zeros(64, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc1 = torch.zeros(64, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    ops.rope_cache(qkv1, pos, slots, cs, kc1, vc1, nq, nkv, D, 0)
+    qkv2 = torch.zeros(T, N, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.splitk_rope_cache(qkv2, ws.contiguous(), S, pos, slots, cs, kc2, vc2, nq, nkv, D, 0,
+                                         b, qw, kw, 1e-6)
+    assert torch.equal(qkv1[:, : nq * D], qkv2[:, : nq * D])
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+
+
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "qwen3_moe"])
+def test_fused_decode_forward_families_bit_exact(ops, family):
+    test_fused_decode_forward_bit_exact(ops, "dgp", family)
+
+
 @pytest.mark.parametrize("choices", ["dgp", "dg", "mixed"])
-def test_fused_decode_forward_bit_exact(ops, choices):
+def test_fused_decode_forward_bit_exact(ops, choices, family="llama"):
     """Model forward on a decode batch: fused epilogues vs the unfused path."""
     from hipserve.models.llama import AttnMeta
 
-    m, cfg = _small_model(ops)
+    m, cfg = _small_model(ops, family=family)
+    assert m.fused_family
     old = dict(gemm.TUNER.table)
     try:
         gemm.TUNER.table.clear()
