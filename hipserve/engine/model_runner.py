@@ -450,12 +450,21 @@ class ModelRunner:
         if not mm["images"]:
             return
         vis = self.model.visual
-        cache = {}
+        # every distinct image of the step goes through the tower in ONE forward (one
+        # attention segment per frame): one GEMM per projection for all of them
+        uniq = {}
+        for _, _, _, pixels, grid, digest in mm["images"]:
+            uniq.setdefault(digest, (pixels, grid))
+        geo = image_geometry([g for _, g in uniq.values()], vis.cfg)
+        emb, ds_all = vis.forward(torch.from_numpy(np.concatenate([p for p, _ in uniq.values()])), geo)
+        cache, off = {}, 0
+        m2 = vis.cfg.spatial_merge_size ** 2
+        for digest, (pixels, _) in uniq.items():
+            n = pixels.shape[0] // m2
+            cache[digest] = (emb[off:off + n], [d[off:off + n] for d in ds_all])
+            off += n
         rows, embs, dss = [], [], []
         for row0, lo, hi, pixels, grid, digest in mm["images"]:
-            if digest not in cache:
-                geo = image_geometry([grid], vis.cfg)
-                cache[digest] = vis.forward(torch.from_numpy(pixels), geo)
             e, ds = cache[digest]
             rows.append(torch.arange(row0, row0 + hi - lo))
             embs.append(e[lo:hi])
