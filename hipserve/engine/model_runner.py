@@ -69,6 +69,8 @@ class ModelRunner:
         self.tp = tp
         self.device = torch.device(device or tp.device or ecfg.device)
         if self.device.type == "cuda":
+            if self.device.index is None:  # plain "cuda": this process's current device
+                self.device = torch.device("cuda", torch.cuda.current_device())
             torch.cuda.set_device(self.device)
         self.dtype = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "auto": torch.bfloat16,
                       "float32": torch.float32, "fp32": torch.float32}[ecfg.dtype]
