@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--concurrency", type=int, default=64)
     ap.add_argument("--input-len", type=int, default=1024)
     ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--block-size", type=int, default=16)
+    ap.add_argument("--decode-partition", type=int, default=512)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -37,7 +39,8 @@ def main():
     from hipserve.parallel.comm import TPGroup
 
     eng = LLMEngine(EngineConfig(model=a.model, load_format="dummy", device="cuda", max_num_seqs=a.concurrency,
-                                 max_num_batched_tokens=8192, max_model_len=a.input_len + a.output_len + 16),
+                                 max_num_batched_tokens=8192, max_model_len=a.input_len + a.output_len + 16,
+                                 block_size=a.block_size, decode_partition=a.decode_partition),
                     tp=TPGroup(0, 1, None, torch.device("cuda", 0)))
     rng = np.random.default_rng(0)
     sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.output_len, ignore_eos=True)
