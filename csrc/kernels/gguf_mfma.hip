@@ -406,7 +406,9 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
   constexpr int XP = XR * 32 / NT;
   static_assert(XP * NT == XR * 32, "x staging must divide evenly (no guarded, sinkable loads)");
   u16x8 xv[XP];
-  const int mrow0 = kMoe ? (int)blockIdx.z * XR : 0;  // kMoe: first slot of the expert tile
+  // kMoe: first slot of the expert tile; dense: first x row of this M tile (prefill
+  // sweeps the prompt in XR-row tiles over blockIdx.z, K15)
+  const int mrow0 = (int)blockIdx.z * XR;
   [[maybe_unused]] const unsigned short* xg[kMoe ? XP : 1];  // kMoe: gathered row of each staging item
   if constexpr (kMoe) {
 #pragma unroll
@@ -424,7 +426,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
       if constexpr (kMoe)
         xv[i] = *reinterpret_cast<const u16x8*>(xg[i] + sb * 256 + kb);
       else
-        xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + sb * 256 + kb);
+        xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(mrow0 + row, M - 1) * x_stride + sb * 256 + kb);
     }
   };
   auto store_x = [&](int buf) {
@@ -505,10 +507,9 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
     }
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      int m = 16 * t + c;
+      const int m = mrow0 + 16 * t + c;  // output row (kMoe: slot)
       long wrow = (long)blockIdx.y * M + m;
       if constexpr (kMoe) {
-        m += mrow0;  // output row = slot
         if (moe.slots[m] < 0) continue;
         wrow = (long)blockIdx.y * moe.nslots + m;
       } else if (m >= M) {
@@ -561,7 +562,8 @@ void launch_t(void* out, long out_stride, float* ws, const void* x, long x_strid
   constexpr int RT = 2, NW = kWaves;
   const int nsb = K / 256;
   const int per = (nsb + S - 1) / S;
-  const dim3 grid(tiles, (nsb + per - 1) / per), block(64 * NW);
+  // M > 64 (K15, prefill): the 64-row body swept over the prompt, one M tile per blockIdx.z
+  const dim3 grid(tiles, (nsb + per - 1) / per, M > 64 ? (M + 63) / 64 : 1), block(64 * NW);
   auto* o = static_cast<unsigned short*>(out);
   auto* xi = static_cast<const unsigned short*>(x);
   if (M <= 16)

@@ -244,7 +244,7 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
               "gguf_gemm_parts: 1-4 parts");
   TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && splits >= 1);
   const int M = x.size(0);
-  TORCH_CHECK(M >= 1 && M <= 64, "gguf_gemm_parts handles 1 <= M <= 64");
+  TORCH_CHECK(M >= 1, "gguf_gemm_parts: M >= 1 (M > 64 sweeps 64-row tiles)");
   TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
   const int nsb = K / 256;
   const int per = (nsb + splits - 1) / splits;

@@ -16,6 +16,8 @@ GEMM.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -29,6 +31,12 @@ FP8, FP8B = 1000, 1001
 INT8 = 1002
 KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7, INT8: 8}
 MAX_FUSED_M = 64
+# prefill chunks up to this many tokens without a bf16 shadow run the dequant-MFMA
+# kernel swept over 64-row M tiles (K15: no [N, K] bf16 dequant pass, which costs more
+# than the GEMM itself at small M); larger chunks dequantise into scratch + hipBLASLt.
+# Llama-3-8B Q4_K gate|up (profiles/r2_k15_prefill_quant_gemm.jsonl): M = 128: 65 us vs
+# 150 dequant + hipBLASLt; M = 512: equal; a resident bf16 shadow beats both (41 / 93 us)
+QPREFILL_MAX_M = int(os.environ.get("HIPSERVE_QPREFILL_MAX_M", "512"))
 
 
 def repack(raw: np.ndarray, qtype: int, N: int, K: int):
@@ -386,6 +394,7 @@ def _empty(device, dtype):
 
 
 def _launch_v2(out, ws, x, w: QuantWeight, S: int):
+    w.groups  # (re)builds v2_args
     a = w.v2_args
     torch.ops.hipserve.gguf_gemm_parts(out, ws, x, a[0], a[1], a[2], a[3], a[4], w.N, w.K, S)
 
@@ -486,6 +495,9 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
         return out
     if w.dense is not None:  # prefill on the resident bf16 copy: no per-call dequant pass
         return torch.nn.functional.linear(x, w.dense)
+    if w.v2 and x.is_cuda and M <= QPREFILL_MAX_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+        _launch_v2(out, _empty(x.device, torch.float32), x, w, 1)  # K15: M-tiled dequant-MFMA GEMM
+        return out
     # prefill: every part dequantised into one contiguous [N, K] scratch, one GEMM
     buf = _dequant_scratch(x.device, w.N * w.K)[: w.N * w.K].view(w.N, w.K)
     off = 0

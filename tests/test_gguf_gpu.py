@@ -393,3 +393,17 @@ def test_dense_shadow_prefill_matches_dequant_path():
     assert torch.equal(quant_linear(x, qw), want)
     assert torch.equal(quant_linear(xs, qw), want_small)
     assert torch.equal(qw.dense, dequantize(qw))
+
+
+@pytest.mark.parametrize("M", [65, 130, 256])
+def test_prefill_m_tiled_kernel_vs_fp32(M):
+    """K15: prefill chunks of up to QPREFILL_MAX_M tokens without a bf16 shadow run the
+    dequant-MFMA kernel swept over 64-row M tiles (one launch for all parts), vs an
+    fp32 matmul of the decoded weights."""
+    from hipserve.ops import quant as Q
+    qw, raws = _rand_qw([(G.Q4_K, 512, 2048), (G.Q6_K, 272, 2048)], seed=M)
+    assert qw.dense is None and M <= Q.QPREFILL_MAX_M
+    x = torch.randn(M, 2048, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense(raws).T
+    got = quant_linear(x, qw).float()
+    assert (got - want).abs().max().item() < 1e-2 * want.abs().max().item() + 1e-3

@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--splits", type=int, nargs="*", default=None)
     ap.add_argument("--fp8", action="store_true", help="FP8 e4m3 per-channel weights of the same shapes")
+    ap.add_argument("--prefill", action="store_true",
+                    help="M > 64: the M-tiled dequant-MFMA kernel vs dequant-to-scratch + hipBLASLt vs a bf16 shadow")
     a = ap.parse_args()
     load_library()
     rng = np.random.default_rng(0)
@@ -85,6 +87,26 @@ def main():
             del raws
         for M in a.m:
             x = torch.randn(M, qw.K, device="cuda", dtype=torch.bfloat16)
+            if a.prefill:
+                out = torch.empty(M, qw.N, device="cuda", dtype=torch.bfloat16)
+                dense = Q.dequantize(qw)
+                buf = torch.empty_like(dense)
+
+                def deq_blas():
+                    off = 0
+                    for p in qw.parts:
+                        Q._dequant_into(buf[off:off + p.N], p)
+                        off += p.N
+                    return torch.nn.functional.linear(x, buf)
+
+                for kern, fn in (("m_tiled_mfma", lambda: Q._launch_v2(out, Q._empty(x.device, torch.float32), x, qw, 1)),
+                                 ("dequant+hipblaslt", deq_blas),
+                                 ("bf16_shadow_hipblaslt", lambda: torch.nn.functional.linear(x, dense))):
+                    us = _time(fn, reps=10, graph_reps=5)
+                    print(json.dumps({"proj": name, "M": M, "kernel": kern, "us": round(us, 1),
+                                      "TFLOPs": round(2 * M * qw.N * qw.K / us / 1e6, 1)}), flush=True)
+                del dense, buf
+                continue
             rows = []
             rows.append(("v2_partial", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw))))
             for S in a.splits or []:
