@@ -338,8 +338,8 @@ class LlamaModel:
         """(N, K) of every dense bf16 projection (for the decode GEMM autotune)."""
         out = set()
         for lw in self.layers[:1]:
-            for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
-                if isinstance(w, torch.Tensor) and w.dim() == 2:
+            for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.router):  # + the MoE router [E, H] (E % 16 == 0)
+                if isinstance(w, torch.Tensor) and w.dim() == 2 and (w is not lw.router or w.shape[0] % 16 == 0):
                     out.add(tuple(w.shape))
         if isinstance(self.lm_head, torch.Tensor):
             out.add(tuple(self.lm_head.shape))

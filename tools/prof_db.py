@@ -111,6 +111,10 @@ def summarize(path, title="rocprofv3 kernel trace"):
             for f, g in acc.items():
                 gaps.setdefault(f, []).append(g)
         gl = sorted(((f, statistics.median(v) / 1e3) for f, v in gaps.items()), key=lambda x: -x[1])[:8]
+        mid = dec[len(dec) // 2]  # one decode step in dispatch order (first 120 kernels)
+        L += ["", "### kernel sequence of one decode step", "", "| # | kernel | us |", "|---:|---|---:|"]
+        for j, (f, b, e) in enumerate(mid[:120]):
+            L.append(f"| {j} | `{f}` | {(e - b) / 1e3:.1f} |")
         L += ["", "### idle gaps inside a decode step, by the kernel that follows (median us/step)", "",
               "| next kernel | gap us/step |", "|---|---:|"]
         for f, g in gl:
