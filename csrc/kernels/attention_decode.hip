@@ -60,7 +60,7 @@ HS_DEVICE void qkv_sum8(float (&o)[8], const float* p, long slice, int S) {
 
 // two register sets for the chunk pipeline: keep VGPR + AGPR <= 256 so two waves fit
 // per SIMD (two 4-wave workgroups per CU — B = 64 x 8 kv heads is 2 per CU)
-template <int D, int kDecWaves, bool kQKV = false>
+template <int D, int kDecWaves, bool kQKV = false, bool kNT = true>
 __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(2, 8))) void paged_decode_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const unsigned short* __restrict__ q, long q_stride,
@@ -235,6 +235,12 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   struct Chunk {
     u16x8 ka[KS], kb[KS], vv[NB];
   };
+  // K / V are read exactly once per step by one wave: non-temporal loads (aux nt) keep
+  // them from evicting the weights' and partials' lines and shorten issue -> landed
+  auto ld = [](const unsigned short* p) -> u16x8 {
+    if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
+    else return *reinterpret_cast<const u16x8*>(p);
+  };
   auto load_chunk = [&](int c, Chunk& ch) {
     const int cs = start + min(c, nchunks - 1) * kChunk;
     // K: tile a row m -> token 8*(m>>2) + (m&3); tile b -> +4
@@ -251,8 +257,8 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
         (long)(tb % block_size) * D + 8 * grp;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      ch.ka[ks] = *reinterpret_cast<const u16x8*>(ka + 32 * ks);
-      ch.kb[ks] = *reinterpret_cast<const u16x8*>(kb + 32 * ks);
+      ch.ka[ks] = ld(ka + 32 * ks);
+      ch.kb[ks] = ld(kb + 32 * ks);
     }
     // V: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
     int tv = cs + 8 * grp;
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
         ((long)bt[(tv - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
         (tv % block_size) + (long)col * block_size;
 #pragma unroll
-    for (int n = 0; n < NB; ++n) ch.vv[n] = *reinterpret_cast<const u16x8*>(vb + (long)16 * n * block_size);
+    for (int n = 0; n < NB; ++n) ch.vv[n] = ld(vb + (long)16 * n * block_size);
   };
   auto compute_chunk = [&](int c, const Chunk& ch) {
     const int cs = start + c * kChunk;
@@ -408,6 +414,18 @@ static int decode_waves() {
   return env == 8 ? 8 : 4;
 }
 
+// K / V load policy. Non-temporal when the grid streams the KV at full chip
+// bandwidth (>= 256 workgroups): Llama-3-8B, B = 64, ctx 1152, cold KV 56.8 -> 51.6 us,
+// decode step 5.51 -> 5.36 ms. Small grids (B = 1, 16 workgroups) are latency-bound and
+// lose with nt (26.7 -> 37.2 us): default policy there. HIPSERVE_DECODE_NT = 0 disables.
+static bool decode_nt(long workgroups) {
+  static const bool env = [] {
+    const char* e = getenv("HIPSERVE_DECODE_NT");
+    return !(e && atoi(e) == 0);
+  }();
+  return env && workgroups >= 256;
+}
+
 void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
                          const void* k_cache, const void* v_cache,
                          const int* block_tables, int bt_stride,
@@ -424,9 +442,16 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
   auto* kc = static_cast<const unsigned short*>(k_cache);
   auto* vc = static_cast<const unsigned short*>(v_cache);
 #define HS_DECODE(DD, WW)                                                                                   \
-  paged_decode_kernel<DD, WW><<<grid, block, smem, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables,    \
-                                                       bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv,     \
-                                                       block_size, part_size, max_parts, scale, window)
+  do {                                                                                                      \
+    if (decode_nt((long)max_parts * nkv * B))                                                               \
+      paged_decode_kernel<DD, WW, false, true><<<grid, block, smem, s>>>(                                   \
+          o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq,  \
+          nkv, block_size, part_size, max_parts, scale, window);                                            \
+    else                                                                                                    \
+      paged_decode_kernel<DD, WW, false, false><<<grid, block, smem, s>>>(                                  \
+          o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq,  \
+          nkv, block_size, part_size, max_parts, scale, window);                                            \
+  } while (0)
 #define HS_DECODE_D(DD)                                                                                      \
   do {                                                                                                      \
     if (waves == 8) HS_DECODE(DD, 8);                                                                       \

@@ -92,8 +92,12 @@ def bench_decode(ops):
                                                      (1, 4096, 32, 8), (64, 4096, 64, 8)] for p in parts]:
         mb = math.ceil(ctx / bs) + 1
         nblocks = B * mb
-        kc = torch.randn(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
-        vc = torch.randn(nblocks, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+        # DECODE_COLD=1: rotate over enough KV copies (> 2x the 256 MB MALL) that every
+        # call streams cold K / V, as in the engine (one step touches every layer's KV)
+        byts = 2 * B * ctx * nkv * D * 2
+        ncopy = max(1, min(8, -(-(768 << 20) // byts))) if os.environ.get("DECODE_COLD") == "1" else 1
+        kcs = [torch.randn(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16) for _ in range(ncopy)]
+        vcs = [torch.randn(nblocks, nkv, D, bs, device=DEV, dtype=torch.bfloat16) for _ in range(ncopy)]
         bt = torch.randperm(nblocks, device=DEV).int().view(B, mb)
         cl = torch.full((B,), ctx, device=DEV, dtype=torch.int32)
         q = torch.randn(B, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
@@ -101,10 +105,17 @@ def bench_decode(ops):
         to = torch.empty(B, nq, mp, D, device=DEV)
         tm = torch.empty(B, nq, mp, 2, device=DEV)
         out = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
-        us = timeit(lambda: ops.paged_decode(out, q, kc, vc, bt, cl, to, tm, nq, nkv, part, 1 / math.sqrt(D)))
-        byts = 2 * B * ctx * nkv * D * 2
-        emit(op="paged_decode", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, us=round(us, 1),
-             TBps=round(byts / us / 1e6, 2))
+        it = [0]
+
+        def call():
+            i = it[0] % ncopy
+            it[0] += 1
+            ops.paged_decode(out, q, kcs[i], vcs[i], bt, cl, to, tm, nq, nkv, part, 1 / math.sqrt(D))
+
+        us = timeit(call)
+        emit(op="paged_decode", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, cold=ncopy > 1,
+             nt=os.environ.get("HIPSERVE_DECODE_NT", "1"), us=round(us, 1), TBps=round(byts / us / 1e6, 2))
+        del kcs, vcs
 
 
 def bench_prefill(ops):
