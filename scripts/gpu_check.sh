@@ -12,7 +12,7 @@ export PYTHONUNBUFFERED=1
 steps="${*:-tests smoke sweep bench prof}"
 
 run_tests() {
-  timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
   local rc=$?
   tail -n 15 $OUT/pytest_gpu.log

@@ -382,10 +382,11 @@ def test_int8_pack_quantized_checkpoint_native(tmp_path):
 
 def test_dense_shadow_prefill_matches_dequant_path():
     """Prefill on the resident bf16 shadow (make_dense_shadows) is bit-identical to the
-    per-call dequant-into-scratch path; decode-sized batches keep the quantised kernel."""
-    from hipserve.ops.quant import make_dense_shadows
+    dequant-then-GEMM path (a chunk above QPREFILL_MAX_M: dequant into scratch +
+    hipBLASLt); decode-sized batches keep the quantised kernel."""
+    from hipserve.ops.quant import QPREFILL_MAX_M, make_dense_shadows
     qw, raws = _rand_qw([(G.Q4_K, 512, 2048), (G.Q6_K, 256, 2048)], seed=5)
-    x = torch.randn(300, 2048, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(QPREFILL_MAX_M + 88, 2048, device="cuda", dtype=torch.bfloat16)
     want = quant_linear(x, qw)
     xs = x[:16].contiguous()
     want_small = quant_linear(xs, qw)
@@ -407,3 +408,25 @@ def test_prefill_m_tiled_kernel_vs_fp32(M):
     want = x.float() @ _dense(raws).T
     got = quant_linear(x, qw).float()
     assert (got - want).abs().max().item() < 1e-2 * want.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K])
+@pytest.mark.parametrize("S", [1, 2, 3, 5, 7, 11])
+def test_mfma_v2_m64_every_slice_length(qt, S):
+    """M = 64 (8 waves x 1 row group, two weight register sets, loop unrolled by two):
+    K slices of 1..11 super-chunks cover the unrolled body and the odd tail, each
+    split's fp32 partials summed vs an fp32 matmul of the decoded weights."""
+    from hipserve.ops.quant import _launch_v2
+    K, M = 2816, 64  # 11 super-chunks
+    qw, raws = _rand_qw([(qt, 256, K), (G.Q6_K if qt == G.Q4_K else qt, 128, K)], seed=S)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense(raws).T
+    tol = 1e-2 * want.abs().max().item() + 1e-3
+    nsb = K // 256
+    per = -(-nsb // S)
+    ny = -(-nsb // per)
+    ws = torch.full((ny * M * qw.N,), float("nan"), dtype=torch.float32, device="cuda")
+    _launch_v2(torch.empty(0, dtype=torch.bfloat16, device="cuda"), ws, x, qw, S)
+    got = ws.view(ny, M, qw.N).sum(0)
+    assert torch.isfinite(got).all()
+    assert (got - want).abs().max().item() < tol
