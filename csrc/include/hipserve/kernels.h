@@ -8,6 +8,9 @@
 namespace hipserve {
 
 // norm.hip — residual != nullptr selects the fused add (residual updated in place)
+void launch_embed_rmsnorm(void* out, void* residual, const void* table, const long* ids, const long* src,
+                          const long* tok, const void* w, bool weight_f32, int rows, int hidden, float eps,
+                          hipStream_t s);
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                     bool weight_f32, int rows, int hidden, long x_stride,
                     long out_stride, float eps, hipStream_t s);
@@ -59,7 +62,7 @@ size_t sample_workspace_floats(int rows, int V);
 void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf16,
                    long stride, int rows, int V, const float* temperature,
                    const int* top_k, const float* top_p, const long* seeds,
-                   const long* steps, float* ws, hipStream_t s);
+                   const long* steps, float* ws, hipStream_t s, bool two_rounds = true);
 
 // penalties.hip — device-side OpenAI penalties + top-n logprobs (graph-capturable).
 // counts int32 [slots, V], seen bits [slots, ceil(V/32)]; slot < 0: row untouched.

@@ -10,16 +10,36 @@
 
 namespace hipserve {
 
-template <int NT, int VPT, bool kAdd, bool kWF32>
+// Token-id source of the gather mode (embedding lookup fused into the first
+// RMSNorm of a decode step): id = src[row] >= 0 ? tok[src[row]] : ids[row]
+// (tok = the previous graph step's sampled ids, src = this step's row in it:
+// the decode lookahead of model_runner.py; src == nullptr: ids only).
+struct GatherIds {
+  const long* ids;
+  const long* src;
+  const long* tok;
+};
+
+// kGather: x is the embedding table, row r reads table row id(r) (GatherIds) and
+// also writes that raw row to `residual` (the layer-0 residual stream): one kernel
+// instead of the id select + embedding gather + residual copy + RMSNorm chain, with
+// the same per-row arithmetic as the plain RMSNorm (bit-identical output).
+template <int NT, int VPT, bool kAdd, bool kWF32, bool kGather = false>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     unsigned short* __restrict__ out, unsigned short* __restrict__ residual,
     const unsigned short* __restrict__ x, const void* __restrict__ weight,
-    int hidden, long x_stride, long out_stride, float eps) {
+    int hidden, long x_stride, long out_stride, float eps, GatherIds gi = GatherIds{}) {
+  static_assert(!(kAdd && kGather), "gather mode writes the residual, it does not add to it");
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
-  const u16x8* xr = reinterpret_cast<const u16x8*>(x + row * x_stride);
-  u16x8* rr = kAdd ? reinterpret_cast<u16x8*>(residual + (long)row * hidden) : nullptr;
+  long xrow = row;
+  if constexpr (kGather) {
+    const long sr = gi.src != nullptr ? gi.src[row] : -1;
+    xrow = sr >= 0 ? gi.tok[sr] : gi.ids[row];
+  }
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + xrow * x_stride);
+  u16x8* rr = (kAdd || kGather) ? reinterpret_cast<u16x8*>(residual + (long)row * hidden) : nullptr;
   float v[VPT][8];
   float ss = 0.f;
 #pragma unroll
@@ -40,6 +60,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] = bf16_to_f32(a[j]);
+        if constexpr (kGather) rr[idx] = a;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
@@ -179,6 +200,39 @@ void launch_qk_rmsnorm(void* qkv, long stride, const float* qw, const float* kw,
     return;
   }
   qk_rmsnorm_kernel<<<dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s>>>(q, stride, qw, kw, T, nq, nkv, D, eps);
+}
+
+template <bool kWF32>
+static void launch_embed_rmsnorm_t(unsigned short* out, unsigned short* residual, const unsigned short* table,
+                                   const void* w, int rows, int hidden, float eps, GatherIds gi, hipStream_t s) {
+  const int nvec = hidden / 8;
+  dim3 grid(rows);
+  const long xs = hidden;
+  if (norm_threads(hidden) == 256) {
+    if (nvec <= 256)
+      rmsnorm_kernel<256, 1, false, kWF32, true><<<grid, 256, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+    else
+      rmsnorm_kernel<256, 2, false, kWF32, true><<<grid, 256, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+  } else {
+    if (nvec <= 512)
+      rmsnorm_kernel<512, 1, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+    else if (nvec <= 1024)
+      rmsnorm_kernel<512, 2, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+    else
+      rmsnorm_kernel<512, 4, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+  }
+}
+
+void launch_embed_rmsnorm(void* out, void* residual, const void* table, const long* ids, const long* src,
+                          const long* tok, const void* w, bool weight_f32, int rows, int hidden, float eps,
+                          hipStream_t s) {
+  if (rows <= 0) return;
+  auto* o = static_cast<unsigned short*>(out);
+  auto* r = static_cast<unsigned short*>(residual);
+  auto* t = static_cast<const unsigned short*>(table);
+  const GatherIds gi{ids, src, tok};
+  if (weight_f32) launch_embed_rmsnorm_t<true>(o, r, t, w, rows, hidden, eps, gi, s);
+  else launch_embed_rmsnorm_t<false>(o, r, t, w, rows, hidden, eps, gi, s);
 }
 
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,

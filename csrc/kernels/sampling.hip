@@ -824,15 +824,17 @@ size_t sample_workspace_floats(int rows, int V) {
 template <typename T>
 static void launch_sample_mc(long* out_tok, float* out_lp, const T* logits, long stride, int rows, int V,
                              const float* temperature, const int* top_k, const float* top_p, const long* seeds,
-                             const long* steps, float* ws, hipStream_t s) {
+                             const long* steps, float* ws, bool two_rounds, hipStream_t s) {
   const int C = (V + kMcChunk - 1) / kMcChunk;
   const dim3 cg(C, rows);
   mc_stats_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, temperature, top_k, top_p, ws, C);
   mc_coarse_kernel<<<rows, 64, 0, s>>>(out_tok, out_lp, temperature, top_k, top_p, V, ws, C);
   mc_fine_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, ws, C, 0);
   mc_thresh_kernel<<<rows, 256, 0, s>>>(top_k, top_p, V, ws, C, 0);
-  mc_fine_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, ws, C, 1);
-  mc_thresh_kernel<<<rows, 256, 0, s>>>(top_k, top_p, V, ws, C, 1);
+  if (two_rounds) {  // rows with top-k AND top-p may need a second fine round; else it is a no-op
+    mc_fine_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, ws, C, 1);
+    mc_thresh_kernel<<<rows, 256, 0, s>>>(top_k, top_p, V, ws, C, 1);
+  }
   mc_gumbel_kernel<T><<<cg, kMcThreads, 0, s>>>(logits, stride, V, seeds, steps, ws, C);
   mc_final_kernel<T><<<rows, 64, 0, s>>>(out_tok, out_lp, logits, stride, V, ws, C);
 }
@@ -840,15 +842,15 @@ static void launch_sample_mc(long* out_tok, float* out_lp, const T* logits, long
 void launch_sample(long* out_tok, float* out_lp, const void* logits, bool is_bf16,
                    long stride, int rows, int V, const float* temperature,
                    const int* top_k, const float* top_p, const long* seeds,
-                   const long* steps, float* ws, hipStream_t s) {
+                   const long* steps, float* ws, hipStream_t s, bool two_rounds) {
   if (rows <= 0) return;
   if (ws != nullptr && V >= kMcMinVocab) {
     if (is_bf16)
       launch_sample_mc(out_tok, out_lp, static_cast<const unsigned short*>(logits), stride, rows, V, temperature,
-                       top_k, top_p, seeds, steps, ws, s);
+                       top_k, top_p, seeds, steps, ws, two_rounds, s);
     else
       launch_sample_mc(out_tok, out_lp, static_cast<const float*>(logits), stride, rows, V, temperature, top_k,
-                       top_p, seeds, steps, ws, s);
+                       top_p, seeds, steps, ws, two_rounds, s);
     return;
   }
   if (is_bf16)

@@ -47,6 +47,32 @@ void fused_add_rmsnorm(at::Tensor& out, const at::Tensor& x, at::Tensor& residua
                            x.stride(0), out.stride(0), (float)eps, cur_stream());
 }
 
+// out = RMSNorm(table[id]) * weight, residual = table[id] per row; id = ids[row], or
+// tok[src[row]] where src[row] >= 0 (device-side decode lookahead ids)
+void embed_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& table, const at::Tensor& ids,
+                   const c10::optional<at::Tensor>& src, const c10::optional<at::Tensor>& tok,
+                   const at::Tensor& weight, double eps) {
+  CHECK_DEV(table); CHECK_BF16(table); CHECK_BF16(out); CHECK_BF16(residual);
+  CHECK_CONTIG(table); CHECK_CONTIG(out); CHECK_CONTIG(residual); CHECK_CONTIG(ids);
+  TORCH_CHECK(table.dim() == 2 && out.dim() == 2 && residual.sizes() == out.sizes());
+  const int hidden = table.size(1), rows = ids.numel();
+  TORCH_CHECK(out.size(0) == rows && out.size(1) == hidden);
+  TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_cuda());
+  TORCH_CHECK(src.has_value() == tok.has_value(), "src and tok come together");
+  if (src.has_value()) {
+    TORCH_CHECK(src->scalar_type() == at::kLong && tok->scalar_type() == at::kLong && src->numel() == rows);
+    TORCH_CHECK(src->is_contiguous() && tok->is_contiguous() && src->is_cuda() && tok->is_cuda());
+  }
+  TORCH_CHECK(weight.numel() == hidden && weight.is_contiguous());
+  TORCH_CHECK(weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  hipserve::launch_embed_rmsnorm(out.data_ptr(), residual.data_ptr(), table.data_ptr(), ids.data_ptr<long>(),
+                                 src.has_value() ? src->data_ptr<long>() : nullptr,
+                                 tok.has_value() ? tok->data_ptr<long>() : nullptr, weight.data_ptr(),
+                                 weight.scalar_type() == at::kFloat, rows, hidden, (float)eps, cur_stream());
+}
+
 void silu_and_mul(at::Tensor& out, const at::Tensor& x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0));
@@ -186,7 +212,7 @@ void gelu_and_mul(at::Tensor& out, const at::Tensor& x) {
 
 void sample(at::Tensor& out_tok, at::Tensor& out_lp, const at::Tensor& logits,
             const at::Tensor& temperature, const at::Tensor& top_k, const at::Tensor& top_p,
-            const at::Tensor& seeds, const at::Tensor& steps) {
+            const at::Tensor& seeds, const at::Tensor& steps, bool two_rounds) {
   CHECK_DEV(logits); CHECK_ROWMAJOR(logits);
   TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat);
   TORCH_CHECK(out_tok.scalar_type() == at::kLong && out_lp.scalar_type() == at::kFloat);
@@ -205,7 +231,8 @@ void sample(at::Tensor& out_tok, at::Tensor& out_lp, const at::Tensor& logits,
                           logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
                           logits.stride(0), rows, logits.size(1), temperature.data_ptr<float>(),
                           top_k.data_ptr<int>(), top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(),
-                          steps.data_ptr<int64_t>(), wsn ? ws.data_ptr<float>() : nullptr, cur_stream());
+                          steps.data_ptr<int64_t>(), wsn ? ws.data_ptr<float>() : nullptr, cur_stream(),
+                          two_rounds);
 }
 
 void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const at::Tensor& d,
@@ -874,6 +901,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("moe_decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k, int N, int splits, bool packed, bool glu) -> ()");
   m.def("moe_combine_partial(Tensor(a!) out, Tensor ws, Tensor w, Tensor pair_slot, int k) -> ()");
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps) -> ()");
+  m.def("embed_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor table, Tensor ids, Tensor? src, Tensor? tok, "
+        "Tensor weight, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
@@ -916,11 +945,12 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("layernorm(Tensor(a!) out, Tensor x, Tensor w, Tensor b, Tensor(b!)? residual, float eps) -> ()");
   m.def("gelu_(Tensor(a!) x, bool tanh_approx) -> ()");
   m.def("vision_attention(Tensor(a!) out, Tensor(b!) qkv, Tensor cos_sin, Tensor cu, Tensor tiles, int nh, int D, float scale) -> ()");
-  m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps) -> ()");
+  m.def("sample(Tensor(a!) out_tok, Tensor(b!) out_lp, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor steps, bool two_rounds=True) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("rmsnorm", &rmsnorm);
+  m.impl("embed_rmsnorm", &embed_rmsnorm);
   m.impl("layernorm", &layernorm);
   m.impl("gelu_", &gelu_);
   m.impl("vision_attention", &vision_attention);

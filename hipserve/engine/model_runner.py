@@ -476,22 +476,30 @@ class ModelRunner:
         meta.mm_deepstack = [torch.cat([d[j] for d in dss]).to(self.model.dtype) for j in range(len(dss[0]))]
 
     # ------------------------------------------------------------ hipGraphs
-    def _graph_forward(self, b: int):
+    def _graph_forward(self, b: int, full: bool = True):
+        """The captured decode step. The lean variant (``full=False``) leaves out the
+        OpenAI penalty and top-n logprob kernels and the sampler's second threshold
+        round (needed only by rows that combine top-k with top-p); a step whose rows
+        need none of them replays it: five launches fewer, ~35 us of a ~5.4 ms
+        Llama-3-8B step."""
         st = self._static
         meta = AttnMeta(num_prefill_tokens=0, num_decode=b, positions=st["pos"][:b],
                         slot_mapping=st["slots"][:b], bt_decode=st["bt"][:b], ctx_decode=st["ctx"][:b],
                         tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
-        src = st["src"][:b]
-        ids = torch.where(src >= 0, st["tok"].index_select(0, src.clamp(min=0)), st["ids"][:b])
-        hidden = self.model.forward(ids, meta, self.kv)
+        # lookahead ids: resolved inside the model's first kernel when it can
+        # (embed_rmsnorm), else by the id select below
+        meta.id_src = (st["src"][:b], st["tok"])
+        hidden = self.model.forward(st["ids"][:b], meta, self.kv)
         logits = self.model.compute_logits(hidden)
         # penalties / top-n logprobs: early-exit kernels for rows that want none
-        self.ops.penalty_apply(logits, st["pslot"][:b], st["pres"][:b], st["freq"][:b], st["rep"][:b],
-                               self.pen_counts, self.pen_seen)
+        if full:
+            self.ops.penalty_apply(logits, st["pslot"][:b], st["pres"][:b], st["freq"][:b], st["rep"][:b],
+                                   self.pen_counts, self.pen_seen)
         self.ops.sample(st["tok"][:b], st["lp"][:b], logits, st["temp"][:b], st["topk"][:b],
-                        st["topp"][:b], st["seeds"][:b], st["steps"][:b])
-        self.ops.penalty_update(st["tok"][:b], st["pslot"][:b], self.pen_counts, self.pen_seen)
-        self.ops.top_logprobs(logits, st["nlp"][:b], st["top_ids"][:b], st["top_lp"][:b])
+                        st["topp"][:b], st["seeds"][:b], st["steps"][:b], two_rounds=full)
+        if full:
+            self.ops.penalty_update(st["tok"][:b], st["pslot"][:b], self.pen_counts, self.pen_seen)
+            self.ops.top_logprobs(logits, st["nlp"][:b], st["top_ids"][:b], st["top_lp"][:b])
 
     def _stage_in(self, b: int, sg):
         """Pinned staging set -> device static inputs, one zero-copy dispatch
@@ -570,14 +578,15 @@ class ModelRunner:
             # copies captured inside, so consecutive steps are back-to-back graphs
             # (a standalone dispatch after a graph waits ~0.2 ms for the graph's end)
             for par in ((0, 1) if self._stage_kernel else (None,)):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self.graph_pool):
-                    if par is not None:
-                        self._stage_in(b, self._stage[par])
-                    self._graph_forward(b)
-                    if par is not None:
-                        self._stage_out(b, self._stage[par])
-                self.graphs[b if par is None else (b, par)] = g
+                for full in (True, False):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self.graph_pool):
+                        if par is not None:
+                            self._stage_in(b, self._stage[par])
+                        self._graph_forward(b, full)
+                        if par is not None:
+                            self._stage_out(b, self._stage[par])
+                    self.graphs[(b, par, full)] = g
         torch.cuda.synchronize(dev)
         self.graph_capture_time = time.time() - t0
 
@@ -635,14 +644,16 @@ class ModelRunner:
             af[3 * mb:3 * mb + n] = 0.0
             af[4 * mb:4 * mb + n] = 1.0
         st = self._static
+        full = (inp.pen_slot is not None or inp.nlogprobs is not None
+                or bool(np.any((inp.top_k[:n] > 0) & (inp.top_p[:n] < 1.0))))
         if self._stage_kernel:  # the graph of this parity stages in/out itself
-            self.graphs[(b, (self._launches - 1) & 1)].replay()
+            self.graphs[(b, (self._launches - 1) & 1, full)].replay()
         else:
             st["d64"].copy_(h64, non_blocking=True)
             st["d32"][: b * W].copy_(h32[: b * W], non_blocking=True)
             st["d32"][mb * W:].copy_(h32[mb * W:], non_blocking=True)
             st["df"].copy_(hf, non_blocking=True)
-            self.graphs[b].replay()
+            self.graphs[(b, None, full)].replay()
             for k in ("tok", "lp", "top_ids", "top_lp"):
                 sg[k][:n].copy_(st[k][:n], non_blocking=True)
         ev = torch.cuda.Event()

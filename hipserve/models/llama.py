@@ -62,6 +62,9 @@ class AttnMeta:
     mm_rows: torch.Tensor | None = None
     mm_embeds: torch.Tensor | None = None
     mm_deepstack: list | None = None
+    # decode lookahead (model_runner): (src, tok) — row i's input id is tok[src[i]]
+    # where src[i] >= 0 (the previous graph step's sampled id), else ids[i]
+    id_src: tuple | None = None
 
 
 @dataclass
@@ -430,6 +433,20 @@ class LlamaModel:
         return (self.fused_decode and meta.num_prefill_tokens == 0
                 and getattr(self.ops, "name", "") == "hip" and self.fused_family)
 
+    def fused_embed_ok(self, meta: AttnMeta) -> bool:
+        """The fused decode forward can take the lookahead ids unresolved (``meta.id_src``):
+        id select + embedding gather + residual copy + first RMSNorm in one kernel
+        (``embed_rmsnorm``, norm.hip). TP=1 only (the vocab-parallel embedding needs a
+        cross-rank sum before the norm)."""
+        return self._fused_ok(meta) and self.tp.world_size == 1 and hasattr(torch.ops.hipserve, "embed_rmsnorm")
+
+    @staticmethod
+    def resolve_ids(ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        if meta.id_src is None:
+            return ids
+        src, tok = meta.id_src
+        return torch.where(src >= 0, tok.index_select(0, src.clamp(min=0)), ids)
+
     def add_rmsnorm(self, out, residual, x, splits, w):
         """residual += x summed over the TP ranks; out = RMSNorm(residual) * w.
         ``x`` is this rank's partial output of a row-parallel projection: fp32
@@ -476,6 +493,7 @@ class LlamaModel:
         Tp, Td = meta.num_prefill_tokens, meta.num_decode
         if self._fused_ok(meta):
             return self.forward_decode_fused(ids, meta, kv_caches)
+        ids = self.resolve_ids(ids, meta)
         h = self.embed_tokens(ids)
         if cfg.embed_scale != 1.0:  # Gemma: embeddings * sqrt(hidden), the scale rounded to the dtype
             h = h * float(torch.tensor(cfg.embed_scale, dtype=h.dtype))
@@ -554,10 +572,16 @@ class LlamaModel:
         T = ids.shape[0]
         D, nq, nkv = self.D, self.nq, self.nkv
         eps = cfg.rms_norm_eps
-        h = self.embed_tokens(ids)
-        residual = h.clone()
-        xn = torch.empty_like(h)
-        ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
+        if meta.id_src is not None and self.fused_embed_ok(meta):
+            residual = torch.empty(T, cfg.hidden_size, device=ids.device, dtype=self.embed.dtype)
+            xn = torch.empty_like(residual)
+            op.embed_rmsnorm(xn, residual, self.embed, ids, meta.id_src[0], meta.id_src[1], self.layers[0].ln1, eps)
+            h = residual
+        else:
+            h = self.embed_tokens(self.resolve_ids(ids, meta))
+            residual = h.clone()
+            xn = torch.empty_like(h)
+            ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
         part, tmp_out, tmp_ml = self._decode_split(T, meta)
         L = len(self.layers)

@@ -98,8 +98,10 @@ class KernelOps:
                                    nq, nkv, scale, window)
         return out
 
-    def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
-        self._op.sample(out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps)
+    def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps, two_rounds=True):
+        """two_rounds=False: no row combines top-k with top-p (the multi-CU sampler's
+        second fine-histogram round is then a no-op and is not launched)."""
+        self._op.sample(out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps, two_rounds)
 
     def penalty_apply(self, logits, slot, pres, freq, rep, counts, seen):
         self._op.penalty_apply(logits, slot, pres, freq, rep, counts, seen)
@@ -219,7 +221,7 @@ class ReferenceOps:
         out.copy_(ref.vision_attention(qkv, cu_seqlens, nh, D, scale))
         return out
 
-    def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps):
+    def sample(self, out_tok, out_lp, logits, temperature, top_k, top_p, seeds, steps, two_rounds=True):
         t, lp = ref.sample(logits, temperature, top_k, top_p, seeds, steps, bf16_row=False)
         n = t.shape[0]
         out_tok[:n].copy_(t)

@@ -23,6 +23,34 @@ def _partials(S, M, N, seed):
     return torch.randn(S, M, N, device=DEV, generator=g) * 0.5
 
 
+@pytest.mark.parametrize("M,H", [(1, 4096), (64, 4096), (37, 2048), (8, 8192), (3, 1024)])
+@pytest.mark.parametrize("wf32", [False, True])
+@pytest.mark.parametrize("lookahead", [False, True])
+def test_embed_rmsnorm_bit_exact(ops, M, H, wf32, lookahead):
+    """embed_rmsnorm (norm.hip gather mode) == id select + F.embedding + clone +
+    rmsnorm, bit for bit; with lookahead, rows with src >= 0 take tok[src]."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + H)
+    V = 5000
+    table = torch.randn(V, H, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = (torch.rand(H, device=DEV, generator=g) + 0.5)
+    w = w if wf32 else w.to(torch.bfloat16)
+    ids = torch.randint(0, V, (M,), device=DEV, generator=g)
+    src = tok = None
+    want_ids = ids
+    if lookahead:
+        tok = torch.randint(0, V, (80,), device=DEV, generator=g)
+        src = torch.randint(-1, 80, (M,), device=DEV, generator=g)
+        want_ids = torch.where(src >= 0, tok.index_select(0, src.clamp(min=0)), ids)
+    h = torch.nn.functional.embedding(want_ids, table)
+    want = torch.empty_like(h)
+    ops.rmsnorm(want, h, w, 1e-5)
+    out = torch.full_like(h, float("nan"))
+    res = torch.full_like(h, float("nan"))
+    torch.ops.hipserve.embed_rmsnorm(out, res, table, ids, src, tok, w, 1e-5)
+    assert torch.equal(res, h)
+    assert torch.equal(out, want)
+
+
 @pytest.mark.parametrize("S,M,N", [(1, 5, 4096), (4, 64, 4096), (8, 17, 2048), (3, 1, 8192)])
 @pytest.mark.parametrize("wf32", [False, True])
 def test_splitk_add_rmsnorm_bit_exact(ops, S, M, N, wf32):
