@@ -97,6 +97,56 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   for (int i = threadIdx.x; i < nbt; i += blockDim.x) bt[i] = btab[i];
   __syncthreads();
 
+  const long kv_head_stride = (long)block_size * D;  // elements per (block, head)
+  const int nchunks = (end - start + kChunk - 1) / kChunk;
+  const int last_tok = ctx - 1;
+  const int bt_base_tok = first_blk * block_size;
+
+  // Software pipeline over this wave's chunks (wave, wave + W, ...): the K / V
+  // loads of the next chunk are issued before the current chunk's MFMAs, from two
+  // register sets used alternately (loop unrolled by 2, no exit inside a pair, loads
+  // unconditional with the chunk index clamped), so each chunk's HBM latency hides
+  // behind the previous chunk's math instead of being exposed once per chunk.
+  struct Chunk {
+    u16x8 ka[KS], kb[KS], vv[NB];
+  };
+  // K / V are read exactly once per step by one wave: non-temporal loads (aux nt) keep
+  // them from evicting the weights' and partials' lines and shorten issue -> landed
+  auto ld = [](const unsigned short* p) -> u16x8 {
+    if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
+    else return *reinterpret_cast<const u16x8*>(p);
+  };
+  auto load_chunk = [&](int c, Chunk& ch) {
+    const int cs = start + min(c, nchunks - 1) * kChunk;
+    // K: tile a row m -> token 8*(m>>2) + (m&3); tile b -> +4
+    const int m = col;
+    int ta = cs + 8 * (m >> 2) + (m & 3);
+    int tb = ta + 4;
+    ta = min(ta, last_tok);
+    tb = min(tb, last_tok);
+    const unsigned short* ka = k_cache +
+        ((long)bt[(ta - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
+        (long)(ta % block_size) * D + 8 * grp;
+    const unsigned short* kb = k_cache +
+        ((long)bt[(tb - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
+        (long)(tb % block_size) * D + 8 * grp;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      ch.ka[ks] = ld(ka + 32 * ks);
+      ch.kb[ks] = ld(kb + 32 * ks);
+    }
+    // V: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
+    int tv = cs + 8 * grp;
+    if (tv > last_tok) tv = last_tok & ~7;
+    const unsigned short* vb = v_cache +
+        ((long)bt[(tv - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
+        (tv % block_size) + (long)col * block_size;
+#pragma unroll
+    for (int n = 0; n < NB; ++n) ch.vv[n] = ld(vb + (long)16 * n * block_size);
+  };
+  Chunk A, B;
+  bool pre = false;  // kQKV: this wave's first chunk already in flight (A)
+
   // Q fragment: B[k = d][n = head]; lane holds head `col`, d = 8*grp + 32*ks + j
   bf16x8 qf[KS];
   if constexpr (!kQKV) {
@@ -110,6 +160,13 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     }
   } else {
     static_assert(!kQKV || KS % 2 == 0, "fused qkv decode: head_dim 64 or 128");
+    // this wave's first K / V chunk goes out before the partial sums below, so their
+    // latency overlaps the stream instead of preceding it — unless that chunk is the
+    // last one, which holds the new token written below
+    if (wave < nchunks && !(end == ctx && wave == nchunks - 1)) {
+      load_chunk(wave, A);
+      pre = true;
+    }
     constexpr int half = D / 2;
     const long pos = qi.positions[b];
     const float* cs = qi.cos_sin + pos * D;
@@ -170,51 +227,59 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
       }
     }
     // --- q: sum, round, RoPE in-lane (partner d +- D/2 is fragment ks +- KS/2;
-    //     interleaved pairs sit inside each 8-run), round
-    float qv[KS][8];
+    //     interleaved pairs sit inside each 8-run), round. Computed ONCE per workgroup:
+    //     wave w owns fragment pair (w, w + KS/2) (rotate-half) or fragment w
+    //     (interleaved), publishes it in LDS, and every wave reads all KS fragments
+    //     after the barrier (which also orders the new token's K / V stores before any
+    //     wave's loads of the last chunk)
+    u16x8* qsh = reinterpret_cast<u16x8*>(olds + kDecWaves * 16 * D);  // [KS][64 lanes]
     const int h = kh * G + col;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    auto q_frag = [&](int ks, float (&v)[8]) {
       if (col < G) {
-        qkv_sum8(qv[ks], wrow + (long)h * D + 8 * grp + 32 * ks, qi.slice, qi.S);
+        qkv_sum8(v, wrow + (long)h * D + 8 * grp + 32 * ks, qi.slice, qi.S);
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qv[ks][j] = 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
       }
-    }
-    if (qi.mode == 0) {
+    };
+    auto q_store = [&](int ks, const float (&v)[8]) {
+      u16x8 u;
 #pragma unroll
-      for (int ks = 0; ks < KS / 2; ++ks)
+      for (int j = 0; j < 8; ++j) u[j] = col < G ? f32_to_bf16(v[j]) : 0;
+      qsh[ks * 64 + lane] = u;
+    };
+    if (qi.mode == 0) {
+      for (int ks = wave; ks < KS / 2; ks += kDecWaves) {
+        float x[8], y[8];
+        q_frag(ks, x);
+        q_frag(ks + KS / 2, y);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int i = 8 * grp + 32 * ks + j;
           const float co = cs[i], si = cs[half + i];
-          const float x = qv[ks][j], y = qv[ks + KS / 2][j];
-          rope_rot(x, y, co, si, qv[ks][j], qv[ks + KS / 2][j]);
+          const float a = x[j], bb = y[j];
+          rope_rot(a, bb, co, si, x[j], y[j]);
         }
+        q_store(ks, x);
+        q_store(ks + KS / 2, y);
+      }
     } else {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+      for (int ks = wave; ks < KS; ks += kDecWaves) {
+        float x[8];
+        q_frag(ks, x);
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const int i = (8 * grp + 32 * ks) / 2 + p;
           const float co = cs[i], si = cs[half + i];
-          const float x = qv[ks][2 * p], y = qv[ks][2 * p + 1];
-          rope_rot(x, y, co, si, qv[ks][2 * p], qv[ks][2 * p + 1]);
+          const float a = x[2 * p], bb = x[2 * p + 1];
+          rope_rot(a, bb, co, si, x[2 * p], x[2 * p + 1]);
         }
+        q_store(ks, x);
+      }
     }
+    __syncthreads();
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      u16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = col < G ? f32_to_bf16(qv[ks][j]) : 0;
-      qf[ks] = __builtin_bit_cast(bf16x8, v);
-    }
-    // the writing wave's own later loads of the last chunk (other lanes) must see its
-    // stores: workgroup-scope release / acquire = wait for the stores to complete (an
-    // agent-scope fence would write back the whole L2 from every workgroup)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, qsh[ks * 64 + lane]);
   }
   const float sl2 = scale * kLog2e;
   f32x4 o[NB];
@@ -222,53 +287,6 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   for (int n = 0; n < NB; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -1e30f, l_run = 0.f;
 
-  const long kv_head_stride = (long)block_size * D;  // elements per (block, head)
-  const int nchunks = (end - start + kChunk - 1) / kChunk;
-  const int last_tok = ctx - 1;
-  const int bt_base_tok = first_blk * block_size;
-
-  // Software pipeline over this wave's chunks (wave, wave + W, ...): the K / V
-  // loads of the next chunk are issued before the current chunk's MFMAs, from two
-  // register sets used alternately (loop unrolled by 2, no exit inside a pair, loads
-  // unconditional with the chunk index clamped), so each chunk's HBM latency hides
-  // behind the previous chunk's math instead of being exposed once per chunk.
-  struct Chunk {
-    u16x8 ka[KS], kb[KS], vv[NB];
-  };
-  // K / V are read exactly once per step by one wave: non-temporal loads (aux nt) keep
-  // them from evicting the weights' and partials' lines and shorten issue -> landed
-  auto ld = [](const unsigned short* p) -> u16x8 {
-    if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
-    else return *reinterpret_cast<const u16x8*>(p);
-  };
-  auto load_chunk = [&](int c, Chunk& ch) {
-    const int cs = start + min(c, nchunks - 1) * kChunk;
-    // K: tile a row m -> token 8*(m>>2) + (m&3); tile b -> +4
-    const int m = col;
-    int ta = cs + 8 * (m >> 2) + (m & 3);
-    int tb = ta + 4;
-    ta = min(ta, last_tok);
-    tb = min(tb, last_tok);
-    const unsigned short* ka = k_cache +
-        ((long)bt[(ta - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
-        (long)(ta % block_size) * D + 8 * grp;
-    const unsigned short* kb = k_cache +
-        ((long)bt[(tb - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
-        (long)(tb % block_size) * D + 8 * grp;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      ch.ka[ks] = ld(ka + 32 * ks);
-      ch.kb[ks] = ld(kb + 32 * ks);
-    }
-    // V: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
-    int tv = cs + 8 * grp;
-    if (tv > last_tok) tv = last_tok & ~7;
-    const unsigned short* vb = v_cache +
-        ((long)bt[(tv - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
-        (tv % block_size) + (long)col * block_size;
-#pragma unroll
-    for (int n = 0; n < NB; ++n) ch.vv[n] = ld(vb + (long)16 * n * block_size);
-  };
   auto compute_chunk = [&](int c, const Chunk& ch) {
     const int cs = start + c * kChunk;
     // ---- S^T = K . Q^T
@@ -318,8 +336,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   constexpr int W = kDecWaves;
   int c = wave;
   if (c < nchunks) {
-    Chunk A, B;
-    load_chunk(c, A);
+    if (!pre) load_chunk(c, A);
     for (; c + W < nchunks; c += 2 * W) {
       load_chunk(c + W, B);
       __builtin_amdgcn_sched_barrier(0);
@@ -398,7 +415,9 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(
 }
 
 static size_t smem_bytes(int D, int waves) {
-  return 1024 + (size_t)2 * waves * 16 * sizeof(float) + (size_t)waves * 16 * D * sizeof(float);
+  // block ids, per-wave (m, l), per-wave O, then the fused path's q fragments [D/32][64] x 16 B
+  return 1024 + (size_t)2 * waves * 16 * sizeof(float) + (size_t)waves * 16 * D * sizeof(float) +
+         (size_t)(D / 32) * 64 * 16;
 }
 
 size_t paged_decode_smem_bytes(int D) { return smem_bytes(D, kDecWavesMax); }
@@ -483,9 +502,16 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
   auto* vc = static_cast<unsigned short*>(v_cache);
   const QkvIn qi{ws, (long)B * N, S, N, positions, slots, cos_sin, kc, vc, mode};
 #define HS_DECODE_QKV(DD, WW)                                                                                  \
-  paged_decode_kernel<DD, WW, true><<<grid, block, smem, s>>>(o, out_stride, nullptr, 0, kc, vc, block_tables,  \
-                                                             bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv,  \
-                                                             block_size, part_size, max_parts, scale, window, qi)
+  do {                                                                                                        \
+    if (decode_nt((long)max_parts * nkv * B))                                                                 \
+      paged_decode_kernel<DD, WW, true, true><<<grid, block, smem, s>>>(                                      \
+          o, out_stride, nullptr, 0, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, \
+          block_size, part_size, max_parts, scale, window, qi);                                               \
+    else                                                                                                      \
+      paged_decode_kernel<DD, WW, true, false><<<grid, block, smem, s>>>(                                     \
+          o, out_stride, nullptr, 0, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, \
+          block_size, part_size, max_parts, scale, window, qi);                                               \
+  } while (0)
 #define HS_DECODE_QKV_D(DD)                                                                                   \
   do {                                                                                                        \
     if (waves == 8) HS_DECODE_QKV(DD, 8);                                                                     \

@@ -111,10 +111,12 @@ class LlamaModel:
     # dequantising them to bf16 at load (weights/safetensors_loader.py)
     native_fp8 = True
     # fused decode: qkv partials -> RoPE + KV write + attention in one kernel
-    # (attention_decode.hip QkvIn), opt-in with HIPSERVE_FUSED_QKV_ATTN=1. Bit-exact,
-    # but measured SLOWER on Llama-3-8B B=64 (5.57 vs 5.49 ms per decode step,
-    # tools/decode_gap.py): every wave re-reads the fp32 partials for q before it can
-    # stream K/V, which costs more than the separate splitk_rope_cache launch saves
+    # (attention_decode.hip QkvIn), opt-in with HIPSERVE_FUSED_QKV_ATTN=1. Bit-exact.
+    # First version: 5.57 vs 5.49 ms per Llama-3-8B B=64 decode step (every wave re-read
+    # the fp32 partials for q before streaming K/V). Now each wave's first K/V chunk is
+    # issued before the partial sums and q is computed once per workgroup (shared via
+    # LDS): 5.322 / 5.332 vs 5.332 / 5.327 ms (tools/decode_gap.py, alternating runs) —
+    # parity, so the separate splitk_rope_cache launch stays the default
     fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "0") == "1"
 
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,

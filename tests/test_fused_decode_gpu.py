@@ -177,13 +177,21 @@ def test_fused_decode_forward_families_bit_exact(ops, family):
     test_fused_decode_forward_bit_exact(ops, "dgp", family)
 
 
+@pytest.mark.parametrize("choices", ["dgp", "mixed"])
+def test_fused_qkv_attention_forward_bit_exact(ops, choices):
+    """The decode layer with qkv partials -> RoPE + KV write + attention in one kernel
+    (paged_decode_qkv) vs the unfused path."""
+    test_fused_decode_forward_bit_exact(ops, choices, qkv_attn=True)
+
+
 @pytest.mark.parametrize("choices", ["dgp", "dg", "mixed"])
-def test_fused_decode_forward_bit_exact(ops, choices, family="llama"):
+def test_fused_decode_forward_bit_exact(ops, choices, family="llama", qkv_attn=False):
     """Model forward on a decode batch: fused epilogues vs the unfused path."""
     from hipserve.models.llama import AttnMeta
 
     m, cfg = _small_model(ops, family=family)
     assert m.fused_family
+    m.fused_qkv_attention = qkv_attn
     old = dict(gemm.TUNER.table)
     try:
         gemm.TUNER.table.clear()

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--kernels", type=int, default=274)
     ap.add_argument("--elems", type=int, default=1 << 16, help="elements touched per kernel")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--event", action="store_true",
+                    help="record a torch.cuda.Event after every replay, as the engine's launch() does")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     x = torch.randn(a.elems, device=dev)
@@ -59,13 +61,15 @@ def main():
     for i in range(a.reps):
         t = time.perf_counter()
         graphs[i & 1].replay()
+        if a.event:
+            torch.cuda.Event().record()
         host.append(time.perf_counter() - t)
     e1.record()
     torch.cuda.synchronize()
     b2b = e0.elapsed_time(e1) / a.reps
     single.sort()
     host.sort()
-    print(json.dumps({"kernels": a.kernels, "graph_device_ms": round(single[len(single) // 2], 4),
+    print(json.dumps({"kernels": a.kernels, "event": a.event, "graph_device_ms": round(single[len(single) // 2], 4),
                       "back_to_back_ms_per_replay": round(b2b, 4),
                       "gap_us": round(1000 * (b2b - single[len(single) // 2]), 1),
                       "host_replay_us_p50": round(1e6 * host[len(host) // 2], 1)}), flush=True)
