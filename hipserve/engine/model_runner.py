@@ -139,6 +139,14 @@ class ModelRunner:
             shapes = [s for s in self.model.gemm_shapes() if s != tuple(getattr(self.model.lm_head, "shape", ()))]
             self.prefill_gemm_report = prefill_tune.tune(shapes, [ecfg.max_num_batched_tokens], self.device)
             torch.cuda.empty_cache()
+        # ragged prefill chunks: hipBLASLt's heuristic picks slower kernels for some
+        # token counts (Llama-3-8B: the 4-projection chain takes 21.7 ms at 7,393 rows
+        # vs 18.8 ms at 8,192, tools/bench_prefill_m.py); rank 0 times the model's
+        # prefill GEMMs per 256-row count once and pads a chunk to the fastest count at
+        # or above it (padding rows: token 0, no KV write, outputs unused)
+        self.prefill_pad = None
+        if (self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0):
+            self.prefill_pad = self._probe_prefill_pad()
         # device penalty state: one slot per concurrently running penalised sequence
         V = mcfg.vocab_size
         nslots = max(1, min(ecfg.max_num_seqs, int(ecfg.extra.get("penalty_slots", 256))))
@@ -220,6 +228,54 @@ class ModelRunner:
         # all TP ranks must agree on the pool size
         return self.tp.min_int(n)
 
+    @torch.inference_mode()
+    def _probe_prefill_pad(self) -> dict | None:
+        """{rows rounded up to 256: the row count (>= it, <= the token budget) whose
+        prefill GEMM chain (qkv, o, gate|up, down of one layer, hipBLASLt) is fastest};
+        None for models whose prefill is not four dense bf16 projections (MoE, quantised)."""
+        import torch.nn.functional as F
+
+        layers = getattr(self.model, "layers", None)
+        if not layers or any(getattr(lw, "router", None) is not None for lw in layers):
+            return None
+        lw = layers[0]
+        ws = [getattr(lw, n, None) for n in ("wqkv", "wo", "wgu", "wd")]
+        if not all(isinstance(w, torch.Tensor) and w.dim() == 2 and w.dtype == torch.bfloat16 for w in ws):
+            return None
+        budget = self.ecfg.max_num_batched_tokens
+        ms = list(range(1024, budget + 1, 256))
+        if len(ms) < 2:
+            return None
+        x = torch.randn(budget, max(w.shape[1] for w in ws), device=self.device, dtype=torch.bfloat16)
+
+        def chain(m):
+            for w in ws:
+                F.linear(x[:m, :w.shape[1]], w)
+
+        times = {}
+        for m in ms:
+            chain(m)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(2):
+                chain(m)
+            e1.record()
+            e1.synchronize()
+            times[m] = e0.elapsed_time(e1)
+        del x
+        pad, best_t, best_m = {}, float("inf"), None
+        for m in reversed(ms):  # prefer the smaller count unless a larger one is >3 % faster
+            if times[m] <= best_t * 1.03:
+                best_t, best_m = min(times[m], best_t), m
+            pad[m] = best_m
+        self.prefill_pad_times = {m: round(t / 2, 3) for m, t in times.items()}
+        return {m: p for m, p in pad.items() if p > m}
+
+    def _pad_rows(self, T: int) -> int:
+        if not self.prefill_pad or T < 1024:
+            return T
+        return self.prefill_pad.get(-(-T // 256) * 256, T)
+
     @property
     def usable_blocks(self) -> int:
         return self.num_blocks - 1
@@ -248,6 +304,14 @@ class ModelRunner:
                 else:
                     ids[t:t + s.num_tokens] = q.all_token_ids()[s.start:s.end]
             t += s.num_tokens
+        if np_ and not any(s.seq.mm is not None for s in seqs):
+            Tpad = self._pad_rows(len(ids))
+            if Tpad > len(ids):  # padding rows: token 0 at position 0, no KV write
+                extra = Tpad - len(ids)
+                ids = np.concatenate([ids, np.zeros(extra, np.int64)])
+                pos = np.concatenate([pos, np.zeros(extra, pos.dtype)])
+                slots = np.concatenate([slots, np.full(extra, -1, slots.dtype)])
+                self.stats["padded_rows"] = self.stats.get("padded_rows", 0) + extra
         Tp = sum(s.num_tokens for s in so.prefill)
         rows = []
         t = 0

@@ -524,8 +524,8 @@ class LlamaModel:
             if Tp:
                 ops.prefill_attention(attn[:Tp], qkv[:Tp], kc, vc, meta.bt_prefill, meta.cu_q,
                                       meta.ctx_prefill, meta.tiles, nq, nkv, self.scale, win)
-            if Td:
-                ops.paged_decode(attn[Tp:], qkv[Tp:], kc, vc, meta.bt_decode, meta.ctx_decode,
+            if Td:  # rows past Tp + Td: prefill padding (model_runner._pad_rows)
+                ops.paged_decode(attn[Tp:Tp + Td], qkv[Tp:Tp + Td], kc, vc, meta.bt_decode, meta.ctx_decode,
                                  tmp_out, tmp_ml, nq, nkv, part, self.scale, win)
             o = self.linear_rowpar(attn, lw.wo)
             if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)

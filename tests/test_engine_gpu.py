@@ -208,3 +208,26 @@ def test_decode_lookahead_stop_tokens():
     assert not e.has_unfinished()
     e.blocks.reset_prefix_cache()
     assert e.blocks.num_free() == free0
+
+
+def test_prefill_row_padding():
+    """A ragged prefill chunk padded to a faster GEMM row count (model_runner._pad_rows:
+    padding rows are token 0 with no KV write) generates what the unpadded engine
+    does: the startup probe's table is replaced by a forced one so padding happens."""
+    def eng():
+        cfg = EngineConfig(model="small-llama", device="cuda", max_num_seqs=16, max_num_batched_tokens=2048,
+                           max_model_len=2048, num_kv_blocks=512)
+        return LLMEngine(cfg, tp=TPGroup(0, 1, None, torch.device("cuda", 0)))
+
+    prompts = [[1] + list(range(10, 700)), [1] + list(range(5, 500)), list(range(3, 310))]  # 1,494 rows
+    sp = SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True)
+    a = eng()
+    a.runner.prefill_pad = {1536: 2048}
+    ra = a.generate(prompts, sp)
+    assert a.runner.stats.get("padded_rows", 0) == 2048 - sum(len(p) for p in prompts)
+    b = eng()
+    b.runner.prefill_pad = None
+    rb = b.generate(prompts, sp)
+    same = sum(x == y for p, q in zip(ra, rb) for x, y in zip(p[0], q[0]))
+    assert all(p[0][0] == q[0][0] for p, q in zip(ra, rb)), (ra, rb)
+    assert same >= 0.9 * 16 * len(prompts), (ra, rb)
