@@ -10,6 +10,8 @@
 //                                              16-byte loads straight to VGPRs)
 // cos_sin: [max_pos, D] fp32 = [cos(D/2) | sin(D/2)].
 // mode: 0 = NeoX rotate-half (HF Llama), 1 = interleaved pairs (GGUF llama).
+#include <cstdlib>
+
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -110,6 +112,124 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
   }
 }
 
+// Prefill form: one workgroup per 16 consecutive tokens. q / k exactly as above
+// (flattened (token, item) loop); V goes through LDS so that the 16 lanes of a group
+// write 16 consecutive tokens of one V^T row of a block (32 contiguous bytes when the
+// tokens share a block) instead of 64 lanes storing 2 bytes 32 bytes apart — the
+// per-token kernel's scattered V stores cost about half of its time at 8K-token chunks.
+constexpr int kRopeTile = 16;
+
+template <int kMode>
+__global__ __launch_bounds__(256) void rope_cache_tile_kernel(
+    unsigned short* __restrict__ qkv, long qkv_stride, const long* __restrict__ positions,
+    const long* __restrict__ slots, const float* __restrict__ cos_sin, unsigned short* __restrict__ k_cache,
+    unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D, int block_size) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short vs[];  // [16][nkv * D + 8]
+  const int t0 = blockIdx.x * kRopeTile;
+  const int nt = min(kRopeTile, T - t0);
+  const int half = D / 2;
+  const int chunks = kMode == 0 ? half / 8 : D / 8;
+  // thread -> (token, 8-wide chunk c, head parity): the chunk's cos / sin sit in
+  // registers and are reused over every second q / k head of the token (the per-token
+  // kernel re-read them from cache for each head: 4x the qkv bytes)
+  const int nh = nq + nkv;
+  const int per_tok = chunks * 2;
+  for (int it = threadIdx.x; it < nt * per_tok; it += blockDim.x) {
+    const int tt = it / per_tok, c = (it % per_tok) >> 1, hpar = it & 1;
+    const int t = t0 + tt;
+    const long pos = positions[t];
+    const long slot = slots[t];
+    const float* cs = cos_sin + pos * D;
+    unsigned short* row = qkv + t * qkv_stride;
+    const long blk = slot >= 0 ? slot / block_size : 0;
+    const int off = slot >= 0 ? (int)(slot % block_size) : 0;
+    if constexpr (kMode == 0) {
+      float co[8], si[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { co[j] = cs[c * 8 + j]; si[j] = cs[half + c * 8 + j]; }
+      // 4 heads per batch with all their loads issued first: the per-thread head
+      // loop is otherwise one dependent memory round trip per head
+      for (int h0 = hpar; h0 < nh; h0 += 8) {
+        u16x8 va[4], vb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int h = min(h0 + 2 * q, nh - 1);
+          va[q] = *reinterpret_cast<const u16x8*>(row + h * D + c * 8);
+          vb[q] = *reinterpret_cast<const u16x8*>(row + h * D + half + c * 8);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int h = h0 + 2 * q;
+          if (h >= nh || (h >= nq && slot < 0)) continue;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float ra, rb;
+            rope_rot(bf16_to_f32(va[q][j]), bf16_to_f32(vb[q][j]), co[j], si[j], ra, rb);
+            va[q][j] = f32_to_bf16(ra);
+            vb[q][j] = f32_to_bf16(rb);
+          }
+          unsigned short* dst = h < nq ? row + h * D
+                                       : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
+          *reinterpret_cast<u16x8*>(dst + c * 8) = va[q];
+          *reinterpret_cast<u16x8*>(dst + half + c * 8) = vb[q];
+        }
+      }
+    } else {
+      float co[4], si[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) { co[p] = cs[c * 4 + p]; si[p] = cs[half + c * 4 + p]; }
+      for (int h0 = hpar; h0 < nh; h0 += 8) {
+        u16x8 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[q] = *reinterpret_cast<const u16x8*>(row + min(h0 + 2 * q, nh - 1) * D + c * 8);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int h = h0 + 2 * q;
+          if (h >= nh || (h >= nq && slot < 0)) continue;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            float ra, rb;
+            rope_rot(bf16_to_f32(v[q][2 * p]), bf16_to_f32(v[q][2 * p + 1]), co[p], si[p], ra, rb);
+            v[q][2 * p] = f32_to_bf16(ra);
+            v[q][2 * p + 1] = f32_to_bf16(rb);
+          }
+          unsigned short* dst = h < nq ? row + h * D
+                                       : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
+          *reinterpret_cast<u16x8*>(dst + c * 8) = v[q];
+        }
+      }
+    }
+  }
+  // V rows of the tile -> LDS (16-byte loads), then token-fastest 2-byte stores
+  const int VW = nkv * D, VR = VW + 8;  // LDS row stride: +16 B keeps the 16 token rows on distinct banks
+  const int vchunks = VW / 8;
+  for (int it = threadIdx.x; it < nt * vchunks; it += blockDim.x) {
+    const int tt = it / vchunks, c = it % vchunks;
+    *reinterpret_cast<u16x8*>(vs + tt * VR + c * 8) =
+        *reinterpret_cast<const u16x8*>(qkv + (t0 + tt) * qkv_stride + (nq + nkv) * D + c * 8);
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < kRopeTile * VW; it += blockDim.x) {
+    const int tt = it & (kRopeTile - 1), r = it / kRopeTile;
+    if (tt >= nt) continue;
+    const long slot = slots[t0 + tt];
+    if (slot < 0) continue;
+    const int kh = r / D, d = r % D;
+    const long blk = slot / block_size;
+    const int off = (int)(slot % block_size);
+    v_cache[(blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off] = vs[tt * VR + r];
+  }
+}
+
+static bool rope_tile_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("HIPSERVE_ROPE_TILE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
                        const long* slots, const float* cos_sin, void* k_cache,
                        void* v_cache, int T, int nq, int nkv, int D,
@@ -119,6 +239,17 @@ void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
   auto* q = static_cast<unsigned short*>(qkv);
   auto* kc = static_cast<unsigned short*>(k_cache);
   auto* vc = static_cast<unsigned short*>(v_cache);
+  if (T >= 128 && nkv * D <= 2048 && rope_tile_enabled()) {  // prefill chunks
+    const dim3 tg((T + kRopeTile - 1) / kRopeTile);
+    const size_t smem = (size_t)kRopeTile * (nkv * D + 8) * sizeof(unsigned short);
+    if (mode == 0)
+      rope_cache_tile_kernel<0><<<tg, block, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq, nkv,
+                                                        D, block_size);
+    else
+      rope_cache_tile_kernel<1><<<tg, block, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq, nkv,
+                                                        D, block_size);
+    return;
+  }
   if (mode == 0)
     rope_cache_kernel<0><<<grid, block, 0, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, nq, nkv, D, block_size);
   else
