@@ -378,10 +378,12 @@ struct Dec {
   }
 };
 
-HS_DEVICE _Float16 to_f16_sat(unsigned short b) {
-  const float f = fminf(fmaxf(bf16_to_f32(b), -65504.f), 65504.f);
-  return static_cast<_Float16>(f);
-}
+// bf16 word halves -> fp32 (exact: one shift or mask), clamped to the f16 range by one
+// v_med3 (fminf/fmaxf add NaN-canonicalising v_max ops: the x staging is a large share
+// of the M = 64 body's VALU issue, which bounds it)
+HS_DEVICE float bf_lo(unsigned w) { return __builtin_bit_cast(float, w << 16); }
+HS_DEVICE float bf_hi(unsigned w) { return __builtin_bit_cast(float, w & 0xFFFF0000u); }
+HS_DEVICE _Float16 sat16(float f) { return static_cast<_Float16>(__builtin_amdgcn_fmed3f(f, -65504.f, 65504.f)); }
 
 // One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
 // x staging. Body per format; the kernel picks it per part (two formats per launch).
@@ -417,26 +419,36 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
       xg[i] = x + (pr < 0 ? 0L : (long)(moe.gather_k > 0 ? pr / moe.gather_k : slot)) * x_stride;
     }
   }
-  auto load_x = [&](int sb) {
+  // dense: element offset of each staging item's row and k run (32-bit; the prefill
+  // M tiles stay far below 2^31 elements), computed once instead of per super-chunk
+  [[maybe_unused]] int xo[kMoe ? 1 : XP];
+  if constexpr (!kMoe) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
-      const int kb = kbase<QT>(fr >> 3, fr & 7);
+      xo[i] = min(mrow0 + row, M - 1) * (int)x_stride + kbase<QT>(fr >> 3, fr & 7);
+    }
+  }
+  auto load_x = [&](int sb) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
       // rows >= M are clamped, never stored (kMoe: padding slots read row 0, never stored)
-      if constexpr (kMoe)
-        xv[i] = *reinterpret_cast<const u16x8*>(xg[i] + sb * 256 + kb);
-      else
-        xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(mrow0 + row, M - 1) * x_stride + sb * 256 + kb);
+      if constexpr (kMoe) {
+        const int fr = (i * NT + tid) & 31;
+        xv[i] = *reinterpret_cast<const u16x8*>(xg[i] + sb * 256 + kbase<QT>(fr >> 3, fr & 7));
+      } else {
+        xv[i] = *reinterpret_cast<const u16x8*>(x + xo[i] + sb * 256);
+      }
     }
   };
   auto store_x = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
-      const u16x8 b = xv[i];
-      f16x8 h;
-      h[0] = to_f16_sat(b[0]); h[1] = to_f16_sat(b[2]); h[2] = to_f16_sat(b[1]); h[3] = to_f16_sat(b[3]);
-      h[4] = to_f16_sat(b[4]); h[5] = to_f16_sat(b[6]); h[6] = to_f16_sat(b[5]); h[7] = to_f16_sat(b[7]);
+      const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);  // bf16 pairs (0,1) (2,3) (4,5) (6,7)
+      f16x8 h;  // pair order {0, 2, 1, 3, 4, 6, 5, 7}
+      h[0] = sat16(bf_lo(w[0])); h[1] = sat16(bf_lo(w[1])); h[2] = sat16(bf_hi(w[0])); h[3] = sat16(bf_hi(w[1]));
+      h[4] = sat16(bf_lo(w[2])); h[5] = sat16(bf_lo(w[3])); h[6] = sat16(bf_hi(w[2])); h[7] = sat16(bf_hi(w[3]));
       *reinterpret_cast<f16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = h;
     }
   };
