@@ -488,15 +488,21 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
     for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
+      // the step's MT x fragments are read from LDS BEFORE the dequant VALU and held in
+      // MT registers: left to itself the compiler reused one fragment register, so every
+      // MFMA waited out a full LDS round trip (ds_read -> lgkmcnt(0) -> MFMA, x MT)
+      f16x8 b[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t)  // one LDS read of x per (s, t), shared by the RT row groups
+        b[t] = *reinterpret_cast<const f16x8*>(xb + 16 * t * kXR + 8 * s);
+      __builtin_amdgcn_sched_barrier(0);
       f16x8 a[RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {  // one LDS read of x per (s, t), shared by the RT row groups
-        const f16x8 b = *reinterpret_cast<const f16x8*>(xb + 16 * t * kXR + 8 * s);
+      for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int r = 0; r < RT; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b, acc[r][t], 0, 0, 0);
-      }
+        for (int r = 0; r < RT; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b[t], acc[r][t], 0, 0, 0);
     }
     store_x(buf ^ 1);
     __syncthreads();
