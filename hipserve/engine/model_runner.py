@@ -62,6 +62,19 @@ class StepInputs:
     extra: dict = field(default_factory=dict)
 
 
+def pad_table(times: dict, tol: float = 1.03) -> dict:
+    """{row count: larger row count to pad it to} from measured GEMM times per row
+    count: the fastest count at or above each one, where a larger count must be more
+    than ``tol`` faster to be chosen over a smaller one; counts that keep themselves
+    are left out."""
+    pad, best_t, best_m = {}, float("inf"), None
+    for m in sorted(times, reverse=True):
+        if times[m] <= best_t * tol:
+            best_t, best_m = min(times[m], best_t), m
+        pad[m] = best_m
+    return {m: p for m, p in pad.items() if p > m}
+
+
 class ModelRunner:
     def __init__(self, ecfg: EngineConfig, mcfg: ModelConfig, tp: TPGroup, device=None):
         self.ecfg = ecfg
@@ -263,13 +276,8 @@ class ModelRunner:
             e1.synchronize()
             times[m] = e0.elapsed_time(e1)
         del x
-        pad, best_t, best_m = {}, float("inf"), None
-        for m in reversed(ms):  # prefer the smaller count unless a larger one is >3 % faster
-            if times[m] <= best_t * 1.03:
-                best_t, best_m = min(times[m], best_t), m
-            pad[m] = best_m
         self.prefill_pad_times = {m: round(t / 2, 3) for m, t in times.items()}
-        return {m: p for m, p in pad.items() if p > m}
+        return pad_table(times)
 
     def _pad_rows(self, T: int) -> int:
         if not self.prefill_pad or T < 1024:

@@ -160,3 +160,15 @@ def test_penalties_and_logprobs():
     toks = eng.generate([[1, 2, 3]], sp)[0][0]
     # a strong frequency penalty makes greedy avoid immediate repeats
     assert len(set(toks)) >= 6
+
+
+def test_prefill_pad_table():
+    """Ragged-chunk padding table (model_runner.pad_table): each 256-row count maps to
+    the fastest count at or above it, a larger one only when >3 % faster."""
+    from hipserve.engine.model_runner import pad_table
+
+    # hipBLASLt-like cliffs: 7424 / 7680 slower than 7936 / 8192 (profiles/r2_prefill_row_padding.md)
+    t = {6912: 2.433, 7168: 2.245, 7424: 2.746, 7680: 2.72, 7936: 2.349, 8192: 2.32}
+    assert pad_table(t) == {6912: 7168, 7424: 7936, 7680: 7936}
+    assert pad_table({1024: 1.0, 1280: 1.0, 1536: 0.99}) == {}  # within 3 %: keep the smaller count
+    assert pad_table({}) == {}
