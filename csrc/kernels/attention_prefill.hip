@@ -227,20 +227,23 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
   // staging: NP K pieces + NP V^T pieces of 16 B per thread per tile
   // two register sets: tile kt+2 loads while tile kt+1's registers wait for their LDS write
   u16x8 ska[NP], sva[NP], skb[NP], svb[NP];
+  // block sizes are powers of two (launcher check): shifts, not integer divisions,
+  // in the per-tile paging math (the divisions were ~1/3 of the tile's VALU)
+  const int bsh = __builtin_ctz(block_size), bmask = block_size - 1;
   auto stage_load = [&](u16x8(&sk)[NP], u16x8(&sv)[NP], int kt) {
     const int kbase = kt * PA2_KT;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int p = tid + NT * i;
       const int key = min(kbase + (p >> 4), ctx - 1);
-      sk[i] = *reinterpret_cast<const u16x8*>(k_cache + ((long)btab[key / block_size] * nkv + kh) * hstride +
-                                              (long)(key % block_size) * D + (p & 15) * 8);
+      sk[i] = *reinterpret_cast<const u16x8*>(k_cache + ((long)btab[key >> bsh] * nkv + kh) * hstride +
+                                              (long)(key & bmask) * D + (p & 15) * 8);
       // V^T: 16-key group sc, row d, 8-key half: one block's [D][16] chunk per 256 threads
       const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
       int vkey = kbase + 16 * sc + 8 * k8;
       if (vkey > ctx - 1) vkey = (ctx - 1) & ~7;
-      sv[i] = *reinterpret_cast<const u16x8*>(v_cache + ((long)btab[vkey / block_size] * nkv + kh) * hstride +
-                                              (long)d * block_size + vkey % block_size);
+      sv[i] = *reinterpret_cast<const u16x8*>(v_cache + ((long)btab[vkey >> bsh] * nkv + kh) * hstride +
+                                              (long)d * block_size + (vkey & bmask));
     }
   };
   auto stage_store = [&](const u16x8(&sk)[NP], const u16x8(&sv)[NP], int buf) {
@@ -303,7 +306,10 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[h2][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx * sl2);
-      if (!__all(m_new == m_run)) {
+      // deferred rescale: the running max is kept while no row's max grew by more than
+      // 8 (log2 units), so P = exp2(s - m_run) stays <= 256 (exact enough in bf16 / fp32;
+      // O and l always share m_run) and the 64-accumulator rescale runs on few tiles
+      if (!__all(m_new - m_run <= 8.f)) {
         const float alpha = exp2f(m_run - m_new);
         l_run *= alpha;
 #pragma unroll
@@ -378,7 +384,8 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               int block_size, float scale, int window, hipStream_t s) {
   if (ntiles <= 0) return;
   const int G = nq / nkv;
-  if (D == 128 && block_size % 16 == 0 && G >= 2 && (G & (G - 1)) == 0 && !getenv_flag("HIPSERVE_PREFILL_ATTN_V1")) {
+  if (D == 128 && block_size % 16 == 0 && (block_size & (block_size - 1)) == 0 && G >= 2 && (G & (G - 1)) == 0 &&
+      !getenv_flag("HIPSERVE_PREFILL_ATTN_V1")) {
     const char* ew = getenv("HIPSERVE_PREFILL_ATTN_WAVES");  // 8 (default) or 4 waves per workgroup
     const int nwv = (ew != nullptr && atoi(ew) == 4) ? 4 : 8;
     const int HG = G >= nwv ? nwv : G;
