@@ -91,8 +91,10 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   float* red = reinterpret_cast<float*>(smem + 1024);          // m,l per wave/head
   float* olds = red + 2 * kDecWaves * 16;                      // [waves][16][D]
 
-  const int first_blk = start / block_size;
-  const int nbt = (end - 1) / block_size - first_blk + 1;
+  // power-of-two block sizes (EngineConfig): shifts / masks in the per-chunk paging math
+  const int bsh = __builtin_ctz(block_size), bmask = block_size - 1;
+  const int first_blk = start >> bsh;
+  const int nbt = ((end - 1) >> bsh) - first_blk + 1;
   const int* btab = block_tables + (long)b * bt_stride + first_blk;
   for (int i = threadIdx.x; i < nbt; i += blockDim.x) bt[i] = btab[i];
   __syncthreads();
@@ -125,11 +127,11 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     ta = min(ta, last_tok);
     tb = min(tb, last_tok);
     const unsigned short* ka = k_cache +
-        ((long)bt[(ta - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
-        (long)(ta % block_size) * D + 8 * grp;
+        ((long)bt[(ta - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
+        (long)(ta & bmask) * D + 8 * grp;
     const unsigned short* kb = k_cache +
-        ((long)bt[(tb - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
-        (long)(tb % block_size) * D + 8 * grp;
+        ((long)bt[(tb - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
+        (long)(tb & bmask) * D + 8 * grp;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       ch.ka[ks] = ld(ka + 32 * ks);
@@ -139,8 +141,8 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     int tv = cs + 8 * grp;
     if (tv > last_tok) tv = last_tok & ~7;
     const unsigned short* vb = v_cache +
-        ((long)bt[(tv - bt_base_tok) / block_size] * nkv + kh) * kv_head_stride +
-        (tv % block_size) + (long)col * block_size;
+        ((long)bt[(tv - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
+        (tv & bmask) + (long)col * block_size;
 #pragma unroll
     for (int n = 0; n < NB; ++n) ch.vv[n] = ld(vb + (long)16 * n * block_size);
   };

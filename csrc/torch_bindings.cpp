@@ -110,7 +110,7 @@ void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cach
   TORCH_CHECK(D == 64 || D == 96 || D == 128, "paged_decode: head_dim 64/96/128");
   TORCH_CHECK(window >= 0, "paged_decode: window >= 0");
   TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "paged_decode: GQA group <= 16");
-  TORCH_CHECK(bs % 16 == 0, "block_size multiple of 16");
+  TORCH_CHECK(bs % 16 == 0 && (bs & (bs - 1)) == 0, "paged_decode: block_size a power of two >= 16");
   TORCH_CHECK(part_size % 128 == 0 && part_size / bs < 255);
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && context_lens.scalar_type() == at::kInt);
   TORCH_CHECK(block_tables.stride(1) == 1);
@@ -140,7 +140,7 @@ void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, con
   TORCH_CHECK(D == 64 || D == 128, "paged_decode_qkv: head_dim 64/128");
   TORCH_CHECK(window >= 0 && (mode == 0 || mode == 1));
   TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "paged_decode_qkv: GQA group <= 16");
-  TORCH_CHECK(bs % 16 == 0 && part_size % 128 == 0 && part_size / bs < 255);
+  TORCH_CHECK(bs % 16 == 0 && (bs & (bs - 1)) == 0 && part_size % 128 == 0 && part_size / bs < 255);
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && context_lens.scalar_type() == at::kInt);
   TORCH_CHECK(block_tables.stride(1) == 1);
   const int B = out.size(0);

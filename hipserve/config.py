@@ -457,6 +457,12 @@ class EngineConfig:
     port: int = 8080
     extra: dict = field(default_factory=dict)
 
+    def __post_init__(self):
+        # the attention kernels index the paged cache with shifts / masks
+        b = self.block_size
+        if b < 16 or b > 256 or b & (b - 1):
+            raise ValueError(f"block_size must be a power of two in [16, 256], got {b}")
+
     def replace(self, **kw) -> "EngineConfig":
         return dataclasses.replace(self, **kw)
 
