@@ -559,7 +559,7 @@ class ModelRunner:
                         slot_mapping=st["slots"][:b], bt_decode=st["bt"][:b], ctx_decode=st["ctx"][:b],
                         tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
         # lookahead ids: resolved inside the model's first kernel when it can
-        # (embed_rmsnorm), else by the id select below
+        # (embed_rmsnorm), else by the model's id select (LlamaModel.resolve_ids)
         meta.id_src = (st["src"][:b], st["tok"])
         hidden = self.model.forward(st["ids"][:b], meta, self.kv)
         logits = self.model.compute_logits(hidden)
