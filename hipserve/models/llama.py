@@ -440,7 +440,8 @@ class LlamaModel:
         id select + embedding gather + residual copy + first RMSNorm in one kernel
         (``embed_rmsnorm``, norm.hip). TP=1 only (the vocab-parallel embedding needs a
         cross-rank sum before the norm)."""
-        return self._fused_ok(meta) and self.tp.world_size == 1 and hasattr(torch.ops.hipserve, "embed_rmsnorm")
+        return (self._fused_ok(meta) and self.tp.world_size == 1 and self.embed.dtype == torch.bfloat16
+                and hasattr(torch.ops.hipserve, "embed_rmsnorm"))
 
     @staticmethod
     def resolve_ids(ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
