@@ -176,6 +176,10 @@ def test_tp2_shared_gpu_matches_tp1(exact):
 
 
 N_TOK_70B = 64
+# 8192-wide hidden states: the bf16 logits (and so the log-probs compared here) move in
+# steps of 1/32-1/16 nat at their magnitude, and an 8-way sharded GEMM / all-gather
+# rounds differently from TP=1, so a near-tie here is up to ~4 such steps
+TIE_70B = 0.125
 
 
 @pytest.mark.timeout(420)
@@ -192,4 +196,4 @@ def test_tp8_70b_shapes_shared_gpu_matches_tp1():
     assert len(info["ties"]) <= N_TOK_70B * 2 // 10, info["ties"]
     for i, j, t1, t2, lp1, lp2 in info["ties"]:
         assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=8 token {t2} not in TP=1's top-5"
-        assert lp1 - lp2 <= TIE, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
+        assert lp1 - lp2 <= TIE_70B, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
