@@ -418,18 +418,26 @@ def _with_preprocessor(cfg: ModelConfig, path: str) -> ModelConfig:
 
 
 def _hf_cache_dir(repo_id: str) -> str | None:
-    """Locate a snapshot of an HF Hub repo in the local cache (offline)."""
+    """Locate a snapshot of an HF Hub repo in the local cache (offline): the
+    revision ``refs/main`` names (what the Hub client resolved last), else the most
+    recently written snapshot that has a config.json."""
     if "/" not in repo_id:
         return None
     home = os.environ.get("HF_HOME", os.path.expanduser("~/.cache/huggingface"))
-    base = os.path.join(home, "hub", "models--" + repo_id.replace("/", "--"), "snapshots")
+    repo = os.path.join(home, "hub", "models--" + repo_id.replace("/", "--"))
+    base = os.path.join(repo, "snapshots")
     if not os.path.isdir(base):
         return None
-    for snap in sorted(os.listdir(base)):
-        p = os.path.join(base, snap)
-        if os.path.exists(os.path.join(p, "config.json")):
-            return p
-    return None
+    try:
+        with open(os.path.join(repo, "refs", "main")) as f:
+            ref = f.read().strip()
+    except OSError:
+        ref = ""
+    if ref and os.path.exists(os.path.join(base, ref, "config.json")):
+        return os.path.join(base, ref)
+    snaps = [os.path.join(base, s) for s in os.listdir(base)]
+    snaps = [p for p in snaps if os.path.exists(os.path.join(p, "config.json"))]
+    return max(snaps, key=lambda p: (os.path.getmtime(p), p)) if snaps else None
 
 
 @dataclass(frozen=True)

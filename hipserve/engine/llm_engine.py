@@ -31,10 +31,13 @@ def prepare_model(cfg: EngineConfig, tp: TPGroup, model_cfg: ModelConfig | None 
     needs: the Hub id is materialised into the (PVC-backed) HF cache first — rank 0
     downloads, the other TP ranks wait — and only then are the config and the
     tokenizer read from it. Collective: every TP rank calls it."""
-    from ..weights.hub import materialize
+    from ..weights.hub import DummyFallback, materialize
 
-    path = materialize(cfg.model, cfg.load_format, tp)
-    if path != cfg.model:
+    path = materialize(cfg.model, cfg.load_format, tp, cfg.served_model_name)
+    if isinstance(path, DummyFallback):  # opted-in random weights: never under the Hub id's name
+        cfg = cfg.replace(model=str(path), served_model_name=path.served_name, load_format="dummy",
+                          tokenizer=cfg.tokenizer if cfg.tokenizer and cfg.tokenizer != cfg.model else None)
+    elif path != cfg.model:
         cfg = cfg.replace(model=path, served_model_name=cfg.served_model_name or cfg.model,
                           tokenizer=cfg.tokenizer if cfg.tokenizer and cfg.tokenizer != cfg.model else None)
     mcfg = model_cfg or resolve_model_config(cfg.model, cfg.served_model_name)
@@ -144,6 +147,8 @@ class LLMEngine:
         for s in so.preempted:
             if s.status == Status.FINISHED:
                 outputs.append(self._finish_output(s))
+            else:  # recompute rebuilds the penalty slot from its ids (pen_init)
+                self.runner.release(s)
         if so.empty:
             return outputs
         t0 = time.monotonic()

@@ -160,9 +160,12 @@ class ModelRunner:
         self.prefill_pad = None
         if (self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0):
             self.prefill_pad = self._probe_prefill_pad()
-        # device penalty state: one slot per concurrently running penalised sequence
+        # device penalty state: one slot per concurrently running sequence (a slot is
+        # held from the first sample to finish / abort / preemption), so a slot is
+        # always free for a running sequence: max_num_seqs x V x ~4.1 B (512 slots of a
+        # 128K vocabulary: 270 MB of 288 GB)
         V = mcfg.vocab_size
-        nslots = max(1, min(ecfg.max_num_seqs, int(ecfg.extra.get("penalty_slots", 256))))
+        nslots = max(1, ecfg.max_num_seqs)
         self.pen_counts = torch.zeros(nslots, V, dtype=torch.int32, device=self.device)
         self.pen_seen = torch.zeros(nslots, (V + 31) // 32, dtype=torch.int32, device=self.device)
         self._free_pen = list(range(nslots - 1, -1, -1))

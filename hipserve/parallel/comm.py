@@ -247,12 +247,14 @@ def init_tp(world_size: int | None = None, backend: str | None = None, device_ty
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    # bound on any one collective; nothing slow (the first weight download) waits
+    # on a collective: weights/hub.py polls a status file instead
+    timeout = datetime.timedelta(seconds=float(os.environ.get("HIPSERVE_DIST_TIMEOUT_S", 600)))
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend, rank=rank, world_size=ws,
-                                timeout=datetime.timedelta(seconds=600))
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws, timeout=timeout)
     g = TPGroup(rank, ws, dist.group.WORLD, dev)
-    g._cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
+    g._cpu_group = dist.new_group(backend="gloo", timeout=timeout) if backend != "gloo" else dist.group.WORLD
     g.setup_shm_ring()
     # the custom collectives are created by the ModelRunner once the message sizes
     # (hidden size x token budget, logits shard) are known: ensure_custom_ar()

@@ -11,7 +11,6 @@ network is reachable.
 """
 from __future__ import annotations
 
-import glob
 import json
 import os
 
@@ -25,14 +24,13 @@ def resolve_checkpoint_dir(model: str) -> str:
         return model
     from ..config import _hf_cache_dir
 
-    d = _hf_cache_dir(model)
-    if d and glob.glob(os.path.join(d, "*.safetensors")):
-        return d
-    try:  # first start of a pod: populate the PVC-backed HF cache
-        from huggingface_hub import snapshot_download
+    from .hub import download, snapshot_problem
 
-        return snapshot_download(model, allow_patterns=["*.json", "*.safetensors", "tokenizer*"],
-                                 token=os.environ.get("HUGGING_FACE_HUB_TOKEN"))
+    d = _hf_cache_dir(model)
+    if snapshot_problem(d, True) is None:
+        return d
+    try:  # normally materialised by prepare_model already; resumes a partial snapshot
+        return download(model, True)
     except Exception as e:  # pragma: no cover - no network in CI
         raise FileNotFoundError(f"checkpoint {model!r} not found locally and download failed: {e}")
 
@@ -41,9 +39,14 @@ class _Ckpt:
     def __init__(self, path: str):
         from safetensors import safe_open
 
-        files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+        from .hub import weight_files
+
+        files = weight_files(path)  # the index's shard list when there is one
         if not files:
             raise FileNotFoundError(f"no *.safetensors in {path}")
+        missing = [os.path.basename(f) for f in files if not os.path.exists(f)]
+        if missing:
+            raise FileNotFoundError(f"{path}: shards listed in the index are missing: {', '.join(missing)}")
         self.handles = [safe_open(f, framework="pt") for f in files]
         self.where = {}
         for h in self.handles:

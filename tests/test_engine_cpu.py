@@ -162,6 +162,19 @@ def test_penalties_and_logprobs():
     assert len(set(toks)) >= 6
 
 
+def test_penalty_slots_cover_every_running_sequence():
+    """more penalised requests than the old 256-slot pool, plus
+    preemptions (a KV pool too small for all of them at once): every step finds a
+    free penalty slot, preempted sequences give theirs back, nothing raises."""
+    eng = make_engine(max_num_seqs=300, max_num_batched_tokens=2048, num_kv_blocks=330, max_model_len=64)
+    sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True, frequency_penalty=0.5,
+                        repetition_penalty=1.2)
+    out = eng.generate([[1 + i % 50, 2, 3, 4 + i % 7] for i in range(300)], sp)
+    assert all(len(r[0]) == 24 for r in out)
+    assert eng.scheduler.num_preemptions > 0
+    assert len(eng.runner._free_pen) == eng.runner.pen_counts.shape[0]  # all returned
+
+
 def test_prefill_pad_table():
     """Ragged-chunk padding table (model_runner.pad_table): each 256-row count maps to
     the fastest count at or above it, a larger one only when >3 % faster."""

@@ -78,11 +78,81 @@ def test_dummy_load_format_fetches_config_only(hub):
 
 
 def test_offline_fallbacks(hub, monkeypatch):
+    """a failed download of a real model is fatal — no silent
+    random weights under the Hub id. The preset fallback is opt-in (dummy load
+    format or HIPSERVE_HUB_DUMMY_FALLBACK=1) and never serves under the Hub id."""
     monkeypatch.setenv("FAKE_HUB_REPOS", "{}")  # every download fails (air-gapped box)
-    eng = _engine("acme/tiny-llama")  # maps to the tiny-llama preset: random weights, loudly
-    assert eng.runner.load_format == "dummy"
+    with pytest.raises(FileNotFoundError, match="HIPSERVE_HUB_DUMMY_FALLBACK"):
+        _engine("acme/tiny-llama")  # maps to the tiny-llama preset, but no opt-in
     with pytest.raises(FileNotFoundError):
         _engine("acme/not-a-preset")
+    eng = _engine("acme/tiny-llama", load_format="dummy")
+    assert eng.runner.load_format == "dummy" and eng.cfg.model_name == "tiny-llama-random"
+    monkeypatch.setenv("HIPSERVE_HUB_DUMMY_FALLBACK", "1")
+    eng = _engine("acme/tiny-llama", served_model_name="chat")
+    assert eng.runner.load_format == "dummy" and eng.cfg.model_name == "chat"
+    with pytest.raises(FileNotFoundError):
+        _engine("acme/not-a-preset")
+
+
+def test_interrupted_download_resumes(hub, monkeypatch):
+    """a pod killed mid-download leaves a partial snapshot (config +
+    index + some shards). The restart must see it as incomplete, resume the
+    download and serve — not crash-loop on the missing shard."""
+    from hipserve.weights.hub import cached_snapshot, snapshot_problem
+
+    monkeypatch.setenv("FAKE_HUB_SHARDS", "3")
+    monkeypatch.setenv("FAKE_HUB_INTERRUPT", "1")
+    with pytest.raises(FileNotFoundError, match="connection reset"):
+        _engine("acme/tiny-chat")
+    from hipserve.config import _hf_cache_dir
+
+    snap = _hf_cache_dir("acme/tiny-chat")
+    assert snap and "missing shard" in snapshot_problem(snap, True)
+    assert cached_snapshot("acme/tiny-chat", True) is None
+    monkeypatch.delenv("FAKE_HUB_INTERRUPT")
+    eng = _engine("acme/tiny-chat")  # restart: resumes, then serves
+    assert len(hub.read_text().splitlines()) == 2
+    assert snapshot_problem(snap, True) is None
+    got = [r[0] for r in eng.generate(PROMPTS, SP)]
+    want = [r[0] for r in _engine(snap, served_model_name="x").generate(PROMPTS, SP)]
+    assert got == want
+    _engine("acme/tiny-chat")  # complete now: no third download
+    assert len(hub.read_text().splitlines()) == 2
+
+
+def test_truncated_shard_is_redownloaded(hub, monkeypatch):
+    from hipserve.config import _hf_cache_dir
+    from hipserve.weights.hub import snapshot_problem
+
+    monkeypatch.setenv("FAKE_HUB_SHARDS", "2")
+    _engine("acme/tiny-chat")
+    snap = _hf_cache_dir("acme/tiny-chat")
+    shard = os.path.join(snap, "model-00002-of-00002.safetensors")
+    with open(shard, "r+b") as f:
+        f.truncate(os.path.getsize(shard) - 100)
+    assert "truncated" in snapshot_problem(snap, True)
+    os.remove(shard)  # the real client's resume re-fetches what is not complete
+    _engine("acme/tiny-chat")
+    assert len(hub.read_text().splitlines()) == 2 and snapshot_problem(snap, True) is None
+
+
+def test_snapshot_follows_refs_main(tmp_path, monkeypatch):
+    from hipserve.config import _hf_cache_dir
+
+    monkeypatch.setenv("HF_HOME", str(tmp_path))
+    repo = tmp_path / "hub" / "models--acme--x"
+    for rev in ("aaaa", "ffff"):
+        (repo / "snapshots" / rev).mkdir(parents=True)
+        (repo / "snapshots" / rev / "config.json").write_text("{}")
+    (repo / "refs").mkdir()
+    (repo / "refs" / "main").write_text("ffff\n")
+    assert _hf_cache_dir("acme/x").endswith("ffff")
+    (repo / "refs" / "main").write_text("aaaa")
+    assert _hf_cache_dir("acme/x").endswith("aaaa")
+    (repo / "refs" / "main").write_text("gone")  # dangling ref: newest snapshot
+    os.utime(repo / "snapshots" / "aaaa", (1, 1))
+    assert _hf_cache_dir("acme/x").endswith("ffff")
 
 
 def _port():
@@ -121,8 +191,18 @@ def _rank(rank, world, port, env, q):
     os._exit(0)
 
 
-def test_first_start_tp2_downloads_once(hub):
-    env = {k: os.environ[k] for k in ("HF_HOME", "FAKE_HUB_REPOS", "FAKE_HUB_LOG", "HIPSERVE_SNAPSHOT_DOWNLOAD")}
+@pytest.mark.parametrize("slow", [False, True])
+def test_first_start_tp2_downloads_once(hub, monkeypatch, slow):
+    """slow: the download outlasts the process groups' collective timeout (8 s
+    here; a 140 GB 70B first download vs the 600 s default) — the non-zero rank
+    polls rank 0's status file instead of sitting in one bounded barrier."""
+    if slow:
+        monkeypatch.setenv("HIPSERVE_DIST_TIMEOUT_S", "8")
+        monkeypatch.setenv("FAKE_HUB_DELAY", "14")
+        monkeypatch.setenv("FAKE_HUB_SHARDS", "2")
+    keys = ("HF_HOME", "FAKE_HUB_REPOS", "FAKE_HUB_LOG", "HIPSERVE_SNAPSHOT_DOWNLOAD", "HIPSERVE_DIST_TIMEOUT_S",
+            "FAKE_HUB_DELAY", "FAKE_HUB_SHARDS")
+    env = {k: os.environ[k] for k in keys if k in os.environ}
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -134,5 +214,7 @@ def test_first_start_tp2_downloads_once(hub):
         p.join(60)
         assert p.exitcode == 0
     assert len(hub.read_text().splitlines()) == 1  # rank 0 downloaded, rank 1 waited
+    monkeypatch.delenv("FAKE_HUB_DELAY", raising=False)
     want = [r[0] for r in _engine("acme/tiny-chat").generate(PROMPTS, SP)]
     assert got == want
+    assert len(hub.read_text().splitlines()) == 1  # the cache was complete: no second download
