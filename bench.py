@@ -16,6 +16,16 @@ OpenAI server with SSE streaming.
 Rank 0 prints ONE JSON line; value = total output tokens/s over all ranks
 (time = max over ranks of the K timed waves, barrier + device sync on both sides).
 
+Second phase, ``tp_strong`` (BASELINE.json's "Llama-3-70B TP=8 over xGMI" config,
+VERDICT r2 next-round item 1): after the headline waves the SAME N ranks serve ONE
+Llama-3-70B sharded TP=N (RCCL process group + the in-house IPC collectives), time
+boxed (``--tp-budget-s``, 150 s); its tok/s, p50 TTFT and ms/step go under the
+``tp_strong`` key of the same JSON line, with the observed process-group backend /
+world size and whether the custom all-reduce was active. The driver's 1/2/4/8-GPU
+runs therefore also measure the 70B strong-scaling curve. Each phase runs in a
+child process per rank (the rank process itself never touches the GPU), so the 8B
+engine's HBM (weights + a 0.9-of-HBM KV pool) is returned before the 70B loads.
+
 ``--tp T`` (T = the torchrun world size) instead serves ONE model sharded over the
 T ranks — BASELINE.json's "Llama-3-70B TP=8 over xGMI" config:
 ``torchrun --nproc-per-node 8 bench.py --model llama-3-70b --tp 8``. Rank 0 runs
@@ -58,6 +68,15 @@ def parse():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: fp32 on the host with gloo collectives (tests of the DP / TP paths)")
     ap.add_argument("--num-kv-blocks", type=int, default=None, help="KV pool size (default: from HBM)")
+    ap.add_argument("--tp-phase", choices=["auto", "on", "off"], default="auto",
+                    help="second phase: one --tp-model sharded over all N ranks (auto: on for the default "
+                         "GPU headline run)")
+    ap.add_argument("--tp-model", default="llama-3-70b")
+    ap.add_argument("--tp-steps", type=int, default=2)
+    ap.add_argument("--tp-warmup", type=int, default=1)
+    ap.add_argument("--tp-budget-s", type=float, default=150.0)
+    ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)  # child -> parent
+    ap.add_argument("--deadline", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--request-rate", type=float, default=None,
                     help="gateway path: open-loop Poisson arrivals at this rate (req/s) for the timed "
                          "region (steps x concurrency requests) instead of closed-loop waves")
@@ -80,6 +99,123 @@ def _self_launch(args) -> int:
     return subprocess.call(cmd)
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run_child(argv, world, rank, local, port, result_file, timeout=None):
+    """One phase as a child process of this rank (own process group on ``port``);
+    returns (exit code, result dict or None). ``timeout``: kill the child's
+    whole process group at that many seconds (exit code 124)."""
+    import signal
+    import subprocess
+
+    env = dict(os.environ, HIPSERVE_BENCH_CHILD="1", WORLD_SIZE=str(world), RANK=str(rank),
+               LOCAL_RANK=str(local), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for k in [k for k in env if k.startswith("TORCHELASTIC_")]:
+        env.pop(k)  # the child's process group owns its own store (no torchrun agent store)
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--result-file", result_file]
+    # the child's stdout goes to our stderr: the ONE JSON line on stdout is ours
+    p = subprocess.Popen(cmd, env=env, stdout=sys.stderr, start_new_session=True)
+    try:
+        rc = p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.wait()
+        rc = 124
+    res = None
+    if rank == 0 and os.path.exists(result_file):
+        with open(result_file) as f:
+            res = json.load(f)
+        os.remove(result_file)
+    return rc, res
+
+
+def _strip(argv, names):
+    """argv without the given ``--flag value`` / ``--flag=value`` options."""
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a in names:
+            skip = True
+            continue
+        if any(a.startswith(n + "=") for n in names):
+            continue
+        out.append(a)
+    return out
+
+
+def orchestrate(args) -> int:
+    """Per-rank parent: phase 1 (the headline) and the optional TP phase, each as a
+    child process; rank 0 prints the merged JSON line. Never touches the GPU."""
+    import tempfile
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    tp_phase = args.tp_phase == "on" or (
+        args.tp_phase == "auto" and args.device == "cuda" and args.tp == 1 and args.model == "llama-3-8b"
+        and not args.quantization and not args.request_rate)
+    dist = None
+    ports = [_free_port(), _free_port()]
+    if world > 1:
+        import datetime
+
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=3600))
+        lst = [ports]
+        dist.broadcast_object_list(lst, src=0)
+        ports = lst[0]
+    tmp = tempfile.mkdtemp(prefix="hipserve_bench_")
+    argv = sys.argv[1:]
+    rc1, res = _run_child(argv, world, rank, local, ports[0], os.path.join(tmp, "phase1.json"))
+    if dist is not None:
+        ok = [rc1 == 0] * world
+        dist.all_gather_object(ok, rc1 == 0)
+        rc1 = 0 if all(ok) else (rc1 or 1)
+    if rc1 == 0 and tp_phase:
+        t0 = time.time()
+        argv2 = _strip(argv, {"--model", "--tp", "--steps", "--warmup", "--out", "--quantization",
+                              "--request-rate", "--tp-phase", "--num-kv-blocks"})
+        argv2 += ["--model", args.tp_model, "--tp", str(world), "--steps", str(args.tp_steps),
+                  "--warmup", str(args.tp_warmup), "--tp-phase", "off",
+                  "--deadline", str(t0 + args.tp_budget_s - 15)]
+        if args.num_kv_blocks and args.device == "cpu":
+            argv2 += ["--num-kv-blocks", str(args.num_kv_blocks)]
+        rc2, tp = _run_child(argv2, world, rank, local, ports[1], os.path.join(tmp, "phase2.json"),
+                             timeout=args.tp_budget_s)
+        if dist is not None:
+            dist.barrier()
+        if rank == 0:
+            if rc2 != 0 or tp is None:
+                tp = {"model": args.tp_model, "tp": world,
+                      "status": "timeout" if rc2 == 124 else f"failed (exit {rc2})"}
+            tp["phase_wall_s"] = round(time.time() - t0, 1)
+            res = dict(res or {}, tp_strong=tp)
+    if rank == 0 and res is not None:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+    return rc1
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -88,6 +224,13 @@ def main():
     if args.gpus != int(world_env or "1"):
         raise SystemExit(f"--gpus {args.gpus} does not match the launched world size {world_env or 1}: "
                          "run one rank per GPU (torch.distributed.run --nproc-per-node N bench.py --gpus N)")
+    if not os.environ.get("HIPSERVE_BENCH_CHILD"):
+        sys.exit(orchestrate(args))
+    run_phase(args)
+
+
+def run_phase(args):
+    """One benchmark phase on this rank (a child process of ``orchestrate``)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -189,8 +332,13 @@ def main():
                     ntok += len(o.new_token_ids)
             return ntok, [s.first_token_time - s.arrival_time for s in seqs]
 
+    steps = args.steps
+    t_w = time.perf_counter()
     for _ in range(args.warmup):
         wave()
+    if args.deadline and args.warmup:  # time-boxed phase: as many timed waves as fit (>= 1)
+        per = (time.perf_counter() - t_w) / args.warmup
+        steps = max(1, min(steps, int((args.deadline - time.time()) / max(per, 1e-3))))
     barrier()
     t0 = time.perf_counter()
     tok_total, ttfts = 0, []
@@ -201,7 +349,7 @@ def main():
                               top_p=args.top_p)
         tok_total, ttfts = sum(r["tokens"] for r in res), [r["ttft"] for r in res]
     else:
-        for _ in range(args.steps):
+        for _ in range(steps):
             n, tt = wave()
             tok_total += n
             ttfts += tt
@@ -227,9 +375,9 @@ def main():
         "value": round(value, 2),
         "unit": "tokens/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "ms_per_step": round(1000 * elapsed / steps, 3),
         "higher_is_better": True,
         "scaling": "strong" if tp_mode else "weak",
         "vs_baseline": None,
@@ -257,6 +405,17 @@ def main():
         "engine_init_s": round(init_s, 1),
         "kv_blocks": engine.runner.num_blocks,
     }
+    if tp_mode or args.deadline:
+        out["tp_info"] = ({"pg_backend": tpg.backend, "pg_world_size": dist.get_world_size(),
+                           "rccl": tpg.backend == "nccl", "custom_allreduce": tpg.custom_ar is not None}
+                          if tp_mode else {"pg_backend": None, "pg_world_size": 1, "rccl": False,
+                                           "custom_allreduce": False})
+        if args.deadline:  # the tp_strong record of orchestrate()
+            out = {"model": args.model, "tp": args.tp, "status": "ok", "tok_s": out["value"],
+                   "p50_ttft_ms": out["p50_ttft_ms"], "ms_per_step": out["ms_per_step"], "steps": steps,
+                   "warmup": args.warmup, "global_batch": args.concurrency,
+                   "input_len": args.input_len, "output_len": args.output_len,
+                   "engine_init_s": out["engine_init_s"], **out["tp_info"]}
     if lg is not None:
         lg.close()
         stack.stop()
@@ -264,7 +423,11 @@ def main():
         engine.shutdown()  # releases the workers from worker_loop
     if rank == 0:
         line = json.dumps(out)
-        print(line, flush=True)
+        if args.result_file:
+            with open(args.result_file, "w") as f:
+                f.write(line + "\n")
+        else:
+            print(line, flush=True)
         if args.out:
             with open(args.out, "w") as f:
                 f.write(line + "\n")

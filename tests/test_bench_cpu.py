@@ -80,6 +80,31 @@ def test_bench_tp8_world8():
     assert out["value"] > 0 and out["p50_ttft_ms"] > 0
 
 
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_tp_strong_phase(n):
+    """the driver's N-rank headline run (DP replicas)
+    ALSO serves one model sharded TP=N over the same ranks (the 70B TP=8 config's
+    strong-scaling point) and reports it under ``tp_strong`` in the SAME JSON
+    line, with the observed process-group backend / world size and the custom
+    all-reduce state. Here: gloo, CPU-sized model with 8 kv heads."""
+    out = _run(_torchrun(n, 29670 + n, ARGS + ["--tp-phase", "on", "--tp-model", "tiny-llama-tp8"]))
+    assert out["n_gpus"] == n and out["config"]["parallelism"] == f"dp{n}" and out["scaling"] == "weak"
+    tp = out["tp_strong"]
+    assert tp["status"] == "ok" and tp["model"] == "tiny-llama-tp8" and tp["tp"] == n
+    assert tp["pg_world_size"] == n and tp["pg_backend"] == "gloo" and tp["rccl"] is False
+    assert tp["custom_allreduce"] is False  # CPU: no IPC collectives
+    assert tp["tok_s"] > 0 and tp["p50_ttft_ms"] > 0 and tp["steps"] >= 1
+    assert abs(tp["tok_s"] - tp["steps"] * 2 * 4 / (tp["ms_per_step"] * tp["steps"] / 1000)) / tp["tok_s"] < 0.02
+
+
+def test_bench_tp_phase_time_box():
+    """A TP phase that cannot finish in its budget is killed and reported, and the
+    headline line is still printed (exit 0)."""
+    out = _run([sys.executable, "bench.py"] + ARGS + ["--tp-phase", "on", "--tp-model", "tiny-llama-tp8",
+                                                       "--tp-budget-s", "0.5"])
+    assert out["value"] > 0 and out["tp_strong"]["status"] == "timeout"
+
+
 def test_bench_gpus_flag_must_match_world():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS, cwd=ROOT, env=env,
