@@ -407,7 +407,8 @@ def run_phase(args):
     }
     if tp_mode or args.deadline:
         out["tp_info"] = ({"pg_backend": tpg.backend, "pg_world_size": dist.get_world_size(),
-                           "rccl": tpg.backend == "nccl", "custom_allreduce": tpg.custom_ar is not None}
+                           "rccl": tpg.backend == "nccl", "custom_allreduce": tpg.custom_ar is not None,
+                           "rccl_min_rows": tpg.rccl_min_rows, "collective_calibration": tpg.collective_report}
                           if tp_mode else {"pg_backend": None, "pg_world_size": 1, "rccl": False,
                                            "custom_allreduce": False})
         if args.deadline:  # the tp_strong record of orchestrate()

@@ -17,6 +17,15 @@
 //            fp32 rounding of TP=1 (the partials are never rounded to bf16 before
 //            the cross-rank sum); bf16 exchange halves the bytes (prefill chunks).
 //
+// Two grid classes per collective: decode-sized messages run on a 64-block grid
+// (few blocks = few barrier pairs = lowest latency); prefill-sized ones (an 8K-token
+// chunk of a 70B layer is a 128 MiB bf16 [8192, 8192] exchange) on a 512-block grid
+// so every CU streams (the fixed 64-block car_norm was 754 us per 64 MiB
+// call, as long as the GEMMs). Each class is an independent instance of the
+// protocol below (own regions, flags and counters), so grids never mix.
+// Whether a prefill-sized message goes through these kernels at all or through
+// RCCL is decided per node by a start-up calibration (parallel/comm.py).
+//
 // Buffers: every rank owns ONE uncached (fine-grained) allocation holding, per
 // collective kind, two data regions used alternately by call parity, plus a flag
 // area; peers map it with HIP IPC. Inputs are staged into the rank's own region,
@@ -55,16 +64,21 @@
 namespace hipserve {
 
 constexpr int CAR_MAX_RANKS = 8;
-constexpr int CAR_NB = 64;        // grid of every comm kernel (fixed: per-block epochs stay in lockstep)
+constexpr int CAR_NB_S = 64;      // decode-sized class grid (fixed per class: per-block epochs stay in lockstep)
+constexpr int CAR_NB_L = 512;     // prefill-sized class grid: 2 blocks per CU
+constexpr int CAR_NB_MAX = CAR_NB_L;
 constexpr int CAR_T = 256;        // threads per block
 constexpr int CAR_GRAN = CAR_T;   // 16-B vectors per block per grid-stride step
 constexpr long CAR_MAX_ROWS = 65536;
-enum { K_AR = 0, K_AG = 1, K_NORM = 2, K_NUM = 3 };
+constexpr long CAR_S_ROWS = 512;                // norm rows of the small class (decode batches)
+constexpr size_t CAR_S_BYTES = 8u << 20;        // message bytes of the small class
+// kinds: all-reduce small / large, all-gather, fused add+RMSNorm small / large
+enum { K_AR_S = 0, K_AR_L = 1, K_AG = 2, K_NORM_S = 3, K_NORM_L = 4, K_NUM = 5 };
 
 struct CarFlags {
-  unsigned int flag[K_NUM][2][CAR_MAX_RANKS][CAR_NB];  // [kind][phase][src rank][block], stored by peers
-  unsigned int counter[K_NUM][CAR_NB];                 // own per-block call counters
-  unsigned int error;                                  // sticky: some rank timed out
+  unsigned int flag[K_NUM][2][CAR_MAX_RANKS][CAR_NB_MAX];  // [kind][phase][src rank][block], stored by peers
+  unsigned int counter[K_NUM][CAR_NB_MAX];                 // own per-block call counters
+  unsigned int error;                                      // sticky: some rank timed out
 };
 
 struct CarPeers {
@@ -165,12 +179,14 @@ HS_DEVICE u16x8 sum_bf16x8(const u16x8 (&v)[W], int n) {
 // ------------------------------------------------------------------ all-reduce
 // nvec = 16-byte vectors in the tensor. Rank order of the sum is fixed, so every
 // rank produces identical bits.
-template <bool TWO_SHOT>
-__global__ __launch_bounds__(CAR_T) void car_ar_kernel(CarPeers P, int rank, int world, const u16x8* __restrict__ inp,
-                                                       u16x8* __restrict__ out, long nvec) {
+template <int NB, bool TWO_SHOT>
+__global__ __launch_bounds__(CAR_T) void car_ar_kernel(CarPeers P, int kind, int rank, int world,
+                                                       const u16x8* __restrict__ inp, u16x8* __restrict__ out,
+                                                       long nvec) {
   __shared__ unsigned int s_epoch;
   __shared__ int s_ok;
   const int blk = blockIdx.x, t = threadIdx.x;
+  const int K_AR = kind;
   const unsigned int epoch = car_epoch(P, rank, K_AR, blk, &s_epoch);
   if ((long)blk * CAR_GRAN >= nvec) {  // nothing of this size maps to this block (same on every rank)
     car_finish(P, rank, K_AR, blk, epoch);
@@ -181,7 +197,7 @@ __global__ __launch_bounds__(CAR_T) void car_ar_kernel(CarPeers P, int rank, int
 #pragma unroll
   for (int p = 0; p < CAR_MAX_RANKS; ++p)
     src[p] = reinterpret_cast<const u16x8*>(car_region(P, p < world ? p : rank, K_AR, epoch));
-  const long step = (long)CAR_NB * CAR_GRAN;
+  const long step = (long)NB * CAR_GRAN;
   for (long i = (long)blk * CAR_GRAN + t; i < nvec; i += step) mine[i] = inp[i];
   if (!car_barrier(P, rank, world, K_AR, 0, blk, epoch, &s_ok)) {
     car_finish(P, rank, K_AR, blk, epoch);
@@ -231,7 +247,7 @@ __global__ __launch_bounds__(CAR_T) void car_ag_kernel(CarPeers P, int rank, int
     return;
   }
   V* mine = reinterpret_cast<V*>(car_region(P, rank, K_AG, epoch));
-  const long step = (long)CAR_NB * CAR_GRAN;
+  const long step = (long)CAR_NB_S * CAR_GRAN;
   for (long j = (long)blk * CAR_GRAN + t; j < nv; j += step) mine[j] = inp[j];
   if (car_barrier(P, rank, world, K_AG, 0, blk, epoch, &s_ok)) {
     const long orow = (long)world * row_v;
@@ -252,15 +268,22 @@ __global__ __launch_bounds__(CAR_T) void car_ag_kernel(CarPeers P, int rank, int
 // ------------------------------------------------------------------ fused norm
 // x: kIn == 0 -> fp32 split-K partials [S, M, N] (slice = M*N), kIn == 1 -> bf16 [M, N].
 // Region of one parity: [A: M*N exchange values][B: M*N/world bf16 residual chunks][C: M fp32 sum of squares]
-template <int kIn, bool kExF32, bool kWF32>
-__global__ __launch_bounds__(CAR_T) void car_norm_kernel(CarPeers P, int rank, int world, const void* __restrict__ x,
-                                                         int S, unsigned short* __restrict__ residual,
+// Rows are dealt to blocks round-robin (row m -> block m % NB). Phase B (the
+// reduce-scatter of one rank's column chunk, cv 16-B vectors wide) gives each row
+// TPR = 64..256 threads so a 70B TP=8 chunk (cv = 128) keeps every lane busy with
+// two rows per pass; a row's sum of squares is reduced wave by wave, in wave order
+// (deterministic).
+template <int NB, int kIn, bool kExF32, bool kWF32>
+__global__ __launch_bounds__(CAR_T) void car_norm_kernel(CarPeers P, int kind, int rank, int world,
+                                                         const void* __restrict__ x, int S,
+                                                         unsigned short* __restrict__ residual,
                                                          const void* __restrict__ weight,
                                                          unsigned short* __restrict__ out, int M, int N, float eps) {
   __shared__ unsigned int s_epoch;
   __shared__ int s_ok;
-  __shared__ float scratch[16];
-  const int blk = blockIdx.x, t = threadIdx.x;
+  __shared__ float scratch[CAR_T / 64];
+  const int blk = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int K_NORM = kind;
   const unsigned int epoch = car_epoch(P, rank, K_NORM, blk, &s_epoch);
   if (blk >= M) {  // no row maps to this block
     car_finish(P, rank, K_NORM, blk, epoch);
@@ -276,7 +299,7 @@ __global__ __launch_bounds__(CAR_T) void car_norm_kernel(CarPeers P, int rank, i
   auto regC = [&](int p) { return reinterpret_cast<float*>(car_region(P, p, K_NORM, epoch) + aBytes + bBytes); };
 
   // A. local sum of this rank's partials -> own exchange region (all columns)
-  for (int m = blk; m < M; m += CAR_NB) {
+  for (int m = blk; m < M; m += NB) {
     for (int v = t; v < nv; v += CAR_T) {
       float h[8];
       if constexpr (kIn == 0) {
@@ -311,63 +334,77 @@ __global__ __launch_bounds__(CAR_T) void car_norm_kernel(CarPeers P, int rank, i
   // B. reduce-scatter by columns: this rank's chunk of every row of the block,
   //    rank-ordered sum, bf16 round (= the unfused GEMM output), residual add
   const int v0 = rank * cv;
-  for (int m = blk; m < M; m += CAR_NB) {
+  const int tpr = cv > 128 ? 256 : (cv > 64 ? 128 : 64);  // threads per row (whole waves)
+  const int rpp = CAR_T / tpr, sub = t / tpr, lt = t - sub * tpr, wpr = tpr / 64;
+  const int nrows = (M - blk + NB - 1) / NB;               // rows of this block
+  for (int i0 = 0; i0 < nrows; i0 += rpp) {
+    const int i = i0 + sub;
+    const int m = blk + i * NB;
     float ss = 0.f;
-    for (int v = v0 + t; v < v0 + cv; v += CAR_T) {
-      float acc[8];
-      if constexpr (kExF32) {
-        f32x4 lo[CAR_MAX_RANKS], hi[CAR_MAX_RANKS];
+    if (i < nrows) {
+      for (int v = v0 + lt; v < v0 + cv; v += tpr) {
+        float acc[8];
+        if constexpr (kExF32) {
+          f32x4 lo[CAR_MAX_RANKS], hi[CAR_MAX_RANKS];
 #pragma unroll
-        for (int p = 0; p < CAR_MAX_RANKS; ++p)
-          if (p < world) {
-            const f32x4* s = reinterpret_cast<const f32x4*>(regA(p) + ((long)m * N + v * 8) * 4);
-            lo[p] = s[0];
-            hi[p] = s[1];
+          for (int p = 0; p < CAR_MAX_RANKS; ++p)
+            if (p < world) {
+              const f32x4* s = reinterpret_cast<const f32x4*>(regA(p) + ((long)m * N + v * 8) * 4);
+              lo[p] = s[0];
+              hi[p] = s[1];
+            }
+          f32x4 a = lo[0], b = hi[0];
+#pragma unroll
+          for (int p = 1; p < CAR_MAX_RANKS; ++p)
+            if (p < world) {
+              a += lo[p];
+              b += hi[p];
+            }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] = a[j];
+            acc[j + 4] = b[j];
           }
-        f32x4 a = lo[0], b = hi[0];
+        } else {
+          u16x8 s[CAR_MAX_RANKS];
 #pragma unroll
-        for (int p = 1; p < CAR_MAX_RANKS; ++p)
-          if (p < world) {
-            a += lo[p];
-            b += hi[p];
-          }
+          for (int p = 0; p < CAR_MAX_RANKS; ++p)
+            if (p < world) s[p] = reinterpret_cast<const u16x8*>(regA(p))[(long)m * nv + v];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[j] = a[j];
-          acc[j + 4] = b[j];
+          for (int j = 0; j < 8; ++j) acc[j] = bf16_to_f32(s[0][j]);
+#pragma unroll
+          for (int p = 1; p < CAR_MAX_RANKS; ++p)
+            if (p < world)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[j] += bf16_to_f32(s[p][j]);
         }
-      } else {
-        u16x8 s[CAR_MAX_RANKS];
+        const u16x8 res = reinterpret_cast<const u16x8*>(residual + (long)m * N)[v];
+        u16x8 r;
 #pragma unroll
-        for (int p = 0; p < CAR_MAX_RANKS; ++p)
-          if (p < world) s[p] = reinterpret_cast<const u16x8*>(regA(p))[(long)m * nv + v];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = bf16_to_f32(s[0][j]);
-#pragma unroll
-        for (int p = 1; p < CAR_MAX_RANKS; ++p)
-          if (p < world)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[j] += bf16_to_f32(s[p][j]);
+        for (int j = 0; j < 8; ++j) {
+          r[j] = f32_to_bf16(bf16_to_f32(f32_to_bf16(acc[j])) + bf16_to_f32(res[j]));
+          const float f = bf16_to_f32(r[j]);
+          ss += f * f;
+        }
+        reinterpret_cast<u16x8*>(regB(rank))[(long)m * cv + (v - v0)] = r;
       }
-      const u16x8 res = reinterpret_cast<const u16x8*>(residual + (long)m * N)[v];
-      u16x8 r;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        r[j] = f32_to_bf16(bf16_to_f32(f32_to_bf16(acc[j])) + bf16_to_f32(res[j]));
-        const float f = bf16_to_f32(r[j]);
-        ss += f * f;
-      }
-      reinterpret_cast<u16x8*>(regB(rank))[(long)m * cv + (v - v0)] = r;
     }
-    ss = block_sum(ss, scratch);
-    if (t == 0) regC(rank)[m] = ss;
+    ss = wave_sum(ss);
+    if (lane == 0) scratch[wave] = ss;
+    __syncthreads();
+    if (i < nrows && lt == 0) {
+      float tot = 0.f;
+      for (int w = sub * wpr; w < (sub + 1) * wpr; ++w) tot += scratch[w];
+      regC(rank)[m] = tot;
+    }
+    __syncthreads();
   }
   if (!car_barrier(P, rank, world, K_NORM, 1, blk, epoch, &s_ok)) {
     car_finish(P, rank, K_NORM, blk, epoch);
     return;
   }
   // C. all-gather the residual chunks, total sum of squares (rank order), RMSNorm
-  for (int m = blk; m < M; m += CAR_NB) {
+  for (int m = blk; m < M; m += NB) {
     float ssum = 0.f;
     for (int p = 0; p < world; ++p) ssum += regC(p)[m];
     const float inv = rsqrtf(ssum / N + eps);
@@ -411,10 +448,14 @@ void* car_create(int rank, int world, size_t max_bytes) {
   st->max_bytes = align_up(max_bytes, 256);
   const size_t B = st->max_bytes;
   // per-parity region of each kind: AR = message; AG = one shard; NORM = fp32
-  // exchange (2B) + bf16 residual chunks (B) + per-row sums of squares
-  st->peers.bytes[K_AR] = B;
+  // exchange (2B) + bf16 residual chunks (B) + per-row sums of squares. The small
+  // class holds decode-sized messages only (SB = min(B, 8 MiB)).
+  const size_t SB = B < CAR_S_BYTES ? B : CAR_S_BYTES;
+  st->peers.bytes[K_AR_S] = SB;
+  st->peers.bytes[K_AR_L] = B;
   st->peers.bytes[K_AG] = B;
-  st->peers.bytes[K_NORM] = 3 * B + align_up(CAR_MAX_ROWS * sizeof(float), 256);
+  st->peers.bytes[K_NORM_S] = 3 * SB + align_up(CAR_S_ROWS * sizeof(float), 256);
+  st->peers.bytes[K_NORM_L] = 3 * B + align_up(CAR_MAX_ROWS * sizeof(float), 256);
   size_t off = 0;
   for (int k = 0; k < K_NUM; ++k) {
     st->peers.off[k] = off;
@@ -486,12 +527,14 @@ void launch_car(void* state, const void* inp, void* out, size_t bytes, bool two_
   (void)blocks;  // one fixed grid for every call
   if (bytes > st->max_bytes || bytes % 16) throw std::invalid_argument("custom all-reduce: bad size");
   const long nvec = (long)(bytes / 16);
-  if (two_shot)
-    car_ar_kernel<true><<<CAR_NB, CAR_T, 0, s>>>(st->peers, st->rank, st->world, static_cast<const u16x8*>(inp),
-                                                 static_cast<u16x8*>(out), nvec);
-  else
-    car_ar_kernel<false><<<CAR_NB, CAR_T, 0, s>>>(st->peers, st->rank, st->world, static_cast<const u16x8*>(inp),
-                                                  static_cast<u16x8*>(out), nvec);
+  auto* i = static_cast<const u16x8*>(inp);
+  auto* o = static_cast<u16x8*>(out);
+  if (bytes <= st->peers.bytes[K_AR_S]) {
+    if (two_shot) car_ar_kernel<CAR_NB_S, true><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_AR_S, st->rank, st->world, i, o, nvec);
+    else car_ar_kernel<CAR_NB_S, false><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_AR_S, st->rank, st->world, i, o, nvec);
+  } else {  // large messages: always reduce-scatter + all-gather (2/N of the bytes per link)
+    car_ar_kernel<CAR_NB_L, true><<<CAR_NB_L, CAR_T, 0, s>>>(st->peers, K_AR_L, st->rank, st->world, i, o, nvec);
+  }
 }
 
 void launch_car_all_gather(void* state, const void* inp, void* out, size_t shard_bytes, size_t row_bytes,
@@ -500,16 +543,16 @@ void launch_car_all_gather(void* state, const void* inp, void* out, size_t shard
   if (shard_bytes > st->max_bytes || row_bytes == 0 || shard_bytes % row_bytes)
     throw std::invalid_argument("custom all-gather: bad size");
   if (row_bytes % 16 == 0)
-    car_ag_kernel<u16x8><<<CAR_NB, CAR_T, 0, s>>>(st->peers, st->rank, st->world, static_cast<const u16x8*>(inp),
+    car_ag_kernel<u16x8><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, st->rank, st->world, static_cast<const u16x8*>(inp),
                                                   static_cast<u16x8*>(out), (long)(shard_bytes / 16),
                                                   (long)(row_bytes / 16));
   else if (row_bytes % 4 == 0)
-    car_ag_kernel<unsigned int><<<CAR_NB, CAR_T, 0, s>>>(st->peers, st->rank, st->world,
+    car_ag_kernel<unsigned int><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, st->rank, st->world,
                                                          static_cast<const unsigned int*>(inp),
                                                          static_cast<unsigned int*>(out), (long)(shard_bytes / 4),
                                                          (long)(row_bytes / 4));
   else if (row_bytes % 2 == 0)
-    car_ag_kernel<unsigned short><<<CAR_NB, CAR_T, 0, s>>>(st->peers, st->rank, st->world,
+    car_ag_kernel<unsigned short><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, st->rank, st->world,
                                                            static_cast<const unsigned short*>(inp),
                                                            static_cast<unsigned short*>(out),
                                                            (long)(shard_bytes / 2), (long)(row_bytes / 2));
@@ -517,11 +560,20 @@ void launch_car_all_gather(void* state, const void* inp, void* out, size_t shard
     throw std::invalid_argument("custom all-gather: rows must be a multiple of 2 bytes");
 }
 
+static bool norm_fits_class(const CarState* st, size_t B, long max_rows, int M, int N, bool exch_f32) {
+  return M <= max_rows && N % (8 * st->world) == 0 && (size_t)M * N * (exch_f32 ? 4 : 2) <= 2 * B &&
+         (size_t)M * N * 2 <= B;
+}
+
+// small class: decode batches (<= 512 rows that fit its 8 MiB regions)
+static bool norm_small(const CarState* st, int M, int N, bool exch_f32) {
+  const size_t SB = (st->peers.bytes[K_NORM_S] - align_up(CAR_S_ROWS * sizeof(float), 256)) / 3;
+  return norm_fits_class(st, SB, CAR_S_ROWS, M, N, exch_f32);
+}
+
 bool car_norm_fits(void* state, int M, int N, bool exch_f32) {
   auto* st = static_cast<CarState*>(state);
-  const size_t B = st->max_bytes;
-  return M <= CAR_MAX_ROWS && N % (8 * st->world) == 0 && (size_t)M * N * (exch_f32 ? 4 : 2) <= 2 * B &&
-         (size_t)M * N * 2 <= B;
+  return norm_small(st, M, N, exch_f32) || norm_fits_class(st, st->max_bytes, CAR_MAX_ROWS, M, N, exch_f32);
 }
 
 void launch_car_add_rmsnorm(void* state, void* out, void* residual, const void* x, bool x_f32, int S,
@@ -530,8 +582,16 @@ void launch_car_add_rmsnorm(void* state, void* out, void* residual, const void* 
   if (!car_norm_fits(state, M, N, exch_f32)) throw std::invalid_argument("custom add+rmsnorm: message too large");
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
+  const bool small = norm_small(st, M, N, exch_f32);
 #define CAR_NORM_LAUNCH(IN, EX, WF)                                                                             \
-  car_norm_kernel<IN, EX, WF><<<CAR_NB, CAR_T, 0, s>>>(st->peers, st->rank, st->world, x, S, r, w, o, M, N, eps)
+  do {                                                                                                         \
+    if (small)                                                                                                 \
+      car_norm_kernel<CAR_NB_S, IN, EX, WF><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_NORM_S, st->rank, st->world,  \
+                                                                       x, S, r, w, o, M, N, eps);              \
+    else                                                                                                       \
+      car_norm_kernel<CAR_NB_L, IN, EX, WF><<<CAR_NB_L, CAR_T, 0, s>>>(st->peers, K_NORM_L, st->rank, st->world,  \
+                                                                       x, S, r, w, o, M, N, eps);              \
+  } while (0)
   if (x_f32) {
     if (exch_f32) { if (weight_f32) CAR_NORM_LAUNCH(0, true, true); else CAR_NORM_LAUNCH(0, true, false); }
     else { if (weight_f32) CAR_NORM_LAUNCH(0, false, true); else CAR_NORM_LAUNCH(0, false, false); }

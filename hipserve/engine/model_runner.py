@@ -108,7 +108,9 @@ class ModelRunner:
                 H = mcfg.hidden_size
                 msg = max(ecfg.max_num_batched_tokens * H * 2,
                           ecfg.max_num_seqs * self.model.vpad * 2, 8 << 20)
-                tp.ensure_custom_ar(msg)
+                if tp.ensure_custom_ar(msg):
+                    # prefill-sized messages: in-house kernel or RCCL, measured on this node
+                    tp.calibrate_collectives(H, ecfg.max_num_batched_tokens)
         self.max_bs = min(ecfg.max_num_seqs, max(GRAPH_BUCKETS))
         self.buckets = [b for b in GRAPH_BUCKETS if b <= max(self.max_bs, 1)]
         if self.buckets[-1] < self.max_bs:

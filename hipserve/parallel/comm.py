@@ -42,6 +42,11 @@ class TPGroup:
         # exact_reduce forces fp32 everywhere (prefill GEMMs then write fp32 too)
         self.fp32_exchange_rows = int(os.environ.get("HIPSERVE_TP_FP32_ROWS", 512))
         self.exact_reduce = os.environ.get("HIPSERVE_TP_EXACT", "0") == "1"
+        # eager (prefill-sized) messages of at least this many rows go through RCCL
+        # instead of the in-house kernels; set per node by calibrate_collectives()
+        # (None: always in-house). HIPSERVE_CAR_RCCL_MIN_ROWS overrides (-1: never).
+        self.rccl_min_rows: int | None = None
+        self.collective_report: list[dict] = []
 
     SHM_SLOT_BYTES = 8 << 20
     SHM_SLOTS = 4
@@ -82,13 +87,19 @@ class TPGroup:
             raise RuntimeError(f"{what} is not covered by the custom collectives and cannot be "
                                "captured on a gloo process group (register a larger custom buffer)")
 
+    def _use_rccl(self, rows: int) -> bool:
+        """Route an eager message of ``rows`` rows through RCCL (calibrated crossover;
+        captured decode graphs always use the in-house kernels)."""
+        return (self.rccl_min_rows is not None and rows >= self.rccl_min_rows and self.backend == "nccl"
+                and not torch.cuda.is_current_stream_capturing())
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over TP ranks: bf16 messages that fit the registered buffer
-        through the HIP-IPC custom all-reduce (when set up), everything else
-        through the process group (RCCL)."""
+        through the HIP-IPC custom all-reduce (when set up) below the calibrated
+        RCCL crossover, everything else through the process group (RCCL)."""
         if self.world_size > 1:
             car = self.custom_ar
-            if car is not None and car.supports(t):
+            if car is not None and car.supports(t) and not self._use_rccl(t.shape[0] if t.dim() > 1 else 1):
                 car.all_reduce(t)
             else:
                 self._uncapturable("all_reduce")
@@ -105,7 +116,7 @@ class TPGroup:
         car = self.custom_ar
         if exch_f32 is None:
             exch_f32 = self.exact_reduce or M <= self.fp32_exchange_rows
-        if car is not None and x.is_cuda:
+        if car is not None and x.is_cuda and not self._use_rccl(M):
             if not car.norm_fits(M, N, exch_f32) and exch_f32 and not self.exact_reduce:
                 exch_f32 = False
             if car.norm_fits(M, N, exch_f32):
@@ -168,6 +179,70 @@ class TPGroup:
             return False
         self.custom_ar = car
         return True
+
+    def calibrate_collectives(self, N: int, max_rows: int, dtype=torch.bfloat16) -> list[dict]:
+        """Collective, at start-up on a TP>1 RCCL node with the in-house kernels up:
+        time the fused cross-rank add+RMSNorm of an eager [M, N] bf16 message both
+        ways — the in-house IPC kernel vs RCCL all-reduce + local fused add+RMSNorm —
+        at prefill-sized row counts, and route M >= the smallest row count from which
+        RCCL is faster at every larger measured size through RCCL. Timings are the max
+        over ranks, so every rank takes the same decision."""
+        env = os.environ.get("HIPSERVE_CAR_RCCL_MIN_ROWS")
+        if env is not None:
+            v = int(env)
+            self.rccl_min_rows = None if v < 0 else v
+            return []
+        car = self.custom_ar
+        if self.world_size == 1 or car is None or self.backend != "nccl":
+            return []
+        dev = self.device
+        ops = _default_ops(dev)
+        rows = [m for m in (256, 512, 1024, 2048, 4096, 8192, 16384) if m <= max_rows] or [max_rows]
+        w = torch.ones(N, dtype=dtype, device=dev)
+        res: list[tuple[int, float, float]] = []
+        self.rccl_min_rows = None
+        for M in rows:
+            if not car.norm_fits(M, N, False):
+                break
+            g = torch.Generator(device=dev).manual_seed(M + self.rank)
+            x = (torch.randn(M, N, device=dev, generator=g) * 0.1).to(dtype)
+            resid = torch.zeros(M, N, dtype=dtype, device=dev)
+            out = torch.empty_like(resid)
+
+            def run_car():
+                car.add_rmsnorm(out, resid, x, 1, w, 1e-5, False)
+
+            def run_rccl():
+                h = x.clone()
+                dist.all_reduce(h, group=self.group)
+                ops.fused_add_rmsnorm(out, h, resid, w, 1e-5)
+
+            ts = []
+            for fn in (run_car, run_rccl):
+                for _ in range(2):
+                    fn()
+                torch.cuda.synchronize(dev)
+                self.barrier()
+                best = float("inf")
+                for _ in range(5):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    fn()
+                    b.record()
+                    b.synchronize()
+                    best = min(best, a.elapsed_time(b) * 1000.0)
+                ts.append(best)
+            tt = torch.tensor(ts, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=self._cpu_group)
+            res.append((M, float(tt[0]), float(tt[1])))
+        self.check()
+        for i, (M, tc, tr) in enumerate(res):
+            if all(r[2] < r[1] for r in res[i:]):
+                self.rccl_min_rows = M
+                break
+        self.collective_report = [{"rows": M, "N": N, "car_us": round(tc, 1), "rccl_us": round(tr, 1)}
+                                  for M, tc, tr in res]
+        return self.collective_report
 
     def all_gather_lastdim(self, t: torch.Tensor) -> torch.Tensor:
         """[n, V/TP] on every rank -> [n, V] on every rank (in-house IPC gather when

@@ -13,7 +13,12 @@ staged copies directly over xGMI:
   cross-rank sum of the local (split-K) partials, residual add and RMSNorm in one
   kernel, exchanging fp32 (TP=N within fp32 rounding of TP=1) or bf16.
 
-Messages larger than the registered buffer stay on RCCL. Enabled only after a
+Each collective has a decode-sized class (64-block grid, lowest latency) and a
+prefill-sized class (512-block grid: every CU streams) with their own buffers and
+flags. Whether an eager prefill-sized message uses these kernels or RCCL
+(all-reduce + local add+RMSNorm) is measured on the node at start-up
+(``TPGroup.calibrate_collectives``); messages larger than the registered buffer
+always use RCCL, and captured decode graphs always use these kernels. Enabled only after a
 self-test against the process-group all-reduce passes on every rank (the
 decision is collective), so a node whose IPC / peer mapping misbehaves keeps the
 RCCL path instead of producing wrong sums. A barrier timeout anywhere sets a
@@ -106,7 +111,11 @@ def self_test(car: CustomAllReduce, group, cpu_group) -> bool:
     and two-shot) plus the all-gather; collective agreement (all ranks must pass)."""
     ok = True
     try:
-        for numel in (8, 4096, 64 * 8192, min(car.max_bytes // 2, 2 << 20)):
+        # one-shot, two-shot (small class) and the 512-block large class (> 8 MiB)
+        sizes = [8, 4096, 64 * 8192, min(car.max_bytes // 2, 2 << 20)]
+        if car.max_bytes >= (12 << 20):
+            sizes.append(6 << 20)  # bf16 elements: 12 MiB
+        for numel in sizes:
             g = torch.Generator(device=car.device).manual_seed(1234 + 17 * car.rank + numel)
             x = torch.randn(numel, device=car.device, dtype=torch.float32, generator=g).to(torch.bfloat16)
             want = x.float().cpu()

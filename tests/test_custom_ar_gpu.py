@@ -60,9 +60,10 @@ def _worker(rank, world, port, q):
     dev = torch.device("cuda", 0)
     res = {}
     try:
-        car = CustomAllReduce(rank, world, dist.group.WORLD, dev, max_bytes=4 << 20)
-        # all-reduce, one-shot and two-shot, sizes interleaved with the other kinds
-        for numel in (8, 1000 * 8, 64 * 4096, 1 << 20, 24, 3 * 4096):
+        car = CustomAllReduce(rank, world, dist.group.WORLD, dev, max_bytes=24 << 20)
+        # all-reduce, one-shot and two-shot, sizes interleaved with the other kinds;
+        # 5M / 9M elements (10 / 18 MiB) run on the 512-block prefill-sized class
+        for numel in (8, 1000 * 8, 64 * 4096, 5 << 20, 1 << 20, 24, 9 << 20, 3 * 4096):
             for it in range(3):
                 x = _inputs(numel, rank, it, torch).to(dev)
                 want = sum(_inputs(numel, r, it, torch).float() for r in range(world))
@@ -80,9 +81,11 @@ def _worker(rank, world, port, q):
             res[("ag", rows, cols, str(dt))] = bool(torch.equal(got.cpu(), want))
         # fused cross-rank add + RMSNorm
         eps = 1e-5
+        # rows > 512: the 512-block class (2 or more rows per block, 64..256 threads a row)
         for S, M, N, exch, wf32, bf_in in ((4, 64, 2048, True, False, False), (1, 1, 1024, True, False, False),
-                                           (2, 70, 1024, False, True, False), (1, 130, 4096, True, True, True),
-                                           (1, 16, 512, False, False, True)):
+                                           (1, 1024, 4096, False, False, True), (2, 70, 1024, False, True, False),
+                                           (1, 130, 4096, True, True, True), (1, 700, 512, False, False, True),
+                                           (1, 16, 512, False, False, True), (1, 1500, 2048, False, True, True)):
             for it in range(2):
                 xs = [_norm_inputs(r, S, M, N, it, torch)[0] for r in range(world)]
                 _, resid, w = _norm_inputs(rank, S, M, N, it, torch)
