@@ -144,6 +144,54 @@ constexpr int DG_GLU = 1, DG_PARTIAL = 2;
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, bool packed, int flags, hipStream_t s);
 
+// decode_layer.hip — decode GEMM (packed weights, RT = 1, M <= 64) with the layer's
+// epilogue inside the launch: split-K slices reduced by the tile's last-arriving
+// workgroup (ws [S, M, N] fp32 + per-tile counters, zero between calls), then
+//   fix 1 (ADD):  residual[M, N] = bf16(bf16(h) + residual), ss_out[N/128, M] = per-tile row sums of squares
+//   fix 2 (ROPE): q -> q_out (rotated), k / v -> the paged cache (bias, q/k RMSNorm optional)
+//   fix 3 (GLU):  out = act [M, N/2] (gate/up-interleaved packing)
+// norm_in: x is the bf16 residual; x is normalised on load with inv = rsqrt(sum(ss_in[Tin, M]) / K + eps)
+// and the bf16 norm weight norm_w [K].
+struct DgfArgs {
+  float* ws;
+  int* counters;
+  const float* ss_in;
+  int Tin;
+  const unsigned short* norm_w;
+  float eps;
+  unsigned short* residual;
+  float* ss_out;
+  unsigned short* q_out;
+  long q_stride;
+  const long* positions;
+  const long* slots;
+  const float* cos_sin;
+  unsigned short* k_cache;
+  unsigned short* v_cache;
+  int nq, nkv, D, block_size, rope_mode;
+  const unsigned short* bias;
+  const float* qw;
+  const float* kw;
+  unsigned short* out;
+  long out_stride;
+};
+bool dgf_supported(int fix, bool norm_in, int M, int N, int K, int S);
+bool launch_dgf(int fix, bool norm_in, const DgfArgs& A, const void* x, long x_stride, const void* w, int M, int N,
+                int K, int S, hipStream_t s);
+
+// prefill_gemm.hip — C[M, N] = A[M, K] . B[N, K]^T (bf16, 256x256x64 MFMA tiles, LDS-DMA
+// staging), N % 256 == 0, K % 64 == 0, any M. Epilogues:
+//   PG_EPI_STORE  C = bf16(acc)
+//   PG_EPI_ADD    C (the residual, in place) = bf16(bf16(acc) + C)
+//   PG_EPI_GLU    B packed by launch_pack_glu_rows; C = act [M, N/2] = silu(gate) * up
+constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2;
+struct PgEpi {
+  int unused;
+};
+bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
+                         int K, const PgEpi& E, hipStream_t s);
+void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);
+
 // decode_fused.hip — split-K partial reductions fused with the next op of the layer
 // ws: [S, M, N] fp32 partials. h = bf16(sum_s ws); residual = bf16(h + residual);
 // out = rmsnorm(residual) * w  (bit-identical to splitk_reduce + fused_add_rmsnorm)

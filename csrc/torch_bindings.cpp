@@ -653,6 +653,113 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
               "decode_gemm_glu: unsupported (rt, K/splits)");
 }
 
+// Prefill GEMM (prefill_gemm.hip): out = x @ w^T with a fused epilogue.
+// epi 0: out [M, N] bf16; 1: out is the residual [M, N], out = bf16(bf16(x w^T) + out);
+// 2: w packed by pack_glu_rows, out = act [M, N/2].
+void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t epi) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w);
+  CHECK_ROWMAJOR(out);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && N % 256 == 0 && K % 64 == 0, "prefill_gemm: w [N % 256, K % 64]");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "prefill_gemm: alignment");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm: out shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::PgEpi E{};
+  TORCH_CHECK(hipserve::launch_prefill_gemm((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
+                                            w.data_ptr(), w.stride(0), M, N, K, E, cur_stream()),
+              "prefill_gemm: unsupported");
+}
+
+void pack_glu_rows(at::Tensor& out, const at::Tensor& w) {
+  CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
+  const int N = w.size(0), K = w.size(1);
+  TORCH_CHECK(N % 256 == 0 && K % 8 == 0 && out.numel() == w.numel(), "pack_glu_rows: [2I % 256, K]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
+  hipserve::launch_pack_glu_rows(out.data_ptr(), w.data_ptr(), N / 2, K, cur_stream());
+}
+
+// Fused decode layer v2 (decode_layer.hip): one packed decode GEMM whose split-K
+// fix-up runs the layer epilogue in the same launch. fix: 1 add (+ss), 2 rope, 3 glu.
+static const void* opt_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+void decode_gemm_fused(int64_t fix, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t splits,
+                       at::Tensor& ws, at::Tensor& counters, const c10::optional<at::Tensor>& ss_in,
+                       const c10::optional<at::Tensor>& norm_w, double eps,
+                       const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& ss_out,
+                       const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& positions,
+                       const c10::optional<at::Tensor>& slots, const c10::optional<at::Tensor>& cos_sin,
+                       const c10::optional<at::Tensor>& k_cache, const c10::optional<at::Tensor>& v_cache,
+                       int64_t nq, int64_t nkv, int64_t head_dim, int64_t block_size, int64_t mode,
+                       const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& q_w,
+                       const c10::optional<at::Tensor>& k_w) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_ROWMAJOR(x); CHECK_CONTIG(wp);
+  const int M = x.size(0), K = x.size(1);
+  const bool norm_in = ss_in.has_value();
+  TORCH_CHECK(wp.numel() == N * K && x.stride(0) % 8 == 0, "decode_gemm_fused: packed weight [N/128 tiles] x K");
+  TORCH_CHECK(hipserve::dgf_supported((int)fix, norm_in, M, (int)N, K, (int)splits),
+              "decode_gemm_fused: unsupported (fix, M, N, K, splits)");
+  TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= N / 128, "decode_gemm_fused: counters");
+  if (splits > 1)
+    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * N,
+                "decode_gemm_fused: ws must hold S*M*N fp32");
+  hipserve::DgfArgs A{};
+  A.ws = splits > 1 ? ws.data_ptr<float>() : nullptr;
+  A.counters = counters.data_ptr<int>();
+  if (norm_in) {
+    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->is_contiguous() && ss_in->numel() % M == 0,
+                "decode_gemm_fused: ss_in [Tin, M] fp32");
+    TORCH_CHECK(norm_w.has_value() && norm_w->scalar_type() == at::kBFloat16 && norm_w->numel() == K,
+                "decode_gemm_fused: bf16 norm weight [K]");
+    A.ss_in = ss_in->data_ptr<float>();
+    A.Tin = ss_in->numel() / M;
+    A.norm_w = static_cast<const unsigned short*>(norm_w->data_ptr());
+  }
+  A.eps = (float)eps;
+  if (fix == 1) {
+    TORCH_CHECK(residual.has_value() && ss_out.has_value(), "decode_gemm_fused(add): residual, ss_out");
+    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "decode_gemm_fused(add): residual [M, N]");
+    TORCH_CHECK(ss_out->scalar_type() == at::kFloat && ss_out->numel() >= (N / 128) * M, "ss_out [N/128, M]");
+    A.residual = static_cast<unsigned short*>(residual->data_ptr());
+    A.ss_out = ss_out->data_ptr<float>();
+  } else if (fix == 2) {
+    TORCH_CHECK(out.has_value() && positions.has_value() && slots.has_value() && cos_sin.has_value() &&
+                k_cache.has_value() && v_cache.has_value(), "decode_gemm_fused(rope): q_out, positions, slots, "
+                "cos_sin, caches");
+    TORCH_CHECK((head_dim == 64 || head_dim == 128) && N == (nq + 2 * nkv) * head_dim, "decode_gemm_fused(rope): heads");
+    CHECK_BF16((*out)); CHECK_ROWMAJOR((*out));
+    TORCH_CHECK(out->size(0) >= M && out->size(1) >= nq * head_dim, "decode_gemm_fused(rope): q_out [M, nq*D]");
+    TORCH_CHECK(positions->scalar_type() == at::kLong && slots->scalar_type() == at::kLong &&
+                cos_sin->scalar_type() == at::kFloat, "decode_gemm_fused(rope): index / table dtypes");
+    A.q_out = static_cast<unsigned short*>(out->data_ptr());
+    A.q_stride = out->stride(0);
+    A.positions = positions->data_ptr<int64_t>();
+    A.slots = slots->data_ptr<int64_t>();
+    A.cos_sin = cos_sin->data_ptr<float>();
+    A.k_cache = static_cast<unsigned short*>(k_cache->data_ptr());
+    A.v_cache = static_cast<unsigned short*>(v_cache->data_ptr());
+    A.nq = nq; A.nkv = nkv; A.D = head_dim; A.block_size = block_size; A.rope_mode = mode;
+    if (bias.has_value()) { CHECK_BF16((*bias)); TORCH_CHECK(bias->numel() == N); }
+    A.bias = static_cast<const unsigned short*>(opt_ptr(bias));
+    if (q_w.has_value()) {
+      TORCH_CHECK(mode == 0 && k_w.has_value() && q_w->scalar_type() == at::kFloat && q_w->numel() == head_dim &&
+                  k_w->scalar_type() == at::kFloat && k_w->numel() == head_dim, "decode_gemm_fused(rope): q/k norm");
+      A.qw = q_w->data_ptr<float>();
+      A.kw = k_w->data_ptr<float>();
+    }
+  } else if (fix == 3) {
+    TORCH_CHECK(out.has_value(), "decode_gemm_fused(glu): act");
+    CHECK_BF16((*out)); CHECK_ROWMAJOR((*out));
+    TORCH_CHECK(out->size(0) == M && out->size(1) == N / 2 && out->stride(0) % 4 == 0, "act [M, N/2]");
+    A.out = static_cast<unsigned short*>(out->data_ptr());
+    A.out_stride = out->stride(0);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_dgf((int)fix, norm_in, A, x.data_ptr(), x.stride(0), wp.data_ptr(), M, (int)N, K,
+                                   (int)splits, cur_stream()),
+              "decode_gemm_fused: launch");
+}
+
 void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
                         const at::Tensor& weight, double eps) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
@@ -932,6 +1039,12 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
+  m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi) -> ()");
+  m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
+  m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
+        "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
+        "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
+        "int head_dim, int block_size, int mode, Tensor? bias, Tensor? q_w, Tensor? k_w) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu) -> ()");
   m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
@@ -973,6 +1086,9 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("pack_decode_weight", &pack_decode_weight);
   m.impl("decode_gemm_partial", &decode_gemm_partial);
   m.impl("decode_gemm_glu", &decode_gemm_glu);
+  m.impl("decode_gemm_fused", &decode_gemm_fused);
+  m.impl("prefill_gemm", &prefill_gemm);
+  m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.impl("splitk_rope_cache", &splitk_rope_cache);
   m.impl("splitk_glu", &splitk_glu);

@@ -118,6 +118,10 @@ class LlamaModel:
     # LDS): 5.322 / 5.332 vs 5.332 / 5.327 ms (tools/decode_gap.py, alternating runs) —
     # parity, so the separate splitk_rope_cache launch stays the default
     fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "0") == "1"
+    # fused decode layer v2 (csrc/kernels/decode_layer.hip): the split-K fix-up and
+    # the layer epilogue inside each decode GEMM launch, RMSNorm applied on load —
+    # five kernels per Llama layer instead of eight (TP = 1 dense families)
+    fused_v2 = os.environ.get("HIPSERVE_FUSED_V2", "1") == "1"
 
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,
                  max_pos: int | None = None):
@@ -371,6 +375,10 @@ class LlamaModel:
             free, _ = torch.cuda.mem_get_info(self.device)
             return free - w.numel() * w.element_size() >= reserve
 
+        if self.device.type == "cuda" and getattr(self, "_dgf_counters", None) is None:
+            # split-K tile tickets of the v2 fused decode GEMMs (zero between calls:
+            # each tile's last arriver resets its own)
+            self._dgf_counters = torch.zeros(8192, dtype=torch.int32, device=self.device)
         for lw in self.layers:
             for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
                 if (isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes
@@ -495,6 +503,9 @@ class LlamaModel:
         eps = cfg.rms_norm_eps
         Tp, Td = meta.num_prefill_tokens, meta.num_decode
         if self._fused_ok(meta):
+            plan = self.v2_plan(T, meta)
+            if plan is not None:
+                return self.forward_decode_v2(ids, meta, kv_caches, plan)
             return self.forward_decode_fused(ids, meta, kv_caches)
         ids = self.resolve_ids(ids, meta)
         h = self.embed_tokens(ids)
@@ -640,6 +651,97 @@ class LlamaModel:
             else:
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(act, lw.wd), 1, nxt)
         return xn
+
+    @staticmethod
+    def _dgf_ok(fix: int, norm_in: bool, M: int, N: int, K: int, S: int) -> bool:
+        """Mirror of decode_layer.hip ``dgf_supported``."""
+        if not (1 <= M <= 64 and N % 128 == 0 and K % 256 == 0 and S >= 1 and K % (256 * S) == 0):
+            return False
+        if K // S // 256 not in (1, 2, 4, 7, 8, 16):
+            return False
+        return (not norm_in) if fix == 1 else (fix == 2 or (fix == 3 and norm_in))
+
+    def v2_plan(self, T: int, meta: AttnMeta):
+        """Split counts (qkv, o, gate|up, down) of the v2 fused decode layer at batch
+        T — the tuned packed decode GEMM's S for each projection — or None when the
+        layer does not qualify (TP > 1, MoE / quantised / sandwich families, a
+        projection the tuner left to hipBLASLt, weights without a packed copy)."""
+        if not (self.fused_v2 and self.tp.world_size == 1 and T <= 64 and self.D in (64, 128)
+                and getattr(self, "_dgf_counters", None) is not None):
+            return None
+        lw0 = self.layers[0]
+        ws = (lw0.wqkv, lw0.wo, lw0.wgu, lw0.wd)
+        if lw0.router is not None or not all(isinstance(w, torch.Tensor) for w in ws):
+            return None
+        if lw0.ln1.dtype != torch.bfloat16 or lw0.ln2.dtype != torch.bfloat16 or self.norm.dtype != torch.bfloat16:
+            return None
+        plan = []
+        for w, fix, norm_in in zip(ws, (2, 1, 3, 1), (True, False, True, False)):
+            N, K = w.shape
+            c = gemm.TUNER.choose(T, N, K)
+            if not (isinstance(c, tuple) and c[0] == "dgp") or not self._dgf_ok(fix, norm_in, T, N, K, c[2]):
+                return None
+            plan.append(c[2])
+        for lw in self.layers:
+            if (gemm.packed_of(lw.wqkv) is None or gemm.packed_of(lw.wo) is None or gemm.glu_of(lw.wgu) is None
+                    or gemm.packed_of(lw.wd) is None):
+                return None
+        return plan
+
+    def forward_decode_v2(self, ids: torch.Tensor, meta: AttnMeta, kv_caches, plan) -> torch.Tensor:
+        """Decode-only forward, five kernels per layer (decode_layer.hip): qkv GEMM
+        (input RMSNorm on load; RoPE + KV write in its split-K fix-up), paged
+        attention, o_proj GEMM (residual add + per-tile sums of squares in the
+        fix-up), gate|up GEMM (post-attention RMSNorm on load, SiLU-GLU epilogue),
+        down GEMM (residual add + sums of squares). Layer 0 takes the embedding's
+        fused first RMSNorm; the final RMSNorm is one row-norm kernel."""
+        ops, cfg, op = self.ops, self.cfg, torch.ops.hipserve
+        T = ids.shape[0]
+        D, nq, nkv = self.D, self.nq, self.nkv
+        H = cfg.hidden_size
+        eps = cfg.rms_norm_eps
+        lw0 = self.layers[0]
+        if meta.id_src is not None and self.fused_embed_ok(meta):
+            residual = torch.empty(T, H, device=ids.device, dtype=self.embed.dtype)
+            xn = torch.empty_like(residual)
+            op.embed_rmsnorm(xn, residual, self.embed, ids, meta.id_src[0], meta.id_src[1], lw0.ln1, eps)
+        else:
+            h = self.embed_tokens(self.resolve_ids(ids, meta))
+            residual = h.clone()
+            xn = torch.empty_like(h)
+            ops.rmsnorm(xn, h, lw0.ln1, eps)
+        Sq, So, Sg, Sd = plan
+        Nq, I2 = lw0.wqkv.shape[0], lw0.wgu.shape[0]
+        dt, dev = residual.dtype, residual.device
+        qbuf = torch.empty(T, Nq, device=dev, dtype=dt)     # q heads in the qkv row layout
+        attn = torch.empty(T, nq * D, device=dev, dtype=dt)
+        act = torch.empty(T, I2 // 2, device=dev, dtype=dt)
+        ss = torch.empty(H // 128, T, device=dev, dtype=torch.float32)
+        ctr = self._dgf_counters
+        e32 = gemm._empty(dev)[1]
+        part, tmp_out, tmp_ml = self._decode_split(T, meta)
+        bs = kv_caches[0][0].shape[2]
+
+        def ws(S, N):
+            return torch.empty(S * T * N, device=dev, dtype=torch.float32) if S > 1 else e32
+
+        for i, lw in enumerate(self.layers):
+            kc, vc = kv_caches[i]
+            x_in, ss_in, nw = (xn, None, None) if i == 0 else (residual, ss, lw.ln1)
+            op.decode_gemm_fused(2, x_in, gemm.packed_of(lw.wqkv), Nq, Sq, ws(Sq, Nq), ctr, ss_in, nw, eps, None,
+                                 None, qbuf, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
+                                 bs, cfg.rope_mode, lw.bqkv, lw.q_norm, lw.k_norm)
+            ops.paged_decode(attn, qbuf, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part,
+                             self.scale)
+            op.decode_gemm_fused(1, attn, gemm.packed_of(lw.wo), H, So, ws(So, H), ctr, None, None, eps, residual,
+                                 ss, None, None, None, None, None, None, 0, 0, 0, 0, 0, None, None, None)
+            op.decode_gemm_fused(3, residual, gemm.glu_of(lw.wgu), I2, Sg, ws(Sg, I2), ctr, ss, lw.ln2, eps, None,
+                                 None, act, None, None, None, None, None, 0, 0, 0, 0, 0, None, None, None)
+            op.decode_gemm_fused(1, act, gemm.packed_of(lw.wd), H, Sd, ws(Sd, H), ctr, None, None, eps, residual,
+                                 ss, None, None, None, None, None, None, 0, 0, 0, 0, 0, None, None, None)
+        out = torch.empty_like(residual)
+        ops.rmsnorm(out, residual, self.norm, eps)
+        return out
 
     def quant_weights(self) -> list:
         """Every GGUF-quantised projection (QuantWeight), lm_head included."""

@@ -52,6 +52,10 @@ prof_run() {
   rm -rf $OUT/$name  # raw traces exceed gpurun's 64 MiB copy-back limit
   return 0
 }
+run_pgemm() {
+  timeout -k 10 300 python -u tools/bench_pgemm.py --model ${PG_MODEL:-8b} > $OUT/bench_pgemm.log 2>&1
+  local rc=$?; tail -n 8 $OUT/bench_pgemm.log; return $rc
+}
 run_bench_mixtral() {
   timeout -k 10 600 python -u bench.py --model mixtral-8x7b --concurrency 32 --out $OUT/bench_mixtral.json \
     > $OUT/bench_mixtral.log 2>&1
@@ -68,6 +72,7 @@ for s in $steps; do
     bench) run_bench ;;
     bench_q4) run_bench_q4 ;;
     bench_mixtral) run_bench_mixtral ;;
+    pgemm) run_pgemm ;;
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;

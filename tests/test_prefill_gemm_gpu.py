@@ -1,0 +1,51 @@
+"""Hand-written prefill GEMM (csrc/kernels/prefill_gemm.hip) vs a plain PyTorch fp32
+reference of the same op: plain store, residual add and the SiLU-GLU epilogue, on
+ragged row counts (M not a multiple of the 256-row tile) and K from one 64-deep tile
+up. Asymmetric random operands catch transposed fragments / swizzles."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+SHAPES = [(256, 256, 64), (300, 512, 1024), (1000, 768, 2048), (2049, 1280, 512), (64, 1024, 4096),
+          (8192, 512, 4096)]
+
+
+def _rnd(g, *s, scale=1.0):
+    return ((torch.rand(*s, device=DEV, generator=g) * 2 - 1) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_prefill_gemm_store(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm(out, x, w, 0)
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES[:4])
+def test_prefill_gemm_residual_add(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(7 + M)
+    x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
+    res0 = _rnd(g, M, N)
+    res = res0.clone()
+    torch.ops.hipserve.prefill_gemm(res, x, w, 1)
+    h = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    want = (h + res0.float()).to(torch.bfloat16).float()
+    torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M,I,K", [(300, 256, 1024), (1000, 384, 512), (2049, 128, 256)])
+def test_prefill_gemm_glu(M, I, K):
+    g = torch.Generator(device=DEV).manual_seed(11 + M)
+    x, w = _rnd(g, M, K), _rnd(g, 2 * I, K, scale=0.05)
+    wp = torch.empty_like(w)
+    torch.ops.hipserve.pack_glu_rows(wp, w)
+    act = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm(act, x, wp, 2)
+    gu = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    want = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    torch.testing.assert_close(act.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())

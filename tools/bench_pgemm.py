@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""The hand-written prefill GEMM (csrc/kernels/prefill_gemm.hip) vs hipBLASLt
+(``F.linear``) on the Llama-3-8B / 70B-TP8 prefill shapes at M = 8192 rows, random
+[-1, 1) operands (cdna_hip_programming.md rule 25), one weight per layer so the 32
+calls stream 32 different weights. Also the fused units: GLU (gate|up GEMM + SiLU·mul)
+and residual add (o / down GEMM + add) vs hipBLASLt + the separate elementwise
+kernel. One JSON line per shape plus a markdown table.
+
+usage: python tools/bench_pgemm.py [--m 8192] [--layers 8] [--model 8b|70b-tp8]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+import torch.nn.functional as F
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--layers", type=int, default=8)
+    ap.add_argument("--model", default="8b")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    from hipserve.ops import KernelOps
+
+    ops = KernelOps()
+    op = torch.ops.hipserve
+    dev = "cuda"
+    H, I, NQKV = (4096, 14336, 6144) if a.model == "8b" else (8192, 3584, 1280)
+    HO = 4096 if a.model == "8b" else 1024
+    shapes = {"qkv": (NQKV, H), "o": (H, HO), "gu": (2 * I, H), "down": (H, I)}
+    M, L = a.m, a.layers
+
+    def rnd(*s):
+        return (torch.rand(*s, device=dev) * 2 - 1).to(torch.bfloat16)
+
+    def time_fn(fn):
+        fn()
+        torch.cuda.synchronize()
+        best = 1e9
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        return best / L
+
+    rows = []
+    for name, (N, K) in shapes.items():
+        x = rnd(M, K)
+        ws = [rnd(N, K) * 0.05 for _ in range(L)]
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        t_blas = time_fn(lambda: [F.linear(x, w) for w in ws])
+        t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0) for w in ws])
+        r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
+             "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1)}
+        if name == "gu":  # GEMM + SiLU-GLU unit
+            act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
+            wg = [torch.empty_like(w) for w in ws]
+            for w, p in zip(ws, wg):
+                op.pack_glu_rows(p, w)
+
+            def blas_glu():
+                for w in ws:
+                    ops.silu_and_mul(act, F.linear(x, w))
+            r["blas_unit_ms"] = round(time_fn(blas_glu), 4)
+            r["pgemm_unit_ms"] = round(time_fn(lambda: [op.prefill_gemm(act, x, p, 2) for p in wg]), 4)
+        if name in ("o", "down"):  # GEMM + residual add unit
+            res = rnd(M, N)
+
+            def blas_add():
+                for w in ws:
+                    res.add_(F.linear(x, w))
+            r["blas_unit_ms"] = round(time_fn(blas_add), 4)
+            r["pgemm_unit_ms"] = round(time_fn(lambda: [op.prefill_gemm(res, x, w, 1) for w in ws]), 4)
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+        del ws, x, out
+        torch.cuda.empty_cache()
+    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | prefill_gemm ms (TF/s) | unit: hipBLASLt + ew | unit: fused |")
+    print("|---|---|---:|---:|---:|---:|")
+    for r in rows:
+        print(f"| {r['shape']} | {r['M']}x{r['N']}x{r['K']} | {r['blas_ms']} ({r['blas_TFs']}) | "
+              f"{r['pgemm_ms']} ({r['pgemm_TFs']}) | {r.get('blas_unit_ms', '—')} | {r.get('pgemm_unit_ms', '—')} |")
+
+
+if __name__ == "__main__":
+    main()
