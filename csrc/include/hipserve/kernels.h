@@ -113,7 +113,7 @@ bool launch_skinny_gemm(void* out, const void* x, long x_stride, const void* w, 
                         int N, int K, int rt, int kw, hipStream_t s);
 
 // allreduce.hip — custom all-reduce over HIP-IPC peer memory (one-shot / two-shot)
-void* car_create(int rank, int world, size_t max_bytes);
+void* car_create(int rank, int world, size_t max_bytes, int nb_large);
 void car_get_handle(void* state, void* handle_out);
 void car_open(void* state, int peer, const void* handle);
 bool car_error(void* state);

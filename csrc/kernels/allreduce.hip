@@ -92,6 +92,7 @@ struct CarPeers {
 
 struct CarState {
   int rank = 0, world = 1;
+  int nb_large = CAR_NB_L;  // grid of the prefill-sized class (smaller when ranks share a GPU)
   size_t max_bytes = 0;
   unsigned char* own = nullptr;
   CarPeers peers{};
@@ -179,8 +180,8 @@ HS_DEVICE u16x8 sum_bf16x8(const u16x8 (&v)[W], int n) {
 // ------------------------------------------------------------------ all-reduce
 // nvec = 16-byte vectors in the tensor. Rank order of the sum is fixed, so every
 // rank produces identical bits.
-template <int NB, bool TWO_SHOT>
-__global__ __launch_bounds__(CAR_T) void car_ar_kernel(CarPeers P, int kind, int rank, int world,
+template <bool TWO_SHOT>
+__global__ __launch_bounds__(CAR_T) void car_ar_kernel(CarPeers P, int kind, int NB, int rank, int world,
                                                        const u16x8* __restrict__ inp, u16x8* __restrict__ out,
                                                        long nvec) {
   __shared__ unsigned int s_epoch;
@@ -273,8 +274,8 @@ __global__ __launch_bounds__(CAR_T) void car_ag_kernel(CarPeers P, int rank, int
 // TPR = 64..256 threads so a 70B TP=8 chunk (cv = 128) keeps every lane busy with
 // two rows per pass; a row's sum of squares is reduced wave by wave, in wave order
 // (deterministic).
-template <int NB, int kIn, bool kExF32, bool kWF32>
-__global__ __launch_bounds__(CAR_T) void car_norm_kernel(CarPeers P, int kind, int rank, int world,
+template <int kIn, bool kExF32, bool kWF32>
+__global__ __launch_bounds__(CAR_T) void car_norm_kernel(CarPeers P, int kind, int NB, int rank, int world,
                                                          const void* __restrict__ x, int S,
                                                          unsigned short* __restrict__ residual,
                                                          const void* __restrict__ weight,
@@ -439,12 +440,15 @@ static void hip_check(hipError_t e, const char* what) {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-void* car_create(int rank, int world, size_t max_bytes) {
+void* car_create(int rank, int world, size_t max_bytes, int nb_large) {
   if (world < 1 || world > CAR_MAX_RANKS || rank < 0 || rank >= world)
     throw std::invalid_argument("custom collectives: bad rank/world");
   auto* st = new CarState();
   st->rank = rank;
   st->world = world;
+  // every block of a call spins on its peers' block: all blocks of all ranks that
+  // share a device must be resident at once (8 blocks of 256 threads per CU)
+  st->nb_large = nb_large < CAR_NB_S ? CAR_NB_S : (nb_large > CAR_NB_MAX ? CAR_NB_MAX : nb_large);
   st->max_bytes = align_up(max_bytes, 256);
   const size_t B = st->max_bytes;
   // per-parity region of each kind: AR = message; AG = one shard; NORM = fp32
@@ -530,10 +534,11 @@ void launch_car(void* state, const void* inp, void* out, size_t bytes, bool two_
   auto* i = static_cast<const u16x8*>(inp);
   auto* o = static_cast<u16x8*>(out);
   if (bytes <= st->peers.bytes[K_AR_S]) {
-    if (two_shot) car_ar_kernel<CAR_NB_S, true><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_AR_S, st->rank, st->world, i, o, nvec);
-    else car_ar_kernel<CAR_NB_S, false><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_AR_S, st->rank, st->world, i, o, nvec);
+    if (two_shot) car_ar_kernel<true><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_AR_S, CAR_NB_S, st->rank, st->world, i, o, nvec);
+    else car_ar_kernel<false><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_AR_S, CAR_NB_S, st->rank, st->world, i, o, nvec);
   } else {  // large messages: always reduce-scatter + all-gather (2/N of the bytes per link)
-    car_ar_kernel<CAR_NB_L, true><<<CAR_NB_L, CAR_T, 0, s>>>(st->peers, K_AR_L, st->rank, st->world, i, o, nvec);
+    const int nb = st->nb_large;
+    car_ar_kernel<true><<<nb, CAR_T, 0, s>>>(st->peers, K_AR_L, nb, st->rank, st->world, i, o, nvec);
   }
 }
 
@@ -585,12 +590,9 @@ void launch_car_add_rmsnorm(void* state, void* out, void* residual, const void* 
   const bool small = norm_small(st, M, N, exch_f32);
 #define CAR_NORM_LAUNCH(IN, EX, WF)                                                                             \
   do {                                                                                                         \
-    if (small)                                                                                                 \
-      car_norm_kernel<CAR_NB_S, IN, EX, WF><<<CAR_NB_S, CAR_T, 0, s>>>(st->peers, K_NORM_S, st->rank, st->world,  \
-                                                                       x, S, r, w, o, M, N, eps);              \
-    else                                                                                                       \
-      car_norm_kernel<CAR_NB_L, IN, EX, WF><<<CAR_NB_L, CAR_T, 0, s>>>(st->peers, K_NORM_L, st->rank, st->world,  \
-                                                                       x, S, r, w, o, M, N, eps);              \
+    const int nb = small ? CAR_NB_S : st->nb_large;                                                            \
+    car_norm_kernel<IN, EX, WF><<<nb, CAR_T, 0, s>>>(st->peers, small ? K_NORM_S : K_NORM_L, nb, st->rank,      \
+                                                     st->world, x, S, r, w, o, M, N, eps);                      \
   } while (0)
   if (x_f32) {
     if (exch_f32) { if (weight_f32) CAR_NORM_LAUNCH(0, true, true); else CAR_NORM_LAUNCH(0, true, false); }

@@ -398,8 +398,8 @@ void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, 
                                     ids.data_ptr<int>(), T, logits.size(1), k, renorm, cur_stream());
 }
 
-int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes) {
-  return reinterpret_cast<int64_t>(hipserve::car_create((int)rank, (int)world, (size_t)max_bytes));
+int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes, int64_t nb_large) {
+  return reinterpret_cast<int64_t>(hipserve::car_create((int)rank, (int)world, (size_t)max_bytes, (int)nb_large));
 }
 
 at::Tensor car_handle(int64_t state) {
@@ -1023,7 +1023,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits) -> int", &gguf_gemm_parts);
   m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
   m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits) -> int", &qmoe_gemm);
-  m.def("car_create(int rank, int world, int max_bytes) -> int", &car_create);
+  m.def("car_create(int rank, int world, int max_bytes, int nb_large=512) -> int", &car_create);
   m.def("car_handle(int state) -> Tensor", &car_handle);
   m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);
   m.def("car_all_reduce(int state, Tensor inp, Tensor(a!) out, bool two_shot) -> ()", &car_all_reduce);

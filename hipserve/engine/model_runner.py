@@ -11,6 +11,7 @@ SURVEY §3.B step 4); prefill / mixed batches run eagerly.
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 import time
@@ -26,6 +27,7 @@ from ..parallel.comm import TPGroup
 from ..runtime import native
 from .scheduler import SchedulerOutput
 
+log = logging.getLogger("hipserve.runner")
 PREFILL_TILE = 128
 TOP_LOGPROBS = 20   # per-row capacity of the device top-logprobs output (OpenAI max)
 GRAPH_BUCKETS = [1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 448, 512]
@@ -154,13 +156,20 @@ class ModelRunner:
             shapes = [s for s in self.model.gemm_shapes() if s != tuple(getattr(self.model.lm_head, "shape", ()))]
             self.prefill_gemm_report = prefill_tune.tune(shapes, [ecfg.max_num_batched_tokens], self.device)
             torch.cuda.empty_cache()
+        # prefill GEMMs: the hand-written kernel with fused epilogues where it beats
+        # hipBLASLt + the separate elementwise kernel (ops/pgemm.py), timed per shape
+        self.pgemm_report = []
+        if self.device.type == "cuda" and ecfg.extra.get("prefill_gemm", True):
+            self.pgemm_report = self._tune_prefill_gemm()
         # ragged prefill chunks: hipBLASLt's heuristic picks slower kernels for some
         # token counts (Llama-3-8B: the 4-projection chain takes 21.7 ms at 7,393 rows
         # vs 18.8 ms at 8,192, tools/bench_prefill_m.py); rank 0 times the model's
         # prefill GEMMs per 256-row count once and pads a chunk to the fastest count at
         # or above it (padding rows: token 0, no KV write, outputs unused)
         self.prefill_pad = None
-        if (self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0):
+        pg_all = bool(self.pgemm_report) and all(r["pgemm"] for r in self.pgemm_report)
+        if (self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0
+                and not pg_all):  # the hand-written GEMM has no row-count cliffs
             self.prefill_pad = self._probe_prefill_pad()
         # device penalty state: one slot per concurrently running sequence (a slot is
         # held from the first sample to finish / abort / preemption), so a slot is
@@ -247,6 +256,39 @@ class ModelRunner:
         return self.tp.min_int(n)
 
     @torch.inference_mode()
+    def _tune_prefill_gemm(self) -> list[dict]:
+        from ..ops import pgemm
+
+        layers = getattr(self.model, "layers", None)
+        if pgemm.MODE == "0" or not layers:
+            return []
+        lw = layers[0]
+        units = set()
+        for kind, w in (("plain", lw.wqkv), ("add", lw.wo), ("glu", lw.wgu), ("add", lw.wd)):
+            if not pgemm.fits(w):
+                continue
+            if kind == "add" and (self.tp.world_size > 1 or getattr(lw, "post_attn_norm", None) is not None):
+                continue
+            if kind == "glu" and (self.mcfg.hidden_act != "silu" or w.shape[0] % 256):
+                continue
+            units.add((kind, w.shape[0], w.shape[1]))
+        if not units:
+            return []
+        M = min(self.ecfg.max_num_batched_tokens, 8192)
+        if M < pgemm.MIN_ROWS:
+            return []
+        rep = pgemm.tune(units, M, self.device, self.ops)
+        if any(k == "glu" and v for (k, _, _), v in pgemm.CHOICE.items()):
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            for l in layers:  # GLU-row copies of the merged gate|up weights (prefill only)
+                w = l.wgu
+                free, _ = torch.cuda.mem_get_info(self.device)
+                if free - w.numel() * w.element_size() < (24 << 30) + total // 4:
+                    log.warning("prefill GLU weights not packed: HBM reserve reached")
+                    break
+                pgemm.register_glu(w)
+        return rep
+
     def _probe_prefill_pad(self) -> dict | None:
         """{rows rounded up to 256: the row count (>= it, <= the token budget) whose
         prefill GEMM chain (qkv, o, gate|up, down of one layer, hipBLASLt) is fastest};

@@ -28,7 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from ..config import ModelConfig
-from ..ops import gemm
+from ..ops import gemm, pgemm
 from ..ops import reference as ref
 from ..parallel.comm import TPGroup
 
@@ -523,8 +523,11 @@ class LlamaModel:
             part, tmp_out, tmp_ml = self._decode_split(Td, meta)
         ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
         L = len(self.layers)
+        tp1 = self.tp.world_size == 1
         for i, lw in enumerate(self.layers):
-            qkv = self.linear(xn, lw.wqkv)
+            # prefill-sized batches: the hand-written GEMM where start-up timing chose it
+            # (ops/pgemm.py), with the residual add / SiLU-GLU in its epilogue
+            qkv = pgemm.gemm(xn, lw.wqkv) if pgemm.use("plain", lw.wqkv, T) else self.linear(xn, lw.wqkv)
             if lw.bqkv is not None:
                 qkv += lw.bqkv
             if lw.q_norm is not None:  # per-head RMSNorm of q and k, before RoPE
@@ -539,21 +542,33 @@ class LlamaModel:
             if Td:  # rows past Tp + Td: prefill padding (model_runner._pad_rows)
                 ops.paged_decode(attn[Tp:Tp + Td], qkv[Tp:Tp + Td], kc, vc, meta.bt_decode, meta.ctx_decode,
                                  tmp_out, tmp_ml, nq, nkv, part, self.scale, win)
-            o = self.linear_rowpar(attn, lw.wo)
-            if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)
-                o = self._tp_sum(o, xn)
-                ops.rmsnorm(o, o, lw.post_attn_norm, eps)
-                ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
+            if tp1 and lw.post_attn_norm is None and pgemm.use("add", lw.wo, T):
+                pgemm.gemm_add_(residual, attn, lw.wo)  # residual += o_proj(attn), in the GEMM epilogue
+                ops.rmsnorm(xn, residual, lw.ln2, eps)
             else:
-                self.add_rmsnorm(xn, residual, o, 1, lw.ln2)
+                o = self.linear_rowpar(attn, lw.wo)
+                if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)
+                    o = self._tp_sum(o, xn)
+                    ops.rmsnorm(o, o, lw.post_attn_norm, eps)
+                    ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
+                else:
+                    self.add_rmsnorm(xn, residual, o, 1, lw.ln2)
+            nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             if lw.router is not None:
                 h = self.moe(xn, lw)
             else:
-                gu = self.linear(xn, lw.wgu)
-                act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
-                self.act_and_mul(act, gu)
+                act = (pgemm.gemm_glu(xn, lw.wgu) if cfg.hidden_act == "silu" and pgemm.use("glu", lw.wgu, T)
+                       else None)
+                if act is None:
+                    gu = self.linear(xn, lw.wgu)
+                    act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
+                    self.act_and_mul(act, gu)
+                if (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
+                        and pgemm.use("add", lw.wd, T)):
+                    pgemm.gemm_add_(residual, act, lw.wd)
+                    ops.rmsnorm(xn, residual, nxt, eps)
+                    continue
                 h = self.linear_rowpar(act, lw.wd)
-            nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             if ds is not None and i < len(ds) and self.tp.rank == 0:
                 # DeepStack: visual features join the residual stream after layer i
                 # (rank 0 only: the row-parallel partials are summed across ranks next)

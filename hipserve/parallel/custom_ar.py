@@ -41,6 +41,15 @@ ONE_SHOT_MAX = int(os.environ.get("HIPSERVE_CAR_ONE_SHOT_MAX", 256 << 10))
 DEFAULT_MAX_BYTES = int(os.environ.get("HIPSERVE_CAR_MAX_BYTES", 8 << 20))
 
 
+def _device_id(device) -> tuple:
+    import socket
+
+    p = torch.cuda.get_device_properties(device)
+    uid = getattr(p, "uuid", None)
+    return (socket.gethostname(), str(uid) if uid is not None else
+            (getattr(p, "pci_bus_id", None), getattr(p, "pci_device_id", None), device.index))
+
+
 class CollectiveError(RuntimeError):
     """A custom collective timed out on some rank (a peer died or hung)."""
 
@@ -52,8 +61,15 @@ class CustomAllReduce:
         load_library()
         self.op = torch.ops.hipserve
         self.rank, self.world, self.device = rank, world, device
+        # ranks sharing this GPU (the 1-GPU test box runs a TP group on one device):
+        # every block of every sharing rank's collective must be resident at once, so
+        # the prefill-sized class gets a smaller grid (<= 1024 blocks per device)
+        ids = [None] * world
+        dist.all_gather_object(ids, _device_id(device), group=cpu_group)
+        self.ranks_per_device = sum(1 for d in ids if d == ids[rank])
+        self.nb_large = max(64, min(512, 1024 // self.ranks_per_device))
         with torch.cuda.device(device):
-            self.state = int(self.op.car_create(rank, world, max_bytes))
+            self.state = int(self.op.car_create(rank, world, max_bytes, self.nb_large))
             self.max_bytes = max_bytes
             mine = self.op.car_handle(self.state)
         handles = [None] * world

