@@ -186,7 +186,7 @@ bool launch_dgf(int fix, bool norm_in, const DgfArgs& A, const void* x, long x_s
 //   PG_EPI_GLU    B packed by launch_pack_glu_rows; C = act [M, N/2] = silu(gate) * up
 constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2;
 struct PgEpi {
-  int unused;
+  int variant;  // 1: one-stage-ahead loop, 2: half-tile pipeline (default)
 };
 bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
                          int K, const PgEpi& E, hipStream_t s);

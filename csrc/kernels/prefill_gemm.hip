@@ -29,6 +29,76 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int PG_BM = 256, PG_BN = 256, PG_BK = 64, PG_T = 512;
 constexpr int PG_TILE = PG_BM * PG_BK * 2;  // bytes of one operand tile per stage
 
+// Epilogue of a 256 x 256 tile: lane holds C[m][n .. n+3] for m = m0 + 128 wr + 16 i + fr,
+// n = n0 + 64 wc + 16 j + 4 fq (acc[j][i]). Uses the whole LDS array (GLU exchange).
+template <int EPI>
+HS_DEVICE void pg_epilogue(f32x4 (&acc)[4][8], unsigned char* lds, unsigned short* __restrict__ C, long ldc, int M,
+                           int m0, int n0, int tn, int wr, int wc, int fr, int fq, int lane) {
+  if constexpr (EPI == PG_EPI_STORE || EPI == PG_EPI_ADD) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wr * 128 + i * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wc * 64 + j * 16 + 4 * fq;
+        uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n);
+        uint2 v;
+        if constexpr (EPI == PG_EPI_ADD) {  // C is the residual: C = bf16(bf16(acc) + C)
+          const uint2 r = *dst;
+          const unsigned short rr[4] = {(unsigned short)(r.x & 0xffff), (unsigned short)(r.x >> 16),
+                                        (unsigned short)(r.y & 0xffff), (unsigned short)(r.y >> 16)};
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = bf16_to_f32(f32_to_bf16(acc[j][i][e])) + bf16_to_f32(rr[e]);
+          v.x = pack_bf16x2(o[0], o[1]);
+          v.y = pack_bf16x2(o[2], o[3]);
+        } else {
+          v.x = pack_bf16x2(acc[j][i][0], acc[j][i][1]);
+          v.y = pack_bf16x2(acc[j][i][2], acc[j][i][3]);
+        }
+        *dst = v;
+      }
+    }
+  } else if constexpr (EPI == PG_EPI_GLU) {
+    // B rows interleaved per 256-row tile: 128 gate rows then their 128 up rows
+    // (pack_glu_rows). Waves wc = 2, 3 hand their bf16-rounded up values to the
+    // gate waves wc = 0, 1 through LDS; act[m, 128 tn + c] = silu(gate) * up.
+    float* ex = reinterpret_cast<float*>(lds);  // [2 wr][2 wc-1][8 i][4 j][64 lanes][4] fp32 = 128 KiB
+    if (wc >= 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = bf16_to_f32(f32_to_bf16(acc[j][i][e]));
+          *reinterpret_cast<f32x4*>(ex + ((((wr * 2 + (wc - 2)) * 8 + i) * 4 + j) * 64 + lane) * 4) = v;
+        }
+    }
+    __syncthreads();
+    if (wc < 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wr * 128 + i * 16 + fr;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 u = *reinterpret_cast<const f32x4*>(ex + ((((wr * 2 + wc) * 8 + i) * 4 + j) * 64 + lane) * 4);
+          unsigned short o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = silu_mul1(f32_to_bf16(acc[j][i][e]), f32_to_bf16(u[e]));
+          uint2 v;
+          v.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+          v.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+          const int c = tn * 128 + wc * 64 + j * 16 + 4 * fq;
+          *reinterpret_cast<uint2*>(C + (long)m * ldc + c) = v;
+        }
+      }
+    }
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(PG_T) void pgemm_kernel(const unsigned short* __restrict__ A, long lda,
                                                      const unsigned short* __restrict__ B, long ldb,
@@ -101,70 +171,126 @@ __global__ __launch_bounds__(PG_T) void pgemm_kernel(const unsigned short* __res
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds C[m][n .. n+3] for m = m0 + 128 wr + 16 i + fr, n = n0 + 64 wc + 16 j + 4 fq
-  if constexpr (EPI == PG_EPI_STORE || EPI == PG_EPI_ADD) {
+  pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
+}
+
+// ---- v2: half-tile pipeline. Each K tile runs as 4 phases (one 64 x 32 output
+// quadrant of the wave's 128 x 64 block per phase: 16 MFMAs), separated by raw
+// s_barriers. The LDS halves are freed in phase order — A rows of quadrant-row 0
+// after phase 1, B columns of quadrant-column 0 after phase 2, the other halves
+// after phase 3 — and each is restaged as soon as it is free: tile kt+2's A-half0
+// in phase 2 and B-half0 in phase 3 (same stage as tile kt), tile kt+1's A-half1 /
+// B-half1 in phase 0 (other stage). One counted wait per tile (vmcnt(4) at the end of
+// phase 3: tile kt+1 complete, tile kt+2's first two halves still in flight) keeps
+// LDS-DMA traffic going across every barrier (cdna_hip_programming.md §5 T3/T4).
+template <int EPI>
+__global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __restrict__ A, long lda,
+                                                      const unsigned short* __restrict__ B, long ldb,
+                                                      unsigned short* __restrict__ C, long ldc, int M, int N, int K,
+                                                      int tiles_m, int tiles_n, PgEpi E) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * PG_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
+  const int m0 = tm * PG_BM, n0 = tn * PG_BN;
+  const int nk = K / PG_BK;
+
+  // half-tile staging: wave w moves half rows [16w, 16w + 16) in 2 instructions of 8 rows
+  const unsigned short* src[2][2][2];  // [operand A/B][half][instr]
+  int dst[2][2][2];                    // LDS byte offset inside a stage
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wr * 128 + i * 16 + fr;
-      if (m >= M) continue;
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wc * 64 + j * 16 + 4 * fq;
-        uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n);
-        uint2 v;
-        if constexpr (EPI == PG_EPI_ADD) {  // C is the residual: C = bf16(bf16(acc) + C)
-          const uint2 r = *dst;
-          const unsigned short rr[4] = {(unsigned short)(r.x & 0xffff), (unsigned short)(r.x >> 16),
-                                        (unsigned short)(r.y & 0xffff), (unsigned short)(r.y >> 16)};
-          float o[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = bf16_to_f32(f32_to_bf16(acc[j][i][e])) + bf16_to_f32(rr[e]);
-          v.x = pack_bf16x2(o[0], o[1]);
-          v.y = pack_bf16x2(o[2], o[3]);
-        } else {
-          v.x = pack_bf16x2(acc[j][i][0], acc[j][i][1]);
-          v.y = pack_bf16x2(acc[j][i][2], acc[j][i][3]);
-        }
-        *dst = v;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int j0 = wave * 16 + i * 8, j = j0 + (lane >> 3);
+      const int ra0 = (j0 >> 6) * 128 + h * 64 + (j0 & 63), ra = (j >> 6) * 128 + h * 64 + (j & 63);
+      const int rb0 = (j0 >> 5) * 64 + h * 32 + (j0 & 31), rb = (j >> 5) * 64 + h * 32 + (j & 31);
+      src[0][h][i] = A + (long)min(m0 + ra, M - 1) * lda + ((lane & 7) ^ ((ra >> 1) & 7)) * 8;
+      src[1][h][i] = B + (long)min(n0 + rb, N - 1) * ldb + ((lane & 7) ^ ((rb >> 1) & 7)) * 8;
+      dst[0][h][i] = ra0 * 128;
+      dst[1][h][i] = PG_TILE + rb0 * 128;
     }
-  } else if constexpr (EPI == PG_EPI_GLU) {
-    // B rows interleaved per 256-row tile: 128 gate rows then their 128 up rows
-    // (pack_glu_rows). Waves wc = 2, 3 hand their bf16-rounded up values to the
-    // gate waves wc = 0, 1 through LDS; act[m, 128 tn + c] = silu(gate) * up.
-    float* ex = reinterpret_cast<float*>(lds);  // [2 wr][2 wc-1][8 i][4 j][64 lanes][4] fp32 = 128 KiB
-    if (wc >= 2) {
+  auto stage_half = [&](int op, int h, int buf, int kt) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[op][h][i] + kt * PG_BK),
+                                       (lds_ptr_t)(lds + buf * 2 * PG_TILE + dst[op][h][i]), 16, 0, 0);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fr >> 1) & 7;
+  const int a_off = (wr * 128 + fr) * 128, b_off = PG_TILE + (wc * 64 + fr) * 128;
+  const int chs[2] = {((0 + fq) ^ sw) * 16, ((4 + fq) ^ sw) * 16};
+
+  f32x4 acc[4][8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f32x4 v;
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = bf16_to_f32(f32_to_bf16(acc[j][i][e]));
-          *reinterpret_cast<f32x4*>(ex + ((((wr * 2 + (wc - 2)) * 8 + i) * 4 + j) * 64 + lane) * 4) = v;
-        }
-    }
-    __syncthreads();
-    if (wc < 2) {
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tile 0 whole, tile 1's A-half0 / B-half0; wait for tile 0
+  stage_half(0, 0, 0, 0);
+  stage_half(1, 0, 0, 0);
+  stage_half(0, 1, 0, 0);
+  stage_half(1, 1, 0, 0);
+  if (nk > 1) {
+    stage_half(0, 0, 1, 1);
+    stage_half(1, 0, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  u16x8 bfr[4][2], afr[4][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const unsigned char* sb = lds + buf * 2 * PG_TILE;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + wr * 128 + i * 16 + fr;
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 u = *reinterpret_cast<const f32x4*>(ex + ((((wr * 2 + wc) * 8 + i) * 4 + j) * 64 + lane) * 4);
-          unsigned short o[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = silu_mul1(f32_to_bf16(acc[j][i][e]), f32_to_bf16(u[e]));
-          uint2 v;
-          v.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
-          v.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-          const int c = tn * 128 + wc * 64 + j * 16 + 4 * fq;
-          *reinterpret_cast<uint2*>(C + (long)m * ldc + c) = v;
-        }
+    for (int p = 0; p < 4; ++p) {
+      const int qm = p >> 1, qn = p & 1;
+      if (p == 0 && kt + 1 < nk) {
+        stage_half(0, 1, buf ^ 1, kt + 1);
+        stage_half(1, 1, buf ^ 1, kt + 1);
       }
+      if (p == 2 && kt + 2 < nk) stage_half(0, 0, buf, kt + 2);
+      if (p == 3 && kt + 2 < nk) stage_half(1, 0, buf, kt + 2);
+      if (p == 0 || p == 1) {  // B columns of quadrant-column qn (kept for phases 2, 3)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            bfr[2 * qn + jj][s2] = *reinterpret_cast<const u16x8*>(sb + b_off + (2 * qn + jj) * 2048 + chs[s2]);
+      }
+      if (p == 0 || p == 2) {  // A rows of quadrant-row qm
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            afr[ii][s2] = *reinterpret_cast<const u16x8*>(sb + a_off + (4 * qm + ii) * 2048 + chs[s2]);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+            acc[2 * qn + jj][4 * qm + ii] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, bfr[2 * qn + jj][s2]), __builtin_bit_cast(bf16x8, afr[ii][s2]),
+                acc[2 * qn + jj][4 * qm + ii], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (p == 3) {  // tile kt+1 complete (kt+2's first halves may stay in flight)
+        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
   }
+  pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
 }
 
 static bool pg_shape_ok(int M, int N, int K) { return M >= 1 && N % PG_BN == 0 && K % PG_BK == 0 && K >= PG_BK; }
@@ -177,6 +303,14 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
   auto* a = static_cast<const unsigned short*>(A);
   auto* b = static_cast<const unsigned short*>(B);
   auto* c = static_cast<unsigned short*>(C);
+  if (E.variant == 2) {
+    switch (epi) {
+      case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_ADD: pgemm2_kernel<PG_EPI_ADD><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      default: return false;
+    }
+  }
   switch (epi) {
     case PG_EPI_STORE: pgemm_kernel<PG_EPI_STORE><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
     case PG_EPI_ADD: pgemm_kernel<PG_EPI_ADD><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;

@@ -656,7 +656,7 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
 // Prefill GEMM (prefill_gemm.hip): out = x @ w^T with a fused epilogue.
 // epi 0: out [M, N] bf16; 1: out is the residual [M, N], out = bf16(bf16(x w^T) + out);
 // 2: w packed by pack_glu_rows, out = act [M, N/2].
-void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t epi) {
+void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t epi, int64_t variant) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w);
   CHECK_ROWMAJOR(out);
   const int M = x.size(0), K = x.size(1), N = w.size(0);
@@ -665,6 +665,7 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
   TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm: out shape");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::PgEpi E{};
+  E.variant = (int)variant;
   TORCH_CHECK(hipserve::launch_prefill_gemm((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
                                             w.data_ptr(), w.stride(0), M, N, K, E, cur_stream()),
               "prefill_gemm: unsupported");
@@ -1039,7 +1040,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
-  m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi) -> ()");
+  m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
         "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "

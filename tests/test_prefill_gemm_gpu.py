@@ -16,12 +16,13 @@ def _rnd(g, *s, scale=1.0):
     return ((torch.rand(*s, device=DEV, generator=g) * 2 - 1) * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("M,N,K", SHAPES)
-def test_prefill_gemm_store(M, N, K):
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("M,N,K", SHAPES + [(512, 256, 128), (700, 512, 192)])
+def test_prefill_gemm_store(M, N, K, variant):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
     out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm(out, x, w, 0)
+    torch.ops.hipserve.prefill_gemm(out, x, w, 0, variant)
     want = x.float() @ w.float().t()
     torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 

@@ -60,8 +60,10 @@ def main():
         ws = [rnd(N, K) * 0.05 for _ in range(L)]
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         t_blas = time_fn(lambda: [F.linear(x, w) for w in ws])
-        t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0) for w in ws])
+        t_v1 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 1) for w in ws])
+        t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 2) for w in ws])
         r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
+             "pgemm_v1_ms": round(t_v1, 4),
              "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1)}
         if name == "gu":  # GEMM + SiLU-GLU unit
             act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
