@@ -120,8 +120,11 @@ class LlamaModel:
     fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "0") == "1"
     # fused decode layer v2 (csrc/kernels/decode_layer.hip): the split-K fix-up and
     # the layer epilogue inside each decode GEMM launch, RMSNorm applied on load —
-    # five kernels per Llama layer instead of eight (TP = 1 dense families)
-    fused_v2 = os.environ.get("HIPSERVE_FUSED_V2", "1") == "1"
+    # five kernels per Llama layer instead of eight (TP = 1 dense families). Opt-in:
+    # the first end-to-end run was SLOWER (6,398 vs 7,650 tok/s): an in-launch split-K
+    # seam (agent release per slice + last-arriver slab reads) costs more than the
+    # kernel boundary + epilogue kernel it replaces (profiles/r3_decode_v2_ab.md)
+    fused_v2 = os.environ.get("HIPSERVE_FUSED_V2", "0") == "1"
 
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,
                  max_pos: int | None = None):

@@ -182,6 +182,7 @@ def test_forward_v2_vs_v1(ops, family, B):
         mk = lambda: AttnMeta(num_prefill_tokens=0, num_decode=B, positions=pos, slot_mapping=slots,
                               bt_decode=bt, ctx_decode=ctx, tmp_out=torch.empty(B, m.nq, parts, D, device=DEV),
                               tmp_ml=torch.empty(B, m.nq, parts, 2, device=DEV))
+        m.fused_v2 = True
         assert m.v2_plan(B, mk()) is not None
         m.fused_v2 = False
         out1 = m.forward(ids, mk(), kv1).clone()
@@ -211,4 +212,4 @@ def test_forward_v2_vs_v1(ops, family, B):
     finally:
         gemm.TUNER.table.clear()
         gemm.TUNER.table.update(old)
-        m.fused_v2 = True
+        m.fused_v2 = type(m).fused_v2
