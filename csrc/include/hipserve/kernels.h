@@ -183,10 +183,12 @@ bool launch_dgf(int fix, bool norm_in, const DgfArgs& A, const void* x, long x_s
 // staging), N % 256 == 0, K % 64 == 0, any M. Epilogues:
 //   PG_EPI_STORE  C = bf16(acc)
 //   PG_EPI_ADD    C (the residual, in place) = bf16(bf16(acc) + C)
-//   PG_EPI_GLU    B packed by launch_pack_glu_rows; C = act [M, N/2] = silu(gate) * up
+//   PG_EPI_GLU    B = the merged [gate; up] weight (N = 2I, I % 128 == 0); C = act [M, I] = silu(gate) * up
 constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2;
 struct PgEpi {
-  int variant;  // 1: one-stage-ahead loop, 2: half-tile pipeline (default)
+  int variant;               // 1: one-stage-ahead loop, 2: half-tile pipeline (default)
+  const int* tile_expert;    // grouped (MoE): expert of each 256-row tile of A, -1 = unused
+  long b_estride;            // grouped: elements between consecutive experts' weights
 };
 bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
                          int K, const PgEpi& E, hipStream_t s);

@@ -29,6 +29,15 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int PG_BM = 256, PG_BN = 256, PG_BK = 64, PG_T = 512;
 constexpr int PG_TILE = PG_BM * PG_BK * 2;  // bytes of one operand tile per stage
 
+// Global weight row of row r of the tile's B panel. GLU: the merged [gate; up] weight
+// (2I rows) is read in its own layout, tile tn taking gate rows 128 tn .. + 127 then
+// the matching up rows I + 128 tn .. + 127 — no repacked copy of the weight.
+template <int EPI>
+HS_DEVICE int pg_brow(int n0, int tn, int r, int N) {
+  if constexpr (EPI == PG_EPI_GLU) return r < 128 ? tn * 128 + r : (N >> 1) + tn * 128 + (r - 128);
+  return min(n0 + r, N - 1);
+}
+
 // Epilogue of a 256 x 256 tile: lane holds C[m][n .. n+3] for m = m0 + 128 wr + 16 i + fr,
 // n = n0 + 64 wc + 16 j + 4 fq (acc[j][i]). Uses the whole LDS array (GLU exchange).
 template <int EPI>
@@ -61,8 +70,8 @@ HS_DEVICE void pg_epilogue(f32x4 (&acc)[4][8], unsigned char* lds, unsigned shor
       }
     }
   } else if constexpr (EPI == PG_EPI_GLU) {
-    // B rows interleaved per 256-row tile: 128 gate rows then their 128 up rows
-    // (pack_glu_rows). Waves wc = 2, 3 hand their bf16-rounded up values to the
+    // tile columns 0..127 = gate rows, 128..255 = the matching up rows (pg_brow).
+    // Waves wc = 2, 3 hand their bf16-rounded up values to the
     // gate waves wc = 0, 1 through LDS; act[m, 128 tn + c] = silu(gate) * up.
     float* ex = reinterpret_cast<float*>(lds);  // [2 wr][2 wc-1][8 i][4 j][64 lanes][4] fp32 = 128 KiB
     if (wc >= 2) {
@@ -120,7 +129,7 @@ __global__ __launch_bounds__(PG_T) void pgemm_kernel(const unsigned short* __res
     const int r = wave * 32 + i * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at physical chunk lane & 7
     asrc[i] = A + (long)min(m0 + r, M - 1) * lda + lc * 8;
-    bsrc[i] = B + (long)min(n0 + r, N - 1) * ldb + lc * 8;
+    bsrc[i] = B + (long)pg_brow<EPI>(n0, tn, r, N) * ldb + lc * 8;
   }
   auto stage = [&](int buf, int kt) {
     unsigned char* base = lds + buf * 2 * PG_TILE;
@@ -183,7 +192,11 @@ __global__ __launch_bounds__(PG_T) void pgemm_kernel(const unsigned short* __res
 // B-half1 in phase 0 (other stage). One counted wait per tile (vmcnt(4) at the end of
 // phase 3: tile kt+1 complete, tile kt+2's first two halves still in flight) keeps
 // LDS-DMA traffic going across every barrier (cdna_hip_programming.md §5 T3/T4).
-template <int EPI>
+// kGroup (MoE prefill experts): A rows are expert-sorted and padded to 256-row tiles
+// (moe_align with tile 256); tile_expert[tm] names the expert whose weight
+// (B + e * b_estride) the m-tile multiplies, -1 = unused tile. Device-side offsets:
+// no host round trip, graph-capturable.
+template <int EPI, bool kGroup>
 __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __restrict__ A, long lda,
                                                       const unsigned short* __restrict__ B, long ldb,
                                                       unsigned short* __restrict__ C, long ldc, int M, int N, int K,
@@ -194,6 +207,11 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
   const int m0 = tm * PG_BM, n0 = tn * PG_BN;
+  if constexpr (kGroup) {
+    const int e = E.tile_expert[tm];
+    if (e < 0) return;
+    B += (long)e * E.b_estride;
+  }
   const int nk = K / PG_BK;
 
   // half-tile staging: wave w moves half rows [16w, 16w + 16) in 2 instructions of 8 rows
@@ -207,7 +225,7 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
       const int ra0 = (j0 >> 6) * 128 + h * 64 + (j0 & 63), ra = (j >> 6) * 128 + h * 64 + (j & 63);
       const int rb0 = (j0 >> 5) * 64 + h * 32 + (j0 & 31), rb = (j >> 5) * 64 + h * 32 + (j & 31);
       src[0][h][i] = A + (long)min(m0 + ra, M - 1) * lda + ((lane & 7) ^ ((ra >> 1) & 7)) * 8;
-      src[1][h][i] = B + (long)min(n0 + rb, N - 1) * ldb + ((lane & 7) ^ ((rb >> 1) & 7)) * 8;
+      src[1][h][i] = B + (long)pg_brow<EPI>(n0, tn, rb, N) * ldb + ((lane & 7) ^ ((rb >> 1) & 7)) * 8;
       dst[0][h][i] = ra0 * 128;
       dst[1][h][i] = PG_TILE + rb0 * 128;
     }
@@ -243,44 +261,58 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  u16x8 bfr[4][2], afr[4][2];
+  // fragments: B for all 4 n-frags (phases 0 / 1 read them), A for both quadrant rows
+  // (qm 0 read in phase 0, qm 1 prefetched in phase 1 behind phase 1's MFMAs), so
+  // only phase 0's reads are exposed at a tile's start
+  u16x8 bfr[4][2], afr[2][4][2];
+  auto read_b = [&](const unsigned char* sb, int qn) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        bfr[2 * qn + jj][s2] = *reinterpret_cast<const u16x8*>(sb + b_off + (2 * qn + jj) * 2048 + chs[s2]);
+  };
+  auto read_a = [&](const unsigned char* sb, int qm) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        afr[qm][ii][s2] = *reinterpret_cast<const u16x8*>(sb + a_off + (4 * qm + ii) * 2048 + chs[s2]);
+  };
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const unsigned char* sb = lds + buf * 2 * PG_TILE;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int qm = p >> 1, qn = p & 1;
+      if (p == 0) {
+        read_a(sb, 0);
+        read_b(sb, 0);
+      }
       if (p == 0 && kt + 1 < nk) {
         stage_half(0, 1, buf ^ 1, kt + 1);
         stage_half(1, 1, buf ^ 1, kt + 1);
       }
       if (p == 2 && kt + 2 < nk) stage_half(0, 0, buf, kt + 2);
       if (p == 3 && kt + 2 < nk) stage_half(1, 0, buf, kt + 2);
-      if (p == 0 || p == 1) {  // B columns of quadrant-column qn (kept for phases 2, 3)
+      if (p == 1) read_a(sb, 1);  // for phases 2, 3, behind phase 1's MFMAs
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-            bfr[2 * qn + jj][s2] = *reinterpret_cast<const u16x8*>(sb + b_off + (2 * qn + jj) * 2048 + chs[s2]);
-      }
-      if (p == 0 || p == 2) {  // A rows of quadrant-row qm
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-            afr[ii][s2] = *reinterpret_cast<const u16x8*>(sb + a_off + (4 * qm + ii) * 2048 + chs[s2]);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < 2; ++s2) {
+        if (p == 0 && s2 == 1) {  // B for phase 1, behind the first half of phase 0's MFMAs
+          __builtin_amdgcn_sched_barrier(0);
+          read_b(sb, 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
           for (int ii = 0; ii < 4; ++ii)
             acc[2 * qn + jj][4 * qm + ii] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, bfr[2 * qn + jj][s2]), __builtin_bit_cast(bf16x8, afr[ii][s2]),
+                __builtin_bit_cast(bf16x8, bfr[2 * qn + jj][s2]), __builtin_bit_cast(bf16x8, afr[qm][ii][s2]),
                 acc[2 * qn + jj][4 * qm + ii], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
+      }
       if (p == 3) {  // tile kt+1 complete (kt+2's first halves may stay in flight)
         if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -303,11 +335,18 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
   auto* a = static_cast<const unsigned short*>(A);
   auto* b = static_cast<const unsigned short*>(B);
   auto* c = static_cast<unsigned short*>(C);
+  if (E.tile_expert != nullptr) {  // grouped (MoE experts): M = tiles_cap * 256 slot rows
+    switch (epi) {
+      case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, true><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, true><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      default: return false;
+    }
+  }
   if (E.variant == 2) {
     switch (epi) {
-      case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_ADD: pgemm2_kernel<PG_EPI_ADD><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_ADD: pgemm2_kernel<PG_EPI_ADD, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       default: return false;
     }
   }

@@ -655,7 +655,7 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
 
 // Prefill GEMM (prefill_gemm.hip): out = x @ w^T with a fused epilogue.
 // epi 0: out [M, N] bf16; 1: out is the residual [M, N], out = bf16(bf16(x w^T) + out);
-// 2: w packed by pack_glu_rows, out = act [M, N/2].
+// 2: w = merged [gate; up] (N = 2I, I % 128 == 0), out = act [M, I] = silu(gate) * up.
 void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t epi, int64_t variant) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w);
   CHECK_ROWMAJOR(out);
@@ -663,6 +663,7 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
   TORCH_CHECK(w.size(1) == K && N % 256 == 0 && K % 64 == 0, "prefill_gemm: w [N % 256, K % 64]");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "prefill_gemm: alignment");
   TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm: out shape");
+  TORCH_CHECK(epi != 2 || (N / 2) % 128 == 0, "prefill_gemm: GLU needs I % 128 == 0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::PgEpi E{};
   E.variant = (int)variant;
@@ -671,12 +672,38 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
               "prefill_gemm: unsupported");
 }
 
+// Grouped (MoE prefill) form: x [tiles * 256, K] expert-sorted rows (moe_align with
+// tile 256, moe_gather), w [E, N, K] (GLU: each expert's merged [gate; up] weight),
+// tile_expert [tiles] int32 from moe_align. No host synchronisation.
+void prefill_gemm_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& tile_expert,
+                          int64_t epi) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_CONTIG(w);
+  CHECK_ROWMAJOR(out); CHECK_CONTIG(tile_expert);
+  TORCH_CHECK(w.dim() == 3 && tile_expert.scalar_type() == at::kInt, "prefill_gemm_grouped: w [E, N, K], int32 tiles");
+  const int M = x.size(0), K = x.size(1), N = w.size(1);
+  TORCH_CHECK(w.size(2) == K && N % 256 == 0 && K % 64 == 0 && M == tile_expert.numel() * 256,
+              "prefill_gemm_grouped: x rows = 256 * tiles, w [E, N % 256, K % 64]");
+  TORCH_CHECK(epi == 0 || epi == 2, "prefill_gemm_grouped: store or glu epilogue");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm_grouped: out shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::PgEpi E{};
+  E.variant = 2;
+  E.tile_expert = tile_expert.data_ptr<int>();
+  E.b_estride = (long)N * K;
+  TORCH_CHECK(hipserve::launch_prefill_gemm((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
+                                            w.data_ptr(), K, M, N, K, E, cur_stream()),
+              "prefill_gemm_grouped: unsupported");
+}
+
 void pack_glu_rows(at::Tensor& out, const at::Tensor& w) {
   CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
-  const int N = w.size(0), K = w.size(1);
-  TORCH_CHECK(N % 256 == 0 && K % 8 == 0 && out.numel() == w.numel(), "pack_glu_rows: [2I % 256, K]");
+  const int N = w.size(-2), K = w.size(-1);
+  const long E = w.dim() == 3 ? w.size(0) : 1;  // [E, 2I, K]: every expert's matrix
+  TORCH_CHECK(N % 256 == 0 && K % 8 == 0 && out.numel() == w.numel(), "pack_glu_rows: [(E,) 2I % 256, K]");
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
-  hipserve::launch_pack_glu_rows(out.data_ptr(), w.data_ptr(), N / 2, K, cur_stream());
+  for (long e = 0; e < E; ++e)
+    hipserve::launch_pack_glu_rows(static_cast<unsigned short*>(out.data_ptr()) + e * N * K,
+                                   static_cast<const unsigned short*>(w.data_ptr()) + e * N * K, N / 2, K, cur_stream());
 }
 
 // Fused decode layer v2 (decode_layer.hip): one packed decode GEMM whose split-K
@@ -1042,6 +1069,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
+  m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
         "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
         "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
@@ -1090,6 +1118,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm_fused", &decode_gemm_fused);
   m.impl("prefill_gemm", &prefill_gemm);
   m.impl("pack_glu_rows", &pack_glu_rows);
+  m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.impl("splitk_rope_cache", &splitk_rope_cache);
   m.impl("splitk_glu", &splitk_glu);

@@ -269,7 +269,7 @@ class ModelRunner:
                 continue
             if kind == "add" and (self.tp.world_size > 1 or getattr(lw, "post_attn_norm", None) is not None):
                 continue
-            if kind == "glu" and (self.mcfg.hidden_act != "silu" or w.shape[0] % 256):
+            if kind == "glu" and (self.mcfg.hidden_act != "silu" or (w.shape[0] // 2) % 128):
                 continue
             units.add((kind, w.shape[0], w.shape[1]))
         if not units:
@@ -277,17 +277,7 @@ class ModelRunner:
         M = min(self.ecfg.max_num_batched_tokens, 8192)
         if M < pgemm.MIN_ROWS:
             return []
-        rep = pgemm.tune(units, M, self.device, self.ops)
-        if any(k == "glu" and v for (k, _, _), v in pgemm.CHOICE.items()):
-            total = torch.cuda.get_device_properties(self.device).total_memory
-            for l in layers:  # GLU-row copies of the merged gate|up weights (prefill only)
-                w = l.wgu
-                free, _ = torch.cuda.mem_get_info(self.device)
-                if free - w.numel() * w.element_size() < (24 << 30) + total // 4:
-                    log.warning("prefill GLU weights not packed: HBM reserve reached")
-                    break
-                pgemm.register_glu(w)
-        return rep
+        return pgemm.tune(units, M, self.device, self.ops)
 
     def _probe_prefill_pad(self) -> dict | None:
         """{rows rounded up to 256: the row count (>= it, <= the token budget) whose

@@ -869,19 +869,19 @@ class LlamaModel:
         """Prefill-sized MoE without a host synchronisation: routing (top-k kernel),
         expert-sorted 16-row-padded slots with per-expert end offsets (moe_align),
         the token rows gathered into that order (moe_gather), the two expert GEMMs
-        as hipBLASLt grouped GEMMs over the device-side offsets (``torch._grouped_mm``
-        — one launch per projection for all experts, no per-expert launch loop), the
-        SiLU-GLU between them and the weighted combine (moe_combine). Replaces the
-        argsort / bincount(.tolist()) / index_add torch loop of round 1 (Mixtral
-        prefill step 234 -> 191 ms, profiles/r2_mixtral_grouped_moe_trace.md). The one
-        host round trip left is inside torch._grouped_mm, which reads the group
-        offsets on the host on this ROCm build (not graph-capturable; prefill runs
-        eager, decode uses moe_hip)."""
+        as ONE grouped launch each on the hand-written prefill GEMM
+        (csrc/kernels/prefill_gemm.hip, 256-row expert tiles, expert ids read on the
+        device: no host round trip, graph-capturable) with the SiLU-GLU in the
+        gate|up epilogue, then the weighted combine (moe_combine). Shapes it does not
+        cover fall back to hipBLASLt grouped GEMMs (``torch._grouped_mm``, which reads
+        the group offsets on the host on this ROCm build) + silu_and_mul."""
         op = torch.ops.hipserve
         cfg = self.cfg
         E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
         T, dev = x.shape[0], x.device
-        P, tile = T * k, 16
+        # 256-row expert tiles for the hand-written grouped GEMM (ops/pgemm.py), 16-row
+        # ones for hipBLASLt's grouped GEMM
+        P, tile = T * k, (256 if pgemm.moe_ok(lw.w13, lw.w2) else 16)
         cap = -(-(P + E * (tile - 1)) // tile) * tile
         logits = gemm.linear(x, lw.router)
         w = torch.empty(T, k, dtype=torch.float32, device=dev)
@@ -895,10 +895,16 @@ class LlamaModel:
         op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
         xs = torch.empty(cap, H, dtype=x.dtype, device=dev)
         op.moe_gather(xs, x, slots, k)
-        gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
-        act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-        self.ops.silu_and_mul(act, gu)
-        y = torch._grouped_mm(act, lw.w2.transpose(1, 2), offs=ends)
+        if tile == 256:  # hand-written grouped expert GEMMs, SiLU-GLU in the first's epilogue
+            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+            op.prefill_gemm_grouped(act, xs, lw.w13, tile_expert, 2)
+            y = torch.empty(cap, H, dtype=x.dtype, device=dev)
+            op.prefill_gemm_grouped(y, act, lw.w2, tile_expert, 0)
+        else:
+            gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
+            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+            self.ops.silu_and_mul(act, gu)
+            y = torch._grouped_mm(act, lw.w2.transpose(1, 2), offs=ends)
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         op.moe_combine(out, y, w, pair_slot, k)
         return out

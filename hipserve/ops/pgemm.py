@@ -5,9 +5,13 @@ timing it against hipBLASLt + the separate elementwise kernel at start-up:
 * qkv        plain store                       (vs ``F.linear``)
 * o / down   residual add in the epilogue      (vs ``F.linear`` + ``fused_add_rmsnorm``;
              the fused unit then runs a plain row RMSNorm)
-* gate|up    SiLU-GLU in the epilogue          (vs ``F.linear`` + ``silu_and_mul``), on a
-             copy of the merged weight whose 256-row tiles hold 128 gate rows and
-             their 128 up rows (``pack_glu_rows``)
+* gate|up    SiLU-GLU in the epilogue          (vs ``F.linear`` + ``silu_and_mul``); each
+             256-column tile streams 128 gate rows and the matching 128 up rows of
+             the merged weight as stored (no repacked copy)
+* MoE experts (``grouped_moe``): one grouped launch per projection over the
+             expert-sorted 256-row tiles of ``moe_align`` (device-side expert ids —
+             no host round trip, unlike ``torch._grouped_mm`` on this ROCm build),
+             SiLU-GLU in the gate|up epilogue
 
 ``HIPSERVE_PREFILL_GEMM``: ``auto`` (default: the timed choice), ``1`` (always, where
 the shape fits), ``0`` (hipBLASLt only).
@@ -16,7 +20,6 @@ from __future__ import annotations
 
 import logging
 import os
-import weakref
 
 import torch
 import torch.nn.functional as F
@@ -26,7 +29,6 @@ log = logging.getLogger("hipserve.pgemm")
 MODE = os.environ.get("HIPSERVE_PREFILL_GEMM", "auto")
 MIN_ROWS = 512        # below this hipBLASLt's smaller tiles win (and decode GEMMs take M <= 64)
 CHOICE: dict[tuple, bool] = {}     # (kind, N, K) -> use prefill_gemm
-GLU_ROWS: dict[int, tuple] = {}    # data_ptr of the merged gate|up weight -> (weakref, packed copy)
 REPORT: list[dict] = []
 
 
@@ -43,22 +45,6 @@ def use(kind: str, w, M: int) -> bool:
     return CHOICE.get((kind, w.shape[0], w.shape[1]), False)
 
 
-def glu_rows_of(w: torch.Tensor):
-    e = GLU_ROWS.get(w.data_ptr())
-    if e is None or e[0]() is not w:
-        return None
-    return e[1]
-
-
-def register_glu(w: torch.Tensor) -> torch.Tensor:
-    p = glu_rows_of(w)
-    if p is None:
-        p = torch.empty_like(w)
-        torch.ops.hipserve.pack_glu_rows(p, w)
-        GLU_ROWS[w.data_ptr()] = (weakref.ref(w), p)
-    return p
-
-
 def gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
     torch.ops.hipserve.prefill_gemm(out, x, w, 0)
@@ -71,13 +57,18 @@ def gemm_add_(residual: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch
     return residual
 
 
-def gemm_glu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
-    p = glu_rows_of(w)
-    if p is None:
-        return None
+def gemm_glu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """act = silu(x @ Wg.T) * (x @ Wu.T) for the merged w = [Wg; Wu]."""
     act = torch.empty(x.shape[0], w.shape[0] // 2, device=x.device, dtype=x.dtype)
-    torch.ops.hipserve.prefill_gemm(act, x, p, 2)
+    torch.ops.hipserve.prefill_gemm(act, x, w, 2)
     return act
+
+
+def moe_ok(w13, w2) -> bool:
+    return (MODE != "0" and isinstance(w13, torch.Tensor) and w13.is_cuda and w13.dim() == 3
+            and w13.dtype == torch.bfloat16 and w13.is_contiguous() and w2.is_contiguous()
+            and w13.shape[1] % 256 == 0 and (w13.shape[1] // 2) % 128 == 0 and w13.shape[2] % 64 == 0
+            and w2.shape[1] % 256 == 0 and w2.shape[2] % 64 == 0)
 
 
 def _time(fn, reps=3):
@@ -109,12 +100,9 @@ def tune(units: dict, M: int, device, ops) -> list[dict]:
         ws = [((torch.rand(N, K, device=device, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(4)]
         x = ((torch.rand(M, K, device=device, generator=g) * 2 - 1)).to(torch.bfloat16)
         if kind == "glu":
-            ps = [torch.empty_like(w) for w in ws]
-            for w, p in zip(ws, ps):
-                torch.ops.hipserve.pack_glu_rows(p, w)
             act = torch.empty(M, N // 2, device=device, dtype=torch.bfloat16)
             t_b = _time(lambda i: ops.silu_and_mul(act, F.linear(x, ws[i])))
-            t_p = _time(lambda i: torch.ops.hipserve.prefill_gemm(act, x, ps[i], 2))
+            t_p = _time(lambda i: torch.ops.hipserve.prefill_gemm(act, x, ws[i], 2))
         elif kind == "add":
             res = torch.randn(M, N, device=device).to(torch.bfloat16)
             nw = torch.ones(N, device=device, dtype=torch.bfloat16)

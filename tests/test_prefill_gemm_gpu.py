@@ -43,10 +43,44 @@ def test_prefill_gemm_residual_add(M, N, K):
 def test_prefill_gemm_glu(M, I, K):
     g = torch.Generator(device=DEV).manual_seed(11 + M)
     x, w = _rnd(g, M, K), _rnd(g, 2 * I, K, scale=0.05)
-    wp = torch.empty_like(w)
-    torch.ops.hipserve.pack_glu_rows(wp, w)
     act = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm(act, x, wp, 2)
+    torch.ops.hipserve.prefill_gemm(act, x, w, 2)
     gu = (x.float() @ w.float().t()).to(torch.bfloat16).float()
     want = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
     torch.testing.assert_close(act.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("E,I,K,glu", [(8, 512, 1024, True), (8, 256, 512, False), (16, 128, 256, True)])
+def test_prefill_gemm_grouped_moe(E, I, K, glu):
+    """Grouped expert GEMM over moe_align's 256-row expert tiles (device offsets, no
+    host sync) vs a per-expert fp32 reference."""
+    g = torch.Generator(device=DEV).manual_seed(E + I + K)
+    T, k = 700, 2
+    ids = torch.stack([torch.randperm(E, device=DEV, generator=g)[:k] for _ in range(T)]).int()
+    N = 2 * I if glu else I
+    w = _rnd(g, E, N, K, scale=0.05)
+    x = _rnd(g, T, K)
+    op = torch.ops.hipserve
+    P, tile = T * k, 256
+    cap = -(-(P + E * (tile - 1)) // tile) * tile
+    slots = torch.empty(cap, dtype=torch.int32, device=DEV)
+    tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=DEV)
+    ntiles = torch.empty(1, dtype=torch.int32, device=DEV)
+    pair_slot = torch.empty(P, dtype=torch.int32, device=DEV)
+    ends = torch.empty(E, dtype=torch.int32, device=DEV)
+    op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
+    xs = torch.empty(cap, K, dtype=torch.bfloat16, device=DEV)
+    op.moe_gather(xs, x, slots, k)
+    out = torch.full((cap, I), float("nan"), device=DEV, dtype=torch.bfloat16)
+    op.prefill_gemm_grouped(out, xs, w, tile_expert, 2 if glu else 0)
+    ps = pair_slot.long()
+    for p in range(0, P, 37):  # check a spread of pairs
+        t, j = p // k, p % k
+        e = int(ids[t, j])
+        h = x[t].float() @ w[e].float().t()
+        if glu:
+            h = h.to(torch.bfloat16).float()
+            want = torch.nn.functional.silu(h[:I]) * h[I:]
+        else:
+            want = h
+        torch.testing.assert_close(out[ps[p]].float(), want, rtol=2e-2, atol=2e-2 * max(1.0, want.abs().max().item()))

@@ -67,9 +67,7 @@ def main():
              "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1)}
         if name == "gu":  # GEMM + SiLU-GLU unit
             act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
-            wg = [torch.empty_like(w) for w in ws]
-            for w, p in zip(ws, wg):
-                op.pack_glu_rows(p, w)
+            wg = ws  # the GLU epilogue reads the merged [gate; up] weight as stored
 
             def blas_glu():
                 for w in ws:
