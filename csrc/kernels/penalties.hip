@@ -13,7 +13,11 @@
 //   penalty_apply   logits rows in place, rows with slot < 0 untouched
 //   penalty_update  count the tokens sampled this step (after the sampler)
 //   top_logprobs    per row with n > 0: n largest log-softmax entries (radix
-//                   select on the order-preserving 16-bit key, ties -> lowest id)
+//                   select on the order-preserving 16-bit key of the bf16-rounded
+//                   value, then every candidate in the selected bin up to 64 is
+//                   ordered by its exact value, ties -> lowest id). The runner calls it
+//                   BEFORE penalty_apply: top-n log-probs are of the raw model
+//                   distribution (vLLM's default raw-logprobs mode).
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(kTopT) void top_logprobs_kernel(const T* __restrict
   __shared__ unsigned int hist[256];
   __shared__ unsigned int s_sel[3];  // threshold key, count strictly above, remaining ties to take
   __shared__ int s_tie_scan[kTopT];
-  __shared__ unsigned int c_key[64];
+  __shared__ float c_val[64];
   __shared__ int c_idx[64];
   __shared__ unsigned int c_n;
   const int r = blockIdx.x, t = threadIdx.x;
@@ -164,7 +168,10 @@ __global__ __launch_bounds__(kTopT) void top_logprobs_kernel(const T* __restrict
   }
   const unsigned int kth = s_sel[0];
   const unsigned int n_above = s_sel[1];
-  const int take_ties = n - (int)n_above;
+  // every key in the selected bin is a candidate (the bin rounds fp32 logits to bf16,
+  // so the true n-th largest may sit anywhere in it) while they fit the 64 slots;
+  // past that the lowest-index ones
+  const int take_ties = 64 - (int)n_above;
   // 3. collect: every key > kth, then the lowest-index ties (contiguous chunks per
   //    thread + a block scan give each tie its global index rank)
   if (t == 0) c_n = 0;
@@ -182,37 +189,38 @@ __global__ __launch_bounds__(kTopT) void top_logprobs_kernel(const T* __restrict
   }
   int rank = s_tie_scan[t] - nt;
   for (int v = lo; v < hi; ++v) {
-    const unsigned int k = key16f(ld_logit(row, v));
+    const float l = ld_logit(row, v);
+    const unsigned int k = key16f(l);
     bool take = k > kth;
     if (k == kth) take = rank++ < take_ties;
     if (take) {
       const unsigned int p = atomicAdd(&c_n, 1u);
       if (p < 64) {
-        c_key[p] = k;
+        c_val[p] = l;
         c_idx[p] = v;
       }
     }
   }
   __syncthreads();
-  // 4. order (key desc, id asc) and write
+  // 4. order (exact value desc, id asc) and write the first n
   if (t == 0) {
     const int cn = min((int)c_n, 64);
     for (int i = 1; i < cn; ++i) {
-      const unsigned int k = c_key[i];
+      const float k = c_val[i];
       const int x = c_idx[i];
       int j = i - 1;
-      while (j >= 0 && (c_key[j] < k || (c_key[j] == k && c_idx[j] > x))) {
-        c_key[j + 1] = c_key[j];
+      while (j >= 0 && (c_val[j] < k || (c_val[j] == k && c_idx[j] > x))) {
+        c_val[j + 1] = c_val[j];
         c_idx[j + 1] = c_idx[j];
         --j;
       }
-      c_key[j + 1] = k;
+      c_val[j + 1] = k;
       c_idx[j + 1] = x;
     }
     for (int i = 0; i < K; ++i) {
       const bool ok = i < n && i < cn;
       out_ids[(long)r * K + i] = ok ? c_idx[i] : -1;
-      out_lp[(long)r * K + i] = ok ? ld_logit(row, c_idx[i]) - lse : -INFINITY;
+      out_lp[(long)r * K + i] = ok ? c_val[i] - lse : -INFINITY;
     }
   }
 }

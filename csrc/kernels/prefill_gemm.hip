@@ -184,14 +184,10 @@ __global__ __launch_bounds__(PG_T) void pgemm_kernel(const unsigned short* __res
 }
 
 // ---- v2: half-tile pipeline. Each K tile runs as 4 phases (one 64 x 32 output
-// quadrant of the wave's 128 x 64 block per phase: 16 MFMAs), separated by raw
-// s_barriers. The LDS halves are freed in phase order — A rows of quadrant-row 0
-// after phase 1, B columns of quadrant-column 0 after phase 2, the other halves
-// after phase 3 — and each is restaged as soon as it is free: tile kt+2's A-half0
-// in phase 2 and B-half0 in phase 3 (same stage as tile kt), tile kt+1's A-half1 /
-// B-half1 in phase 0 (other stage). One counted wait per tile (vmcnt(4) at the end of
-// phase 3: tile kt+1 complete, tile kt+2's first two halves still in flight) keeps
-// LDS-DMA traffic going across every barrier (cdna_hip_programming.md §5 T3/T4).
+// quadrant of the wave's 128 x 64 block per phase: 16 MFMAs) with raw s_barriers
+// and counted vmcnt waits, so LDS-DMA traffic of the next two tiles stays in flight
+// across every barrier (cdna_hip_programming.md §5 T3/T4) and no fragment read is
+// waited on by the MFMAs that follow it (schedule in the loop below).
 // kGroup (MoE prefill experts): A rows are expert-sorted and padded to 256-row tiles
 // (moe_align with tile 256); tile_expert[tm] names the expert whose weight
 // (B + e * b_estride) the m-tile multiplies, -1 = unused tile. Device-side offsets:
@@ -214,9 +210,12 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
   }
   const int nk = K / PG_BK;
 
-  // half-tile staging: wave w moves half rows [16w, 16w + 16) in 2 instructions of 8 rows
-  const unsigned short* src[2][2][2];  // [operand A/B][half][instr]
-  int dst[2][2][2];                    // LDS byte offset inside a stage
+  // half-tile staging: wave w moves half rows [16w, 16w + 16) in 2 instructions of 8
+  // rows, as buffer_load ... lds with a per-lane 32-bit offset (8 VGPRs for all the
+  // staging addresses; 64-bit pointers would push the loop past 256 VGPRs into
+  // scratch, whose reload waits drain the LDS-DMA queue) and the K step in soffset
+  unsigned int voff[2][2][2];  // [operand A/B][half][instr]
+  int dst[2][2][2];            // LDS byte offset inside a stage (wave-uniform)
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -224,16 +223,19 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
       const int j0 = wave * 16 + i * 8, j = j0 + (lane >> 3);
       const int ra0 = (j0 >> 6) * 128 + h * 64 + (j0 & 63), ra = (j >> 6) * 128 + h * 64 + (j & 63);
       const int rb0 = (j0 >> 5) * 64 + h * 32 + (j0 & 31), rb = (j >> 5) * 64 + h * 32 + (j & 31);
-      src[0][h][i] = A + (long)min(m0 + ra, M - 1) * lda + ((lane & 7) ^ ((ra >> 1) & 7)) * 8;
-      src[1][h][i] = B + (long)pg_brow<EPI>(n0, tn, rb, N) * ldb + ((lane & 7) ^ ((rb >> 1) & 7)) * 8;
+      voff[0][h][i] = (unsigned)((long)min(m0 + ra, M - 1) * lda * 2 + ((lane & 7) ^ ((ra >> 1) & 7)) * 16);
+      voff[1][h][i] = (unsigned)((long)pg_brow<EPI>(n0, tn, rb, N) * ldb * 2 + ((lane & 7) ^ ((rb >> 1) & 7)) * 16);
       dst[0][h][i] = ra0 * 128;
       dst[1][h][i] = PG_TILE + rb0 * 128;
     }
+  const __amdgpu_buffer_rsrc_t rsrc[2] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min((long)M * lda * 2, 0x7fffffffL), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)min((long)N * ldb * 2, 0x7fffffffL), 0x00020000)};
   auto stage_half = [&](int op, int h, int buf, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src[op][h][i] + kt * PG_BK),
-                                       (lds_ptr_t)(lds + buf * 2 * PG_TILE + dst[op][h][i]), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc[op], (lds_ptr_t)(lds + buf * 2 * PG_TILE + dst[op][h][i]), 16,
+                                               voff[op][h][i], kt * PG_BK * 2, 0, 0);
   };
   const int fr = lane & 15, fq = lane >> 4;
   const int sw = (fr >> 1) & 7;
@@ -246,24 +248,16 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: tile 0 whole, tile 1's A-half0 / B-half0; wait for tile 0
-  stage_half(0, 0, 0, 0);
-  stage_half(1, 0, 0, 0);
-  stage_half(0, 1, 0, 0);
-  stage_half(1, 1, 0, 0);
-  if (nk > 1) {
-    stage_half(0, 0, 1, 1);
-    stage_half(1, 0, 1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  // fragments: B for all 4 n-frags (phases 0 / 1 read them), A for both quadrant rows
-  // (qm 0 read in phase 0, qm 1 prefetched in phase 1 behind phase 1's MFMAs), so
-  // only phase 0's reads are exposed at a tile's start
+  // fragments in registers: A rows of both quadrant rows, B columns of both quadrant
+  // columns. Every read is issued one phase (or more) before its MFMAs:
+  //   phase 0  MFMA (A0, B0)  | read B1 of this tile
+  //   phase 1  MFMA (A0, B1)  | read A1 of this tile
+  //   phase 2  MFMA (A1, B0)  |
+  //   phase 3  MFMA (A1, B1)  | read A0, B0 of the NEXT tile (other stage)
+  // LDS-DMA: tile kt+2's A0/B0 halves into this stage in phase 0 (this tile's A0/B0
+  // were read during the previous tile's phase 3), its A1/B1 halves in phase 2 (read
+  // in phases 0 / 1). Waits: end of phase 2 -> the next tile's A0/B0 landed (vmcnt 12),
+  // end of phase 3 -> its A1/B1 landed (vmcnt 8). Barriers after phases 1, 2, 3.
   u16x8 bfr[4][2], afr[2][4][2];
   auto read_b = [&](const unsigned char* sb, int qn) {
 #pragma unroll
@@ -279,28 +273,54 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
       for (int s2 = 0; s2 < 2; ++s2)
         afr[qm][ii][s2] = *reinterpret_cast<const u16x8*>(sb + a_off + (4 * qm + ii) * 2048 + chs[s2]);
   };
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // prologue: tiles 0 and 1 in flight; tile 0 and tile 1's A0/B0 landed; tile 0's A0/B0 read
+  stage_half(0, 0, 0, 0);
+  stage_half(1, 0, 0, 0);
+  stage_half(0, 1, 0, 0);
+  stage_half(1, 1, 0, 0);
+  if (nk > 1) {
+    stage_half(0, 0, 1, 1);
+    stage_half(1, 0, 1, 1);
+    stage_half(0, 1, 1, 1);
+    stage_half(1, 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+  read_a(lds, 0);
+  read_b(lds, 0);
+
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const unsigned char* sb = lds + buf * 2 * PG_TILE;
+    const bool more2 = kt + 2 < nk, more1 = kt + 1 < nk;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int qm = p >> 1, qn = p & 1;
-      if (p == 0) {
-        read_a(sb, 0);
-        read_b(sb, 0);
+      if (p == 0 && more2) {
+        stage_half(0, 0, buf, kt + 2);
+        stage_half(1, 0, buf, kt + 2);
       }
-      if (p == 0 && kt + 1 < nk) {
-        stage_half(0, 1, buf ^ 1, kt + 1);
-        stage_half(1, 1, buf ^ 1, kt + 1);
+      if (p == 2 && more2) {
+        stage_half(0, 1, buf, kt + 2);
+        stage_half(1, 1, buf, kt + 2);
       }
-      if (p == 2 && kt + 2 < nk) stage_half(0, 0, buf, kt + 2);
-      if (p == 3 && kt + 2 < nk) stage_half(1, 0, buf, kt + 2);
-      if (p == 1) read_a(sb, 1);  // for phases 2, 3, behind phase 1's MFMAs
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        if (p == 0 && s2 == 1) {  // B for phase 1, behind the first half of phase 0's MFMAs
+        if (s2 == 1) {  // the next phase's fragments, behind the first half of this phase's MFMAs
           __builtin_amdgcn_sched_barrier(0);
-          read_b(sb, 1);
+          if (p == 0) read_b(sb, 1);
+          if (p == 1) read_a(sb, 1);
+          if (p == 3 && more1) {
+            read_a(lds + (buf ^ 1) * 2 * PG_TILE, 0);
+            read_b(lds + (buf ^ 1) * 2 * PG_TILE, 0);
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_s_setprio(1);
@@ -313,13 +333,16 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
                 acc[2 * qn + jj][4 * qm + ii], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
-      if (p == 3) {  // tile kt+1 complete (kt+2's first halves may stay in flight)
-        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (p == 2) {  // the next tile's A0 / B0 halves landed (read in phase 3)
+        if (more2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if (more1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+      if (p == 3) {  // the next tile's A1 / B1 halves landed (read in its phases 0 / 1)
+        if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (p != 0) barrier();
     }
   }
   pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);

@@ -876,7 +876,7 @@ void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots
   CHECK_DEV(ids);
   TORCH_CHECK(ids.scalar_type() == at::kInt && slots.scalar_type() == at::kInt &&
               tile_expert.scalar_type() == at::kInt && pair_slot.scalar_type() == at::kInt);
-  TORCH_CHECK(E <= 128 && (tile == 16 || tile == 32 || tile == 64));
+  TORCH_CHECK(E <= 128 && (tile == 16 || tile == 32 || tile == 64 || tile == 256));
   const int npairs = ids.numel();
   TORCH_CHECK(slots.numel() >= npairs + E * (tile - 1) && slots.numel() % tile == 0,
               "slots capacity must cover padding and be a multiple of the tile");

@@ -520,6 +520,11 @@ class ModelRunner:
             return np.zeros(0, np.int64), np.zeros(0, np.float32), None
         rows = self._t(inp.logits_rows)
         logits = self.model.compute_logits(hidden.index_select(0, rows))
+        top = None
+        if inp.top_logprobs:  # raw (pre-penalty) log-probs, as vLLM's default mode
+            ti = torch.empty(n, TOP_LOGPROBS, dtype=torch.int32, device=self.device)
+            tl = torch.empty(n, TOP_LOGPROBS, dtype=torch.float32, device=self.device)
+            self.ops.top_logprobs(logits, self._t(inp.nlogprobs), ti, tl)
         pslot = None
         if inp.pen_slot is not None:
             if inp.pen_init is not None:
@@ -533,11 +538,7 @@ class ModelRunner:
                         self._t(inp.top_p), self._t(inp.seeds), self._t(inp.steps))
         if pslot is not None:
             self.ops.penalty_update(tok, pslot, self.pen_counts, self.pen_seen)
-        top = None
         if inp.top_logprobs:
-            ti = torch.empty(n, TOP_LOGPROBS, dtype=torch.int32, device=self.device)
-            tl = torch.empty(n, TOP_LOGPROBS, dtype=torch.float32, device=self.device)
-            self.ops.top_logprobs(logits, self._t(inp.nlogprobs), ti, tl)
             top = (ti.cpu().numpy(), tl.cpu().numpy())
         return tok.cpu().numpy(), lp.cpu().numpy(), top
 
@@ -600,15 +601,16 @@ class ModelRunner:
         meta.id_src = (st["src"][:b], st["tok"])
         hidden = self.model.forward(st["ids"][:b], meta, self.kv)
         logits = self.model.compute_logits(hidden)
-        # penalties / top-n logprobs: early-exit kernels for rows that want none
+        # penalties / top-n logprobs: early-exit kernels for rows that want none; top-n
+        # log-probs of the raw (pre-penalty) distribution, as vLLM's default mode
         if full:
+            self.ops.top_logprobs(logits, st["nlp"][:b], st["top_ids"][:b], st["top_lp"][:b])
             self.ops.penalty_apply(logits, st["pslot"][:b], st["pres"][:b], st["freq"][:b], st["rep"][:b],
                                    self.pen_counts, self.pen_seen)
         self.ops.sample(st["tok"][:b], st["lp"][:b], logits, st["temp"][:b], st["topk"][:b],
                         st["topp"][:b], st["seeds"][:b], st["steps"][:b], two_rounds=full)
         if full:
             self.ops.penalty_update(st["tok"][:b], st["pslot"][:b], self.pen_counts, self.pen_seen)
-            self.ops.top_logprobs(logits, st["nlp"][:b], st["top_ids"][:b], st["top_lp"][:b])
 
     def _stage_in(self, b: int, sg):
         """Pinned staging set -> device static inputs, one zero-copy dispatch

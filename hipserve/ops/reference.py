@@ -374,10 +374,8 @@ def top_logprobs(logits, nreq, out_ids, out_lp):
             continue
         l = logits[r].float()
         ls = l - torch.logsumexp(l, 0)
-        # order by (bf16-rounded value desc, id asc) like the kernel's 16-bit keys
-        key = l.to(torch.bfloat16).float()
-        order = sorted(range(l.shape[0]), key=lambda i: (-key[i].item(), i))[:n] if l.shape[0] <= 4096 else \
-            torch.argsort(-key, stable=True)[:n].tolist()
+        # order by (exact value desc, id asc): stable sort keeps equal values in id order
+        order = torch.argsort(-l, stable=True)[:n].tolist()
         for i, v in enumerate(order):
             out_ids[r, i] = v
             out_lp[r, i] = ls[v]

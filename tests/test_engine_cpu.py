@@ -162,6 +162,29 @@ def test_penalties_and_logprobs():
     assert len(set(toks)) >= 6
 
 
+def test_top_logprobs_are_raw_with_penalties():
+    """top-n log-probs report the raw model distribution (vLLM's
+    default raw-logprobs mode) even when penalties change what is sampled: the first
+    step's top-5 of a heavily penalised request equals the unpenalised one's, while the
+    penalised greedy pick avoids the prompt's tokens."""
+    eng = make_engine()
+    p = [1, 2, 3, 2, 3, 2, 3]
+    plain = SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True, logprobs=5)
+    pen = SamplingParams(temperature=0.0, max_tokens=1, ignore_eos=True, logprobs=5, repetition_penalty=50.0,
+                         frequency_penalty=2.0)
+    rids = [eng.add_request(None, p, sp).request_id for sp in (plain, pen)]
+    tops, toks = {}, {}
+    while eng.has_unfinished():
+        for o in eng.step():
+            toks[o.request_id] = o.new_token_ids
+            tops[o.request_id] = o.logprobs[1] if o.logprobs else None
+    a, b = tops[rids[0]], tops[rids[1]]
+    assert a is not None and [t for t, _ in a] == [t for t, _ in b]
+    assert all(abs(x - y) < 1e-5 for (_, x), (_, y) in zip(a, b))
+    assert [v for _, v in a] == sorted((v for _, v in a), reverse=True)
+    assert toks[rids[1]][0] not in p
+
+
 def test_penalty_slots_cover_every_running_sequence():
     """more penalised requests than the old 256-slot pool, plus
     preemptions (a KV pool too small for all of them at once): every step finds a

@@ -470,8 +470,12 @@ def test_penalty_and_top_logprobs_kernels(V, dt):
     assert torch.equal(got.cpu()[[1, 3, 4, 5]], logits[[1, 3, 4, 5]])
     rel = 1e-5 if dt == torch.float32 else 2.0 ** -7  # one bf16 ulp
     assert ((got.cpu().float() - want.float()).abs() <= want.float().abs() * rel + 1e-5).all()
-    # top-n logprobs (with forced ties in row 2)
+    # top-n logprobs (with forced ties in row 2); with fp32 logits, row 5's top entries
+    # sit within one bf16 step of each other, increasing with id: the exact-value
+    # order is the reverse of the id order
     want[2, 100:110] = want[2].max() + 1
+    if dt == torch.float32:
+        want[5, 300:310] = want[5].max() + 1 + torch.arange(10) * 1e-4
     got = want.to(dev)
     nreq = torch.tensor([5, 0, 20, 1, 3, 7], dtype=torch.int32)
     ids = torch.empty(rows, 20, dtype=torch.int32, device=dev)
@@ -481,6 +485,8 @@ def test_penalty_and_top_logprobs_kernels(V, dt):
     rlp = torch.empty(rows, 20)
     R.top_logprobs(want, nreq, rid, rlp)
     assert torch.equal(ids.cpu(), rid)
+    if dt == torch.float32:
+        assert ids.cpu()[5, :7].tolist() == list(range(309, 302, -1))
     fin = torch.isfinite(rlp)
     assert torch.equal(torch.isfinite(lps.cpu()), fin)
     assert (lps.cpu()[fin] - rlp[fin]).abs().max().item() < 1e-3

@@ -8,6 +8,13 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    from hipserve.ops import load_library
+
+    load_library()
+
 SHAPES = [(256, 256, 64), (300, 512, 1024), (1000, 768, 2048), (2049, 1280, 512), (64, 1024, 4096),
           (8192, 512, 4096)]
 
