@@ -341,13 +341,16 @@ def run_phase(args):
         steps = max(1, min(steps, int((args.deadline - time.time()) / max(per, 1e-3))))
     barrier()
     t0 = time.perf_counter()
-    tok_total, ttfts = 0, []
+    tok_total, ttfts, ol_summary = 0, [], None
     if args.request_rate and args.path == "gateway":
         res, _ = lg.open_loop(url=stack.url, model=args.model, rate=args.request_rate,
                               num_requests=args.steps * args.concurrency, input_len=args.input_len,
                               output_len=args.output_len, vocab=min(V, 100000), temperature=args.temperature,
                               top_p=args.top_p)
         tok_total, ttfts = sum(r["tokens"] for r in res), [r["ttft"] for r in res]
+        from hipserve.bench.loadgen import summarize
+
+        ol_summary = summarize(res, time.perf_counter() - t0)
     else:
         for _ in range(steps):
             n, tt = wave()
@@ -405,6 +408,10 @@ def run_phase(args):
         "engine_init_s": round(init_s, 1),
         "kv_blocks": engine.runner.num_blocks,
     }
+    if ol_summary:  # open loop: TTFT tail and inter-token latency of every request
+        out["open_loop"] = {"rate_req_s": args.request_rate, "requests": ol_summary["requests"],
+                            **{k: round(ol_summary[k], 2) for k in ("p50_ttft_ms", "p90_ttft_ms", "p50_itl_ms",
+                                                                    "p90_itl_ms") if ol_summary[k] is not None}}
     if tp_mode or args.deadline:
         out["tp_info"] = ({"pg_backend": tpg.backend, "pg_world_size": dist.get_world_size(),
                            "rccl": tpg.backend == "nccl", "custom_allreduce": tpg.custom_ar is not None,

@@ -116,3 +116,6 @@ def test_bench_open_loop_request_rate():
     """--request-rate: open-loop Poisson arrivals through the gateway path."""
     out = _run([sys.executable, "bench.py"] + ARGS + ["--request-rate", "20", "--steps", "2"])
     assert out["load"].startswith("open-loop") and out["value"] > 0 and out["p50_ttft_ms"] > 0
+    ol = out["open_loop"]
+    assert ol["rate_req_s"] == 20 and ol["p90_ttft_ms"] >= ol["p50_ttft_ms"] > 0
+    assert ol["p90_itl_ms"] >= ol["p50_itl_ms"] > 0
