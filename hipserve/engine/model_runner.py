@@ -272,6 +272,9 @@ class ModelRunner:
             if kind == "glu" and (self.mcfg.hidden_act != "silu" or (w.shape[0] // 2) % 128):
                 continue
             units.add((kind, w.shape[0], w.shape[1]))
+        if lw.w13 is not None and pgemm.moe_ok(lw.w13, lw.w2) and self.mcfg.hidden_act == "silu":
+            E, N13, H = lw.w13.shape
+            units.add(("moe", E, N13 // 2, H, self.mcfg.num_experts_per_tok))
         if not units:
             return []
         M = min(self.ecfg.max_num_batched_tokens, 8192)

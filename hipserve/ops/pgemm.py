@@ -8,7 +8,8 @@ timing it against hipBLASLt + the separate elementwise kernel at start-up:
 * gate|up    SiLU-GLU in the epilogue          (vs ``F.linear`` + ``silu_and_mul``); each
              256-column tile streams 128 gate rows and the matching 128 up rows of
              the merged weight as stored (no repacked copy)
-* MoE experts (``grouped_moe``): one grouped launch per projection over the
+* MoE experts (``moe_grouped``, timed as a unit against hipBLASLt's grouped GEMM):
+             one grouped launch per projection over the
              expert-sorted 256-row tiles of ``moe_align`` (device-side expert ids —
              no host round trip, unlike ``torch._grouped_mm`` on this ROCm build),
              SiLU-GLU in the gate|up epilogue
@@ -64,11 +65,22 @@ def gemm_glu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return act
 
 
-def moe_ok(w13, w2) -> bool:
-    return (MODE != "0" and isinstance(w13, torch.Tensor) and w13.is_cuda and w13.dim() == 3
+def moe_fits(w13, w2) -> bool:
+    return (isinstance(w13, torch.Tensor) and w13.is_cuda and w13.dim() == 3
             and w13.dtype == torch.bfloat16 and w13.is_contiguous() and w2.is_contiguous()
             and w13.shape[1] % 256 == 0 and (w13.shape[1] // 2) % 128 == 0 and w13.shape[2] % 64 == 0
             and w2.shape[1] % 256 == 0 and w2.shape[2] % 64 == 0)
+
+
+def moe_ok(w13, w2) -> bool:
+    """Grouped expert GEMMs on the hand-written kernel (else hipBLASLt's grouped GEMM):
+    ``1`` wherever the shapes fit, ``auto`` where the start-up timing chose it."""
+    if MODE == "0" or not moe_fits(w13, w2):
+        return False
+    if MODE == "1":
+        return True
+    E, N13, H = w13.shape
+    return any(CHOICE.get(("moe", E, N13 // 2, H, k), False) for k in range(1, 9))
 
 
 def _time(fn, reps=3):
@@ -86,14 +98,68 @@ def _time(fn, reps=3):
     return best
 
 
+def _tune_moe(E: int, inter: int, H: int, k: int, T: int, device, ops) -> dict:
+    """The two grouped expert GEMMs of one MoE layer (+ SiLU-GLU) for T tokens routed
+    uniformly at random: hand-written grouped kernel over moe_align's 256-row tiles vs
+    hipBLASLt's grouped GEMM (torch._grouped_mm) over 16-row-padded groups."""
+    op = torch.ops.hipserve
+    g = torch.Generator(device=device).manual_seed(E + inter + H)
+    w13 = ((torch.rand(E, 2 * inter, H, device=device, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16)
+    w2 = ((torch.rand(E, H, inter, device=device, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16)
+    x = (torch.rand(T, H, device=device, generator=g) * 2 - 1).to(torch.bfloat16)
+    ids = torch.rand(T, E, device=device, generator=g).argsort(-1)[:, :k].int().contiguous()
+    P = T * k
+
+    def layout(tile):
+        cap = -(-(P + E * (tile - 1)) // tile) * tile
+        slots = torch.empty(cap, dtype=torch.int32, device=device)
+        te = torch.empty(cap // tile, dtype=torch.int32, device=device)
+        nt = torch.empty(1, dtype=torch.int32, device=device)
+        ps = torch.empty(P, dtype=torch.int32, device=device)
+        ends = torch.empty(E, dtype=torch.int32, device=device)
+        op.moe_align(ids, E, tile, slots, te, nt, ps, ends)
+        xs = torch.empty(cap, H, dtype=x.dtype, device=device)
+        op.moe_gather(xs, x, slots, k)
+        return cap, te, ends, xs
+
+    cap, te, _, xs = layout(256)
+    act = torch.empty(cap, inter, dtype=x.dtype, device=device)
+    y = torch.empty(cap, H, dtype=x.dtype, device=device)
+
+    def p_moe(i):
+        op.prefill_gemm_grouped(act, xs, w13, te, 2)
+        op.prefill_gemm_grouped(y, act, w2, te, 0)
+
+    t_p = _time(p_moe, reps=2)
+    cap16, _, ends, xs16 = layout(16)
+    act16 = torch.empty(cap16, inter, dtype=x.dtype, device=device)
+
+    def b_moe(i):
+        ops.silu_and_mul(act16, torch._grouped_mm(xs16, w13.transpose(1, 2), offs=ends))
+        torch._grouped_mm(act16, w2.transpose(1, 2), offs=ends)
+
+    t_b = _time(b_moe, reps=2)
+    key = ("moe", E, inter, H, k)
+    CHOICE[key] = t_p < t_b * 0.99
+    r = {"kind": "moe", "M": T, "E": E, "I": inter, "H": H, "top_k": k, "blas_unit_ms": round(t_b, 4),
+         "pgemm_unit_ms": round(t_p, 4), "pgemm": CHOICE[key]}
+    log.info("prefill GEMM %s", r)
+    return r
+
+
 @torch.inference_mode()
 def tune(units: dict, M: int, device, ops) -> list[dict]:
-    """units: {(kind, N, K)} with kind in {"plain", "add", "glu"}; times both ways on
-    4 weight copies (streams weights like a prefill step) and fills CHOICE."""
+    """units: {(kind, N, K)} with kind in {"plain", "add", "glu"} and
+    ("moe", E, I, H, top_k); times both ways (dense kinds on 4 weight copies, streaming
+    weights like a prefill step) and fills CHOICE."""
     if MODE == "0":
         return []
     out = []
-    for (kind, N, K) in sorted(units):
+    for u in sorted(units):
+        if u[0] == "moe":
+            out.append(_tune_moe(*u[1:], M, device, ops))
+            continue
+        kind, N, K = u
         if N % 256 or K % 64:
             continue
         g = torch.Generator(device=device).manual_seed(N + K)

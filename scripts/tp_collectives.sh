@@ -24,6 +24,11 @@ ar() {  # ar <world> <hidden>
 }
 
 trace8() {
+  # one HW queue per process: 8 processes x the default 4 queues oversubscribe the
+  # device's hardware queue slots, and the CP then time-slices queues (~10 ms quanta),
+  # so every spin-waiting collective kernel would wait out whole quanta for its peers
+  # (measured: 10.6-21 ms per hipGraph all-reduce at 4 queues, 81 us at 1)
+  export GPU_MAX_HW_QUEUES=1
   local port=29631 pids=()
   for r in 1 2 3 4 5 6 7; do
     RANK=$r WORLD_SIZE=8 MASTER_PORT=$port timeout -k 10 420 python3 tools/tp_shared_gpu.py --model llama-3-70b \
