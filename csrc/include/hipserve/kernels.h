@@ -184,7 +184,8 @@ bool launch_dgf(int fix, bool norm_in, const DgfArgs& A, const void* x, long x_s
 //   PG_EPI_STORE  C = bf16(acc)
 //   PG_EPI_ADD    C (the residual, in place) = bf16(bf16(acc) + C)
 //   PG_EPI_GLU    B = the merged [gate; up] weight (N = 2I, I % 128 == 0); C = act [M, I] = silu(gate) * up
-constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2;
+//   PG_EPI_GEGLU  as GLU with tanh-GELU(gate) * up (Gemma)
+constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2, PG_EPI_GEGLU = 3;
 struct PgEpi {
   int variant;               // 1: one-stage-ahead loop, 2: half-tile pipeline (default)
   const int* tile_expert;    // grouped (MoE): expert of each 256-row tile of A, -1 = unused
@@ -192,6 +193,27 @@ struct PgEpi {
 };
 bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
                          int K, const PgEpi& E, hipStream_t s);
+// FP8 (W8A8) form: A = per-token e4m3 activations [M, K] bytes (row scale xs[M]),
+// B = e4m3 weights in the decode kernel's tiled layout (gguf_mfma.hip: [N/16][K/256]
+// [4096 B]) as up to 4 parts stacked along N (each rows % 256 == 0; GLU: part 0 =
+// gate, part 1 = up, equal rows % 128 == 0), per-row scale rs (x 256, the decode
+// path's convention). C = epilogue(acc * xs[m] * rs[n] / 256). K % 256 == 0.
+constexpr int kPgF8Parts = 4;
+struct PgF8Part {
+  const unsigned char* q;
+  const float* rs;
+  int rows;
+  int tile0;  // first 256-column tile of the part (non-GLU)
+};
+struct PgF8 {
+  PgF8Part p[kPgF8Parts];
+  int n;
+  const float* xs;
+};
+bool launch_prefill_gemm_f8(int epi, void* C, long ldc, const void* A, long lda, const PgF8& W, int M, int N, int K,
+                            hipStream_t s);
+// per-token dynamic e4m3 quantisation: xs[m] = max|x[m, :]| / 448, q = sat(x / xs)
+void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s);
 void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);
 
 // decode_fused.hip — split-K partial reductions fused with the next op of the layer

@@ -23,8 +23,8 @@
 //  * the MFMA k order inside each 8-element fragment is therefore the pair order
 //    {0, 2, 1, 3, 4, 6, 5, 7}: x is converted to f16 ONCE per workgroup while
 //    staging into LDS, already in that order, so A and B agree on every k;
-//  * v_mfma_f32_16x16x32_f16 (same rate as bf16), fp32 accumulation; x is
-//    clamped to the f16 range on staging;
+//  * v_mfma_f32_16x16x32_f16 (same rate as bf16), fp32 accumulation; x rows beyond
+//    the f16 range are caught on staging and rerun pre-scaled (qgemm2_body);
 //  * all parts of a merged projection are one launch (part table: format, column
 //    offset, rows; two formats per launch for the Q4_K/Q5_K + Q6_K mixes); split-K
 //    writes fp32 partials [S, M, N_total] that the decode layer's fused epilogues
@@ -378,17 +378,26 @@ struct Dec {
   }
 };
 
-// bf16 word halves -> fp32 (exact: one shift or mask), clamped to the f16 range by one
-// v_med3 (fminf/fmaxf add NaN-canonicalising v_max ops: the x staging is a large share
-// of the M = 64 body's VALU issue, which bounds it)
+// bf16 word halves -> fp32 (exact: one shift or mask)
 HS_DEVICE float bf_lo(unsigned w) { return __builtin_bit_cast(float, w << 16); }
 HS_DEVICE float bf_hi(unsigned w) { return __builtin_bit_cast(float, w & 0xFFFF0000u); }
-HS_DEVICE _Float16 sat16(float f) { return static_cast<_Float16>(__builtin_amdgcn_fmed3f(f, -65504.f, 65504.f)); }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+HS_DEVICE u16x2 as_u16x2(unsigned u) { return __builtin_bit_cast(u16x2, u); }
+
+// f16 range of the staged x: a value beyond +-65504 (bf16 activations reach ~3e38;
+// Gemma-family hidden states are known to exceed the f16 range) converts to +-inf
+// and is caught, not clamped: every staged f16 pair's |bits| go into a running
+// v_pk_max_u16 (as many VALU ops as the v_med3 clamp this replaced), a workgroup
+// vote at the end of the K loop, and only then a second pass with each x row
+// pre-scaled by a power of two 2^-k (k from the row's max over the workgroup's K
+// range) that the epilogue undoes exactly (scale_x_rows / acc *= 2^k).
+constexpr unsigned kF16AbsMask = 0x7FFF7FFFu;
 
 // One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
 // x staging. Body per format; the kernel picks it per part (two formats per launch).
 template <int QT, int MT, int RT, int NWAVES, bool kMoe = false>
-HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short* __restrict__ out, long out_stride,
+HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, unsigned short* __restrict__ out,
+                           long out_stride,
                            float* __restrict__ ws, const unsigned short* __restrict__ x, long x_stride,
                            const Part& P, int M, int Ntot, int K, int sb_per_split, const MoeQ& moe = MoeQ{}) {
   constexpr int XR = 16 * MT;           // staged x rows (M padded)
@@ -441,34 +450,50 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
       }
     }
   };
-  auto store_x = [&](int buf) {
+  u16x2 om = {0, 0};  // running max of the staged f16 |bits| (first pass)
+  auto store_x = [&](int buf, auto scaled) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
       const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);  // bf16 pairs (0,1) (2,3) (4,5) (6,7)
-      f16x8 h;  // pair order {0, 2, 1, 3, 4, 6, 5, 7}
-      h[0] = sat16(bf_lo(w[0])); h[1] = sat16(bf_lo(w[1])); h[2] = sat16(bf_hi(w[0])); h[3] = sat16(bf_hi(w[1]));
-      h[4] = sat16(bf_lo(w[2])); h[5] = sat16(bf_lo(w[3])); h[6] = sat16(bf_hi(w[2])); h[7] = sat16(bf_hi(w[3]));
+      // pair order {0, 2, 1, 3, 4, 6, 5, 7}
+      float f[8] = {bf_lo(w[0]), bf_lo(w[1]), bf_hi(w[0]), bf_hi(w[1]),
+                    bf_lo(w[2]), bf_lo(w[3]), bf_hi(w[2]), bf_hi(w[3])};
+      if constexpr (decltype(scaled)::value) {
+        const float sc = xrow[row];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] *= sc;
+      }
+      f16x8 h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = static_cast<_Float16>(f[e]);
+      if constexpr (!decltype(scaled)::value) {
+        const u32x4 u = __builtin_bit_cast(u32x4, h);
+        om = __builtin_elementwise_max(
+            om, __builtin_elementwise_max(__builtin_elementwise_max(as_u16x2(u[0] & kF16AbsMask), as_u16x2(u[1] & kF16AbsMask)),
+                                          __builtin_elementwise_max(as_u16x2(u[2] & kF16AbsMask), as_u16x2(u[3] & kF16AbsMask))));
+      }
       *reinterpret_cast<f16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = h;
     }
   };
 
   f32x4 acc[RT][MT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // Two register sets for the weights, used alternately (loop unrolled by 2): no
   // copies between iterations, so the only wait for a super-chunk's weights is at
   // their first use. Per iteration the x loads of the next super-chunk go out before
   // its weight loads: store_x's in-order vmcnt wait then leaves the weights in flight.
   Raw rawA[RT], rawB[RT];
+  auto run = [&](auto scaled) {
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (sb0 < sb1) {
     load_x(sb0);
 #pragma unroll
     for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sb0 * CB, g, c, lane, rawA[r]);
-    store_x(0);
+    store_x(0, scaled);
   }
   __syncthreads();
   auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
@@ -504,7 +529,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
 #pragma unroll
         for (int r = 0; r < RT; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b[t], acc[r][t], 0, 0, 0);
     }
-    store_x(buf ^ 1);
+    store_x(buf ^ 1, scaled);
     __syncthreads();
   };
   int sb = sb0;
@@ -513,6 +538,38 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], unsigned short*
     iter(sb + 1, rawB, rawA);
   }
   if (sb < sb1) iter(sb, rawA, rawB);
+  };
+  run(std::false_type{});
+  // some staged x beyond the f16 range (rare): per-row power-of-two pre-scale, second pass
+  if (__syncthreads_or(om[0] >= 0x7C00 || om[1] >= 0x7C00)) {
+    unsigned* xb = reinterpret_cast<unsigned*>(xrow);
+    if (tid < XR) xb[tid] = 0u;
+    __syncthreads();
+    for (int sb2 = sb0; sb2 < sb1; ++sb2) {  // max |x| per staged row (ds_max_u32 on non-negative float bits)
+      load_x(sb2);
+#pragma unroll
+      for (int i = 0; i < XP; ++i) {
+        const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
+        unsigned mx = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = max(mx, max((w[e] << 16) & 0x7FFF0000u, w[e] & 0x7FFF0000u));
+        atomicMax(&xb[(i * NT + tid) >> 5], mx);
+      }
+    }
+    __syncthreads();
+    if (tid < XR) {  // 2^-k with max |x| 2^-k < 2^15 (inf / NaN rows: k = 126, the result stays non-finite)
+      const int ex = (int)(xb[tid] >> 23) - 127;
+      xrow[tid] = __builtin_bit_cast(float, (unsigned)(127 - min(126, max(0, ex - 14))) << 23);
+    }
+    __syncthreads();
+    run(std::true_type{});
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const float un = 1.f / xrow[16 * t + c];  // exact: a power of two
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r][t] *= un;
+    }
+  }
   // C: col m = 16t + c, rows n = 16 gi + 4g + j
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
@@ -551,6 +608,7 @@ __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __r
                                                             long x_stride, Parts parts, int M, int Ntot, int K,
                                                             int sb_per_split) {
   __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<MT>()];
+  __shared__ float xrow[16 * MT];  // per staged x row: power-of-two pre-scale (f16 range guard)
   const int tile = blockIdx.x;
   int pi = 0;
 #pragma unroll
@@ -558,9 +616,9 @@ __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __r
     if (i < parts.n && tile >= parts.p[i].tile0) pi = i;
   const Part& P = parts.p[pi];
   if (QA == QB || P.qt == QA)
-    qgemm2_body<QA, MT, RT, NWAVES>(xs, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+    qgemm2_body<QA, MT, RT, NWAVES>(xs, xrow, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
   else
-    qgemm2_body<QB, MT, RT, NWAVES>(xs, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+    qgemm2_body<QB, MT, RT, NWAVES>(xs, xrow, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
 }
 
 // 33 <= M <= 64 body shape (HIPSERVE_QGEMM_M64, for A/B measurement): 0 = 8 waves x 1
@@ -603,10 +661,12 @@ __global__ __launch_bounds__(64 * NWAVES) void qmoe_kernel(unsigned short* __res
                                                           const float* __restrict__ rs, MoeQ moe, int N, int K,
                                                           int sb_per_split) {
   __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<MT>()];
+  __shared__ float xrow[16 * MT];
   const int e = moe.tile_expert[blockIdx.z];
   if (e < 0) return;
   const Part P{q + (long)e * moe.w_estride, rs != nullptr ? rs + (long)e * moe.rs_estride : nullptr, QT, N, 0, 0};
-  qgemm2_body<QT, MT, RT, NWAVES, true>(xs, out, out_stride, ws, x, x_stride, P, 16 * MT, N, K, sb_per_split, moe);
+  qgemm2_body<QT, MT, RT, NWAVES, true>(xs, xrow, out, out_stride, ws, x, x_stride, P, 16 * MT, N, K, sb_per_split,
+                                        moe);
 }
 
 template <int QT>

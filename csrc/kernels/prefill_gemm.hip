@@ -34,7 +34,7 @@ constexpr int PG_TILE = PG_BM * PG_BK * 2;  // bytes of one operand tile per sta
 // the matching up rows I + 128 tn .. + 127 — no repacked copy of the weight.
 template <int EPI>
 HS_DEVICE int pg_brow(int n0, int tn, int r, int N) {
-  if constexpr (EPI == PG_EPI_GLU) return r < 128 ? tn * 128 + r : (N >> 1) + tn * 128 + (r - 128);
+  if constexpr (EPI == PG_EPI_GLU || EPI == PG_EPI_GEGLU) return r < 128 ? tn * 128 + r : (N >> 1) + tn * 128 + (r - 128);
   return min(n0 + r, N - 1);
 }
 
@@ -69,7 +69,7 @@ HS_DEVICE void pg_epilogue(f32x4 (&acc)[4][8], unsigned char* lds, unsigned shor
         *dst = v;
       }
     }
-  } else if constexpr (EPI == PG_EPI_GLU) {
+  } else if constexpr (EPI == PG_EPI_GLU || EPI == PG_EPI_GEGLU) {
     // tile columns 0..127 = gate rows, 128..255 = the matching up rows (pg_brow).
     // Waves wc = 2, 3 hand their bf16-rounded up values to the
     // gate waves wc = 0, 1 through LDS; act[m, 128 tn + c] = silu(gate) * up.
@@ -96,7 +96,9 @@ HS_DEVICE void pg_epilogue(f32x4 (&acc)[4][8], unsigned char* lds, unsigned shor
           const f32x4 u = *reinterpret_cast<const f32x4*>(ex + ((((wr * 2 + wc) * 8 + i) * 4 + j) * 64 + lane) * 4);
           unsigned short o[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = silu_mul1(f32_to_bf16(acc[j][i][e]), f32_to_bf16(u[e]));
+          for (int e = 0; e < 4; ++e)
+            o[e] = EPI == PG_EPI_GEGLU ? gelu_mul1(f32_to_bf16(acc[j][i][e]), f32_to_bf16(u[e]))
+                                       : silu_mul1(f32_to_bf16(acc[j][i][e]), f32_to_bf16(u[e]));
           uint2 v;
           v.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
           v.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
@@ -348,6 +350,251 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
   pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
 }
 
+// ---- FP8 W8A8 (the FP8-Dynamic checkpoints: per-channel e4m3 weights, per-token
+// dynamic e4m3 activations) on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block
+// scales (E8M0 127): twice the bf16 MFMA rate per clock (MI355X_MICROARCH.md, matrix
+// cores). The pgemm2 structure unchanged in bytes: a K tile is 128 e4m3 = the same
+// 128-byte LDS rows, swizzle and half-tile LDS-DMA pipeline, so a tile costs the same
+// LDS traffic and MFMA cycles as a bf16 tile for twice the K.
+//   * operands: one MFMA takes 32 bytes per lane, the two 16-byte chunks the bf16 loop
+//     fed to its two K=32 MFMAs (chunks fq and 4 + fq of the row); A and B use the same
+//     lane -> k assignment, so the products pair up whatever order the hardware sums in;
+//   * B is read straight from the decode kernel's tiled FP8 layout (no second copy and
+//     no bf16 shadow): 16-byte piece (row n, k 16 c) of K tile kt sits at
+//     [(n >> 4) nsb + kt / 2] 4096 + (c & 3) 1024 + (c >> 2) 256 + (n & 15) 16 + (kt & 1) 512,
+//     a per-lane constant plus a wave-uniform buffer soffset;
+//   * epilogue: acc * xs[m] * rs[n] / 256, then the bf16 store / residual add / GLU.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int EPI>
+__global__ __launch_bounds__(PG_T) void pgemm_f8_kernel(const unsigned char* __restrict__ A, long lda, PgF8 W,
+                                                        unsigned short* __restrict__ C, long ldc, int M, int K,
+                                                        int tiles_m, int tiles_n) {
+  constexpr bool kGlu = EPI == PG_EPI_GLU || EPI == PG_EPI_GEGLU;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * PG_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
+  const int m0 = tm * PG_BM, n0 = tn * PG_BN;
+  const int nk = K >> 7, nsb = K >> 8;
+  // B part of this tile (GLU: gate for tile rows < 128, up above)
+  int pi = 0;
+  if constexpr (!kGlu) {
+#pragma unroll
+    for (int i = 1; i < kPgF8Parts; ++i)
+      if (i < W.n && tn >= W.p[i].tile0) pi = i;
+  }
+  // part row of B tile row r
+  auto prow = [&](int r) {
+    if constexpr (kGlu) return tn * 128 + (r & 127);
+    return (tn - W.p[pi].tile0) * PG_BN + r;
+  };
+  const int pst = kGlu ? (wave >= 4 ? 1 : 0) : pi;  // part this wave stages (rows < 128 <=> wave < 4)
+
+  unsigned int voff[2][2][2];
+  int dst[2][2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j0 = wave * 16 + i * 8, j = j0 + (lane >> 3);
+      const int ra0 = (j0 >> 6) * 128 + h * 64 + (j0 & 63), ra = (j >> 6) * 128 + h * 64 + (j & 63);
+      const int rb0 = (j0 >> 5) * 64 + h * 32 + (j0 & 31), rb = (j >> 5) * 64 + h * 32 + (j & 31);
+      const int lca = (lane & 7) ^ ((ra >> 1) & 7), lcb = (lane & 7) ^ ((rb >> 1) & 7);
+      const int n = prow(rb);
+      voff[0][h][i] = (unsigned)((long)min(m0 + ra, M - 1) * lda + lca * 16);
+      voff[1][h][i] = (unsigned)(((long)(n >> 4) * nsb) * 4096 + (lcb & 3) * 1024 + (lcb >> 2) * 256 + (n & 15) * 16);
+      dst[0][h][i] = ra0 * 128;
+      dst[1][h][i] = PG_TILE + rb0 * 128;
+    }
+  const __amdgpu_buffer_rsrc_t rsrc[2] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min((long)M * lda, 0x7fffffffL), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)W.p[pst].q, 0, (int)min((long)W.p[pst].rows * K, 0x7fffffffL),
+                                        0x00020000)};
+  auto stage_half = [&](int op, int h, int buf, int kt) {
+    const int so = op == 0 ? kt * 128 : (kt >> 1) * 4096 + (kt & 1) * 512;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc[op], (lds_ptr_t)(lds + buf * 2 * PG_TILE + dst[op][h][i]), 16,
+                                               voff[op][h][i], so, 0, 0);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fr >> 1) & 7;
+  const int a_off = (wr * 128 + fr) * 128, b_off = PG_TILE + (wc * 64 + fr) * 128;
+  const int chs[2] = {((0 + fq) ^ sw) * 16, ((4 + fq) ^ sw) * 16};
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment registers as pgemm2_kernel, one 8-VGPR tuple per fragment (the MFMA
+  // operand as is). Schedule: a tile's A0 / B0 fragments are read at its phase 0 (not
+  // in the previous tile's phase 3: with the scaled MFMA that variant needs > 256
+  // VGPRs and spills); B1 behind phase 0's first 4 MFMAs, A1 behind phase 1's. LDS-DMA
+  // of tile kt + 2: A0 / B0 halves at phase 1 (after the barrier that closes phase 0's
+  // reads), A1 / B1 halves at phase 2. Waits as pgemm2: end of phase 3 -> all of tile
+  // kt + 1 landed (vmcnt 8). Barriers after every phase.
+  i32x8 bfr[4], afr[2][4];
+  auto rd = [&](const unsigned char* p) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(p + chs[0]), hi = *reinterpret_cast<const u32x4*>(p + chs[1]);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  auto read_b = [&](const unsigned char* sb, int qn) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) bfr[2 * qn + jj] = rd(sb + b_off + (2 * qn + jj) * 2048);
+  };
+  auto read_a = [&](const unsigned char* sb, int qm) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) afr[qm][ii] = rd(sb + a_off + (4 * qm + ii) * 2048);
+  };
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  stage_half(0, 0, 0, 0);
+  stage_half(1, 0, 0, 0);
+  stage_half(0, 1, 0, 0);
+  stage_half(1, 1, 0, 0);
+  if (nk > 1) {
+    stage_half(0, 0, 1, 1);
+    stage_half(1, 0, 1, 1);
+    stage_half(0, 1, 1, 1);
+    stage_half(1, 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const unsigned char* sb = lds + buf * 2 * PG_TILE;
+    const bool more2 = kt + 2 < nk, more1 = kt + 1 < nk;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int qm = p >> 1, qn = p & 1;
+      if (p == 0) {
+        read_a(sb, 0);
+        read_b(sb, 0);
+      }
+      if (p == 1 && more2) {
+        stage_half(0, 0, buf, kt + 2);
+        stage_half(1, 0, buf, kt + 2);
+      }
+      if (p == 2 && more2) {
+        stage_half(0, 1, buf, kt + 2);
+        stage_half(1, 1, buf, kt + 2);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        if (jj == 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (p == 0) read_b(sb, 1);
+          if (p == 1) read_a(sb, 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+          acc[2 * qn + jj][4 * qm + ii] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              bfr[2 * qn + jj], afr[qm][ii], acc[2 * qn + jj][4 * qm + ii], 0, 0, 0, 127, 0, 127);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      if (p == 2) {
+        if (more2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if (more1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (p == 3) {
+        if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      barrier();
+    }
+  }
+  // dequantise: acc * xs[m] * rs[n] / 256 (rs carries the decode path's x 256)
+  {
+    const float* rs = W.p[kGlu ? (wc >= 2 ? 1 : 0) : pi].rs;
+    f32x4 wsc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wsc[j] = *reinterpret_cast<const f32x4*>(rs + prow(wc * 64 + j * 16 + 4 * fq));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xsc = W.xs[min(m0 + wr * 128 + i * 16 + fr, M - 1)] * 0.00390625f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j][i] *= wsc[j] * xsc;
+    }
+  }
+  pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
+}
+
+bool launch_prefill_gemm_f8(int epi, void* C, long ldc, const void* A, long lda, const PgF8& W, int M, int N, int K,
+                            hipStream_t s) {
+  if (M < 1 || K % 256 || W.n < 1 || W.n > kPgF8Parts) return false;
+  const bool glu = epi == PG_EPI_GLU || epi == PG_EPI_GEGLU;
+  if (glu) {
+    if (W.n != 2 || W.p[0].rows != W.p[1].rows || W.p[0].rows % 128 || N != 2 * W.p[0].rows) return false;
+  } else {
+    int rows = 0;
+    for (int i = 0; i < W.n; ++i) {
+      if (W.p[i].rows % PG_BN || W.p[i].tile0 * PG_BN != rows) return false;
+      rows += W.p[i].rows;
+    }
+    if (rows != N) return false;
+  }
+  const int tiles_m = (M + PG_BM - 1) / PG_BM, tiles_n = N / PG_BN;
+  const dim3 grid(tiles_m * tiles_n);
+  auto* a = static_cast<const unsigned char*>(A);
+  auto* c = static_cast<unsigned short*>(C);
+  switch (epi) {
+    case PG_EPI_STORE: pgemm_f8_kernel<PG_EPI_STORE><<<grid, PG_T, 0, s>>>(a, lda, W, c, ldc, M, K, tiles_m, tiles_n); return true;
+    case PG_EPI_ADD: pgemm_f8_kernel<PG_EPI_ADD><<<grid, PG_T, 0, s>>>(a, lda, W, c, ldc, M, K, tiles_m, tiles_n); return true;
+    case PG_EPI_GLU: pgemm_f8_kernel<PG_EPI_GLU><<<grid, PG_T, 0, s>>>(a, lda, W, c, ldc, M, K, tiles_m, tiles_n); return true;
+    case PG_EPI_GEGLU: pgemm_f8_kernel<PG_EPI_GEGLU><<<grid, PG_T, 0, s>>>(a, lda, W, c, ldc, M, K, tiles_m, tiles_n); return true;
+    default: return false;
+  }
+}
+
+// Per-token dynamic e4m3: one workgroup per row, max |x| then x * 448 / max saturated
+// to +-448 and converted in pairs by v_cvt_pk_fp8_f32 (OCP e4m3fn, round to nearest even).
+__global__ __launch_bounds__(256) void act_quant_fp8_kernel(unsigned char* __restrict__ q, float* __restrict__ xs,
+                                                            const unsigned short* __restrict__ x, long x_stride, int K) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  const unsigned short* xr = x + row * x_stride;
+  float amax = 0.f;
+  for (int c = threadIdx.x * 8; c < K; c += 256 * 8) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(xr + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(bf16_to_f32(v[e])));
+  }
+  amax = block_max(amax, red);
+  const float inv = amax > 0.f ? 448.f / amax : 1.f;
+  if (threadIdx.x == 0) xs[row] = amax > 0.f ? amax / 448.f : 1.f;
+  for (int c = threadIdx.x * 8; c < K; c += 256 * 8) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(xr + c);
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = __builtin_amdgcn_fmed3f(bf16_to_f32(v[e]) * inv, -448.f, 448.f);
+    uint2 o;
+    o.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    o.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], (int)o.x, true);
+    o.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+    o.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], (int)o.y, true);
+    *reinterpret_cast<uint2*>(q + row * K + c) = o;
+  }
+}
+
+void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s) {
+  if (M < 1) return;
+  act_quant_fp8_kernel<<<M, 256, 0, s>>>(static_cast<unsigned char*>(q), xs, static_cast<const unsigned short*>(x),
+                                         x_stride, K);
+}
+
 static bool pg_shape_ok(int M, int N, int K) { return M >= 1 && N % PG_BN == 0 && K % PG_BK == 0 && K >= PG_BK; }
 
 bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
@@ -370,6 +617,7 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
       case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       case PG_EPI_ADD: pgemm2_kernel<PG_EPI_ADD, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_GEGLU: pgemm2_kernel<PG_EPI_GEGLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       default: return false;
     }
   }

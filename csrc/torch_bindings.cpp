@@ -672,6 +672,47 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
               "prefill_gemm: unsupported");
 }
 
+// FP8 W8A8 form: xq [M, K] uint8 e4m3 + xs [M] fp32 (act_quant_fp8), the weight as
+// tiled FP8 parts (ops/quant.py QuantPart.from_fp8: q [N/16, K/256, 4096] uint8 and
+// rs [N] fp32) stacked along N. epi 0 / 1 as prefill_gemm; 2 / 3: parts = (gate, up),
+// out = act [M, I] = silu / gelu_tanh(gate) * up.
+void prefill_gemm_f8(at::Tensor& out, const at::Tensor& xq, const at::Tensor& xs, const std::vector<at::Tensor>& q,
+                     const std::vector<at::Tensor>& rs, int64_t epi) {
+  CHECK_DEV(xq); CHECK_CONTIG(xq); CHECK_CONTIG(xs); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(xq.scalar_type() == at::kByte && xs.scalar_type() == at::kFloat, "prefill_gemm_f8: xq uint8, xs fp32");
+  const int M = xq.size(0), K = xq.size(1);
+  TORCH_CHECK(xs.numel() == M && K % 256 == 0 && out.stride(0) % 4 == 0, "prefill_gemm_f8: shapes");
+  TORCH_CHECK(!q.empty() && q.size() <= (size_t)hipserve::kPgF8Parts && rs.size() == q.size(), "prefill_gemm_f8: parts");
+  hipserve::PgF8 W{};
+  W.n = (int)q.size();
+  W.xs = xs.data_ptr<float>();
+  int rows = 0;
+  for (size_t i = 0; i < q.size(); ++i) {
+    CHECK_CONTIG(q[i]); CHECK_CONTIG(rs[i]);
+    const int n = rs[i].numel();
+    TORCH_CHECK(q[i].scalar_type() == at::kByte && rs[i].scalar_type() == at::kFloat && q[i].numel() == (long)n * K,
+                "prefill_gemm_f8: part ", i, " must be tiled FP8 [N/16, K/256, 4096] with rs [N]");
+    W.p[i] = hipserve::PgF8Part{q[i].data_ptr<uint8_t>(), rs[i].data_ptr<float>(), n, rows / 256};
+    rows += n;
+  }
+  const bool glu = epi == 2 || epi == 3;
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? rows / 2 : rows), "prefill_gemm_f8: out shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(xq.device());
+  TORCH_CHECK(hipserve::launch_prefill_gemm_f8((int)epi, out.data_ptr(), out.stride(0), xq.data_ptr(), K, W, M, rows, K,
+                                               cur_stream()),
+              "prefill_gemm_f8: unsupported part shapes (rows % 256; GLU: two equal parts, rows % 128)");
+}
+
+void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_CONTIG(xq); CHECK_CONTIG(xs);
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(xq.scalar_type() == at::kByte && xq.size(0) == M && xq.size(1) == K && xs.scalar_type() == at::kFloat &&
+                  xs.numel() == M && K % 8 == 0 && x.stride(0) % 8 == 0,
+              "act_quant_fp8: xq uint8 [M, K], xs fp32 [M], K % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_act_quant_fp8(xq.data_ptr(), xs.data_ptr<float>(), x.data_ptr(), x.stride(0), M, K, cur_stream());
+}
+
 // Grouped (MoE prefill) form: x [tiles * 256, K] expert-sorted rows (moe_align with
 // tile 256, moe_gather), w [E, N, K] (GLU: each expert's merged [gate; up] weight),
 // tile_expert [tiles] int32 from moe_align. No host synchronisation.
@@ -1069,6 +1110,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
+  m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
+  m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
   m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
         "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
@@ -1117,6 +1160,8 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm_glu", &decode_gemm_glu);
   m.impl("decode_gemm_fused", &decode_gemm_fused);
   m.impl("prefill_gemm", &prefill_gemm);
+  m.impl("prefill_gemm_f8", &prefill_gemm_f8);
+  m.impl("act_quant_fp8", &act_quant_fp8);
   m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -269,7 +269,7 @@ class ModelRunner:
                 continue
             if kind == "add" and (self.tp.world_size > 1 or getattr(lw, "post_attn_norm", None) is not None):
                 continue
-            if kind == "glu" and (self.mcfg.hidden_act != "silu" or (w.shape[0] // 2) % 128):
+            if kind == "glu" and (self.mcfg.hidden_act not in ("silu", "gelu_tanh") or (w.shape[0] // 2) % 128):
                 continue
             units.add((kind, w.shape[0], w.shape[1]))
         if lw.w13 is not None and pgemm.moe_ok(lw.w13, lw.w2) and self.mcfg.hidden_act == "silu":

@@ -560,8 +560,12 @@ class LlamaModel:
             if lw.router is not None:
                 h = self.moe(xn, lw)
             else:
-                act = (pgemm.gemm_glu(xn, lw.wgu) if cfg.hidden_act == "silu" and pgemm.use("glu", lw.wgu, T)
-                       else None)
+                gelu = cfg.hidden_act == "gelu_tanh"
+                act = None
+                if pgemm.f8_use(lw.wgu, T, glu=True):  # FP8 gate|up: GLU in the e4m3 GEMM's epilogue
+                    act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2)
+                elif cfg.hidden_act in ("silu", "gelu_tanh") and pgemm.use("glu", lw.wgu, T):
+                    act = pgemm.gemm_glu(xn, lw.wgu, gelu)
                 if act is None:
                     gu = self.linear(xn, lw.wgu)
                     act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)

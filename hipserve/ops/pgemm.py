@@ -58,11 +58,62 @@ def gemm_add_(residual: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch
     return residual
 
 
-def gemm_glu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """act = silu(x @ Wg.T) * (x @ Wu.T) for the merged w = [Wg; Wu]."""
+def gemm_glu(x: torch.Tensor, w: torch.Tensor, gelu: bool = False) -> torch.Tensor:
+    """act = silu(x @ Wg.T) * (x @ Wu.T) for the merged w = [Wg; Wu] (gelu: tanh-GELU,
+    Gemma's GeGLU)."""
     act = torch.empty(x.shape[0], w.shape[0] // 2, device=x.device, dtype=x.dtype)
-    torch.ops.hipserve.prefill_gemm(act, x, w, 2)
+    torch.ops.hipserve.prefill_gemm(act, x, w, 3 if gelu else 2)
     return act
+
+
+# ---- FP8 W8A8 prefill (the FP8-Dynamic checkpoints): per-token e4m3 activations x
+# the e4m3 weights in the decode kernel's tiled layout, on the scaled FP8 MFMA
+# (prefill_gemm.hip pgemm_f8_kernel). No bf16 shadow of the weights is needed.
+FP8_MODE = os.environ.get("HIPSERVE_FP8_PREFILL", "1")
+F8_MIN_ROWS = 128
+
+
+def _f8_parts(w):
+    from . import quant as Q
+    if not isinstance(w, Q.QuantWeight) or not w.parts or not w.parts[0].q.is_cuda:
+        return None
+    if any(p.qtype != Q.FP8 or not p.tiled or p.K % 256 for p in w.parts) or len(w.parts) > 4:
+        return None
+    return w.parts
+
+
+def f8_fits(w, glu: bool = False) -> bool:
+    ps = _f8_parts(w)
+    if ps is None or FP8_MODE == "0" or not hasattr(torch.ops.hipserve, "prefill_gemm_f8"):
+        return False
+    if glu:
+        return len(ps) == 2 and ps[0].N == ps[1].N and ps[0].N % 128 == 0
+    return all(p.N % 256 == 0 for p in ps)
+
+
+def f8_use(w, M: int, glu: bool = False) -> bool:
+    return M >= F8_MIN_ROWS and f8_fits(w, glu)
+
+
+def act_quant(x: torch.Tensor):
+    """Per-token dynamic e4m3: (xq uint8 [M, K], xs fp32 [M]) with x ~= e4m3(xq) * xs."""
+    xq = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    xs = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    torch.ops.hipserve.act_quant_fp8(xq, xs, x)
+    return xq, xs
+
+
+def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """epi 0: out = x @ W^T (bf16 [M, N]); 1: out (the residual) += x @ W^T;
+    2 / 3: W = (gate, up) parts, out = silu / gelu_tanh(x Wg^T) * (x Wu^T)."""
+    ps = w.parts
+    M = x.shape[0]
+    if out is None:
+        n = ps[0].N if epi in (2, 3) else w.N
+        out = torch.empty(M, n, dtype=torch.bfloat16, device=x.device)
+    xq, xs = act_quant(x)
+    torch.ops.hipserve.prefill_gemm_f8(out, xq, xs, [p.q for p in ps], [p.rs for p in ps], epi)
+    return out
 
 
 def moe_fits(w13, w2) -> bool:

@@ -493,6 +493,9 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
                                          p.N, p.K, ws, sp)
             off += p.N
         return out
+    from . import pgemm
+    if pgemm.f8_use(w, M):  # FP8 W8A8 on the scaled e4m3 MFMA, straight from the tiled weights
+        return pgemm.f8_gemm(x, w, 0, out)
     if w.dense is not None:  # prefill on the resident bf16 copy: no per-call dequant pass
         return torch.nn.functional.linear(x, w.dense)
     if w.v2 and x.is_cuda and M <= QPREFILL_MAX_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
@@ -520,10 +523,11 @@ def make_dense_shadows(weights, device, reserve_bytes: int) -> int:
 
     if os.environ.get("HIPSERVE_QUANT_SHADOW", "1") == "0" or torch.device(device).type != "cuda":
         return 0
+    from . import pgemm
     added = 0
     for w in sorted(weights, key=lambda w: -w.N * w.K):
-        if w.dense is not None:
-            continue
+        if w.dense is not None or pgemm.f8_fits(w) or pgemm.f8_fits(w, glu=True):
+            continue  # FP8 prefill runs on the e4m3 MFMA from the quantised weights
         need = w.N * w.K * 2
         free, _ = torch.cuda.mem_get_info(device)
         if free - need < reserve_bytes:

@@ -18,6 +18,12 @@ run_tests() {
   tail -n 15 $OUT/pytest_gpu.log
   return $rc
 }
+run_one() {  # one GPU test file
+  local n; n=$(basename "$1" .py)
+  timeout -k 10 300 python -u -m pytest "$1" -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+    > $OUT/$n.log 2>&1
+  local rc=$?; tail -n 15 $OUT/$n.log; return $rc
+}
 run_smoke() {
   timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   local rc=$?; tail -n 3 $OUT/smoke.log; return $rc
@@ -53,8 +59,9 @@ prof_run() {
   return 0
 }
 run_pgemm() {
-  timeout -k 10 300 python -u tools/bench_pgemm.py --model ${PG_MODEL:-8b} > $OUT/bench_pgemm.log 2>&1
-  local rc=$?; tail -n 8 $OUT/bench_pgemm.log; return $rc
+  local m=${1:-8b}
+  timeout -k 10 300 python -u tools/bench_pgemm.py --model $m --fp8 > $OUT/bench_pgemm_$m.log 2>&1
+  local rc=$?; tail -n 8 $OUT/bench_pgemm_$m.log; return $rc
 }
 run_bench_mixtral() {
   timeout -k 10 600 python -u bench.py --model mixtral-8x7b --concurrency 32 --out $OUT/bench_mixtral.json \
@@ -72,7 +79,10 @@ for s in $steps; do
     bench) run_bench ;;
     bench_q4) run_bench_q4 ;;
     bench_mixtral) run_bench_mixtral ;;
-    pgemm) run_pgemm ;;
+    pgemm) run_pgemm 8b ;;
+    pgemm_g27) run_pgemm gemma27b ;;
+    f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
+    f16test) run_one tests/test_gguf_gpu.py ;;
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;

@@ -430,3 +430,53 @@ def test_mfma_v2_m64_every_slice_length(qt, S):
     got = ws.view(ny, M, qw.N).sum(0)
     assert torch.isfinite(got).all()
     assert (got - want).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K, G.Q8_0])
+@pytest.mark.parametrize("M", [1, 16, 64, 130])
+def test_mfma_v2_beyond_f16_range(qt, M):
+    """x rows holding values past the f16 range (|x| > 1e5, up to 3e6) through the f16
+    MFMA kernel: the overflow is caught on staging and the workgroup reruns with
+    power-of-two row pre-scales — no saturation at 65504. Rows
+    of ordinary magnitude in the same launch keep full accuracy."""
+    from hipserve.ops.quant import quant_partial
+    K = 2048
+    qw, raws = _rand_qw([(qt, 512, K), (qt, 256, K)], seed=7 + M)
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = torch.randn(M, K, device="cuda", generator=g)
+    big = list(range(0, M, 3))
+    x[big] *= torch.logspace(5, 6.5, len(big), device="cuda").unsqueeze(1)  # 1e5 .. 3e6 scale rows
+    x[M // 2, 5] = 2.0e5  # one outlier in an otherwise ordinary row
+    x = x.to(torch.bfloat16)
+    want = x.float() @ _dense(raws).T
+    rowmax = want.abs().amax(1, keepdim=True)
+    y = quant_linear(x, qw).float()
+    assert torch.isfinite(y).all()
+    err = ((y - want).abs() / rowmax).max().item()
+    assert err < 1e-2, err
+    if M <= 64:  # split-K partials (the fused decode epilogues' input) too
+        ws, S = quant_partial(x, qw)
+        part = ws.view(S, M, qw.N).sum(0)
+        assert ((part - want).abs() / rowmax).max().item() < 1e-2
+
+
+def test_fp8_linear_beyond_f16_range():
+    """FP8 e4m3 weights (the Gemma-3-27B FP8-Dynamic path) with activations past the
+    f16 range, decode-sized M (f16 MFMA kernel) and prefill-sized M (e4m3 MFMA with
+    per-token scales)."""
+    from hipserve.ops import quant as Q
+    N, K = 512, 2048
+    w = torch.randn(N, K, device="cuda") * 0.02
+    s = w.abs().amax(1, keepdim=True) / 448.0
+    q = (w / s).to(torch.float8_e4m3fn)
+    qw = Q.QuantWeight([Q.QuantPart.from_fp8(q, s, "cuda")])
+    wd = q.float() * s
+    for M in (8, 64, 300):
+        x = torch.randn(M, K, device="cuda")
+        x[::2] *= 3e5
+        x = x.to(torch.bfloat16)
+        want = x.float() @ wd.T
+        y = Q.quant_linear(x, qw).float()
+        assert torch.isfinite(y).all()
+        rel = ((y - want).norm(dim=1) / want.norm(dim=1)).max().item()
+        assert rel < (5e-2 if M > 64 else 1e-2), (M, rel)

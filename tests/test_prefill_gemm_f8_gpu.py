@@ -1,0 +1,135 @@
+"""FP8 W8A8 prefill GEMM (csrc/kernels/prefill_gemm.hip pgemm_f8_kernel, the scaled
+e4m3 MFMA over the decode kernel's tiled FP8 weights) and the per-token dynamic
+activation quantiser, each against a plain PyTorch fp32 reference of the same op:
+the reference dequantises the kernel's own e4m3 activations (so only the GEMM is
+compared) and the e4m3 weights, multiplies in fp32 and applies the same epilogue.
+Ragged M, multi-part (q|k|v-like) weights, residual add, SiLU- and GELU-GLU."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    from hipserve.ops import load_library
+
+    load_library()
+
+
+def _fp8_weight(g, N, K):
+    from hipserve.ops import quant as Q
+
+    w = (torch.rand(N, K, device=DEV, generator=g) * 2 - 1) * (0.02 + torch.rand(N, 1, device=DEV, generator=g))
+    s = w.abs().amax(1, keepdim=True) / 448.0
+    q = (w / s).to(torch.float8_e4m3fn)
+    return Q.QuantPart.from_fp8(q, s, DEV), q.float() * s
+
+
+def _weight(g, rows, K):
+    from hipserve.ops import quant as Q
+
+    parts = [_fp8_weight(g, n, K) for n in rows]
+    return Q.QuantWeight([p for p, _ in parts]), torch.cat([d for _, d in parts])
+
+
+def _x(g, M, K):
+    x = torch.rand(M, K, device=DEV, generator=g) * 2 - 1
+    x = x * torch.logspace(-2, 2, M, device=DEV).unsqueeze(1)  # rows of very different magnitude
+    x[M // 2] = 0.0
+    return x.to(torch.bfloat16)
+
+
+def _deq_x(xq, xs):
+    return xq.view(torch.float8_e4m3fn).float() * xs.unsqueeze(1)
+
+
+def test_act_quant_fp8():
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    M, K = 777, 5376
+    x = _x(g, M, K)
+    x[5, 17] = 1.5e5  # beyond the f16 range: a per-row scale takes it
+    xq, xs = pgemm.act_quant(x)
+    amax = x.float().abs().amax(1)
+    want_s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    torch.testing.assert_close(xs, want_s, rtol=1e-6, atol=0)
+    ref = (x.float() / want_s.unsqueeze(1)).clamp(-448, 448).to(torch.float8_e4m3fn).float()
+    got = xq.view(torch.float8_e4m3fn).float()
+    assert torch.isfinite(got).all()
+    diff = (got != ref)
+    # x * (448 / max) vs x / (max / 448): a value on an e4m3 rounding midpoint may go either way
+    assert diff.float().mean().item() < 5e-3
+    step = torch.where(ref.abs() > 0, ref.abs() / 8, torch.full_like(ref, 2.0 ** -9))
+    assert ((got - ref).abs() <= step + 1e-12)[diff].all()
+    assert (got.abs().amax(1)[amax > 0] == 448).all()
+
+
+@pytest.mark.parametrize("M,rows,K", [(300, [256], 256), (1000, [512, 256, 256], 1024), (2049, [768], 512),
+                                      (4096, [1024, 256], 4096), (130, [256], 5376)])
+def test_prefill_gemm_f8_store(M, rows, K):
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    w, wd = _weight(g, rows, K)
+    x = _x(g, M, K)
+    xq, xs = pgemm.act_quant(x)
+    out = torch.full((M, sum(rows)), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm_f8(out, xq, xs, [p.q for p in w.parts], [p.rs for p in w.parts], 0)
+    want = _deq_x(xq, xs) @ wd.t()
+    scale = want.abs().amax(1, keepdim=True).clamp_min(1e-30)
+    torch.testing.assert_close(out.float() / scale, want / scale, rtol=0, atol=1e-2)
+    # the pgemm.f8_gemm wrapper (quantises x itself) gives the same result
+    out2 = pgemm.f8_gemm(x, w)
+    assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 1024), (1000, 512, 512)])
+def test_prefill_gemm_f8_residual_add(M, N, K):
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(5 + M)
+    w, wd = _weight(g, [N], K)
+    x = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    res0 = (torch.rand(M, N, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    xq, xs = pgemm.act_quant(x)
+    res = res0.clone()
+    torch.ops.hipserve.prefill_gemm_f8(res, xq, xs, [w.parts[0].q], [w.parts[0].rs], 1)
+    h = (_deq_x(xq, xs) @ wd.t()).to(torch.bfloat16).float()
+    want = (h + res0.float()).to(torch.bfloat16).float()
+    torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu"])
+@pytest.mark.parametrize("M,I,K", [(300, 128, 512), (1000, 384, 1024), (2049, 256, 256)])
+def test_prefill_gemm_f8_glu(M, I, K, act):
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(11 + M + I)
+    w, wd = _weight(g, [I, I], K)
+    x = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    xq, xs = pgemm.act_quant(x)
+    out = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm_f8(out, xq, xs, [p.q for p in w.parts], [p.rs for p in w.parts],
+                                       2 if act == "silu" else 3)
+    gu = (_deq_x(xq, xs) @ wd.t()).to(torch.bfloat16).float()
+    gate = gu[:, :I]
+    f = torch.nn.functional.silu(gate) if act == "silu" else torch.nn.functional.gelu(gate, approximate="tanh")
+    want = f * gu[:, I:]
+    torch.testing.assert_close(out.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
+
+
+def test_quant_linear_prefill_uses_f8():
+    """quant_linear at prefill sizes runs the FP8 MFMA path, not a bf16 shadow."""
+    from hipserve.ops import quant as Q
+
+    g = torch.Generator(device=DEV).manual_seed(1)
+    w, wd = _weight(g, [512, 256, 256], 2048)
+    assert w.dense is None
+    x = (torch.rand(1024, 2048, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    y = Q.quant_linear(x, w)
+    want = x.float() @ wd.t()
+    rel = (y.float() - want).norm() / want.norm()
+    assert rel < 5e-2, rel  # e4m3 activations: ~2.6 % RMS relative rounding per element

@@ -27,14 +27,15 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--model", default="8b")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--fp8", action="store_true", help="also the FP8 W8A8 kernel (act quant + e4m3 MFMA GEMM)")
     a = ap.parse_args()
     from hipserve.ops import KernelOps
 
     ops = KernelOps()
     op = torch.ops.hipserve
     dev = "cuda"
-    H, I, NQKV = (4096, 14336, 6144) if a.model == "8b" else (8192, 3584, 1280)
-    HO = 4096 if a.model == "8b" else 1024
+    H, I, NQKV, HO = {"8b": (4096, 14336, 6144, 4096), "70b-tp8": (8192, 3584, 1280, 1024),
+                      "gemma27b": (5376, 21504, 8192, 4096)}[a.model]
     shapes = {"qkv": (NQKV, H), "o": (H, HO), "gu": (2 * I, H), "down": (H, I)}
     M, L = a.m, a.layers
 
@@ -65,6 +66,18 @@ def main():
         r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
              "pgemm_v1_ms": round(t_v1, 4),
              "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1)}
+        if a.fp8:
+            from hipserve.ops import pgemm, quant as Q
+
+            qws = []
+            for w in ws:
+                sc = w.float().abs().amax(1, keepdim=True) / 448.0
+                qws.append(Q.QuantWeight([Q.QuantPart.from_fp8((w.float() / sc).to(torch.float8_e4m3fn), sc, dev)]))
+            t_q = time_fn(lambda: [pgemm.act_quant(x) for _ in qws])
+            t_f8 = time_fn(lambda: [pgemm.f8_gemm(x, q, 0, out) for q in qws])
+            r.update({"fp8_ms": round(t_f8, 4), "fp8_quant_ms": round(t_q, 4),
+                      "fp8_TFs": round(2 * M * N * K / t_f8 / 1e9, 1)})
+            del qws
         if name == "gu":  # GEMM + SiLU-GLU unit
             act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
             wg = ws  # the GLU epilogue reads the merged [gate; up] weight as stored
@@ -86,11 +99,13 @@ def main():
         print(json.dumps(r), flush=True)
         del ws, x, out
         torch.cuda.empty_cache()
-    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | prefill_gemm ms (TF/s) | unit: hipBLASLt + ew | unit: fused |")
-    print("|---|---|---:|---:|---:|---:|")
+    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | prefill_gemm ms (TF/s) | unit: hipBLASLt + ew | unit: fused "
+          f"| FP8 quant + GEMM ms (TF/s) |")
+    print("|---|---|---:|---:|---:|---:|---:|")
     for r in rows:
+        f8 = f"{r['fp8_ms']} ({r['fp8_TFs']})" if "fp8_ms" in r else "—"
         print(f"| {r['shape']} | {r['M']}x{r['N']}x{r['K']} | {r['blas_ms']} ({r['blas_TFs']}) | "
-              f"{r['pgemm_ms']} ({r['pgemm_TFs']}) | {r.get('blas_unit_ms', '—')} | {r.get('pgemm_unit_ms', '—')} |")
+              f"{r['pgemm_ms']} ({r['pgemm_TFs']}) | {r.get('blas_unit_ms', '—')} | {r.get('pgemm_unit_ms', '—')} | {f8} |")
 
 
 if __name__ == "__main__":
