@@ -49,7 +49,7 @@ run_bench_q4() {
 prof_run() {
   local here=$PWD name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/$name \
-     -o run -- python3 $here/bench.py --path engine --steps 1 --warmup 1 "$@" > $here/$OUT/$name.log 2>&1)
+     -o run -- python3 $here/bench.py --path engine --steps 1 --warmup 1 --tp-phase off "$@" > $here/$OUT/$name.log 2>&1)
   local rc=$?; tail -n 3 $OUT/$name.log
   [ $rc -eq 0 ] || return $rc
   local db; db=$(find $OUT/$name -name '*results.db' | head -n 1)
@@ -62,6 +62,16 @@ run_pgemm() {
   local m=${1:-8b}
   timeout -k 10 300 python -u tools/bench_pgemm.py --model $m --fp8 > $OUT/bench_pgemm_$m.log 2>&1
   local rc=$?; tail -n 8 $OUT/bench_pgemm_$m.log; return $rc
+}
+# bench_named <name> <env assignments...> -- <bench args...>
+bench_named() {
+  local name=$1; shift
+  local envs=()
+  while [ $# -gt 0 ] && [ "$1" != "--" ]; do envs+=("$1"); shift; done
+  shift
+  timeout -k 10 600 env "${envs[@]}" python -u bench.py --tp-phase off --out $OUT/bench_$name.json "$@" \
+    > $OUT/bench_$name.log 2>&1
+  local rc=$?; tail -n 2 $OUT/bench_$name.log; return $rc
 }
 run_bench_mixtral() {
   timeout -k 10 600 python -u bench.py --model mixtral-8x7b --concurrency 32 --out $OUT/bench_mixtral.json \
@@ -80,6 +90,11 @@ for s in $steps; do
     bench_q4) run_bench_q4 ;;
     bench_mixtral) run_bench_mixtral ;;
     pgemm) run_pgemm 8b ;;
+    g27fp8) bench_named g27fp8 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b --quantization fp8 ;;
+    g27fp8_shadow) bench_named g27fp8_shadow HIPSERVE_FP8_PREFILL=0 -- --model gemma-3-27b --quantization fp8 ;;
+    g27bf16) bench_named g27bf16 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b ;;
+    q4km) bench_named q4km HIPSERVE_QUANT_SHADOW=1 -- --quantization q4_k_m ;;
+    q4km_noshadow) bench_named q4km_noshadow HIPSERVE_QUANT_SHADOW=0 -- --quantization q4_k_m ;;
     pgemm_g27) run_pgemm gemma27b ;;
     f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
     f16test) run_one tests/test_gguf_gpu.py ;;

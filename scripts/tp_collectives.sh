@@ -15,6 +15,9 @@ steps="${*:-ar2 ar8 trace8}"
 
 ar() {  # ar <world> <hidden>
   local w=$1 h=$2
+  # one HW queue per process (see trace8): 8 ranks x 4 queues oversubscribe the
+  # device's queue slots and the CP time-slices spin-waiting collective kernels
+  export GPU_MAX_HW_QUEUES=1
   for g in "" "--graph"; do
     timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $w --master-addr 127.0.0.1 \
       --master-port 29$((500 + w)) tools/bench_allreduce.py --shared-gpu --iters 20 --norm $h $g \
