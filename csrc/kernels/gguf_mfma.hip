@@ -205,6 +205,26 @@ HS_DEVICE int kbase(int g, int s) {
   }
 }
 
+// Subnormal-integer dequant (Dec::sub_ints / step): the integer q of a weight is
+// placed at bit kSub of an f16 (q << kSub < 1024: a subnormal, exactly q 2^(kSub-24)),
+// and ONE v_pk_fma per pair computes q * (d 2^(24-kSub)) + c, where c holds the
+// format's zero point (-8 d, -32 d, -128 d) or the K-quant min. Every factor is a
+// power-of-two multiple of the f16-rounded scale, so the weights are bit-identical to
+// the magic-number path (1024 + q, v_pk_add -1024, v_pk_fma) at 2 instead of 3 ops per
+// pair word and no v_pk_add. Range: d 2^(24-kSub) must stay below 65504 —
+// ops/quant.py sub_scale_ok() checks every block's scale at load (Q4_K / Q4_0 / Q4_1
+// d sc < 0.25, Q5_K < 0.125, Q6_K < 0.0625, Q8_0 < 0.0156) and sends weights beyond
+// it to the v1 kernel.
+template <int QT>
+constexpr int sub_shift() { return QT == Q5_K ? 5 : QT == Q6_K ? 4 : QT == Q8_0 ? 2 : 6; }
+template <int QT>
+constexpr float sub_up() {
+  return QT == Q4_K || QT == Q5_K || QT == Q6_K || QT == Q8_0 || QT == Q4_0 || QT == Q4_1
+             ? (float)(1 << (24 - sub_shift<QT>())) : 1.f;
+}
+template <int QT>
+constexpr float sub_zero() { return QT == Q4_0 ? -8.f : QT == Q6_K ? -32.f : QT == Q8_0 ? -128.f : 0.f; }
+
 // Decode step s (8 weights) of the lane's super-chunk. ints(): the 8 quantised
 // integers (minus the format's zero point) as exact f16, pair order; step(): the
 // weights in f16 (one v_pk_fma per pair with the block scale / min); scale():
@@ -244,10 +264,19 @@ struct Dec {
         fcB = h2f(r.h[3]);
       }
     }
-    dA = splat(fdA);
-    dB = splat(fdB);
-    cA = splat(fcA);
-    cB = splat(fcB);
+    // step(): integers enter as subnormal f16 q 2^(kSub - 24) (sub_ints), so the
+    // scale pairs carry 2^(24 - kSub) and the zero point moves into the FMA addend
+    // (exact: power-of-two multiples of the f16-rounded scale)
+    constexpr float up = sub_up<QT>(), zp = sub_zero<QT>();
+    dA = splat(fdA * up);
+    dB = splat(fdB * up);
+    if constexpr (QT == Q4_0 || QT == Q8_0) {
+      cA = splat(zp * (float)(_Float16)fdA);
+      cB = splat(zp * (float)(_Float16)fdB);
+    } else {
+      cA = splat(fcA);
+      cB = splat(fcB);
+    }
   }
 
   HS_DEVICE void scale(const Raw& r, int g, int s, float& d, float& c) const {
@@ -342,7 +371,84 @@ struct Dec {
     return frag(as_h2(p[0]) + off, as_h2(p[1]) + off, as_h2(p[2]) + off, as_h2(p[3]) + off);
   }
 
+  // the 8 quantised integers of step s as SUBNORMAL f16 q * 2^(kSub - 24) (exact:
+  // q << kSub < 1024 stays in the mantissa), pair order; no magic-number OR and no
+  // zero-point subtraction: the step's one v_pk_fma applies scale, zero point and min
+  HS_DEVICE f16x8 sub_ints(const Raw& r, int g, int s) const {
+    constexpr int S = sub_shift<QT>();
+    unsigned p[4];
+    if constexpr (QT == Q4_K || QT == Q5_K || QT == Q4_0 || QT == Q4_1) {
+      unsigned wa, wb;
+      int sh;
+      if constexpr (QT == Q4_K || QT == Q5_K) {
+        const u32x4 qs[2] = {r.v[1], r.v[2]};
+        sh = s < 4 ? 0 : 4;
+        wa = word(qs, 2 * (s & 3));
+        wb = word(qs, 2 * (s & 3) + 1);
+      } else {
+        const u32x4 v[2] = {r.v[0], r.v[1]};
+        const int blk = s >> 2, e = s & 3;
+        sh = e < 2 ? 0 : 4;
+        wa = word(v, 4 * blk + 2 * (e & 1));
+        wb = word(v, 4 * blk + 2 * (e & 1) + 1);
+      }
+      constexpr unsigned m = 0x000F000Fu << S;
+      // nibble at bit sh of bytes (0, 2) / (1, 3) moved to bit S: one shift + one and
+      p[0] = (sh <= S ? wa << (S - sh) : wa >> (sh - S)) & m;
+      p[1] = (wa >> (sh + 8 - S)) & m;
+      p[2] = (sh <= S ? wb << (S - sh) : wb >> (sh - S)) & m;
+      p[3] = (wb >> (sh + 8 - S)) & m;
+      if constexpr (QT == Q5_K) {  // + 16 where the high bit of the element is set
+        const u32x4 qh[2] = {r.v[3], r.v[4]};
+        const int bit = 2 * g + (s >> 2);
+        const unsigned ha = word(qh, 2 * (s & 3)), hb = word(qh, 2 * (s & 3) + 1);
+        p[0] |= ((ha >> bit) & 0x00010001u) << (4 + S);
+        p[1] |= ((ha >> (bit + 8)) & 0x00010001u) << (4 + S);
+        p[2] |= ((hb >> bit) & 0x00010001u) << (4 + S);
+        p[3] |= ((hb >> (bit + 8)) & 0x00010001u) << (4 + S);
+      }
+    } else if constexpr (QT == Q6_K) {
+      const u32x4 ql[2] = {r.v[0], r.v[1]};
+      const u32x4 qh[2] = {r.v[2], r.v[3]};
+      const int q = (g & 1) + 2 * (s >> 2);
+      const int sh = s < 4 ? 0 : 4;
+      const unsigned la = word(ql, 2 * (s & 3)), lb = word(ql, 2 * (s & 3) + 1);
+      const unsigned ha = word(qh, 2 * (s & 3)) >> (2 * q), hb = word(qh, 2 * (s & 3) + 1) >> (2 * q);
+      constexpr unsigned m = 0x000F000Fu << S;
+      p[0] = ((sh <= S ? la << (S - sh) : la >> (sh - S)) & m) | ((ha & 0x00030003u) << (4 + S));
+      p[1] = ((la >> (sh + 8 - S)) & m) | (((ha >> 8) & 0x00030003u) << (4 + S));
+      p[2] = ((sh <= S ? lb << (S - sh) : lb >> (sh - S)) & m) | ((hb & 0x00030003u) << (4 + S));
+      p[3] = ((lb >> (sh + 8 - S)) & m) | (((hb >> 8) & 0x00030003u) << (4 + S));
+    } else {  // Q8_0: int8 + 128 in [0, 255]
+      const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+      const unsigned wa = qv[s >> 1][2 * (s & 1)] ^ 0x80808080u, wb = qv[s >> 1][2 * (s & 1) + 1] ^ 0x80808080u;
+      constexpr unsigned m = 0x00FF00FFu << S;
+      p[0] = (wa << S) & m;
+      p[1] = (wa >> (8 - S)) & m;
+      p[2] = (wb << S) & m;
+      p[3] = (wb >> (8 - S)) & m;
+    }
+    return frag(as_h2(p[0]), as_h2(p[1]), as_h2(p[2]), as_h2(p[3]));
+  }
+
   HS_DEVICE f16x8 step(const Raw& r, int g, int s) const {
+    if constexpr (QT == Q4_K || QT == Q5_K || QT == Q6_K || QT == Q8_0 || QT == Q4_0 || QT == Q4_1) {
+      const u32x4 qu = __builtin_bit_cast(u32x4, sub_ints(r, g, s));
+      h2 dd, cc;
+      if constexpr (QT == Q6_K) {
+        float d, c;
+        scale(r, g, s, d, c);
+        dd = splat(d * sub_up<QT>());
+        cc = splat(sub_zero<QT>() * (float)(_Float16)d);
+      } else if constexpr (QT == Q4_0 || QT == Q4_1) {
+        dd = (s >> 2) ? dB : dA;
+        cc = (s >> 2) ? cB : cA;
+      } else {
+        dd = s < 4 ? dA : dB;
+        cc = s < 4 ? cA : cB;
+      }
+      return frag(as_h2(qu[0]) * dd + cc, as_h2(qu[1]) * dd + cc, as_h2(qu[2]) * dd + cc, as_h2(qu[3]) * dd + cc);
+    }
     if constexpr (QT == INT8) {  // (1024 + u + off) * s: exact integer, one rounding
       const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
       const unsigned wa = qv[s >> 1][2 * (s & 1)], wb = qv[s >> 1][2 * (s & 1) + 1];
@@ -381,17 +487,14 @@ struct Dec {
 // bf16 word halves -> fp32 (exact: one shift or mask)
 HS_DEVICE float bf_lo(unsigned w) { return __builtin_bit_cast(float, w << 16); }
 HS_DEVICE float bf_hi(unsigned w) { return __builtin_bit_cast(float, w & 0xFFFF0000u); }
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-HS_DEVICE u16x2 as_u16x2(unsigned u) { return __builtin_bit_cast(u16x2, u); }
 
 // f16 range of the staged x: a value beyond +-65504 (bf16 activations reach ~3e38;
 // Gemma-family hidden states are known to exceed the f16 range) converts to +-inf
-// and is caught, not clamped: every staged f16 pair's |bits| go into a running
-// v_pk_max_u16 (as many VALU ops as the v_med3 clamp this replaced), a workgroup
-// vote at the end of the K loop, and only then a second pass with each x row
-// pre-scaled by a power of two 2^-k (k from the row's max over the workgroup's K
-// range) that the epilogue undoes exactly (scale_x_rows / acc *= 2^k).
-constexpr unsigned kF16AbsMask = 0x7FFF7FFFu;
+// and is caught, not clamped: the inf makes every accumulator of its x row
+// non-finite, so a workgroup vote on the accumulators after the K loop (no per-value
+// test in the loop) triggers a second pass with each x row pre-scaled by a power of
+// two 2^-k (k from the row's max over the workgroup's K range) that the epilogue
+// undoes exactly (acc *= 2^k).
 
 // One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
 // x staging. Body per format; the kernel picks it per part (two formats per launch).
@@ -450,7 +553,6 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
       }
     }
   };
-  u16x2 om = {0, 0};  // running max of the staged f16 |bits| (first pass)
   auto store_x = [&](int buf, auto scaled) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
@@ -467,12 +569,6 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
       f16x8 h;
 #pragma unroll
       for (int e = 0; e < 8; ++e) h[e] = static_cast<_Float16>(f[e]);
-      if constexpr (!decltype(scaled)::value) {
-        const u32x4 u = __builtin_bit_cast(u32x4, h);
-        om = __builtin_elementwise_max(
-            om, __builtin_elementwise_max(__builtin_elementwise_max(as_u16x2(u[0] & kF16AbsMask), as_u16x2(u[1] & kF16AbsMask)),
-                                          __builtin_elementwise_max(as_u16x2(u[2] & kF16AbsMask), as_u16x2(u[3] & kF16AbsMask))));
-      }
       *reinterpret_cast<f16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = h;
     }
   };
@@ -540,8 +636,16 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
   if (sb < sb1) iter(sb, rawA, rawB);
   };
   run(std::false_type{});
-  // some staged x beyond the f16 range (rare): per-row power-of-two pre-scale, second pass
-  if (__syncthreads_or(om[0] >= 0x7C00 || om[1] >= 0x7C00)) {
+  // some staged x beyond the f16 range (rare) became +-inf, which leaves a non-finite
+  // accumulator in every output of its row: per-row power-of-two pre-scale, second pass
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(acc[r][t][e]);
+  if (__syncthreads_or(bad)) {
     unsigned* xb = reinterpret_cast<unsigned*>(xrow);
     if (tid < XR) xb[tid] = 0u;
     __syncthreads();

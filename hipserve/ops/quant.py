@@ -113,6 +113,32 @@ def repack_tiled(raw: np.ndarray, qtype: int, N: int, K: int) -> np.ndarray:
     return np.ascontiguousarray(out)
 
 
+# gguf_mfma.hip places each quantised integer at bit SUB_SHIFT of a subnormal f16 and
+# scales it by 2^(24 - SUB_SHIFT) inside the f16 FMA: every block scale must stay below
+# 65504 / 2^(24 - SUB_SHIFT) (|w| up to ~2-4). Weights beyond that (none in practice)
+# run on the v1 kernel.
+SUB_SHIFT = {G.Q4_K: 6, G.Q5_K: 5, G.Q6_K: 4, G.Q8_0: 2, G.Q4_0: 6, G.Q4_1: 6}
+
+
+def sub_scale_ok(raw, qtype: int) -> bool:
+    if qtype not in SUB_SHIFT:
+        return True
+    lim = 65504.0 / 2.0 ** (24 - SUB_SHIFT[qtype])
+    _, bb = G.BLOCK[qtype]
+    b = np.asarray(raw, np.uint8).reshape(-1, bb)
+
+    def f16(a):
+        return np.abs(np.ascontiguousarray(a).view(np.float16).astype(np.float32).reshape(-1))
+    if qtype in (G.Q4_K, G.Q5_K):
+        sc, _ = G._scale_min_k4(b[:, 4:16])
+        m = f16(b[:, 0:2]) * sc.max(1)
+    elif qtype == G.Q6_K:
+        m = f16(b[:, 208:210]) * np.abs(np.ascontiguousarray(b[:, 192:208]).view(np.int8).astype(np.float32)).max(1)
+    else:
+        m = f16(b[:, 0:2])
+    return bool(m.size == 0 or np.max(m) < lim)
+
+
 def tileable(N: int, K: int) -> bool:
     return N % 16 == 0 and K % 256 == 0
 
@@ -123,11 +149,12 @@ class QuantPart:
     scales. FP8 parts carry ``rs``, the fp32 per-row output scale (256 x the
     channel scale: the kernel's e4m3 -> f16 bit move yields value / 256)."""
 
-    def __init__(self, qtype, N, K, q, d, m, row_bytes, tiled=False, rs=None):
+    def __init__(self, qtype, N, K, q, d, m, row_bytes, tiled=False, rs=None, sub_ok=True):
         self.qtype, self.N, self.K = qtype, N, K
         self.kqt = KERNEL_QT[qtype]
         self.q, self.d, self.m, self.row_bytes = q, d, m, row_bytes
         self.tiled = tiled
+        self.sub_ok = sub_ok  # block scales in the v2 kernel's subnormal-dequant range
         self.rs = rs if rs is not None else torch.empty(0, dtype=torch.float32, device=q.device)
 
     @classmethod
@@ -185,7 +212,8 @@ class QuantPart:
             return torch.from_numpy(np.array(a, copy=True, order='C')).view(dt).to(device)
         if tileable(N, K):
             e = torch.empty(0, dtype=torch.int16, device=device)
-            return cls(qtype, N, K, to(repack_tiled(raw, qtype, N, K), torch.uint8), e, e, 0, tiled=True)
+            return cls(qtype, N, K, to(repack_tiled(raw, qtype, N, K), torch.uint8), e, e, 0, tiled=True,
+                       sub_ok=sub_scale_ok(raw, qtype))
         q, d, m, rb = repack(raw, qtype, N, K)
         return cls(qtype, N, K, to(q, torch.uint8), to(d, torch.int16), to(m, torch.int16), rb)
 
@@ -217,7 +245,7 @@ class QuantWeight:
                 cols.append(off)
                 off += p.N
             self._groups = [(kqt, ps, cols) for kqt, (ps, cols) in groups.items()]
-            self._v2 = all(p.tiled for p in self.parts)
+            self._v2 = all(p.tiled and p.sub_ok for p in self.parts)
             cols = np.cumsum([0] + [p.N for p in self.parts])[:-1].tolist()
             self.v2_args = ([p.q for p in self.parts], [p.rs for p in self.parts], [p.kqt for p in self.parts],
                             [p.N for p in self.parts], cols)

@@ -90,6 +90,7 @@ for s in $steps; do
     bench_q4) run_bench_q4 ;;
     bench_mixtral) run_bench_mixtral ;;
     pgemm) run_pgemm 8b ;;
+    gguf) timeout -k 10 300 python -u tools/bench_gguf.py --m 1 16 64 > $OUT/bench_gguf.log 2>&1; rc=$?; tail -n 30 $OUT/bench_gguf.log; [ $rc -eq 0 ] ;;
     g27fp8) bench_named g27fp8 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b --quantization fp8 ;;
     g27fp8_shadow) bench_named g27fp8_shadow HIPSERVE_FP8_PREFILL=0 -- --model gemma-3-27b --quantization fp8 ;;
     g27bf16) bench_named g27bf16 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b ;;

@@ -138,3 +138,25 @@ def test_synthetic_quant_engine_cpu():
     assert torch.isfinite(m.layers[0].wd).all()
     res = eng.generate([[1, 5, 6, 7]], SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
     assert len(res[0][0]) == 6
+
+
+def test_sub_scale_range_guard():
+    """ops/quant.py sub_scale_ok: the v2 kernel's subnormal-integer dequant needs every
+    block scale below 65504 / 2^(24 - shift); random synthetic blocks pass, a block with
+    a huge scale sends the weight to the v1 kernel."""
+    from hipserve.ops import quant as Q
+
+    rng = np.random.default_rng(0)
+    for qt in (G.Q4_K, G.Q5_K, G.Q6_K, G.Q8_0, G.Q4_0, G.Q4_1):
+        raw = Q.random_blocks(rng, qt, 32, 512).copy()
+        assert Q.sub_scale_ok(raw, qt), G.TYPE_NAMES.get(qt, qt)
+        _, bb = G.BLOCK[qt]
+        b = raw.reshape(-1, bb)
+        off = 208 if qt == G.Q6_K else 0
+        b[3, off:off + 2] = np.frombuffer(np.float16(8.0).tobytes(), np.uint8)  # one block, scale 8
+        if qt in (G.Q4_K, G.Q5_K):
+            b[3, 4:16] = 0xFF  # 6-bit scales at 63
+        if qt == G.Q6_K:
+            b[3, 192:208] = 100
+        assert not Q.sub_scale_ok(raw, qt), G.TYPE_NAMES.get(qt, qt)
+    assert Q.sub_scale_ok(np.zeros(0, np.uint8), G.Q4_K)

@@ -480,3 +480,21 @@ def test_fp8_linear_beyond_f16_range():
         assert torch.isfinite(y).all()
         rel = ((y - want).norm(dim=1) / want.norm(dim=1)).max().item()
         assert rel < (5e-2 if M > 64 else 1e-2), (M, rel)
+
+
+def test_wide_scale_weight_runs_v1():
+    """A Q4_K weight with a block scale beyond the v2 kernel's subnormal-dequant range
+    (ops/quant.py sub_scale_ok) is served by the v1 kernel, still matching fp32."""
+    from hipserve.ops.quant import random_blocks
+    rng = np.random.default_rng(3)
+    N, K = 256, 1024
+    raw = random_blocks(rng, G.Q4_K, N, K).copy()
+    b = raw.reshape(-1, 144)
+    b[5, 0:2] = np.frombuffer(np.float16(0.05).tobytes(), np.uint8)
+    b[5, 4:16] = 0xFF  # d * sc = 0.05 * 63 > 0.25
+    qw = QuantWeight.from_raw([(G.Q4_K, N, K, raw)], "cuda")
+    assert not qw.v2
+    x = torch.randn(16, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense([(G.Q4_K, N, K, raw)]).T
+    y = quant_linear(x, qw).float()
+    assert (y - want).abs().max().item() < 1e-2 * want.abs().max().item() + 1e-3
