@@ -33,6 +33,9 @@ trace8() {
   # (measured: 10.6-21 ms per hipGraph all-reduce at 4 queues, 81 us at 1)
   export GPU_MAX_HW_QUEUES=1
   local port=29631 pids=()
+  # heartbeat: 8 ranks time-sharing one GPU run for minutes without writing anything
+  (while sleep 30; do echo "trace8 heartbeat $(date +%T)"; done) &
+  local hb=$!
   for r in 1 2 3 4 5 6 7; do
     RANK=$r WORLD_SIZE=8 MASTER_PORT=$port timeout -k 10 420 python3 tools/tp_shared_gpu.py --model llama-3-70b \
       --layers 2 --batch 8 --input-len 1024 --output-len 32 > $OUT/trace8_r$r.log 2>&1 &
@@ -43,6 +46,7 @@ trace8() {
      --batch 8 --input-len 1024 --output-len 32 > $HERE/$OUT/trace8_r0.log 2>&1)
   local rc=$?
   for p in "${pids[@]}"; do wait $p || rc=$((rc ? rc : 1)); done
+  kill $hb 2>/dev/null
   tail -3 $OUT/trace8_r0.log
   [ $rc -eq 0 ] || return $rc
   local db; db=$(find $OUT/trace8 -name '*results.db' | head -n 1)

@@ -23,7 +23,7 @@ def _rnd(g, *s, scale=1.0):
     return ((torch.rand(*s, device=DEV, generator=g) * 2 - 1) * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("M,N,K", SHAPES + [(512, 256, 128), (700, 512, 192)])
 def test_prefill_gemm_store(M, N, K, variant):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
@@ -34,26 +34,30 @@ def test_prefill_gemm_store(M, N, K, variant):
     torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 
 
+@pytest.mark.parametrize("variant", [2, 3])
 @pytest.mark.parametrize("M,N,K", SHAPES[:4])
-def test_prefill_gemm_residual_add(M, N, K):
+def test_prefill_gemm_residual_add(M, N, K, variant):
     g = torch.Generator(device=DEV).manual_seed(7 + M)
     x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
     res0 = _rnd(g, M, N)
     res = res0.clone()
-    torch.ops.hipserve.prefill_gemm(res, x, w, 1)
+    torch.ops.hipserve.prefill_gemm(res, x, w, 1, variant)
     h = (x.float() @ w.float().t()).to(torch.bfloat16).float()
     want = (h + res0.float()).to(torch.bfloat16).float()
     torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("variant,act", [(2, "silu"), (3, "silu"), (2, "gelu"), (3, "gelu")])
 @pytest.mark.parametrize("M,I,K", [(300, 256, 1024), (1000, 384, 512), (2049, 128, 256)])
-def test_prefill_gemm_glu(M, I, K):
+def test_prefill_gemm_glu(M, I, K, variant, act):
     g = torch.Generator(device=DEV).manual_seed(11 + M)
     x, w = _rnd(g, M, K), _rnd(g, 2 * I, K, scale=0.05)
-    act = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm(act, x, w, 2)
+    out = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm(out, x, w, 2 if act == "silu" else 3, variant)
     gu = (x.float() @ w.float().t()).to(torch.bfloat16).float()
-    want = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    f = torch.nn.functional.silu if act == "silu" else (lambda t: torch.nn.functional.gelu(t, approximate="tanh"))
+    want = f(gu[:, :I]) * gu[:, I:]
+    act = out
     torch.testing.assert_close(act.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
 
 

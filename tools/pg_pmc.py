@@ -20,7 +20,8 @@ out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(3):
     F.linear(x, w)
 torch.cuda.synchronize()
-for _ in range(3):
-    torch.ops.hipserve.prefill_gemm(out, x, w, 0, 2)
-torch.cuda.synchronize()
+for v in (2, 3):
+    for _ in range(3):
+        torch.ops.hipserve.prefill_gemm(out, x, w, 0, v)
+    torch.cuda.synchronize()
 print("ok", M, N, K)
