@@ -350,114 +350,6 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
   pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
 }
 
-// ---- v3: the pgemm2 wave layout (8 waves, 128 x 64 per wave, acc[4][8]) with ONE
-// barrier per K tile. PMC on the Llama-3-8B gate|up shape (scripts/pg_pmc.sh): pgemm2
-// parks 28 % of its wave cycles on s_waitcnt / barriers (four per K tile) against ~7 %
-// for hipBLASLt's persistent kernel. A K tile runs as its two 32-deep halves:
-//   MFMAs of half 0 (32), with half 1's fragments read from LDS behind them;
-//   wait for tile kt + 1's LDS-DMA (the only one in flight) + lgkmcnt(0), s_barrier;
-//   LDS-DMA of tile kt + 2 into the stage just released; half 0 of tile kt + 1 read
-//   behind the MFMAs of half 1.
-// Two fragment register sets (one per half): 96 VGPRs beside the 128 accumulators.
-template <int EPI, bool kGroup>
-__global__ __launch_bounds__(PG_T) void pgemm3_kernel(const unsigned short* __restrict__ A, long lda,
-                                                      const unsigned short* __restrict__ B, long ldb,
-                                                      unsigned short* __restrict__ C, long ldc, int M, int N, int K,
-                                                      int tiles_m, int tiles_n, PgEpi E) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * PG_TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
-  const int m0 = tm * PG_BM, n0 = tn * PG_BN;
-  if constexpr (kGroup) {
-    const int e = E.tile_expert[tm];
-    if (e < 0) return;
-    B += (long)e * E.b_estride;
-  }
-  const int nk = K / PG_BK;
-  // staging: wave w moves rows [32w, 32w + 32) of both tiles, 8 rows per instruction,
-  // as buffer_load ... lds with per-lane 32-bit offsets and the K step in soffset
-  unsigned int voff[2][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = wave * 32 + i * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ ((r >> 1) & 7);
-    voff[0][i] = (unsigned)((long)min(m0 + r, M - 1) * lda * 2 + lc * 16);
-    voff[1][i] = (unsigned)((long)pg_brow<EPI>(n0, tn, r, N) * ldb * 2 + lc * 16);
-  }
-  const __amdgpu_buffer_rsrc_t rsrc[2] = {
-      __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min((long)M * lda * 2, 0x7fffffffL), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)min((long)N * ldb * 2, 0x7fffffffL), 0x00020000)};
-  auto stage = [&](int buf, int kt) {
-#pragma unroll
-    for (int op = 0; op < 2; ++op)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsrc[op], (lds_ptr_t)(lds + buf * 2 * PG_TILE + op * PG_TILE + (wave * 32 + i * 8) * 128), 16,
-            voff[op][i], kt * PG_BK * 2, 0, 0);
-  };
-  const int fr = lane & 15, fq = lane >> 4;
-  const int sw = (fr >> 1) & 7;
-  const int a_off = (wr * 128 + fr) * 128, b_off = PG_TILE + (wc * 64 + fr) * 128;
-  const int chs[2] = {((0 + fq) ^ sw) * 16, ((4 + fq) ^ sw) * 16};
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u16x8 af[2][8], bf[2][4];
-  auto read = [&](const unsigned char* sb, int h) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[h][j] = *reinterpret_cast<const u16x8*>(sb + b_off + j * 2048 + chs[h]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[h][i] = *reinterpret_cast<const u16x8*>(sb + a_off + i * 2048 + chs[h]);
-  };
-  auto mfma = [&](int h) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[h][j]),
-                                                            __builtin_bit_cast(bf16x8, af[h][i]), acc[j][i], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  stage(0, 0);
-  if (nk > 1) {
-    stage(1, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  read(lds, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const unsigned char* sb = lds + buf * 2 * PG_TILE;
-    read(sb, 1);
-    mfma(0);
-    __builtin_amdgcn_sched_barrier(0);
-    // tile kt + 1 landed (the only LDS-DMA in flight), every wave done with stage buf
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + 2 < nk) stage(buf, kt + 2);
-    // half 0 of tile kt + 1 behind this tile's half 1 (the last tile reads a drained
-    // stage: unused, and no phi on the fragments)
-    read(lds + (buf ^ 1) * 2 * PG_TILE, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma(1);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // the GLU exchange reuses the staging LDS
-  pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
-}
-
 // ---- FP8 W8A8 (the FP8-Dynamic checkpoints: per-channel e4m3 weights, per-token
 // dynamic e4m3 activations) on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block
 // scales (E8M0 127): twice the bf16 MFMA rate per clock (MI355X_MICROARCH.md, matrix
@@ -717,15 +609,6 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
     switch (epi) {
       case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, true><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, true><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      default: return false;
-    }
-  }
-  if (E.variant == 3) {
-    switch (epi) {
-      case PG_EPI_STORE: pgemm3_kernel<PG_EPI_STORE, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_ADD: pgemm3_kernel<PG_EPI_ADD, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GLU: pgemm3_kernel<PG_EPI_GLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GEGLU: pgemm3_kernel<PG_EPI_GEGLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       default: return false;
     }
   }

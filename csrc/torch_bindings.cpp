@@ -655,15 +655,16 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
 
 // Prefill GEMM (prefill_gemm.hip): out = x @ w^T with a fused epilogue.
 // epi 0: out [M, N] bf16; 1: out is the residual [M, N], out = bf16(bf16(x w^T) + out);
-// 2: w = merged [gate; up] (N = 2I, I % 128 == 0), out = act [M, I] = silu(gate) * up.
+// 2 / 3: w = merged [gate; up] (N = 2I, I % 128 == 0), out = act [M, I] = silu / gelu_tanh(gate) * up.
 void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t epi, int64_t variant) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w);
   CHECK_ROWMAJOR(out);
   const int M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && N % 256 == 0 && K % 64 == 0, "prefill_gemm: w [N % 256, K % 64]");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "prefill_gemm: alignment");
-  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm: out shape");
-  TORCH_CHECK(epi != 2 || (N / 2) % 128 == 0, "prefill_gemm: GLU needs I % 128 == 0");
+  const bool glu = epi == 2 || epi == 3;
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? N / 2 : N), "prefill_gemm: out shape");
+  TORCH_CHECK(!glu || (N / 2) % 128 == 0, "prefill_gemm: GLU needs I % 128 == 0");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::PgEpi E{};
   E.variant = (int)variant;
@@ -717,7 +718,7 @@ void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
 // tile 256, moe_gather), w [E, N, K] (GLU: each expert's merged [gate; up] weight),
 // tile_expert [tiles] int32 from moe_align. No host synchronisation.
 void prefill_gemm_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& tile_expert,
-                          int64_t epi) {
+                          int64_t epi, int64_t variant) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_CONTIG(w);
   CHECK_ROWMAJOR(out); CHECK_CONTIG(tile_expert);
   TORCH_CHECK(w.dim() == 3 && tile_expert.scalar_type() == at::kInt, "prefill_gemm_grouped: w [E, N, K], int32 tiles");
@@ -728,7 +729,7 @@ void prefill_gemm_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor
   TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm_grouped: out shape");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::PgEpi E{};
-  E.variant = 2;
+  E.variant = (int)variant;
   E.tile_expert = tile_expert.data_ptr<int>();
   E.b_estride = (long)N * K;
   TORCH_CHECK(hipserve::launch_prefill_gemm((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
@@ -1112,7 +1113,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
-  m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi) -> ()");
+  m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi, int variant=2) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
         "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
         "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "

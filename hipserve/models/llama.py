@@ -901,9 +901,9 @@ class LlamaModel:
         op.moe_gather(xs, x, slots, k)
         if tile == 256:  # hand-written grouped expert GEMMs, SiLU-GLU in the first's epilogue
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-            op.prefill_gemm_grouped(act, xs, lw.w13, tile_expert, 2)
+            op.prefill_gemm_grouped(act, xs, lw.w13, tile_expert, 2, pgemm.VARIANT)
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
-            op.prefill_gemm_grouped(y, act, lw.w2, tile_expert, 0)
+            op.prefill_gemm_grouped(y, act, lw.w2, tile_expert, 0, pgemm.VARIANT)
         else:
             gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)

@@ -28,6 +28,9 @@ import torch.nn.functional as F
 log = logging.getLogger("hipserve.pgemm")
 
 MODE = os.environ.get("HIPSERVE_PREFILL_GEMM", "auto")
+# kernel schedule (prefill_gemm.hip): 1 = one-stage-ahead loop, 2 = half-tile pipeline (default;
+# a one-barrier-per-K-tile schedule measured 11 % slower, profiles/r3_pgemm_pmc.md)
+VARIANT = int(os.environ.get("HIPSERVE_PGEMM_VARIANT", "2"))
 MIN_ROWS = 512        # below this hipBLASLt's smaller tiles win (and decode GEMMs take M <= 64)
 CHOICE: dict[tuple, bool] = {}     # (kind, N, K) -> use prefill_gemm
 REPORT: list[dict] = []
@@ -48,13 +51,13 @@ def use(kind: str, w, M: int) -> bool:
 
 def gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
-    torch.ops.hipserve.prefill_gemm(out, x, w, 0)
+    torch.ops.hipserve.prefill_gemm(out, x, w, 0, VARIANT)
     return out
 
 
 def gemm_add_(residual: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """residual = bf16(bf16(x @ w.T) + residual), in place."""
-    torch.ops.hipserve.prefill_gemm(residual, x, w, 1)
+    torch.ops.hipserve.prefill_gemm(residual, x, w, 1, VARIANT)
     return residual
 
 
@@ -62,7 +65,7 @@ def gemm_glu(x: torch.Tensor, w: torch.Tensor, gelu: bool = False) -> torch.Tens
     """act = silu(x @ Wg.T) * (x @ Wu.T) for the merged w = [Wg; Wu] (gelu: tanh-GELU,
     Gemma's GeGLU)."""
     act = torch.empty(x.shape[0], w.shape[0] // 2, device=x.device, dtype=x.dtype)
-    torch.ops.hipserve.prefill_gemm(act, x, w, 3 if gelu else 2)
+    torch.ops.hipserve.prefill_gemm(act, x, w, 3 if gelu else 2, VARIANT)
     return act
 
 
@@ -178,8 +181,8 @@ def _tune_moe(E: int, inter: int, H: int, k: int, T: int, device, ops) -> dict:
     y = torch.empty(cap, H, dtype=x.dtype, device=device)
 
     def p_moe(i):
-        op.prefill_gemm_grouped(act, xs, w13, te, 2)
-        op.prefill_gemm_grouped(y, act, w2, te, 0)
+        op.prefill_gemm_grouped(act, xs, w13, te, 2, VARIANT)
+        op.prefill_gemm_grouped(y, act, w2, te, 0, VARIANT)
 
     t_p = _time(p_moe, reps=2)
     cap16, _, ends, xs16 = layout(16)
@@ -219,7 +222,7 @@ def tune(units: dict, M: int, device, ops) -> list[dict]:
         if kind == "glu":
             act = torch.empty(M, N // 2, device=device, dtype=torch.bfloat16)
             t_b = _time(lambda i: ops.silu_and_mul(act, F.linear(x, ws[i])))
-            t_p = _time(lambda i: torch.ops.hipserve.prefill_gemm(act, x, ws[i], 2))
+            t_p = _time(lambda i: torch.ops.hipserve.prefill_gemm(act, x, ws[i], 2, VARIANT))
         elif kind == "add":
             res = torch.randn(M, N, device=device).to(torch.bfloat16)
             nw = torch.ones(N, device=device, dtype=torch.bfloat16)
@@ -227,13 +230,13 @@ def tune(units: dict, M: int, device, ops) -> list[dict]:
             t_b = _time(lambda i: ops.fused_add_rmsnorm(xn, F.linear(x, ws[i]), res, nw, 1e-5))
 
             def p_add(i):
-                torch.ops.hipserve.prefill_gemm(res, x, ws[i], 1)
+                torch.ops.hipserve.prefill_gemm(res, x, ws[i], 1, VARIANT)
                 ops.rmsnorm(xn, res, nw, 1e-5)
             t_p = _time(p_add)
         else:
             o = torch.empty(M, N, device=device, dtype=torch.bfloat16)
             t_b = _time(lambda i: F.linear(x, ws[i]))
-            t_p = _time(lambda i: torch.ops.hipserve.prefill_gemm(o, x, ws[i], 0))
+            t_p = _time(lambda i: torch.ops.hipserve.prefill_gemm(o, x, ws[i], 0, VARIANT))
         CHOICE[(kind, N, K)] = t_p < t_b * 0.99
         r = {"kind": kind, "M": M, "N": N, "K": K, "blas_unit_ms": round(t_b, 4), "pgemm_unit_ms": round(t_p, 4),
              "pgemm": CHOICE[(kind, N, K)]}

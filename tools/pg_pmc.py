@@ -20,7 +20,7 @@ out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(3):
     F.linear(x, w)
 torch.cuda.synchronize()
-for v in (2, 3):
+for v in (2,):
     for _ in range(3):
         torch.ops.hipserve.prefill_gemm(out, x, w, 0, v)
     torch.cuda.synchronize()
