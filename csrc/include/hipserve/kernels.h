@@ -93,8 +93,11 @@ struct GgufPart {
   int col;
 };
 int gguf_tiled_chunk_bytes(int qtype);
+// x16 (optional, M <= 64): x as f16 in the kernel's staging pair order {0,2,1,3,4,6,5,7}
+// per aligned 8-run, row stride x_stride (decode_fused.hip producers write it)
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
-                            const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s);
+                            const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
+                            const void* x16 = nullptr);
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s);
 // quantised MoE experts (tiled layout per expert, stacked [E][N/16][K/256][chunk]) over
 // moe_align tiles of 16/32/64 slots: out[slot, N] bf16 (S == 1) or ws[S, nslots, N] fp32.
@@ -219,13 +222,15 @@ void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s)
 // decode_fused.hip — split-K partial reductions fused with the next op of the layer
 // ws: [S, M, N] fp32 partials. h = bf16(sum_s ws); residual = bf16(h + residual);
 // out = rmsnorm(residual) * w  (bit-identical to splitk_reduce + fused_add_rmsnorm)
+// out16 (optional): out also as f16 in the quantised GEMM's staging pair order (gguf_mfma.hip kX16)
 void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
-                               int M, int N, float eps, hipStream_t s);
+                               int M, int N, float eps, hipStream_t s, void* out16 = nullptr);
 // qkv = bf16(sum_s ws) -> RoPE(q, k) -> q into qkv[:, :nq*D], k/v into the paged cache
 // out[M, N] (bf16, row stride out_stride) = sum of the fp32 partials ws[S, M, N] (decode_gemm.hip)
 void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, int N, int S, hipStream_t s);
 // act[M, I] = GLU of the plain [gate | up] partials ws[S, M, 2I] (decode_fused.hip)
-void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s);
+void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s,
+                       void* act16 = nullptr);
 // bias (bf16 [N]) and per-head q/k RMSNorm (fp32 weights [D], mode 0, D/16 a power of two)
 // optional: nullptr skips them (Qwen2 / Qwen3 families)
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,

@@ -26,6 +26,17 @@ HS_DEVICE void add_bias8(float (&x)[8], const unsigned short* __restrict__ b) {
   for (int j = 0; j < 8; ++j) x[j] = bf16_to_f32(f32_to_bf16(x[j] + bf16_to_f32(v[j])));
 }
 
+// 8 bf16 values -> f16 in the quantised decode GEMM's staging pair order
+// {0, 2, 1, 3, 4, 6, 5, 7} (gguf_mfma.hip kX16): bf16 -> fp32 exact, -> f16 round to
+// nearest — the conversion the GEMM would otherwise run in every workgroup
+HS_DEVICE u16x8 f16_pairs8(const u16x8 v) {
+  constexpr int ord[8] = {0, 2, 1, 3, 4, 6, 5, 7};
+  u16x8 h;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = __builtin_bit_cast(unsigned short, static_cast<_Float16>(bf16_to_f32(v[ord[j]])));
+  return h;
+}
+
 HS_DEVICE void sum8_bf16(float (&o)[8], const float* __restrict__ p, long slice, int S) {
   f32x4 lo, hi;
   sum_slices8(lo, hi, p, slice, S);
@@ -41,7 +52,7 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
                                                                  unsigned short* __restrict__ residual,
                                                                  const float* __restrict__ ws, int S,
                                                                  const void* __restrict__ weight, int M, int N,
-                                                                 float eps) {
+                                                                 float eps, unsigned short* __restrict__ out16) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = N >> 3;
@@ -99,31 +110,33 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
         o[j] = f32_to_bf16(v[i][j] * inv * wj);
       }
       orow[idx] = o;
+      if (out16 != nullptr) reinterpret_cast<u16x8*>(out16 + (long)row * N)[idx] = f16_pairs8(o);
     }
   }
 }
 
 template <bool kWF32>
 static void add_rmsnorm_t(void* out, void* residual, const float* ws, int S, const void* w, int M, int N, float eps,
-                          hipStream_t s) {
+                          hipStream_t s, unsigned short* o16) {
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
   const int nvec = N / 8;
   if (norm_threads(N) == 256) {
-    if (nvec <= 256) splitk_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps);
-    else splitk_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps);
+    if (nvec <= 256) splitk_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
+    else splitk_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
   } else {
-    if (nvec <= 512) splitk_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps);
-    else if (nvec <= 1024) splitk_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps);
-    else splitk_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps);
+    if (nvec <= 512) splitk_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
+    else if (nvec <= 1024) splitk_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
+    else splitk_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
   }
 }
 
 void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
-                               int M, int N, float eps, hipStream_t s) {
+                               int M, int N, float eps, hipStream_t s, void* out16) {
   if (M <= 0) return;
-  if (weight_f32) add_rmsnorm_t<true>(out, residual, ws, S, w, M, N, eps, s);
-  else add_rmsnorm_t<false>(out, residual, ws, S, w, M, N, eps, s);
+  auto* o16 = static_cast<unsigned short*>(out16);
+  if (weight_f32) add_rmsnorm_t<true>(out, residual, ws, S, w, M, N, eps, s, o16);
+  else add_rmsnorm_t<false>(out, residual, ws, S, w, M, N, eps, s, o16);
 }
 
 // The rope_cache kernel (rope_cache.hip) reading its input from the split-K
@@ -260,7 +273,8 @@ void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S
 // followed by silu_and_mul / gelu_and_mul. grid (M, ceil(I / 2048)), 8 per thread.
 template <bool kGelu>
 __global__ __launch_bounds__(256) void splitk_glu_kernel(unsigned short* __restrict__ act, long act_stride,
-                                                         const float* __restrict__ ws, int S, int M, int I) {
+                                                         const float* __restrict__ ws, int S, int M, int I,
+                                                         unsigned short* __restrict__ act16) {
   const int m = blockIdx.x;
   const int c = blockIdx.y * 256 + threadIdx.x;
   if (c * 8 >= I) return;
@@ -274,15 +288,19 @@ __global__ __launch_bounds__(256) void splitk_glu_kernel(unsigned short* __restr
     gb[j] = f32_to_bf16(g[j]);
     ub[j] = f32_to_bf16(u[j]);
   }
-  *reinterpret_cast<u16x8*>(act + m * act_stride + c * 8) = kGelu ? gelu_mul8(gb, ub) : silu_mul8(gb, ub);
+  const u16x8 o = kGelu ? gelu_mul8(gb, ub) : silu_mul8(gb, ub);
+  *reinterpret_cast<u16x8*>(act + m * act_stride + c * 8) = o;
+  if (act16 != nullptr) *reinterpret_cast<u16x8*>(act16 + m * act_stride + c * 8) = f16_pairs8(o);
 }
 
-void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s) {
+void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s,
+                       void* act16) {
   if (M <= 0) return;
   const dim3 grid(M, (I / 8 + 255) / 256);
   auto* a = static_cast<unsigned short*>(act);
-  if (gelu) splitk_glu_kernel<true><<<grid, 256, 0, s>>>(a, act_stride, ws, S, M, I);
-  else splitk_glu_kernel<false><<<grid, 256, 0, s>>>(a, act_stride, ws, S, M, I);
+  auto* a16 = static_cast<unsigned short*>(act16);
+  if (gelu) splitk_glu_kernel<true><<<grid, 256, 0, s>>>(a, act_stride, ws, S, M, I, a16);
+  else splitk_glu_kernel<false><<<grid, 256, 0, s>>>(a, act_stride, ws, S, M, I, a16);
 }
 
 }  // namespace hipserve

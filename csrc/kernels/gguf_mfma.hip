@@ -498,11 +498,12 @@ HS_DEVICE float bf_hi(unsigned w) { return __builtin_bit_cast(float, w & 0xFFFF0
 
 // One wave = RT row groups of 16 x the workgroup's K range; 8 waves share the
 // x staging. Body per format; the kernel picks it per part (two formats per launch).
-template <int QT, int MT, int RT, int NWAVES, bool kMoe = false>
+template <int QT, int MT, int RT, int NWAVES, bool kMoe = false, bool kX16 = false>
 HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, unsigned short* __restrict__ out,
                            long out_stride,
                            float* __restrict__ ws, const unsigned short* __restrict__ x, long x_stride,
-                           const Part& P, int M, int Ntot, int K, int sb_per_split, const MoeQ& moe = MoeQ{}) {
+                           const Part& P, int M, int Ntot, int K, int sb_per_split, const MoeQ& moe = MoeQ{},
+                           const unsigned short* __restrict__ x16 = nullptr) {
   constexpr int XR = 16 * MT;           // staged x rows (M padded)
   constexpr int NT = 64 * NWAVES;
   constexpr int CB = chunk_bytes<QT>();
@@ -541,19 +542,33 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
       xo[i] = min(mrow0 + row, M - 1) * (int)x_stride + kbase<QT>(fr >> 3, fr & 7);
     }
   }
-  auto load_x = [&](int sb) {
+  // kX16: the producer of x (decode_fused.hip splitk_add_rmsnorm / splitk_glu) also
+  // wrote it as f16 in the staging pair order (x16, same row stride): the first pass
+  // stages those bits as they are — no per-workgroup bf16 -> f16 conversion (a
+  // quarter of this body's VALU at M = 64). The pre-scaled second pass reads bf16 x.
+  auto load_x = [&](int sb, auto scaled) {
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       // rows >= M are clamped, never stored (kMoe: padding slots read row 0, never stored)
       if constexpr (kMoe) {
         const int fr = (i * NT + tid) & 31;
         xv[i] = *reinterpret_cast<const u16x8*>(xg[i] + sb * 256 + kbase<QT>(fr >> 3, fr & 7));
+      } else if constexpr (kX16 && !decltype(scaled)::value) {
+        xv[i] = *reinterpret_cast<const u16x8*>(x16 + xo[i] + sb * 256);
       } else {
         xv[i] = *reinterpret_cast<const u16x8*>(x + xo[i] + sb * 256);
       }
     }
   };
   auto store_x = [&](int buf, auto scaled) {
+    if constexpr (kX16 && !decltype(scaled)::value) {
+#pragma unroll
+      for (int i = 0; i < XP; ++i) {
+        const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
+        *reinterpret_cast<u16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = xv[i];
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
@@ -586,7 +601,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (sb0 < sb1) {
-    load_x(sb0);
+    load_x(sb0, scaled);
 #pragma unroll
     for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sb0 * CB, g, c, lane, rawA[r]);
     store_x(0, scaled);
@@ -598,7 +613,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
     // unconditionally (the last iteration re-reads its own chunk) so no branch splits
     // the loads from their uses and the vmcnt waits stay counted, not drained
     const int sn = min(sb + 1, sb1 - 1);
-    load_x(sn);
+    load_x(sn, scaled);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
@@ -650,7 +665,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
     if (tid < XR) xb[tid] = 0u;
     __syncthreads();
     for (int sb2 = sb0; sb2 < sb1; ++sb2) {  // max |x| per staged row (ds_max_u32 on non-negative float bits)
-      load_x(sb2);
+      load_x(sb2, std::true_type{});
 #pragma unroll
       for (int i = 0; i < XP; ++i) {
         const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
@@ -706,11 +721,11 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
   }
 }
 
-template <int QA, int QB, int MT, int RT, int NWAVES>
+template <int QA, int QB, int MT, int RT, int NWAVES, bool kX16 = false>
 __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __restrict__ out, long out_stride,
                                                             float* __restrict__ ws, const unsigned short* __restrict__ x,
                                                             long x_stride, Parts parts, int M, int Ntot, int K,
-                                                            int sb_per_split) {
+                                                            int sb_per_split, const unsigned short* __restrict__ x16) {
   __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<MT>()];
   __shared__ float xrow[16 * MT];  // per staged x row: power-of-two pre-scale (f16 range guard)
   const int tile = blockIdx.x;
@@ -720,9 +735,11 @@ __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __r
     if (i < parts.n && tile >= parts.p[i].tile0) pi = i;
   const Part& P = parts.p[pi];
   if (QA == QB || P.qt == QA)
-    qgemm2_body<QA, MT, RT, NWAVES>(xs, xrow, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+    qgemm2_body<QA, MT, RT, NWAVES, false, kX16>(xs, xrow, out, out_stride, ws, x, x_stride, P, M, Ntot, K,
+                                                 sb_per_split, MoeQ{}, x16);
   else
-    qgemm2_body<QB, MT, RT, NWAVES>(xs, xrow, out, out_stride, ws, x, x_stride, P, M, Ntot, K, sb_per_split);
+    qgemm2_body<QB, MT, RT, NWAVES, false, kX16>(xs, xrow, out, out_stride, ws, x, x_stride, P, M, Ntot, K,
+                                                 sb_per_split, MoeQ{}, x16);
 }
 
 // 33 <= M <= 64 body shape (HIPSERVE_QGEMM_M64, for A/B measurement): 0 = 8 waves x 1
@@ -738,7 +755,7 @@ int m64_variant() {
 
 template <int QA, int QB>
 void launch_t(void* out, long out_stride, float* ws, const void* x, long x_stride, const Parts& P, int tiles,
-              int M, int Ntot, int K, int S, hipStream_t s) {
+              int M, int Ntot, int K, int S, hipStream_t s, const void* x16) {
   constexpr int RT = 2, NW = kWaves;
   const int nsb = K / 256;
   const int per = (nsb + S - 1) / S;
@@ -746,14 +763,19 @@ void launch_t(void* out, long out_stride, float* ws, const void* x, long x_strid
   const dim3 grid(tiles, (nsb + per - 1) / per, M > 64 ? (M + 63) / 64 : 1), block(64 * NW);
   auto* o = static_cast<unsigned short*>(out);
   auto* xi = static_cast<const unsigned short*>(x);
+  auto* xh = static_cast<const unsigned short*>(x16);
   if (M <= 16)
-    qgemm2_kernel<QA, QB, 1, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+    qgemm2_kernel<QA, QB, 1, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per, nullptr);
   else if (M <= 32)
-    qgemm2_kernel<QA, QB, 2, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+    qgemm2_kernel<QA, QB, 2, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per, nullptr);
   else if (m64_variant() == 1)  // 4 waves x 2 row groups
-    qgemm2_kernel<QA, QB, 4, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+    qgemm2_kernel<QA, QB, 4, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per, nullptr);
+  else if (xh != nullptr && M <= 64)  // 8 waves x 1 row group, x staged from the producer's f16 copy
+    qgemm2_kernel<QA, QB, 4, 1, 8, true><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per,
+                                                                    xh);
   else  // 8 waves x 1 row group: half the accumulators and weight registers per wave
-    qgemm2_kernel<QA, QB, 4, 1, 8><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per);
+    qgemm2_kernel<QA, QB, 4, 1, 8><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per,
+                                                              nullptr);
 }
 
 // MoE experts: grid (row tiles of N, K splits, expert tiles); workgroups of tiles past
@@ -846,7 +868,8 @@ int gguf_tiled_chunk_bytes(int qtype) {
 // out (S must be 1). Parts of one format, or of the pairs Q4_K+Q6_K / Q5_K+Q6_K
 // (the K-quant mixes), share one launch; any other mix launches per format.
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
-                            const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s) {
+                            const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
+                            const void* x16) {
   constexpr int ROWS = 16 * 2 * kWaves;
   int fmts[kMaxParts], nf = 0;
   for (int i = 0; i < nparts; ++i) {
@@ -870,23 +893,23 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
     const int a = fmts[0] < fmts[1] ? fmts[0] : fmts[1], b = fmts[0] < fmts[1] ? fmts[1] : fmts[0];
     if ((a == Q4_K || a == Q5_K) && b == Q6_K) {
       const Parts P = table(a, b, tiles);
-      if (a == Q4_K) launch_t<Q4_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s);
-      else launch_t<Q5_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s);
+      if (a == Q4_K) launch_t<Q4_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16);
+      else launch_t<Q5_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16);
       return;
     }
   }
   for (int f = 0; f < nf; ++f) {
     const Parts P = table(fmts[f], fmts[f], tiles);
     switch (fmts[f]) {
-      case Q4_0: launch_t<Q4_0, Q4_0>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case Q4_1: launch_t<Q4_1, Q4_1>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case Q8_0: launch_t<Q8_0, Q8_0>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case Q4_K: launch_t<Q4_K, Q4_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case Q5_K: launch_t<Q5_K, Q5_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case Q6_K: launch_t<Q6_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case FP8: launch_t<FP8, FP8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case FP8B: launch_t<FP8B, FP8B>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
-      case INT8: launch_t<INT8, INT8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s); break;
+      case Q4_0: launch_t<Q4_0, Q4_0>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case Q4_1: launch_t<Q4_1, Q4_1>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case Q8_0: launch_t<Q8_0, Q8_0>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case Q4_K: launch_t<Q4_K, Q4_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case Q5_K: launch_t<Q5_K, Q5_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case Q6_K: launch_t<Q6_K, Q6_K>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case FP8: launch_t<FP8, FP8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case FP8B: launch_t<FP8B, FP8B>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case INT8: launch_t<INT8, INT8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
     }
   }
 }

@@ -264,7 +264,8 @@ void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const 
 // (returned S_actual = ceil(nsb / ceil(nsb / S))); else bf16 out [M, >= Ntot], S == 1.
 int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const std::vector<at::Tensor>& qs,
                         const std::vector<at::Tensor>& rss, const std::vector<int64_t>& qtypes, const std::vector<int64_t>& rows,
-                        const std::vector<int64_t>& cols, int64_t Ntot, int64_t K, int64_t splits) {
+                        const std::vector<int64_t>& cols, int64_t Ntot, int64_t K, int64_t splits,
+                        const c10::optional<at::Tensor>& x16) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x);
   const int np = qs.size();
   TORCH_CHECK(np >= 1 && np <= 4 && (int)qtypes.size() == np && (int)rss.size() == np && (int)rows.size() == np && (int)cols.size() == np,
@@ -301,9 +302,16 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
     CHECK_BF16(out); CHECK_ROWMAJOR(out);
     TORCH_CHECK(out.size(0) == M && out.size(1) >= Ntot && out.stride(0) % 4 == 0 && out.device() == x.device());
   }
+  const void* x16p = nullptr;
+  if (x16.has_value() && x16->defined()) {  // f16 pair-order copy of x from the producer (M <= 64)
+    TORCH_CHECK(x16->scalar_type() == at::kHalf && x16->size(0) == M && x16->size(1) >= K &&
+                    x16->stride(0) == x.stride(0) && x16->stride(1) == 1 && x16->device() == x.device(),
+                "gguf_gemm_parts: x16 f16 [M, >= K] with x's row stride");
+    x16p = x16->data_ptr();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::launch_gguf_gemm_parts(wp ? nullptr : out.data_ptr(), wp ? 0 : out.stride(0), wp, x.data_ptr(),
-                                   x.stride(0), P, np, M, Ntot, K, splits, cur_stream());
+                                   x.stride(0), P, np, M, Ntot, K, splits, cur_stream(), x16p);
   return S;
 }
 
@@ -831,7 +839,7 @@ void decode_gemm_fused(int64_t fix, const at::Tensor& x, const at::Tensor& wp, i
 }
 
 void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
-                        const at::Tensor& weight, double eps) {
+                        const at::Tensor& weight, double eps, const c10::optional<at::Tensor>& out16) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous());
   const int M = residual.size(0), N = residual.size(1);
@@ -839,9 +847,15 @@ void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor&
   TORCH_CHECK(weight.numel() == N && weight.is_contiguous() &&
               (weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat));
   c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  void* o16 = nullptr;
+  if (out16.has_value() && out16->defined()) {
+    TORCH_CHECK(out16->scalar_type() == at::kHalf && out16->sizes() == out.sizes() && out16->is_contiguous(),
+                "splitk_add_rmsnorm: out16 f16 like out");
+    o16 = out16->data_ptr();
+  }
   hipserve::launch_splitk_add_rmsnorm(out.data_ptr(), residual.data_ptr(), ws.data_ptr<float>(), splits,
                                       weight.data_ptr(), weight.scalar_type() == at::kFloat, M, N, (float)eps,
-                                      cur_stream());
+                                      cur_stream(), o16);
 }
 
 void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
@@ -893,14 +907,22 @@ void splitk_reduce(at::Tensor& out, const at::Tensor& ws, int64_t splits) {
   hipserve::launch_splitk_reduce(out.data_ptr(), out.stride(0), ws.data_ptr<float>(), M, N, splits, cur_stream());
 }
 
-void splitk_glu(at::Tensor& act, const at::Tensor& ws, int64_t splits, bool gelu) {
+void splitk_glu(at::Tensor& act, const at::Tensor& ws, int64_t splits, bool gelu,
+                const c10::optional<at::Tensor>& act16) {
   CHECK_DEV(act); CHECK_BF16(act); CHECK_ROWMAJOR(act);
   const int M = act.size(0), I = act.size(1);
   TORCH_CHECK(I % 8 == 0 && act.stride(0) % 8 == 0, "splitk_glu: I % 8 == 0");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * 2L * I);
   c10::hip::HIPGuardMasqueradingAsCUDA g(act.device());
+  void* a16 = nullptr;
+  if (act16.has_value() && act16->defined()) {
+    TORCH_CHECK(act16->scalar_type() == at::kHalf && act16->sizes() == act.sizes() &&
+                    act16->stride(0) == act.stride(0) && act16->stride(1) == 1,
+                "splitk_glu: act16 f16 like act");
+    a16 = act16->data_ptr();
+  }
   hipserve::launch_splitk_glu(act.data_ptr(), act.stride(0), ws.data_ptr<float>(), splits, M, I, gelu,
-                              cur_stream());
+                              cur_stream(), a16);
 }
 
 void pack_decode_weight(at::Tensor& out, const at::Tensor& w, bool glu) {
@@ -1090,7 +1112,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_gemm(Tensor(a!) out, Tensor x, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K, Tensor(b!) ws, int splits) -> ()");
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
   // custom all-reduce control ops carry an opaque state handle: catch-all kernels
-  m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits) -> int", &gguf_gemm_parts);
+  m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits, Tensor? x16=None) -> int", &gguf_gemm_parts);
   m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
   m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits) -> int", &qmoe_gemm);
   m.def("car_create(int rank, int world, int max_bytes, int nb_large=512) -> int", &car_create);
@@ -1118,8 +1140,8 @@ TORCH_LIBRARY(hipserve, m) {
         "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
         "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
         "int head_dim, int block_size, int mode, Tensor? bias, Tensor? q_w, Tensor? k_w) -> ()");
-  m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps) -> ()");
-  m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu) -> ()");
+  m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None) -> ()");
+  m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
   m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode, Tensor? bias=None, Tensor? q_w=None, Tensor? k_w=None, float eps=1e-6) -> ()");

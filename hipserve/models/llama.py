@@ -461,7 +461,7 @@ class LlamaModel:
         src, tok = meta.id_src
         return torch.where(src >= 0, tok.index_select(0, src.clamp(min=0)), ids)
 
-    def add_rmsnorm(self, out, residual, x, splits, w):
+    def add_rmsnorm(self, out, residual, x, splits, w, out16=None):
         """residual += x summed over the TP ranks; out = RMSNorm(residual) * w.
         ``x`` is this rank's partial output of a row-parallel projection: fp32
         split-K partials [S, M, N] of a decode GEMM, or the plain projection output
@@ -469,10 +469,12 @@ class LlamaModel:
         kernels; TP>1 the in-house cross-rank epilogue (parallel/comm.py)."""
         eps = self.cfg.rms_norm_eps
         if self.tp.world_size > 1:
+            assert out16 is None, "out16 needs TP = 1"
             return self.tp.add_rmsnorm(out, residual, x, splits, w, eps, ops=self.ops)
         if x.dtype == torch.float32 and residual.dtype != torch.float32:
-            torch.ops.hipserve.splitk_add_rmsnorm(out, residual, x, splits, w, eps)
+            torch.ops.hipserve.splitk_add_rmsnorm(out, residual, x, splits, w, eps, out16)
         else:
+            assert out16 is None, "out16 needs the split-K partial path"
             self.ops.fused_add_rmsnorm(out, x, residual, w, eps)
         return out
 
@@ -623,9 +625,10 @@ class LlamaModel:
         L = len(self.layers)
         lw0 = self.layers[0]
         extras = lw0.bqkv is not None or lw0.q_norm is not None
+        xn16 = None  # f16 pair-order copy of xn from its producer (quantised GEMM input)
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
-            pt = self._partial(xn, lw.wqkv)
+            pt = self._partial(xn, lw.wqkv, xn16)
             if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
@@ -649,28 +652,34 @@ class LlamaModel:
                                  nq, nkv, part, self.scale)
             pt = self._partial(attn, lw.wo)
             if pt is not None:
-                self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2)
+                xn16 = self._x16(xn, lw.wgu) if lw.router is None else None
+                self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2, xn16)
             else:
+                xn16 = None
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(attn, lw.wo), 1, lw.ln2)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             if lw.router is not None:  # MoE MLP: routed expert GEMMs, then residual + next norm
                 self.add_rmsnorm(xn, residual, self.moe(xn, lw), 1, nxt)
                 continue
             gc = gemm.glu_choice(T, lw.wgu)
-            pt = None if gc is not None or isinstance(lw.wgu, torch.Tensor) else self._partial(xn, lw.wgu)
+            pt = None if gc is not None or isinstance(lw.wgu, torch.Tensor) else self._partial(xn, lw.wgu, xn16)
+            act16 = None
             if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
             elif pt is not None:   # quantised gate|up: GLU over the plain-layout partials
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
-                op.splitk_glu(act, pt[0], pt[1], False)
+                act16 = self._x16(act, lw.wd)
+                op.splitk_glu(act, pt[0], pt[1], self.cfg.hidden_act == "gelu_tanh", act16)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 ops.silu_and_mul(act, gu)
-            pt = self._partial(act, lw.wd)
+            pt = self._partial(act, lw.wd, act16)
             if pt is not None:
-                self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt)
+                xn16 = self._x16(xn, self.layers[i + 1].wqkv) if i + 1 < L else None
+                self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt, xn16)
             else:
+                xn16 = None
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(act, lw.wd), 1, nxt)
         return xn
 
@@ -771,17 +780,30 @@ class LlamaModel:
         ws = [self.lm_head] + [getattr(lw, n) for lw in self.layers for n in ("wqkv", "wo", "wgu", "wd")]
         return [w for w in ws if isinstance(w, Q.QuantWeight)]
 
-    def _partial(self, x: torch.Tensor, w):
+    def _partial(self, x: torch.Tensor, w, x16: torch.Tensor | None = None):
         """(fp32 split-K partials [S, M, N], S) of ``x @ w.T`` for a fused decode
         epilogue: the tuned bf16 decode GEMM, or the GGUF MFMA GEMM for a
-        ``QuantWeight``; None when the projection runs unfused (hipBLASLt choice)."""
+        ``QuantWeight`` (``x16``: the producer's f16 copy of x, see ``_x16``); None
+        when the projection runs unfused (hipBLASLt choice)."""
         if isinstance(w, torch.Tensor):
             fc = gemm.fused_choice(x.shape[0], w)
             return gemm.gemm_partial(x, w, fc) if fc is not None else None
         from ..ops import quant as Q
         if getattr(w, "v2", False) and x.shape[0] <= Q.MAX_FUSED_M and x.is_cuda:
-            return Q.quant_partial(x, w)
+            return Q.quant_partial(x, w, x16)
         return None
+
+    X16 = os.environ.get("HIPSERVE_QGEMM_X16", "1") != "0"
+
+    def _x16(self, like: torch.Tensor, consumer):
+        """f16 buffer for the pair-order copy of ``like`` that its producer
+        (splitk_add_rmsnorm / splitk_glu) writes when the consumer is a quantised
+        decode GEMM at 33..64 rows (gguf_mfma.hip kX16: no bf16 -> f16 conversion in
+        every workgroup); None otherwise."""
+        if (not self.X16 or self.tp.world_size != 1 or not like.is_cuda or not 32 < like.shape[0] <= 64
+                or not getattr(consumer, "v2", False) or not hasattr(torch.ops.hipserve, "splitk_glu")):
+            return None
+        return torch.empty(like.shape, dtype=torch.float16, device=like.device)
 
     def _decode_split(self, Td: int, meta: AttnMeta):
         """Context partition size for the decode attention: with >= 512 (sequence,

@@ -421,10 +421,10 @@ def _empty(device, dtype):
     return t
 
 
-def _launch_v2(out, ws, x, w: QuantWeight, S: int):
+def _launch_v2(out, ws, x, w: QuantWeight, S: int, x16=None):
     w.groups  # (re)builds v2_args
     a = w.v2_args
-    torch.ops.hipserve.gguf_gemm_parts(out, ws, x, a[0], a[1], a[2], a[3], a[4], w.N, w.K, S)
+    torch.ops.hipserve.gguf_gemm_parts(out, ws, x, a[0], a[1], a[2], a[3], a[4], w.N, w.K, S, x16)
 
 
 def _graph_time_us(fn, reps: int = 10, rounds: int = 3) -> float:
@@ -481,13 +481,15 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
     return report
 
 
-def quant_partial(x: torch.Tensor, w: QuantWeight):
+def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = None):
     """Decode GEMM writing fp32 split-K partials ws[S, M, N] for a fused epilogue
-    (splitk_rope_cache / splitk_add_rmsnorm / splitk_glu); returns (ws, S)."""
+    (splitk_rope_cache / splitk_add_rmsnorm / splitk_glu); returns (ws, S). ``x16``:
+    the producer's f16 pair-order copy of x (splitk_add_rmsnorm / splitk_glu
+    ``out16``), staged as is instead of converting x in every workgroup."""
     M = x.shape[0]
     S = v2_splits(w, M)
     ws = torch.empty(S * M * w.N, dtype=torch.float32, device=x.device)
-    _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S)
+    _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S, x16)
     return ws, S
 
 

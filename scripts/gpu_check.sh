@@ -99,6 +99,7 @@ for s in $steps; do
     pgemm_g27) run_pgemm gemma27b ;;
     f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
     f16test) run_one tests/test_gguf_gpu.py ;;
+    fusedtest) run_one tests/test_fused_decode_gpu.py ;;
     pgtest) run_one tests/test_prefill_gemm_gpu.py ;;
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof) prof_run prof ;;

@@ -498,3 +498,45 @@ def test_wide_scale_weight_runs_v1():
     want = x.float() @ _dense([(G.Q4_K, N, K, raw)]).T
     y = quant_linear(x, qw).float()
     assert (y - want).abs().max().item() < 1e-2 * want.abs().max().item() + 1e-3
+
+
+def _pair_order_f16(x):
+    """x (bf16 [M, K]) -> f16 in the quantised GEMM's staging pair order per 8-run."""
+    h = x.float().to(torch.float16).reshape(x.shape[0], -1, 8)
+    return h[:, :, [0, 2, 1, 3, 4, 6, 5, 7]].reshape(x.shape).contiguous()
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K, G.Q8_0])
+def test_x16_staging_matches_conversion(qt):
+    """gguf_mfma.hip kX16: staging the producer's f16 pair-order copy of x gives the
+    same partials, bit for bit, as converting bf16 x in every workgroup (M = 33..64);
+    rows past the f16 range still take the pre-scaled second pass."""
+    from hipserve.ops.quant import quant_partial
+    K = 2048
+    qw, raws = _rand_qw([(qt, 512, K), (qt, 256, K)], seed=11)
+    for M in (40, 64):
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        x[3] *= 2e5  # beyond f16: inf in x16 -> caught on the accumulators
+        ws0, S0 = quant_partial(x, qw)
+        ws1, S1 = quant_partial(x, qw, _pair_order_f16(x))
+        assert S0 == S1 and torch.equal(ws0, ws1)
+
+
+def test_producers_write_pair_order_f16():
+    """splitk_add_rmsnorm / splitk_glu out16: the f16 pair-order copy of their bf16
+    output, exactly."""
+    op = torch.ops.hipserve
+    M, N, S = 48, 4096, 3
+    ws = torch.randn(S, M, N, device="cuda")
+    res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    w = (torch.rand(N, device="cuda") + 0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    out16 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    op.splitk_add_rmsnorm(out, res, ws, S, w, 1e-5, out16)
+    assert torch.equal(out16, _pair_order_f16(out))
+    I = 2048
+    wsg = torch.randn(S, M, 2 * I, device="cuda")
+    act = torch.empty(M, I, device="cuda", dtype=torch.bfloat16)
+    act16 = torch.empty(M, I, device="cuda", dtype=torch.float16)
+    op.splitk_glu(act, wsg, S, False, act16)
+    assert torch.equal(act16, _pair_order_f16(act))

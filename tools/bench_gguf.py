@@ -109,6 +109,10 @@ def main():
                 continue
             rows = []
             rows.append(("v2_partial", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw))))
+            if 32 < M <= 64:  # x staged from a producer's f16 pair-order copy (kX16)
+                h = x.float().to(torch.float16).reshape(M, -1, 8)[:, :, [0, 2, 1, 3, 4, 6, 5, 7]].reshape(M, -1)
+                x16 = h.contiguous()
+                rows.append(("v2_partial_x16", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw, x16))))
             for S in a.splits or []:
                 def run(S=S):
                     ws = torch.empty(S * M * qw.N, dtype=torch.float32, device="cuda")
