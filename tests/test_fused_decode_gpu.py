@@ -271,3 +271,45 @@ def test_paged_decode_qkv_bit_exact(ops, mode, S, part, D):
                                         nq, nkv, part, scale, 0, mode)
     assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
     assert torch.equal(out1, out2)
+
+
+@pytest.mark.parametrize("scheme", ["q4_k_m", "fp8"])
+@pytest.mark.parametrize("x16", [True, False])
+def test_fused_decode_forward_quantised_bit_exact(ops, scheme, x16):
+    """Quantised model (GGUF Q4_K_M / FP8 weights) at a 48-row decode batch: the fused
+    forward (quantised GEMM partials -> fused epilogues; x16 = the producers' f16
+    pair-order copy of x staged by the GEMM) is bit-identical to the unfused forward."""
+    from hipserve.config import PRESETS
+    from hipserve.models.llama import AttnMeta, LlamaModel
+    from hipserve.parallel.comm import TPGroup
+
+    cfg = PRESETS["llama-3-8b"].replace(hidden_size=1024, intermediate_size=3584, num_heads=8, num_kv_heads=2,
+                                        num_layers=3, vocab_size=4096, max_position_embeddings=2048)
+    m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, ops, max_pos=2048)
+    m.allocate_random_quant(scheme, seed=3)
+    m.X16 = x16
+    B, bs, D = 48, 16, cfg.head_dim
+    g = torch.Generator(device=DEV).manual_seed(5)
+    ctx = torch.randint(1, 300, (B,), device=DEV, dtype=torch.int32, generator=g)
+    nblk = 64
+    bt = torch.randperm(B * nblk, device=DEV, generator=g).int().view(B, nblk)
+    pos = (ctx - 1).long()
+    slots = (bt.gather(1, (pos // bs).view(-1, 1).int()).view(-1).long() * bs + pos % bs)
+    ids = torch.randint(0, cfg.vocab_size, (B,), device=DEV, generator=g)
+    kv1 = m.allocate_kv_cache(B * nblk, bs)
+    for kc, vc in kv1:
+        kc.normal_(generator=g)
+        vc.normal_(generator=g)
+    kv2 = [(k.clone(), v.clone()) for k, v in kv1]
+    parts = math.ceil(nblk * bs / 512)
+    mk = lambda: AttnMeta(num_prefill_tokens=0, num_decode=B, positions=pos, slot_mapping=slots,
+                          bt_decode=bt, ctx_decode=ctx, tmp_out=torch.empty(B, m.nq, parts, D, device=DEV),
+                          tmp_ml=torch.empty(B, m.nq, parts, 2, device=DEV))
+    m.fused_decode = False
+    out1 = m.forward(ids, mk(), kv1).clone()
+    m.fused_decode = True
+    assert m._fused_ok(mk())
+    out2 = m.forward(ids, mk(), kv2).clone()
+    assert torch.equal(out1, out2)
+    for (k1, v1), (k2, v2) in zip(kv1, kv2):
+        assert torch.equal(k1, k2) and torch.equal(v1, v2)
