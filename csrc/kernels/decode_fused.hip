@@ -139,6 +139,118 @@ void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S
   else add_rmsnorm_t<false>(out, residual, ws, S, w, M, N, eps, s, o16);
 }
 
+// Sandwich-norm epilogue (Gemma-3: post-attention / post-feedforward RMSNorm on the
+// projection output BEFORE the residual add): h = bf16(sum_s ws); p = bf16(RMSNorm(h)
+// * w_post); residual = bf16(p + residual); out = RMSNorm(residual) * w_next — the
+// unfused chain splitk_reduce -> rmsnorm -> fused_add_rmsnorm in one kernel, with each
+// norm reduced in the row-norm kernels' order (same thread -> element map), so the
+// result is bit-identical.
+template <bool kWF32>
+HS_DEVICE void norm_w8(float (&w)[8], const void* __restrict__ weight, int idx) {
+  if constexpr (kWF32) {
+    const f32x4* wp = reinterpret_cast<const f32x4*>(weight) + idx * 2;
+    const f32x4 w0 = wp[0], w1 = wp[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w[j] = w0[j];
+      w[j + 4] = w1[j];
+    }
+  } else {
+    const u16x8 wv = reinterpret_cast<const u16x8*>(weight)[idx];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = bf16_to_f32(wv[j]);
+  }
+}
+
+template <int NT, int VPT, bool kWF32>
+__global__ __launch_bounds__(NT) void splitk_post_add_rmsnorm_kernel(unsigned short* __restrict__ out,
+                                                                      unsigned short* __restrict__ residual,
+                                                                      const float* __restrict__ ws, int S,
+                                                                      const void* __restrict__ w_post,
+                                                                      const void* __restrict__ w_next, int M, int N,
+                                                                      float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = N >> 3;
+  const long slice = (long)M * N;
+  u16x8 res[VPT];
+  u16x8* rr = reinterpret_cast<u16x8*>(residual + (long)row * N);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) res[i] = rr[idx];
+  }
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      sum8_bf16(v[i], ws + (long)row * N + idx * 8, slice, S);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv1 = rsqrtf(ss / N + eps);
+  float ss2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      float w[8];
+      norm_w8<kWF32>(w, w_post, idx);
+      u16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = bf16_to_f32(f32_to_bf16(v[i][j] * inv1 * w[j]));
+        r[j] = f32_to_bf16(p + bf16_to_f32(res[i][j]));
+        v[i][j] = bf16_to_f32(r[j]);
+        ss2 += v[i][j] * v[i][j];
+      }
+      rr[idx] = r;
+    }
+  }
+  ss2 = block_sum(ss2, scratch);
+  const float inv2 = rsqrtf(ss2 / N + eps);
+  u16x8* orow = reinterpret_cast<u16x8*>(out + (long)row * N);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      float w[8];
+      norm_w8<kWF32>(w, w_next, idx);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv2 * w[j]);
+      orow[idx] = o;
+    }
+  }
+}
+
+template <bool kWF32>
+static void post_add_rmsnorm_t(void* out, void* residual, const float* ws, int S, const void* wp, const void* wn,
+                               int M, int N, float eps, hipStream_t s) {
+  auto* o = static_cast<unsigned short*>(out);
+  auto* r = static_cast<unsigned short*>(residual);
+  const int nvec = N / 8;
+  if (norm_threads(N) == 256) {
+    if (nvec <= 256) splitk_post_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+    else splitk_post_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+  } else {
+    if (nvec <= 512) splitk_post_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+    else if (nvec <= 1024) splitk_post_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+    else splitk_post_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+  }
+}
+
+void launch_splitk_post_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w_post,
+                                    const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s) {
+  if (M <= 0) return;
+  if (weight_f32) post_add_rmsnorm_t<true>(out, residual, ws, S, w_post, w_next, M, N, eps, s);
+  else post_add_rmsnorm_t<false>(out, residual, ws, S, w_post, w_next, M, N, eps, s);
+}
+
 // The rope_cache kernel (rope_cache.hip) reading its input from the split-K
 // partials instead of a bf16 qkv row. Work item = one 8-wide chunk: (q/k head,
 // chunk) pairs first, then the v chunks; 64-thread workgroups over

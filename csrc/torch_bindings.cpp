@@ -858,6 +858,22 @@ void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor&
                                       cur_stream(), o16);
 }
 
+void splitk_post_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
+                             const at::Tensor& w_post, const at::Tensor& w_next, double eps) {
+  CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous());
+  const int M = residual.size(0), N = residual.size(1);
+  TORCH_CHECK(out.sizes() == residual.sizes() && ws.numel() >= splits * M * N && N % 8 == 0 && N <= 16384);
+  TORCH_CHECK(w_post.numel() == N && w_next.numel() == N && w_post.is_contiguous() && w_next.is_contiguous() &&
+                  w_post.scalar_type() == w_next.scalar_type() &&
+                  (w_post.scalar_type() == at::kBFloat16 || w_post.scalar_type() == at::kFloat),
+              "splitk_post_add_rmsnorm: both norm weights bf16 or both fp32 [N]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  hipserve::launch_splitk_post_add_rmsnorm(out.data_ptr(), residual.data_ptr(), ws.data_ptr<float>(), splits,
+                                           w_post.data_ptr(), w_next.data_ptr(), w_post.scalar_type() == at::kFloat,
+                                           M, N, (float)eps, cur_stream());
+}
+
 void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
                        const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
                        int64_t nq, int64_t nkv, int64_t head_dim, int64_t mode,
@@ -1141,6 +1157,7 @@ TORCH_LIBRARY(hipserve, m) {
         "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
         "int head_dim, int block_size, int mode, Tensor? bias, Tensor? q_w, Tensor? k_w) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None) -> ()");
+  m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
   m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
@@ -1184,6 +1201,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm_fused", &decode_gemm_fused);
   m.impl("prefill_gemm", &prefill_gemm);
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);
+  m.impl("splitk_post_add_rmsnorm", &splitk_post_add_rmsnorm);
   m.impl("act_quant_fp8", &act_quant_fp8);
   m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);

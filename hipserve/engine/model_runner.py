@@ -125,7 +125,8 @@ class ModelRunner:
             from ..ops import gemm
 
             ms = [b for b in self.buckets if b <= 64]
-            self.model.fused_decode = bool(ecfg.extra.get("fused_decode", True))
+            self.model.fused_decode = bool(ecfg.extra.get("fused_decode",
+                                                          os.environ.get("HIPSERVE_FUSED_DECODE", "1") != "0"))
             fused = self.model.fused_gemm_shapes() if self.model.fused_decode else {}
             self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms, fused=fused)
             if ecfg.extra.get("packed_decode", True):

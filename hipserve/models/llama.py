@@ -149,12 +149,13 @@ class LlamaModel:
         self.vanilla = not (cfg.qkv_bias or cfg.qk_norm or cfg.sandwich_norm or cfg.hidden_act != "silu"
                             or any(cfg.layer_windows) or cfg.embed_scale != 1.0)
         # families the fused decode layer covers: Llama-style plus q/k/v bias (Qwen2),
-        # per-head q/k RMSNorm (Qwen3; folded into the split-K RoPE epilogue) and MoE
-        # MLPs (Mixtral, Qwen3-MoE / Qwen3-VL-MoE); Gemma-3 (sandwich norms, GeGLU,
-        # sliding windows, embedding scale) keeps the unfused layer
-        self.fused_family = not (cfg.sandwich_norm or cfg.hidden_act != "silu" or any(cfg.layer_windows)
-                                 or cfg.embed_scale != 1.0) and (
-            not cfg.qk_norm or (cfg.rope_mode == 0 and self.D in (64, 128, 256)))
+        # per-head q/k RMSNorm (Qwen3; folded into the split-K RoPE epilogue), MoE MLPs
+        # (Mixtral, Qwen3-MoE / Qwen3-VL-MoE) and, at TP = 1, Gemma-3 (sandwich norms
+        # in splitk_post_add_rmsnorm, GeGLU over the gate|up partials, sliding-window
+        # layers with their local RoPE table, embedding scale)
+        self.fused_family = (cfg.hidden_act in ("silu", "gelu_tanh")
+                             and (not cfg.sandwich_norm or tp.world_size == 1)
+                             and (not cfg.qk_norm or (cfg.rope_mode == 0 and self.D in (64, 128, 256))))
         self.decode_partition = 512
         self.block_size_hint = 16  # KV block size (set by the runner)
         self.quant_linear = None  # set by the GGUF loader: callable(x, qweight) -> y
@@ -364,7 +365,7 @@ class LlamaModel:
         With the fused decode path the merged gate|up weight is packed
         gate/up-interleaved instead (``PACKED_GLU``: the SiLU-GLU runs in its epilogue)."""
         n = 0
-        glu = self.fused_decode and self.fused_family
+        glu = self.fused_decode and self.fused_family and self.cfg.hidden_act == "silu"
         # HBM budget: a packed copy is only made while >= 24 GiB + a quarter of the
         # device stay free for the KV cache (a 70B model on ONE 288 GB MI355X keeps
         # most weights unpacked; the tuner's packed choice then runs on the plain layout)
@@ -438,8 +439,8 @@ class LlamaModel:
             out[tuple(lw.wd.shape)] = ("norm",)
         if isinstance(lw.wqkv, torch.Tensor):
             out[tuple(lw.wqkv.shape)] = ("rope", self.nq, self.nkv, self.D, self.cfg.rope_mode)
-        if isinstance(lw.wgu, torch.Tensor) and lw.wgu.shape[0] % 128 == 0:
-            out[tuple(lw.wgu.shape)] = ("glu",)
+        if isinstance(lw.wgu, torch.Tensor) and lw.wgu.shape[0] % 128 == 0 and self.cfg.hidden_act == "silu":
+            out[tuple(lw.wgu.shape)] = ("glu",)  # GeGLU: plain partials + splitk_glu (tuned as a plain GEMM)
         return out
 
     def _fused_ok(self, meta: AttnMeta) -> bool:
@@ -452,7 +453,7 @@ class LlamaModel:
         (``embed_rmsnorm``, norm.hip). TP=1 only (the vocab-parallel embedding needs a
         cross-rank sum before the norm)."""
         return (self._fused_ok(meta) and self.tp.world_size == 1 and self.embed.dtype == torch.bfloat16
-                and hasattr(torch.ops.hipserve, "embed_rmsnorm"))
+                and self.cfg.embed_scale == 1.0 and hasattr(torch.ops.hipserve, "embed_rmsnorm"))
 
     @staticmethod
     def resolve_ids(ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
@@ -476,6 +477,24 @@ class LlamaModel:
         else:
             assert out16 is None, "out16 needs the split-K partial path"
             self.ops.fused_add_rmsnorm(out, x, residual, w, eps)
+        return out
+
+    def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next):
+        """Sandwich-norm epilogue (Gemma-3, TP = 1): residual += RMSNorm(x @ w.T) *
+        w_post; out = RMSNorm(residual) * w_next — one kernel over the split-K
+        partials ``pt`` when the decode GEMM wrote them, else the unfused chain of
+        ``forward`` (bit-identical either way)."""
+        eps = self.cfg.rms_norm_eps
+        if pt is not None and w_post.dtype == w_next.dtype and residual.dtype == torch.bfloat16:
+            torch.ops.hipserve.splitk_post_add_rmsnorm(out, residual, pt[0], pt[1], w_post, w_next, eps)
+            return out
+        if pt is not None:
+            o = torch.empty_like(residual)
+            torch.ops.hipserve.splitk_reduce(o, pt[0], pt[1])
+        else:
+            o = self.linear_rowpar(x, w)
+        self.ops.rmsnorm(o, o, w_post, eps)
+        self.ops.fused_add_rmsnorm(out, o, residual, w_next, eps)
         return out
 
     def linear_rowpar(self, x: torch.Tensor, w) -> torch.Tensor:
@@ -617,6 +636,8 @@ class LlamaModel:
             h = residual
         else:
             h = self.embed_tokens(self.resolve_ids(ids, meta))
+            if cfg.embed_scale != 1.0:  # Gemma: as forward()
+                h = h * float(torch.tensor(cfg.embed_scale, dtype=h.dtype))
             residual = h.clone()
             xn = torch.empty_like(h)
             ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
@@ -628,8 +649,10 @@ class LlamaModel:
         xn16 = None  # f16 pair-order copy of xn from its producer (quantised GEMM input)
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
+            win = cfg.window_of(i)
+            cs = self.cos_sin_local if win else self.cos_sin
             pt = self._partial(xn, lw.wqkv, xn16)
-            if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras:
+            if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras and not win:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
                                     meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part, self.scale,
@@ -637,7 +660,7 @@ class LlamaModel:
             elif pt is not None:  # + q/k/v bias and per-head q/k RMSNorm of the family, if any
                 ws, S = pt
                 qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)
-                op.splitk_rope_cache(qkv, ws, S, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
+                op.splitk_rope_cache(qkv, ws, S, meta.positions, meta.slot_mapping, cs, kc, vc,
                                      nq, nkv, D, cfg.rope_mode, lw.bqkv, lw.q_norm, lw.k_norm, eps)
             else:
                 qkv = self.linear(xn, lw.wqkv)
@@ -645,13 +668,16 @@ class LlamaModel:
                     qkv += lw.bqkv
                 if lw.q_norm is not None:
                     ops.qk_rmsnorm(qkv, lw.q_norm, lw.k_norm, nq, nkv, D, eps)
-                ops.rope_cache(qkv, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
+                ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cs, kc, vc, nq, nkv, D,
                                cfg.rope_mode)
-            if pt is None or not (self.fused_qkv_attention and D in (64, 128) and not extras):
+            if pt is None or not (self.fused_qkv_attention and D in (64, 128) and not extras and not win):
                 ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
-                                 nq, nkv, part, self.scale)
+                                 nq, nkv, part, self.scale, win)
             pt = self._partial(attn, lw.wo)
-            if pt is not None:
+            if lw.post_attn_norm is not None:  # Gemma sandwich norm (TP = 1: fused_family)
+                xn16 = None
+                self.post_add_rmsnorm(xn, residual, pt, attn, lw.wo, lw.post_attn_norm, lw.ln2)
+            elif pt is not None:
                 xn16 = self._x16(xn, lw.wgu) if lw.router is None else None
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2, xn16)
             else:
@@ -661,21 +687,26 @@ class LlamaModel:
             if lw.router is not None:  # MoE MLP: routed expert GEMMs, then residual + next norm
                 self.add_rmsnorm(xn, residual, self.moe(xn, lw), 1, nxt)
                 continue
-            gc = gemm.glu_choice(T, lw.wgu)
-            pt = None if gc is not None or isinstance(lw.wgu, torch.Tensor) else self._partial(xn, lw.wgu, xn16)
+            gelu = cfg.hidden_act == "gelu_tanh"
+            gc = None if gelu else gemm.glu_choice(T, lw.wgu)
+            pt = (None if gc is not None or (isinstance(lw.wgu, torch.Tensor) and not gelu)
+                  else self._partial(xn, lw.wgu, xn16))
             act16 = None
             if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
-            elif pt is not None:   # quantised gate|up: GLU over the plain-layout partials
+            elif pt is not None:   # quantised gate|up, or GeGLU: the GLU over the plain-layout partials
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 act16 = self._x16(act, lw.wd)
-                op.splitk_glu(act, pt[0], pt[1], self.cfg.hidden_act == "gelu_tanh", act16)
+                op.splitk_glu(act, pt[0], pt[1], gelu, act16)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
-                ops.silu_and_mul(act, gu)
+                self.act_and_mul(act, gu)
             pt = self._partial(act, lw.wd, act16)
-            if pt is not None:
+            if lw.post_ff_norm is not None:
+                xn16 = None
+                self.post_add_rmsnorm(xn, residual, pt, act, lw.wd, lw.post_ff_norm, nxt)
+            elif pt is not None:
                 xn16 = self._x16(xn, self.layers[i + 1].wqkv) if i + 1 < L else None
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt, xn16)
             else:
@@ -697,8 +728,11 @@ class LlamaModel:
         T — the tuned packed decode GEMM's S for each projection — or None when the
         layer does not qualify (TP > 1, MoE / quantised / sandwich families, a
         projection the tuner left to hipBLASLt, weights without a packed copy)."""
+        cfg = self.cfg
         if not (self.fused_v2 and self.tp.world_size == 1 and T <= 64 and self.D in (64, 128)
                 and getattr(self, "_dgf_counters", None) is not None):
+            return None
+        if cfg.sandwich_norm or cfg.hidden_act != "silu" or any(cfg.layer_windows) or cfg.embed_scale != 1.0:
             return None
         lw0 = self.layers[0]
         ws = (lw0.wqkv, lw0.wo, lw0.wgu, lw0.wd)

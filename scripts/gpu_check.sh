@@ -94,6 +94,8 @@ for s in $steps; do
     g27fp8) bench_named g27fp8 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b --quantization fp8 ;;
     g27fp8_shadow) bench_named g27fp8_shadow HIPSERVE_FP8_PREFILL=0 -- --model gemma-3-27b --quantization fp8 ;;
     g27bf16) bench_named g27bf16 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b ;;
+    g27bf16_unfused) bench_named g27bf16_unfused HIPSERVE_FUSED_DECODE=0 -- --model gemma-3-27b ;;
+    g27fp8_unfused) bench_named g27fp8_unfused HIPSERVE_FUSED_DECODE=0 -- --model gemma-3-27b --quantization fp8 ;;
     q4km) bench_named q4km HIPSERVE_QUANT_SHADOW=1 -- --quantization q4_k_m ;;
     q4km_x16off) bench_named q4km_x16off HIPSERVE_QGEMM_X16=0 -- --quantization q4_k_m ;;
     q4km_noshadow) bench_named q4km_noshadow HIPSERVE_QUANT_SHADOW=0 -- --quantization q4_k_m ;;

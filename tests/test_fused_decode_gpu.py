@@ -122,6 +122,10 @@ def _small_model(ops, seed=0, family="llama"):
         cfg = cfg.replace(family="qwen2", qkv_bias=True)
     elif family == "qwen3":
         cfg = cfg.replace(family="qwen3", qk_norm=True)
+    elif family == "gemma3":  # sandwich norms, GeGLU, local/global layers, embedding scale, q/k norm
+        cfg = cfg.replace(family="gemma3", qk_norm=True, hidden_act="gelu_tanh", sandwich_norm=True,
+                          norm_offset=True, embed_scale=1024 ** 0.5, attn_scale=128 ** -0.5, sliding_window=96,
+                          layer_windows=(96, 0, 96), rope_local_theta=1e4, rms_norm_eps=1e-6)
     elif family == "qwen3_moe":
         cfg = cfg.replace(family="qwen3_moe", architecture="mixtral", qk_norm=True, num_experts=8,
                           num_experts_per_tok=2, moe_intermediate_size=512)
@@ -134,6 +138,10 @@ def _small_model(ops, seed=0, family="llama"):
         if lw.q_norm is not None:
             lw.q_norm = 1 + 0.2 * torch.randn(lw.q_norm.shape, device=DEV, generator=g)
             lw.k_norm = 1 + 0.2 * torch.randn(lw.k_norm.shape, device=DEV, generator=g)
+        if lw.post_attn_norm is not None:
+            for n in ("post_attn_norm", "post_ff_norm", "ln1", "ln2"):
+                t = getattr(lw, n)
+                setattr(lw, n, (1 + 0.2 * torch.randn(t.shape, device=DEV, generator=g)).to(t.dtype))
     return m, cfg
 
 
@@ -172,7 +180,7 @@ def test_splitk_rope_cache_extras_bit_exact(ops, bias, norm, D, S):
     assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
 
 
-@pytest.mark.parametrize("family", ["qwen2", "qwen3", "qwen3_moe"])
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "qwen3_moe", "gemma3"])
 def test_fused_decode_forward_families_bit_exact(ops, family):
     test_fused_decode_forward_bit_exact(ops, "dgp", family)
 
