@@ -228,7 +228,8 @@ void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S
 // sandwich norm (Gemma-3): residual = bf16(RMSNorm(bf16(sum_s ws)) * w_post + residual);
 // out = RMSNorm(residual) * w_next (both weights bf16, or both fp32)
 void launch_splitk_post_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w_post,
-                                    const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s);
+                                    const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s,
+                                    void* out16 = nullptr);
 // qkv = bf16(sum_s ws) -> RoPE(q, k) -> q into qkv[:, :nq*D], k/v into the paged cache
 // out[M, N] (bf16, row stride out_stride) = sum of the fp32 partials ws[S, M, N] (decode_gemm.hip)
 void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, int N, int S, hipStream_t s);

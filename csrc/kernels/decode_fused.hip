@@ -168,7 +168,7 @@ __global__ __launch_bounds__(NT) void splitk_post_add_rmsnorm_kernel(unsigned sh
                                                                       const float* __restrict__ ws, int S,
                                                                       const void* __restrict__ w_post,
                                                                       const void* __restrict__ w_next, int M, int N,
-                                                                      float eps) {
+                                                                      float eps, unsigned short* __restrict__ out16) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = N >> 3;
@@ -224,31 +224,34 @@ __global__ __launch_bounds__(NT) void splitk_post_add_rmsnorm_kernel(unsigned sh
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv2 * w[j]);
       orow[idx] = o;
+      if (out16 != nullptr) reinterpret_cast<u16x8*>(out16 + (long)row * N)[idx] = f16_pairs8(o);
     }
   }
 }
 
 template <bool kWF32>
 static void post_add_rmsnorm_t(void* out, void* residual, const float* ws, int S, const void* wp, const void* wn,
-                               int M, int N, float eps, hipStream_t s) {
+                               int M, int N, float eps, hipStream_t s, unsigned short* o16) {
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
   const int nvec = N / 8;
   if (norm_threads(N) == 256) {
-    if (nvec <= 256) splitk_post_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
-    else splitk_post_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+    if (nvec <= 256) splitk_post_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
+    else splitk_post_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
   } else {
-    if (nvec <= 512) splitk_post_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
-    else if (nvec <= 1024) splitk_post_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
-    else splitk_post_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps);
+    if (nvec <= 512) splitk_post_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
+    else if (nvec <= 1024) splitk_post_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
+    else splitk_post_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
   }
 }
 
 void launch_splitk_post_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w_post,
-                                    const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s) {
+                                    const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s,
+                                    void* out16) {
   if (M <= 0) return;
-  if (weight_f32) post_add_rmsnorm_t<true>(out, residual, ws, S, w_post, w_next, M, N, eps, s);
-  else post_add_rmsnorm_t<false>(out, residual, ws, S, w_post, w_next, M, N, eps, s);
+  auto* o16 = static_cast<unsigned short*>(out16);
+  if (weight_f32) post_add_rmsnorm_t<true>(out, residual, ws, S, w_post, w_next, M, N, eps, s, o16);
+  else post_add_rmsnorm_t<false>(out, residual, ws, S, w_post, w_next, M, N, eps, s, o16);
 }
 
 // The rope_cache kernel (rope_cache.hip) reading its input from the split-K

@@ -859,7 +859,8 @@ void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor&
 }
 
 void splitk_post_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
-                             const at::Tensor& w_post, const at::Tensor& w_next, double eps) {
+                             const at::Tensor& w_post, const at::Tensor& w_next, double eps,
+                             const c10::optional<at::Tensor>& out16) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous());
   const int M = residual.size(0), N = residual.size(1);
@@ -868,10 +869,16 @@ void splitk_post_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Te
                   w_post.scalar_type() == w_next.scalar_type() &&
                   (w_post.scalar_type() == at::kBFloat16 || w_post.scalar_type() == at::kFloat),
               "splitk_post_add_rmsnorm: both norm weights bf16 or both fp32 [N]");
+  void* o16 = nullptr;
+  if (out16.has_value() && out16->defined()) {
+    TORCH_CHECK(out16->scalar_type() == at::kHalf && out16->sizes() == out.sizes() && out16->is_contiguous(),
+                "splitk_post_add_rmsnorm: out16 f16 like out");
+    o16 = out16->data_ptr();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
   hipserve::launch_splitk_post_add_rmsnorm(out.data_ptr(), residual.data_ptr(), ws.data_ptr<float>(), splits,
                                            w_post.data_ptr(), w_next.data_ptr(), w_post.scalar_type() == at::kFloat,
-                                           M, N, (float)eps, cur_stream());
+                                           M, N, (float)eps, cur_stream(), o16);
 }
 
 void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
@@ -1157,7 +1164,7 @@ TORCH_LIBRARY(hipserve, m) {
         "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
         "int head_dim, int block_size, int mode, Tensor? bias, Tensor? q_w, Tensor? k_w) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None) -> ()");
-  m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps) -> ()");
+  m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
   m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");

@@ -479,15 +479,16 @@ class LlamaModel:
             self.ops.fused_add_rmsnorm(out, x, residual, w, eps)
         return out
 
-    def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next):
+    def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next, out16=None):
         """Sandwich-norm epilogue (Gemma-3, TP = 1): residual += RMSNorm(x @ w.T) *
         w_post; out = RMSNorm(residual) * w_next — one kernel over the split-K
-        partials ``pt`` when the decode GEMM wrote them, else the unfused chain of
-        ``forward`` (bit-identical either way)."""
+        partials ``pt`` when the decode GEMM wrote them (also writing ``out16``, the
+        f16 pair-order copy for a quantised consumer; returns True), else the unfused
+        chain of ``forward`` (bit-identical either way; returns False: no out16)."""
         eps = self.cfg.rms_norm_eps
         if pt is not None and w_post.dtype == w_next.dtype and residual.dtype == torch.bfloat16:
-            torch.ops.hipserve.splitk_post_add_rmsnorm(out, residual, pt[0], pt[1], w_post, w_next, eps)
-            return out
+            torch.ops.hipserve.splitk_post_add_rmsnorm(out, residual, pt[0], pt[1], w_post, w_next, eps, out16)
+            return True
         if pt is not None:
             o = torch.empty_like(residual)
             torch.ops.hipserve.splitk_reduce(o, pt[0], pt[1])
@@ -495,7 +496,7 @@ class LlamaModel:
             o = self.linear_rowpar(x, w)
         self.ops.rmsnorm(o, o, w_post, eps)
         self.ops.fused_add_rmsnorm(out, o, residual, w_next, eps)
-        return out
+        return False
 
     def linear_rowpar(self, x: torch.Tensor, w) -> torch.Tensor:
         """Row-parallel projection (o_proj / down_proj). Under exact TP reduction
@@ -675,8 +676,9 @@ class LlamaModel:
                                  nq, nkv, part, self.scale, win)
             pt = self._partial(attn, lw.wo)
             if lw.post_attn_norm is not None:  # Gemma sandwich norm (TP = 1: fused_family)
-                xn16 = None
-                self.post_add_rmsnorm(xn, residual, pt, attn, lw.wo, lw.post_attn_norm, lw.ln2)
+                xn16 = self._x16(xn, lw.wgu) if pt is not None else None
+                if not self.post_add_rmsnorm(xn, residual, pt, attn, lw.wo, lw.post_attn_norm, lw.ln2, xn16):
+                    xn16 = None
             elif pt is not None:
                 xn16 = self._x16(xn, lw.wgu) if lw.router is None else None
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2, xn16)
@@ -704,8 +706,9 @@ class LlamaModel:
                 self.act_and_mul(act, gu)
             pt = self._partial(act, lw.wd, act16)
             if lw.post_ff_norm is not None:
-                xn16 = None
-                self.post_add_rmsnorm(xn, residual, pt, act, lw.wd, lw.post_ff_norm, nxt)
+                xn16 = self._x16(xn, self.layers[i + 1].wqkv) if pt is not None and i + 1 < L else None
+                if not self.post_add_rmsnorm(xn, residual, pt, act, lw.wd, lw.post_ff_norm, nxt, xn16):
+                    xn16 = None
             elif pt is not None:
                 xn16 = self._x16(xn, self.layers[i + 1].wqkv) if i + 1 < L else None
                 self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt, xn16)

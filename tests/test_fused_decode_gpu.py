@@ -281,9 +281,9 @@ def test_paged_decode_qkv_bit_exact(ops, mode, S, part, D):
     assert torch.equal(out1, out2)
 
 
-@pytest.mark.parametrize("scheme", ["q4_k_m", "fp8"])
+@pytest.mark.parametrize("scheme,family", [("q4_k_m", "llama"), ("fp8", "llama"), ("fp8", "gemma3")])
 @pytest.mark.parametrize("x16", [True, False])
-def test_fused_decode_forward_quantised_bit_exact(ops, scheme, x16):
+def test_fused_decode_forward_quantised_bit_exact(ops, scheme, family, x16):
     """Quantised model (GGUF Q4_K_M / FP8 weights) at a 48-row decode batch: the fused
     forward (quantised GEMM partials -> fused epilogues; x16 = the producers' f16
     pair-order copy of x staged by the GEMM) is bit-identical to the unfused forward."""
@@ -293,6 +293,10 @@ def test_fused_decode_forward_quantised_bit_exact(ops, scheme, x16):
 
     cfg = PRESETS["llama-3-8b"].replace(hidden_size=1024, intermediate_size=3584, num_heads=8, num_kv_heads=2,
                                         num_layers=3, vocab_size=4096, max_position_embeddings=2048)
+    if family == "gemma3":
+        cfg = cfg.replace(family="gemma3", qk_norm=True, hidden_act="gelu_tanh", sandwich_norm=True,
+                          norm_offset=True, embed_scale=1024 ** 0.5, attn_scale=128 ** -0.5, sliding_window=96,
+                          layer_windows=(96, 0, 96), rope_local_theta=1e4, rms_norm_eps=1e-6)
     m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, ops, max_pos=2048)
     m.allocate_random_quant(scheme, seed=3)
     m.X16 = x16
