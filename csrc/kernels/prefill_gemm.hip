@@ -625,6 +625,7 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
     case PG_EPI_STORE: pgemm_kernel<PG_EPI_STORE><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
     case PG_EPI_ADD: pgemm_kernel<PG_EPI_ADD><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
     case PG_EPI_GLU: pgemm_kernel<PG_EPI_GLU><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+    case PG_EPI_GEGLU: pgemm_kernel<PG_EPI_GEGLU><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
     default: return false;
   }
 }
