@@ -436,7 +436,7 @@ __global__ __launch_bounds__(PG_T) void pgemm_f8_kernel(const unsigned char* __r
   // VGPRs and spills); B1 behind phase 0's first 4 MFMAs, A1 behind phase 1's. LDS-DMA
   // of tile kt + 2: A0 / B0 halves at phase 1 (after the barrier that closes phase 0's
   // reads), A1 / B1 halves at phase 2. Waits as pgemm2: end of phase 3 -> all of tile
-  // kt + 1 landed (vmcnt 8). Barriers after every phase.
+  // kt + 1 landed (vmcnt 8). Barriers after phases 0, 1 and 3.
   i32x8 bfr[4], afr[2][4];
   auto rd = [&](const unsigned char* p) {
     const u32x4 lo = *reinterpret_cast<const u32x4*>(p + chs[0]), hi = *reinterpret_cast<const u32x4*>(p + chs[1]);
@@ -504,16 +504,14 @@ __global__ __launch_bounds__(PG_T) void pgemm_f8_kernel(const unsigned char* __r
               bfr[2 * qn + jj], afr[qm][ii], acc[2 * qn + jj][4 * qm + ii], 0, 0, 0, 127, 0, 127);
         __builtin_amdgcn_s_setprio(0);
       }
-      if (p == 2) {
-        if (more2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else if (more1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      if (p == 3) {
+      if (p == 3) {  // all of tile kt + 1 landed (its two halves are the oldest 8 in flight)
         if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      barrier();
+      // barriers: after phase 0 (tile kt's A0 / B0 reads done before the kt + 2 DMA into
+      // them at phase 1), after phase 1 (A1 / B1 reads done before phase 2's DMA), after
+      // phase 3 (tile kt + 1 landed for every wave); phase 2 reads nothing, needs none
+      if (p != 2) barrier();
     }
   }
   // dequantise: acc * xs[m] * rs[n] / 256 (rs carries the decode path's x 256)
