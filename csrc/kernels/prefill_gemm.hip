@@ -350,6 +350,184 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
   pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
 }
 
+// ---- v5: hipBLASLt's wave shape. 256 threads = 4 waves as 2 (m) x 2 (n), each a
+// 128 x 128 output block: 64 accumulators = all 256 AGPRs, one wave per SIMD, half the
+// LDS fragment traffic per MFMA of v2's 128 x 64 blocks (r3_pgemm_pmc.md). K tile 32
+// in four LDS stages of 32 KiB (A then B, 256 rows x 64 B), LDS-DMA issued three tiles
+// ahead, fragments of the next tile read behind the current tile's 64 MFMAs, one
+// barrier per tile. The MFMAs are inline asm on AGPR accumulators ("+a"): with the
+// builtin, hipcc shuttled the 256 accumulators between AGPRs and VGPRs inside the
+// loop. 64-byte rows: 16-B chunk c of row r sits at chunk c ^ ((r >> 2) & 3), so the
+// 16 rows of a ds_read_b128 lane group cover all 16 slots of a bank row.
+constexpr int P5_T = 256, P5_BK = 32, P5_STAGE = 2 * 256 * 64;
+
+HS_DEVICE void p5_mfma(f32x4& acc, const u32x4& b, const u32x4& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+// lane holds C[m][n .. n+3], m = m0 + 128 wr + 16 i + fr, n = n0 + 128 wc + 16 j + 4 fq (acc[j][i])
+template <int EPI>
+HS_DEVICE void p5_epilogue(f32x4 (&acc)[8][8], unsigned char* lds, unsigned short* __restrict__ C, long ldc, int M,
+                           int m0, int n0, int tn, int wr, int wc, int fr, int fq, int lane) {
+  if constexpr (EPI == PG_EPI_STORE || EPI == PG_EPI_ADD) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wr * 128 + i * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n0 + wc * 128 + j * 16 + 4 * fq);
+        uint2 v;
+        if constexpr (EPI == PG_EPI_ADD) {
+          const uint2 r = *dst;
+          const unsigned short rr[4] = {(unsigned short)(r.x & 0xffff), (unsigned short)(r.x >> 16),
+                                        (unsigned short)(r.y & 0xffff), (unsigned short)(r.y >> 16)};
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = bf16_to_f32(f32_to_bf16(acc[j][i][e])) + bf16_to_f32(rr[e]);
+          v.x = pack_bf16x2(o[0], o[1]);
+          v.y = pack_bf16x2(o[2], o[3]);
+        } else {
+          v.x = pack_bf16x2(acc[j][i][0], acc[j][i][1]);
+          v.y = pack_bf16x2(acc[j][i][2], acc[j][i][3]);
+        }
+        *dst = v;
+      }
+    }
+  } else if constexpr (EPI == PG_EPI_GLU || EPI == PG_EPI_GEGLU) {
+    // wc = 1 holds the up rows of the gate columns wc = 0 holds: bf16(up) through LDS
+    uint2* ex = reinterpret_cast<uint2*>(lds);  // [2 wr][8 j][8 i][64 lanes] = 64 KiB
+    if (wc == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          ex[((wr * 8 + j) * 8 + i) * 64 + lane] = uint2{pack_bf16x2(acc[j][i][0], acc[j][i][1]),
+                                                         pack_bf16x2(acc[j][i][2], acc[j][i][3])};
+    }
+    __syncthreads();
+    if (wc == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wr * 128 + i * 16 + fr;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint2 u = ex[((wr * 8 + j) * 8 + i) * 64 + lane];
+          const unsigned short uu[4] = {(unsigned short)(u.x & 0xffff), (unsigned short)(u.x >> 16),
+                                        (unsigned short)(u.y & 0xffff), (unsigned short)(u.y >> 16)};
+          unsigned short o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = EPI == PG_EPI_GEGLU ? gelu_mul1(f32_to_bf16(acc[j][i][e]), uu[e])
+                                       : silu_mul1(f32_to_bf16(acc[j][i][e]), uu[e]);
+          *reinterpret_cast<uint2*>(C + (long)m * ldc + tn * 128 + j * 16 + 4 * fq) =
+              uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+        }
+      }
+    }
+  }
+}
+
+template <int EPI, bool kGroup>
+__global__ __launch_bounds__(P5_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgemm5_kernel(
+    const unsigned short* __restrict__ A, long lda, const unsigned short* __restrict__ B, long ldb,
+    unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n, PgEpi E) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[4 * P5_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
+  const int m0 = tm * PG_BM, n0 = tn * PG_BN;
+  if constexpr (kGroup) {
+    const int e = E.tile_expert[tm];
+    if (e < 0) return;
+    B += (long)e * E.b_estride;
+  }
+  const int nk = K / P5_BK;
+
+  // staging: wave w moves rows [64 w, 64 w + 64) of A (instructions 0..3) and of B
+  // (4..7), 16 rows of 64 B per instruction; the K step rides in soffset
+  unsigned int voff[8];
+  int dst[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int op = t >> 2, r0 = wave * 64 + (t & 3) * 16, r = r0 + (lane >> 2);
+    const int c = (lane & 3) ^ ((lane >> 4) & 3);
+    const long row = op == 0 ? (long)min(m0 + r, M - 1) : (long)pg_brow<EPI>(n0, tn, r, N);
+    voff[t] = (unsigned)(row * (op == 0 ? lda : ldb) * 2 + c * 16);
+    dst[t] = op * (P5_STAGE / 2) + r0 * 64;
+  }
+  const __amdgpu_buffer_rsrc_t rsrc[2] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)min((long)M * lda * 2, 0x7fffffffL), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)min((long)N * ldb * 2, 0x7fffffffL), 0x00020000)};
+  // the K step rides in soffset, clamped to the last tile: the loop below runs the same
+  // code for every tile and stages / reads three tiles past the end, which it never uses
+  auto issue = [&](int t, int kt) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc[t >> 2], (lds_ptr_t)(lds + (kt & 3) * P5_STAGE + dst[t]), 16,
+                                             voff[t], min(kt, nk - 1) * P5_BK * 2, 0, 0);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ch = (fq ^ ((fr >> 2) & 3)) * 16;
+  const int a_off = (wr * 128 + fr) * 64 + ch, b_off = P5_STAGE / 2 + (wc * 128 + fr) * 64 + ch;
+  auto frag_off = [&](int q) { return q < 8 ? a_off + q * 1024 : b_off + (q - 8) * 1024; };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 f[2][16];  // [buffer][A frags 0..7, B frags 8..15]
+
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // one K tile on buffer CUR: 64 MFMAs; the DMA of tile kt + 4 (into this tile's
+  // stage, whose fragments are already in registers) behind the first 8, the 16
+  // fragment reads of tile kt + 1 behind every third of the rest; then wait for this
+  // wave's DMA of tile kt + 2 (two tiles issued after it) and barrier, after which tile
+  // kt + 2 is in LDS for every wave and nobody reads tile kt + 1's stage any more
+  auto tile = [&](auto cur_c, int kt) {
+    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+    const unsigned char* nb = lds + ((kt + 1) & 3) * P5_STAGE;
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      p5_mfma(acc[t >> 3][t & 7], f[cur][8 + (t >> 3)], f[cur][t & 7]);
+      if (t < 8) {
+        issue(t, kt + 4);
+      } else if ((t - 8) % 3 == 0 && (t - 8) / 3 < 16) {
+        const int q = (t - 8) / 3;
+        f[nxt][q] = *reinterpret_cast<const u32x4*>(nb + frag_off(q));
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    barrier();
+  };
+
+  // prologue: tiles 0..3 in flight; tile 0 read into buffer 0; tile 1 landed
+  for (int k = 0; k < 4; ++k)  // in tile order: the vmcnt waits count whole tiles
+#pragma unroll
+    for (int t = 0; t < 8; ++t) issue(t, k);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  barrier();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) f[0][q] = *reinterpret_cast<const u32x4*>(lds + frag_off(q));
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  barrier();
+  for (int kt = 0; kt < nk; kt += 2) {  // nk is even (K % 64 == 0)
+    tile(std::integral_constant<int, 0>(), kt);
+    tile(std::integral_constant<int, 1>(), kt + 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end tiles, before LDS is reused
+  barrier();
+  // the MFMA results are read by VALU next: asm MFMAs are invisible to the hazard
+  // recognizer, so cover the longest MFMA -> VALU read dependency by hand
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  p5_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
+}
+
 // ---- FP8 W8A8 (the FP8-Dynamic checkpoints: per-channel e4m3 weights, per-token
 // dynamic e4m3 activations) on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block
 // scales (E8M0 127): twice the bf16 MFMA rate per clock (MI355X_MICROARCH.md, matrix
@@ -607,6 +785,15 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
     switch (epi) {
       case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, true><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, true><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      default: return false;
+    }
+  }
+  if (E.variant == 5) {
+    switch (epi) {
+      case PG_EPI_STORE: pgemm5_kernel<PG_EPI_STORE, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_ADD: pgemm5_kernel<PG_EPI_ADD, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_GLU: pgemm5_kernel<PG_EPI_GLU, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+      case PG_EPI_GEGLU: pgemm5_kernel<PG_EPI_GEGLU, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
       default: return false;
     }
   }

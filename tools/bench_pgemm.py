@@ -63,8 +63,9 @@ def main():
         t_blas = time_fn(lambda: [F.linear(x, w) for w in ws])
         t_v1 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 1) for w in ws])
         t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 2) for w in ws])
+        t_v5 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 5) for w in ws])
         r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
-             "pgemm_v1_ms": round(t_v1, 4),
+             "pgemm_v1_ms": round(t_v1, 4), "pgemm_v5_ms": round(t_v5, 4),
              "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1)}
         if a.fp8:
             from hipserve.ops import pgemm, quant as Q

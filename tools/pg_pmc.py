@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Minimal driver for PMC passes on one prefill-GEMM shape: 3 hipBLASLt calls then 3
-hand-written prefill_gemm calls (variant 2) on the same operands, so one rocprofv3
+hand-written prefill_gemm calls per variant in $PG_VARIANTS (default 2) on the same operands, so one rocprofv3
 --pmc pass gives per-dispatch counters of both kernels side by side.
 usage: python tools/pg_pmc.py [M N K]"""
 import os
@@ -20,7 +20,7 @@ out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(3):
     F.linear(x, w)
 torch.cuda.synchronize()
-for v in (2,):
+for v in (int(t) for t in os.environ.get("PG_VARIANTS", "2").split()):
     for _ in range(3):
         torch.ops.hipserve.prefill_gemm(out, x, w, 0, v)
     torch.cuda.synchronize()
