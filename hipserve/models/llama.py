@@ -150,11 +150,11 @@ class LlamaModel:
                             or any(cfg.layer_windows) or cfg.embed_scale != 1.0)
         # families the fused decode layer covers: Llama-style plus q/k/v bias (Qwen2),
         # per-head q/k RMSNorm (Qwen3; folded into the split-K RoPE epilogue), MoE MLPs
-        # (Mixtral, Qwen3-MoE / Qwen3-VL-MoE) and, at TP = 1, Gemma-3 (sandwich norms
-        # in splitk_post_add_rmsnorm, GeGLU over the gate|up partials, sliding-window
+        # (Mixtral, Qwen3-MoE / Qwen3-VL-MoE) and Gemma-3 (sandwich norms in
+        # splitk_post_add_rmsnorm at TP = 1, reduce + all-reduce + norms at TP > 1;
+        # GeGLU over the gate|up partials, sliding-window
         # layers with their local RoPE table, embedding scale)
         self.fused_family = (cfg.hidden_act in ("silu", "gelu_tanh")
-                             and (not cfg.sandwich_norm or tp.world_size == 1)
                              and (not cfg.qk_norm or (cfg.rope_mode == 0 and self.D in (64, 128, 256))))
         self.decode_partition = 512
         self.block_size_hint = 16  # KV block size (set by the runner)
@@ -480,20 +480,28 @@ class LlamaModel:
         return out
 
     def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next, out16=None):
-        """Sandwich-norm epilogue (Gemma-3, TP = 1): residual += RMSNorm(x @ w.T) *
-        w_post; out = RMSNorm(residual) * w_next — one kernel over the split-K
-        partials ``pt`` when the decode GEMM wrote them (also writing ``out16``, the
-        f16 pair-order copy for a quantised consumer; returns True), else the unfused
-        chain of ``forward`` (bit-identical either way; returns False: no out16)."""
+        """Sandwich-norm epilogue (Gemma-3): residual += RMSNorm(sum over the TP ranks
+        of x @ w.T) * w_post; out = RMSNorm(residual) * w_next. At TP = 1 one kernel
+        over the split-K partials ``pt`` when the decode GEMM wrote them (also writing
+        ``out16``, the f16 pair-order copy for a quantised consumer; returns True);
+        otherwise the chain of ``forward`` — partials reduced (bf16, or fp32 under
+        exact TP reduction) or the projection itself, the cross-rank sum, then the two
+        norms (bit-identical to ``forward`` at TP = 1; returns False: no out16)."""
         eps = self.cfg.rms_norm_eps
-        if pt is not None and w_post.dtype == w_next.dtype and residual.dtype == torch.bfloat16:
+        tp1 = self.tp.world_size == 1
+        if tp1 and pt is not None and w_post.dtype == w_next.dtype and residual.dtype == torch.bfloat16:
             torch.ops.hipserve.splitk_post_add_rmsnorm(out, residual, pt[0], pt[1], w_post, w_next, eps, out16)
             return True
-        if pt is not None:
+        if pt is not None and not tp1 and self.tp.exact_reduce:
+            S, (M, N) = pt[1], residual.shape  # fp32: the cross-rank sum rounds once
+            o = pt[0].reshape(-1)[:S * M * N].view(S, M, N).sum(0)
+        elif pt is not None:
             o = torch.empty_like(residual)
             torch.ops.hipserve.splitk_reduce(o, pt[0], pt[1])
         else:
             o = self.linear_rowpar(x, w)
+        if not tp1:
+            o = self._tp_sum(o, residual)
         self.ops.rmsnorm(o, o, w_post, eps)
         self.ops.fused_add_rmsnorm(out, o, residual, w_next, eps)
         return False
@@ -675,7 +683,7 @@ class LlamaModel:
                 ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
                                  nq, nkv, part, self.scale, win)
             pt = self._partial(attn, lw.wo)
-            if lw.post_attn_norm is not None:  # Gemma sandwich norm (TP = 1: fused_family)
+            if lw.post_attn_norm is not None:  # Gemma sandwich norm
                 xn16 = self._x16(xn, lw.wgu) if pt is not None else None
                 if not self.post_add_rmsnorm(xn, residual, pt, attn, lw.wo, lw.post_attn_norm, lw.ln2, xn16):
                     xn16 = None

@@ -49,15 +49,22 @@ def _model_cfg(shape="small"):
         # every rank holds ONE kv head and 8 q heads, as in the 70B TP=8 pod
         return PRESETS["llama-3-70b"].replace(name="llama-3-70b-tp-test", num_layers=2, vocab_size=32000,
                                               max_position_embeddings=1024)
-    return PRESETS["llama-3-8b"].replace(name="llama-3-tp-test", num_layers=3, hidden_size=1024,
-                                         intermediate_size=3584, num_heads=8, num_kv_heads=2,
-                                         vocab_size=32000, max_position_embeddings=1024)
+    small = PRESETS["llama-3-8b"].replace(name="llama-3-tp-test", num_layers=3, hidden_size=1024,
+                                          intermediate_size=3584, num_heads=8, num_kv_heads=2,
+                                          vocab_size=32000, max_position_embeddings=1024)
+    if shape == "gemma":
+        # Gemma-3 features at small shapes: sandwich norms, GeGLU, q/k norm, embedding
+        # scale, sliding-window (96) / global layers with the local RoPE table
+        return small.replace(name="gemma-3-tp-test", family="gemma3", qk_norm=True, hidden_act="gelu_tanh",
+                             sandwich_norm=True, norm_offset=True, embed_scale=1024 ** 0.5, attn_scale=128 ** -0.5,
+                             sliding_window=96, layer_windows=(96, 0, 96), rope_local_theta=1e4, rms_norm_eps=1e-6)
+    return small
 
 
 def _engine_cfg(tp, exact, shape="small"):
     from hipserve.config import EngineConfig
 
-    name = "llama-3-70b-tp-test" if shape == "70b" else "llama-3-tp-test"
+    name = {"70b": "llama-3-70b-tp-test", "gemma": "gemma-3-tp-test"}.get(shape, "llama-3-tp-test")
     return EngineConfig(model=name, load_format="dummy", device="cuda", max_num_seqs=8,
                         max_num_batched_tokens=256, max_model_len=640, num_kv_blocks=512,
                         tensor_parallel_size=tp, extra={"tp_exact_reduce": exact})
@@ -160,11 +167,12 @@ def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK):
     try:
         tp = init_tp(world, backend="gloo", device_type="cuda")
         cfg = _engine_cfg(world, exact, shape)
-        prompts = PROMPTS if shape == "small" else PROMPTS[:2]
+        prompts = PROMPTS[:2] if shape == "70b" else PROMPTS
         if rank == 0:
             eng = LLMEngine(cfg, tp=tp, model_cfg=_model_cfg(shape))
             info = {"graphs": len(eng.runner.graphs), "lookahead": eng.lookahead,
-                    "custom_ar": tp.custom_ar is not None, "shm_ring": tp._ring is not None}
+                    "custom_ar": tp.custom_ar is not None, "shm_ring": tp._ring is not None,
+                    "fused_family": eng.runner.model.fused_family}
             # the TP=1 reference lives in this process too (rank 1 idles in its loop)
             from hipserve.parallel.comm import TPGroup
 
@@ -281,3 +289,21 @@ def test_tp8_70b_shapes_shared_gpu_matches_tp1():
         assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=8 token {t2} not in TP=1's top-5"
         assert lp1 - lp2 <= min(TIE_70B, info["logit"]["bound"]), \
             f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
+
+
+def test_tp2_gemma3_shared_gpu_matches_tp1():
+    """Gemma-3 features (sandwich norms, GeGLU, sliding-window layers, q/k norm,
+    embedding scale) at TP=2 through the fused decode forward (split-K partials ->
+    reduce + in-house all-reduce + post-norm + residual + next norm; GeGLU over the
+    column-parallel gate|up partials) reproduces TP=1 up to near-ties, as the Llama
+    test. Reference: the Gemma-3 deployments run at TP=2
+    (vllm-models/helm-chart/values.yaml:3,5)."""
+    _, info = _run_tp(2, False, shape="gemma")
+    assert info["fused_family"], info
+    assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
+    assert info["car_failed"] is False
+    print("exact prefix per prompt:", info["exact_prefix"], "divergences:", len(info["ties"]))
+    assert len(info["ties"]) <= N_TOK * len(PROMPTS) // 10, info["ties"]
+    for i, j, t1, t2, lp1, lp2 in info["ties"]:
+        assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=2 token {t2} not in TP=1's top-5"
+        assert lp1 - lp2 <= TIE, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
