@@ -215,6 +215,10 @@ struct PgF8 {
 };
 bool launch_prefill_gemm_f8(int epi, void* C, long ldc, const void* A, long lda, const PgF8& W, int M, int N, int K,
                             hipStream_t s);
+// FP8 W8A8 decode GEMM (fp8_decode.hip), M <= 64: fp32 split-K partials
+// ws[S, M, N] = (xq . wq^T over K slice s) * xs[m] * rs[n] / 256; (K / 256) / S in
+// {1, 2, 3, 4, 6, 7, 8, 12, 14, 16, 21}; part rows % 16 == 0. W.xs = xs.
+bool launch_fp8_decode_gemm(float* ws, const void* xq, const PgF8& W, int M, int N, int K, int S, hipStream_t s);
 // per-token dynamic e4m3 quantisation: xs[m] = max|x[m, :]| / 448, q = sat(x / xs)
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s);
 void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);
@@ -223,13 +227,16 @@ void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s)
 // ws: [S, M, N] fp32 partials. h = bf16(sum_s ws); residual = bf16(h + residual);
 // out = rmsnorm(residual) * w  (bit-identical to splitk_reduce + fused_add_rmsnorm)
 // out16 (optional): out also as f16 in the quantised GEMM's staging pair order (gguf_mfma.hip kX16)
+// out8 / xs8 (optional): out also as per-token e4m3 + row scale for the W8A8 decode GEMM
+// (fp8_decode.hip), bit-identical to act_quant_fp8 of out
 void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
-                               int M, int N, float eps, hipStream_t s, void* out16 = nullptr);
+                               int M, int N, float eps, hipStream_t s, void* out16 = nullptr, void* out8 = nullptr,
+                               float* xs8 = nullptr);
 // sandwich norm (Gemma-3): residual = bf16(RMSNorm(bf16(sum_s ws)) * w_post + residual);
 // out = RMSNorm(residual) * w_next (both weights bf16, or both fp32)
 void launch_splitk_post_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w_post,
                                     const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s,
-                                    void* out16 = nullptr);
+                                    void* out16 = nullptr, void* out8 = nullptr, float* xs8 = nullptr);
 // qkv = bf16(sum_s ws) -> RoPE(q, k) -> q into qkv[:, :nq*D], k/v into the paged cache
 // out[M, N] (bf16, row stride out_stride) = sum of the fp32 partials ws[S, M, N] (decode_gemm.hip)
 void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, int N, int S, hipStream_t s);

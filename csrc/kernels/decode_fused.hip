@@ -37,6 +37,41 @@ HS_DEVICE u16x8 f16_pairs8(const u16x8 v) {
   return h;
 }
 
+// per-token dynamic e4m3 copy of a bf16 row for the W8A8 decode GEMM (fp8_decode.hip),
+// bit-identical to act_quant_fp8 (prefill_gemm.hip) on the same bf16 values: xs = amax /
+// 448 (1 for a zero row), q = sat(x * (448 / amax)) with the same conversions
+HS_DEVICE uint2 e4m3_8(const u16x8 o, float inv) {
+  float f[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = __builtin_amdgcn_fmed3f(bf16_to_f32(o[e]) * inv, -448.f, 448.f);
+  uint2 r;
+  r.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  r.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], (int)r.x, true);
+  r.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+  r.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], (int)r.y, true);
+  return r;
+}
+
+template <int VPT, int NT>
+HS_DEVICE void row_e4m3(const u16x8 (&ov)[VPT], int nvec, int row, int N, unsigned char* __restrict__ out8,
+                        float* __restrict__ xs8, float* scratch) {
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+    if (threadIdx.x + i * NT < nvec)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(bf16_to_f32(ov[i][j])));
+  __syncthreads();  // scratch was the norm's reduction buffer
+  amax = block_max(amax, scratch);
+  const float inv = amax > 0.f ? 448.f / amax : 1.f;
+  if (threadIdx.x == 0) xs8[row] = amax > 0.f ? amax / 448.f : 1.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) *reinterpret_cast<uint2*>(out8 + (long)row * N + idx * 8) = e4m3_8(ov[i], inv);
+  }
+}
+
 HS_DEVICE void sum8_bf16(float (&o)[8], const float* __restrict__ p, long slice, int S) {
   f32x4 lo, hi;
   sum_slices8(lo, hi, p, slice, S);
@@ -52,7 +87,9 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
                                                                  unsigned short* __restrict__ residual,
                                                                  const float* __restrict__ ws, int S,
                                                                  const void* __restrict__ weight, int M, int N,
-                                                                 float eps, unsigned short* __restrict__ out16) {
+                                                                 float eps, unsigned short* __restrict__ out16,
+                                                                 unsigned char* __restrict__ out8,
+                                                                 float* __restrict__ xs8) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = N >> 3;
@@ -97,6 +134,7 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
   ss = block_sum(ss, scratch);
   const float inv = rsqrtf(ss / N + eps);
   u16x8* orow = reinterpret_cast<u16x8*>(out + (long)row * N);
+  u16x8 ov[VPT];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * NT;
@@ -110,33 +148,36 @@ __global__ __launch_bounds__(NT) void splitk_add_rmsnorm_kernel(unsigned short* 
         o[j] = f32_to_bf16(v[i][j] * inv * wj);
       }
       orow[idx] = o;
+      ov[i] = o;
       if (out16 != nullptr) reinterpret_cast<u16x8*>(out16 + (long)row * N)[idx] = f16_pairs8(o);
     }
   }
+  if (out8 != nullptr) row_e4m3<VPT, NT>(ov, nvec, row, N, out8, xs8, scratch);
 }
 
 template <bool kWF32>
 static void add_rmsnorm_t(void* out, void* residual, const float* ws, int S, const void* w, int M, int N, float eps,
-                          hipStream_t s, unsigned short* o16) {
+                          hipStream_t s, unsigned short* o16, unsigned char* o8, float* x8) {
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
   const int nvec = N / 8;
   if (norm_threads(N) == 256) {
-    if (nvec <= 256) splitk_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
-    else splitk_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
+    if (nvec <= 256) splitk_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps, o16, o8, x8);
+    else splitk_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, w, M, N, eps, o16, o8, x8);
   } else {
-    if (nvec <= 512) splitk_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
-    else if (nvec <= 1024) splitk_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
-    else splitk_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16);
+    if (nvec <= 512) splitk_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16, o8, x8);
+    else if (nvec <= 1024) splitk_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16, o8, x8);
+    else splitk_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, w, M, N, eps, o16, o8, x8);
   }
 }
 
 void launch_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w, bool weight_f32,
-                               int M, int N, float eps, hipStream_t s, void* out16) {
+                               int M, int N, float eps, hipStream_t s, void* out16, void* out8, float* xs8) {
   if (M <= 0) return;
   auto* o16 = static_cast<unsigned short*>(out16);
-  if (weight_f32) add_rmsnorm_t<true>(out, residual, ws, S, w, M, N, eps, s, o16);
-  else add_rmsnorm_t<false>(out, residual, ws, S, w, M, N, eps, s, o16);
+  auto* o8 = static_cast<unsigned char*>(out8);
+  if (weight_f32) add_rmsnorm_t<true>(out, residual, ws, S, w, M, N, eps, s, o16, o8, xs8);
+  else add_rmsnorm_t<false>(out, residual, ws, S, w, M, N, eps, s, o16, o8, xs8);
 }
 
 // Sandwich-norm epilogue (Gemma-3: post-attention / post-feedforward RMSNorm on the
@@ -168,7 +209,9 @@ __global__ __launch_bounds__(NT) void splitk_post_add_rmsnorm_kernel(unsigned sh
                                                                       const float* __restrict__ ws, int S,
                                                                       const void* __restrict__ w_post,
                                                                       const void* __restrict__ w_next, int M, int N,
-                                                                      float eps, unsigned short* __restrict__ out16) {
+                                                                      float eps, unsigned short* __restrict__ out16,
+                                                                      unsigned char* __restrict__ out8,
+                                                                      float* __restrict__ xs8) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = N >> 3;
@@ -214,6 +257,7 @@ __global__ __launch_bounds__(NT) void splitk_post_add_rmsnorm_kernel(unsigned sh
   ss2 = block_sum(ss2, scratch);
   const float inv2 = rsqrtf(ss2 / N + eps);
   u16x8* orow = reinterpret_cast<u16x8*>(out + (long)row * N);
+  u16x8 ov[VPT];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * NT;
@@ -224,34 +268,38 @@ __global__ __launch_bounds__(NT) void splitk_post_add_rmsnorm_kernel(unsigned sh
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv2 * w[j]);
       orow[idx] = o;
+      ov[i] = o;
       if (out16 != nullptr) reinterpret_cast<u16x8*>(out16 + (long)row * N)[idx] = f16_pairs8(o);
     }
   }
+  if (out8 != nullptr) row_e4m3<VPT, NT>(ov, nvec, row, N, out8, xs8, scratch);
 }
 
 template <bool kWF32>
 static void post_add_rmsnorm_t(void* out, void* residual, const float* ws, int S, const void* wp, const void* wn,
-                               int M, int N, float eps, hipStream_t s, unsigned short* o16) {
+                               int M, int N, float eps, hipStream_t s, unsigned short* o16, unsigned char* o8,
+                               float* x8) {
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
   const int nvec = N / 8;
   if (norm_threads(N) == 256) {
-    if (nvec <= 256) splitk_post_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
-    else splitk_post_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
+    if (nvec <= 256) splitk_post_add_rmsnorm_kernel<256, 1, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16, o8, x8);
+    else splitk_post_add_rmsnorm_kernel<256, 2, kWF32><<<M, 256, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16, o8, x8);
   } else {
-    if (nvec <= 512) splitk_post_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
-    else if (nvec <= 1024) splitk_post_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
-    else splitk_post_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16);
+    if (nvec <= 512) splitk_post_add_rmsnorm_kernel<512, 1, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16, o8, x8);
+    else if (nvec <= 1024) splitk_post_add_rmsnorm_kernel<512, 2, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16, o8, x8);
+    else splitk_post_add_rmsnorm_kernel<512, 4, kWF32><<<M, 512, 0, s>>>(o, r, ws, S, wp, wn, M, N, eps, o16, o8, x8);
   }
 }
 
 void launch_splitk_post_add_rmsnorm(void* out, void* residual, const float* ws, int S, const void* w_post,
                                     const void* w_next, bool weight_f32, int M, int N, float eps, hipStream_t s,
-                                    void* out16) {
+                                    void* out16, void* out8, float* xs8) {
   if (M <= 0) return;
   auto* o16 = static_cast<unsigned short*>(out16);
-  if (weight_f32) post_add_rmsnorm_t<true>(out, residual, ws, S, w_post, w_next, M, N, eps, s, o16);
-  else post_add_rmsnorm_t<false>(out, residual, ws, S, w_post, w_next, M, N, eps, s, o16);
+  auto* o8 = static_cast<unsigned char*>(out8);
+  if (weight_f32) post_add_rmsnorm_t<true>(out, residual, ws, S, w_post, w_next, M, N, eps, s, o16, o8, xs8);
+  else post_add_rmsnorm_t<false>(out, residual, ws, S, w_post, w_next, M, N, eps, s, o16, o8, xs8);
 }
 
 // The rope_cache kernel (rope_cache.hip) reading its input from the split-K

@@ -712,6 +712,36 @@ void prefill_gemm_f8(at::Tensor& out, const at::Tensor& xq, const at::Tensor& xs
               "prefill_gemm_f8: unsupported part shapes (rows % 256; GLU: two equal parts, rows % 128)");
 }
 
+// FP8 W8A8 decode form (fp8_decode.hip): fp32 split-K partials ws [S, M, N] of the
+// per-token e4m3 activations xq / xs against the tiled FP8 parts, for the fused decode
+// epilogues or splitk_reduce.
+void fp8_decode_gemm(at::Tensor& ws, const at::Tensor& xq, const at::Tensor& xs, const std::vector<at::Tensor>& q,
+                     const std::vector<at::Tensor>& rs, int64_t splits) {
+  CHECK_DEV(xq); CHECK_CONTIG(xq); CHECK_CONTIG(xs); CHECK_CONTIG(ws);
+  TORCH_CHECK(xq.scalar_type() == at::kByte && xs.scalar_type() == at::kFloat && ws.scalar_type() == at::kFloat,
+              "fp8_decode_gemm: xq uint8, xs / ws fp32");
+  const int M = xq.size(0), K = xq.size(1);
+  TORCH_CHECK(xs.numel() == M && K % 256 == 0, "fp8_decode_gemm: shapes");
+  TORCH_CHECK(!q.empty() && q.size() <= (size_t)hipserve::kPgF8Parts && rs.size() == q.size(), "fp8_decode_gemm: parts");
+  hipserve::PgF8 W{};
+  W.n = (int)q.size();
+  W.xs = xs.data_ptr<float>();
+  int rows = 0;
+  for (size_t i = 0; i < q.size(); ++i) {
+    CHECK_CONTIG(q[i]); CHECK_CONTIG(rs[i]);
+    const int n = rs[i].numel();
+    TORCH_CHECK(q[i].scalar_type() == at::kByte && rs[i].scalar_type() == at::kFloat && q[i].numel() == (long)n * K,
+                "fp8_decode_gemm: part ", i, " must be tiled FP8 [N/16, K/256, 4096] with rs [N]");
+    W.p[i] = hipserve::PgF8Part{q[i].data_ptr<uint8_t>(), rs[i].data_ptr<float>(), n, 0};
+    rows += n;
+  }
+  TORCH_CHECK(ws.numel() >= splits * (long)M * rows, "fp8_decode_gemm: ws too small");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(xq.device());
+  TORCH_CHECK(hipserve::launch_fp8_decode_gemm(ws.data_ptr<float>(), xq.data_ptr(), W, M, rows, K, (int)splits,
+                                               cur_stream()),
+              "fp8_decode_gemm: unsupported (M <= 64, part rows % 16, (K / 256) / splits in the kernel's step set)");
+}
+
 void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_CONTIG(xq); CHECK_CONTIG(xs);
   const int M = x.size(0), K = x.size(1);
@@ -838,8 +868,24 @@ void decode_gemm_fused(int64_t fix, const at::Tensor& x, const at::Tensor& wp, i
               "decode_gemm_fused: launch");
 }
 
+// optional per-token e4m3 copy (out8 uint8 like out, xs8 fp32 [M]) of a norm epilogue's output
+static void e4m3_out_args(const c10::optional<at::Tensor>& out8, const c10::optional<at::Tensor>& xs8,
+                          const at::Tensor& out, void** o8, float** x8, const char* who) {
+  *o8 = nullptr;
+  *x8 = nullptr;
+  if (out8.has_value() && out8->defined()) {
+    TORCH_CHECK(xs8.has_value() && xs8->defined(), who, ": out8 needs xs8");
+    TORCH_CHECK(out8->scalar_type() == at::kByte && out8->sizes() == out.sizes() && out8->is_contiguous() &&
+                    xs8->scalar_type() == at::kFloat && xs8->numel() == out.size(0) && xs8->is_contiguous(),
+                who, ": out8 uint8 like out, xs8 fp32 [M]");
+    *o8 = out8->data_ptr();
+    *x8 = xs8->data_ptr<float>();
+  }
+}
+
 void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
-                        const at::Tensor& weight, double eps, const c10::optional<at::Tensor>& out16) {
+                        const at::Tensor& weight, double eps, const c10::optional<at::Tensor>& out16,
+                        const c10::optional<at::Tensor>& out8, const c10::optional<at::Tensor>& xs8) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous());
   const int M = residual.size(0), N = residual.size(1);
@@ -853,14 +899,18 @@ void splitk_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor&
                 "splitk_add_rmsnorm: out16 f16 like out");
     o16 = out16->data_ptr();
   }
+  void* o8;
+  float* x8;
+  e4m3_out_args(out8, xs8, out, &o8, &x8, "splitk_add_rmsnorm");
   hipserve::launch_splitk_add_rmsnorm(out.data_ptr(), residual.data_ptr(), ws.data_ptr<float>(), splits,
                                       weight.data_ptr(), weight.scalar_type() == at::kFloat, M, N, (float)eps,
-                                      cur_stream(), o16);
+                                      cur_stream(), o16, o8, x8);
 }
 
 void splitk_post_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& ws, int64_t splits,
                              const at::Tensor& w_post, const at::Tensor& w_next, double eps,
-                             const c10::optional<at::Tensor>& out16) {
+                             const c10::optional<at::Tensor>& out16, const c10::optional<at::Tensor>& out8,
+                             const c10::optional<at::Tensor>& xs8) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous());
   const int M = residual.size(0), N = residual.size(1);
@@ -875,10 +925,13 @@ void splitk_post_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Te
                 "splitk_post_add_rmsnorm: out16 f16 like out");
     o16 = out16->data_ptr();
   }
+  void* o8;
+  float* x8;
+  e4m3_out_args(out8, xs8, out, &o8, &x8, "splitk_post_add_rmsnorm");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
   hipserve::launch_splitk_post_add_rmsnorm(out.data_ptr(), residual.data_ptr(), ws.data_ptr<float>(), splits,
                                            w_post.data_ptr(), w_next.data_ptr(), w_post.scalar_type() == at::kFloat,
-                                           M, N, (float)eps, cur_stream(), o16);
+                                           M, N, (float)eps, cur_stream(), o16, o8, x8);
 }
 
 void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
@@ -1157,14 +1210,15 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
+  m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
   m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
   m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi, int variant=2) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
         "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
         "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
         "int head_dim, int block_size, int mode, Tensor? bias, Tensor? q_w, Tensor? k_w) -> ()");
-  m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None) -> ()");
-  m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None) -> ()");
+  m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
+  m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
   m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
@@ -1210,6 +1264,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);
   m.impl("splitk_post_add_rmsnorm", &splitk_post_add_rmsnorm);
   m.impl("act_quant_fp8", &act_quant_fp8);
+  m.impl("fp8_decode_gemm", &fp8_decode_gemm);
   m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -462,7 +462,7 @@ class LlamaModel:
         src, tok = meta.id_src
         return torch.where(src >= 0, tok.index_select(0, src.clamp(min=0)), ids)
 
-    def add_rmsnorm(self, out, residual, x, splits, w, out16=None):
+    def add_rmsnorm(self, out, residual, x, splits, w, out16=None, out8=None):
         """residual += x summed over the TP ranks; out = RMSNorm(residual) * w.
         ``x`` is this rank's partial output of a row-parallel projection: fp32
         split-K partials [S, M, N] of a decode GEMM, or the plain projection output
@@ -470,16 +470,17 @@ class LlamaModel:
         kernels; TP>1 the in-house cross-rank epilogue (parallel/comm.py)."""
         eps = self.cfg.rms_norm_eps
         if self.tp.world_size > 1:
-            assert out16 is None, "out16 needs TP = 1"
+            assert out16 is None and out8 is None, "out16 / out8 need TP = 1"
             return self.tp.add_rmsnorm(out, residual, x, splits, w, eps, ops=self.ops)
         if x.dtype == torch.float32 and residual.dtype != torch.float32:
-            torch.ops.hipserve.splitk_add_rmsnorm(out, residual, x, splits, w, eps, out16)
+            q8, s8 = out8 if out8 is not None else (None, None)
+            torch.ops.hipserve.splitk_add_rmsnorm(out, residual, x, splits, w, eps, out16, q8, s8)
         else:
-            assert out16 is None, "out16 needs the split-K partial path"
+            assert out16 is None and out8 is None, "out16 / out8 need the split-K partial path"
             self.ops.fused_add_rmsnorm(out, x, residual, w, eps)
         return out
 
-    def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next, out16=None):
+    def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next, out16=None, out8=None):
         """Sandwich-norm epilogue (Gemma-3): residual += RMSNorm(sum over the TP ranks
         of x @ w.T) * w_post; out = RMSNorm(residual) * w_next. At TP = 1 one kernel
         over the split-K partials ``pt`` when the decode GEMM wrote them (also writing
@@ -490,7 +491,8 @@ class LlamaModel:
         eps = self.cfg.rms_norm_eps
         tp1 = self.tp.world_size == 1
         if tp1 and pt is not None and w_post.dtype == w_next.dtype and residual.dtype == torch.bfloat16:
-            torch.ops.hipserve.splitk_post_add_rmsnorm(out, residual, pt[0], pt[1], w_post, w_next, eps, out16)
+            q8, s8 = out8 if out8 is not None else (None, None)
+            torch.ops.hipserve.splitk_post_add_rmsnorm(out, residual, pt[0], pt[1], w_post, w_next, eps, out16, q8, s8)
             return True
         if pt is not None and not tp1 and self.tp.exact_reduce:
             S, (M, N) = pt[1], residual.shape  # fp32: the cross-rank sum rounds once
@@ -656,11 +658,12 @@ class LlamaModel:
         lw0 = self.layers[0]
         extras = lw0.bqkv is not None or lw0.q_norm is not None
         xn16 = None  # f16 pair-order copy of xn from its producer (quantised GEMM input)
+        xn8 = None   # (e4m3 xn, row scales) from its producer (W8A8 FP8 decode GEMM input)
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
             win = cfg.window_of(i)
             cs = self.cos_sin_local if win else self.cos_sin
-            pt = self._partial(xn, lw.wqkv, xn16)
+            pt = self._partial(xn, lw.wqkv, xn16, xn8)
             if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras and not win:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
@@ -685,13 +688,15 @@ class LlamaModel:
             pt = self._partial(attn, lw.wo)
             if lw.post_attn_norm is not None:  # Gemma sandwich norm
                 xn16 = self._x16(xn, lw.wgu) if pt is not None else None
-                if not self.post_add_rmsnorm(xn, residual, pt, attn, lw.wo, lw.post_attn_norm, lw.ln2, xn16):
-                    xn16 = None
+                xn8 = self._x8(xn, lw.wgu) if pt is not None else None
+                if not self.post_add_rmsnorm(xn, residual, pt, attn, lw.wo, lw.post_attn_norm, lw.ln2, xn16, xn8):
+                    xn16 = xn8 = None
             elif pt is not None:
                 xn16 = self._x16(xn, lw.wgu) if lw.router is None else None
-                self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2, xn16)
+                xn8 = self._x8(xn, lw.wgu) if lw.router is None else None
+                self.add_rmsnorm(xn, residual, pt[0], pt[1], lw.ln2, xn16, xn8)
             else:
-                xn16 = None
+                xn16 = xn8 = None
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(attn, lw.wo), 1, lw.ln2)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             if lw.router is not None:  # MoE MLP: routed expert GEMMs, then residual + next norm
@@ -700,7 +705,7 @@ class LlamaModel:
             gelu = cfg.hidden_act == "gelu_tanh"
             gc = None if gelu else gemm.glu_choice(T, lw.wgu)
             pt = (None if gc is not None or (isinstance(lw.wgu, torch.Tensor) and not gelu)
-                  else self._partial(xn, lw.wgu, xn16))
+                  else self._partial(xn, lw.wgu, xn16, xn8))
             act16 = None
             if gc is not None:     # SiLU-GLU in the gate|up GEMM's epilogue
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
@@ -715,13 +720,15 @@ class LlamaModel:
             pt = self._partial(act, lw.wd, act16)
             if lw.post_ff_norm is not None:
                 xn16 = self._x16(xn, self.layers[i + 1].wqkv) if pt is not None and i + 1 < L else None
-                if not self.post_add_rmsnorm(xn, residual, pt, act, lw.wd, lw.post_ff_norm, nxt, xn16):
-                    xn16 = None
+                xn8 = self._x8(xn, self.layers[i + 1].wqkv) if pt is not None and i + 1 < L else None
+                if not self.post_add_rmsnorm(xn, residual, pt, act, lw.wd, lw.post_ff_norm, nxt, xn16, xn8):
+                    xn16 = xn8 = None
             elif pt is not None:
                 xn16 = self._x16(xn, self.layers[i + 1].wqkv) if i + 1 < L else None
-                self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt, xn16)
+                xn8 = self._x8(xn, self.layers[i + 1].wqkv) if i + 1 < L else None
+                self.add_rmsnorm(xn, residual, pt[0], pt[1], nxt, xn16, xn8)
             else:
-                xn16 = None
+                xn16 = xn8 = None
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(act, lw.wd), 1, nxt)
         return xn
 
@@ -825,7 +832,7 @@ class LlamaModel:
         ws = [self.lm_head] + [getattr(lw, n) for lw in self.layers for n in ("wqkv", "wo", "wgu", "wd")]
         return [w for w in ws if isinstance(w, Q.QuantWeight)]
 
-    def _partial(self, x: torch.Tensor, w, x16: torch.Tensor | None = None):
+    def _partial(self, x: torch.Tensor, w, x16: torch.Tensor | None = None, x8=None):
         """(fp32 split-K partials [S, M, N], S) of ``x @ w.T`` for a fused decode
         epilogue: the tuned bf16 decode GEMM, or the GGUF MFMA GEMM for a
         ``QuantWeight`` (``x16``: the producer's f16 copy of x, see ``_x16``); None
@@ -835,7 +842,7 @@ class LlamaModel:
             return gemm.gemm_partial(x, w, fc) if fc is not None else None
         from ..ops import quant as Q
         if getattr(w, "v2", False) and x.shape[0] <= Q.MAX_FUSED_M and x.is_cuda:
-            return Q.quant_partial(x, w, x16)
+            return Q.quant_partial(x, w, x16, x8)
         return None
 
     X16 = os.environ.get("HIPSERVE_QGEMM_X16", "1") != "0"
@@ -845,10 +852,24 @@ class LlamaModel:
         (splitk_add_rmsnorm / splitk_glu) writes when the consumer is a quantised
         decode GEMM at 33..64 rows (gguf_mfma.hip kX16: no bf16 -> f16 conversion in
         every workgroup); None otherwise."""
+        from ..ops import quant as Q
         if (not self.X16 or self.tp.world_size != 1 or not like.is_cuda or not 32 < like.shape[0] <= 64
-                or not getattr(consumer, "v2", False) or not hasattr(torch.ops.hipserve, "splitk_glu")):
+                or not getattr(consumer, "v2", False) or not hasattr(torch.ops.hipserve, "splitk_glu")
+                or Q.f8_decode_ok(consumer)):  # the W8A8 decode GEMM quantises x itself
             return None
         return torch.empty(like.shape, dtype=torch.float16, device=like.device)
+
+    def _x8(self, like: torch.Tensor, consumer):
+        """(e4m3 [M, K] uint8, row scales fp32 [M]) buffers for the per-token FP8 copy of
+        ``like`` that its producer (splitk_add_rmsnorm / splitk_post_add_rmsnorm) writes
+        when the consumer runs the W8A8 FP8 decode GEMM (bit-identical to quantising
+        ``like`` afterwards; one act_quant_fp8 launch fewer); None otherwise."""
+        from ..ops import quant as Q
+        if (self.tp.world_size != 1 or not like.is_cuda or like.shape[0] > Q.MAX_FUSED_M
+                or not Q.f8_decode_ok(consumer)):
+            return None
+        return (torch.empty(like.shape, dtype=torch.uint8, device=like.device),
+                torch.empty(like.shape[0], dtype=torch.float32, device=like.device))
 
     def _decode_split(self, Td: int, meta: AttnMeta):
         """Context partition size for the decode attention: with >= 512 (sequence,

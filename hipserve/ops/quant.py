@@ -464,6 +464,9 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
     empty = _empty(device, torch.bfloat16)
     for sig, w in seen.items():
         nsb = w.K // 256
+        if f8_decode_ok(w):  # these run the W8A8 FP8 decode GEMM at M <= 64
+            report += _tune_f8_decode(w, ms, ws)
+            continue
         for M in ms:
             x = torch.randn(M, w.K, device=device, dtype=torch.bfloat16)
             cands = sorted({_actual_splits(nsb, s) for s in (1, 2, 4, 8, 16, 32, 64) if s <= nsb})
@@ -481,12 +484,96 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
     return report
 
 
-def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = None):
+# FP8 W8A8 decode (fp8_decode.hip): per-token e4m3 activations x per-channel e4m3
+# weights on the scaled FP8 MFMA, no dequant VALU — the FP8-Dynamic checkpoints'
+# activation scheme, as the prefill GEMM (ops/pgemm.py f8_gemm). HIPSERVE_FP8_DECODE=0
+# keeps the W8A16 v2 kernel (f16 activations).
+F8_DECODE = os.environ.get("HIPSERVE_FP8_DECODE", "1") != "0"
+F8D_STEPS = (1, 2, 3, 4, 6, 7, 8, 12, 14, 16, 21)  # (K / 256) / S the kernel is built for
+F8D_MIN_WGS = 160  # untuned default; measured at 64 rows, 170-250 workgroups of 8 waves stream best
+
+
+def f8_decode_ok(w) -> bool:
+    """The FP8 decode GEMM takes ``w``: per-channel FP8 parts only (no 128-block
+    scales), tiled, at most 4 parts, and a K whose 256-k steps split into a built
+    step count."""
+    parts = getattr(w, "parts", None)
+    if not (F8_DECODE and parts and len(parts) <= 4 and hasattr(torch.ops.hipserve, "fp8_decode_gemm")):
+        return False
+    if not all(p.qtype == FP8 and p.tiled and p.N % 16 == 0 for p in parts) or w.K % 256:
+        return False
+    return f8_decode_splits(w, 64) > 0
+
+
+F8_SPLIT_TABLE: dict = {}  # (weight signature, M bucket) -> S, measured by tune_splits
+
+
+def _f8_valid_splits(w) -> list:
+    tiles, nsb = -(-w.N // 128), w.K // 256
+    return [S for S in range(1, nsb + 1) if nsb % S == 0 and nsb // S in F8D_STEPS and tiles * S <= 1024]
+
+
+def f8_decode_splits(w, M: int) -> int:
+    """K slices: the tuned choice for (weight shape, M bucket) if any, else the smallest
+    S (with (K/256)/S a built step count) giving >= F8D_MIN_WGS workgroups of 128 rows,
+    else the largest one under 1024; 0 if none."""
+    S = F8_SPLIT_TABLE.get((_sig(w), _bucket(M)))
+    if S is not None:
+        return S
+    tiles, nsb = -(-w.N // 128), w.K // 256
+    valid = [S for S in range(1, nsb + 1) if nsb % S == 0 and nsb // S in F8D_STEPS]
+    if not valid:
+        return 0
+    for S in valid:
+        if tiles * S >= F8D_MIN_WGS:
+            return S
+    under = [S for S in valid if tiles * S <= 1024]
+    return max(under) if under else valid[0]
+
+
+def f8_decode_partial(x: torch.Tensor, w: QuantWeight, x8=None):
+    """(fp32 split-K partials [S, M, N], S) of x @ w.T, W8A8 (x quantised per token;
+    ``x8``: its (e4m3, scales) already written by the producer)."""
+    from . import pgemm
+    M = x.shape[0]
+    xq, xs = x8 if x8 is not None else pgemm.act_quant(x)
+    S = f8_decode_splits(w, M)
+    ws = torch.empty(S * M * w.N, dtype=torch.float32, device=x.device)
+    torch.ops.hipserve.fp8_decode_gemm(ws, xq, xs, [p.q for p in w.parts], [p.rs for p in w.parts], S)
+    return ws, S
+
+
+def _tune_f8_decode(w, ms, ws) -> list:
+    """F8_SPLIT_TABLE for one weight shape: each valid S timed in a hipGraph per M
+    bucket, plus the epilogue's re-read of the partials (as tune_splits)."""
+    from . import pgemm
+    rows = []
+    for M in ms:
+        x = torch.randn(M, w.K, device=ws.device, dtype=torch.bfloat16)
+        xq, xs = pgemm.act_quant(x)
+        qs, rs = [p.q for p in w.parts], [p.rs for p in w.parts]
+        cost = {}
+        for S in _f8_valid_splits(w):
+            if S * M * w.N > ws.numel():
+                continue
+            t = _graph_time_us(lambda S=S: torch.ops.hipserve.fp8_decode_gemm(ws, xq, xs, qs, rs, S))
+            cost[S] = t + 1e6 * S * M * w.N * 4 / PARTIAL_READ_BPS
+        if cost:
+            best = min(cost, key=cost.get)
+            F8_SPLIT_TABLE[(_sig(w), _bucket(M))] = best
+            rows.append({"K": w.K, "N": w.N, "M": M, "S": best, "kernel": "fp8_w8a8",
+                         "us": {k: round(v, 2) for k, v in sorted(cost.items())}})
+    return rows
+
+
+def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = None, x8=None):
     """Decode GEMM writing fp32 split-K partials ws[S, M, N] for a fused epilogue
     (splitk_rope_cache / splitk_add_rmsnorm / splitk_glu); returns (ws, S). ``x16``:
     the producer's f16 pair-order copy of x (splitk_add_rmsnorm / splitk_glu
     ``out16``), staged as is instead of converting x in every workgroup."""
     M = x.shape[0]
+    if M <= MAX_FUSED_M and f8_decode_ok(w):
+        return f8_decode_partial(x, w, x8)
     S = v2_splits(w, M)
     ws = torch.empty(S * M * w.N, dtype=torch.float32, device=x.device)
     _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S, x16)
@@ -499,6 +586,10 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
     if M == 0:
         return out
     if M <= MAX_FUSED_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+        if x.is_cuda and f8_decode_ok(w):  # the fused path's partials, reduced: bit-identical to it
+            ws, S = f8_decode_partial(x, w)
+            torch.ops.hipserve.splitk_reduce(out, ws, S)
+            return out
         if w.v2 and x.is_cuda:
             S = v2_splits(w, M)
             if S == 1:

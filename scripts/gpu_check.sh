@@ -111,6 +111,7 @@ for s in $steps; do
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     prof_qwen3moe) prof_run profqm --model qwen3-30b-a3b ;;
     prof_gemma3) prof_run profg3 --model gemma-3-27b ;;
+    prof_g27fp8) prof_run profg3f8 --model gemma-3-27b --quantization fp8 ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done
