@@ -77,6 +77,41 @@ HS_DEVICE float block_max(float v, float* scratch) {
   return r;
 }
 
+// per-token dynamic e4m3 copy of a bf16 row for the W8A8 decode GEMM (fp8_decode.hip) and the FP8 prefill GEMM,
+// bit-identical to act_quant_fp8 (prefill_gemm.hip) on the same bf16 values: xs = amax /
+// 448 (1 for a zero row), q = sat(x * (448 / amax)) with the same conversions
+HS_DEVICE uint2 e4m3_8(const u16x8 o, float inv) {
+  float f[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = __builtin_amdgcn_fmed3f(bf16_to_f32(o[e]) * inv, -448.f, 448.f);
+  uint2 r;
+  r.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  r.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], (int)r.x, true);
+  r.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+  r.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], (int)r.y, true);
+  return r;
+}
+
+template <int VPT, int NT>
+HS_DEVICE void row_e4m3(const u16x8 (&ov)[VPT], int nvec, int row, int N, unsigned char* __restrict__ out8,
+                        float* __restrict__ xs8, float* scratch) {
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+    if (threadIdx.x + i * NT < nvec)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(bf16_to_f32(ov[i][j])));
+  __syncthreads();  // scratch was the norm's reduction buffer
+  amax = block_max(amax, scratch);
+  const float inv = amax > 0.f ? 448.f / amax : 1.f;
+  if (threadIdx.x == 0) xs8[row] = amax > 0.f ? amax / 448.f : 1.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) *reinterpret_cast<uint2*>(out8 + (long)row * N + idx * 8) = e4m3_8(ov[i], inv);
+  }
+}
+
 HS_HOST_DEVICE int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // SiLU(gate) * up on 8 bf16 lanes, fp32 math, one bf16 rounding (shared by the

@@ -11,9 +11,10 @@ namespace hipserve {
 void launch_embed_rmsnorm(void* out, void* residual, const void* table, const long* ids, const long* src,
                           const long* tok, const void* w, bool weight_f32, int rows, int hidden, float eps,
                           hipStream_t s);
+// out8 / xs8 (optional): out also as per-token e4m3 + row scale (= act_quant_fp8 of out)
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                     bool weight_f32, int rows, int hidden, long x_stride,
-                    long out_stride, float eps, hipStream_t s);
+                    long out_stride, float eps, hipStream_t s, void* out8 = nullptr, float* xs8 = nullptr);
 // per-head q/k RMSNorm inside the qkv rows, in place (fp32 weights [D], D <= 256)
 void launch_qk_rmsnorm(void* qkv, long stride, const float* qw, const float* kw, int T, int nq, int nkv, int D,
                        float eps, hipStream_t s);

@@ -28,7 +28,8 @@ template <int NT, int VPT, bool kAdd, bool kWF32, bool kGather = false>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     unsigned short* __restrict__ out, unsigned short* __restrict__ residual,
     const unsigned short* __restrict__ x, const void* __restrict__ weight,
-    int hidden, long x_stride, long out_stride, float eps, GatherIds gi = GatherIds{}) {
+    int hidden, long x_stride, long out_stride, float eps, GatherIds gi = GatherIds{},
+    unsigned char* __restrict__ out8 = nullptr, float* __restrict__ xs8 = nullptr) {
   static_assert(!(kAdd && kGather), "gather mode writes the residual, it does not add to it");
   __shared__ float scratch[16];
   const int row = blockIdx.x;
@@ -69,6 +70,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   ss = block_sum(ss, scratch);
   const float inv = rsqrtf(ss / hidden + eps);
   u16x8* orow = reinterpret_cast<u16x8*>(out + row * out_stride);
+  u16x8 ov[VPT];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * NT;
@@ -88,29 +90,32 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(v[i][j] * inv * w[j]);
       orow[idx] = o;
+      ov[i] = o;
     }
   }
+  // optional per-token e4m3 copy (the FP8 W8A8 GEMM's input, = act_quant_fp8 of out)
+  if (out8 != nullptr) row_e4m3<VPT, NT>(ov, nvec, row, hidden, out8, xs8, scratch);
 }
 
 template <bool kAdd, bool kWF32>
 static void launch_rmsnorm_t(unsigned short* out, unsigned short* residual,
                              const unsigned short* x, const void* w, int rows,
                              int hidden, long x_stride, long out_stride, float eps,
-                             hipStream_t s) {
+                             hipStream_t s, unsigned char* o8, float* x8) {
   const int nvec = hidden / 8;
   dim3 grid(rows);
   if (norm_threads(hidden) == 256) {  // hidden < 4096: nvec < 512
     if (nvec <= 256)
-      rmsnorm_kernel<256, 1, kAdd, kWF32><<<grid, 256, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+      rmsnorm_kernel<256, 1, kAdd, kWF32><<<grid, 256, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps, GatherIds{}, o8, x8);
     else
-      rmsnorm_kernel<256, 2, kAdd, kWF32><<<grid, 256, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+      rmsnorm_kernel<256, 2, kAdd, kWF32><<<grid, 256, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps, GatherIds{}, o8, x8);
   } else {
     if (nvec <= 512)
-      rmsnorm_kernel<512, 1, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+      rmsnorm_kernel<512, 1, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps, GatherIds{}, o8, x8);
     else if (nvec <= 1024)
-      rmsnorm_kernel<512, 2, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+      rmsnorm_kernel<512, 2, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps, GatherIds{}, o8, x8);
     else
-      rmsnorm_kernel<512, 4, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps);
+      rmsnorm_kernel<512, 4, kAdd, kWF32><<<grid, 512, 0, s>>>(out, residual, x, w, hidden, x_stride, out_stride, eps, GatherIds{}, o8, x8);
   }
 }
 
@@ -237,16 +242,17 @@ void launch_embed_rmsnorm(void* out, void* residual, const void* table, const lo
 
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                     bool weight_f32, int rows, int hidden, long x_stride,
-                    long out_stride, float eps, hipStream_t s) {
+                    long out_stride, float eps, hipStream_t s, void* out8, float* xs8) {
+  auto* o8 = static_cast<unsigned char*>(out8);
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
   auto* xi = static_cast<const unsigned short*>(x);
   if (residual) {
-    if (weight_f32) launch_rmsnorm_t<true, true>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
-    else launch_rmsnorm_t<true, false>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
+    if (weight_f32) launch_rmsnorm_t<true, true>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s, o8, xs8);
+    else launch_rmsnorm_t<true, false>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s, o8, xs8);
   } else {
-    if (weight_f32) launch_rmsnorm_t<false, true>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
-    else launch_rmsnorm_t<false, false>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s);
+    if (weight_f32) launch_rmsnorm_t<false, true>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s, o8, xs8);
+    else launch_rmsnorm_t<false, false>(o, r, xi, w, rows, hidden, x_stride, out_stride, eps, s, o8, xs8);
   }
 }
 

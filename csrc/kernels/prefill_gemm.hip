@@ -772,13 +772,14 @@ bool launch_prefill_gemm_f8(int epi, void* C, long ldc, const void* A, long lda,
 
 // Per-token dynamic e4m3: one workgroup per row, max |x| then x * 448 / max saturated
 // to +-448 and converted in pairs by v_cvt_pk_fp8_f32 (OCP e4m3fn, round to nearest even).
-__global__ __launch_bounds__(256) void act_quant_fp8_kernel(unsigned char* __restrict__ q, float* __restrict__ xs,
-                                                            const unsigned short* __restrict__ x, long x_stride, int K) {
+__global__ __launch_bounds__(1024) void act_quant_fp8_kernel(unsigned char* __restrict__ q, float* __restrict__ xs,
+                                                             const unsigned short* __restrict__ x, long x_stride, int K) {
   __shared__ float red[16];
   const long row = blockIdx.x;
+  const int step = blockDim.x * 8;
   const unsigned short* xr = x + row * x_stride;
   float amax = 0.f;
-  for (int c = threadIdx.x * 8; c < K; c += 256 * 8) {
+  for (int c = threadIdx.x * 8; c < K; c += step) {
     const u16x8 v = *reinterpret_cast<const u16x8*>(xr + c);
 #pragma unroll
     for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(bf16_to_f32(v[e])));
@@ -786,7 +787,7 @@ __global__ __launch_bounds__(256) void act_quant_fp8_kernel(unsigned char* __res
   amax = block_max(amax, red);
   const float inv = amax > 0.f ? 448.f / amax : 1.f;
   if (threadIdx.x == 0) xs[row] = amax > 0.f ? amax / 448.f : 1.f;
-  for (int c = threadIdx.x * 8; c < K; c += 256 * 8) {
+  for (int c = threadIdx.x * 8; c < K; c += step) {
     const u16x8 v = *reinterpret_cast<const u16x8*>(xr + c);
     float f[8];
 #pragma unroll
@@ -802,8 +803,11 @@ __global__ __launch_bounds__(256) void act_quant_fp8_kernel(unsigned char* __res
 
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s) {
   if (M < 1) return;
-  act_quant_fp8_kernel<<<M, 256, 0, s>>>(static_cast<unsigned char*>(q), xs, static_cast<const unsigned short*>(x),
-                                         x_stride, K);
+  // one block per row; at decode batch sizes (few rows, long K) a wider block cuts the
+  // two dependent passes over the row: 256 threads per 2048 k up to 1024
+  const int nt = M >= 512 ? 256 : min(1024, max(256, ((K / 8 + 255) / 256) * 256 / 2));
+  act_quant_fp8_kernel<<<M, nt, 0, s>>>(static_cast<unsigned char*>(q), xs, static_cast<const unsigned short*>(x),
+                                        x_stride, K);
 }
 
 static bool pg_shape_ok(int M, int N, int K) { return M >= 1 && N % PG_BN == 0 && K % PG_BK == 0 && K >= PG_BK; }

@@ -20,31 +20,42 @@ hipStream_t cur_stream() {
 #define CHECK_ROWMAJOR(x) TORCH_CHECK((x).stride(-1) == 1, #x " must have unit inner stride")
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 
-void rmsnorm(at::Tensor& out, const at::Tensor& x, const at::Tensor& weight, double eps) {
+static void e4m3_out_args(const c10::optional<at::Tensor>& out8, const c10::optional<at::Tensor>& xs8,
+                          const at::Tensor& out, void** o8, float** x8, const char* who);
+
+void rmsnorm(at::Tensor& out, const at::Tensor& x, const at::Tensor& weight, double eps,
+             const c10::optional<at::Tensor>& out8, const c10::optional<at::Tensor>& xs8) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "rmsnorm expects 2-D [rows, hidden]");
   const int hidden = x.size(1);
   TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384, "hidden must be a multiple of 8, <= 16384");
   TORCH_CHECK(weight.numel() == hidden && weight.is_contiguous());
   TORCH_CHECK(weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat);
+  void* o8;
+  float* x8;
+  e4m3_out_args(out8, xs8, out, &o8, &x8, "rmsnorm");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::launch_rmsnorm(out.data_ptr(), nullptr, x.data_ptr(), weight.data_ptr(),
                            weight.scalar_type() == at::kFloat, x.size(0), hidden,
-                           x.stride(0), out.stride(0), (float)eps, cur_stream());
+                           x.stride(0), out.stride(0), (float)eps, cur_stream(), o8, x8);
 }
 
 void fused_add_rmsnorm(at::Tensor& out, const at::Tensor& x, at::Tensor& residual,
-                       const at::Tensor& weight, double eps) {
+                       const at::Tensor& weight, double eps, const c10::optional<at::Tensor>& out8,
+                       const c10::optional<at::Tensor>& xs8) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_BF16(residual);
   CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out); CHECK_CONTIG(residual);
   TORCH_CHECK(x.dim() == 2 && residual.sizes() == x.sizes());
   const int hidden = x.size(1);
   TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384);
   TORCH_CHECK(weight.numel() == hidden && weight.is_contiguous());
+  void* o8;
+  float* x8;
+  e4m3_out_args(out8, xs8, out, &o8, &x8, "fused_add_rmsnorm");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::launch_rmsnorm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), weight.data_ptr(),
                            weight.scalar_type() == at::kFloat, x.size(0), hidden,
-                           x.stride(0), out.stride(0), (float)eps, cur_stream());
+                           x.stride(0), out.stride(0), (float)eps, cur_stream(), o8, x8);
 }
 
 // out = RMSNorm(table[id]) * weight, residual = table[id] per row; id = ids[row], or
@@ -1175,10 +1186,10 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor w, Tensor pair_slot, int k) -> ()");
   m.def("moe_decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k, int N, int splits, bool packed, bool glu) -> ()");
   m.def("moe_combine_partial(Tensor(a!) out, Tensor ws, Tensor w, Tensor pair_slot, int k) -> ()");
-  m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps) -> ()");
+  m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps, Tensor(b!)? out8=None, Tensor(c!)? xs8=None) -> ()");
   m.def("embed_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor table, Tensor ids, Tensor? src, Tensor? tok, "
         "Tensor weight, float eps) -> ()");
-  m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps) -> ()");
+  m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps, Tensor(c!)? out8=None, Tensor(d!)? xs8=None) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale, int window=0) -> ()");

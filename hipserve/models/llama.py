@@ -462,7 +462,7 @@ class LlamaModel:
         src, tok = meta.id_src
         return torch.where(src >= 0, tok.index_select(0, src.clamp(min=0)), ids)
 
-    def add_rmsnorm(self, out, residual, x, splits, w, out16=None, out8=None):
+    def add_rmsnorm(self, out, residual, x, splits, w, out16=None, out8=None, out8p=None):
         """residual += x summed over the TP ranks; out = RMSNorm(residual) * w.
         ``x`` is this rank's partial output of a row-parallel projection: fp32
         split-K partials [S, M, N] of a decode GEMM, or the plain projection output
@@ -470,14 +470,14 @@ class LlamaModel:
         kernels; TP>1 the in-house cross-rank epilogue (parallel/comm.py)."""
         eps = self.cfg.rms_norm_eps
         if self.tp.world_size > 1:
-            assert out16 is None and out8 is None, "out16 / out8 need TP = 1"
+            assert out16 is None and out8 is None and out8p is None, "out16 / out8 need TP = 1"
             return self.tp.add_rmsnorm(out, residual, x, splits, w, eps, ops=self.ops)
         if x.dtype == torch.float32 and residual.dtype != torch.float32:
             q8, s8 = out8 if out8 is not None else (None, None)
             torch.ops.hipserve.splitk_add_rmsnorm(out, residual, x, splits, w, eps, out16, q8, s8)
-        else:
+        else:  # out8p: the FP8 prefill GEMM's e4m3 input (the decode out8 needs the partial path)
             assert out16 is None and out8 is None, "out16 / out8 need the split-K partial path"
-            self.ops.fused_add_rmsnorm(out, x, residual, w, eps)
+            self.ops.fused_add_rmsnorm(out, x, residual, w, eps, out8=out8p)
         return out
 
     def post_add_rmsnorm(self, out, residual, pt, x, w, w_post, w_next, out16=None, out8=None):
@@ -556,13 +556,17 @@ class LlamaModel:
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
         if Td:
             part, tmp_out, tmp_ml = self._decode_split(Td, meta)
-        ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
+        x8 = self._x8p(xn, self.layers[0].wqkv)  # FP8 models: the norm writes the e4m3 GEMM input too
+        ops.rmsnorm(xn, h, self.layers[0].ln1, eps, out8=x8)
         L = len(self.layers)
         tp1 = self.tp.world_size == 1
         for i, lw in enumerate(self.layers):
             # prefill-sized batches: the hand-written GEMM where start-up timing chose it
             # (ops/pgemm.py), with the residual add / SiLU-GLU in its epilogue
-            qkv = pgemm.gemm(xn, lw.wqkv) if pgemm.use("plain", lw.wqkv, T) else self.linear(xn, lw.wqkv)
+            if x8 is not None:
+                qkv = pgemm.f8_gemm(xn, lw.wqkv, 0, x8=x8)
+            else:
+                qkv = pgemm.gemm(xn, lw.wqkv) if pgemm.use("plain", lw.wqkv, T) else self.linear(xn, lw.wqkv)
             if lw.bqkv is not None:
                 qkv += lw.bqkv
             if lw.q_norm is not None:  # per-head RMSNorm of q and k, before RoPE
@@ -577,25 +581,27 @@ class LlamaModel:
             if Td:  # rows past Tp + Td: prefill padding (model_runner._pad_rows)
                 ops.paged_decode(attn[Tp:Tp + Td], qkv[Tp:Tp + Td], kc, vc, meta.bt_decode, meta.ctx_decode,
                                  tmp_out, tmp_ml, nq, nkv, part, self.scale, win)
+            x8 = self._x8p(xn, lw.wgu, glu=True)
             if tp1 and lw.post_attn_norm is None and pgemm.use("add", lw.wo, T):
                 pgemm.gemm_add_(residual, attn, lw.wo)  # residual += o_proj(attn), in the GEMM epilogue
-                ops.rmsnorm(xn, residual, lw.ln2, eps)
+                ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
             else:
                 o = self.linear_rowpar(attn, lw.wo)
                 if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)
                     o = self._tp_sum(o, xn)
                     ops.rmsnorm(o, o, lw.post_attn_norm, eps)
-                    ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps)
+                    ops.fused_add_rmsnorm(xn, o, residual, lw.ln2, eps, out8=x8)
                 else:
-                    self.add_rmsnorm(xn, residual, o, 1, lw.ln2)
+                    self.add_rmsnorm(xn, residual, o, 1, lw.ln2, out8p=x8)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
+            x8n = self._x8p(xn, self.layers[i + 1].wqkv) if i + 1 < L else None  # next layer's qkv input
             if lw.router is not None:
                 h = self.moe(xn, lw)
             else:
                 gelu = cfg.hidden_act == "gelu_tanh"
                 act = None
                 if pgemm.f8_use(lw.wgu, T, glu=True):  # FP8 gate|up: GLU in the e4m3 GEMM's epilogue
-                    act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2)
+                    act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2, x8=x8)
                 elif cfg.hidden_act in ("silu", "gelu_tanh") and pgemm.use("glu", lw.wgu, T):
                     act = pgemm.gemm_glu(xn, lw.wgu, gelu)
                 if act is None:
@@ -605,7 +611,8 @@ class LlamaModel:
                 if (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
                         and pgemm.use("add", lw.wd, T)):
                     pgemm.gemm_add_(residual, act, lw.wd)
-                    ops.rmsnorm(xn, residual, nxt, eps)
+                    ops.rmsnorm(xn, residual, nxt, eps, out8=x8n)
+                    x8 = x8n
                     continue
                 h = self.linear_rowpar(act, lw.wd)
             if ds is not None and i < len(ds) and self.tp.rank == 0:
@@ -615,9 +622,10 @@ class LlamaModel:
             if lw.post_ff_norm is not None:
                 h = self._tp_sum(h, xn)
                 ops.rmsnorm(h, h, lw.post_ff_norm, eps)
-                ops.fused_add_rmsnorm(xn, h, residual, nxt, eps)
+                ops.fused_add_rmsnorm(xn, h, residual, nxt, eps, out8=x8n)
             else:
-                self.add_rmsnorm(xn, residual, h, 1, nxt)
+                self.add_rmsnorm(xn, residual, h, 1, nxt, out8p=x8n)
+            x8 = x8n
         return xn
 
     def act_and_mul(self, out: torch.Tensor, gu: torch.Tensor):
@@ -858,6 +866,17 @@ class LlamaModel:
                 or Q.f8_decode_ok(consumer)):  # the W8A8 decode GEMM quantises x itself
             return None
         return torch.empty(like.shape, dtype=torch.float16, device=like.device)
+
+    def _x8p(self, like: torch.Tensor, consumer, glu: bool = False):
+        """(e4m3, row scales) buffers for the per-token FP8 copy of ``like`` that its
+        producing RMSNorm writes when ``consumer`` runs the FP8 W8A8 prefill GEMM at this
+        row count (= act_quant_fp8 of ``like``; one kernel and one pass over x fewer);
+        None otherwise. TP = 1 (the TP > 1 norms are the cross-rank epilogue)."""
+        if (self.tp.world_size != 1 or not like.is_cuda or isinstance(consumer, torch.Tensor)
+                or getattr(self.ops, "name", "") != "hip" or not pgemm.f8_use(consumer, like.shape[0], glu)):
+            return None
+        return (torch.empty(like.shape, dtype=torch.uint8, device=like.device),
+                torch.empty(like.shape[0], dtype=torch.float32, device=like.device))
 
     def _x8(self, like: torch.Tensor, consumer):
         """(e4m3 [M, K] uint8, row scales fp32 [M]) buffers for the per-token FP8 copy of

@@ -60,12 +60,13 @@ class KernelOps:
         load_library()
         self._op = torch.ops.hipserve
 
-    def rmsnorm(self, out, x, w, eps):
-        self._op.rmsnorm(out, x, w, eps)
+    def rmsnorm(self, out, x, w, eps, out8=None):
+        """out8: (e4m3 [rows, hidden] uint8, scales fp32 [rows]) per-token FP8 copy of out."""
+        self._op.rmsnorm(out, x, w, eps, *(out8 if out8 is not None else (None, None)))
         return out
 
-    def fused_add_rmsnorm(self, out, x, residual, w, eps):
-        self._op.fused_add_rmsnorm(out, x, residual, w, eps)
+    def fused_add_rmsnorm(self, out, x, residual, w, eps, out8=None):
+        self._op.fused_add_rmsnorm(out, x, residual, w, eps, *(out8 if out8 is not None else (None, None)))
         return out
 
     def silu_and_mul(self, out, x):
@@ -150,11 +151,13 @@ class ReferenceOps:
     def fill_uniform(self, out, row0, col0, gcols, key, scale):
         return ref.fill_uniform(out, row0, col0, gcols, key, scale)
 
-    def rmsnorm(self, out, x, w, eps):
+    def rmsnorm(self, out, x, w, eps, out8=None):
+        assert out8 is None, "the FP8 copy is a HIP-kernel output"
         out.copy_(ref.rmsnorm(x, w, eps))
         return out
 
-    def fused_add_rmsnorm(self, out, x, residual, w, eps):
+    def fused_add_rmsnorm(self, out, x, residual, w, eps, out8=None):
+        assert out8 is None, "the FP8 copy is a HIP-kernel output"
         y, r = ref.fused_add_rmsnorm(x, residual, w, eps)
         residual.copy_(r)
         out.copy_(y)

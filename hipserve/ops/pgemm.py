@@ -106,15 +106,16 @@ def act_quant(x: torch.Tensor):
     return xq, xs
 
 
-def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x8=None) -> torch.Tensor:
     """epi 0: out = x @ W^T (bf16 [M, N]); 1: out (the residual) += x @ W^T;
-    2 / 3: W = (gate, up) parts, out = silu / gelu_tanh(x Wg^T) * (x Wu^T)."""
+    2 / 3: W = (gate, up) parts, out = silu / gelu_tanh(x Wg^T) * (x Wu^T). ``x8``:
+    x's per-token e4m3 copy already written by its producer (an RMSNorm with out8)."""
     ps = w.parts
     M = x.shape[0]
     if out is None:
         n = ps[0].N if epi in (2, 3) else w.N
         out = torch.empty(M, n, dtype=torch.bfloat16, device=x.device)
-    xq, xs = act_quant(x)
+    xq, xs = x8 if x8 is not None else act_quant(x)
     torch.ops.hipserve.prefill_gemm_f8(out, xq, xs, [p.q for p in ps], [p.rs for p in ps], epi)
     return out
 

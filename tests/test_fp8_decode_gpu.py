@@ -100,3 +100,26 @@ def test_norm_epilogue_e4m3_copy_is_act_quant(post, M, N):
         torch.ops.hipserve.splitk_add_rmsnorm(out, res, ws, S, w1, 1e-6, None, q8, s8)
     xq, xs = pgemm.act_quant(out)
     assert torch.equal(q8, xq) and torch.equal(s8, xs)
+
+
+@pytest.mark.parametrize("add", [False, True])
+@pytest.mark.parametrize("M,N", [(3, 5376), (300, 4096), (1000, 1024)])
+def test_rmsnorm_e4m3_copy_is_act_quant(add, M, N):
+    """rmsnorm / fused_add_rmsnorm ``out8`` / ``xs8`` (the FP8 prefill GEMM's input,
+    written by the norm instead of a separate act_quant_fp8 pass) is bit-identical to
+    act_quant_fp8 of the bf16 output."""
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(M + N + add)
+    x = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(N, device=DEV, generator=g)).to(torch.bfloat16)
+    out = torch.empty_like(x)
+    q8 = torch.empty(M, N, device=DEV, dtype=torch.uint8)
+    s8 = torch.empty(M, device=DEV, dtype=torch.float32)
+    if add:
+        torch.ops.hipserve.fused_add_rmsnorm(out, x, res, w, 1e-6, q8, s8)
+    else:
+        torch.ops.hipserve.rmsnorm(out, x, w, 1e-6, q8, s8)
+    xq, xs = pgemm.act_quant(out)
+    assert torch.equal(q8, xq) and torch.equal(s8, xs)
