@@ -79,6 +79,21 @@ def main():
             r.update({"fp8_ms": round(t_f8, 4), "fp8_quant_ms": round(t_q, 4),
                       "fp8_TFs": round(2 * M * N * K / t_f8 / 1e9, 1)})
             del qws
+            # hipBLASLt FP8 with row-wise scales (torch._scaled_mm) on a plain [N, K] e4m3
+            # copy, for reference: the library's FP8 rate on the same shapes
+            try:
+                w8 = [(w.float() / (w.float().abs().amax(1, keepdim=True) / 448.0)).to(torch.float8_e4m3fn)
+                      for w in ws]
+                sw = [(w.float().abs().amax(1) / 448.0).reshape(1, -1).contiguous() for w in ws]
+                xq8, xs8 = pgemm.act_quant(x)
+                xf8 = xq8.view(torch.float8_e4m3fn)
+                sx = xs8.reshape(-1, 1).contiguous()
+                t_sm = time_fn(lambda: [torch._scaled_mm(xf8, w.t(), scale_a=sx, scale_b=s_, out_dtype=torch.bfloat16)
+                                        for w, s_ in zip(w8, sw)])
+                r.update({"blas_fp8_rowwise_ms": round(t_sm, 4), "blas_fp8_TFs": round(2 * M * N * K / t_sm / 1e9, 1)})
+                del w8
+            except Exception as e:  # noqa: BLE001 - report what the library refused
+                r["blas_fp8_rowwise"] = f"unsupported: {type(e).__name__}: {str(e)[:120]}"
         if name == "gu":  # GEMM + SiLU-GLU unit
             act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
             wg = ws  # the GLU epilogue reads the merged [gate; up] weight as stored
