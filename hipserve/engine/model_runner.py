@@ -146,6 +146,8 @@ class ModelRunner:
                     total = torch.cuda.get_device_properties(self.device).total_memory
                     self.quant_shadow_bytes = getattr(self, "quant_shadow_bytes", 0) + Q.make_dense_shadows(
                         qws, self.device, (24 << 30) + total // 4)
+                    # FP8: plain e4m3 copies for the hipBLASLt FP8 prefill GEMMs
+                    self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()
         # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
         # budget (measured no faster than the heuristic on sustained prefill chains,

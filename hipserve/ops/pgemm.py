@@ -112,10 +112,24 @@ def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x
     x's per-token e4m3 copy already written by its producer (an RMSNorm with out8)."""
     ps = w.parts
     M = x.shape[0]
+    out_given = out is not None
     if out is None:
         n = ps[0].N if epi in (2, 3) else w.N
         out = torch.empty(M, n, dtype=torch.bfloat16, device=x.device)
     xq, xs = x8 if x8 is not None else act_quant(x)
+    wp = getattr(w, "f8_plain", None)
+    if wp is not None and M % 16 == 0:  # hipBLASLt FP8, row-wise scales, on the plain e4m3 copy
+        y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wp.t(), scale_a=xs.reshape(-1, 1),
+                             scale_b=w.f8_scale, out_dtype=torch.bfloat16)
+        if epi == 0:
+            if not out_given:
+                return y
+            out.copy_(y)
+        elif epi == 1:
+            out.add_(y)
+        else:  # [gate | up] -> act
+            (torch.ops.hipserve.silu_and_mul if epi == 2 else torch.ops.hipserve.gelu_and_mul)(out, y)
+        return out
     torch.ops.hipserve.prefill_gemm_f8(out, xq, xs, [p.q for p in ps], [p.rs for p in ps], epi)
     return out
 

@@ -615,8 +615,8 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
             off += p.N
         return out
     from . import pgemm
-    if pgemm.f8_use(w, M):  # FP8 W8A8 on the scaled e4m3 MFMA, straight from the tiled weights
-        return pgemm.f8_gemm(x, w, 0, out)
+    if pgemm.f8_use(w, M):  # FP8 W8A8: the scaled e4m3 MFMA from the tiled weights, or hipBLASLt FP8
+        return pgemm.f8_gemm(x, w, 0, None if getattr(w, "f8_plain", None) is not None else out)
     if w.dense is not None:  # prefill on the resident bf16 copy: no per-call dequant pass
         return torch.nn.functional.linear(x, w.dense)
     if w.v2 and x.is_cuda and M <= QPREFILL_MAX_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
@@ -630,6 +630,41 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
         off += p.N
     return torch.nn.functional.linear(x, buf)
 
+
+
+def fp8_plain(p: QuantPart) -> torch.Tensor:
+    """The plain [N, K] e4m3 bytes of a per-channel FP8 part (inverse of from_fp8's
+    tiled permutation)."""
+    R, nsb = p.N // 16, p.K // 256
+    return p.q.reshape(R, nsb, 4, 4, 16, 16).permute(0, 4, 1, 3, 2, 5).reshape(p.N, p.K)
+
+
+def make_fp8_plain(weights, device, reserve_bytes: int) -> int:
+    """Plain [N, K] e4m3 copies (and [1, N] fp32 scales) of the FP8 projections for the
+    prefill GEMMs on hipBLASLt's FP8 kernels with row-wise scales (torch._scaled_mm:
+    2.0-2.4 PFLOP/s on the Gemma-3-27B shapes vs 1.6-1.9 for the hand-written e4m3
+    kernel, tools/bench_pgemm.py --fp8), while ``reserve_bytes`` of HBM stay free: the
+    same bytes as the tiled decode copy (27 GB for Gemma-3-27B on a 288 GB part). The
+    decode GEMMs keep the tiled copy. HIPSERVE_FP8_PREFILL_LIB=0 disables it."""
+    import os
+
+    if os.environ.get("HIPSERVE_FP8_PREFILL_LIB", "1") == "0" or torch.device(device).type != "cuda":
+        return 0
+    from . import pgemm
+    added = 0
+    for w in sorted(weights, key=lambda w: -w.N * w.K):
+        if getattr(w, "f8_plain", None) is not None or not (pgemm.f8_fits(w) or pgemm.f8_fits(w, glu=True)):
+            continue
+        if not all(p.qtype == FP8 for p in w.parts):
+            continue
+        need = w.N * w.K
+        free, _ = torch.cuda.mem_get_info(device)
+        if free - need < reserve_bytes:
+            continue
+        w.f8_plain = torch.cat([fp8_plain(p) for p in w.parts]).view(torch.float8_e4m3fn)
+        w.f8_scale = (torch.cat([p.rs for p in w.parts]) / 256.0).reshape(1, -1).contiguous()
+        added += need
+    return added
 
 
 def make_dense_shadows(weights, device, reserve_bytes: int) -> int:
