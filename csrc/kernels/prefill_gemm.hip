@@ -801,8 +801,51 @@ __global__ __launch_bounds__(1024) void act_quant_fp8_kernel(unsigned char* __re
   }
 }
 
+// single pass for rows that fit in registers (<= 4 x 8 elements per thread): the row is
+// read once, its amax reduced, then quantised from registers — at decode batch sizes the
+// kernel is the latency of its dependent global reads, and this drops one of them
+template <int VPT>
+__global__ __launch_bounds__(1024) void act_quant_fp8_reg_kernel(unsigned char* __restrict__ q,
+                                                                 float* __restrict__ xs,
+                                                                 const unsigned short* __restrict__ x,
+                                                                 long x_stride, int K) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  const int nvec = K >> 3;
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + row * x_stride);
+  u16x8 v[VPT];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      v[i] = xr[idx];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(bf16_to_f32(v[i][e])));
+    }
+  }
+  amax = block_max(amax, red);
+  const float inv = amax > 0.f ? 448.f / amax : 1.f;
+  if (threadIdx.x == 0) xs[row] = amax > 0.f ? amax / 448.f : 1.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) *reinterpret_cast<uint2*>(q + row * K + idx * 8) = e4m3_8(v[i], inv);
+  }
+}
+
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s) {
   if (M < 1) return;
+  if (M < 512 && K % 8 == 0 && K <= 1024 * 8 * 4) {
+    auto* qo = static_cast<unsigned char*>(q);
+    auto* xi = static_cast<const unsigned short*>(x);
+    const int nvec = K / 8;
+    if (nvec <= 512) act_quant_fp8_reg_kernel<1><<<M, max(64, (nvec + 63) / 64 * 64), 0, s>>>(qo, xs, xi, x_stride, K);
+    else if (nvec <= 1024) act_quant_fp8_reg_kernel<2><<<M, 512, 0, s>>>(qo, xs, xi, x_stride, K);
+    else if (nvec <= 2048) act_quant_fp8_reg_kernel<2><<<M, 1024, 0, s>>>(qo, xs, xi, x_stride, K);
+    else act_quant_fp8_reg_kernel<4><<<M, 1024, 0, s>>>(qo, xs, xi, x_stride, K);
+    return;
+  }
   // one block per row; at decode batch sizes (few rows, long K) a wider block cuts the
   // two dependent passes over the row: 256 threads per 2048 k up to 1024
   const int nt = M >= 512 ? 256 : min(1024, max(256, ((K / 8 + 255) / 256) * 256 / 2));

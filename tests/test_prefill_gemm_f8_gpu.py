@@ -157,3 +157,19 @@ def test_f8_gemm_library_path_matches_kernel(epi):
     b = res0.clone() if epi == 1 else None
     b = pgemm.f8_gemm(x, w, epi, b)
     torch.testing.assert_close(b.float(), a.float(), rtol=2e-2, atol=2e-2 * a.float().abs().max().item())
+
+
+@pytest.mark.parametrize("M,K", [(7, 5376), (64, 21504), (33, 512), (100, 4096)])
+def test_act_quant_fp8_register_path(M, K):
+    """Decode batch sizes take the single-pass act_quant kernel (row held in registers);
+    it quantises exactly like the two-pass kernel (same scale, same conversion)."""
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    x = _x(g, M, K)
+    xq, xs = pgemm.act_quant(x)
+    # the same rows inside a >= 512-row batch run the two-pass kernel
+    big = torch.cat([x, torch.zeros(512, K, device=DEV, dtype=x.dtype)])
+    bq, bs = pgemm.act_quant(big)
+    assert torch.equal(xq, bq[:M]) and torch.equal(xs, bs[:M])
+    assert torch.equal(bs[M:], torch.ones(512, device=DEV))
