@@ -220,6 +220,10 @@ bool launch_prefill_gemm_f8(int epi, void* C, long ldc, const void* A, long lda,
 // ws[S, M, N] = (xq . wq^T over K slice s) * xs[m] * rs[n] / 256; (K / 256) / S in
 // {1, 2, 3, 4, 6, 7, 8, 12, 14, 16, 21}; part rows % 16 == 0. W.xs = xs.
 bool launch_fp8_decode_gemm(float* ws, const void* xq, const PgF8& W, int M, int N, int K, int S, hipStream_t s);
+// act = silu / gelu_tanh(gate) * up of [gate | up] rows, written as per-token e4m3 q8 [rows,
+// inter] + xs [rows] (and bf16 into out if non-null); inter / 8 <= 4096. activation.hip
+bool launch_glu_quant(bool gelu, void* out, void* q8, float* xs, const void* in, long rows, int inter,
+                      long in_stride, hipStream_t s);
 // per-token dynamic e4m3 quantisation: xs[m] = max|x[m, :]| / 448, q = sat(x / xs)
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s);
 void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);

@@ -753,6 +753,27 @@ void fp8_decode_gemm(at::Tensor& ws, const at::Tensor& xq, const at::Tensor& xs,
               "fp8_decode_gemm: unsupported (M <= 64, part rows % 16, (K / 256) / splits in the kernel's step set)");
 }
 
+// [gate | up] rows -> per-token e4m3 act (q8 [rows, I] uint8, xs [rows] fp32), optionally
+// the bf16 act too: glu_and_mul -> act_quant_fp8 in one pass
+void glu_quant(const c10::optional<at::Tensor>& out, at::Tensor& q8, at::Tensor& xs, const at::Tensor& x, bool gelu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_CONTIG(q8); CHECK_CONTIG(xs);
+  const long rows = x.size(0);
+  const int inter = x.size(1) / 2;
+  TORCH_CHECK(q8.scalar_type() == at::kByte && q8.size(0) == rows && q8.size(1) == inter &&
+                  xs.scalar_type() == at::kFloat && xs.numel() == rows && x.stride(0) % 8 == 0,
+              "glu_quant: q8 uint8 [rows, I], xs fp32 [rows]");
+  void* o = nullptr;
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(out->scalar_type() == at::kBFloat16 && out->is_contiguous() && out->size(0) == rows &&
+                out->size(1) == inter, "glu_quant: out bf16 [rows, I]");
+    o = out->data_ptr();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_glu_quant(gelu, o, q8.data_ptr(), xs.data_ptr<float>(), x.data_ptr(), rows, inter,
+                                         x.stride(0), cur_stream()),
+              "glu_quant: I % 8 == 0 and I <= 32768");
+}
+
 void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_CONTIG(xq); CHECK_CONTIG(xs);
   const int M = x.size(0), K = x.size(1);
@@ -1222,6 +1243,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
+  m.def("glu_quant(Tensor(a!)? out, Tensor(b!) q8, Tensor(c!) xs, Tensor x, bool gelu) -> ()");
   m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
   m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi, int variant=2) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
@@ -1276,6 +1298,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("splitk_post_add_rmsnorm", &splitk_post_add_rmsnorm);
   m.impl("act_quant_fp8", &act_quant_fp8);
   m.impl("fp8_decode_gemm", &fp8_decode_gemm);
+  m.impl("glu_quant", &glu_quant);
   m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);

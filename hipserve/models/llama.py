@@ -599,22 +599,28 @@ class LlamaModel:
                 h = self.moe(xn, lw)
             else:
                 gelu = cfg.hidden_act == "gelu_tanh"
-                act = None
-                if pgemm.f8_use(lw.wgu, T, glu=True):  # FP8 gate|up: GLU in the e4m3 GEMM's epilogue
-                    act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2, x8=x8)
+                act = act8 = None
+                if pgemm.f8_use(lw.wgu, T, glu=True):  # FP8 gate|up
+                    if pgemm.f8_use(lw.wd, T):  # FP8 down too: act straight to e4m3 (glu_quant)
+                        act8 = pgemm.f8_glu_q8(xn, lw.wgu, gelu, x8)
+                    if act8 is None:  # GLU in the e4m3 GEMM's epilogue
+                        act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2, x8=x8)
                 elif cfg.hidden_act in ("silu", "gelu_tanh") and pgemm.use("glu", lw.wgu, T):
                     act = pgemm.gemm_glu(xn, lw.wgu, gelu)
-                if act is None:
+                if act8 is not None:
+                    h = pgemm.f8_gemm(None, lw.wd, 0, x8=act8)
+                elif act is None:
                     gu = self.linear(xn, lw.wgu)
                     act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                     self.act_and_mul(act, gu)
-                if (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
-                        and pgemm.use("add", lw.wd, T)):
+                if act8 is None and (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
+                                     and pgemm.use("add", lw.wd, T)):
                     pgemm.gemm_add_(residual, act, lw.wd)
                     ops.rmsnorm(xn, residual, nxt, eps, out8=x8n)
                     x8 = x8n
                     continue
-                h = self.linear_rowpar(act, lw.wd)
+                if act8 is None:
+                    h = self.linear_rowpar(act, lw.wd)
             if ds is not None and i < len(ds) and self.tp.rank == 0:
                 # DeepStack: visual features join the residual stream after layer i
                 # (rank 0 only: the row-parallel partials are summed across ranks next)

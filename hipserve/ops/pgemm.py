@@ -111,11 +111,12 @@ def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x
     2 / 3: W = (gate, up) parts, out = silu / gelu_tanh(x Wg^T) * (x Wu^T). ``x8``:
     x's per-token e4m3 copy already written by its producer (an RMSNorm with out8)."""
     ps = w.parts
-    M = x.shape[0]
+    M = x.shape[0] if x is not None else x8[0].shape[0]
+    dev = x.device if x is not None else x8[0].device
     out_given = out is not None
     if out is None:
         n = ps[0].N if epi in (2, 3) else w.N
-        out = torch.empty(M, n, dtype=torch.bfloat16, device=x.device)
+        out = torch.empty(M, n, dtype=torch.bfloat16, device=dev)
     xq, xs = x8 if x8 is not None else act_quant(x)
     wp = getattr(w, "f8_plain", None)
     if wp is not None and M % 16 == 0:  # hipBLASLt FP8, row-wise scales, on the plain e4m3 copy
@@ -132,6 +133,25 @@ def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x
         return out
     torch.ops.hipserve.prefill_gemm_f8(out, xq, xs, [p.q for p in ps], [p.rs for p in ps], epi)
     return out
+
+
+def f8_glu_q8(x: torch.Tensor, w, gelu: bool, x8=None):
+    """FP8 gate|up on hipBLASLt FP8 (the plain e4m3 copy), then GLU and the per-token e4m3
+    quantisation of act in one kernel (glu_quant): (xq, xs) of act for the FP8 down
+    projection — no bf16 act round trip and no separate act_quant. None when the
+    weight has no plain copy (the caller runs f8_gemm's GLU epilogue instead)."""
+    wp = getattr(w, "f8_plain", None)
+    M = x.shape[0]
+    if wp is None or M % 16 or not hasattr(torch.ops.hipserve, "glu_quant"):
+        return None
+    xq, xs = x8 if x8 is not None else act_quant(x)
+    y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wp.t(), scale_a=xs.reshape(-1, 1),
+                         scale_b=w.f8_scale, out_dtype=torch.bfloat16)
+    inter = y.shape[1] // 2
+    q8 = torch.empty(M, inter, dtype=torch.uint8, device=x.device)
+    s8 = torch.empty(M, dtype=torch.float32, device=x.device)
+    torch.ops.hipserve.glu_quant(None, q8, s8, y, gelu)
+    return q8, s8
 
 
 def moe_fits(w13, w2) -> bool:

@@ -173,3 +173,25 @@ def test_act_quant_fp8_register_path(M, K):
     bq, bs = pgemm.act_quant(big)
     assert torch.equal(xq, bq[:M]) and torch.equal(xs, bs[:M])
     assert torch.equal(bs[M:], torch.ones(512, device=DEV))
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+@pytest.mark.parametrize("M,I", [(5, 21504), (256, 4096), (1000, 14336), (64, 384)])
+def test_glu_quant_is_glu_then_act_quant(gelu, M, I):
+    """glu_quant ([gate | up] -> per-token e4m3 act, the FP8 down projection's input) is
+    bit-identical to glu_and_mul followed by act_quant_fp8, and its optional bf16 act
+    to glu_and_mul."""
+    from hipserve.ops import pgemm
+
+    g = torch.Generator(device=DEV).manual_seed(M + I + gelu)
+    gu = (torch.randn(M, 2 * I, device=DEV, generator=g) * 3).to(torch.bfloat16)
+    act = torch.empty(M, I, device=DEV, dtype=torch.bfloat16)
+    (torch.ops.hipserve.gelu_and_mul if gelu else torch.ops.hipserve.silu_and_mul)(act, gu)
+    xq, xs = pgemm.act_quant(act)
+    q8 = torch.empty(M, I, device=DEV, dtype=torch.uint8)
+    s8 = torch.empty(M, device=DEV, dtype=torch.float32)
+    a2 = torch.empty_like(act)
+    torch.ops.hipserve.glu_quant(a2, q8, s8, gu, gelu)
+    assert torch.equal(a2, act) and torch.equal(q8, xq) and torch.equal(s8, xs)
+    torch.ops.hipserve.glu_quant(None, q8, s8, gu, gelu)
+    assert torch.equal(q8, xq)
