@@ -224,6 +224,9 @@ bool launch_fp8_decode_gemm(float* ws, const void* xq, const PgF8& W, int M, int
 // inter] + xs [rows] (and bf16 into out if non-null); inter / 8 <= 4096. activation.hip
 bool launch_glu_quant(bool gelu, void* out, void* q8, float* xs, const void* in, long rows, int inter,
                       long in_stride, hipStream_t s);
+// decode_fused.hip: splitk_glu with the per-token e4m3 act for an FP8 down projection
+bool launch_splitk_glu_q8(void* act, const float* ws, int S, int M, int I, bool gelu, void* q8, float* xs8,
+                          hipStream_t s);
 // per-token dynamic e4m3 quantisation: xs[m] = max|x[m, :]| / 448, q = sat(x / xs)
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s);
 void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);

@@ -774,6 +774,27 @@ void glu_quant(const c10::optional<at::Tensor>& out, at::Tensor& q8, at::Tensor&
               "glu_quant: I % 8 == 0 and I <= 32768");
 }
 
+// fp32 split-K partials of the merged gate|up [S, M, 2I] -> GLU -> per-token e4m3 act
+// (q8 [M, I], xs8 [M]) for the W8A8 down projection; act (bf16) optional
+void splitk_glu_q8(const c10::optional<at::Tensor>& act, const at::Tensor& ws, int64_t splits, bool gelu,
+                   at::Tensor& q8, at::Tensor& xs8) {
+  CHECK_DEV(ws); CHECK_CONTIG(q8); CHECK_CONTIG(xs8);
+  const int M = q8.size(0), I = q8.size(1);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * 2L * I &&
+                  q8.scalar_type() == at::kByte && xs8.scalar_type() == at::kFloat && xs8.numel() == M,
+              "splitk_glu_q8: ws fp32 [S, M, 2I], q8 uint8 [M, I], xs8 fp32 [M]");
+  void* a = nullptr;
+  if (act.has_value() && act->defined()) {
+    TORCH_CHECK(act->scalar_type() == at::kBFloat16 && act->is_contiguous() && act->sizes() == q8.sizes(),
+                "splitk_glu_q8: act bf16 [M, I]");
+    a = act->data_ptr();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  TORCH_CHECK(hipserve::launch_splitk_glu_q8(a, ws.data_ptr<float>(), (int)splits, M, I, gelu, q8.data_ptr(),
+                                             xs8.data_ptr<float>(), cur_stream()),
+              "splitk_glu_q8: I % 8 == 0, I <= 32768");
+}
+
 void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_CONTIG(xq); CHECK_CONTIG(xs);
   const int M = x.size(0), K = x.size(1);
@@ -1244,6 +1265,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
   m.def("glu_quant(Tensor(a!)? out, Tensor(b!) q8, Tensor(c!) xs, Tensor x, bool gelu) -> ()");
+  m.def("splitk_glu_q8(Tensor(a!)? act, Tensor ws, int splits, bool gelu, Tensor(b!) q8, Tensor(c!) xs8) -> ()");
   m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
   m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi, int variant=2) -> ()");
   m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
@@ -1299,6 +1321,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("act_quant_fp8", &act_quant_fp8);
   m.impl("fp8_decode_gemm", &fp8_decode_gemm);
   m.impl("glu_quant", &glu_quant);
+  m.impl("splitk_glu_q8", &splitk_glu_q8);
   m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);

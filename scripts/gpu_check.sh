@@ -97,6 +97,7 @@ for s in $steps; do
     q3int8) bench_named q3int8 HIPSERVE_FUSED_DECODE=1 -- --model qwen3-30b-a3b --quantization int8 ;;
     q06) bench_named q06 HIPSERVE_FUSED_DECODE=1 -- --model qwen3-0.6b ;;
     g27bf16_unfused) bench_named g27bf16_unfused HIPSERVE_FUSED_DECODE=0 -- --model gemma-3-27b ;;
+    g27fp8_gluq8off) bench_named g27fp8_gluq8off HIPSERVE_GLU_Q8=0 -- --model gemma-3-27b --quantization fp8 ;;
     g27fp8_unfused) bench_named g27fp8_unfused HIPSERVE_FUSED_DECODE=0 -- --model gemma-3-27b --quantization fp8 ;;
     q4km) bench_named q4km HIPSERVE_QUANT_SHADOW=1 -- --quantization q4_k_m ;;
     q4km_x16off) bench_named q4km_x16off HIPSERVE_QGEMM_X16=0 -- --quantization q4_k_m ;;
