@@ -406,6 +406,7 @@ def run_phase(args):
             "sampling": {"temperature": args.temperature, "top_p": args.top_p},
         },
         "engine_init_s": round(init_s, 1),
+        "init_breakdown_s": getattr(engine.runner, "init_times", {}),
         "kv_blocks": engine.runner.num_blocks,
     }
     if ol_summary:  # open loop: TTFT tail and inter-token latency of every request
@@ -423,7 +424,8 @@ def run_phase(args):
                    "p50_ttft_ms": out["p50_ttft_ms"], "ms_per_step": out["ms_per_step"], "steps": steps,
                    "warmup": args.warmup, "global_batch": args.concurrency,
                    "input_len": args.input_len, "output_len": args.output_len,
-                   "engine_init_s": out["engine_init_s"], **out["tp_info"]}
+                   "engine_init_s": out["engine_init_s"], "init_breakdown_s": out["init_breakdown_s"],
+                   "kv_blocks": out["kv_blocks"], **out["tp_info"]}
     if lg is not None:
         lg.close()
         stack.stop()

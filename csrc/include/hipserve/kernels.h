@@ -197,6 +197,14 @@ struct PgEpi {
 };
 bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
                          int K, const PgEpi& E, hipStream_t s);
+// prefill_gemm_packed.hip — C[M, N] = X[M, K] . W[N, K]^T with W in pack_decode_weight's
+// layout (the decode GEMMs' copy; no second copy of the weight), K % 256 == 0, any M, N.
+// wm = 1: 128 x 512 workgroup tiles, wm = 2: 256 x 256. bias (bf16 [N], STORE only) may be null.
+//   PW_EPI_STORE / PW_EPI_ADD as PG_*; PW_EPI_GLU / PW_EPI_GEGLU: W packed with glu = true
+//   (merged [gate; up], N = 2I, I % 64 == 0), C = act [M, I]
+constexpr int PW_EPI_STORE = 0, PW_EPI_ADD = 1, PW_EPI_GLU = 2, PW_EPI_GEGLU = 3;
+bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
+                                int K, const void* bias, int wm, hipStream_t s);
 // FP8 (W8A8) form: A = per-token e4m3 activations [M, K] bytes (row scale xs[M]),
 // B = e4m3 weights in the decode kernel's tiled layout (gguf_mfma.hip: [N/16][K/256]
 // [4096 B]) as up to 4 parts stacked along N (each rows % 256 == 0; GLU: part 0 =

@@ -28,6 +28,9 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int PG_BM = 256, PG_BN = 256, PG_BK = 64, PG_T = 512;
 constexpr int PG_TILE = PG_BM * PG_BK * 2;  // bytes of one operand tile per stage
+// the staging loads address A and B through 32-bit buffer offsets (range clamped to 2 GiB):
+// larger operands would read zeros / wrap, so such shapes are refused (callers fall back)
+static bool pg_offsets_ok(long a_bytes, long b_bytes) { return a_bytes < (1L << 31) && b_bytes < (1L << 31); }
 
 // Global weight row of row r of the tile's B panel. GLU: the merged [gate; up] weight
 // (2I rows) is read in its own layout, tile tn taking gate rows 128 tn .. + 127 then
@@ -746,6 +749,9 @@ __global__ __launch_bounds__(PG_T) void pgemm_f8_kernel(const unsigned char* __r
 bool launch_prefill_gemm_f8(int epi, void* C, long ldc, const void* A, long lda, const PgF8& W, int M, int N, int K,
                             hipStream_t s) {
   if (M < 1 || K % 256 || W.n < 1 || W.n > kPgF8Parts) return false;
+  if (!pg_offsets_ok((long)M * lda, 0)) return false;
+  for (int i = 0; i < W.n; ++i)
+    if (!pg_offsets_ok(0, (long)W.p[i].rows * K)) return false;
   const bool glu = epi == PG_EPI_GLU || epi == PG_EPI_GEGLU;
   if (glu) {
     if (W.n != 2 || W.p[0].rows != W.p[1].rows || W.p[0].rows % 128 || N != 2 * W.p[0].rows) return false;
@@ -858,6 +864,7 @@ static bool pg_shape_ok(int M, int N, int K) { return M >= 1 && N % PG_BN == 0 &
 bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
                          int K, const PgEpi& E, hipStream_t s) {
   if (!pg_shape_ok(M, N, K)) return false;
+  if (!pg_offsets_ok((long)M * lda * 2, (long)N * ldb * 2)) return false;  // grouped: B = one expert
   const int tiles_m = (M + PG_BM - 1) / PG_BM, tiles_n = N / PG_BN;
   const dim3 grid(tiles_m * tiles_n);
   auto* a = static_cast<const unsigned short*>(A);

@@ -1,0 +1,269 @@
+// Prefill GEMM over the decode kernels' packed weight layout (VERDICT r3, next round item
+// 1: one weight layout for prefill and decode, hand-written MFMA on the prefill hot path):
+//
+//   C[M, N] = X[M, K] . W[N, K]^T      bf16 in, fp32 accumulate, epilogue fused
+//
+// W is read from pack_decode_weight's copy (decode_gemm.hip),
+// [ceil(N/128)][K/256][8 row groups][8 k-slots][64 lanes][8 bf16]: every 1 KiB
+// (row group, k-slot) piece is exactly the first operand of one
+// v_mfma_f32_16x16x32_bf16 for a wave (lane l: row 16 rg + (l & 15), k 32 s + 8 (l >> 4)).
+// Weight fragments therefore go global -> VGPR with ONE coalesced buffer_load_dwordx4
+// each and never touch LDS. Only X is staged through LDS. Per 32-deep K step a wave issues
+// 8 LDS fragment reads + XP/2 staging writes, against 16 reads (+ 8 writes) when both
+// operands are staged — LDS issue was what held the previous kernels at ~55 % MFMA
+// busy (profiles/r3_pgemm_pmc.md).
+//
+// Geometry: 256 threads = 4 waves, one per SIMD (512 registers each), every wave a
+// 128 (m) x 128 (n) output block = ONE packed weight tile: 64 accumulator tiles
+// acc[rg][i] (rg: 16-row weight group, i: 16-row X group) = 256 fp32 per lane.
+// WM x WN waves per workgroup: WM = 1 -> 128 x 512 (X staged once for four weight
+// tiles), WM = 2 -> 256 x 256 (two waves stream the same weight tile, the second read
+// is an L1 / L2 hit).
+//
+// Pipeline, per 64-deep K stage st (two 32-deep slots, 64 MFMAs per wave each):
+//   slot 2st   : MFMA(wa, xa) row group by row group; after a group's 8 MFMAs its
+//                weight register is reloaded with slot 2st + 2; the X fragments of slot
+//                2st + 1 (xb) are read from LDS stage st; stage st + 1 (registers,
+//                loaded two slots ago) is written to the other LDS buffer and stage
+//                st + 2 is loaded from global; ONE barrier closes the slot.
+//   slot 2st+1 : MFMA(wb, xb); wb reloaded with slot 2st + 3; xa <- LDS stage st + 1.
+// Weight and X global loads are two slots (~2,000 MFMA cycles) ahead of their use. Loads
+// past the end re-read the last slot / stage (clamped offsets: no branches in the loop,
+// so the compiler's vmcnt waits stay exact). Rows past M read as zero (buffer range).
+//
+// Epilogues (lane holds C[m][n .. n+3], m = m0 + 128 wm + 16 i + (l & 15),
+// n = 128 t + 16 rg + 4 (l >> 4)):
+//   PW_EPI_STORE  C = bf16(acc) (+ bias[n])
+//   PW_EPI_ADD    C (the residual, in place) = bf16(bf16(acc) + C)
+//   PW_EPI_GLU    W packed with glu=true (each tile: 64 gate rows then their 64 up
+//                 rows): gate rg and up rg + 4 sit in the same lane, so
+//                 act[m, 64 t + 16 rg + 4 (l >> 4) + j] = silu(gate) * up in registers
+//   PW_EPI_GEGLU  as GLU with tanh-GELU (Gemma)
+#include "hipserve/common.h"
+#include "hipserve/kernels.h"
+
+namespace hipserve {
+
+constexpr int PW_T = 256;
+
+// workgroup -> (tm, tn): XCD-aware (consecutive ids on one XCD), then groups of PW_GM
+// m-tiles walked n-major inside, so the ~32 workgroups an XCD runs at once cover
+// 8 m-tiles x 4 n-tiles and share both operands in its L2
+constexpr int PW_GM = 8;
+HS_DEVICE void pw_tile(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int id = xcd_remap(bid, tiles_m * tiles_n);
+  const int grp = id / (PW_GM * tiles_n), first = grp * PW_GM;
+  const int gsz = min(PW_GM, tiles_m - first);
+  const int r = id - first * tiles_n;
+  tm = first + r % gsz;
+  tn = r / gsz;
+}
+
+HS_DEVICE void pw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// MFMA on an AGPR accumulator as inline asm: with the builtin, hipcc moved the 256
+// accumulators between AGPRs inside the loop (tools/asm_stats.py: ~200 v_accvgpr moves
+// per 128 MFMAs). asm MFMAs are invisible to the hazard recognizer: the epilogue covers the
+// MFMA -> VALU read of the accumulators by hand.
+HS_DEVICE void pw_mfma(f32x4& acc, const u32x4& w, const u32x4& x) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(x));
+}
+
+template <int WM, int EPI>
+__global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
+    const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
+    unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n,
+    const unsigned short* __restrict__ bias) {
+  constexpr int WN = 4 / WM, BM = 128 * WM, STAGE = BM * 128, XP = BM / 32;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  int tm, tn;
+  pw_tile(blockIdx.x, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM;
+  const int ntiles = (N + 127) >> 7;
+  const int t = tn * WN + wn;           // this wave's packed weight tile
+  const int tl = min(t, ntiles - 1);    // waves past the last tile compute a copy, store nothing
+  const int KS = K >> 8, nq = K >> 5, nst = K >> 6;
+
+  // this wave's weight stream: tile tl, 64 KiB per 256-deep K step
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + (long)tl * KS * 32768), 0, KS * 65536, 0x00020000);
+  const int wvo = lane * 16;
+  auto wload = [&](int q, int rg) -> u32x4 {  // 32-deep slot q (clamped), row group rg
+    q = min(q, nq - 1);
+    return __builtin_amdgcn_raw_buffer_load_b128(wrs, wvo, (q >> 3) * 65536 + rg * 8192 + (q & 7) * 1024, 0);
+  };
+  // X staging: thread -> rows 32 p + (tid >> 3), 16-byte chunk tid & 7 of the 128-byte
+  // (64-deep) row; rows >= M fall outside the buffer range and read as zero
+  const int rows = min(BM, M - m0);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X + (long)m0 * ldx), 0, (int)((long)rows * ldx * 2), 0x00020000);
+  int xvo[XP];
+#pragma unroll
+  for (int p = 0; p < XP; ++p) xvo[p] = (p * 32 + (tid >> 3)) * (int)ldx * 2 + (tid & 7) * 16;
+  // LDS image [BM rows][128 B]: 16-byte chunk c of row r at chunk c ^ ((r >> 1) & 7), which
+  // spreads each ds_read_b128 lane group (rows 0-3 / 12-15 of one chunk, 4-11 of the
+  // next) over all 16 slots of a 256-byte bank row; (r >> 1) & 7 is the same for rows
+  // r and r + 32 p
+  const int xdo = (tid >> 3) * 128 + (((tid & 7) ^ ((tid >> 4) & 7)) * 16);
+  u32x4 xst[XP];
+  auto xload = [&](int st) {
+    st = min(st, nst - 1);
+#pragma unroll
+    for (int p = 0; p < XP; ++p) xst[p] = __builtin_amdgcn_raw_buffer_load_b128(xrs, xvo[p], st * 128, 0);
+  };
+  auto xstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < XP; ++p) *reinterpret_cast<u32x4*>(lds + buf * STAGE + p * 4096 + xdo) = xst[p];
+  };
+  const int fr = lane & 15, fq = lane >> 4, sw = (fr >> 1) & 7;
+  const int foff = (wm * 128 + fr) * 128;
+  const int ch[2] = {(fq ^ sw) * 16, ((4 + fq) ^ sw) * 16};
+  auto xfrag = [&](int buf, int h, int i) -> u32x4 {
+    return *reinterpret_cast<const u32x4*>(lds + buf * STAGE + foff + i * 2048 + ch[h]);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int rg = 0; rg < 8; ++rg)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[rg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 wa[8], wb[8], xa[8], xb[8];
+
+  // prologue: stage 0 in LDS, stage 1 in registers, weight slots 0 and 1 in flight
+  xload(0);
+  xstore(0);
+  xload(1);
+#pragma unroll
+  for (int rg = 0; rg < 8; ++rg) wa[rg] = wload(0, rg);
+#pragma unroll
+  for (int rg = 0; rg < 8; ++rg) wb[rg] = wload(1, rg);
+  pw_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xa[i] = xfrag(0, 0, i);
+
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    // ---- slot 2 st
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        pw_mfma(acc[rg][i], wa[rg], xa[i]);
+      wa[rg] = wload(2 * st + 2, rg);
+      xb[rg] = xfrag(buf, 1, rg);
+      if (rg == 2) xstore(buf ^ 1);  // stage st + 1 (loaded during slot 2 st - 2)
+      if (rg == 3) xload(st + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    pw_barrier();  // stage st + 1 visible; every read of stage st - 1 long done
+    // ---- slot 2 st + 1
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        pw_mfma(acc[rg][i], wb[rg], xb[i]);
+      wb[rg] = wload(2 * st + 3, rg);
+      xa[rg] = xfrag(buf ^ 1, 0, rg);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> VALU reads
+  if (t >= ntiles) return;
+  const int mb = m0 + wm * 128 + fr;
+  if constexpr (EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU) {
+    const int I = N >> 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mb + 16 * i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int c = t * 64 + rg * 16 + 4 * fq;
+        unsigned short o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned short g = f32_to_bf16(acc[rg][i][j]), u = f32_to_bf16(acc[rg + 4][i][j]);
+          o[j] = EPI == PW_EPI_GEGLU ? gelu_mul1(g, u) : silu_mul1(g, u);
+        }
+        if (c < I)
+          *reinterpret_cast<uint2*>(C + (long)m * ldc + c) =
+              uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+      }
+    }
+  } else {
+    float bv[8][4];
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = t * 128 + rg * 16 + 4 * fq + j;
+        bv[rg][j] = (bias != nullptr && n < N) ? bf16_to_f32(bias[n]) : 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mb + 16 * i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int rg = 0; rg < 8; ++rg) {
+        const int n = t * 128 + rg * 16 + 4 * fq;
+        if (n >= N) continue;
+        uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n);
+        float o[4];
+        if constexpr (EPI == PW_EPI_ADD) {  // C is the residual: C = bf16(bf16(acc) + C)
+          const uint2 r = *dst;
+          const unsigned short rr[4] = {(unsigned short)(r.x & 0xffff), (unsigned short)(r.x >> 16),
+                                        (unsigned short)(r.y & 0xffff), (unsigned short)(r.y >> 16)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[rg][i][j])) + bf16_to_f32(rr[j]);
+        } else {  // bias added to the fp32 accumulator, one rounding
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = acc[rg][i][j] + bv[rg][j];
+        }
+        *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+      }
+    }
+  }
+}
+
+bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
+                                int K, const void* bias, int wm, hipStream_t s) {
+  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2)) return false;
+  const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
+  if (glu && (N % 128 || bias != nullptr)) return false;
+  if (epi == PW_EPI_ADD && bias != nullptr) return false;
+  // 32-bit buffer offsets: the weight stream of one tile and one workgroup's X rows
+  if ((long)(K / 256) * 65536 >= (1L << 31) || (long)128 * wm * ldx * 2 >= (1L << 31)) return false;
+  const int BM = 128 * wm, WN = 4 / wm;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = ((N + 127) / 128 + WN - 1) / WN;
+  const dim3 grid(tiles_m * tiles_n);
+  auto* x = static_cast<const unsigned short*>(X);
+  auto* w = static_cast<const unsigned short*>(Wp);
+  auto* c = static_cast<unsigned short*>(C);
+  auto* b = static_cast<const unsigned short*>(bias);
+#define PW_LAUNCH(WM_, E_) \
+  pgw_kernel<WM_, E_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b)
+#define PW_EPIS(WM_)                                          \
+  switch (epi) {                                              \
+    case PW_EPI_STORE: PW_LAUNCH(WM_, PW_EPI_STORE); return true; \
+    case PW_EPI_ADD: PW_LAUNCH(WM_, PW_EPI_ADD); return true;     \
+    case PW_EPI_GLU: PW_LAUNCH(WM_, PW_EPI_GLU); return true;     \
+    case PW_EPI_GEGLU: PW_LAUNCH(WM_, PW_EPI_GEGLU); return true; \
+    default: return false;                                    \
+  }
+  if (wm == 1) {
+    PW_EPIS(1)
+  }
+  PW_EPIS(2)
+#undef PW_EPIS
+#undef PW_LAUNCH
+}
+
+}  // namespace hipserve

@@ -692,6 +692,30 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
               "prefill_gemm: unsupported");
 }
 
+// Prefill GEMM over the packed decode layout (prefill_gemm_packed.hip): wp =
+// pack_decode_weight(w[N, K], glu) (flat, ceil(N/128)*128*K bf16). epi as prefill_gemm
+// (2 / 3 need the glu packing); bias (epi 0 only) bf16 [N] or None; wm 1 or 2.
+void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
+                         const c10::optional<at::Tensor>& bias, int64_t wm) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(wp.is_contiguous(), "prefill_gemm_packed: packed weight must be contiguous");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 256 == 0 && wp.numel() == (N + 127) / 128 * 128 * K, "prefill_gemm_packed: wp = pack(w[N, K % 256])");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "prefill_gemm_packed: alignment");
+  const bool glu = epi == 2 || epi == 3;
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? N / 2 : N), "prefill_gemm_packed: out shape");
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "prefill_gemm_packed: bias [N]");
+    bp = bias->data_ptr();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(hipserve::launch_prefill_gemm_packed((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
+                                                   wp.data_ptr(), M, (int)N, K, bp, (int)wm, cur_stream()),
+              "prefill_gemm_packed: unsupported (glu needs N % 128, bias only with epi 0, 32-bit offsets)");
+}
+
 // FP8 W8A8 form: xq [M, K] uint8 e4m3 + xs [M] fp32 (act_quant_fp8), the weight as
 // tiled FP8 parts (ops/quant.py QuantPart.from_fp8: q [N/16, K/256, 4096] uint8 and
 // rs [N] fp32) stacked along N. epi 0 / 1 as prefill_gemm; 2 / 3: parts = (gate, up),
@@ -1261,6 +1285,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
+  m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
@@ -1316,6 +1341,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm_glu", &decode_gemm_glu);
   m.impl("decode_gemm_fused", &decode_gemm_fused);
   m.impl("prefill_gemm", &prefill_gemm);
+  m.impl("prefill_gemm_packed", &prefill_gemm_packed);
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);
   m.impl("splitk_post_add_rmsnorm", &splitk_post_add_rmsnorm);
   m.impl("act_quant_fp8", &act_quant_fp8);

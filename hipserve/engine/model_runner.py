@@ -101,6 +101,9 @@ class ModelRunner:
         t0 = time.time()
         self._load_weights()
         self.load_time = time.time() - t0
+        # start-up breakdown (bench.py reports it: the 70B TP=8 phase must visibly fit its box)
+        self.init_times = {"weights_s": round(self.load_time, 2)}
+        t1 = time.time()
         if tp.world_size > 1:
             if "tp_exact_reduce" in ecfg.extra:
                 tp.exact_reduce = bool(ecfg.extra["tp_exact_reduce"])
@@ -113,10 +116,14 @@ class ModelRunner:
                 if tp.ensure_custom_ar(msg):
                     # prefill-sized messages: in-house kernel or RCCL, measured on this node
                     tp.calibrate_collectives(H, ecfg.max_num_batched_tokens)
+        self.init_times["collectives_s"] = round(time.time() - t1, 2)
         self.max_bs = min(ecfg.max_num_seqs, max(GRAPH_BUCKETS))
         self.buckets = [b for b in GRAPH_BUCKETS if b <= max(self.max_bs, 1)]
         if self.buckets[-1] < self.max_bs:
             self.buckets.append(self.max_bs)
+        # decode-sized messages stay on the in-house collectives, captured or eager
+        tp.rccl_floor_rows = max(tp.rccl_floor_rows, self.buckets[-1])
+        t1 = time.time()
         # decode GEMM autotune BEFORE the KV pool takes the memory: its cold-weight
         # copies need scratch, and weights whose winner is the packed decode GEMM get
         # their pre-shuffled copy (gemm.PACKED) allocated before the pool is sized
@@ -152,6 +159,8 @@ class ModelRunner:
         # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
         # budget (measured no faster than the heuristic on sustained prefill chains,
         # profiles/r1_prefill_gemm_tunableop.md)
+        self.init_times["decode_gemm_tune_s"] = round(time.time() - t1, 2)
+        t1 = time.time()
         self.prefill_gemm_report = []
         if self.device.type == "cuda" and ecfg.extra.get("prefill_gemm_tune", False):
             from ..ops import prefill_tune
@@ -169,6 +178,8 @@ class ModelRunner:
         # vs 18.8 ms at 8,192, tools/bench_prefill_m.py); rank 0 times the model's
         # prefill GEMMs per 256-row count once and pads a chunk to the fastest count at
         # or above it (padding rows: token 0, no KV write, outputs unused)
+        self.init_times["prefill_gemm_tune_s"] = round(time.time() - t1, 2)
+        t1 = time.time()
         self.prefill_pad = None
         pg_all = bool(self.pgemm_report) and all(r["pgemm"] for r in self.pgemm_report)
         if (self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0
@@ -183,8 +194,11 @@ class ModelRunner:
         self.pen_counts = torch.zeros(nslots, V, dtype=torch.int32, device=self.device)
         self.pen_seen = torch.zeros(nslots, (V + 31) // 32, dtype=torch.int32, device=self.device)
         self._free_pen = list(range(nslots - 1, -1, -1))
+        self.init_times["pad_probe_s"] = round(time.time() - t1, 2)
+        t1 = time.time()
         self.num_blocks = self._num_kv_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.block_size)
+        self.init_times["kv_alloc_s"] = round(time.time() - t1, 2)
         self.pad_block = self.num_blocks - 1          # scratch block for graph padding rows
         self.width = -(-self.max_model_len // self.block_size)
         part = ecfg.decode_partition
@@ -201,6 +215,7 @@ class ModelRunner:
         self.use_graphs = self.device.type == "cuda" and not ecfg.enforce_eager
         if self.use_graphs:
             self._capture_graphs()
+        self.init_times["graph_capture_s"] = round(getattr(self, "graph_capture_time", 0.0), 2)
 
     # ------------------------------------------------------------ setup
     def _load_weights(self):

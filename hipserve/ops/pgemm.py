@@ -36,13 +36,22 @@ CHOICE: dict[tuple, bool] = {}     # (kind, N, K) -> use prefill_gemm
 REPORT: list[dict] = []
 
 
+# the kernels address each operand through 32-bit buffer offsets (prefill_gemm.hip
+# pg_offsets_ok): larger operands go to hipBLASLt
+OFFSET_LIMIT = 1 << 31
+
+
+def offsets_ok(M: int, K: int, N: int, elem: int = 2) -> bool:
+    return M * K * elem < OFFSET_LIMIT and N * K * elem < OFFSET_LIMIT
+
+
 def fits(w) -> bool:
     return isinstance(w, torch.Tensor) and w.is_cuda and w.dim() == 2 and w.dtype == torch.bfloat16 \
         and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0 and w.stride(1) == 1
 
 
 def use(kind: str, w, M: int) -> bool:
-    if MODE == "0" or M < MIN_ROWS or not fits(w):
+    if MODE == "0" or M < MIN_ROWS or not fits(w) or not offsets_ok(M, w.shape[1], w.shape[0]):
         return False
     if MODE == "1":
         return True
@@ -95,7 +104,8 @@ def f8_fits(w, glu: bool = False) -> bool:
 
 
 def f8_use(w, M: int, glu: bool = False) -> bool:
-    return M >= F8_MIN_ROWS and f8_fits(w, glu)
+    return (M >= F8_MIN_ROWS and f8_fits(w, glu) and M * w.parts[0].K < OFFSET_LIMIT
+            and all(p.N * p.K < OFFSET_LIMIT for p in w.parts))
 
 
 def act_quant(x: torch.Tensor):

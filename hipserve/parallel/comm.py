@@ -27,6 +27,31 @@ import torch
 import torch.distributed as dist
 
 
+def rccl_crossover(results) -> int | None:
+    """Pure decision of ``TPGroup.calibrate_collectives``: ``results`` are (rows,
+    in-house kernel time, RCCL time) by increasing rows (max over ranks). Returns the
+    smallest row count from which RCCL is faster at EVERY larger measured size, None
+    when the in-house kernel wins at the largest size (a size where RCCL wins but a
+    larger one where it loses does not move the crossover down: the routing is a
+    single threshold)."""
+    res = sorted(results)
+    for i, (M, _, _) in enumerate(res):
+        if all(tr < tc for _, tc, tr in res[i:]):
+            return M
+    return None
+
+
+def route_rccl(rows: int, min_rows: int | None, floor_rows: int, backend: str | None, capturing: bool) -> bool:
+    """Pure routing of one eager message of ``rows`` rows: RCCL only on an RCCL group,
+    outside a hipGraph capture, at or above the calibrated crossover AND above
+    ``floor_rows`` (the largest decode-graph batch): every decode-sized message stays
+    on the in-house kernel whether its step runs captured or eager (penalty
+    initialisation steps run eager), so graph and eager decode steps reduce in the
+    same order."""
+    return (min_rows is not None and backend == "nccl" and not capturing
+            and rows >= min_rows and rows > floor_rows)
+
+
 class TPGroup:
     def __init__(self, rank: int = 0, world_size: int = 1, group=None, device=None):
         self.rank = rank
@@ -46,6 +71,9 @@ class TPGroup:
         # instead of the in-house kernels; set per node by calibrate_collectives()
         # (None: always in-house). HIPSERVE_CAR_RCCL_MIN_ROWS overrides (-1: never).
         self.rccl_min_rows: int | None = None
+        # messages of at most this many rows always take the in-house kernels (set by
+        # the runner to its largest decode-graph batch)
+        self.rccl_floor_rows = self.fp32_exchange_rows
         self.collective_report: list[dict] = []
 
     SHM_SLOT_BYTES = 8 << 20
@@ -90,8 +118,8 @@ class TPGroup:
     def _use_rccl(self, rows: int) -> bool:
         """Route an eager message of ``rows`` rows through RCCL (calibrated crossover;
         captured decode graphs always use the in-house kernels)."""
-        return (self.rccl_min_rows is not None and rows >= self.rccl_min_rows and self.backend == "nccl"
-                and not torch.cuda.is_current_stream_capturing())
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        return route_rccl(rows, self.rccl_min_rows, self.rccl_floor_rows, self.backend, capturing)
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over TP ranks: bf16 messages that fit the registered buffer
@@ -236,10 +264,7 @@ class TPGroup:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=self._cpu_group)
             res.append((M, float(tt[0]), float(tt[1])))
         self.check()
-        for i, (M, tc, tr) in enumerate(res):
-            if all(r[2] < r[1] for r in res[i:]):
-                self.rccl_min_rows = M
-                break
+        self.rccl_min_rows = rccl_crossover(res)
         self.collective_report = [{"rows": M, "N": N, "car_us": round(tc, 1), "rccl_us": round(tr, 1)}
                                   for M, tc, tr in res]
         return self.collective_report

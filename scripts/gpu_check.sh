@@ -107,6 +107,7 @@ for s in $steps; do
     f16test) run_one tests/test_gguf_gpu.py ;;
     fusedtest) run_one tests/test_fused_decode_gpu.py ;;
     pgtest) run_one tests/test_prefill_gemm_gpu.py ;;
+    pwtest) run_one tests/test_prefill_gemm_packed_gpu.py ;;
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;

@@ -15,6 +15,7 @@ pass() {  # pass <name> <counters...>
 }
 pass p1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU && \
 pass p2 SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT && \
+pass p3 SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_WAVES TCC_HIT_sum TCC_MISS_sum && \
 cd $HERE && python3 - <<'PY'
 import csv, collections, glob
 for f in sorted(glob.glob("gpurun_out/pmc/p*.csv")):

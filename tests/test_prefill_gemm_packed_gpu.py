@@ -1,0 +1,93 @@
+"""Prefill GEMM over the packed decode-weight layout (csrc/kernels/prefill_gemm_packed.hip)
+vs a plain PyTorch fp32 reference of the same op: plain store (+ bias), residual add and
+the SiLU / GELU GLU epilogues, both workgroup shapes (wm = 1: 128 x 512, wm = 2: 256 x 256),
+ragged M (not a multiple of the row tile, and fewer rows than one tile), N that is not a
+multiple of 128 (zero-padded packed rows) or of the workgroup's 512 / 256 columns (waves
+past the last weight tile), K from one 256-deep packed step up. Asymmetric random
+operands catch transposed fragments and swizzles."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    from hipserve.ops import load_library
+
+    load_library()
+
+
+def _rnd(g, *s, scale=1.0):
+    return ((torch.rand(*s, device=DEV, generator=g) * 2 - 1) * scale).to(torch.bfloat16)
+
+
+def _pack(w, glu=False):
+    N, K = w.shape
+    wp = torch.empty(-(-N // 128) * 128 * K, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.pack_decode_weight(wp, w, glu)
+    return wp
+
+
+SHAPES = [(256, 512, 256), (300, 640, 1024), (1000, 200, 512), (77, 1536, 768), (2049, 384, 2048),
+          (1, 128, 256), (8192, 512, 4096)]
+
+
+@pytest.mark.parametrize("wm", [1, 2])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_packed_store(M, N, K, wm):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, _pack(w), N, 0, None, wm)
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("wm", [1, 2])
+def test_packed_store_bias_and_strided_x(wm):
+    g = torch.Generator(device=DEV).manual_seed(5)
+    M, N, K = 700, 896, 512
+    xb = _rnd(g, M, K + 64)
+    x = xb[:, 32:32 + K]  # row stride K + 64
+    w, b = _rnd(g, N, K, scale=0.05), _rnd(g, N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, _pack(w), N, 0, b, wm)
+    want = x.float() @ w.float().t() + b.float()
+    torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("wm", [1, 2])
+@pytest.mark.parametrize("M,N,K", [(300, 512, 1024), (1000, 384, 512), (2049, 1024, 256)])
+def test_packed_residual_add(M, N, K, wm):
+    g = torch.Generator(device=DEV).manual_seed(7 + M)
+    x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
+    res0 = _rnd(g, M, N)
+    res = res0.clone()
+    torch.ops.hipserve.prefill_gemm_packed(res, x, _pack(w), N, 1, None, wm)
+    h = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    want = (h + res0.float()).to(torch.bfloat16).float()
+    torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("wm,act", [(1, "silu"), (2, "silu"), (1, "gelu"), (2, "gelu")])
+@pytest.mark.parametrize("M,I,K", [(300, 256, 1024), (1000, 192, 512), (2049, 64, 256), (513, 1344, 768)])
+def test_packed_glu(M, I, K, wm, act):
+    g = torch.Generator(device=DEV).manual_seed(11 + M)
+    x, w = _rnd(g, M, K), _rnd(g, 2 * I, K, scale=0.05)
+    out = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, _pack(w, glu=True), 2 * I, 2 if act == "silu" else 3, None, wm)
+    gu = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    f = torch.nn.functional.silu if act == "silu" else (lambda t: torch.nn.functional.gelu(t, approximate="tanh"))
+    want = f(gu[:, :I]) * gu[:, I:]
+    torch.testing.assert_close(out.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
+
+
+def test_packed_rejects_bad_shapes():
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x, w = _rnd(g, 64, 320), _rnd(g, 128, 320)
+    out = torch.empty(64, 128, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):  # K % 256
+        torch.ops.hipserve.prefill_gemm_packed(out, x, torch.empty(128 * 320, device=DEV, dtype=torch.bfloat16),
+                                               128, 0, None, 1)

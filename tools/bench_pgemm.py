@@ -64,9 +64,19 @@ def main():
         t_v1 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 1) for w in ws])
         t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 2) for w in ws])
         t_v5 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 5) for w in ws])
+        # the packed-layout kernel (prefill_gemm_packed.hip) on the decode copy of each weight
+        glu_pack = name == "gu"
+        wps = []
+        for w in ws:
+            wp = torch.empty(-(-N // 128) * 128 * K, device=dev, dtype=torch.bfloat16)
+            op.pack_decode_weight(wp, w, False)
+            wps.append(wp)
+        t_pw = {wm: time_fn(lambda: [op.prefill_gemm_packed(out, x, wp, N, 0, None, wm) for wp in wps]) for wm in (1, 2)}
         r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
              "pgemm_v1_ms": round(t_v1, 4), "pgemm_v5_ms": round(t_v5, 4),
-             "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1)}
+             "packed_wm1_ms": round(t_pw[1], 4), "packed_wm2_ms": round(t_pw[2], 4),
+             "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1),
+             "packed_TFs": round(2 * M * N * K / min(t_pw.values()) / 1e9, 1)}
         if a.fp8:
             from hipserve.ops import pgemm, quant as Q
 
@@ -103,6 +113,10 @@ def main():
                     ops.silu_and_mul(act, F.linear(x, w))
             r["blas_unit_ms"] = round(time_fn(blas_glu), 4)
             r["pgemm_unit_ms"] = round(time_fn(lambda: [op.prefill_gemm(act, x, p, 2) for p in wg]), 4)
+            for w, wp in zip(ws, wps):
+                op.pack_decode_weight(wp, w, True)
+            r["packed_unit_ms"] = {wm: round(time_fn(lambda: [op.prefill_gemm_packed(act, x, wp, N, 2, None, wm)
+                                                              for wp in wps]), 4) for wm in (1, 2)}
         if name in ("o", "down"):  # GEMM + residual add unit
             res = rnd(M, N)
 
@@ -111,17 +125,20 @@ def main():
                     res.add_(F.linear(x, w))
             r["blas_unit_ms"] = round(time_fn(blas_add), 4)
             r["pgemm_unit_ms"] = round(time_fn(lambda: [op.prefill_gemm(res, x, w, 1) for w in ws]), 4)
+            r["packed_unit_ms"] = {wm: round(time_fn(lambda: [op.prefill_gemm_packed(res, x, wp, N, 1, None, wm)
+                                                              for wp in wps]), 4) for wm in (1, 2)}
         rows.append(r)
         print(json.dumps(r), flush=True)
-        del ws, x, out
+        del ws, wps, x, out
         torch.cuda.empty_cache()
-    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | prefill_gemm ms (TF/s) | unit: hipBLASLt + ew | unit: fused "
-          f"| FP8 quant + GEMM ms (TF/s) |")
-    print("|---|---|---:|---:|---:|---:|---:|")
+    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | prefill_gemm ms (TF/s) | packed wm1 / wm2 ms (TF/s) "
+          f"| unit: hipBLASLt + ew | unit: fused | unit: packed | FP8 quant + GEMM ms (TF/s) |")
+    print("|---|---|---:|---:|---:|---:|---:|---:|---:|")
     for r in rows:
         f8 = f"{r['fp8_ms']} ({r['fp8_TFs']})" if "fp8_ms" in r else "—"
         print(f"| {r['shape']} | {r['M']}x{r['N']}x{r['K']} | {r['blas_ms']} ({r['blas_TFs']}) | "
-              f"{r['pgemm_ms']} ({r['pgemm_TFs']}) | {r.get('blas_unit_ms', '—')} | {r.get('pgemm_unit_ms', '—')} | {f8} |")
+              f"{r['pgemm_ms']} ({r['pgemm_TFs']}) | {r['packed_wm1_ms']} / {r['packed_wm2_ms']} ({r['packed_TFs']}) | "
+              f"{r.get('blas_unit_ms', '—')} | {r.get('pgemm_unit_ms', '—')} | {r.get('packed_unit_ms', '—')} | {f8} |")
 
 
 if __name__ == "__main__":

@@ -20,8 +20,15 @@ out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(3):
     F.linear(x, w)
 torch.cuda.synchronize()
-for v in (int(t) for t in os.environ.get("PG_VARIANTS", "2").split()):
+wp = None
+for v in os.environ.get("PG_VARIANTS", "2").split():
     for _ in range(3):
-        torch.ops.hipserve.prefill_gemm(out, x, w, 0, v)
+        if v.startswith("p"):  # packed-layout kernel (prefill_gemm_packed.hip), p1 / p2 = wm
+            if wp is None:
+                wp = torch.empty(-(-N // 128) * 128 * K, device="cuda", dtype=torch.bfloat16)
+                torch.ops.hipserve.pack_decode_weight(wp, w, False)
+            torch.ops.hipserve.prefill_gemm_packed(out, x, wp, N, 0, None, int(v[1:]))
+        else:
+            torch.ops.hipserve.prefill_gemm(out, x, w, 0, int(v))
     torch.cuda.synchronize()
 print("ok", M, N, K)
