@@ -46,15 +46,15 @@ namespace hipserve {
 
 constexpr int PW_T = 256;
 
-// workgroup -> (tm, tn): XCD-aware (consecutive ids on one XCD), then groups of PW_GM
-// m-tiles walked n-major inside, so the ~32 workgroups an XCD runs at once cover
-// 8 m-tiles x 4 n-tiles and share both operands in its L2
+// Persistent tile walk: G workgroups (one per CU), workgroup b takes tiles
+// L = it * G + r (r = b remapped so an XCD's workgroups hold consecutive r), and a
+// logical tile L -> (tm, tn) walks groups of PW_GM m-tiles n-major: the ~32 workgroups an
+// XCD runs at once cover 8 m-tiles x 4 n-tiles and share both operands in its L2.
 constexpr int PW_GM = 8;
-HS_DEVICE void pw_tile(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
-  const int id = xcd_remap(bid, tiles_m * tiles_n);
-  const int grp = id / (PW_GM * tiles_n), first = grp * PW_GM;
+HS_DEVICE void pw_tile(int L, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int grp = L / (PW_GM * tiles_n), first = grp * PW_GM;
   const int gsz = min(PW_GM, tiles_m - first);
-  const int r = id - first * tiles_n;
+  const int r = L - first * tiles_n;
   tm = first + r % gsz;
   tn = r / gsz;
 }
@@ -73,6 +73,29 @@ HS_DEVICE void pw_mfma(f32x4& acc, const u32x4& w, const u32x4& x) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(x));
 }
 
+// per-tile operand streams of one wave: its weight tile and the workgroup's X rows
+struct PwTile {
+  __amdgpu_buffer_rsrc_t w, x;
+  int m0, t;
+};
+
+template <int WM>
+HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned short* X, long ldx,
+                         const unsigned short* Wp, int M, int ntiles, int KS) {
+  constexpr int WN = 4 / WM, BM = 128 * WM;
+  int tm, tn;
+  pw_tile(L, tiles_m, tiles_n, tm, tn);
+  PwTile T;
+  T.m0 = tm * BM;
+  T.t = tn * WN + wn;
+  const int tl = min(T.t, ntiles - 1);  // waves past the last weight tile compute a copy, store nothing
+  T.w = __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + (long)tl * KS * 32768), 0, KS * 65536, 0x00020000);
+  // rows >= M fall outside the buffer range and read as zero
+  T.x = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long)T.m0 * ldx), 0,
+                                          (int)((long)min(BM, M - T.m0) * ldx * 2), 0x00020000);
+  return T;
+}
+
 template <int WM, int EPI>
 __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
     const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
@@ -83,27 +106,26 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  int tm, tn;
-  pw_tile(blockIdx.x, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * BM;
   const int ntiles = (N + 127) >> 7;
-  const int t = tn * WN + wn;           // this wave's packed weight tile
-  const int tl = min(t, ntiles - 1);    // waves past the last tile compute a copy, store nothing
   const int KS = K >> 8, nq = K >> 5, nst = K >> 6;
+  const int total = tiles_m * tiles_n, G = gridDim.x;
+  const int r = xcd_remap(blockIdx.x, G);
+  if (r >= total) return;
 
-  // this wave's weight stream: tile tl, 64 KiB per 256-deep K step
-  const __amdgpu_buffer_rsrc_t wrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + (long)tl * KS * 32768), 0, KS * 65536, 0x00020000);
+  // cur: the tile whose MFMAs run; nxt: the one the loads past cur's end stream in, so
+  // the pipeline runs on across the tile boundary (only the epilogue sits between)
+  PwTile cur = pw_make<WM>(r, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS);
+  PwTile nxt = r + G < total ? pw_make<WM>(r + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS) : cur;
+
   const int wvo = lane * 16;
-  auto wload = [&](int q, int rg) -> u32x4 {  // 32-deep slot q (clamped), row group rg
-    q = min(q, nq - 1);
-    return __builtin_amdgcn_raw_buffer_load_b128(wrs, wvo, (q >> 3) * 65536 + rg * 8192 + (q & 7) * 1024, 0);
+  auto wload = [&](int q, int rg) -> u32x4 {  // 32-deep slot q of cur (q >= nq: of nxt), row group rg
+    const bool n = q >= nq;
+    q = n ? q - nq : q;
+    return __builtin_amdgcn_raw_buffer_load_b128(n ? nxt.w : cur.w, wvo, (q >> 3) * 65536 + rg * 8192 + (q & 7) * 1024,
+                                                 0);
   };
   // X staging: thread -> rows 32 p + (tid >> 3), 16-byte chunk tid & 7 of the 128-byte
-  // (64-deep) row; rows >= M fall outside the buffer range and read as zero
-  const int rows = min(BM, M - m0);
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(X + (long)m0 * ldx), 0, (int)((long)rows * ldx * 2), 0x00020000);
+  // (64-deep) row
   int xvo[XP];
 #pragma unroll
   for (int p = 0; p < XP; ++p) xvo[p] = (p * 32 + (tid >> 3)) * (int)ldx * 2 + (tid & 7) * 16;
@@ -113,10 +135,12 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   // r and r + 32 p
   const int xdo = (tid >> 3) * 128 + (((tid & 7) ^ ((tid >> 4) & 7)) * 16);
   u32x4 xst[XP];
-  auto xload = [&](int st) {
-    st = min(st, nst - 1);
+  auto xload = [&](int st) {  // 64-deep stage st of cur (st >= nst: of nxt)
+    const bool n = st >= nst;
+    st = n ? st - nst : st;
 #pragma unroll
-    for (int p = 0; p < XP; ++p) xst[p] = __builtin_amdgcn_raw_buffer_load_b128(xrs, xvo[p], st * 128, 0);
+    for (int p = 0; p < XP; ++p)
+      xst[p] = __builtin_amdgcn_raw_buffer_load_b128(n ? nxt.x : cur.x, xvo[p], st * 128, 0);
   };
   auto xstore = [&](int buf) {
 #pragma unroll
@@ -130,13 +154,10 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   };
 
   f32x4 acc[8][8];
-#pragma unroll
-  for (int rg = 0; rg < 8; ++rg)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[rg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   u32x4 wa[8], wb[8], xa[8], xb[8];
 
-  // prologue: stage 0 in LDS, stage 1 in registers, weight slots 0 and 1 in flight
+  // prologue (first tile only): stage 0 in LDS, stage 1 in registers, weight slots 0 and
+  // 1 in flight; later tiles find theirs loaded by the previous tile's last stages
   xload(0);
   xstore(0);
   xload(1);
@@ -148,93 +169,102 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 #pragma unroll
   for (int i = 0; i < 8; ++i) xa[i] = xfrag(0, 0, i);
 
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    // ---- slot 2 st
-#pragma unroll
-    for (int rg = 0; rg < 8; ++rg) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        pw_mfma(acc[rg][i], wa[rg], xa[i]);
-      wa[rg] = wload(2 * st + 2, rg);
-      xb[rg] = xfrag(buf, 1, rg);
-      if (rg == 2) xstore(buf ^ 1);  // stage st + 1 (loaded during slot 2 st - 2)
-      if (rg == 3) xload(st + 2);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    pw_barrier();  // stage st + 1 visible; every read of stage st - 1 long done
-    // ---- slot 2 st + 1
-#pragma unroll
-    for (int rg = 0; rg < 8; ++rg) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        pw_mfma(acc[rg][i], wb[rg], xb[i]);
-      wb[rg] = wload(2 * st + 3, rg);
-      xa[rg] = xfrag(buf ^ 1, 0, rg);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> VALU reads
-  if (t >= ntiles) return;
-  const int mb = m0 + wm * 128 + fr;
-  if constexpr (EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU) {
-    const int I = N >> 1;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mb + 16 * i;
-      if (m >= M) continue;
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int c = t * 64 + rg * 16 + 4 * fq;
-        unsigned short o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const unsigned short g = f32_to_bf16(acc[rg][i][j]), u = f32_to_bf16(acc[rg + 4][i][j]);
-          o[j] = EPI == PW_EPI_GEGLU ? gelu_mul1(g, u) : silu_mul1(g, u);
-        }
-        if (c < I)
-          *reinterpret_cast<uint2*>(C + (long)m * ldc + c) =
-              uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
-      }
-    }
-  } else {
-    float bv[8][4];
+  for (int L = r;;) {
 #pragma unroll
     for (int rg = 0; rg < 8; ++rg)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = t * 128 + rg * 16 + 4 * fq + j;
-        bv[rg][j] = (bias != nullptr && n < N) ? bf16_to_f32(bias[n]) : 0.f;
-      }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mb + 16 * i;
-      if (m >= M) continue;
+      for (int i = 0; i < 8; ++i) acc[rg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int st = 0; st < nst; ++st) {
+      const int buf = st & 1;  // nst is even: a tile starts in buffer 0
+      // ---- slot 2 st
 #pragma unroll
       for (int rg = 0; rg < 8; ++rg) {
-        const int n = t * 128 + rg * 16 + 4 * fq;
-        if (n >= N) continue;
-        uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n);
-        float o[4];
-        if constexpr (EPI == PW_EPI_ADD) {  // C is the residual: C = bf16(bf16(acc) + C)
-          const uint2 r = *dst;
-          const unsigned short rr[4] = {(unsigned short)(r.x & 0xffff), (unsigned short)(r.x >> 16),
-                                        (unsigned short)(r.y & 0xffff), (unsigned short)(r.y >> 16)};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[rg][i][j])) + bf16_to_f32(rr[j]);
-        } else {  // bias added to the fp32 accumulator, one rounding
+        for (int i = 0; i < 8; ++i) pw_mfma(acc[rg][i], wa[rg], xa[i]);
+        wa[rg] = wload(2 * st + 2, rg);
+        xb[rg] = xfrag(buf, 1, rg);
+        if (rg == 2) xstore(buf ^ 1);  // stage st + 1 (loaded during slot 2 st - 2)
+        if (rg == 3) xload(st + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pw_barrier();  // stage st + 1 visible; every read of stage st - 1 long done
+      // ---- slot 2 st + 1
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = acc[rg][i][j] + bv[rg][j];
-        }
-        *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+      for (int rg = 0; rg < 8; ++rg) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pw_mfma(acc[rg][i], wb[rg], xb[i]);
+        wb[rg] = wload(2 * st + 3, rg);
+        xa[rg] = xfrag(buf ^ 1, 0, rg);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> VALU reads
+    const int t = cur.t, mb = cur.m0 + wm * 128 + fr;
+    if (t < ntiles) {
+      if constexpr (EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU) {
+        const int I = N >> 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mb + 16 * i;
+          if (m >= M) continue;
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            const int c = t * 64 + rg * 16 + 4 * fq;
+            unsigned short o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const unsigned short g = f32_to_bf16(acc[rg][i][j]), u = f32_to_bf16(acc[rg + 4][i][j]);
+              o[j] = EPI == PW_EPI_GEGLU ? gelu_mul1(g, u) : silu_mul1(g, u);
+            }
+            if (c < I)
+              *reinterpret_cast<uint2*>(C + (long)m * ldc + c) =
+                  uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+          }
+        }
+      } else {
+        float bv[8][4];
+#pragma unroll
+        for (int rg = 0; rg < 8; ++rg)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = t * 128 + rg * 16 + 4 * fq + j;
+            bv[rg][j] = (bias != nullptr && n < N) ? bf16_to_f32(bias[n]) : 0.f;
+          }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mb + 16 * i;
+          if (m >= M) continue;
+#pragma unroll
+          for (int rg = 0; rg < 8; ++rg) {
+            const int n = t * 128 + rg * 16 + 4 * fq;
+            if (n >= N) continue;
+            uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n);
+            float o[4];
+            if constexpr (EPI == PW_EPI_ADD) {  // C is the residual: C = bf16(bf16(acc) + C)
+              const uint2 rv = *dst;
+              const unsigned short rr[4] = {(unsigned short)(rv.x & 0xffff), (unsigned short)(rv.x >> 16),
+                                            (unsigned short)(rv.y & 0xffff), (unsigned short)(rv.y >> 16)};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[rg][i][j])) + bf16_to_f32(rr[j]);
+            } else {  // bias added to the fp32 accumulator, one rounding
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] = acc[rg][i][j] + bv[rg][j];
+            }
+            *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+          }
+        }
+      }
+    }
+    L += G;
+    if (L >= total) break;
+    cur = nxt;
+    if (L + G < total) nxt = pw_make<WM>(L + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS);
   }
 }
 
 bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
-                                int K, const void* bias, int wm, hipStream_t s) {
+                                int K, const void* bias, int wm, int grid_req, hipStream_t s) {
   if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2)) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;
@@ -243,7 +273,15 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   if ((long)(K / 256) * 65536 >= (1L << 31) || (long)128 * wm * ldx * 2 >= (1L << 31)) return false;
   const int BM = 128 * wm, WN = 4 / wm;
   const int tiles_m = (M + BM - 1) / BM, tiles_n = ((N + 127) / 128 + WN - 1) / WN;
-  const dim3 grid(tiles_m * tiles_n);
+  // persistent: one workgroup per CU (grid <= 0) unless the caller asks for a grid
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  }
+  const int total = tiles_m * tiles_n;
+  const dim3 grid(min(total, grid_req > 0 ? grid_req : ncu));
   auto* x = static_cast<const unsigned short*>(X);
   auto* w = static_cast<const unsigned short*>(Wp);
   auto* c = static_cast<unsigned short*>(C);

@@ -696,7 +696,7 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
 // pack_decode_weight(w[N, K], glu) (flat, ceil(N/128)*128*K bf16). epi as prefill_gemm
 // (2 / 3 need the glu packing); bias (epi 0 only) bf16 [N] or None; wm 1 or 2.
 void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
-                         const c10::optional<at::Tensor>& bias, int64_t wm) {
+                         const c10::optional<at::Tensor>& bias, int64_t wm, int64_t grid) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(wp.is_contiguous(), "prefill_gemm_packed: packed weight must be contiguous");
   const int M = x.size(0), K = x.size(1);
@@ -712,7 +712,7 @@ void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor&
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_prefill_gemm_packed((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
-                                                   wp.data_ptr(), M, (int)N, K, bp, (int)wm, cur_stream()),
+                                                   wp.data_ptr(), M, (int)N, K, bp, (int)wm, (int)grid, cur_stream()),
               "prefill_gemm_packed: unsupported (glu needs N % 128, bias only with epi 0, 32-bit offsets)");
 }
 
@@ -1285,7 +1285,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
-  m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1) -> ()");
+  m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");

@@ -350,6 +350,11 @@ PRESETS: dict[str, ModelConfig] = {
                                num_kv_heads=2, head_dim=64, intermediate_size=1024,
                                vocab_size=1024, rope_theta=10000.0, max_position_embeddings=4096,
                                bos_token_id=1, eos_token_id=(2,)),
+    # long-context tests: Llama-3 head geometry (head_dim 128, GQA 4), 64K positions
+    "small-llama-long": ModelConfig(name="small-llama-long", hidden_size=1024, num_layers=2, num_heads=8,
+                                    num_kv_heads=2, head_dim=128, intermediate_size=2048,
+                                    vocab_size=2048, rope_theta=500000.0, max_position_embeddings=65536,
+                                    bos_token_id=1, eos_token_id=(2,)),
     "small-mixtral": ModelConfig(name="small-mixtral", architecture="mixtral", hidden_size=512,
                                  num_layers=2, num_heads=8, num_kv_heads=2, head_dim=64,
                                  intermediate_size=768, vocab_size=1024, rope_theta=1e6,

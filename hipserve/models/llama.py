@@ -298,27 +298,33 @@ class LlamaModel:
         self.allocate_random(seed=seed)  # norms, embeddings, lm_head, bf16 projections (replaced below)
         dev = self.device
 
-        def q8(w):  # -> (QuantPart or None, dequantised dense)
+        def q8(w, rowpar=False):  # -> (QuantPart or None, dequantised dense)
+            # per-output-channel scale over the WHOLE row: a row-parallel shard (o / down /
+            # expert w2 at TP > 1) takes the max over the ranks' K slices, so every TP
+            # degree quantises the same model as TP = 1 (a sharded checkpoint's scale)
             wf = w.float()
+            amax = wf.abs().amax(1, keepdim=True)
+            if rowpar and self.tp.world_size > 1:
+                amax = self.tp.max_(amax)
             if kind == "int8":
-                s = wf.abs().amax(1, keepdim=True).clamp_min(1e-12) / 127.0
+                s = amax.clamp_min(1e-12) / 127.0
                 qi = torch.round(wf / s).clamp(-127, 127)
                 dense = (qi * s).to(self.dtype)
                 ok = dev.type == "cuda" and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0
                 return (Q.QuantPart.from_int8((qi + 128).to(torch.uint8), s, None, dev) if ok else None), dense
-            s = wf.abs().amax(1, keepdim=True).clamp_min(1e-12) / 448.0
+            s = amax.clamp_min(1e-12) / 448.0
             q = (wf / s).to(torch.float8_e4m3fn)
             ok = dev.type == "cuda" and w.shape[0] % 16 == 0 and w.shape[1] % 256 == 0
             return (Q.QuantPart.from_fp8(q, s, dev) if ok else None), (q.float() * s).to(self.dtype)
 
-        def quant(w, splits):
-            parts = [q8(t) for t in torch.split(w, splits, 0)]
+        def quant(w, splits, rowpar=False):
+            parts = [q8(t, rowpar) for t in torch.split(w, splits, 0)]
             if all(p is not None for p, _ in parts):
                 return Q.QuantWeight([p for p, _ in parts])
             return torch.cat([d for _, d in parts])
 
-        def experts(w):
-            parts = [q8(w[e]) for e in range(w.shape[0])]
+        def experts(w, rowpar=False):
+            parts = [q8(w[e], rowpar) for e in range(w.shape[0])]
             if all(p is not None for p, _ in parts) and Q.QuantMoE.supported(parts[0][0].kqt, *w.shape[1:]):
                 return Q.QuantMoE([p for p, _ in parts])
             return torch.stack([d for _, d in parts])
@@ -326,12 +332,12 @@ class LlamaModel:
         D = self.D
         for lw in self.layers:
             lw.wqkv = quant(lw.wqkv, [self.nq * D, self.nkv * D, self.nkv * D])
-            lw.wo = quant(lw.wo, [lw.wo.shape[0]])
+            lw.wo = quant(lw.wo, [lw.wo.shape[0]], rowpar=True)
             if lw.wgu is not None:
                 lw.wgu = quant(lw.wgu, [self.inter, self.inter])
-                lw.wd = quant(lw.wd, [lw.wd.shape[0]])
+                lw.wd = quant(lw.wd, [lw.wd.shape[0]], rowpar=True)
             if lw.w13 is not None:
-                lw.w13, lw.w2 = experts(lw.w13), experts(lw.w2)
+                lw.w13, lw.w2 = experts(lw.w13), experts(lw.w2, rowpar=True)
         if dev.type == "cuda":
             torch.cuda.empty_cache()
         self.quant_linear = Q.quant_linear

@@ -311,6 +311,15 @@ class TPGroup:
         if self.world_size > 1:
             dist.barrier(group=self._cpu_group)
 
+    def max_(self, t: torch.Tensor) -> torch.Tensor:
+        """Element-wise maximum over ranks of a small tensor (CPU group: start-up use,
+        e.g. per-channel quantisation scales of row-parallel shards)."""
+        if self.world_size == 1:
+            return t
+        c = t.detach().float().cpu().contiguous()
+        dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self._cpu_group)
+        return c.to(device=t.device, dtype=t.dtype)
+
     def min_int(self, n: int) -> int:
         """Minimum of a host integer over ranks (CPU group: no device collective)."""
         if self.world_size == 1:

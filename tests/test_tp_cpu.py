@@ -25,10 +25,12 @@ def _port():
 
 
 def _cfg(ckpt, tp):
+    ckpt, _, quant = ckpt.partition(":")  # "tiny-llama:fp8": random-init 8-bit weights
     fmt = "safetensors" if os.path.isdir(ckpt) else "dummy"
     return EngineConfig(model=ckpt, load_format=fmt, device="cpu", dtype="float32",
                         tensor_parallel_size=tp, num_kv_blocks=128, max_model_len=256,
-                        max_num_batched_tokens=32, max_num_seqs=4)
+                        max_num_batched_tokens=32, max_num_seqs=4,
+                        extra={"quantization": quant} if quant else {})
 
 
 def _worker(rank, world, port, ckpt, q):
@@ -49,7 +51,7 @@ def _worker(rank, world, port, ckpt, q):
             eng.shutdown()
             q.put([r[0] for r in res])
         else:
-            runner = ModelRunner(cfg, resolve_model_config(ckpt), tp)
+            runner = ModelRunner(cfg, resolve_model_config(ckpt.partition(":")[0]), tp)
             worker_loop(runner, tp)
     finally:
         dist.destroy_process_group()
@@ -106,10 +108,12 @@ def test_tp_families_match_tp1(tmp_path, family):
     assert _run_tp(ckpt, 2) == want
 
 
-@pytest.mark.parametrize("preset,world", [("tiny-llama", 2), ("tiny-mixtral", 4)])
+@pytest.mark.parametrize("preset,world", [("tiny-llama", 2), ("tiny-mixtral", 4), ("tiny-llama:fp8", 2),
+                                          ("tiny-mixtral:int8", 2)])
 def test_dummy_weights_tp_invariant(preset, world):
     """On-device synthetic init (K16) is keyed by global coordinates: a TP=N engine
-    with --load-format dummy runs the same model as TP=1."""
+    with --load-format dummy runs the same model as TP=1 — also with 8-bit weights,
+    whose row-parallel per-channel scales are the max over the ranks' K slices."""
     from hipserve.engine.llm_engine import LLMEngine
     from hipserve.parallel.comm import TPGroup
 

@@ -41,9 +41,29 @@ def _port():
     return p
 
 
+def _split(shape):
+    """'moe:int8' -> ('moe', 'int8')"""
+    base, _, quant = shape.partition(":")
+    return base, quant or None
+
+
 def _model_cfg(shape="small"):
     from hipserve.config import PRESETS
 
+    shape, _ = _split(shape)
+    if shape == "moe":
+        # Mixtral-8x7B's MoE block at small shapes (8 experts, top-2, renormalised): the
+        # hf-models chart's Mixtral runs at TP=2 (deploy/charts/hf-models/values.yaml)
+        return PRESETS["mixtral-8x7b"].replace(name="mixtral-tp-test", num_layers=2, hidden_size=1024,
+                                               num_heads=8, num_kv_heads=2, intermediate_size=1024,
+                                               vocab_size=32000, max_position_embeddings=1024)
+    if shape == "qwen3moe":
+        # Qwen3-MoE features (the text model of the reference's Qwen3-VL-30B-A3B default,
+        # vllm-models/helm-chart/values.yaml:8-12): 16 experts top-4 renormalised, q/k norm
+        return PRESETS["qwen3-30b-a3b"].replace(name="qwen3moe-tp-test", num_layers=2, hidden_size=1024,
+                                                num_heads=8, num_kv_heads=2, moe_intermediate_size=512,
+                                                num_experts=16, num_experts_per_tok=4, vocab_size=32000,
+                                                max_position_embeddings=1024, eos_token_id=(2,))
     if shape == "70b":
         # Llama-3-70B layer shapes (hidden 8192, 64 q / 8 kv heads, FFN 28672): at TP=8
         # every rank holds ONE kv head and 8 q heads, as in the 70B TP=8 pod
@@ -64,10 +84,14 @@ def _model_cfg(shape="small"):
 def _engine_cfg(tp, exact, shape="small"):
     from hipserve.config import EngineConfig
 
-    name = {"70b": "llama-3-70b-tp-test", "gemma": "gemma-3-tp-test"}.get(shape, "llama-3-tp-test")
+    base, quant = _split(shape)
+    name = _model_cfg(shape).name
+    extra = {"tp_exact_reduce": exact}
+    if quant:  # random-init 8-bit weights kept native (FP8 e4m3 / INT8 weight-only, per-channel scales)
+        extra["quantization"] = quant
     return EngineConfig(model=name, load_format="dummy", device="cuda", max_num_seqs=8,
                         max_num_batched_tokens=256, max_model_len=640, num_kv_blocks=512,
-                        tensor_parallel_size=tp, extra={"tp_exact_reduce": exact})
+                        tensor_parallel_size=tp, extra=extra)
 
 
 def _generate(eng, prompts, n, top2=False):
@@ -100,27 +124,54 @@ def _fp32_logprobs(model, ids):
 
     from hipserve.ops import reference as R
 
+    from hipserve.ops import quant as Q
+
+    def dense(w):  # fp32 copy of a bf16 / quantised (dequantised exactly) weight
+        if isinstance(w, torch.Tensor):
+            return w.float()
+        if isinstance(w, Q.QuantMoE):
+            return w.dequantize().float()
+        return Q.dequantize(w).float()
+
     cfg = model.cfg
     D, nq, nkv = model.D, cfg.num_heads, cfg.num_kv_heads
+    eps = cfg.rms_norm_eps
     idt = torch.tensor(ids, device=model.embed.device)
     x = model.embed[idt].float()
     T = len(ids)
     pos = torch.arange(T, device=x.device)
     mask = torch.triu(torch.ones(T, T, dtype=torch.bool, device=x.device), 1)
     for lw in model.layers:
-        h = R.rmsnorm(x, lw.ln1, cfg.rms_norm_eps)
-        qkv = h @ lw.wqkv.float().T
-        q = R.apply_rope(qkv[:, :nq * D].view(T, nq, D), pos, model.cos_sin, cfg.rope_mode)
-        k = R.apply_rope(qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D), pos, model.cos_sin, cfg.rope_mode)
+        h = R.rmsnorm(x, lw.ln1, eps)
+        qkv = h @ dense(lw.wqkv).T
+        q, k = qkv[:, :nq * D].view(T, nq, D), qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
+        if lw.q_norm is not None:  # Qwen3: per-head RMSNorm of q and k before RoPE
+            q, k = R.rmsnorm(q, lw.q_norm, eps), R.rmsnorm(k, lw.k_norm, eps)
+        q = R.apply_rope(q, pos, model.cos_sin, cfg.rope_mode)
+        k = R.apply_rope(k, pos, model.cos_sin, cfg.rope_mode)
         v = qkv[:, (nq + nkv) * D:].view(T, nkv, D)
         k, v = k.repeat_interleave(nq // nkv, 1), v.repeat_interleave(nq // nkv, 1)
         sc = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(D)
         o = torch.einsum("hqk,khd->qhd", torch.softmax(sc.masked_fill(mask, float("-inf")), -1), v)
-        x = x + o.reshape(T, nq * D) @ lw.wo.float().T
-        h = R.rmsnorm(x, lw.ln2, cfg.rms_norm_eps)
-        gu = h @ lw.wgu.float().T
+        x = x + o.reshape(T, nq * D) @ dense(lw.wo).T
+        h = R.rmsnorm(x, lw.ln2, eps)
+        if lw.router is not None:  # MoE: softmax top-k routing (renormalised), SiLU-GLU experts
+            pr, idx = torch.topk(torch.softmax(h @ lw.router.float().T, -1), cfg.num_experts_per_tok, -1)
+            if cfg.norm_topk_prob:
+                pr = pr / pr.sum(-1, keepdim=True)
+            w13, w2 = dense(lw.w13), dense(lw.w2)
+            inter = w13.shape[1] // 2
+            y = torch.zeros_like(x)
+            for e in range(w13.shape[0]):
+                tok, slot = (idx == e).nonzero(as_tuple=True)
+                if tok.numel():
+                    gu = h[tok] @ w13[e].T
+                    y.index_add_(0, tok, ((F.silu(gu[:, :inter]) * gu[:, inter:]) @ w2[e].T) * pr[tok, slot, None])
+            x = x + y
+            continue
+        gu = h @ dense(lw.wgu).T
         inter = gu.shape[1] // 2
-        x = x + (F.silu(gu[:, :inter]) * gu[:, inter:]) @ lw.wd.float().T
+        x = x + (F.silu(gu[:, :inter]) * gu[:, inter:]) @ dense(lw.wd).T
     x = R.rmsnorm(x, model.norm, cfg.rms_norm_eps)
     return torch.log_softmax(x @ model.lm_head[:cfg.vocab_size].float().T, -1)
 
@@ -199,7 +250,7 @@ def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK):
                         break
                     g = _generate(eng, [p + want[i][:j0]], n_tok - j0)[0][0]
             info["ties"] = ties
-            if exact:
+            if _split(shape)[0] != "gemma":  # the fp32 oracle covers Llama / MoE / Qwen3 / 8-bit weights
                 info["logit"] = _logit_bound(eng, ref.runner.model, prompts, want, top2, N_BOUND)
             info["car_failed"] = tp.custom_ar.failed() if tp.custom_ar else None
             eng.shutdown()
@@ -241,26 +292,53 @@ def _run_tp(world, exact, shape="small", n_tok=N_TOK, timeout=140):
 TIE = 0.05  # nats between TP=1's choice and TP=2's
 
 
+def _check_ties(info, tie=0.05):
+    print("exact prefix per prompt:", info["exact_prefix"], "divergences:", len(info["ties"]))
+    assert len(info["ties"]) <= N_TOK * len(PROMPTS) // 10, info["ties"]
+    for i, j, t1, t2, lp1, lp2 in info["ties"]:
+        assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=N token {t2} not in TP=1's top-5"
+        assert lp1 - lp2 <= tie, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
+
+
 @pytest.mark.parametrize("exact", [True, False])
 def test_tp2_shared_gpu_matches_tp1(exact):
     _, info = _run_tp(2, exact)
     assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
     assert info["car_failed"] is False
-    print("exact prefix per prompt:", info["exact_prefix"], "divergences:", len(info["ties"]))
-    assert len(info["ties"]) <= N_TOK * len(PROMPTS) // 10, info["ties"]
-    for i, j, t1, t2, lp1, lp2 in info["ties"]:
-        assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=2 token {t2} not in TP=1's top-5"
-        assert lp1 - lp2 <= TIE, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
-    if exact:
-        _check_bound(info["logit"])
+    _check_ties(info)
+    _check_bound(info["logit"], exact)
 
 
-def _check_bound(lb):
-    """under exact reduction, max |log-softmax(TP=N) - log-softmax(TP=1)|
-    over the prefill + 32 decode steps <= 2x TP=1's own deviation from fp32."""
+# The logit bound: max |log-softmax(TP=N) - log-softmax(TP=1)| over the
+# prefill + 32 decode steps of every prompt vs TP=1's own largest deviation from an fp32
+# forward of the same weights. Exact reduction (fp32 exchange): <= 2x (each engine's error
+# to fp32 is its own bf16 rounding, sharding may reorder but not add to it). Default
+# bf16 exchange of prefill-sized messages: <= 3x (one extra bf16 rounding of each rank's
+# partial sum before the cross-rank add, an error of the same order as the output's own).
+BOUND_FACTOR = {True: 2.0, False: 3.0}
+
+
+def _check_bound(lb, exact=True):
     print("logit bound:", lb)
     assert 0 < lb["tp1_vs_fp32"] < 1.0, lb  # the fp32 oracle itself agrees with TP=1
-    assert lb["tpn_vs_tp1"] <= lb["bound"], lb
+    assert lb["tpn_vs_tp1"] <= BOUND_FACTOR[exact] / 2.0 * lb["bound"], lb
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("shape", ["moe", "small:fp8", "qwen3moe:int8", "moe:fp8"])
+def test_tp2_quant_and_moe_shared_gpu_matches_tp1(shape):
+    """The reference's TP=2 deployments (vllm-models/helm-chart/values.yaml:3-12;
+    templates/model-deployments.yaml:37-38): FP8 weights (Gemma-3-27B-FP8-Dynamic), 8-bit
+    integer MoE experts (Qwen3-VL-30B-A3B AWQ-8bit) and the chart's Mixtral, as two ranks
+    sharing cuda:0 in the default (bf16 prefill exchange) mode: near-ties only, and the
+    stated logit bound against the fp32 oracle of the same (dequantised) weights. Every
+    TP degree quantises the same model (row-parallel scales are the max over the ranks'
+    K slices)."""
+    _, info = _run_tp(2, False, shape=shape, timeout=280)
+    assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
+    assert info["car_failed"] is False
+    _check_ties(info)
+    _check_bound(info["logit"], False)
 
 
 N_TOK_70B = 64
@@ -304,8 +382,4 @@ def test_tp2_gemma3_shared_gpu_matches_tp1():
     assert info["fused_family"], info
     assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
     assert info["car_failed"] is False
-    print("exact prefix per prompt:", info["exact_prefix"], "divergences:", len(info["ties"]))
-    assert len(info["ties"]) <= N_TOK * len(PROMPTS) // 10, info["ties"]
-    for i, j, t1, t2, lp1, lp2 in info["ties"]:
-        assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=2 token {t2} not in TP=1's top-5"
-        assert lp1 - lp2 <= TIE, f"prompt {i} pos {j}: TP=1 margin {lp1 - lp2:.4f} is not a near-tie"
+    _check_ties(info)
