@@ -407,6 +407,8 @@ def run_phase(args):
         },
         "engine_init_s": round(init_s, 1),
         "init_breakdown_s": getattr(engine.runner, "init_times", {}),
+        "single_weight_layout": getattr(engine.runner, "single_layout", None),
+        "packed_prefill_timing": getattr(engine.runner, "packed_prefill_report", None),
         "kv_blocks": engine.runner.num_blocks,
     }
     if ol_summary:  # open loop: TTFT tail and inter-token latency of every request

@@ -209,9 +209,13 @@ HS_DEVICE int kbase(int g, int s) {
 // placed at bit kSub of an f16 (q << kSub < 1024: a subnormal, exactly q 2^(kSub-24)),
 // and ONE v_pk_fma per pair computes q * (d 2^(24-kSub)) + c, where c holds the
 // format's zero point (-8 d, -32 d, -128 d) or the K-quant min. Every factor is a
-// power-of-two multiple of the f16-rounded scale, so the weights are bit-identical to
-// the magic-number path (1024 + q, v_pk_add -1024, v_pk_fma) at 2 instead of 3 ops per
-// pair word and no v_pk_add. Range: d 2^(24-kSub) must stay below 65504 —
+// power-of-two multiple of the f16-rounded scale, so for scales in the f16 normal range
+// the weights are bit-identical to the magic-number path (1024 + q, v_pk_add -1024,
+// v_pk_fma) at 2 instead of 3 ops per pair word and no v_pk_add. NOT bit-identical when
+// a block's d sc is itself f16-subnormal (< 2^-14 ~ 6.1e-5): there d sc 2^(24-kSub) is a
+// normal f16 that keeps more mantissa bits than the magic path's subnormal scale, so v2
+// is the closer of the two to the fp32 block decoder (tests/test_gguf_gpu.py
+// test_mfma_v2_tiny_scales). Range: d 2^(24-kSub) must stay below 65504 —
 // ops/quant.py sub_scale_ok() checks every block's scale at load (Q4_K / Q4_0 / Q4_1
 // d sc < 0.25, Q5_K < 0.125, Q6_K < 0.0625, Q8_0 < 0.0156) and sends weights beyond
 // it to the v1 kernel.

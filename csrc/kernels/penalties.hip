@@ -170,7 +170,8 @@ __global__ __launch_bounds__(kTopT) void top_logprobs_kernel(const T* __restrict
   const unsigned int n_above = s_sel[1];
   // every key in the selected bin is a candidate (the bin rounds fp32 logits to bf16,
   // so the true n-th largest may sit anywhere in it) while they fit the 64 slots;
-  // past that the lowest-index ones
+  // past that the lowest-index ones — the one documented bound on exactness (more than
+  // 64 logits within one bf16 ulp of the n-th largest; hipserve/ops/reference.py)
   const int take_ties = 64 - (int)n_above;
   // 3. collect: every key > kth, then the lowest-index ties (contiguous chunks per
   //    thread + a block scan give each tie its global index rank)

@@ -77,6 +77,9 @@ def pad_table(times: dict, tol: float = 1.03) -> dict:
     return {m: p for m, p in pad.items() if p > m}
 
 
+_PACKED_TIMING: dict = {}  # (prefill units, rows) -> packed vs hipBLASLt timing (ops/pgemm.py tune_packed)
+
+
 class ModelRunner:
     def __init__(self, ecfg: EngineConfig, mcfg: ModelConfig, tp: TPGroup, device=None):
         self.ecfg = ecfg
@@ -136,8 +139,14 @@ class ModelRunner:
                                                           os.environ.get("HIPSERVE_FUSED_DECODE", "1") != "0"))
             fused = self.model.fused_gemm_shapes() if self.model.fused_decode else {}
             self.gemm_report = gemm.TUNER.tune(self.model.gemm_shapes(), self.device, ms, fused=fused)
+            self.single_layout = None
             if ecfg.extra.get("packed_decode", True):
-                self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
+                why = self._single_layout_reason()
+                if why:  # ONE resident copy per dense weight, in the packed layout
+                    n, freed = self.model.to_single_layout()
+                    self.single_layout = {"reason": why, "weights": n, "row_major_gb_freed": round(freed / 2**30, 2)}
+                else:
+                    self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
             moes = self.model.quant_moes() if hasattr(self.model, "quant_moes") else []
             if moes and ecfg.extra.get("quant_dense_shadow", True):  # bf16 experts for prefill
                 from ..ops import quant as Q
@@ -247,6 +256,43 @@ class ModelRunner:
         else:
             raise ValueError(f"unknown load_format {fmt}")
         self.load_format = fmt
+
+    def _single_layout_reason(self) -> str | None:
+        """Whether the dense projections keep ONLY their packed copy (``gemm.PackedLinear``).
+        HIPSERVE_SINGLE_LAYOUT=1 forces it, 0 keeps row-major + packed copies; ``auto``
+        (default): single when the two copies would not leave 24 GiB + a quarter of HBM
+        for the KV cache (e.g. Llama-3-70B on one MI355X), or when the packed prefill GEMM
+        times at least as fast as hipBLASLt on this model's prefill units."""
+        mode = os.environ.get("HIPSERVE_SINGLE_LAYOUT", self.ecfg.extra.get("single_layout", "auto"))
+        m = self.model
+        if str(mode) == "0" or not hasattr(m, "single_layout_ok") or not m.single_layout_ok():
+            return None
+        if str(mode) == "1":
+            return "forced"
+        from ..ops import gemm, pgemm
+
+        lw = m.layers[0]
+        ws = [w for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd) if isinstance(w, torch.Tensor)]
+        per_layer = sum(w.numel() * w.element_size() for w in ws if gemm.packable(*w.shape))
+        need = per_layer * len(m.layers)
+        free, total = torch.cuda.mem_get_info(self.device)
+        if free - need < (24 << 30) + total // 4:
+            return "memory"
+        units = []
+        for kind, w in (("plain", lw.wqkv), ("add", lw.wo), ("glu", lw.wgu), ("add", lw.wd)):
+            if isinstance(w, torch.Tensor) and gemm.packable(*w.shape) and (kind != "glu" or w.shape[0] % 128 == 0):
+                units.append((kind, w.shape[0], w.shape[1]))
+        M = self.ecfg.max_num_batched_tokens
+        # TP: the o / down epilogue is the cross-rank norm; small token budgets: prefill
+        # GEMMs are not the bottleneck (and every engine of a test process decides alike)
+        if not units or self.tp.world_size > 1 or M < 2048:
+            return None
+        key = (tuple(units), M)
+        r = _PACKED_TIMING.get(key)
+        if r is None:  # one timing per shape set and process: engines in one process agree
+            r = _PACKED_TIMING[key] = pgemm.tune_packed(units, M, self.device, self.ops)
+        self.packed_prefill_report = r
+        return "prefill timing" if r["packed_ms"] <= r["blas_ms"] else None
 
     def _num_kv_blocks(self) -> int:
         if self.ecfg.num_kv_blocks:

@@ -349,7 +349,7 @@ class LlamaModel:
 
     # ---------------------------------------------------------------- forward
     def linear(self, x: torch.Tensor, w, name: str | None = None) -> torch.Tensor:
-        if isinstance(w, torch.Tensor):
+        if isinstance(w, (torch.Tensor, gemm.PackedLinear)):
             return gemm.linear(x, w)
         return self.quant_linear(x, w)
 
@@ -358,9 +358,10 @@ class LlamaModel:
         out = set()
         for lw in self.layers[:1]:
             for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.router):  # + the MoE router [E, H] (E % 16 == 0)
-                if isinstance(w, torch.Tensor) and w.dim() == 2 and (w is not lw.router or w.shape[0] % 16 == 0):
+                if (isinstance(w, (torch.Tensor, gemm.PackedLinear)) and w.dim() == 2
+                        and (w is not lw.router or w.shape[0] % 16 == 0)):
                     out.add(tuple(w.shape))
-        if isinstance(self.lm_head, torch.Tensor):
+        if isinstance(self.lm_head, (torch.Tensor, gemm.PackedLinear)):
             out.add(tuple(self.lm_head.shape))
         return sorted(out)
 
@@ -401,6 +402,51 @@ class LlamaModel:
             n += w.numel() * w.element_size()
         return n + self.pack_moe_weights()
 
+    def single_layout_ok(self) -> bool:
+        """Families whose dense projections can live ONLY in the packed layout
+        (``gemm.PackedLinear``): the fused decode path and the packed prefill GEMM cover
+        every use — bf16 weights, SiLU-GLU (or MoE) MLPs, HIP ops, no exact-fp32 TP
+        reduction (whose prefill GEMMs write fp32)."""
+        return (getattr(self.ops, "name", "") == "hip" and self.fused_decode and self.fused_family
+                and self.cfg.hidden_act == "silu" and not self.tp.exact_reduce and self.dtype == torch.bfloat16
+                and hasattr(torch.ops.hipserve, "prefill_gemm_packed"))
+
+    def to_single_layout(self) -> tuple[int, int]:
+        """Replace every dense projection (qkv, o, gate|up, down, an untied lm_head) by its
+        packed copy (``gemm.PackedLinear``; gate|up GLU-interleaved) and drop the
+        row-major original: ONE resident copy per weight. One
+        weight at a time, so the peak is the model plus one projection. Returns (weights
+        converted, bytes freed)."""
+        n = freed = 0
+
+        def conv(w, glu=False):
+            nonlocal n, freed
+            if not (isinstance(w, torch.Tensor) and w.dim() == 2 and w.dtype == torch.bfloat16
+                    and gemm.packable(*w.shape) and (not glu or w.shape[0] % 128 == 0)):
+                return w
+            wp = (gemm.glu_of(w) if glu else gemm.packed_of(w))
+            if wp is None:
+                wp = gemm.pack(w, glu=glu)
+            # the registries are keyed by the plain tensor, which goes away now (other
+            # engines in this process keep their entries)
+            gemm.PACKED.pop(w.data_ptr(), None)
+            gemm.PACKED_GLU.pop(w.data_ptr(), None)
+            n += 1
+            freed += w.numel() * w.element_size()
+            return gemm.PackedLinear(wp, w.shape[0], w.shape[1], glu=glu)
+
+        for lw in self.layers:
+            lw.wqkv = conv(lw.wqkv)
+            lw.wo = conv(lw.wo)
+            if lw.wgu is not None:
+                lw.wgu = conv(lw.wgu, glu=True)
+                lw.wd = conv(lw.wd)
+        if self.lm_head is not self.embed:
+            self.lm_head = conv(self.lm_head)
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        return n, freed
+
     def pack_moe_weights(self) -> int:
         """Per-expert packed copies of the MoE weights for the decode expert GEMM
         (``moe_hip``): w13 gate/up-interleaved (SiLU-GLU in the GEMM epilogue), w2
@@ -439,13 +485,14 @@ class LlamaModel:
             return {}
         lw = self.layers[0]
         out = {}
-        if isinstance(lw.wo, torch.Tensor):
+        dense = (torch.Tensor, gemm.PackedLinear)
+        if isinstance(lw.wo, dense):
             out[tuple(lw.wo.shape)] = ("norm",)
-        if isinstance(lw.wd, torch.Tensor):
+        if isinstance(lw.wd, dense):
             out[tuple(lw.wd.shape)] = ("norm",)
-        if isinstance(lw.wqkv, torch.Tensor):
+        if isinstance(lw.wqkv, dense):
             out[tuple(lw.wqkv.shape)] = ("rope", self.nq, self.nkv, self.D, self.cfg.rope_mode)
-        if isinstance(lw.wgu, torch.Tensor) and lw.wgu.shape[0] % 128 == 0 and self.cfg.hidden_act == "silu":
+        if isinstance(lw.wgu, dense) and lw.wgu.shape[0] % 128 == 0 and self.cfg.hidden_act == "silu":
             out[tuple(lw.wgu.shape)] = ("glu",)  # GeGLU: plain partials + splitk_glu (tuned as a plain GEMM)
         return out
 
@@ -588,7 +635,10 @@ class LlamaModel:
                 ops.paged_decode(attn[Tp:Tp + Td], qkv[Tp:Tp + Td], kc, vc, meta.bt_decode, meta.ctx_decode,
                                  tmp_out, tmp_ml, nq, nkv, part, self.scale, win)
             x8 = self._x8p(xn, lw.wgu, glu=True)
-            if tp1 and lw.post_attn_norm is None and pgemm.use("add", lw.wo, T):
+            if tp1 and lw.post_attn_norm is None and isinstance(lw.wo, gemm.PackedLinear) and T > 64:
+                gemm.packed_prefill(attn, lw.wo, 1, out=residual)  # residual += o_proj(attn), packed layout
+                ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
+            elif tp1 and lw.post_attn_norm is None and pgemm.use("add", lw.wo, T):
                 pgemm.gemm_add_(residual, attn, lw.wo)  # residual += o_proj(attn), in the GEMM epilogue
                 ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
             else:
@@ -611,6 +661,8 @@ class LlamaModel:
                         act8 = pgemm.f8_glu_q8(xn, lw.wgu, gelu, x8)
                     if act8 is None:  # GLU in the e4m3 GEMM's epilogue
                         act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2, x8=x8)
+                elif isinstance(lw.wgu, gemm.PackedLinear) and lw.wgu.glu:  # GLU in the packed GEMM's epilogue
+                    act = gemm.packed_glu(xn, lw.wgu, gelu)
                 elif cfg.hidden_act in ("silu", "gelu_tanh") and pgemm.use("glu", lw.wgu, T):
                     act = pgemm.gemm_glu(xn, lw.wgu, gelu)
                 if act8 is not None:
@@ -620,8 +672,12 @@ class LlamaModel:
                     act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                     self.act_and_mul(act, gu)
                 if act8 is None and (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
-                                     and pgemm.use("add", lw.wd, T)):
-                    pgemm.gemm_add_(residual, act, lw.wd)
+                                     and (pgemm.use("add", lw.wd, T)
+                                          or (isinstance(lw.wd, gemm.PackedLinear) and T > 64))):
+                    if isinstance(lw.wd, gemm.PackedLinear):
+                        gemm.packed_prefill(act, lw.wd, 1, out=residual)
+                    else:
+                        pgemm.gemm_add_(residual, act, lw.wd)
                     ops.rmsnorm(xn, residual, nxt, eps, out8=x8n)
                     x8 = x8n
                     continue
@@ -862,7 +918,7 @@ class LlamaModel:
         epilogue: the tuned bf16 decode GEMM, or the GGUF MFMA GEMM for a
         ``QuantWeight`` (``x16``: the producer's f16 copy of x, see ``_x16``); None
         when the projection runs unfused (hipBLASLt choice)."""
-        if isinstance(w, torch.Tensor):
+        if isinstance(w, (torch.Tensor, gemm.PackedLinear)):
             fc = gemm.fused_choice(x.shape[0], w)
             return gemm.gemm_partial(x, w, fc) if fc is not None else None
         from ..ops import quant as Q

@@ -41,6 +41,9 @@ TUNE_MS = [1, 2, 4, 8, 16, 24, 32, 48, 64]
 class GemmTuner:
     def __init__(self):
         self.table: dict[tuple, object] = {}
+        # best packed-layout decode GEMM per (M, N, K), whatever won overall: the choice
+        # for weights kept only in the packed layout (PackedLinear)
+        self.best_packed: dict[tuple, tuple] = {}
         self.report: list[dict] = []
 
     def packed_shapes(self) -> set:
@@ -54,6 +57,23 @@ class GemmTuner:
             if m >= M:
                 return self.table.get((m, N, K), "blas")
         return "blas"
+
+    def choose_packed(self, M: int, N: int, K: int) -> tuple:
+        """The decode GEMM config for a packed-only weight at M <= 64: the overall winner
+        when it is a packed config, else the fastest packed config timed for that M
+        bucket (a split-K default when the shape was never tuned)."""
+        for m in TUNE_MS:
+            if m >= M:
+                c = self.table.get((m, N, K))
+                if isinstance(c, tuple) and c[0] == "dgp":
+                    return c
+                bp = self.best_packed.get((m, N, K))
+                if bp is not None:
+                    return bp[0]
+                break
+        ks = K // 256
+        S = next((s for s in (8, 4, 2, 1) if ks % s == 0 and (ks // s) in DG_STEPS and -(-N // 128) * s >= 64), 1)
+        return ("dgp", 1, S)
 
     @staticmethod
     def _time(fn, n=16, reps=5):
@@ -118,6 +138,10 @@ class GemmTuner:
                     else:
                         fn = (lambda i: run_choice(cfg, out, x, ws_[i % ncopy], wp_[i % ncopy] if wp_ else None))
                     t = self._time(fn, n=n)
+                    if cfg[0] == "dgp":
+                        bp = self.best_packed.get((M, N, K))
+                        if bp is None or t < bp[1]:
+                            self.best_packed[(M, N, K)] = (cfg, t)
                     if t < best_t * 0.97:
                         best, best_t = cfg, t
                 self.table[(M, N, K)] = best
@@ -247,6 +271,53 @@ def pack(w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     return out
 
 
+class PackedLinear:
+    """A dense bf16 projection kept ONLY in the packed layout of ``pack_decode_weight``
+    (one weight layout for prefill and decode, no second resident copy).
+    The decode GEMMs (``decode_gemm_packed`` / ``decode_gemm_glu`` / the split-K partial
+    kernels) and the packed prefill GEMM (csrc/kernels/prefill_gemm_packed.hip) read it
+    directly. ``glu``: a merged [gate; up] weight packed gate/up-interleaved per 128-row
+    tile (the GLU epilogues pair gate and up in registers). ``unpack()`` rebuilds the
+    row-major [N, K] matrix (tests, fp32 oracles, rare fallbacks) — never on a hot path."""
+
+    def __init__(self, wp: torch.Tensor, N: int, K: int, glu: bool = False):
+        self.wp, self.N, self.K, self.glu = wp, N, K, glu
+        self.shape = (N, K)
+        self.dtype, self.device = wp.dtype, wp.device
+        self.is_cuda = wp.is_cuda
+
+    def dim(self) -> int:
+        return 2
+
+    def numel(self) -> int:
+        return self.N * self.K
+
+    def element_size(self) -> int:
+        return self.wp.element_size()
+
+    def data_ptr(self) -> int:
+        return self.wp.data_ptr()
+
+    def unpack(self) -> torch.Tensor:
+        """Row-major [N, K] (the inverse of pack_decode_weight's permutation)."""
+        T, KS = -(-self.N // 128), self.K // 256
+        # packed [t][ks][rg][s][lane = g*16 + c][e] holds W[128 t + 16 rg + c][256 ks + 32 s + 8 g + e]
+        v = self.wp.view(T, KS, 8, 8, 4, 16, 8).permute(0, 2, 5, 1, 3, 4, 6).reshape(T, 128, self.K)
+        if self.glu:  # tile t: 64 gate rows [64t, 64t + 64), then the matching up rows
+            v = v.view(T, 2, 64, self.K)
+            return torch.cat([v[:, 0].reshape(-1, self.K), v[:, 1].reshape(-1, self.K)])[:self.N]
+        return v.reshape(T * 128, self.K)[:self.N]
+
+    def float(self) -> torch.Tensor:
+        return self.unpack().float()
+
+    def to(self, *a, **k) -> torch.Tensor:
+        return self.unpack().to(*a, **k)
+
+    def t(self) -> torch.Tensor:
+        return self.unpack().t()
+
+
 def _lookup(reg, w):
     e = reg.get(w.data_ptr())
     if e is None:
@@ -258,12 +329,17 @@ def _lookup(reg, w):
     return wp
 
 
-def packed_of(w: torch.Tensor):
-    """The packed copy of ``w`` — only if registered for this very tensor."""
+def packed_of(w):
+    """The packed copy of ``w`` — only if registered for this very tensor (or ``w``'s
+    own layout when it is a ``PackedLinear`` without GLU interleaving)."""
+    if isinstance(w, PackedLinear):
+        return None if w.glu else w.wp
     return _lookup(PACKED, w)
 
 
-def glu_of(w: torch.Tensor):
+def glu_of(w):
+    if isinstance(w, PackedLinear):
+        return w.wp if w.glu else None
     return _lookup(PACKED_GLU, w)
 
 
@@ -287,6 +363,10 @@ def decode_gemm_packed(out, x, wp, N, rt, splits):
 def fused_choice(M: int, w):
     """(choice, packed weight or None) when the tuned decode GEMM for ``w`` at M can
     write split-K partials for a fused epilogue; None for hipBLASLt / skinny."""
+    if isinstance(w, PackedLinear):
+        if M > 64 or w.glu:
+            return None
+        return TUNER.choose_packed(M, w.N, w.K), w.wp
     if not isinstance(w, torch.Tensor) or M > 64 or not TUNER.table:
         return None
     c = TUNER.choose(M, w.shape[0], w.shape[1])
@@ -309,6 +389,11 @@ def gemm_partial(x, w, fc):
 def glu_choice(M: int, w):
     """(rt, S, glu-packed weight) when the tuned decode GEMM for the merged gate|up
     weight ``w`` at M is the packed kernel and a GLU-interleaved copy exists."""
+    if isinstance(w, PackedLinear):
+        if M > 64 or not w.glu:
+            return None
+        c = TUNER.choose_packed(M, w.N, w.K)
+        return c[1], c[2], w.wp
     if not isinstance(w, torch.Tensor) or M > 64 or not TUNER.table:
         return None
     c = TUNER.choose(M, w.shape[0], w.shape[1])
@@ -345,7 +430,50 @@ def run_choice(c, out, x, w, wp=None):
     raise ValueError(c)
 
 
+# packed prefill GEMM (prefill_gemm_packed.hip) workgroup shape: 1 = 128 x 512, 2 = 256 x 256
+PW_WM = int(__import__("os").environ.get("HIPSERVE_PW_WM", "1"))
+
+
+def packed_prefill(x: torch.Tensor, w: PackedLinear, epi: int = 0, out: torch.Tensor | None = None,
+                   bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Prefill-sized GEMM on the packed layout: epi 0 out = x W^T (+ bias), 1 out (the
+    residual) += x W^T, 2 / 3 (glu weights) out = silu / gelu_tanh(gate) * up."""
+    M = x.shape[0]
+    if out is None:
+        out = torch.empty(M, w.N // 2 if epi in (2, 3) else w.N, device=x.device, dtype=x.dtype)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, w.wp, w.N, epi, bias, PW_WM)
+    return out
+
+
+def packed_linear(x: torch.Tensor, w: PackedLinear) -> torch.Tensor:
+    """out = x W^T for a packed-only (non-GLU) weight: the packed decode GEMM up to 64
+    rows, the packed prefill GEMM above."""
+    assert not w.glu, "a GLU-interleaved weight has no plain x W^T (use packed_glu)"
+    M = x.shape[0]
+    if x.stride(1) != 1 or x.stride(0) % 8:
+        x = x.contiguous()
+    if M <= 64:
+        c = TUNER.choose_packed(M, w.N, w.K)
+        out = torch.empty(M, w.N, device=x.device, dtype=x.dtype)
+        return decode_gemm_packed(out, x, w.wp, w.N, c[1], c[2])
+    return packed_prefill(x, w)
+
+
+def packed_glu(x: torch.Tensor, w: PackedLinear, gelu: bool = False) -> torch.Tensor:
+    """act = silu / gelu_tanh(x Wg^T) * (x Wu^T) for a GLU-packed merged gate|up weight."""
+    assert w.glu
+    M = x.shape[0]
+    if x.stride(1) != 1 or x.stride(0) % 8:
+        x = x.contiguous()
+    if M <= 64 and not gelu:
+        c = TUNER.choose_packed(M, w.N, w.K)
+        return gemm_glu(x, w, (c[1], c[2], w.wp))
+    return packed_prefill(x, w, 3 if gelu else 2)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if isinstance(w, PackedLinear):
+        return packed_linear(x, w)
     M = x.shape[0]
     if M <= 64 and x.is_cuda and TUNER.table:
         c = TUNER.choose(M, w.shape[0], w.shape[1])

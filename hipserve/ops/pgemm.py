@@ -291,3 +291,42 @@ def tune(units: dict, M: int, device, ops) -> list[dict]:
     torch.cuda.empty_cache()
     REPORT.extend(out)
     return out
+
+
+@torch.inference_mode()
+def tune_packed(units: list, M: int, device, ops) -> dict:
+    """Start-up timing of the packed-layout prefill GEMM (prefill_gemm_packed.hip) against
+    hipBLASLt on the layer's prefill units at M rows, random operands, 4 weight copies
+    streamed like a prefill step: ``units`` = [(kind, N, K)] with kind "plain" (qkv),
+    "add" (o / down: + residual add), "glu" (gate|up + SiLU-GLU). Returns the per-unit
+    times and the layer totals; the runner keeps the single packed weight layout when
+    the packed total is not slower."""
+    from . import gemm as G
+
+    op = torch.ops.hipserve
+    rows, tp_, tb_ = [], 0.0, 0.0
+    for kind, N, K in units:
+        g = torch.Generator(device=device).manual_seed(N + K)
+        ws = [((torch.rand(N, K, device=device, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(4)]
+        wps = [G.PackedLinear(G.pack(w, glu=kind == "glu"), N, K, glu=kind == "glu") for w in ws]
+        x = (torch.rand(M, K, device=device, generator=g) * 2 - 1).to(torch.bfloat16)
+        if kind == "glu":
+            act = torch.empty(M, N // 2, device=device, dtype=torch.bfloat16)
+            t_b = _time(lambda i: ops.silu_and_mul(act, F.linear(x, ws[i])))
+            t_p = _time(lambda i: G.packed_prefill(x, wps[i], 2, out=act))
+        elif kind == "add":
+            res = torch.randn(M, N, device=device).to(torch.bfloat16)
+            t_b = _time(lambda i: res.add_(F.linear(x, ws[i])))
+            t_p = _time(lambda i: G.packed_prefill(x, wps[i], 1, out=res))
+        else:
+            o = torch.empty(M, N, device=device, dtype=torch.bfloat16)
+            t_b = _time(lambda i: F.linear(x, ws[i]))
+            t_p = _time(lambda i: G.packed_prefill(x, wps[i], 0, out=o))
+        rows.append({"kind": kind, "M": M, "N": N, "K": K, "blas_unit_ms": round(t_b, 4),
+                     "packed_unit_ms": round(t_p, 4)})
+        tp_, tb_ = tp_ + t_p, tb_ + t_b
+        del ws, wps, x
+    torch.cuda.empty_cache()
+    r = {"units": rows, "packed_ms": round(tp_, 4), "blas_ms": round(tb_, 4)}
+    log.info("packed prefill GEMM vs hipBLASLt: %s", r)
+    return r

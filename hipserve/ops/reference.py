@@ -364,7 +364,13 @@ def penalty_init(counts, seen, slots, off, n_prompt, toks):
 
 
 def top_logprobs(logits, nreq, out_ids, out_lp):
-    """n largest log-softmax entries per row (ties -> lowest id), K = out width."""
+    """n largest log-softmax entries per row (ties -> lowest id), K = out width.
+
+    Exact over the whole row. The device kernel (csrc/kernels/penalties.hip
+    top_logprobs) is exact too unless more than 64 keys share the bf16 bin of the n-th
+    largest value: it then keeps the lowest-index 64 of them, so in a row
+    with > 64 logits within one bf16 ulp of the n-th largest the two may name different
+    (equally probable to bf16 precision) entries."""
     K = out_ids.shape[1]
     out_ids.fill_(-1)
     out_lp.fill_(float("-inf"))

@@ -132,9 +132,38 @@ def cached_snapshot(model: str, need_weights: bool) -> str | None:
     return d if snapshot_problem(d, need_weights) is None else None
 
 
+def drop_truncated(d: str | None) -> list[str]:
+    """Delete the truncated shards of snapshot ``d`` (and, for the Hub cache's
+    symlinks, the blob each points to) so the next download fetches them again: the
+    Hub client skips a file that already exists in the snapshot, truncated or not, so
+    leaving it would turn a killed download into a permanent crash loop."""
+    gone = []
+    if not d or not os.path.isdir(d):
+        return gone
+    try:
+        files = weight_files(d)
+    except (OSError, ValueError):
+        return gone
+    for f in files:
+        if os.path.lexists(f) and not safetensors_intact(f):
+            if os.path.islink(f):
+                blob = os.path.realpath(f)
+                if os.path.exists(blob):
+                    os.remove(blob)
+            os.remove(f)
+            gone.append(os.path.basename(f))
+    if gone:
+        log.warning("re-downloading truncated shards: %s", ", ".join(gone))
+    return gone
+
+
 def download(model: str, need_weights: bool) -> str:
+    from ..config import _hf_cache_dir
+
     fn = _downloader()
     patterns = WEIGHT_PATTERNS if need_weights else CONFIG_PATTERNS
+    if need_weights:
+        drop_truncated(_hf_cache_dir(model))
     log.info("downloading %s from the Hugging Face Hub (%s)", model, "weights" if need_weights else "config")
     path = fn(model, allow_patterns=patterns, token=_token())
     why = snapshot_problem(path, need_weights)

@@ -10,7 +10,7 @@ Failure modes of a real first start, for the cache-hardening tests:
 * ``FAKE_HUB_SHARDS=n``: write n shards + ``model.safetensors.index.json``;
 * ``FAKE_HUB_INTERRUPT=k``: die (raise) after writing k shards — the pod killed
   mid-download; like the real client, a later call resumes (skips shards that
-  are already complete) and finishes;
+  are already in the snapshot — complete or not) and finishes;
 * ``FAKE_HUB_DELAY=s``: the download takes s seconds (slower than a collective
   timeout)."""
 import fnmatch
@@ -49,8 +49,8 @@ def _sharded(snap, cfg, tensors, n, interrupt):
     wrote = 0
     for fn, p in zip(files, parts):
         path = os.path.join(snap, fn)
-        if os.path.exists(path) and safetensors_intact(path):
-            continue  # resume: already complete
+        if os.path.exists(path):
+            continue  # like the real client: a file already in the snapshot is not re-fetched
         if interrupt is not None and wrote >= interrupt:
             raise RuntimeError("connection reset (pod killed mid-download)")
         save_file({k: tensors[k].contiguous() for k in p}, path)

@@ -13,10 +13,10 @@ from hipserve.parallel.comm import TPGroup
 pytestmark = pytest.mark.gpu
 
 
-def _engine(eager, device="cuda", dtype="bfloat16", model="small-llama"):
+def _engine(eager, device="cuda", dtype="bfloat16", model="small-llama", single=None):
     cfg = EngineConfig(model=model, device=device, dtype=dtype, max_num_seqs=16,
                        max_num_batched_tokens=256, max_model_len=2048, num_kv_blocks=512,
-                       enforce_eager=eager)
+                       enforce_eager=eager, extra={} if single is None else {"single_layout": single})
     dev = torch.device(device, 0) if device == "cuda" else torch.device("cpu")
     return LLMEngine(cfg, tp=TPGroup(0, 1, None, dev))
 
@@ -24,13 +24,15 @@ def _engine(eager, device="cuda", dtype="bfloat16", model="small-llama"):
 PROMPTS = [[1] + list(range(10, 300)), [1, 7, 8, 9], [1] + [42] * 40, list(range(3, 600))]
 
 
-def test_graph_matches_eager():
+@pytest.mark.parametrize("single", ["0", "1"])
+def test_graph_matches_eager(single):
     """hipGraph decode vs eager decode, batch = a graph bucket (no padding rows):
-    every greedy token must match exactly (same kernels, same GEMM choices)."""
+    every greedy token must match exactly (same kernels, same GEMM choices); also with
+    the single packed weight layout."""
     sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
-    g = _engine(False)
+    g = _engine(False, single=single)
     assert g.runner.use_graphs and g.runner.graphs
-    e = _engine(True)
+    e = _engine(True, single=single)
     rg = g.generate(PROMPTS, sp)  # 4 sequences: bucket 4
     re_ = e.generate(PROMPTS, sp)
     assert g.runner.stats["graph_steps"] >= 20 and e.runner.stats["graph_steps"] == 0
@@ -74,11 +76,19 @@ def test_penalties_and_logprobs_stay_on_graph():
     assert len(g.runner._free_pen) == g.runner.pen_counts.shape[0]  # slot returned
 
 
-def test_full_model_logits_vs_fp32_reference():
+@pytest.mark.parametrize("single", ["0", "1"])
+def test_full_model_logits_vs_fp32_reference(single):
     """Prefill logits of the GPU engine (HIP kernels, bf16) vs the CPU fp32 engine
     with identical weights: max |error| <= 0.05 (logit std ~0.45) and the argmax
-    agrees on >= 90% of positions."""
-    g = _engine(True)
+    agrees on >= 90% of positions. single = "1": every dense projection (and the LM
+    head) kept ONLY in the packed layout (gemm.PackedLinear: packed prefill GEMM with
+    the GLU / residual epilogues + the packed decode GEMMs), "0": row-major + packed."""
+    g = _engine(True, single=single)
+    if single == "1":
+        from hipserve.ops.gemm import PackedLinear
+
+        lw = g.runner.model.layers[0]
+        assert g.runner.single_layout and all(isinstance(w, PackedLinear) for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd))
     c = _engine(True, device="cpu", dtype="float32")
     gm, cm = g.runner.model, c.runner.model
     cm.embed, cm.lm_head, cm.norm = gm.embed.float().cpu(), gm.lm_head.float().cpu(), gm.norm.float().cpu()

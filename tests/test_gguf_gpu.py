@@ -552,3 +552,25 @@ def test_producers_write_pair_order_f16():
     act16 = torch.empty(M, I, device="cuda", dtype=torch.float16)
     op.splitk_glu(act, wsg, S, False, act16)
     assert torch.equal(act16, _pair_order_f16(act))
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K, G.Q8_0])
+def test_mfma_v2_tiny_scales(qt):
+    """Blocks whose scale product d * sc is an f16 SUBNORMAL (< 2^-14): the v2 kernel's
+    subnormal-integer dequant keeps the scale as a normal f16 (more mantissa bits than
+    the magic-number path), so it is not bit-identical to that path there — but it must
+    still match the fp32 numpy block decoder (gguf_mfma.hip comment)."""
+    from hipserve.ops.quant import random_blocks
+    rng = np.random.default_rng(9)
+    N, K = 256, 1024
+    raw = random_blocks(rng, qt, N, K).copy()
+    _, bb = G.BLOCK[qt]
+    b = raw.reshape(-1, bb)
+    off = 208 if qt == G.Q6_K else 0
+    b[::3, off:off + 2] = np.frombuffer(np.float16(3e-6).tobytes(), np.uint8)  # f16-subnormal d
+    qw = QuantWeight.from_raw([(qt, N, K, raw)], "cuda")
+    assert qw.v2
+    x = torch.randn(32, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense([(qt, N, K, raw)]).T
+    y = quant_linear(x, qw).float()
+    assert (y - want).abs().max().item() < 1e-2 * want.abs().max().item() + 1e-4

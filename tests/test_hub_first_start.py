@@ -132,7 +132,8 @@ def test_truncated_shard_is_redownloaded(hub, monkeypatch):
     with open(shard, "r+b") as f:
         f.truncate(os.path.getsize(shard) - 100)
     assert "truncated" in snapshot_problem(snap, True)
-    os.remove(shard)  # the real client's resume re-fetches what is not complete
+    # the client skips files already in the snapshot (tests/fake_hub.py, like the real
+    # one): the engine must drop the truncated shard itself before re-downloading
     _engine("acme/tiny-chat")
     assert len(hub.read_text().splitlines()) == 2 and snapshot_problem(snap, True) is None
 

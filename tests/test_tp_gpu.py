@@ -126,9 +126,11 @@ def _fp32_logprobs(model, ids):
 
     from hipserve.ops import quant as Q
 
-    def dense(w):  # fp32 copy of a bf16 / quantised (dequantised exactly) weight
+    def dense(w):  # fp32 copy of a bf16 / packed-only / quantised (dequantised exactly) weight
         if isinstance(w, torch.Tensor):
             return w.float()
+        if hasattr(w, "unpack"):  # gemm.PackedLinear (single weight layout)
+            return w.unpack().float()
         if isinstance(w, Q.QuantMoE):
             return w.dequantize().float()
         return Q.dequantize(w).float()
