@@ -79,9 +79,9 @@ struct PwTile {
   int m0, t;
 };
 
-template <int WM>
+template <int WM, bool kGroup>
 HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned short* X, long ldx,
-                         const unsigned short* Wp, int M, int ntiles, int KS) {
+                         const unsigned short* Wp, int M, int ntiles, int KS, const PwGroup& grp) {
   constexpr int WN = 4 / WM, BM = 128 * WM;
   int tm, tn;
   pw_tile(L, tiles_m, tiles_n, tm, tn);
@@ -89,6 +89,7 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
   T.m0 = tm * BM;
   T.t = tn * WN + wn;
   const int tl = min(T.t, ntiles - 1);  // waves past the last weight tile compute a copy, store nothing
+  if constexpr (kGroup) Wp += (long)grp.tile_expert[tm] * grp.estride;  // this m-tile's expert
   T.w = __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + (long)tl * KS * 32768), 0, KS * 65536, 0x00020000);
   // rows >= M fall outside the buffer range and read as zero
   T.x = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long)T.m0 * ldx), 0,
@@ -96,11 +97,15 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
   return T;
 }
 
-template <int WM, int EPI>
+// kGroup (MoE prefill experts): X rows are expert-sorted slots in BM-row tiles
+// (moe_align with tile BM, moe_gather); m-tile tm multiplies expert grp.tile_expert[tm]'s
+// packed weight (Wp + e * estride) and only the first *grp.num_tiles m-tiles (the
+// device-side count: no host round trip, graph-capturable) are walked.
+template <int WM, int EPI, bool kGroup>
 __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
     const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
     unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n,
-    const unsigned short* __restrict__ bias) {
+    const unsigned short* __restrict__ bias, PwGroup grp) {
   constexpr int WN = 4 / WM, BM = 128 * WM, STAGE = BM * 128, XP = BM / 32;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -108,14 +113,15 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int ntiles = (N + 127) >> 7;
   const int KS = K >> 8, nq = K >> 5, nst = K >> 6;
+  if constexpr (kGroup) tiles_m = min(tiles_m, __builtin_amdgcn_readfirstlane(*grp.num_tiles));
   const int total = tiles_m * tiles_n, G = gridDim.x;
   const int r = xcd_remap(blockIdx.x, G);
   if (r >= total) return;
 
   // cur: the tile whose MFMAs run; nxt: the one the loads past cur's end stream in, so
   // the pipeline runs on across the tile boundary (only the epilogue sits between)
-  PwTile cur = pw_make<WM>(r, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS);
-  PwTile nxt = r + G < total ? pw_make<WM>(r + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS) : cur;
+  PwTile cur = pw_make<WM, kGroup>(r, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp);
+  PwTile nxt = r + G < total ? pw_make<WM, kGroup>(r + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp) : cur;
 
   const int wvo = lane * 16;
   auto wload = [&](int q, int rg) -> u32x4 {  // 32-deep slot q of cur (q >= nq: of nxt), row group rg
@@ -259,12 +265,15 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     L += G;
     if (L >= total) break;
     cur = nxt;
-    if (L + G < total) nxt = pw_make<WM>(L + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS);
+    if (L + G < total) nxt = pw_make<WM, kGroup>(L + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp);
   }
 }
 
 bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
-                                int K, const void* bias, int wm, int grid_req, hipStream_t s) {
+                                int K, const void* bias, int wm, int grid_req, hipStream_t s, const PwGroup* group) {
+  const PwGroup grp = group != nullptr ? *group : PwGroup{nullptr, nullptr, 0};
+  const bool grouped = group != nullptr;
+  if (grouped && (bias != nullptr || epi == PW_EPI_ADD)) return false;
   if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2)) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;
@@ -286,8 +295,13 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   auto* w = static_cast<const unsigned short*>(Wp);
   auto* c = static_cast<unsigned short*>(C);
   auto* b = static_cast<const unsigned short*>(bias);
-#define PW_LAUNCH(WM_, E_) \
-  pgw_kernel<WM_, E_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b)
+#define PW_LAUNCH(WM_, E_)                                                                                 \
+  do {                                                                                                     \
+    if (grouped)                                                                                           \
+      pgw_kernel<WM_, E_, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp);  \
+    else                                                                                                   \
+      pgw_kernel<WM_, E_, false><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+  } while (0)
 #define PW_EPIS(WM_)                                          \
   switch (epi) {                                              \
     case PW_EPI_STORE: PW_LAUNCH(WM_, PW_EPI_STORE); return true; \

@@ -716,6 +716,28 @@ void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor&
               "prefill_gemm_packed: unsupported (glu needs N % 128, bias only with epi 0, 32-bit offsets)");
 }
 
+// Grouped (MoE prefill experts) form: x = expert-sorted slot rows [cap, K] (moe_align
+// with tile 128 * wm + moe_gather), wp = [E, packed expert] (pack_decode_weight per
+// expert, glu for w13), tile_expert / num_tiles from moe_align. epi 0 or 2 / 3.
+void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
+                                 const at::Tensor& tile_expert, const at::Tensor& num_tiles, int64_t wm) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(wp.dim() == 2 && wp.is_contiguous(), "prefill_gemm_packed_grouped: wp [E, packed]");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 256 == 0 && wp.size(1) == (N + 127) / 128 * 128 * K, "prefill_gemm_packed_grouped: wp per expert");
+  TORCH_CHECK(M % (128 * wm) == 0 && tile_expert.numel() >= M / (128 * wm), "prefill_gemm_packed_grouped: tiles");
+  TORCH_CHECK(tile_expert.scalar_type() == at::kInt && num_tiles.scalar_type() == at::kInt, "int32 tile tables");
+  const bool glu = epi == 2 || epi == 3;
+  TORCH_CHECK(epi == 0 || glu, "prefill_gemm_packed_grouped: store or glu epilogue");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? N / 2 : N), "prefill_gemm_packed_grouped: out shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::PwGroup grp{tile_expert.data_ptr<int>(), num_tiles.data_ptr<int>(), (long)wp.size(1)};
+  TORCH_CHECK(hipserve::launch_prefill_gemm_packed((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
+                                                   wp.data_ptr(), M, (int)N, K, nullptr, (int)wm, 0, cur_stream(),
+                                                   &grp),
+              "prefill_gemm_packed_grouped: unsupported");
+}
+
 // FP8 W8A8 form: xq [M, K] uint8 e4m3 + xs [M] fp32 (act_quant_fp8), the weight as
 // tiled FP8 parts (ops/quant.py QuantPart.from_fp8: q [N/16, K/256, 4096] uint8 and
 // rs [N] fp32) stacked along N. epi 0 / 1 as prefill_gemm; 2 / 3: parts = (gate, up),
@@ -1286,6 +1308,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0) -> ()");
+  m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
@@ -1342,6 +1365,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("decode_gemm_fused", &decode_gemm_fused);
   m.impl("prefill_gemm", &prefill_gemm);
   m.impl("prefill_gemm_packed", &prefill_gemm_packed);
+  m.impl("prefill_gemm_packed_grouped", &prefill_gemm_packed_grouped);
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);
   m.impl("splitk_post_add_rmsnorm", &splitk_post_add_rmsnorm);
   m.impl("act_quant_fp8", &act_quant_fp8);

@@ -443,11 +443,14 @@ class LlamaModel:
                 lw.wd = conv(lw.wd)
         if self.lm_head is not self.embed:
             self.lm_head = conv(self.lm_head)
+        # MoE experts: their packed decode copy serves prefill too (the packed grouped
+        # GEMM), so the row-major experts go, layer by layer
+        freed += self.pack_moe_weights(drop_plain=True)
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
         return n, freed
 
-    def pack_moe_weights(self) -> int:
+    def pack_moe_weights(self, drop_plain: bool = False) -> int:
         """Per-expert packed copies of the MoE weights for the decode expert GEMM
         (``moe_hip``): w13 gate/up-interleaved (SiLU-GLU in the GEMM epilogue), w2
         plain. The row-major originals stay for prefill (per-expert hipBLASLt), so
@@ -461,22 +464,31 @@ class LlamaModel:
         if not lws:
             return 0
         need = sum(2 * (lw.w13.numel() + lw.w2.numel()) for lw in lws)
+        if drop_plain:  # the packed copy REPLACES the row-major experts (one layer at a time)
+            if not all(lw.moe_packed is not None or self.cfg.hidden_act == "silu" for lw in lws):
+                return 0
+            need = 0
         if self.device.type == "cuda":
             free, _ = torch.cuda.mem_get_info(self.device)
             if need + (24 << 30) > free:
                 log.warning("MoE decode weights not packed: %.1f GB needed, %.1f GB free", need / 2**30, free / 2**30)
                 return 0
         op = torch.ops.hipserve
+        freed = 0
         for lw in lws:
-            E, N13, K13 = lw.w13.shape
-            _, N2, K2 = lw.w2.shape
-            p13 = torch.empty(E, N13 * K13, dtype=lw.w13.dtype, device=lw.w13.device)
-            p2 = torch.empty(E, -(-N2 // 128) * 128 * K2, dtype=lw.w2.dtype, device=lw.w2.device)
-            for e in range(E):
-                op.pack_decode_weight(p13[e], lw.w13[e], True)
-                op.pack_decode_weight(p2[e], lw.w2[e], False)
-            lw.moe_packed = (p13, p2)
-        return need
+            if lw.moe_packed is None:
+                E, N13, K13 = lw.w13.shape
+                _, N2, K2 = lw.w2.shape
+                p13 = torch.empty(E, N13 * K13, dtype=lw.w13.dtype, device=lw.w13.device)
+                p2 = torch.empty(E, -(-N2 // 128) * 128 * K2, dtype=lw.w2.dtype, device=lw.w2.device)
+                for e in range(E):
+                    op.pack_decode_weight(p13[e], lw.w13[e], True)
+                    op.pack_decode_weight(p2[e], lw.w2[e], False)
+                lw.moe_packed = (p13, p2)
+            if drop_plain and self.moe_packed_prefill(lw):
+                freed += 2 * (lw.w13.numel() + lw.w2.numel())
+                lw.w13 = lw.w2 = None
+        return freed if drop_plain else need
 
     def fused_gemm_shapes(self) -> dict:
         """{(N, K): epilogue spec} of the projections whose decode GEMM output feeds
@@ -994,7 +1006,7 @@ class LlamaModel:
         k = cfg.num_experts_per_tok
         T = x.shape[0]
         P = T * k
-        if not isinstance(lw.w13, torch.Tensor):  # quantised experts (ops/quant.py QuantMoE)
+        if lw.w13 is not None and not isinstance(lw.w13, torch.Tensor):  # quantised experts (ops/quant.py QuantMoE)
             if P <= MOE_KERNEL_MAX_PAIRS:
                 return self.moe_quant(x, lw)
             from ..ops import quant as Q
@@ -1006,6 +1018,8 @@ class LlamaModel:
                 and (P <= MOE_KERNEL_MAX_PAIRS
                      or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts and self._moe_decode_ok(lw)))):
             return self.moe_hip(x, lw)
+        if self.ops.name == "hip" and cfg.num_experts <= 128 and self.moe_packed_prefill(lw):
+            return self.moe_grouped(x, lw)
         if self.ops.name == "hip" and hasattr(torch, "_grouped_mm") and cfg.num_experts <= 128 \
                 and cfg.hidden_size % 8 == 0 and self.inter % 8 == 0 and isinstance(lw.w13, torch.Tensor):
             return self.moe_grouped(x, lw)
@@ -1067,9 +1081,12 @@ class LlamaModel:
         cfg = self.cfg
         E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
         T, dev = x.shape[0], x.device
-        # 256-row expert tiles for the hand-written grouped GEMM (ops/pgemm.py), 16-row
-        # ones for hipBLASLt's grouped GEMM
-        P, tile = T * k, (256 if pgemm.moe_ok(lw.w13, lw.w2) else 16)
+        # packed experts (the decode copy, moe_packed): the packed-layout grouped GEMM
+        # (prefill_gemm_packed.hip kGroup) over (128 * wm)-row tiles; else 256-row tiles
+        # for the hand-written grouped GEMM (ops/pgemm.py), 16-row ones for hipBLASLt's
+        packed = self.moe_packed_prefill(lw)
+        P = T * k
+        tile = 128 * gemm.PW_WM if packed else (256 if pgemm.moe_ok(lw.w13, lw.w2) else 16)
         cap = -(-(P + E * (tile - 1)) // tile) * tile
         logits = gemm.linear(x, lw.router)
         w = torch.empty(T, k, dtype=torch.float32, device=dev)
@@ -1083,7 +1100,13 @@ class LlamaModel:
         op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
         xs = torch.empty(cap, H, dtype=x.dtype, device=dev)
         op.moe_gather(xs, x, slots, k)
-        if tile == 256:  # hand-written grouped expert GEMMs, SiLU-GLU in the first's epilogue
+        if packed:  # packed-layout grouped expert GEMMs, SiLU-GLU in the first's epilogue
+            p13, p2 = lw.moe_packed
+            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+            op.prefill_gemm_packed_grouped(act, xs, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM)
+            y = torch.empty(cap, H, dtype=x.dtype, device=dev)
+            op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM)
+        elif tile == 256:  # hand-written grouped expert GEMMs, SiLU-GLU in the first's epilogue
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
             op.prefill_gemm_grouped(act, xs, lw.w13, tile_expert, 2, pgemm.VARIANT)
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
@@ -1096,6 +1119,15 @@ class LlamaModel:
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         op.moe_combine(out, y, w, pair_slot, k)
         return out
+
+    MOE_PACKED_PREFILL = os.environ.get("HIPSERVE_MOE_PACKED_PREFILL", "1") != "0"
+
+    def moe_packed_prefill(self, lw: LayerWeights) -> bool:
+        """Prefill experts on the packed-layout grouped GEMM (the decode kernels' copy of
+        the experts, ``pack_moe_weights``): SiLU-GLU experts, K of both GEMMs % 256."""
+        return (self.MOE_PACKED_PREFILL and lw.moe_packed is not None and self.cfg.hidden_act == "silu"
+                and self.cfg.hidden_size % 256 == 0 and self.inter % 256 == 0 and (2 * self.inter) % 128 == 0
+                and hasattr(torch.ops.hipserve, "prefill_gemm_packed_grouped"))
 
     def moe_hip(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Graph-capturable MoE on the gfx950 kernels (decode-sized batches): top-k

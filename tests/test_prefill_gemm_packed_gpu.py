@@ -96,3 +96,42 @@ def test_packed_rejects_bad_shapes():
     with pytest.raises(RuntimeError):  # K % 256
         torch.ops.hipserve.prefill_gemm_packed(out, x, torch.empty(128 * 320, device=DEV, dtype=torch.bfloat16),
                                                128, 0, None, 1)
+
+
+@pytest.mark.parametrize("wm", [1, 2])
+@pytest.mark.parametrize("E,I,K,glu", [(8, 512, 1024, True), (8, 256, 512, False), (16, 128, 256, True)])
+def test_packed_grouped_moe(E, I, K, glu, wm):
+    """Grouped expert GEMM over moe_align's expert-sorted (128 * wm)-row tiles with each
+    expert's weight in the packed decode layout (moe_packed: w13 GLU-interleaved), the
+    valid tile count read on the device, vs a per-expert fp32 reference."""
+    g = torch.Generator(device=DEV).manual_seed(E + I + K)
+    T, k = 700, 2
+    ids = torch.stack([torch.randperm(E, device=DEV, generator=g)[:k] for _ in range(T)]).int()
+    N = 2 * I if glu else I
+    w = _rnd(g, E, N, K, scale=0.05)
+    wp = torch.stack([_pack(w[e], glu) for e in range(E)])
+    x = _rnd(g, T, K)
+    op = torch.ops.hipserve
+    P, tile = T * k, 128 * wm
+    cap = -(-(P + E * (tile - 1)) // tile) * tile
+    slots = torch.empty(cap, dtype=torch.int32, device=DEV)
+    tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=DEV)
+    ntiles = torch.empty(1, dtype=torch.int32, device=DEV)
+    pair_slot = torch.empty(P, dtype=torch.int32, device=DEV)
+    ends = torch.empty(E, dtype=torch.int32, device=DEV)
+    op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
+    xs = torch.empty(cap, K, dtype=torch.bfloat16, device=DEV)
+    op.moe_gather(xs, x, slots, k)
+    out = torch.full((cap, I), float("nan"), device=DEV, dtype=torch.bfloat16)
+    op.prefill_gemm_packed_grouped(out, xs, wp, N, 2 if glu else 0, tile_expert, ntiles, wm)
+    ps = pair_slot.long()
+    for p in range(0, P, 37):  # a spread of pairs
+        t, j = p // k, p % k
+        e = int(ids[t, j])
+        h = x[t].float() @ w[e].float().t()
+        if glu:
+            h = h.to(torch.bfloat16).float()
+            want = torch.nn.functional.silu(h[:I]) * h[I:]
+        else:
+            want = h
+        torch.testing.assert_close(out[ps[p]].float(), want, rtol=2e-2, atol=2e-2 * max(1.0, want.abs().max().item()))
