@@ -204,6 +204,7 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
 //   (merged [gate; up], N = 2I, I % 64 == 0), C = act [M, I]
 constexpr int PW_EPI_STORE = 0, PW_EPI_ADD = 1, PW_EPI_GLU = 2, PW_EPI_GEGLU = 3;
 // grid_req <= 0: persistent (one workgroup per CU walking the tiles), else that many workgroups.
+// rw: weight register sets in flight (2 or 4 32-deep slots ahead).
 // group (MoE experts, STORE / GLU): X = expert-sorted slots in 128 * wm-row tiles, m-tile tm
 // uses expert tile_expert[tm]'s packed weight at Wp + e * estride; *num_tiles valid m-tiles.
 struct PwGroup {
@@ -213,7 +214,7 @@ struct PwGroup {
 };
 bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
                                 int K, const void* bias, int wm, int grid_req, hipStream_t s,
-                                const PwGroup* group = nullptr);
+                                const PwGroup* group = nullptr, int rw = 4);
 // FP8 (W8A8) form: A = per-token e4m3 activations [M, K] bytes (row scale xs[M]),
 // B = e4m3 weights in the decode kernel's tiled layout (gguf_mfma.hip: [N/16][K/256]
 // [4096 B]) as up to 4 parts stacked along N (each rows % 256 == 0; GLU: part 0 =

@@ -101,7 +101,7 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
 // (moe_align with tile BM, moe_gather); m-tile tm multiplies expert grp.tile_expert[tm]'s
 // packed weight (Wp + e * estride) and only the first *grp.num_tiles m-tiles (the
 // device-side count: no host round trip, graph-capturable) are walked.
-template <int WM, int EPI, bool kGroup>
+template <int WM, int EPI, bool kGroup, int RW>
 __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
     const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
     unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n,
@@ -140,17 +140,21 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   // next) over all 16 slots of a 256-byte bank row; (r >> 1) & 7 is the same for rows
   // r and r + 32 p
   const int xdo = (tid >> 3) * 128 + (((tid & 7) ^ ((tid >> 4) & 7)) * 16);
-  u32x4 xst[XP];
-  auto xload = [&](int st) {  // 64-deep stage st of cur (st >= nst: of nxt)
+  // RW weight register sets (one per 32-deep slot in flight: a set's next slot is
+  // loaded right after its MFMAs, RW slots ahead) and XS = RW / 2 X staging sets (stage
+  // s + 1 + XS is loaded into the set stage s + 1 was just written to LDS from)
+  constexpr int XS = RW / 2;
+  u32x4 xst[XS][XP];
+  auto xload = [&](int st, u32x4 (&xs)[XP]) {  // 64-deep stage st of cur (st >= nst: of nxt)
     const bool n = st >= nst;
     st = n ? st - nst : st;
 #pragma unroll
     for (int p = 0; p < XP; ++p)
-      xst[p] = __builtin_amdgcn_raw_buffer_load_b128(n ? nxt.x : cur.x, xvo[p], st * 128, 0);
+      xs[p] = __builtin_amdgcn_raw_buffer_load_b128(n ? nxt.x : cur.x, xvo[p], st * 128, 0);
   };
-  auto xstore = [&](int buf) {
+  auto xstore = [&](int buf, const u32x4 (&xs)[XP]) {
 #pragma unroll
-    for (int p = 0; p < XP; ++p) *reinterpret_cast<u32x4*>(lds + buf * STAGE + p * 4096 + xdo) = xst[p];
+    for (int p = 0; p < XP; ++p) *reinterpret_cast<u32x4*>(lds + buf * STAGE + p * 4096 + xdo) = xs[p];
   };
   const int fr = lane & 15, fq = lane >> 4, sw = (fr >> 1) & 7;
   const int foff = (wm * 128 + fr) * 128;
@@ -160,48 +164,61 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   };
 
   f32x4 acc[8][8];
-  u32x4 wa[8], wb[8], xa[8], xb[8];
+  u32x4 w[RW][8], xa[8], xb[8];
 
-  // prologue (first tile only): stage 0 in LDS, stage 1 in registers, weight slots 0 and
-  // 1 in flight; later tiles find theirs loaded by the previous tile's last stages
-  xload(0);
-  xstore(0);
-  xload(1);
+  // prologue (first tile only): stage 0 in LDS, stages 1 .. XS in registers, weight
+  // slots 0 .. RW - 1 in flight; later tiles find theirs loaded by the previous tile's
+  // last slots
+  xload(0, xst[0]);
+  xstore(0, xst[0]);
 #pragma unroll
-  for (int rg = 0; rg < 8; ++rg) wa[rg] = wload(0, rg);
+  for (int s = 1; s <= XS; ++s) xload(s, xst[s % XS]);
 #pragma unroll
-  for (int rg = 0; rg < 8; ++rg) wb[rg] = wload(1, rg);
+  for (int j = 0; j < RW; ++j)
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) w[j][rg] = wload(j, rg);
   pw_barrier();
 #pragma unroll
   for (int i = 0; i < 8; ++i) xa[i] = xfrag(0, 0, i);
+
+  // one 32-deep slot: J (compile time) = slot index inside the RW-slot loop body
+  auto slot = [&](auto jc, int q0, int s0) {
+    constexpr int J = decltype(jc)::value, H = J & 1;
+    const int s = s0 + J / 2, buf = s & 1;
+    constexpr int XI = (J / 2 + 1) % XS;  // staging set of stage s + 1 (s0 is a multiple of XS)
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pw_mfma(acc[rg][i], w[J][rg], H ? xb[i] : xa[i]);
+      w[J][rg] = wload(q0 + J + RW, rg);
+      if constexpr (H == 0) {
+        xb[rg] = xfrag(buf, 1, rg);
+        if (rg == 2) xstore(buf ^ 1, xst[XI]);     // stage s + 1 (loaded XS stages ago)
+        if (rg == 3) xload(s + 1 + XS, xst[XI]);
+      } else {
+        xa[rg] = xfrag(buf ^ 1, 0, rg);            // stage s + 1, visible since the barrier
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (H == 0) pw_barrier();  // stage s + 1 visible; every read of stage s - 1 done
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
 
   for (int L = r;;) {
 #pragma unroll
     for (int rg = 0; rg < 8; ++rg)
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[rg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int st = 0; st < nst; ++st) {
-      const int buf = st & 1;  // nst is even: a tile starts in buffer 0
-      // ---- slot 2 st
-#pragma unroll
-      for (int rg = 0; rg < 8; ++rg) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pw_mfma(acc[rg][i], wa[rg], xa[i]);
-        wa[rg] = wload(2 * st + 2, rg);
-        xb[rg] = xfrag(buf, 1, rg);
-        if (rg == 2) xstore(buf ^ 1);  // stage st + 1 (loaded during slot 2 st - 2)
-        if (rg == 3) xload(st + 2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      pw_barrier();  // stage st + 1 visible; every read of stage st - 1 long done
-      // ---- slot 2 st + 1
-#pragma unroll
-      for (int rg = 0; rg < 8; ++rg) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pw_mfma(acc[rg][i], wb[rg], xb[i]);
-        wb[rg] = wload(2 * st + 3, rg);
-        xa[rg] = xfrag(buf ^ 1, 0, rg);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int q0 = 0; q0 < nq; q0 += RW) {  // nq % 8 == 0; a tile starts in LDS buffer 0
+      const int s0 = q0 >> 1;
+      slot(I0(), q0, s0);
+      slot(I1(), q0, s0);
+      if constexpr (RW == 4) {
+        slot(I2(), q0, s0);
+        slot(I3(), q0, s0);
       }
     }
 
@@ -229,22 +246,18 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
           }
         }
       } else {
-        float bv[8][4];
 #pragma unroll
-        for (int rg = 0; rg < 8; ++rg)
+        for (int rg = 0; rg < 8; ++rg) {
+          const int n = t * 128 + rg * 16 + 4 * fq;
+          if (n >= N) continue;
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (bias != nullptr)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int n = t * 128 + rg * 16 + 4 * fq + j;
-            bv[rg][j] = (bias != nullptr && n < N) ? bf16_to_f32(bias[n]) : 0.f;
-          }
+            for (int j = 0; j < 4; ++j) bv[j] = n + j < N ? bf16_to_f32(bias[n + j]) : 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int m = mb + 16 * i;
-          if (m >= M) continue;
-#pragma unroll
-          for (int rg = 0; rg < 8; ++rg) {
-            const int n = t * 128 + rg * 16 + 4 * fq;
-            if (n >= N) continue;
+          for (int i = 0; i < 8; ++i) {
+            const int m = mb + 16 * i;
+            if (m >= M) continue;
             uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n);
             float o[4];
             if constexpr (EPI == PW_EPI_ADD) {  // C is the residual: C = bf16(bf16(acc) + C)
@@ -255,7 +268,7 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
               for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[rg][i][j])) + bf16_to_f32(rr[j]);
             } else {  // bias added to the fp32 accumulator, one rounding
 #pragma unroll
-              for (int j = 0; j < 4; ++j) o[j] = acc[rg][i][j] + bv[rg][j];
+              for (int j = 0; j < 4; ++j) o[j] = acc[rg][i][j] + bv[j];
             }
             *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
           }
@@ -270,11 +283,12 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 }
 
 bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
-                                int K, const void* bias, int wm, int grid_req, hipStream_t s, const PwGroup* group) {
+                                int K, const void* bias, int wm, int grid_req, hipStream_t s, const PwGroup* group,
+                                int rw) {
   const PwGroup grp = group != nullptr ? *group : PwGroup{nullptr, nullptr, 0};
   const bool grouped = group != nullptr;
   if (grouped && (bias != nullptr || epi == PW_EPI_ADD)) return false;
-  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2)) return false;
+  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4)) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;
   if (epi == PW_EPI_ADD && bias != nullptr) return false;
@@ -295,12 +309,19 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   auto* w = static_cast<const unsigned short*>(Wp);
   auto* c = static_cast<unsigned short*>(C);
   auto* b = static_cast<const unsigned short*>(bias);
-#define PW_LAUNCH(WM_, E_)                                                                                 \
-  do {                                                                                                     \
-    if (grouped)                                                                                           \
-      pgw_kernel<WM_, E_, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp);  \
-    else                                                                                                   \
-      pgw_kernel<WM_, E_, false><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+#define PW_LAUNCH1(WM_, E_, RW_)                                                                               \
+  do {                                                                                                         \
+    if (grouped)                                                                                               \
+      pgw_kernel<WM_, E_, true, RW_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp);  \
+    else                                                                                                       \
+      pgw_kernel<WM_, E_, false, RW_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+  } while (0)
+#define PW_LAUNCH(WM_, E_)        \
+  do {                            \
+    if (rw == 4)                  \
+      PW_LAUNCH1(WM_, E_, 4);     \
+    else                          \
+      PW_LAUNCH1(WM_, E_, 2);     \
   } while (0)
 #define PW_EPIS(WM_)                                          \
   switch (epi) {                                              \
@@ -316,6 +337,7 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   PW_EPIS(2)
 #undef PW_EPIS
 #undef PW_LAUNCH
+#undef PW_LAUNCH1
 }
 
 }  // namespace hipserve

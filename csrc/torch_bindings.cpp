@@ -696,7 +696,7 @@ void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int
 // pack_decode_weight(w[N, K], glu) (flat, ceil(N/128)*128*K bf16). epi as prefill_gemm
 // (2 / 3 need the glu packing); bias (epi 0 only) bf16 [N] or None; wm 1 or 2.
 void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
-                         const c10::optional<at::Tensor>& bias, int64_t wm, int64_t grid) {
+                         const c10::optional<at::Tensor>& bias, int64_t wm, int64_t grid, int64_t rw) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(wp.is_contiguous(), "prefill_gemm_packed: packed weight must be contiguous");
   const int M = x.size(0), K = x.size(1);
@@ -712,7 +712,8 @@ void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor&
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_prefill_gemm_packed((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
-                                                   wp.data_ptr(), M, (int)N, K, bp, (int)wm, (int)grid, cur_stream()),
+                                                   wp.data_ptr(), M, (int)N, K, bp, (int)wm, (int)grid, cur_stream(),
+                                                   nullptr, (int)rw),
               "prefill_gemm_packed: unsupported (glu needs N % 128, bias only with epi 0, 32-bit offsets)");
 }
 
@@ -720,7 +721,7 @@ void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor&
 // with tile 128 * wm + moe_gather), wp = [E, packed expert] (pack_decode_weight per
 // expert, glu for w13), tile_expert / num_tiles from moe_align. epi 0 or 2 / 3.
 void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
-                                 const at::Tensor& tile_expert, const at::Tensor& num_tiles, int64_t wm) {
+                                 const at::Tensor& tile_expert, const at::Tensor& num_tiles, int64_t wm, int64_t rw) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(wp.dim() == 2 && wp.is_contiguous(), "prefill_gemm_packed_grouped: wp [E, packed]");
   const int M = x.size(0), K = x.size(1);
@@ -734,7 +735,7 @@ void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at:
   hipserve::PwGroup grp{tile_expert.data_ptr<int>(), num_tiles.data_ptr<int>(), (long)wp.size(1)};
   TORCH_CHECK(hipserve::launch_prefill_gemm_packed((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
                                                    wp.data_ptr(), M, (int)N, K, nullptr, (int)wm, 0, cur_stream(),
-                                                   &grp),
+                                                   &grp, (int)rw),
               "prefill_gemm_packed_grouped: unsupported");
 }
 
@@ -1115,7 +1116,7 @@ void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots
   CHECK_DEV(ids);
   TORCH_CHECK(ids.scalar_type() == at::kInt && slots.scalar_type() == at::kInt &&
               tile_expert.scalar_type() == at::kInt && pair_slot.scalar_type() == at::kInt);
-  TORCH_CHECK(E <= 128 && (tile == 16 || tile == 32 || tile == 64 || tile == 256));
+  TORCH_CHECK(E <= 128 && (tile == 16 || tile == 32 || tile == 64 || tile == 128 || tile == 256));
   const int npairs = ids.numel();
   TORCH_CHECK(slots.numel() >= npairs + E * (tile - 1) && slots.numel() % tile == 0,
               "slots capacity must cover padding and be a multiple of the tile");
@@ -1307,8 +1308,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
-  m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0) -> ()");
-  m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1) -> ()");
+  m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
+  m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");

@@ -1103,9 +1103,9 @@ class LlamaModel:
         if packed:  # packed-layout grouped expert GEMMs, SiLU-GLU in the first's epilogue
             p13, p2 = lw.moe_packed
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-            op.prefill_gemm_packed_grouped(act, xs, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM)
+            op.prefill_gemm_packed_grouped(act, xs, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
-            op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM)
+            op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
         elif tile == 256:  # hand-written grouped expert GEMMs, SiLU-GLU in the first's epilogue
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
             op.prefill_gemm_grouped(act, xs, lw.w13, tile_expert, 2, pgemm.VARIANT)

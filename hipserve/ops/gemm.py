@@ -432,6 +432,8 @@ def run_choice(c, out, x, w, wp=None):
 
 # packed prefill GEMM (prefill_gemm_packed.hip) workgroup shape: 1 = 128 x 512, 2 = 256 x 256
 PW_WM = int(__import__("os").environ.get("HIPSERVE_PW_WM", "1"))
+# weight register sets in flight (2 or 4 32-deep slots ahead of the MFMAs)
+PW_RW = int(__import__("os").environ.get("HIPSERVE_PW_RW", "4"))
 
 
 def packed_prefill(x: torch.Tensor, w: PackedLinear, epi: int = 0, out: torch.Tensor | None = None,
@@ -441,7 +443,7 @@ def packed_prefill(x: torch.Tensor, w: PackedLinear, epi: int = 0, out: torch.Te
     M = x.shape[0]
     if out is None:
         out = torch.empty(M, w.N // 2 if epi in (2, 3) else w.N, device=x.device, dtype=x.dtype)
-    torch.ops.hipserve.prefill_gemm_packed(out, x, w.wp, w.N, epi, bias, PW_WM)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, w.wp, w.N, epi, bias, PW_WM, 0, PW_RW)
     return out
 
 

@@ -36,14 +36,15 @@ SHAPES = [(256, 512, 256), (300, 640, 1024), (1000, 200, 512), (77, 1536, 768), 
 
 # grid: 0 = persistent (one workgroup per CU walking the tiles), 3 = three workgroups
 # walking many tiles each (uneven counts), 1 << 30 = one tile per workgroup
+@pytest.mark.parametrize("rw", [2, 4])  # weight slots in flight
 @pytest.mark.parametrize("grid", [0, 3, 1 << 30])
 @pytest.mark.parametrize("wm", [1, 2])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_packed_store(M, N, K, wm, grid):
+def test_packed_store(M, N, K, wm, grid, rw):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
     out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm_packed(out, x, _pack(w), N, 0, None, wm, grid)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, _pack(w), N, 0, None, wm, grid, rw)
     want = x.float() @ w.float().t()
     torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 
@@ -68,21 +69,22 @@ def test_packed_residual_add(M, N, K, wm):
     x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
     res0 = _rnd(g, M, N)
     res = res0.clone()
-    torch.ops.hipserve.prefill_gemm_packed(res, x, _pack(w), N, 1, None, wm, 7)  # 7 workgroups: many tiles each
+    torch.ops.hipserve.prefill_gemm_packed(res, x, _pack(w), N, 1, None, wm, 7, 4)  # 7 workgroups: many tiles each
     h = (x.float() @ w.float().t()).to(torch.bfloat16).float()
     want = (h + res0.float()).to(torch.bfloat16).float()
     torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("rw", [2, 4])
 @pytest.mark.parametrize("grid", [0, 5])
 @pytest.mark.parametrize("wm,act", [(1, "silu"), (2, "silu"), (1, "gelu"), (2, "gelu")])
 @pytest.mark.parametrize("M,I,K", [(300, 256, 1024), (1000, 192, 512), (2049, 64, 256), (513, 1344, 768)])
-def test_packed_glu(M, I, K, wm, act, grid):
+def test_packed_glu(M, I, K, wm, act, grid, rw):
     g = torch.Generator(device=DEV).manual_seed(11 + M)
     x, w = _rnd(g, M, K), _rnd(g, 2 * I, K, scale=0.05)
     out = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
     torch.ops.hipserve.prefill_gemm_packed(out, x, _pack(w, glu=True), 2 * I, 2 if act == "silu" else 3, None, wm,
-                                           grid)
+                                           grid, rw)
     gu = (x.float() @ w.float().t()).to(torch.bfloat16).float()
     f = torch.nn.functional.silu if act == "silu" else (lambda t: torch.nn.functional.gelu(t, approximate="tanh"))
     want = f(gu[:, :I]) * gu[:, I:]

@@ -49,10 +49,14 @@ def main():
             return best
         r = {"M": M, "N": N, "K": K, "epi": a.epi, "blas_ms": round(t(lambda: [F.linear(x, w) for w in ws]), 4)}
         for wm in (1, 2):
-            r[f"wm{wm}_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, wm) for wp in wps]), 4)
+            for rw in (2, 4):
+                r[f"wm{wm}_rw{rw}_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, wm, 0, rw)
+                                                          for wp in wps]), 4)
         # one tile per workgroup (non-persistent launch)
-        r["wm1_1tile_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, 1, 1 << 30)
-                                             for wp in wps]), 4)
+        for rw in (2, 4):
+            r[f"wm1_rw{rw}_1tile_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, 1, 1 << 30, rw)
+                                                         for wp in wps]), 4)
+        r["wm1_ms"] = min(v for k, v in r.items() if k.startswith("wm1_"))
         r["wm1_TFs"] = round(2 * M * N * K / r["wm1_ms"] / 1e9, 1)
         r["blas_TFs"] = round(2 * M * N * K / r["blas_ms"] / 1e9, 1)
         print(json.dumps(r), flush=True)

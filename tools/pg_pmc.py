@@ -27,7 +27,7 @@ for v in os.environ.get("PG_VARIANTS", "2").split():
             if wp is None:
                 wp = torch.empty(-(-N // 128) * 128 * K, device="cuda", dtype=torch.bfloat16)
                 torch.ops.hipserve.pack_decode_weight(wp, w, False)
-            torch.ops.hipserve.prefill_gemm_packed(out, x, wp, N, 0, None, int(v[1:]))
+            torch.ops.hipserve.prefill_gemm_packed(out, x, wp, N, 0, None, int(v[1]), 0, int(os.environ.get("PW_RW", "4")))
         else:
             torch.ops.hipserve.prefill_gemm(out, x, w, 0, int(v))
     torch.cuda.synchronize()
