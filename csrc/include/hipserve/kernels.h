@@ -204,7 +204,8 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
 //   (merged [gate; up], N = 2I, I % 64 == 0), C = act [M, I]
 constexpr int PW_EPI_STORE = 0, PW_EPI_ADD = 1, PW_EPI_GLU = 2, PW_EPI_GEGLU = 3;
 // grid_req <= 0: persistent (one workgroup per CU walking the tiles), else that many workgroups.
-// rw: weight register sets in flight (2 or 4 32-deep slots ahead).
+// rw: weight register sets in flight (2 or 4 32-deep slots ahead; 5 = 4 with each reload
+// issued one MFMA group later).
 // group (MoE experts, STORE / GLU): X = expert-sorted slots in 128 * wm-row tiles, m-tile tm
 // uses expert tile_expert[tm]'s packed weight at Wp + e * estride; *num_tiles valid m-tiles.
 struct PwGroup {

@@ -101,7 +101,7 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
 // (moe_align with tile BM, moe_gather); m-tile tm multiplies expert grp.tile_expert[tm]'s
 // packed weight (Wp + e * estride) and only the first *grp.num_tiles m-tiles (the
 // device-side count: no host round trip, graph-capturable) are walked.
-template <int WM, int EPI, bool kGroup, int RW>
+template <int WM, int EPI, bool kGroup, int RW, bool LDLY = false, int DBG = 0>
 __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
     const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
     unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n,
@@ -165,6 +165,9 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 
   f32x4 acc[8][8];
   u32x4 w[RW][8], xa[8], xb[8];
+  int wvoj[RW];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) wvoj[j] = wvo + j * 1024;
 
   // prologue (first tile only): stage 0 in LDS, stages 1 .. XS in registers, weight
   // slots 0 .. RW - 1 in flight; later tiles find theirs loaded by the previous tile's
@@ -181,8 +184,12 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 #pragma unroll
   for (int i = 0; i < 8; ++i) xa[i] = xfrag(0, 0, i);
 
-  // one 32-deep slot: J (compile time) = slot index inside the RW-slot loop body
-  auto slot = [&](auto jc, int q0, int s0) {
+  // one 32-deep slot: J (compile time) = slot index inside the RW-slot loop body. The
+  // weight loads of one loop body all stream the same tile (nq % RW == 0): their buffer
+  // resource and K offset are chosen once per body (wrs, wk), so a load costs one scalar
+  // add — per-load selects cost ~6 SALU each and delayed the next MFMA group
+  // (tools/asm_stats.py)
+  auto slot = [&](auto jc, int s0, const __amdgpu_buffer_rsrc_t& wrs, int wk) {
     constexpr int J = decltype(jc)::value, H = J & 1;
     const int s = s0 + J / 2, buf = s & 1;
     constexpr int XI = (J / 2 + 1) % XS;  // staging set of stage s + 1 (s0 is a multiple of XS)
@@ -190,11 +197,24 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     for (int rg = 0; rg < 8; ++rg) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) pw_mfma(acc[rg][i], w[J][rg], H ? xb[i] : xa[i]);
-      w[J][rg] = wload(q0 + J + RW, rg);
+      // slot J's 1 KiB offset rides in a per-slot VGPR offset: 8 scalar adds per body, not 32.
+      // LDLY: reload a group's weight register one group later, so the load is not issued
+      // right behind the MFMAs still reading that register
+      if constexpr (DBG & 1) {  // diagnostic: no weight loads (registers keep stale data)
+      } else if constexpr (DBG & 4) {  // diagnostic: half the weight loads (even row groups)
+        if ((rg & 1) == 0) w[J][rg] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + rg * 8192, 0);
+      } else if constexpr (LDLY) {
+        if (rg > 0) w[J][rg - 1] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + (rg - 1) * 8192, 0);
+        if (rg == 7) w[J][7] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + 7 * 8192, 0);
+      } else {
+        w[J][rg] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + rg * 8192, 0);
+      }
       if constexpr (H == 0) {
         xb[rg] = xfrag(buf, 1, rg);
-        if (rg == 2) xstore(buf ^ 1, xst[XI]);     // stage s + 1 (loaded XS stages ago)
-        if (rg == 3) xload(s + 1 + XS, xst[XI]);
+        if constexpr ((DBG & 2) == 0) {  // diagnostic 2: no X staging (LDS keeps stale data)
+          if (rg == 2) xstore(buf ^ 1, xst[XI]);     // stage s + 1 (loaded XS stages ago)
+          if (rg == 3) xload(s + 1 + XS, xst[XI]);
+        }
       } else {
         xa[rg] = xfrag(buf ^ 1, 0, rg);            // stage s + 1, visible since the barrier
       }
@@ -214,11 +234,15 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
       for (int i = 0; i < 8; ++i) acc[rg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int q0 = 0; q0 < nq; q0 += RW) {  // nq % 8 == 0; a tile starts in LDS buffer 0
       const int s0 = q0 >> 1;
-      slot(I0(), q0, s0);
-      slot(I1(), q0, s0);
+      const bool wn = q0 + RW >= nq;  // this body's weight loads stream the next tile
+      const int wq = wn ? q0 + RW - nq : q0 + RW;
+      const __amdgpu_buffer_rsrc_t wrs = wn ? nxt.w : cur.w;
+      const int wk = (wq >> 3) * 65536 + (wq & 7) * 1024;  // (wq & 7) + J <= 7
+      slot(I0(), s0, wrs, wk);
+      slot(I1(), s0, wrs, wk);
       if constexpr (RW == 4) {
-        slot(I2(), q0, s0);
-        slot(I3(), q0, s0);
+        slot(I2(), s0, wrs, wk);
+        slot(I3(), s0, wrs, wk);
       }
     }
 
@@ -288,7 +312,7 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   const PwGroup grp = group != nullptr ? *group : PwGroup{nullptr, nullptr, 0};
   const bool grouped = group != nullptr;
   if (grouped && (bias != nullptr || epi == PW_EPI_ADD)) return false;
-  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4)) return false;
+  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4 && rw != 5 && (rw < 11 || rw > 15))) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;
   if (epi == PW_EPI_ADD && bias != nullptr) return false;
@@ -316,12 +340,22 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
     else                                                                                                       \
       pgw_kernel<WM_, E_, false, RW_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
   } while (0)
-#define PW_LAUNCH(WM_, E_)        \
-  do {                            \
-    if (rw == 4)                  \
-      PW_LAUNCH1(WM_, E_, 4);     \
-    else                          \
-      PW_LAUNCH1(WM_, E_, 2);     \
+#define PW_LAUNCH(WM_, E_)                                                                                   \
+  do {                                                                                                       \
+    if (rw == 4)                                                                                             \
+      PW_LAUNCH1(WM_, E_, 4);                                                                                \
+    else if (rw == 2)                                                                                        \
+      PW_LAUNCH1(WM_, E_, 2);                                                                                \
+    else if (rw >= 11 && rw <= 15 && !grouped && WM_ == 1 && E_ == 0) {                                        \
+      if (rw == 11) pgw_kernel<1, 0, false, 4, false, 1><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+      if (rw == 12) pgw_kernel<1, 0, false, 4, false, 2><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+      if (rw == 13) pgw_kernel<1, 0, false, 4, false, 3><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+      if (rw == 14) pgw_kernel<1, 0, false, 4, false, 4><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+      if (rw == 15) pgw_kernel<1, 0, false, 4, false, 6><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+    } else if (grouped)                                                                                      \
+      pgw_kernel<WM_, E_, true, 4, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp);  \
+    else                                                                                                     \
+      pgw_kernel<WM_, E_, false, 4, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
   } while (0)
 #define PW_EPIS(WM_)                                          \
   switch (epi) {                                              \

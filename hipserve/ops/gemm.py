@@ -434,6 +434,9 @@ def run_choice(c, out, x, w, wp=None):
 PW_WM = int(__import__("os").environ.get("HIPSERVE_PW_WM", "1"))
 # weight register sets in flight (2 or 4 32-deep slots ahead of the MFMAs)
 PW_RW = int(__import__("os").environ.get("HIPSERVE_PW_RW", "4"))
+# workgroups: 0 = persistent (one per CU walking the tiles), large = one tile each. One tile
+# per workgroup measured 2-5 % faster at 8192 rows (profiles/r4_pw_scaling_v3.log)
+PW_GRID = int(__import__("os").environ.get("HIPSERVE_PW_GRID", str(1 << 30)))
 
 
 def packed_prefill(x: torch.Tensor, w: PackedLinear, epi: int = 0, out: torch.Tensor | None = None,
@@ -443,7 +446,7 @@ def packed_prefill(x: torch.Tensor, w: PackedLinear, epi: int = 0, out: torch.Te
     M = x.shape[0]
     if out is None:
         out = torch.empty(M, w.N // 2 if epi in (2, 3) else w.N, device=x.device, dtype=x.dtype)
-    torch.ops.hipserve.prefill_gemm_packed(out, x, w.wp, w.N, epi, bias, PW_WM, 0, PW_RW)
+    torch.ops.hipserve.prefill_gemm_packed(out, x, w.wp, w.N, epi, bias, PW_WM, PW_GRID, PW_RW)
     return out
 
 

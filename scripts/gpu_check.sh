@@ -115,6 +115,9 @@ for s in $steps; do
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
+    prof70) prof_run prof70 --model llama-3-70b ;;
+    bench_mixtral_packed) bench_named mixtral_packed HIPSERVE_MOE_PACKED_PREFILL=1 -- --model mixtral-8x7b --concurrency 32 ;;
+    bench_mixtral_old) bench_named mixtral_old HIPSERVE_MOE_PACKED_PREFILL=0 -- --model mixtral-8x7b --concurrency 32 ;;
     prof_qwen3moe) prof_run profqm --model qwen3-30b-a3b ;;
     prof_gemma3) prof_run profg3 --model gemma-3-27b ;;
     prof_g27fp8) prof_run profg3f8 --model gemma-3-27b --quantization fp8 ;;

@@ -49,11 +49,11 @@ def main():
             return best
         r = {"M": M, "N": N, "K": K, "epi": a.epi, "blas_ms": round(t(lambda: [F.linear(x, w) for w in ws]), 4)}
         for wm in (1, 2):
-            for rw in (2, 4):
+            for rw in ((4, 11, 12, 13, 14, 15) if wm == 1 else (2,)):
                 r[f"wm{wm}_rw{rw}_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, wm, 0, rw)
                                                           for wp in wps]), 4)
         # one tile per workgroup (non-persistent launch)
-        for rw in (2, 4):
+        for rw in (4, 5):
             r[f"wm1_rw{rw}_1tile_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, 1, 1 << 30, rw)
                                                          for wp in wps]), 4)
         r["wm1_ms"] = min(v for k, v in r.items() if k.startswith("wm1_"))
