@@ -148,41 +148,6 @@ constexpr int DG_GLU = 1, DG_PARTIAL = 2;
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, bool packed, int flags, hipStream_t s);
 
-// decode_layer.hip — decode GEMM (packed weights, RT = 1, M <= 64) with the layer's
-// epilogue inside the launch: split-K slices reduced by the tile's last-arriving
-// workgroup (ws [S, M, N] fp32 + per-tile counters, zero between calls), then
-//   fix 1 (ADD):  residual[M, N] = bf16(bf16(h) + residual), ss_out[N/128, M] = per-tile row sums of squares
-//   fix 2 (ROPE): q -> q_out (rotated), k / v -> the paged cache (bias, q/k RMSNorm optional)
-//   fix 3 (GLU):  out = act [M, N/2] (gate/up-interleaved packing)
-// norm_in: x is the bf16 residual; x is normalised on load with inv = rsqrt(sum(ss_in[Tin, M]) / K + eps)
-// and the bf16 norm weight norm_w [K].
-struct DgfArgs {
-  float* ws;
-  int* counters;
-  const float* ss_in;
-  int Tin;
-  const unsigned short* norm_w;
-  float eps;
-  unsigned short* residual;
-  float* ss_out;
-  unsigned short* q_out;
-  long q_stride;
-  const long* positions;
-  const long* slots;
-  const float* cos_sin;
-  unsigned short* k_cache;
-  unsigned short* v_cache;
-  int nq, nkv, D, block_size, rope_mode;
-  const unsigned short* bias;
-  const float* qw;
-  const float* kw;
-  unsigned short* out;
-  long out_stride;
-};
-bool dgf_supported(int fix, bool norm_in, int M, int N, int K, int S);
-bool launch_dgf(int fix, bool norm_in, const DgfArgs& A, const void* x, long x_stride, const void* w, int M, int N,
-                int K, int S, hipStream_t s);
-
 // prefill_gemm.hip — C[M, N] = A[M, K] . B[N, K]^T (bf16, 256x256x64 MFMA tiles, LDS-DMA
 // staging), N % 256 == 0, K % 64 == 0, any M. Epilogues:
 //   PG_EPI_STORE  C = bf16(acc)
@@ -191,7 +156,7 @@ bool launch_dgf(int fix, bool norm_in, const DgfArgs& A, const void* x, long x_s
 //   PG_EPI_GEGLU  as GLU with tanh-GELU(gate) * up (Gemma)
 constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2, PG_EPI_GEGLU = 3;
 struct PgEpi {
-  int variant;               // 1: one-stage-ahead loop, 2: half-tile pipeline (default)
+  int variant;               // kept for the API: 2 = the half-tile pipeline (the only one left)
   const int* tile_expert;    // grouped (MoE): expert of each 256-row tile of A, -1 = unused
   long b_estride;            // grouped: elements between consecutive experts' weights
 };
@@ -243,9 +208,6 @@ bool launch_fp8_decode_gemm(float* ws, const void* xq, const PgF8& W, int M, int
 // inter] + xs [rows] (and bf16 into out if non-null); inter / 8 <= 4096. activation.hip
 bool launch_glu_quant(bool gelu, void* out, void* q8, float* xs, const void* in, long rows, int inter,
                       long in_stride, hipStream_t s);
-// decode_fused.hip: splitk_glu with the per-token e4m3 act for an FP8 down projection
-bool launch_splitk_glu_q8(void* act, const float* ws, int S, int M, int I, bool gelu, void* q8, float* xs8,
-                          hipStream_t s);
 // per-token dynamic e4m3 quantisation: xs[m] = max|x[m, :]| / 448, q = sat(x / xs)
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s);
 void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);

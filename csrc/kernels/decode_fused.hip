@@ -421,66 +421,6 @@ __global__ __launch_bounds__(256) void splitk_glu_kernel(unsigned short* __restr
   if (act16 != nullptr) *reinterpret_cast<u16x8*>(act16 + m * act_stride + c * 8) = f16_pairs8(o);
 }
 
-// splitk_glu for an FP8 down projection (W8A8 decode GEMM): one 1024-thread block per
-// row keeps the row's act in registers, reduces its amax and writes the per-token e4m3
-// copy + scale (bit-identical to splitk_glu -> act_quant_fp8); the bf16 act is written
-// only if act != nullptr. I / 8 <= 4096.
-template <bool kGelu, int VPT>
-__global__ __launch_bounds__(1024) void splitk_glu_q8_kernel(unsigned short* __restrict__ act,
-                                                             const float* __restrict__ ws, int S, int M, int I,
-                                                             unsigned char* __restrict__ q8,
-                                                             float* __restrict__ xs8) {
-  __shared__ float red[16];
-  const int m = blockIdx.x;
-  const int nvec = I >> 3;
-  const long N = 2L * I, slice = (long)M * N;
-  u16x8 a[VPT];
-  float amax = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int c = threadIdx.x + i * 1024;
-    if (c < nvec) {
-      float g[8], u[8];
-      sum8_bf16(g, ws + m * N + c * 8, slice, S);
-      sum8_bf16(u, ws + m * N + I + c * 8, slice, S);
-      u16x8 gb, ub;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        gb[j] = f32_to_bf16(g[j]);
-        ub[j] = f32_to_bf16(u[j]);
-      }
-      a[i] = kGelu ? gelu_mul8(gb, ub) : silu_mul8(gb, ub);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(bf16_to_f32(a[i][j])));
-      if (act != nullptr) *reinterpret_cast<u16x8*>(act + (long)m * I + c * 8) = a[i];
-    }
-  }
-  amax = block_max(amax, red);
-  const float inv = amax > 0.f ? 448.f / amax : 1.f;
-  if (threadIdx.x == 0) xs8[m] = amax > 0.f ? amax / 448.f : 1.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int c = threadIdx.x + i * 1024;
-    if (c < nvec) *reinterpret_cast<uint2*>(q8 + (long)m * I + c * 8) = e4m3_8(a[i], inv);
-  }
-}
-
-bool launch_splitk_glu_q8(void* act, const float* ws, int S, int M, int I, bool gelu, void* q8, float* xs8,
-                          hipStream_t s) {
-  const int nvec = I / 8;
-  if (M <= 0 || I % 8 || nvec > 4096) return false;
-  auto* a = static_cast<unsigned short*>(act);
-  auto* q = static_cast<unsigned char*>(q8);
-#define SGQ(V)                                                                                  \
-  if (gelu) splitk_glu_q8_kernel<true, V><<<M, 1024, 0, s>>>(a, ws, S, M, I, q, xs8);           \
-  else splitk_glu_q8_kernel<false, V><<<M, 1024, 0, s>>>(a, ws, S, M, I, q, xs8);               \
-  return true;
-  if (nvec <= 1024) { SGQ(1) }
-  if (nvec <= 2048) { SGQ(2) }
-  SGQ(4)
-#undef SGQ
-}
-
 void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M, int I, bool gelu, hipStream_t s,
                        void* act16) {
   if (M <= 0) return;

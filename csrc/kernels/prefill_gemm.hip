@@ -113,81 +113,6 @@ HS_DEVICE void pg_epilogue(f32x4 (&acc)[4][8], unsigned char* lds, unsigned shor
   }
 }
 
-template <int EPI>
-__global__ __launch_bounds__(PG_T) void pgemm_kernel(const unsigned short* __restrict__ A, long lda,
-                                                     const unsigned short* __restrict__ B, long ldb,
-                                                     unsigned short* __restrict__ C, long ldc, int M, int N, int K,
-                                                     int tiles_m, int tiles_n, PgEpi E) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * PG_TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
-  const int m0 = tm * PG_BM, n0 = tn * PG_BN;
-  const int nk = K / PG_BK;
-
-  // staging sources: wave w fills rows [32w, 32w + 32) of both tiles, 8 rows per instruction
-  const unsigned short* asrc[4];
-  const unsigned short* bsrc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = wave * 32 + i * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at physical chunk lane & 7
-    asrc[i] = A + (long)min(m0 + r, M - 1) * lda + lc * 8;
-    bsrc[i] = B + (long)pg_brow<EPI>(n0, tn, r, N) * ldb + lc * 8;
-  }
-  auto stage = [&](int buf, int kt) {
-    unsigned char* base = lds + buf * 2 * PG_TILE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kt * PG_BK),
-                                       (lds_ptr_t)(base + (wave * 32 + i * 8) * 128), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + kt * PG_BK),
-                                       (lds_ptr_t)(base + PG_TILE + (wave * 32 + i * 8) * 128), 16, 0, 0);
-  };
-  // fragment read offsets: rows (lane & 15) + 16 i, chunk 4 s + (lane >> 4), swizzled
-  const int fr = lane & 15, fq = lane >> 4;
-  const int sw = (fr >> 1) & 7;
-  const int a_off = (wr * 128 + fr) * 128, b_off = PG_TILE + (wc * 64 + fr) * 128;
-  const int ch0 = ((0 + fq) ^ sw) * 16, ch1 = ((4 + fq) ^ sw) * 16;
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
-    const unsigned char* sb = lds + buf * 2 * PG_TILE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = s ? ch1 : ch0;
-      u16x8 bf[4], af[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u16x8*>(sb + b_off + j * 2048 + ch);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const u16x8*>(sb + a_off + i * 2048 + ch);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
-                                                              __builtin_bit_cast(bf16x8, af[i]), acc[j][i], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
-}
-
 // ---- v2: half-tile pipeline. Each K tile runs as 4 phases (one 64 x 32 output
 // quadrant of the wave's 128 x 64 block per phase: 16 MFMAs) with raw s_barriers
 // and counted vmcnt waits, so LDS-DMA traffic of the next two tiles stays in flight
@@ -351,219 +276,6 @@ __global__ __launch_bounds__(PG_T) void pgemm2_kernel(const unsigned short* __re
     }
   }
   pg_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
-}
-
-// ---- v5: hipBLASLt's wave shape. 256 threads = 4 waves as 2 (m) x 2 (n), each a
-// 128 x 128 output block: 64 accumulators = all 256 AGPRs, one wave per SIMD, half the
-// LDS fragment traffic per MFMA of v2's 128 x 64 blocks (r3_pgemm_pmc.md). K tile 32
-// in three LDS stages of 32 KiB (A then B, 256 rows x 64 B). Staging goes through
-// VGPRs (buffer_load_dwordx4 four tiles ahead into two register tiles, ds_write_b128
-// two tiles ahead), not LDS-DMA: at one wave per SIMD an LDS-DMA piece holds its wave
-// for 60-185 cycles (MI355X_MICROARCH.md, cycle constants), 8 per tile on top of 64
-// MFMAs x 16; a load and a ds_write fit in MFMA issue gaps. Fragments of the next
-// tile are read behind the current tile's 64 MFMAs; one barrier per tile. The MFMAs
-// are inline asm on AGPR accumulators ("+a"): with the builtin, hipcc shuttled the 256
-// accumulators between AGPRs and VGPRs inside the loop. 64-byte rows: 16-B chunk c of
-// row r sits at chunk c ^ ((r >> 2) & 2). A ds_read_b128 lane group
-// (MI355X_MICROARCH.md §LDS: {0-3, 12-15, 20-27}, ...) holds rows 0-3 and 12-15 of one
-// chunk and rows 4-11 of the next; with this swizzle its 16 lanes land on the 16
-// different 16-B slots of a bank row. ds_write_b128 (8 contiguous lanes = 2 rows x 4
-// chunks per group) is conflict-free for any per-row chunk permutation.
-constexpr int P5_T = 256, P5_BK = 32, P5_STAGE = 2 * 256 * 64, P5_NS = 3;
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-HS_DEVICE i32x4 p5_rsrc(const void* p, long bytes) {  // raw buffer descriptor, stride 0
-  const unsigned long a = reinterpret_cast<unsigned long>(p);
-  return i32x4{(int)(a & 0xffffffffu), (int)((a >> 32) & 0xffff), (int)min(bytes, 0x7fffffffL), 0x00020000};
-}
-
-HS_DEVICE void p5_mfma(f32x4& acc, const u32x4& b, const u32x4& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
-}
-
-// lane holds C[m][n .. n+3], m = m0 + 128 wr + 16 i + fr, n = n0 + 128 wc + 16 j + 4 fq (acc[j][i])
-template <int EPI>
-HS_DEVICE void p5_epilogue(f32x4 (&acc)[8][8], unsigned char* lds, unsigned short* __restrict__ C, long ldc, int M,
-                           int m0, int n0, int tn, int wr, int wc, int fr, int fq, int lane) {
-  if constexpr (EPI == PG_EPI_STORE || EPI == PG_EPI_ADD) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wr * 128 + i * 16 + fr;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        uint2* dst = reinterpret_cast<uint2*>(C + (long)m * ldc + n0 + wc * 128 + j * 16 + 4 * fq);
-        uint2 v;
-        if constexpr (EPI == PG_EPI_ADD) {
-          const uint2 r = *dst;
-          const unsigned short rr[4] = {(unsigned short)(r.x & 0xffff), (unsigned short)(r.x >> 16),
-                                        (unsigned short)(r.y & 0xffff), (unsigned short)(r.y >> 16)};
-          float o[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = bf16_to_f32(f32_to_bf16(acc[j][i][e])) + bf16_to_f32(rr[e]);
-          v.x = pack_bf16x2(o[0], o[1]);
-          v.y = pack_bf16x2(o[2], o[3]);
-        } else {
-          v.x = pack_bf16x2(acc[j][i][0], acc[j][i][1]);
-          v.y = pack_bf16x2(acc[j][i][2], acc[j][i][3]);
-        }
-        *dst = v;
-      }
-    }
-  } else if constexpr (EPI == PG_EPI_GLU || EPI == PG_EPI_GEGLU) {
-    // wc = 1 holds the up rows of the gate columns wc = 0 holds: bf16(up) through LDS
-    uint2* ex = reinterpret_cast<uint2*>(lds);  // [2 wr][8 j][8 i][64 lanes] = 64 KiB
-    if (wc == 1) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          ex[((wr * 8 + j) * 8 + i) * 64 + lane] = uint2{pack_bf16x2(acc[j][i][0], acc[j][i][1]),
-                                                         pack_bf16x2(acc[j][i][2], acc[j][i][3])};
-    }
-    __syncthreads();
-    if (wc == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + wr * 128 + i * 16 + fr;
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint2 u = ex[((wr * 8 + j) * 8 + i) * 64 + lane];
-          const unsigned short uu[4] = {(unsigned short)(u.x & 0xffff), (unsigned short)(u.x >> 16),
-                                        (unsigned short)(u.y & 0xffff), (unsigned short)(u.y >> 16)};
-          unsigned short o[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            o[e] = EPI == PG_EPI_GEGLU ? gelu_mul1(f32_to_bf16(acc[j][i][e]), uu[e])
-                                       : silu_mul1(f32_to_bf16(acc[j][i][e]), uu[e]);
-          *reinterpret_cast<uint2*>(C + (long)m * ldc + tn * 128 + j * 16 + 4 * fq) =
-              uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
-        }
-      }
-    }
-  }
-}
-
-template <int EPI, bool kGroup>
-__global__ __launch_bounds__(P5_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgemm5_kernel(
-    const unsigned short* __restrict__ A, long lda, const unsigned short* __restrict__ B, long ldb,
-    unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n, PgEpi E) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[P5_NS * P5_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tn = bid / tiles_m, tm = bid - tn * tiles_m;
-  const int m0 = tm * PG_BM, n0 = tn * PG_BN;
-  if constexpr (kGroup) {
-    const int e = E.tile_expert[tm];
-    if (e < 0) return;
-    B += (long)e * E.b_estride;
-  }
-  const int nk = K / P5_BK;
-
-  // staging: a register tile holds a PAIR of K tiles (64 k = one 128-byte line per row,
-  // so every line fetched from L2 is used whole; loading 64-byte halves per K tile
-  // doubled the L2 -> L1 traffic). Wave w loads rows [64 w, 64 w + 64) of A (t = 0..7)
-  // and of B (t = 8..15), 8 rows per instruction: lane l takes row 8 (t & 7) + rl,
-  // rl = 2 (l >> 4) + ((l >> 2) & 1), K tile h = (l >> 3) & 1 of the pair, 16-byte chunk
-  // l & 3 of it. Each 8-lane ds_write_b128 group is then two whole 64-byte rows of one
-  // stage (conflict-free); the instruction still covers 8 whole 128-byte lines.
-  const int rl = 2 * (lane >> 4) + ((lane >> 2) & 1), half = (lane >> 3) & 1, c4 = lane & 3;
-  unsigned int voff[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int op = t >> 3, r = wave * 64 + (t & 7) * 8 + rl;
-    const long row = op == 0 ? (long)min(m0 + r, M - 1) : (long)pg_brow<EPI>(n0, tn, r, N);
-    voff[t] = (unsigned)(row * (op == 0 ? lda : ldb) * 2 + (half * 4 + c4) * 16);
-  }
-  auto dso = [&](int t) {  // LDS byte offset inside a stage: row r, chunk c4 swizzled; (r >> 2) & 2 == (t & 1) * 2
-    const int op = t >> 3, r = wave * 64 + (t & 7) * 8 + rl;
-    return op * (P5_STAGE / 2) + r * 64 + ((c4 ^ ((t & 1) * 2)) * 16);
-  };
-  const i32x4 rsrc[2] = {p5_rsrc(A, (long)M * lda * 2), p5_rsrc(B, (long)N * ldb * 2)};
-  u32x4 g[16];  // the register tile in flight
-  // the K step rides in soffset, clamped to the last pair: the loop below runs the same
-  // code for every tile and loads / stages / reads up to four tiles past the end, which
-  // it never uses. The loads are asm: as builtins the compiler sank the warm-up's loads
-  // into one group before the loop, and its own vmcnt waits at the loop head then
-  // drained more than the tile they were for; here the waits are explicit
-  auto gload = [&](int t, int kt) {  // kt even: pair (kt, kt + 1)
-    const unsigned vo = voff[t];
-    const i32x4 rs = rsrc[t >> 3];
-    const int so = min(kt, nk - 2) * P5_BK * 2;
-    u32x4 v;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(vo), "s"(rs), "s"(so) : "memory");
-    g[t] = v;
-  };
-  const int fr = lane & 15, fq = lane >> 4;
-  const int ch = (fq ^ ((fr >> 2) & 2)) * 16;
-  const int a_off = (wr * 128 + fr) * 64 + ch, b_off = P5_STAGE / 2 + (wc * 128 + fr) * 64 + ch;
-  auto frag_off = [&](int q) { return q < 8 ? a_off + q * 1024 : b_off + (q - 8) * 1024; };
-  auto stage = [](int k) { return ((k + 2 * P5_NS) % P5_NS) * P5_STAGE; };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u32x4 f[2][16];  // [buffer][A frags 0..7, B frags 8..15]
-
-  auto barrier = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  // one K tile, fragments F[CUR] (CUR = kt & 1). Even tiles also move the register tile
-  // (pair kt + 2, kt + 3, loaded two tiles ago) into LDS stages (kt + 2) % 3 and
-  // (kt + 3) % 3 — tiles kt - 1 and kt, both read into registers before the last
-  // barrier — and load pair kt + 4, kt + 5 into it. Every tile reads tile kt + 1's
-  // fragments into F[NXT] behind its 64 MFMAs and ends on a barrier (writes visible,
-  // reads of tile kt + 1's stage done). kMfma = false: the warm-up passes (tiles -4 ..
-  // -1) run the same memory-op sequence without MFMAs, so the loop is entered with its
-  // own loads in flight.
-  auto tile = [&](auto cur_c, auto mfma_c, int kt) {
-    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
-    constexpr bool kMfma = decltype(mfma_c)::value;
-    const unsigned char* nb = lds + stage(kt + 1);
-    unsigned char* wb = lds + (half ? stage(kt + 3) : stage(kt + 2));
-    if constexpr (cur == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pair kt + 2 landed
-#pragma unroll
-    for (int t = 0; t < 64; ++t) {
-      if constexpr (kMfma) p5_mfma(acc[t >> 3][t & 7], f[cur][8 + (t >> 3)], f[cur][t & 7]);
-      if constexpr (cur == 0) {
-        if (t < 16) *reinterpret_cast<u32x4*>(wb + dso(t)) = g[t];
-        else if (t >= 20 && t < 36) gload(t - 20, kt + 4);
-      }
-      const int t0 = cur == 0 ? 36 : 8;  // fragment reads after the staging traffic
-      if (t >= t0 && (t - t0) % (cur == 0 ? 1 : 3) == 0 && (t - t0) / (cur == 0 ? 1 : 3) < 16) {
-        const int q = (t - t0) / (cur == 0 ? 1 : 3);
-        f[nxt][q] = *reinterpret_cast<const u32x4*>(nb + frag_off(q));
-      }
-    }
-    barrier();
-  };
-
-  // warm-up: pairs (0, 1) in LDS, tile 0's fragments in F[0], pair (2, 3) in flight
-#pragma unroll
-  for (int t = 0; t < 16; ++t) g[t] = u32x4{0u, 0u, 0u, 0u};
-  using F0 = std::integral_constant<bool, false>;
-  using F1 = std::integral_constant<bool, true>;
-  for (int kt = -4; kt < 0; kt += 2) {
-    tile(I0(), F0(), kt);
-    tile(I1(), F0(), kt + 1);
-  }
-  for (int kt = 0; kt < nk; kt += 2) {  // nk is even (K % 64 == 0)
-    tile(I0(), F1(), kt);
-    tile(I1(), F1(), kt + 1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end loads
-  // the MFMA results are read by VALU next: asm MFMAs are invisible to the hazard
-  // recognizer, so cover the longest MFMA -> VALU read dependency by hand
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  p5_epilogue<EPI>(acc, lds, C, ldc, M, m0, n0, tn, wr, wc, fr, fq, lane);
 }
 
 // ---- FP8 W8A8 (the FP8-Dynamic checkpoints: per-channel e4m3 weights, per-token
@@ -877,29 +589,11 @@ bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, co
       default: return false;
     }
   }
-  if (E.variant == 5) {
-    switch (epi) {
-      case PG_EPI_STORE: pgemm5_kernel<PG_EPI_STORE, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_ADD: pgemm5_kernel<PG_EPI_ADD, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GLU: pgemm5_kernel<PG_EPI_GLU, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GEGLU: pgemm5_kernel<PG_EPI_GEGLU, false><<<grid, P5_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      default: return false;
-    }
-  }
-  if (E.variant == 2) {
-    switch (epi) {
-      case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_ADD: pgemm2_kernel<PG_EPI_ADD, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      case PG_EPI_GEGLU: pgemm2_kernel<PG_EPI_GEGLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-      default: return false;
-    }
-  }
-  switch (epi) {
-    case PG_EPI_STORE: pgemm_kernel<PG_EPI_STORE><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-    case PG_EPI_ADD: pgemm_kernel<PG_EPI_ADD><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-    case PG_EPI_GLU: pgemm_kernel<PG_EPI_GLU><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
-    case PG_EPI_GEGLU: pgemm_kernel<PG_EPI_GEGLU><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+  switch (epi) {  // the half-tile pipeline (v1 and the hipBLASLt-shaped v5 measured slower, removed)
+    case PG_EPI_STORE: pgemm2_kernel<PG_EPI_STORE, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+    case PG_EPI_ADD: pgemm2_kernel<PG_EPI_ADD, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+    case PG_EPI_GLU: pgemm2_kernel<PG_EPI_GLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
+    case PG_EPI_GEGLU: pgemm2_kernel<PG_EPI_GEGLU, false><<<grid, PG_T, 0, s>>>(a, lda, b, ldb, c, ldc, M, N, K, tiles_m, tiles_n, E); return true;
     default: return false;
   }
 }

@@ -821,27 +821,6 @@ void glu_quant(const c10::optional<at::Tensor>& out, at::Tensor& q8, at::Tensor&
               "glu_quant: I % 8 == 0 and I <= 32768");
 }
 
-// fp32 split-K partials of the merged gate|up [S, M, 2I] -> GLU -> per-token e4m3 act
-// (q8 [M, I], xs8 [M]) for the W8A8 down projection; act (bf16) optional
-void splitk_glu_q8(const c10::optional<at::Tensor>& act, const at::Tensor& ws, int64_t splits, bool gelu,
-                   at::Tensor& q8, at::Tensor& xs8) {
-  CHECK_DEV(ws); CHECK_CONTIG(q8); CHECK_CONTIG(xs8);
-  const int M = q8.size(0), I = q8.size(1);
-  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * 2L * I &&
-                  q8.scalar_type() == at::kByte && xs8.scalar_type() == at::kFloat && xs8.numel() == M,
-              "splitk_glu_q8: ws fp32 [S, M, 2I], q8 uint8 [M, I], xs8 fp32 [M]");
-  void* a = nullptr;
-  if (act.has_value() && act->defined()) {
-    TORCH_CHECK(act->scalar_type() == at::kBFloat16 && act->is_contiguous() && act->sizes() == q8.sizes(),
-                "splitk_glu_q8: act bf16 [M, I]");
-    a = act->data_ptr();
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
-  TORCH_CHECK(hipserve::launch_splitk_glu_q8(a, ws.data_ptr<float>(), (int)splits, M, I, gelu, q8.data_ptr(),
-                                             xs8.data_ptr<float>(), cur_stream()),
-              "splitk_glu_q8: I % 8 == 0, I <= 32768");
-}
-
 void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_CONTIG(xq); CHECK_CONTIG(xs);
   const int M = x.size(0), K = x.size(1);
@@ -886,87 +865,7 @@ void pack_glu_rows(at::Tensor& out, const at::Tensor& w) {
                                    static_cast<const unsigned short*>(w.data_ptr()) + e * N * K, N / 2, K, cur_stream());
 }
 
-// Fused decode layer v2 (decode_layer.hip): one packed decode GEMM whose split-K
-// fix-up runs the layer epilogue in the same launch. fix: 1 add (+ss), 2 rope, 3 glu.
 static const void* opt_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
-
-void decode_gemm_fused(int64_t fix, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t splits,
-                       at::Tensor& ws, at::Tensor& counters, const c10::optional<at::Tensor>& ss_in,
-                       const c10::optional<at::Tensor>& norm_w, double eps,
-                       const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& ss_out,
-                       const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& positions,
-                       const c10::optional<at::Tensor>& slots, const c10::optional<at::Tensor>& cos_sin,
-                       const c10::optional<at::Tensor>& k_cache, const c10::optional<at::Tensor>& v_cache,
-                       int64_t nq, int64_t nkv, int64_t head_dim, int64_t block_size, int64_t mode,
-                       const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& q_w,
-                       const c10::optional<at::Tensor>& k_w) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_ROWMAJOR(x); CHECK_CONTIG(wp);
-  const int M = x.size(0), K = x.size(1);
-  const bool norm_in = ss_in.has_value();
-  TORCH_CHECK(wp.numel() == N * K && x.stride(0) % 8 == 0, "decode_gemm_fused: packed weight [N/128 tiles] x K");
-  TORCH_CHECK(hipserve::dgf_supported((int)fix, norm_in, M, (int)N, K, (int)splits),
-              "decode_gemm_fused: unsupported (fix, M, N, K, splits)");
-  TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= N / 128, "decode_gemm_fused: counters");
-  if (splits > 1)
-    TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= splits * M * N,
-                "decode_gemm_fused: ws must hold S*M*N fp32");
-  hipserve::DgfArgs A{};
-  A.ws = splits > 1 ? ws.data_ptr<float>() : nullptr;
-  A.counters = counters.data_ptr<int>();
-  if (norm_in) {
-    TORCH_CHECK(ss_in->scalar_type() == at::kFloat && ss_in->is_contiguous() && ss_in->numel() % M == 0,
-                "decode_gemm_fused: ss_in [Tin, M] fp32");
-    TORCH_CHECK(norm_w.has_value() && norm_w->scalar_type() == at::kBFloat16 && norm_w->numel() == K,
-                "decode_gemm_fused: bf16 norm weight [K]");
-    A.ss_in = ss_in->data_ptr<float>();
-    A.Tin = ss_in->numel() / M;
-    A.norm_w = static_cast<const unsigned short*>(norm_w->data_ptr());
-  }
-  A.eps = (float)eps;
-  if (fix == 1) {
-    TORCH_CHECK(residual.has_value() && ss_out.has_value(), "decode_gemm_fused(add): residual, ss_out");
-    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
-    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "decode_gemm_fused(add): residual [M, N]");
-    TORCH_CHECK(ss_out->scalar_type() == at::kFloat && ss_out->numel() >= (N / 128) * M, "ss_out [N/128, M]");
-    A.residual = static_cast<unsigned short*>(residual->data_ptr());
-    A.ss_out = ss_out->data_ptr<float>();
-  } else if (fix == 2) {
-    TORCH_CHECK(out.has_value() && positions.has_value() && slots.has_value() && cos_sin.has_value() &&
-                k_cache.has_value() && v_cache.has_value(), "decode_gemm_fused(rope): q_out, positions, slots, "
-                "cos_sin, caches");
-    TORCH_CHECK((head_dim == 64 || head_dim == 128) && N == (nq + 2 * nkv) * head_dim, "decode_gemm_fused(rope): heads");
-    CHECK_BF16((*out)); CHECK_ROWMAJOR((*out));
-    TORCH_CHECK(out->size(0) >= M && out->size(1) >= nq * head_dim, "decode_gemm_fused(rope): q_out [M, nq*D]");
-    TORCH_CHECK(positions->scalar_type() == at::kLong && slots->scalar_type() == at::kLong &&
-                cos_sin->scalar_type() == at::kFloat, "decode_gemm_fused(rope): index / table dtypes");
-    A.q_out = static_cast<unsigned short*>(out->data_ptr());
-    A.q_stride = out->stride(0);
-    A.positions = positions->data_ptr<int64_t>();
-    A.slots = slots->data_ptr<int64_t>();
-    A.cos_sin = cos_sin->data_ptr<float>();
-    A.k_cache = static_cast<unsigned short*>(k_cache->data_ptr());
-    A.v_cache = static_cast<unsigned short*>(v_cache->data_ptr());
-    A.nq = nq; A.nkv = nkv; A.D = head_dim; A.block_size = block_size; A.rope_mode = mode;
-    if (bias.has_value()) { CHECK_BF16((*bias)); TORCH_CHECK(bias->numel() == N); }
-    A.bias = static_cast<const unsigned short*>(opt_ptr(bias));
-    if (q_w.has_value()) {
-      TORCH_CHECK(mode == 0 && k_w.has_value() && q_w->scalar_type() == at::kFloat && q_w->numel() == head_dim &&
-                  k_w->scalar_type() == at::kFloat && k_w->numel() == head_dim, "decode_gemm_fused(rope): q/k norm");
-      A.qw = q_w->data_ptr<float>();
-      A.kw = k_w->data_ptr<float>();
-    }
-  } else if (fix == 3) {
-    TORCH_CHECK(out.has_value(), "decode_gemm_fused(glu): act");
-    CHECK_BF16((*out)); CHECK_ROWMAJOR((*out));
-    TORCH_CHECK(out->size(0) == M && out->size(1) == N / 2 && out->stride(0) % 4 == 0, "act [M, N/2]");
-    A.out = static_cast<unsigned short*>(out->data_ptr());
-    A.out_stride = out->stride(0);
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  TORCH_CHECK(hipserve::launch_dgf((int)fix, norm_in, A, x.data_ptr(), x.stride(0), wp.data_ptr(), M, (int)N, K,
-                                   (int)splits, cur_stream()),
-              "decode_gemm_fused: launch");
-}
 
 // optional per-token e4m3 copy (out8 uint8 like out, xs8 fp32 [M]) of a norm epilogue's output
 static void e4m3_out_args(const c10::optional<at::Tensor>& out8, const c10::optional<at::Tensor>& xs8,
@@ -1314,13 +1213,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
   m.def("glu_quant(Tensor(a!)? out, Tensor(b!) q8, Tensor(c!) xs, Tensor x, bool gelu) -> ()");
-  m.def("splitk_glu_q8(Tensor(a!)? act, Tensor ws, int splits, bool gelu, Tensor(b!) q8, Tensor(c!) xs8) -> ()");
   m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
   m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi, int variant=2) -> ()");
-  m.def("decode_gemm_fused(int fix, Tensor x, Tensor wp, int N, int splits, Tensor(a!) ws, Tensor(b!) counters, "
-        "Tensor? ss_in, Tensor? norm_w, float eps, Tensor(c!)? residual, Tensor(d!)? ss_out, Tensor(e!)? out, "
-        "Tensor? positions, Tensor? slots, Tensor? cos_sin, Tensor(f!)? k_cache, Tensor(g!)? v_cache, int nq, int nkv, "
-        "int head_dim, int block_size, int mode, Tensor? bias, Tensor? q_w, Tensor? k_w) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
@@ -1363,7 +1257,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("pack_decode_weight", &pack_decode_weight);
   m.impl("decode_gemm_partial", &decode_gemm_partial);
   m.impl("decode_gemm_glu", &decode_gemm_glu);
-  m.impl("decode_gemm_fused", &decode_gemm_fused);
   m.impl("prefill_gemm", &prefill_gemm);
   m.impl("prefill_gemm_packed", &prefill_gemm_packed);
   m.impl("prefill_gemm_packed_grouped", &prefill_gemm_packed_grouped);
@@ -1372,7 +1265,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("act_quant_fp8", &act_quant_fp8);
   m.impl("fp8_decode_gemm", &fp8_decode_gemm);
   m.impl("glu_quant", &glu_quant);
-  m.impl("splitk_glu_q8", &splitk_glu_q8);
   m.impl("pack_glu_rows", &pack_glu_rows);
   m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);

@@ -118,13 +118,9 @@ class LlamaModel:
     # LDS): 5.322 / 5.332 vs 5.332 / 5.327 ms (tools/decode_gap.py, alternating runs) —
     # parity, so the separate splitk_rope_cache launch stays the default
     fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "0") == "1"
-    # fused decode layer v2 (csrc/kernels/decode_layer.hip): the split-K fix-up and
-    # the layer epilogue inside each decode GEMM launch, RMSNorm applied on load —
-    # five kernels per Llama layer instead of eight (TP = 1 dense families). Opt-in:
-    # the first end-to-end run was SLOWER (6,398 vs 7,650 tok/s): an in-launch split-K
-    # seam (agent release per slice + last-arriver slab reads) costs more than the
-    # kernel boundary + epilogue kernel it replaces (profiles/r3_decode_v2_ab.md)
-    fused_v2 = os.environ.get("HIPSERVE_FUSED_V2", "0") == "1"
+    # (round 3 tried a "v2" decode layer with the split-K fix-up and the epilogue inside each
+    # decode GEMM launch: slower, 6,398 vs 7,650 tok/s, profiles/r3_bench_v2_first.json —
+    # an in-launch split-K seam costs more than the kernel boundary it replaces; removed)
 
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device, dtype=torch.bfloat16, ops=None,
                  max_pos: int | None = None):
@@ -386,10 +382,6 @@ class LlamaModel:
             free, _ = torch.cuda.mem_get_info(self.device)
             return free - w.numel() * w.element_size() >= reserve
 
-        if self.device.type == "cuda" and getattr(self, "_dgf_counters", None) is None:
-            # split-K tile tickets of the v2 fused decode GEMMs (zero between calls:
-            # each tile's last arriver resets its own)
-            self._dgf_counters = torch.zeros(8192, dtype=torch.int32, device=self.device)
         for lw in self.layers:
             for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
                 if (isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes
@@ -485,7 +477,7 @@ class LlamaModel:
                     op.pack_decode_weight(p13[e], lw.w13[e], True)
                     op.pack_decode_weight(p2[e], lw.w2[e], False)
                 lw.moe_packed = (p13, p2)
-            if drop_plain and self.moe_packed_prefill(lw):
+            if drop_plain and self.moe_packed_prefill(lw, for_drop=True):
                 freed += 2 * (lw.w13.numel() + lw.w2.numel())
                 lw.w13 = lw.w2 = None
         return freed if drop_plain else need
@@ -603,9 +595,6 @@ class LlamaModel:
         eps = cfg.rms_norm_eps
         Tp, Td = meta.num_prefill_tokens, meta.num_decode
         if self._fused_ok(meta):
-            plan = self.v2_plan(T, meta)
-            if plan is not None:
-                return self.forward_decode_v2(ids, meta, kv_caches, plan)
             return self.forward_decode_fused(ids, meta, kv_caches)
         ids = self.resolve_ids(ids, meta)
         h = self.embed_tokens(ids)
@@ -799,13 +788,8 @@ class LlamaModel:
                 act = gemm.gemm_glu(xn, lw.wgu, gc)
             elif pt is not None:   # quantised gate|up, or GeGLU: the GLU over the plain-layout partials
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
-                act8 = (self._x8(act, lw.wd) if self.GLU_Q8 and hasattr(op, "splitk_glu_q8")
-                        and getattr(lw.wd, "v2", False) else None)  # (v2: _partial takes the quantised decode path, so act itself is never read)
-                if act8 is not None:  # FP8 down: act only as its e4m3 copy (the W8A8 GEMM's input)
-                    op.splitk_glu_q8(None, pt[0], pt[1], gelu, act8[0], act8[1])
-                else:
-                    act16 = self._x16(act, lw.wd)
-                    op.splitk_glu(act, pt[0], pt[1], gelu, act16)
+                act16 = self._x16(act, lw.wd)
+                op.splitk_glu(act, pt[0], pt[1], gelu, act16)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
@@ -824,100 +808,6 @@ class LlamaModel:
                 xn16 = xn8 = None
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(act, lw.wd), 1, nxt)
         return xn
-
-    @staticmethod
-    def _dgf_ok(fix: int, norm_in: bool, M: int, N: int, K: int, S: int) -> bool:
-        """Mirror of decode_layer.hip ``dgf_supported``."""
-        if not (1 <= M <= 64 and N % 128 == 0 and K % 256 == 0 and S >= 1 and K % (256 * S) == 0):
-            return False
-        if K // S // 256 not in (1, 2, 4, 7, 8, 16):
-            return False
-        return (not norm_in) if fix == 1 else (fix == 2 or (fix == 3 and norm_in))
-
-    def v2_plan(self, T: int, meta: AttnMeta):
-        """Split counts (qkv, o, gate|up, down) of the v2 fused decode layer at batch
-        T — the tuned packed decode GEMM's S for each projection — or None when the
-        layer does not qualify (TP > 1, MoE / quantised / sandwich families, a
-        projection the tuner left to hipBLASLt, weights without a packed copy)."""
-        cfg = self.cfg
-        if not (self.fused_v2 and self.tp.world_size == 1 and T <= 64 and self.D in (64, 128)
-                and getattr(self, "_dgf_counters", None) is not None):
-            return None
-        if cfg.sandwich_norm or cfg.hidden_act != "silu" or any(cfg.layer_windows) or cfg.embed_scale != 1.0:
-            return None
-        lw0 = self.layers[0]
-        ws = (lw0.wqkv, lw0.wo, lw0.wgu, lw0.wd)
-        if lw0.router is not None or not all(isinstance(w, torch.Tensor) for w in ws):
-            return None
-        if lw0.ln1.dtype != torch.bfloat16 or lw0.ln2.dtype != torch.bfloat16 or self.norm.dtype != torch.bfloat16:
-            return None
-        plan = []
-        for w, fix, norm_in in zip(ws, (2, 1, 3, 1), (True, False, True, False)):
-            N, K = w.shape
-            c = gemm.TUNER.choose(T, N, K)
-            if not (isinstance(c, tuple) and c[0] == "dgp") or not self._dgf_ok(fix, norm_in, T, N, K, c[2]):
-                return None
-            plan.append(c[2])
-        for lw in self.layers:
-            if (gemm.packed_of(lw.wqkv) is None or gemm.packed_of(lw.wo) is None or gemm.glu_of(lw.wgu) is None
-                    or gemm.packed_of(lw.wd) is None):
-                return None
-        return plan
-
-    def forward_decode_v2(self, ids: torch.Tensor, meta: AttnMeta, kv_caches, plan) -> torch.Tensor:
-        """Decode-only forward, five kernels per layer (decode_layer.hip): qkv GEMM
-        (input RMSNorm on load; RoPE + KV write in its split-K fix-up), paged
-        attention, o_proj GEMM (residual add + per-tile sums of squares in the
-        fix-up), gate|up GEMM (post-attention RMSNorm on load, SiLU-GLU epilogue),
-        down GEMM (residual add + sums of squares). Layer 0 takes the embedding's
-        fused first RMSNorm; the final RMSNorm is one row-norm kernel."""
-        ops, cfg, op = self.ops, self.cfg, torch.ops.hipserve
-        T = ids.shape[0]
-        D, nq, nkv = self.D, self.nq, self.nkv
-        H = cfg.hidden_size
-        eps = cfg.rms_norm_eps
-        lw0 = self.layers[0]
-        if meta.id_src is not None and self.fused_embed_ok(meta):
-            residual = torch.empty(T, H, device=ids.device, dtype=self.embed.dtype)
-            xn = torch.empty_like(residual)
-            op.embed_rmsnorm(xn, residual, self.embed, ids, meta.id_src[0], meta.id_src[1], lw0.ln1, eps)
-        else:
-            h = self.embed_tokens(self.resolve_ids(ids, meta))
-            residual = h.clone()
-            xn = torch.empty_like(h)
-            ops.rmsnorm(xn, h, lw0.ln1, eps)
-        Sq, So, Sg, Sd = plan
-        Nq, I2 = lw0.wqkv.shape[0], lw0.wgu.shape[0]
-        dt, dev = residual.dtype, residual.device
-        qbuf = torch.empty(T, Nq, device=dev, dtype=dt)     # q heads in the qkv row layout
-        attn = torch.empty(T, nq * D, device=dev, dtype=dt)
-        act = torch.empty(T, I2 // 2, device=dev, dtype=dt)
-        ss = torch.empty(H // 128, T, device=dev, dtype=torch.float32)
-        ctr = self._dgf_counters
-        e32 = gemm._empty(dev)[1]
-        part, tmp_out, tmp_ml = self._decode_split(T, meta)
-        bs = kv_caches[0][0].shape[2]
-
-        def ws(S, N):
-            return torch.empty(S * T * N, device=dev, dtype=torch.float32) if S > 1 else e32
-
-        for i, lw in enumerate(self.layers):
-            kc, vc = kv_caches[i]
-            x_in, ss_in, nw = (xn, None, None) if i == 0 else (residual, ss, lw.ln1)
-            op.decode_gemm_fused(2, x_in, gemm.packed_of(lw.wqkv), Nq, Sq, ws(Sq, Nq), ctr, ss_in, nw, eps, None,
-                                 None, qbuf, meta.positions, meta.slot_mapping, self.cos_sin, kc, vc, nq, nkv, D,
-                                 bs, cfg.rope_mode, lw.bqkv, lw.q_norm, lw.k_norm)
-            ops.paged_decode(attn, qbuf, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part,
-                             self.scale)
-            op.decode_gemm_fused(1, attn, gemm.packed_of(lw.wo), H, So, ws(So, H), ctr, None, None, eps, residual,
-                                 ss, None, None, None, None, None, None, 0, 0, 0, 0, 0, None, None, None)
-            op.decode_gemm_fused(3, residual, gemm.glu_of(lw.wgu), I2, Sg, ws(Sg, I2), ctr, ss, lw.ln2, eps, None,
-                                 None, act, None, None, None, None, None, 0, 0, 0, 0, 0, None, None, None)
-            op.decode_gemm_fused(1, act, gemm.packed_of(lw.wd), H, Sd, ws(Sd, H), ctr, None, None, eps, residual,
-                                 ss, None, None, None, None, None, None, 0, 0, 0, 0, 0, None, None, None)
-        out = torch.empty_like(residual)
-        ops.rmsnorm(out, residual, self.norm, eps)
-        return out
 
     def quant_weights(self) -> list:
         """Every GGUF-quantised projection (QuantWeight), lm_head included."""
@@ -939,10 +829,9 @@ class LlamaModel:
         return None
 
     X16 = os.environ.get("HIPSERVE_QGEMM_X16", "1") != "0"
-    # decode: split-K GLU -> e4m3 act in one kernel (one block per row). Off: measured
-    # 2,794 / 2,806 vs 2,836 / 2,851 tok/s on Gemma-3-27B FP8 (same box, alternating) —
-    # 64 row-blocks read the partials slower than splitk_glu's 700-block grid + act_quant
-    GLU_Q8 = os.environ.get("HIPSERVE_GLU_Q8", "0") == "1"
+    # (a split-K GLU -> e4m3 act kernel, one block per row, measured slower than splitk_glu's
+    # 700-block grid + act_quant on Gemma-3-27B FP8 — 2,794 / 2,806 vs 2,836 / 2,851 tok/s —
+    # and was removed in round 4)
 
     def _x16(self, like: torch.Tensor, consumer):
         """f16 buffer for the pair-order copy of ``like`` that its producer
@@ -1120,12 +1009,19 @@ class LlamaModel:
         op.moe_combine(out, y, w, pair_slot, k)
         return out
 
-    MOE_PACKED_PREFILL = os.environ.get("HIPSERVE_MOE_PACKED_PREFILL", "1") != "0"
+    # packed-layout grouped expert GEMMs for prefill: always when the row-major experts were
+    # dropped (single weight layout), else opt-in — with both copies resident, hipBLASLt's
+    # grouped GEMM measured faster on Mixtral-8x7B (1,632 vs 1,602 tok/s, TTFT 561 vs 641 ms,
+    # profiles/r4_bench_mixtral_*.json) despite its host round trip
+    MOE_PACKED_PREFILL = os.environ.get("HIPSERVE_MOE_PACKED_PREFILL", "auto")
 
-    def moe_packed_prefill(self, lw: LayerWeights) -> bool:
+    def moe_packed_prefill(self, lw: LayerWeights, for_drop: bool = False) -> bool:
         """Prefill experts on the packed-layout grouped GEMM (the decode kernels' copy of
         the experts, ``pack_moe_weights``): SiLU-GLU experts, K of both GEMMs % 256."""
-        return (self.MOE_PACKED_PREFILL and lw.moe_packed is not None and self.cfg.hidden_act == "silu"
+        mode = self.MOE_PACKED_PREFILL
+        if mode == "0" or (mode == "auto" and not for_drop and lw.w13 is not None):
+            return False
+        return (lw.moe_packed is not None and self.cfg.hidden_act == "silu"
                 and self.cfg.hidden_size % 256 == 0 and self.inter % 256 == 0 and (2 * self.inter) % 128 == 0
                 and hasattr(torch.ops.hipserve, "prefill_gemm_packed_grouped"))
 

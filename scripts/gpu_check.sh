@@ -97,7 +97,6 @@ for s in $steps; do
     q3int8) bench_named q3int8 HIPSERVE_FUSED_DECODE=1 -- --model qwen3-30b-a3b --quantization int8 ;;
     q06) bench_named q06 HIPSERVE_FUSED_DECODE=1 -- --model qwen3-0.6b ;;
     g27bf16_unfused) bench_named g27bf16_unfused HIPSERVE_FUSED_DECODE=0 -- --model gemma-3-27b ;;
-    g27fp8_gluq8off) bench_named g27fp8_gluq8off HIPSERVE_GLU_Q8=0 -- --model gemma-3-27b --quantization fp8 ;;
     g27fp8_unfused) bench_named g27fp8_unfused HIPSERVE_FUSED_DECODE=0 -- --model gemma-3-27b --quantization fp8 ;;
     q4km) bench_named q4km HIPSERVE_QUANT_SHADOW=1 -- --quantization q4_k_m ;;
     q4km_x16off) bench_named q4km_x16off HIPSERVE_QGEMM_X16=0 -- --quantization q4_k_m ;;
@@ -116,6 +115,8 @@ for s in $steps; do
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     prof70) prof_run prof70 --model llama-3-70b ;;
+    long8k) bench_named long8k X=1 -- --input-len 8192 --output-len 256 --concurrency 16 --max-num-batched-tokens 8192 --steps 2 ;;
+    long32k) bench_named long32k X=1 -- --input-len 32768 --output-len 256 --concurrency 4 --max-num-batched-tokens 8192 --steps 2 ;;
     bench_mixtral_packed) bench_named mixtral_packed HIPSERVE_MOE_PACKED_PREFILL=1 -- --model mixtral-8x7b --concurrency 32 ;;
     bench_mixtral_old) bench_named mixtral_old HIPSERVE_MOE_PACKED_PREFILL=0 -- --model mixtral-8x7b --concurrency 32 ;;
     prof_qwen3moe) prof_run profqm --model qwen3-30b-a3b ;;

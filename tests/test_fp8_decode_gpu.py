@@ -123,22 +123,3 @@ def test_rmsnorm_e4m3_copy_is_act_quant(add, M, N):
         torch.ops.hipserve.rmsnorm(out, x, w, 1e-6, q8, s8)
     xq, xs = pgemm.act_quant(out)
     assert torch.equal(q8, xq) and torch.equal(s8, xs)
-
-
-@pytest.mark.parametrize("gelu", [False, True])
-@pytest.mark.parametrize("M,I,S", [(1, 21504, 1), (48, 14336, 3), (64, 384, 2)])
-def test_splitk_glu_q8_is_splitk_glu_then_act_quant(gelu, M, I, S):
-    """splitk_glu_q8 (decode: split-K gate|up partials -> GLU -> per-token e4m3 act for the
-    FP8 down projection) is bit-identical to splitk_glu followed by act_quant_fp8."""
-    from hipserve.ops import pgemm
-
-    g = torch.Generator(device=DEV).manual_seed(M + I + S + gelu)
-    ws = torch.randn(S * M * 2 * I, device=DEV, generator=g) * 2
-    act = torch.empty(M, I, device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.splitk_glu(act, ws, S, gelu)
-    xq, xs = pgemm.act_quant(act)
-    q8 = torch.empty(M, I, device=DEV, dtype=torch.uint8)
-    s8 = torch.empty(M, device=DEV, dtype=torch.float32)
-    a2 = torch.empty_like(act)
-    torch.ops.hipserve.splitk_glu_q8(a2, ws, S, gelu, q8, s8)
-    assert torch.equal(a2, act) and torch.equal(q8, xq) and torch.equal(s8, xs)

@@ -200,7 +200,6 @@ def test_fused_decode_forward_bit_exact(ops, choices, family="llama", qkv_attn=F
     m, cfg = _small_model(ops, family=family)
     assert m.fused_family
     m.fused_qkv_attention = qkv_attn
-    m.fused_v2 = False  # v1 (bit-exact); v2 is tests/test_decode_v2_gpu.py
     old = dict(gemm.TUNER.table)
     try:
         gemm.TUNER.table.clear()

@@ -23,7 +23,7 @@ def _rnd(g, *s, scale=1.0):
     return ((torch.rand(*s, device=DEV, generator=g) * 2 - 1) * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 5])
+@pytest.mark.parametrize("variant", [2])
 @pytest.mark.parametrize("M,N,K", SHAPES + [(512, 256, 128), (700, 512, 192)])
 def test_prefill_gemm_store(M, N, K, variant):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
@@ -34,7 +34,7 @@ def test_prefill_gemm_store(M, N, K, variant):
     torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 
 
-@pytest.mark.parametrize("variant", [1, 2, 5])
+@pytest.mark.parametrize("variant", [2])
 @pytest.mark.parametrize("M,N,K", SHAPES[:4])
 def test_prefill_gemm_residual_add(M, N, K, variant):
     g = torch.Generator(device=DEV).manual_seed(7 + M)
@@ -47,7 +47,7 @@ def test_prefill_gemm_residual_add(M, N, K, variant):
     torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant,act", [(1, "silu"), (2, "silu"), (5, "silu"), (1, "gelu"), (2, "gelu"), (5, "gelu")])
+@pytest.mark.parametrize("variant,act", [(2, "silu"), (2, "gelu")])
 @pytest.mark.parametrize("M,I,K", [(300, 256, 1024), (1000, 384, 512), (2049, 128, 256)])
 def test_prefill_gemm_glu(M, I, K, variant, act):
     g = torch.Generator(device=DEV).manual_seed(11 + M)

@@ -61,9 +61,7 @@ def main():
         ws = [rnd(N, K) * 0.05 for _ in range(L)]
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         t_blas = time_fn(lambda: [F.linear(x, w) for w in ws])
-        t_v1 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 1) for w in ws])
         t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 2) for w in ws])
-        t_v5 = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 5) for w in ws])
         # the packed-layout kernel (prefill_gemm_packed.hip) on the decode copy of each weight
         glu_pack = name == "gu"
         wps = []
@@ -73,7 +71,6 @@ def main():
             wps.append(wp)
         t_pw = {wm: time_fn(lambda: [op.prefill_gemm_packed(out, x, wp, N, 0, None, wm) for wp in wps]) for wm in (1, 2)}
         r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
-             "pgemm_v1_ms": round(t_v1, 4), "pgemm_v5_ms": round(t_v5, 4),
              "packed_wm1_ms": round(t_pw[1], 4), "packed_wm2_ms": round(t_pw[2], 4),
              "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1),
              "packed_TFs": round(2 * M * N * K / min(t_pw.values()) / 1e9, 1)}
