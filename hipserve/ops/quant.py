@@ -452,6 +452,8 @@ def _graph_time_us(fn, reps: int = 10, rounds: int = 3) -> float:
     return best
 
 
+@torch.inference_mode()  # like the engine's graph capture: a process may hold several engines, and the
+# generator state tensors a capture registers must not switch between inference and normal tensors
 def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) -> list:
     """Measure the v2 decode GEMM per distinct QuantWeight shape and M bucket for
     S in {1, 2, 4, ...} and keep the S minimising kernel time + the epilogue's

@@ -118,4 +118,5 @@ def test_bench_open_loop_request_rate():
     assert out["load"].startswith("open-loop") and out["value"] > 0 and out["p50_ttft_ms"] > 0
     ol = out["open_loop"]
     assert ol["rate_req_s"] == 20 and ol["p90_ttft_ms"] >= ol["p50_ttft_ms"] > 0
-    assert ol["p90_itl_ms"] >= ol["p50_itl_ms"] > 0
+    # the tiny CPU model can emit a request's tokens back to back (median gap rounds to 0.00 ms)
+    assert ol["p90_itl_ms"] >= ol["p50_itl_ms"] >= 0

@@ -327,7 +327,7 @@ def _check_bound(lb, exact=True):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("shape", ["moe", "small:fp8", "qwen3moe:int8", "moe:fp8"])
+@pytest.mark.parametrize("shape", ["small:fp8", "moe", "qwen3moe:int8", "moe:fp8"])
 def test_tp2_quant_and_moe_shared_gpu_matches_tp1(shape):
     """The reference's TP=2 deployments (vllm-models/helm-chart/values.yaml:3-12;
     templates/model-deployments.yaml:37-38): FP8 weights (Gemma-3-27B-FP8-Dynamic), 8-bit
@@ -336,11 +336,15 @@ def test_tp2_quant_and_moe_shared_gpu_matches_tp1(shape):
     stated logit bound against the fp32 oracle of the same (dequantised) weights. Every
     TP degree quantises the same model (row-parallel scales are the max over the ranks'
     K slices)."""
-    _, info = _run_tp(2, False, shape=shape, timeout=280)
+    # MoE: top-k routing turns a bf16-ulp difference of the hidden state into a different
+    # expert set (a discontinuity, not noise), so the MoE shapes run with exact (fp32)
+    # exchange, where TP=2's hidden states round like TP=1's
+    moe = _split(shape)[0] in ("moe", "qwen3moe")
+    _, info = _run_tp(2, moe, shape=shape, timeout=280)
     assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
     assert info["car_failed"] is False
     _check_ties(info)
-    _check_bound(info["logit"], False)
+    _check_bound(info["logit"], moe)
 
 
 N_TOK_70B = 64
