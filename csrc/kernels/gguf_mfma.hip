@@ -851,6 +851,281 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
   }
 }
 
+// ---------------------------------------------------------------- prefill GEMM
+// qpf_kernel (GGUF prefill without the resident bf16 shadow):
+// C[M, N] = X[M, K] . W^T straight from the tiled blocks, every weight dequantised ONCE
+// per 128-token tile (the M-swept qgemm2 above does it once per 64 tokens and stages x
+// for 128 weight rows; a dequantise-into-scratch + hipBLASLt pass writes and re-reads a
+// bf16 copy of the whole matrix per call).
+//   * workgroup = 8 waves x 2 row groups = 256 weight rows x 128 tokens, two waves per
+//     SIMD (64 accumulators, <= 256 registers each: one wave's dequant VALU runs beside
+//     the other's MFMAs); x (bf16 -> f16, the weights' pair order)
+//     staged once per 256-k super-chunk into a double-buffered LDS image (2 x 72 KiB),
+//     ONE barrier per super-chunk; the next super-chunk's x and weight blocks are in
+//     flight while this one is dequantised and multiplied;
+//   * per 32-k step a wave dequantises 2 weight fragments (2 VALU per pair,
+//     Dec::step) and issues 16 f16 MFMAs against 8 x fragments read from LDS: the
+//     dequant cost per MFMA is 1/8 of the decode kernel's at M = 16;
+//   * weight bytes per MFMA are 3.5x (Q4_K) fewer than a bf16 GEMM's, which is what
+//     bounded the bf16 packed-layout kernel (profiles/r4_pw_diag_and_bench.log);
+//   * epilogues: STORE (part columns), ADD (C is the residual: C = bf16(bf16(acc) + C)),
+//     GLU (parts 0 / 1 = gate / up of the same format: a wave's row group 0 is gate
+//     rows, 1 the matching up rows, act = silu(gate) * up in registers);
+//   * f16 range: the same non-finite vote + per-row power-of-two rescale pass as qgemm2.
+constexpr int QF_RT = 2, QF_MT = 8, QF_W = 8, QF_T = 64 * QF_W;
+constexpr int QF_ROWS = 16 * QF_RT * QF_W;  // weight rows per STORE / ADD tile (GLU: 128 act columns)
+// tokens per tile: 128 (MT = 8); Q5_K / Q6_K / Q8_0 (larger raw blocks: 16-19 registers per row
+// group and buffer) 64, which keeps them within 256 registers without spills
+template <int QT>
+constexpr int qf_mt() { return QT == Q5_K || QT == Q6_K || QT == Q8_0 ? 4 : 8; }
+struct QfArgs {
+  Parts parts;
+  const unsigned short* x;
+  long ldx;
+  unsigned short* out;
+  long ldo;
+  int M, K, tiles_n, tiles_m;
+};
+
+template <int QT, int EPI>
+HS_DEVICE void qpf_body(_Float16 (&xs)[2][4 * x_plane<qf_mt<QT>()>()], float* xrow, const QfArgs& A, int pi, int tm,
+                        int tn) {
+  constexpr int RT = QF_RT, MT = qf_mt<QT>(), NT = QF_T, XR = 16 * MT;
+  constexpr int CB = chunk_bytes<QT>();
+  constexpr bool kGlu = EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int K = A.K, M = A.M, nsb = K >> 8;
+  const Part& P = A.parts.p[pi];
+  const int ngroups = P.rows >> 4;
+  int gi[RT];
+  const unsigned char* base[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    // GLU: row groups 0 .. RT/2 - 1 gate, RT/2 .. RT - 1 the matching up rows
+    gi[r] = kGlu ? (tn * QF_W + wave) * (RT / 2) + r % (RT / 2) : (tn - P.tile0) * (QF_ROWS / 16) + wave * RT + r;
+    const unsigned char* q = kGlu && r >= RT / 2 ? A.parts.p[1].q : P.q;
+    base[r] = q + (long)min(gi[r], ngroups - 1) * nsb * CB;
+  }
+  constexpr int XP = XR * 32 / NT, XH = XP / 2;  // 8 fragments of 8 per thread and super-chunk, in 2 halves
+  const int mrow0 = tm * XR;
+  const unsigned short* xg = A.x + (long)mrow0 * A.ldx;
+  int xo[XP];  // rows >= M clamped to M - 1 (computed, never stored)
+#pragma unroll
+  for (int i = 0; i < XP; ++i) {
+    const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
+    xo[i] = (min(mrow0 + row, M - 1) - mrow0) * (int)A.ldx + kbase<QT>(fr >> 3, fr & 7);
+  }
+  u16x8 xv[XH];  // one half of the staging items in registers at a time
+  auto load_x = [&](int sb, int h) {
+#pragma unroll
+    for (int i = 0; i < XH; ++i) xv[i] = *reinterpret_cast<const u16x8*>(xg + xo[h * XH + i] + sb * 256);
+  };
+  auto store_x = [&](int buf, int h, auto scaled) {
+#pragma unroll
+    for (int i = 0; i < XH; ++i) {
+      const int idx = (h * XH + i) * NT + tid, row = idx >> 5, fr = idx & 31;
+      const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
+      float f[8] = {bf_lo(w[0]), bf_lo(w[1]), bf_hi(w[0]), bf_hi(w[1]),
+                    bf_lo(w[2]), bf_lo(w[3]), bf_hi(w[2]), bf_hi(w[3])};  // pair order {0, 2, 1, 3, 4, 6, 5, 7}
+      if constexpr (decltype(scaled)::value) {
+        const float sc = xrow[row];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] *= sc;
+      }
+      f16x8 hv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hv[e] = static_cast<_Float16>(f[e]);
+      *reinterpret_cast<f16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = hv;
+    }
+  };
+
+  f32x4 acc[RT][MT];
+  Raw rawA[RT], rawB[RT];
+  auto run = [&](auto scaled) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r], g, c, lane, rawA[r]);
+    load_x(0, 0);
+    store_x(0, 0, scaled);
+    load_x(0, 1);
+    store_x(0, 1, scaled);
+    __syncthreads();
+    // per super-chunk: the next one's weight blocks and first x half go out first; the x
+    // half is written to the other LDS buffer (read last in the previous super-chunk, so
+    // free since its barrier) after step 3, when the second half is loaded, and that one
+    // at the end: 4 x registers per thread instead of 8. The last super-chunk re-reads
+    // itself (no branch; its stores land in the unused buffer).
+    auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
+      const int buf = sb & 1;
+      const int sn = min(sb + 1, nsb - 1);
+      load_x(sn, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
+      __builtin_amdgcn_sched_barrier(0);
+      const _Float16* xb = &xs[buf][g * x_plane<MT>() + c * kXR];
+      Dec<QT> dec[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s == 4) {
+          store_x(buf ^ 1, 0, scaled);
+          load_x(sn, 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        f16x8 a[RT];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          // 4 x fragments read from LDS ahead of their MFMAs (left alone the compiler
+          // reuses one register and every MFMA waits out an LDS round trip)
+          f16x8 b[MT / 2];
+#pragma unroll
+          for (int t = 0; t < MT / 2; ++t) b[t] = *reinterpret_cast<const f16x8*>(xb + 16 * (h * MT / 2 + t) * kXR + 8 * s);
+          __builtin_amdgcn_sched_barrier(0);
+          if (h == 0) {
+#pragma unroll
+            for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
+          }
+#pragma unroll
+          for (int t = 0; t < MT / 2; ++t)
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+              acc[r][h * MT / 2 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b[t], acc[r][h * MT / 2 + t], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      store_x(buf ^ 1, 1, scaled);
+      __syncthreads();
+    };
+    int sb = 0;
+    for (; sb + 1 < nsb; sb += 2) {
+      iter(sb, rawA, rawB);
+      iter(sb + 1, rawB, rawA);
+    }
+    if (sb < nsb) iter(sb, rawA, rawB);
+  };
+  run(std::false_type{});
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(acc[r][t][e]);
+  if (__syncthreads_or(bad)) {  // some x beyond the f16 range: per-row 2^-k pre-scale, second pass
+    unsigned* xm = reinterpret_cast<unsigned*>(xrow);
+    if (tid < XR) xm[tid] = 0u;
+    __syncthreads();
+    for (int sb2 = 0; sb2 < nsb; ++sb2)
+      for (int h = 0; h < 2; ++h) {
+        load_x(sb2, h);
+#pragma unroll
+        for (int i = 0; i < XH; ++i) {
+          const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
+          unsigned mx = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mx = max(mx, max((w[e] << 16) & 0x7FFF0000u, w[e] & 0x7FFF0000u));
+          atomicMax(&xm[((h * XH + i) * NT + tid) >> 5], mx);
+        }
+      }
+    __syncthreads();
+    if (tid < XR) {
+      const int ex = (int)(xm[tid] >> 23) - 127;
+      xrow[tid] = __builtin_bit_cast(float, (unsigned)(127 - min(126, max(0, ex - 14))) << 23);
+    }
+    __syncthreads();
+    run(std::true_type{});
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const float un = 1.f / xrow[16 * t + c];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r][t] *= un;
+    }
+  }
+  // lane holds C[m = mrow0 + 16 t + c][rows 16 gi + 4 g + j]
+  if constexpr (kGlu) {
+#pragma unroll
+    for (int r = 0; r < RT / 2; ++r) {
+      if (gi[r] >= ngroups) continue;
+      const int col = 16 * gi[r] + 4 * g;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = mrow0 + 16 * t + c;
+        if (m >= M) continue;
+        unsigned short o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned short gv = f32_to_bf16(acc[r][t][j]), uv = f32_to_bf16(acc[r + RT / 2][t][j]);
+          o[j] = EPI == PW_EPI_GEGLU ? gelu_mul1(gv, uv) : silu_mul1(gv, uv);
+        }
+        *reinterpret_cast<uint2*>(A.out + (long)m * A.ldo + col) =
+            uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      if (gi[r] >= ngroups) continue;
+      const int col = P.col + 16 * gi[r] + 4 * g;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = mrow0 + 16 * t + c;
+        if (m >= M) continue;
+        uint2* dst = reinterpret_cast<uint2*>(A.out + (long)m * A.ldo + col);
+        float o[4];
+        if constexpr (EPI == PW_EPI_ADD) {
+          const uint2 rv = *dst;
+          const unsigned short rr[4] = {(unsigned short)(rv.x & 0xffff), (unsigned short)(rv.x >> 16),
+                                        (unsigned short)(rv.y & 0xffff), (unsigned short)(rv.y >> 16)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[r][t][j])) + bf16_to_f32(rr[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = acc[r][t][j];
+        }
+        *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+      }
+    }
+  }
+}
+
+// tiles: n-major groups of 8 m-tiles (an XCD's concurrent workgroups share x rows and
+// weight blocks in its L2), blockIdx remapped so an XCD holds consecutive tiles
+template <int QT, int EPI>
+__global__ __launch_bounds__(QF_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void qpf_kernel(QfArgs A) {
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<qf_mt<QT>()>()];
+  __shared__ float xrow[16 * qf_mt<QT>()];
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int grp = L / (GM * A.tiles_n), first = grp * GM;
+  const int gsz = min(GM, A.tiles_m - first);
+  const int rr = L - first * A.tiles_n;
+  const int tm = first + rr % gsz, tn = rr / gsz;
+  int pi = 0;
+  if constexpr (EPI != PW_EPI_GLU && EPI != PW_EPI_GEGLU) {
+#pragma unroll
+    for (int i = 1; i < kMaxParts; ++i)
+      if (i < A.parts.n && tn >= A.parts.p[i].tile0) pi = i;
+  }
+  qpf_body<QT, EPI>(xs, xrow, A, pi, tm, tn);
+}
+
+template <int QT>
+void qpf_launch(int epi, const QfArgs& A, hipStream_t s) {
+  const dim3 grid(A.tiles_n * A.tiles_m);
+  switch (epi) {
+    case PW_EPI_STORE: qpf_kernel<QT, PW_EPI_STORE><<<grid, QF_T, 0, s>>>(A); break;
+    case PW_EPI_ADD: qpf_kernel<QT, PW_EPI_ADD><<<grid, QF_T, 0, s>>>(A); break;
+    case PW_EPI_GLU: qpf_kernel<QT, PW_EPI_GLU><<<grid, QF_T, 0, s>>>(A); break;
+    case PW_EPI_GEGLU: qpf_kernel<QT, PW_EPI_GEGLU><<<grid, QF_T, 0, s>>>(A); break;
+  }
+}
+
 }  // namespace
 
 int gguf_tiled_chunk_bytes(int qtype) {
@@ -929,6 +1204,57 @@ bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long
     case INT8: moe_launch_t<INT8>(out, out_stride, ws, x, x_stride, q, rs, moe, tiles_cap, tile, N, K, S, s); return true;
   }
   return false;
+}
+
+// Prefill GEMM over tiled GGUF parts (qpf_kernel). STORE: out[:, col .. col + rows) per
+// part; ADD: out is the residual (updated in place); GLU / GEGLU: parts 0 / 1 are gate / up
+// (same format and rows), out[M, rows] = act(gate) * up. Formats: GGUF (Q4_0 .. Q6_K);
+// a mix of formats launches once per format (one body per launch: a two-format kernel
+// spills). Returns false for shapes / formats it does not take (the caller falls back).
+bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x, long ldx, const GgufPart* parts, int nparts,
+                         int M, int K, hipStream_t s) {
+  const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
+  if (M < 1 || K < 256 || K % 256 || nparts < 1 || nparts > kMaxParts || (glu && nparts != 2)) return false;
+  if (epi != PW_EPI_STORE && epi != PW_EPI_ADD && !glu) return false;
+  // 32-bit x offsets inside one 128-row tile
+  if ((long)16 * QF_MT * ldx >= (1L << 31)) return false;
+  for (int i = 0; i < nparts; ++i)
+    if (parts[i].qtype < Q4_0 || parts[i].qtype > Q6_K || parts[i].rows % 16) return false;
+  if (glu && (parts[0].qtype != parts[1].qtype || parts[0].rows != parts[1].rows)) return false;
+  int fmts[kMaxParts], nf = 0;
+  for (int i = 0; i < nparts; ++i) {
+    bool seen = false;
+    for (int j = 0; j < nf; ++j) seen |= fmts[j] == parts[i].qtype;
+    if (!seen) fmts[nf++] = parts[i].qtype;
+  }
+  auto run = [&](int fa) {
+    QfArgs A{};
+    A.x = static_cast<const unsigned short*>(x);
+    A.ldx = ldx;
+    A.out = static_cast<unsigned short*>(out);
+    A.ldo = ldo;
+    A.M = M;
+    A.K = K;
+    int tiles = 0;
+    for (int i = 0; i < nparts; ++i) {
+      if (parts[i].qtype != fa) continue;
+      A.parts.p[A.parts.n++] = Part{static_cast<const unsigned char*>(parts[i].q), nullptr, parts[i].qtype,
+                                    parts[i].rows, parts[i].col, tiles};
+      tiles += (parts[i].rows + QF_ROWS - 1) / QF_ROWS;
+    }
+    A.tiles_n = glu ? (parts[0].rows + QF_ROWS / 2 - 1) / (QF_ROWS / 2) : tiles;
+#define QF_CASE(QT_)                                              \
+  if (fa == QT_) {                                                  \
+    A.tiles_m = (M + 16 * qf_mt<QT_>() - 1) / (16 * qf_mt<QT_>());  \
+    qpf_launch<QT_>(epi, A, s);                                     \
+    return;                                                         \
+  }
+    QF_CASE(Q4_0) QF_CASE(Q4_1) QF_CASE(Q8_0) QF_CASE(Q4_K) QF_CASE(Q5_K) QF_CASE(Q6_K)
+#undef QF_CASE
+  };
+  if (glu && nf != 1) return false;
+  for (int f = 0; f < nf; ++f) run(fmts[f]);
+  return true;
 }
 
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s) {

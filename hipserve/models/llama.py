@@ -29,6 +29,7 @@ import torch.nn.functional as F
 
 from ..config import ModelConfig
 from ..ops import gemm, pgemm
+from ..ops import quant as Q
 from ..ops import reference as ref
 from ..parallel.comm import TPGroup
 
@@ -642,6 +643,9 @@ class LlamaModel:
             elif tp1 and lw.post_attn_norm is None and pgemm.use("add", lw.wo, T):
                 pgemm.gemm_add_(residual, attn, lw.wo)  # residual += o_proj(attn), in the GEMM epilogue
                 ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
+            elif tp1 and lw.post_attn_norm is None and Q.qprefill_ok(lw.wo, T):
+                Q.qprefill(attn, lw.wo, 1, out=residual)  # GGUF blocks, residual add in the epilogue
+                ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
             else:
                 o = self.linear_rowpar(attn, lw.wo)
                 if lw.post_attn_norm is not None:  # Gemma sandwich norm (after the TP reduction)
@@ -666,6 +670,8 @@ class LlamaModel:
                     act = gemm.packed_glu(xn, lw.wgu, gelu)
                 elif cfg.hidden_act in ("silu", "gelu_tanh") and pgemm.use("glu", lw.wgu, T):
                     act = pgemm.gemm_glu(xn, lw.wgu, gelu)
+                elif cfg.hidden_act in ("silu", "gelu_tanh") and Q.qprefill_ok(lw.wgu, T, glu=True):
+                    act = Q.qprefill(xn, lw.wgu, 3 if gelu else 2)  # GGUF blocks, GLU in the epilogue
                 if act8 is not None:
                     h = pgemm.f8_gemm(None, lw.wd, 0, x8=act8)
                 elif act is None:
@@ -673,10 +679,12 @@ class LlamaModel:
                     act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                     self.act_and_mul(act, gu)
                 if act8 is None and (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
-                                     and (pgemm.use("add", lw.wd, T)
+                                     and (pgemm.use("add", lw.wd, T) or Q.qprefill_ok(lw.wd, T)
                                           or (isinstance(lw.wd, gemm.PackedLinear) and T > 64))):
                     if isinstance(lw.wd, gemm.PackedLinear):
                         gemm.packed_prefill(act, lw.wd, 1, out=residual)
+                    elif isinstance(lw.wd, Q.QuantWeight):
+                        Q.qprefill(act, lw.wd, 1, out=residual)
                     else:
                         pgemm.gemm_add_(residual, act, lw.wd)
                     ops.rmsnorm(xn, residual, nxt, eps, out8=x8n)

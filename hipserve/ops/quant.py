@@ -584,6 +584,47 @@ def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = No
     return ws, S
 
 
+# Prefill (M > MAX_FUSED_M) straight from the tiled GGUF blocks (gguf_mfma.hip qpf_kernel:
+# each weight dequantised once per 64-128-token tile, f16 MFMA, store / residual-add / GLU
+# epilogues): no resident bf16 shadow and no per-call dequantise-into-scratch pass.
+# HIPSERVE_QPREFILL=0 restores the scratch + hipBLASLt path.
+QPREFILL = os.environ.get("HIPSERVE_QPREFILL", "1") != "0"
+GGUF_KQT = (0, 1, 2, 3, 4, 5)  # kernel qtypes Q4_0 .. Q6_K
+
+
+def qprefill_ok(w, M: int, glu: bool = False) -> bool:
+    """The block prefill GEMM takes ``w`` at ``M`` rows: a prefill-sized batch, a GGUF
+    QuantWeight without a bf16 shadow whose parts are all tiled with block scales in the
+    subnormal-dequant range; ``glu``: exactly two parts (gate, up) of one format."""
+    if not (QPREFILL and isinstance(w, QuantWeight) and M > MAX_FUSED_M and w.dense is None):
+        return False
+    if not (w.v2 and all(p.kqt in GGUF_KQT for p in w.parts) and hasattr(torch.ops.hipserve, "gguf_prefill")):
+        return False
+    if glu:
+        ps = w.parts
+        return len(ps) == 2 and ps[0].kqt == ps[1].kqt and ps[0].N == ps[1].N
+    return True
+
+
+def _qargs(w: QuantWeight):
+    w.groups  # (re)builds v2_args
+    a = w.v2_args
+    return a[0], a[2], a[3], a[4]
+
+
+def qprefill(x: torch.Tensor, w: QuantWeight, epi: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x @ w.T from the blocks: epi 0 store (into ``out`` or a new [M, N]), 1 residual add
+    (``out`` += ...), 2 / 3 SiLU / GELU GLU of the (gate, up) parts into [M, N/2]."""
+    M = x.shape[0]
+    if out is None:
+        out = torch.empty(M, w.N // 2 if epi in (2, 3) else w.N, dtype=torch.bfloat16, device=x.device)
+    if x.stride(1) != 1 or x.stride(0) % 8:
+        x = x.contiguous()
+    if not torch.ops.hipserve.gguf_prefill(out, x, *_qargs(w), w.K, epi):
+        raise RuntimeError(f"gguf_prefill refused parts {[(p.kqt, p.N) for p in w.parts]} K={w.K} epi={epi}")
+    return out
+
+
 def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
     M = x.shape[0]
     out = torch.empty(M, w.N, dtype=torch.bfloat16, device=x.device)
@@ -623,6 +664,8 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
         return pgemm.f8_gemm(x, w, 0, None if getattr(w, "f8_plain", None) is not None else out)
     if w.dense is not None:  # prefill on the resident bf16 copy: no per-call dequant pass
         return torch.nn.functional.linear(x, w.dense)
+    if x.is_cuda and qprefill_ok(w, M):
+        return qprefill(x, w, 0, out)
     if w.v2 and x.is_cuda and M <= QPREFILL_MAX_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
         _launch_v2(out, _empty(x.device, torch.float32), x, w, 1)  # K15: M-tiled dequant-MFMA GEMM
         return out
@@ -677,8 +720,9 @@ def make_dense_shadows(weights, device, reserve_bytes: int) -> int:
     16 GB of bf16 shadows next to its 4.5 GB of blocks). Decode keeps streaming the
     quantised blocks (the v2 dequant-MFMA kernel: 3.6x fewer bytes); prefill skips the
     per-call dequant pass (~18 GB of HBM traffic per 8K-token Llama-3-8B chunk) and
-    runs hipBLASLt on the copy. Largest weights first (lm_head, gate|up, ...).
-    Returns the bytes added. HIPSERVE_QUANT_SHADOW=0 disables it."""
+    runs hipBLASLt on the copy. Largest weights first (lm_head, gate|up, ...). GGUF
+    weights the block prefill GEMM takes (``qprefill_ok``) get none: their prefill reads
+    the blocks. Returns the bytes added. HIPSERVE_QUANT_SHADOW=0 disables it."""
     import os
 
     if os.environ.get("HIPSERVE_QUANT_SHADOW", "1") == "0" or torch.device(device).type != "cuda":
@@ -688,6 +732,8 @@ def make_dense_shadows(weights, device, reserve_bytes: int) -> int:
     for w in sorted(weights, key=lambda w: -w.N * w.K):
         if w.dense is not None or pgemm.f8_fits(w) or pgemm.f8_fits(w, glu=True):
             continue  # FP8 prefill runs on the e4m3 MFMA from the quantised weights
+        if qprefill_ok(w, MAX_FUSED_M + 1):
+            continue  # GGUF: prefill runs from the blocks (qpf_kernel), HBM holds blocks only
         need = w.N * w.K * 2
         free, _ = torch.cuda.mem_get_info(device)
         if free - need < reserve_bytes:

@@ -108,6 +108,8 @@ for s in $steps; do
     pgtest) run_one tests/test_prefill_gemm_gpu.py ;;
     pwtest) run_one tests/test_prefill_gemm_packed_gpu.py ;;
     longtest) run_one tests/test_long_context_gpu.py ;;
+    qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
+    qpfbench) timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 2048 8192 > $OUT/bench_qpf.log 2>&1; rc=$?; tail -n 40 $OUT/bench_qpf.log; [ $rc -eq 0 ] ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
     tptest) timeout -k 10 1000 python -u -m pytest tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread \
               -p no:cacheprovider > $OUT/test_tp_gpu.log 2>&1; rc=$?; tail -n 20 $OUT/test_tp_gpu.log; [ $rc -eq 0 ] ;;

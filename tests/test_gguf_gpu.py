@@ -391,13 +391,16 @@ def test_int8_pack_quantized_checkpoint_native(tmp_path):
     assert (a - b).abs().max().item() < 5e-2 * b.abs().max().item() + 1e-3
 
 
-def test_dense_shadow_prefill_matches_dequant_path():
+def test_dense_shadow_prefill_matches_dequant_path(monkeypatch):
     """Prefill on the resident bf16 shadow (make_dense_shadows) is bit-identical to the
-    dequant-then-GEMM path (a chunk above QPREFILL_MAX_M: dequant into scratch +
-    hipBLASLt); decode-sized batches keep the quantised kernel."""
+    dequant-then-GEMM path (a chunk above QPREFILL_MAX_M with the block prefill GEMM
+    off: dequant into scratch + hipBLASLt); decode-sized batches keep the quantised
+    kernel."""
+    from hipserve.ops import quant as Q
     from hipserve.ops.quant import QPREFILL_MAX_M, make_dense_shadows
     qw, raws = _rand_qw([(G.Q4_K, 512, 2048), (G.Q6_K, 256, 2048)], seed=5)
     x = torch.randn(QPREFILL_MAX_M + 88, 2048, device="cuda", dtype=torch.bfloat16)
+    monkeypatch.setattr(Q, "QPREFILL", False)
     want = quant_linear(x, qw)
     xs = x[:16].contiguous()
     want_small = quant_linear(xs, qw)
@@ -409,9 +412,8 @@ def test_dense_shadow_prefill_matches_dequant_path():
 
 @pytest.mark.parametrize("M", [65, 130, 256])
 def test_prefill_m_tiled_kernel_vs_fp32(M):
-    """K15: prefill chunks of up to QPREFILL_MAX_M tokens without a bf16 shadow run the
-    dequant-MFMA kernel swept over 64-row M tiles (one launch for all parts), vs an
-    fp32 matmul of the decoded weights."""
+    """K15: prefill chunks without a bf16 shadow run the block prefill GEMM (qpf_kernel,
+    one launch per format), vs an fp32 matmul of the decoded weights."""
     from hipserve.ops import quant as Q
     qw, raws = _rand_qw([(G.Q4_K, 512, 2048), (G.Q6_K, 272, 2048)], seed=M)
     assert qw.dense is None and M <= Q.QPREFILL_MAX_M

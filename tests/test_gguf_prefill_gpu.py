@@ -1,0 +1,122 @@
+"""GGUF prefill GEMM straight from the tiled blocks (gguf_mfma.hip qpf_kernel) vs a plain
+PyTorch fp32 reference on the numpy block decoder's weights: plain store into part
+columns (mixed formats, as Q4_K_M's q|k|v), residual add, SiLU / GELU GLU of gate / up
+parts, ragged M / N, and the f16-range rescale pass for activations beyond 65504."""
+import numpy as np
+import pytest
+import torch
+
+from hipserve.ops import load_library
+from hipserve.ops.quant import QuantWeight
+from hipserve.weights import gguf as G
+
+pytestmark = pytest.mark.gpu
+QTYPES = [G.Q4_0, G.Q4_1, G.Q8_0, G.Q4_K, G.Q5_K, G.Q6_K]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib():
+    load_library()
+
+
+def _mat(N, K, seed):
+    return np.random.default_rng(seed).standard_normal((N, K)).astype(np.float32) * 0.05
+
+
+def _ref_w(w, qt):
+    """fp32 weights as the numpy block decoder reads the quantised blocks."""
+    N, K = w.shape
+    return torch.from_numpy(G.dequantize(G.quantize(w, qt), qt, N * K).reshape(N, K)).cuda()
+
+
+def _args(qw):
+    cols = np.cumsum([0] + [p.N for p in qw.parts])[:-1].tolist()
+    return [p.q for p in qw.parts], [p.kqt for p in qw.parts], [p.N for p in qw.parts], cols
+
+
+def _close(got, want, tol=1e-2):
+    err = (got.float() - want).abs().max().item()
+    assert err <= tol * want.abs().max().item() + 1e-3, (err, want.abs().max().item())
+
+
+@pytest.mark.parametrize("qt", QTYPES)
+@pytest.mark.parametrize("M,N,K", [(130, 272, 512), (1000, 512, 1024), (37, 1024, 256), (300, 4096, 512)])
+def test_store(qt, M, N, K):
+    w = _mat(N, K, M + N)
+    qw = QuantWeight.from_float(w, qt, "cuda")
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 0)
+    _close(out, x.float() @ _ref_w(w, qt).T)
+
+
+def test_mixed_formats_strided():
+    """q | k | v with v in Q6_K (Q4_K_M), written at their columns of a wider output;
+    x a strided view."""
+    K, M = 768, 333
+    mats = [_mat(512, K, 1), _mat(128, K, 2), _mat(128, K, 3)]
+    qw = QuantWeight.from_float(mats[:2], G.Q4_K, "cuda")
+    qw.parts.append(QuantWeight.from_float(mats[2], G.Q6_K, "cuda").parts[0])
+    xb = torch.randn(M, K + 64, device="cuda", dtype=torch.bfloat16)
+    x = xb[:, 16:16 + K]
+    out = torch.full((M, 800), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 0)
+    wd = torch.cat([_ref_w(m, t) for m, t in zip(mats, (G.Q4_K, G.Q4_K, G.Q6_K))])
+    _close(out[:, :768], x.float() @ wd.T)
+    assert out[:, 768:].isnan().all()  # untouched past the parts
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K])
+def test_residual_add(qt):
+    M, N, K = 517, 1024, 1024
+    w = _mat(N, K, 9)
+    qw = QuantWeight.from_float(w, qt, "cuda")
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    res0 = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    res = res0.clone()
+    assert torch.ops.hipserve.gguf_prefill(res, x, *_args(qw), K, 1)
+    h = (x.float() @ _ref_w(w, qt).T).to(torch.bfloat16).float()
+    _close(res, h + res0.float(), tol=2e-2)
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q4_0, G.Q6_K])
+@pytest.mark.parametrize("act", ["silu", "gelu"])
+@pytest.mark.parametrize("M,I", [(700, 384), (64, 1088)])
+def test_glu(qt, act, M, I):
+    K = 512
+    g, u = _mat(I, K, 3), _mat(I, K, 4)
+    qw = QuantWeight.from_float([g, u], qt, "cuda")
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.full((M, I), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 2 if act == "silu" else 3)
+    gv = (x.float() @ _ref_w(g, qt).T).to(torch.bfloat16).float()
+    uv = (x.float() @ _ref_w(u, qt).T).to(torch.bfloat16).float()
+    f = torch.nn.functional.silu if act == "silu" else (lambda t: torch.nn.functional.gelu(t, approximate="tanh"))
+    _close(out, f(gv) * uv, tol=2e-2)
+
+
+@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K])
+def test_f16_range_rescale(qt):
+    """Rows with activations beyond the f16 range take the per-row power-of-two rescale
+    pass and stay exact; the other rows are unaffected."""
+    M, N, K = 200, 256, 512
+    w = _mat(N, K, 5)
+    qw = QuantWeight.from_float(w, qt, "cuda")
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    x[3, 7] = 3.0e5
+    x[150, :] *= 1.0e6
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 0)
+    want = x.float() @ _ref_w(w, qt).T
+    assert out.isfinite().all()
+    for r in (3, 150, 0, 199):
+        _close(out[r], want[r])
+
+
+def test_rejects():
+    K = 256
+    qw = QuantWeight.from_float([_mat(64, K, 1), _mat(64, K, 2)], G.Q4_K, "cuda")
+    qw.parts[1] = QuantWeight.from_float(_mat(64, K, 2), G.Q6_K, "cuda").parts[0]
+    x = torch.randn(10, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(10, 64, device="cuda", dtype=torch.bfloat16)
+    assert not torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 2)  # GLU over two formats

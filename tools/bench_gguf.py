@@ -66,7 +66,9 @@ def main():
     ap.add_argument("--splits", type=int, nargs="*", default=None)
     ap.add_argument("--fp8", action="store_true", help="FP8 e4m3 per-channel weights of the same shapes")
     ap.add_argument("--prefill", action="store_true",
-                    help="M > 64: the M-tiled dequant-MFMA kernel vs dequant-to-scratch + hipBLASLt vs a bf16 shadow")
+                    help="M > 64: the prefill GEMM from the blocks (qpf) and the M-tiled dequant-MFMA kernel vs "
+                         "dequant-to-scratch + hipBLASLt vs a bf16 shadow")
+    ap.add_argument("--no-mtiled", action="store_true", help="--prefill: skip the (slow at large M) M-tiled kernel")
     a = ap.parse_args()
     load_library()
     rng = np.random.default_rng(0)
@@ -99,9 +101,17 @@ def main():
                         off += p.N
                     return torch.nn.functional.linear(x, buf)
 
-                for kern, fn in (("m_tiled_mfma", lambda: Q._launch_v2(out, Q._empty(x.device, torch.float32), x, qw, 1)),
-                                 ("dequant+hipblaslt", deq_blas),
-                                 ("bf16_shadow_hipblaslt", lambda: torch.nn.functional.linear(x, dense))):
+                cols = np.cumsum([0] + [p.N for p in qw.parts])[:-1].tolist()
+                qargs = ([p.q for p in qw.parts], [p.kqt for p in qw.parts], [p.N for p in qw.parts], cols)
+                act = torch.empty(M, qw.N // 2, device="cuda", dtype=torch.bfloat16)
+                kerns = [("qpf_prefill", lambda: torch.ops.hipserve.gguf_prefill(out, x, *qargs, qw.K, 0))]
+                if name == "gate_up":
+                    kerns.append(("qpf_prefill_glu", lambda: torch.ops.hipserve.gguf_prefill(act, x, *qargs, qw.K, 2)))
+                if not a.no_mtiled:
+                    kerns.append(("m_tiled_mfma", lambda: Q._launch_v2(out, Q._empty(x.device, torch.float32), x, qw, 1)))
+                kerns += [("dequant+hipblaslt", deq_blas),
+                          ("bf16_shadow_hipblaslt", lambda: torch.nn.functional.linear(x, dense))]
+                for kern, fn in kerns:
                     us = _time(fn, reps=10, graph_reps=5)
                     print(json.dumps({"proj": name, "M": M, "kernel": kern, "us": round(us, 1),
                                       "TFLOPs": round(2 * M * qw.N * qw.K / us / 1e6, 1)}), flush=True)
