@@ -100,10 +100,13 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16 = nullptr);
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s);
-// prefill GEMM straight from the tiled GGUF blocks (epi: PW_EPI_STORE / ADD / GLU / GEGLU;
-// GLU: parts 0 / 1 = gate / up); false if the formats / shapes are not taken
-bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x, long ldx, const GgufPart* parts, int nparts,
-                         int M, int K, hipStream_t s);
+// prefill GEMM straight from the tiled GGUF blocks on launch_x_f16_pairs' x16 / rsc (epi:
+// PW_EPI_STORE / ADD / GLU / GEGLU; GLU: parts 0 / 1 = gate / up); false if the formats /
+// shapes are not taken
+bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x16, const float* rsc, const GgufPart* parts,
+                         int nparts, int M, int K, hipStream_t s);
+// x [M, K] bf16 -> x16 [M, K] f16 (pair order, rows pre-scaled by 1 / rsc[m], powers of two)
+void launch_x_f16_pairs(void* x16, float* rsc, const void* x, long ldx, int M, int K, hipStream_t s);
 // quantised MoE experts (tiled layout per expert, stacked [E][N/16][K/256][chunk]) over
 // moe_align tiles of 16/32/64 slots: out[slot, N] bf16 (S == 1) or ws[S, nslots, N] fp32.
 // qtype: FP8 (rs [E, N]) or INT8 (the checkpoint expert formats). Returns false for an

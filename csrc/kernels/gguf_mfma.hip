@@ -854,43 +854,53 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
 // ---------------------------------------------------------------- prefill GEMM
 // qpf_kernel (GGUF prefill without the resident bf16 shadow):
 // C[M, N] = X[M, K] . W^T straight from the tiled blocks, every weight dequantised ONCE
-// per 128-token tile (the M-swept qgemm2 above does it once per 64 tokens and stages x
-// for 128 weight rows; a dequantise-into-scratch + hipBLASLt pass writes and re-reads a
+// per 64-128-token tile (the M-swept qgemm2 above does it once per 64 tokens and stages
+// x for 128 weight rows; a dequantise-into-scratch + hipBLASLt pass writes and re-reads a
 // bf16 copy of the whole matrix per call).
+//   * X arrives as x16 (x_f16_pairs_kernel below): f16 in the weights' pair order, each
+//     row pre-scaled by a power of two 2^-k that keeps it inside the f16 range, the
+//     2^k in rsc[m] applied in the epilogue. Staging is then a plain 16-byte copy into
+//     LDS: converting bf16 x in every workgroup was 40 % of the kernel's VALU
+//     (tools/asm_stats.py: 380 VALU per super-chunk and wave, 160 of them x conversion);
 //   * workgroup = 8 waves x 2 row groups = 256 weight rows x 128 tokens, two waves per
 //     SIMD (64 accumulators, <= 256 registers each: one wave's dequant VALU runs beside
-//     the other's MFMAs); x (bf16 -> f16, the weights' pair order)
-//     staged once per 256-k super-chunk into a double-buffered LDS image (2 x 72 KiB),
-//     ONE barrier per super-chunk; the next super-chunk's x and weight blocks are in
-//     flight while this one is dequantised and multiplied;
+//     the other's MFMAs); x staged once per 256-k super-chunk into a double-buffered LDS
+//     image (2 x 72 KiB), ONE barrier per super-chunk; the next super-chunk's x and
+//     weight blocks are in flight while this one is dequantised and multiplied;
 //   * per 32-k step a wave dequantises 2 weight fragments (2 VALU per pair,
-//     Dec::step) and issues 16 f16 MFMAs against 8 x fragments read from LDS: the
-//     dequant cost per MFMA is 1/8 of the decode kernel's at M = 16;
+//     Dec::step) and issues 16 f16 MFMAs against 8 x fragments read from LDS;
 //   * weight bytes per MFMA are 3.5x (Q4_K) fewer than a bf16 GEMM's, which is what
 //     bounded the bf16 packed-layout kernel (profiles/r4_pw_diag_and_bench.log);
 //   * epilogues: STORE (part columns), ADD (C is the residual: C = bf16(bf16(acc) + C)),
 //     GLU (parts 0 / 1 = gate / up of the same format: a wave's row group 0 is gate
-//     rows, 1 the matching up rows, act = silu(gate) * up in registers);
-//   * f16 range: the same non-finite vote + per-row power-of-two rescale pass as qgemm2.
-constexpr int QF_RT = 2, QF_MT = 8, QF_W = 8, QF_T = 64 * QF_W;
-constexpr int QF_ROWS = 16 * QF_RT * QF_W;  // weight rows per STORE / ADD tile (GLU: 128 act columns)
-// tokens per tile: 128 (MT = 8); Q5_K / Q6_K / Q8_0 (larger raw blocks: 16-19 registers per row
-// group and buffer) 64, which keeps them within 256 registers without spills
-template <int QT>
-constexpr int qf_mt() { return QT == Q5_K || QT == Q6_K || QT == Q8_0 ? 4 : 8; }
+//     rows, 1 the matching up rows, act = silu(gate) * up in registers).
+// Two shapes, both 256 weight rows x (64 or 128) tokens per workgroup (QF_ROWS):
+//   (RT 2, 8 waves): two waves per SIMD, <= 256 registers each; every x fragment read
+//     from LDS feeds 2 MFMAs — at 128 B per clock of LDS per CU that caps the MFMA pipe;
+//   (RT 4, 4 waves): one wave per SIMD (512 registers), every x fragment feeds 4 MFMAs:
+//     half the LDS traffic per MFMA, dequant VALU and MFMAs interleaved in one wave.
+constexpr int QF_ROWS = 256;  // weight rows per STORE / ADD tile (GLU: 128 act columns)
+constexpr int QF_MT = 8;
+HS_HOST_DEVICE constexpr int qf_waves(int rt) { return QF_ROWS / 16 / rt; }
+// tokens per tile: 128 (MT = 8); at RT 4, Q5_K / Q6_K (larger raw blocks: 16-19
+// registers per row group and buffer) 64, which keeps them within 512 registers
+template <int QT, int RT>
+constexpr int qf_mt() { return RT == 4 && (QT == Q5_K || QT == Q6_K) ? 4 : 8; }
 struct QfArgs {
   Parts parts;
-  const unsigned short* x;
+  const unsigned short* x16;  // [M, ldx] f16, pair order, row m scaled by 1 / rsc[m]
+  const float* rsc;           // [M] power-of-two row scales
   long ldx;
   unsigned short* out;
   long ldo;
   int M, K, tiles_n, tiles_m;
 };
 
-template <int QT, int EPI>
-HS_DEVICE void qpf_body(_Float16 (&xs)[2][4 * x_plane<qf_mt<QT>()>()], float* xrow, const QfArgs& A, int pi, int tm,
-                        int tn) {
-  constexpr int RT = QF_RT, MT = qf_mt<QT>(), NT = QF_T, XR = 16 * MT;
+template <int QT, int EPI, int RT>
+HS_DEVICE void qpf_body(_Float16* xs_, const QfArgs& A, int pi, int tm, int tn) {
+  constexpr int NW = qf_waves(RT), MT = qf_mt<QT, RT>(), NT = 64 * NW, XR = 16 * MT;
+  constexpr int XSZ = 4 * x_plane<MT>();  // one LDS buffer (f16)
+  auto xs = [&](int buf) { return xs_ + buf * XSZ; };
   constexpr int CB = chunk_bytes<QT>();
   constexpr bool kGlu = EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -903,149 +913,97 @@ HS_DEVICE void qpf_body(_Float16 (&xs)[2][4 * x_plane<qf_mt<QT>()>()], float* xr
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
     // GLU: row groups 0 .. RT/2 - 1 gate, RT/2 .. RT - 1 the matching up rows
-    gi[r] = kGlu ? (tn * QF_W + wave) * (RT / 2) + r % (RT / 2) : (tn - P.tile0) * (QF_ROWS / 16) + wave * RT + r;
+    gi[r] = kGlu ? (tn * NW + wave) * (RT / 2) + r % (RT / 2) : (tn - P.tile0) * (QF_ROWS / 16) + wave * RT + r;
     const unsigned char* q = kGlu && r >= RT / 2 ? A.parts.p[1].q : P.q;
     base[r] = q + (long)min(gi[r], ngroups - 1) * nsb * CB;
   }
-  constexpr int XP = XR * 32 / NT, XH = XP / 2;  // 8 fragments of 8 per thread and super-chunk, in 2 halves
+  constexpr int XP = XR * 32 / NT;  // 16-byte x fragments per thread and super-chunk
+  // thread -> x row 8 i + (tid >> 5) (i < XP), fragment tid & 31: one VGPR offset, the row
+  // step a scalar; rows >= M lie outside the buffer range and read as zero
+  static_assert(NT % 32 == 0 && XP * NT == XR * 32, "x staging must divide evenly");
+  constexpr int RS = NT / 32;  // rows per staging pass
   const int mrow0 = tm * XR;
-  const unsigned short* xg = A.x + (long)mrow0 * A.ldx;
-  int xo[XP];  // rows >= M clamped to M - 1 (computed, never stored)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A.x16 + (long)mrow0 * A.ldx), 0, (int)((long)min(XR, M - mrow0) * A.ldx * 2), 0x00020000);
+  const int xfr = tid & 31, xrow = tid >> 5;
+  const int xo = (xrow * (int)A.ldx + kbase<QT>(xfr >> 3, xfr & 7)) * 2;
+  const int xd = (xfr >> 3) * x_plane<MT>() + xrow * kXR + (xfr & 7) * 8;
+  const int xstep = RS * (int)A.ldx * 2;
+  u32x4 xv[XP];
+  auto load_x = [&](int sb) {
 #pragma unroll
-  for (int i = 0; i < XP; ++i) {
-    const int idx = i * NT + tid, row = idx >> 5, fr = idx & 31;
-    xo[i] = (min(mrow0 + row, M - 1) - mrow0) * (int)A.ldx + kbase<QT>(fr >> 3, fr & 7);
-  }
-  u16x8 xv[XH];  // one half of the staging items in registers at a time
-  auto load_x = [&](int sb, int h) {
-#pragma unroll
-    for (int i = 0; i < XH; ++i) xv[i] = *reinterpret_cast<const u16x8*>(xg + xo[h * XH + i] + sb * 256);
+    for (int i = 0; i < XP; ++i) xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, xo, i * xstep + sb * 512, 0);
   };
-  auto store_x = [&](int buf, int h, auto scaled) {
+  auto store_x = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < XH; ++i) {
-      const int idx = (h * XH + i) * NT + tid, row = idx >> 5, fr = idx & 31;
-      const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
-      float f[8] = {bf_lo(w[0]), bf_lo(w[1]), bf_hi(w[0]), bf_hi(w[1]),
-                    bf_lo(w[2]), bf_lo(w[3]), bf_hi(w[2]), bf_hi(w[3])};  // pair order {0, 2, 1, 3, 4, 6, 5, 7}
-      if constexpr (decltype(scaled)::value) {
-        const float sc = xrow[row];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] *= sc;
-      }
-      f16x8 hv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) hv[e] = static_cast<_Float16>(f[e]);
-      *reinterpret_cast<f16x8*>(&xs[buf][(fr >> 3) * x_plane<MT>() + row * kXR + (fr & 7) * 8]) = hv;
-    }
+    for (int i = 0; i < XP; ++i) *reinterpret_cast<u32x4*>(xs(buf) + xd + i * RS * kXR) = xv[i];
   };
 
   f32x4 acc[RT][MT];
-  Raw rawA[RT], rawB[RT];
-  auto run = [&](auto scaled) {
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r], g, c, lane, rawA[r]);
-    load_x(0, 0);
-    store_x(0, 0, scaled);
-    load_x(0, 1);
-    store_x(0, 1, scaled);
-    __syncthreads();
-    // per super-chunk: the next one's weight blocks and first x half go out first; the x
-    // half is written to the other LDS buffer (read last in the previous super-chunk, so
-    // free since its barrier) after step 3, when the second half is loaded, and that one
-    // at the end: 4 x registers per thread instead of 8. The last super-chunk re-reads
-    // itself (no branch; its stores land in the unused buffer).
-    auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
-      const int buf = sb & 1;
-      const int sn = min(sb + 1, nsb - 1);
-      load_x(sn, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
-      __builtin_amdgcn_sched_barrier(0);
-      const _Float16* xb = &xs[buf][g * x_plane<MT>() + c * kXR];
-      Dec<QT> dec[RT];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        if (s == 4) {
-          store_x(buf ^ 1, 0, scaled);
-          load_x(sn, 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        f16x8 a[RT];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          // 4 x fragments read from LDS ahead of their MFMAs (left alone the compiler
-          // reuses one register and every MFMA waits out an LDS round trip)
-          f16x8 b[MT / 2];
-#pragma unroll
-          for (int t = 0; t < MT / 2; ++t) b[t] = *reinterpret_cast<const f16x8*>(xb + 16 * (h * MT / 2 + t) * kXR + 8 * s);
-          __builtin_amdgcn_sched_barrier(0);
-          if (h == 0) {
-#pragma unroll
-            for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
-          }
-#pragma unroll
-          for (int t = 0; t < MT / 2; ++t)
-#pragma unroll
-            for (int r = 0; r < RT; ++r)
-              acc[r][h * MT / 2 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b[t], acc[r][h * MT / 2 + t], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      store_x(buf ^ 1, 1, scaled);
-      __syncthreads();
-    };
-    int sb = 0;
-    for (; sb + 1 < nsb; sb += 2) {
-      iter(sb, rawA, rawB);
-      iter(sb + 1, rawB, rawA);
-    }
-    if (sb < nsb) iter(sb, rawA, rawB);
-  };
-  run(std::false_type{});
-  bool bad = false;
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Raw rawA[RT], rawB[RT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(acc[r][t][e]);
-  if (__syncthreads_or(bad)) {  // some x beyond the f16 range: per-row 2^-k pre-scale, second pass
-    unsigned* xm = reinterpret_cast<unsigned*>(xrow);
-    if (tid < XR) xm[tid] = 0u;
-    __syncthreads();
-    for (int sb2 = 0; sb2 < nsb; ++sb2)
+  for (int r = 0; r < RT; ++r) load_raw<QT>(base[r], g, c, lane, rawA[r]);
+  load_x(0);
+  store_x(0);
+  __syncthreads();
+  // per super-chunk: the next one's x and weight blocks go out first (x first: the
+  // in-order vmcnt wait before its LDS store leaves the weights in flight) and the x is
+  // written to the other LDS buffer (read last in the previous super-chunk, free since
+  // its barrier) at the end. The last super-chunk re-reads itself (no branch; its store
+  // lands in the unused buffer).
+  auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
+    const int buf = sb & 1;
+    const int sn = min(sb + 1, nsb - 1);
+    load_x(sn);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
+    __builtin_amdgcn_sched_barrier(0);
+    const _Float16* xb = xs(buf) + g * x_plane<MT>() + c * kXR;
+    Dec<QT> dec[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      f16x8 a[RT];
+#pragma unroll
       for (int h = 0; h < 2; ++h) {
-        load_x(sb2, h);
+        // half the step's x fragments read from LDS ahead of their MFMAs (left alone the
+        // compiler reuses one register and every MFMA waits out an LDS round trip)
+        f16x8 b[MT / 2];
 #pragma unroll
-        for (int i = 0; i < XH; ++i) {
-          const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
-          unsigned mx = 0;
+        for (int t = 0; t < MT / 2; ++t) b[t] = *reinterpret_cast<const f16x8*>(xb + 16 * (h * MT / 2 + t) * kXR + 8 * s);
+        __builtin_amdgcn_sched_barrier(0);
+        if (h == 0) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) mx = max(mx, max((w[e] << 16) & 0x7FFF0000u, w[e] & 0x7FFF0000u));
-          atomicMax(&xm[((h * XH + i) * NT + tid) >> 5], mx);
+          for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
         }
+#pragma unroll
+        for (int t = 0; t < MT / 2; ++t)
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            acc[r][h * MT / 2 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b[t], acc[r][h * MT / 2 + t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    __syncthreads();
-    if (tid < XR) {
-      const int ex = (int)(xm[tid] >> 23) - 127;
-      xrow[tid] = __builtin_bit_cast(float, (unsigned)(127 - min(126, max(0, ex - 14))) << 23);
     }
+    store_x(buf ^ 1);
     __syncthreads();
-    run(std::true_type{});
+  };
+  int sb = 0;
+  for (; sb + 1 < nsb; sb += 2) {
+    iter(sb, rawA, rawB);
+    iter(sb + 1, rawB, rawA);
+  }
+  if (sb < nsb) iter(sb, rawA, rawB);
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const float un = 1.f / xrow[16 * t + c];
+  for (int t = 0; t < MT; ++t) {  // undo the row pre-scale (exact: a power of two)
+    const float sc = A.rsc[min(mrow0 + 16 * t + c, M - 1)];
 #pragma unroll
-      for (int r = 0; r < RT; ++r) acc[r][t] *= un;
-    }
+    for (int r = 0; r < RT; ++r) acc[r][t] *= sc;
   }
   // lane holds C[m = mrow0 + 16 t + c][rows 16 gi + 4 g + j]
   if constexpr (kGlu) {
@@ -1096,10 +1054,11 @@ HS_DEVICE void qpf_body(_Float16 (&xs)[2][4 * x_plane<qf_mt<QT>()>()], float* xr
 
 // tiles: n-major groups of 8 m-tiles (an XCD's concurrent workgroups share x rows and
 // weight blocks in its L2), blockIdx remapped so an XCD holds consecutive tiles
-template <int QT, int EPI>
-__global__ __launch_bounds__(QF_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void qpf_kernel(QfArgs A) {
-  __shared__ __attribute__((aligned(16))) _Float16 xs[2][4 * x_plane<qf_mt<QT>()>()];
-  __shared__ float xrow[16 * qf_mt<QT>()];
+template <int QT, int EPI, int RT>
+__global__ __launch_bounds__(64 * qf_waves(RT)) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 2 : 1, RT == 2 ? 2 : 1)))
+void qpf_kernel(QfArgs A) {
+  constexpr int XSZ = 4 * x_plane<qf_mt<QT, RT>()>();
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XSZ];
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int GM = 8;
   const int grp = L / (GM * A.tiles_n), first = grp * GM;
@@ -1112,17 +1071,79 @@ __global__ __launch_bounds__(QF_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     for (int i = 1; i < kMaxParts; ++i)
       if (i < A.parts.n && tn >= A.parts.p[i].tile0) pi = i;
   }
-  qpf_body<QT, EPI>(xs, xrow, A, pi, tm, tn);
+  qpf_body<QT, EPI, RT>(xs, A, pi, tm, tn);
+}
+
+template <int QT, int RT>
+void qpf_launch_rt(int epi, const QfArgs& A, hipStream_t s) {
+  const dim3 grid(A.tiles_n * A.tiles_m), block(64 * qf_waves(RT));
+  switch (epi) {
+    case PW_EPI_STORE: qpf_kernel<QT, PW_EPI_STORE, RT><<<grid, block, 0, s>>>(A); break;
+    case PW_EPI_ADD: qpf_kernel<QT, PW_EPI_ADD, RT><<<grid, block, 0, s>>>(A); break;
+    case PW_EPI_GLU: qpf_kernel<QT, PW_EPI_GLU, RT><<<grid, block, 0, s>>>(A); break;
+    case PW_EPI_GEGLU: qpf_kernel<QT, PW_EPI_GEGLU, RT><<<grid, block, 0, s>>>(A); break;
+  }
+}
+
+// HIPSERVE_QPF_RT: row groups per wave (2: 8 waves, 4: 4 waves); default 4
+int qpf_rt() {
+  static const int v = [] {
+    const char* e = getenv("HIPSERVE_QPF_RT");
+    return e != nullptr && atoi(e) == 2 ? 2 : 4;
+  }();
+  return v;
 }
 
 template <int QT>
-void qpf_launch(int epi, const QfArgs& A, hipStream_t s) {
-  const dim3 grid(A.tiles_n * A.tiles_m);
-  switch (epi) {
-    case PW_EPI_STORE: qpf_kernel<QT, PW_EPI_STORE><<<grid, QF_T, 0, s>>>(A); break;
-    case PW_EPI_ADD: qpf_kernel<QT, PW_EPI_ADD><<<grid, QF_T, 0, s>>>(A); break;
-    case PW_EPI_GLU: qpf_kernel<QT, PW_EPI_GLU><<<grid, QF_T, 0, s>>>(A); break;
-    case PW_EPI_GEGLU: qpf_kernel<QT, PW_EPI_GEGLU><<<grid, QF_T, 0, s>>>(A); break;
+void qpf_launch(int epi, QfArgs A, hipStream_t s) {
+  const int rt = QT == Q8_0 ? 2 : qpf_rt();  // Q8_0 spills at RT 4
+  const int bm = 16 * (rt == 2 ? qf_mt<QT, 2>() : qf_mt<QT, 4>());
+  A.tiles_m = (A.M + bm - 1) / bm;
+  if constexpr (QT == Q8_0) {
+    qpf_launch_rt<QT, 2>(epi, A, s);
+  } else {
+    if (rt == 2)
+      qpf_launch_rt<QT, 2>(epi, A, s);
+    else
+      qpf_launch_rt<QT, 4>(epi, A, s);
+  }
+}
+
+// x [M, K] bf16 -> x16 [M, K] f16 in the pair order {0, 2, 1, 3, 4, 6, 5, 7} of every
+// aligned 8-run, each row scaled by 2^-k (k >= 0, the smallest keeping max |x| below
+// 2^15), rsc[m] = 2^k: the prefill GEMM's operand, converted once per activation instead
+// of in every workgroup; bf16 -> f32 exact, -> f16 round to nearest (values below the f16
+// normal range lose low bits, as in the decode kernel's staging)
+__global__ __launch_bounds__(256) void x_f16_pairs_kernel(unsigned short* __restrict__ x16, float* __restrict__ rsc,
+                                                          const unsigned short* __restrict__ x, long ldx, int K) {
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const u16x8* src = reinterpret_cast<const u16x8*>(x + (long)row * ldx);
+  u16x8* dst = reinterpret_cast<u16x8*>(x16 + (long)row * K);
+  const int n8 = K >> 3;
+  unsigned mx = 0;
+  for (int j = tid; j < n8; j += 256) {
+    const u32x4 w = __builtin_bit_cast(u32x4, src[j]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mx = max(mx, max((w[e] << 16) & 0x7FFF0000u, w[e] & 0x7FFF0000u));
+  }
+  __shared__ unsigned red[4];
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = max(max(red[0], red[1]), max(red[2], red[3]));
+  // 2^-k with max |x| 2^-k < 2^15 (inf / NaN rows: k = 126, the result stays non-finite)
+  const int ex = (int)(mx >> 23) - 127;
+  const int k = min(126, max(0, ex - 14));
+  const float down = __builtin_bit_cast(float, (unsigned)(127 - k) << 23);
+  if (tid == 0) rsc[row] = __builtin_bit_cast(float, (unsigned)(127 + k) << 23);
+  constexpr int ord[8] = {0, 2, 1, 3, 4, 6, 5, 7};
+  for (int j = tid; j < n8; j += 256) {
+    const u16x8 v = src[j];
+    u16x8 h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      h[e] = __builtin_bit_cast(unsigned short, static_cast<_Float16>(bf16_to_f32(v[ord[e]]) * down));
+    dst[j] = h;
   }
 }
 
@@ -1206,18 +1227,25 @@ bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long
   return false;
 }
 
-// Prefill GEMM over tiled GGUF parts (qpf_kernel). STORE: out[:, col .. col + rows) per
+// Prefill GEMM over tiled GGUF parts (qpf_kernel) on x16 / rsc from launch_x_f16_pairs
+// (row stride K). STORE: out[:, col .. col + rows) per
 // part; ADD: out is the residual (updated in place); GLU / GEGLU: parts 0 / 1 are gate / up
 // (same format and rows), out[M, rows] = act(gate) * up. Formats: GGUF (Q4_0 .. Q6_K);
 // a mix of formats launches once per format (one body per launch: a two-format kernel
 // spills). Returns false for shapes / formats it does not take (the caller falls back).
-bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x, long ldx, const GgufPart* parts, int nparts,
-                         int M, int K, hipStream_t s) {
+void launch_x_f16_pairs(void* x16, float* rsc, const void* x, long ldx, int M, int K, hipStream_t s) {
+  x_f16_pairs_kernel<<<M, 256, 0, s>>>(static_cast<unsigned short*>(x16), rsc, static_cast<const unsigned short*>(x),
+                                       ldx, K);
+}
+
+bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x16, const float* rsc, const GgufPart* parts,
+                         int nparts, int M, int K, hipStream_t s) {
+  const long ldx = K;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (M < 1 || K < 256 || K % 256 || nparts < 1 || nparts > kMaxParts || (glu && nparts != 2)) return false;
   if (epi != PW_EPI_STORE && epi != PW_EPI_ADD && !glu) return false;
   // 32-bit x offsets inside one 128-row tile
-  if ((long)16 * QF_MT * ldx >= (1L << 31)) return false;
+  if ((long)16 * QF_MT * ldx * 2 >= (1L << 31)) return false;
   for (int i = 0; i < nparts; ++i)
     if (parts[i].qtype < Q4_0 || parts[i].qtype > Q6_K || parts[i].rows % 16) return false;
   if (glu && (parts[0].qtype != parts[1].qtype || parts[0].rows != parts[1].rows)) return false;
@@ -1229,7 +1257,8 @@ bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x, long ldx, 
   }
   auto run = [&](int fa) {
     QfArgs A{};
-    A.x = static_cast<const unsigned short*>(x);
+    A.x16 = static_cast<const unsigned short*>(x16);
+    A.rsc = rsc;
     A.ldx = ldx;
     A.out = static_cast<unsigned short*>(out);
     A.ldo = ldo;
@@ -1243,11 +1272,10 @@ bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x, long ldx, 
       tiles += (parts[i].rows + QF_ROWS - 1) / QF_ROWS;
     }
     A.tiles_n = glu ? (parts[0].rows + QF_ROWS / 2 - 1) / (QF_ROWS / 2) : tiles;
-#define QF_CASE(QT_)                                              \
-  if (fa == QT_) {                                                  \
-    A.tiles_m = (M + 16 * qf_mt<QT_>() - 1) / (16 * qf_mt<QT_>());  \
-    qpf_launch<QT_>(epi, A, s);                                     \
-    return;                                                         \
+#define QF_CASE(QT_)          \
+  if (fa == QT_) {              \
+    qpf_launch<QT_>(epi, A, s); \
+    return;                     \
   }
     QF_CASE(Q4_0) QF_CASE(Q4_1) QF_CASE(Q8_0) QF_CASE(Q4_K) QF_CASE(Q5_K) QF_CASE(Q6_K)
 #undef QF_CASE

@@ -326,25 +326,44 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   return S;
 }
 
-// prefill GEMM on the tiled GGUF parts (gguf_mfma.hip qpf_kernel): epi 0 store at each
-// part's column, 1 residual add (out += x . W^T, in place), 2 / 3 SiLU / GELU GLU of parts
-// 0 (gate) and 1 (up) into out[M, rows]. Returns false when the kernel does not take it.
-bool gguf_prefill(at::Tensor& out, const at::Tensor& x, const std::vector<at::Tensor>& qs,
+// x [M, >= K] bf16 -> x16 [M, K] f16 in the GGUF kernels' pair order, each row scaled by
+// 1 / rsc[m] (a power of two keeping it in the f16 range): the prefill GEMM's operand
+void x_f16_pairs(at::Tensor& x16, at::Tensor& rsc, const at::Tensor& x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x);
+  const int M = x.size(0), K = x16.size(1);
+  TORCH_CHECK(x16.scalar_type() == at::kHalf && x16.is_contiguous() && x16.size(0) == M && K % 8 == 0 &&
+                  x.size(1) >= K && x.stride(0) % 8 == 0 && x16.device() == x.device(),
+              "x_f16_pairs: x16 f16 [M, K] contiguous, K % 8, 16-byte x rows");
+  TORCH_CHECK(rsc.scalar_type() == at::kFloat && rsc.is_contiguous() && rsc.numel() >= M && rsc.device() == x.device(),
+              "x_f16_pairs: rsc fp32 [M]");
+  if (M == 0) return;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  hipserve::launch_x_f16_pairs(x16.data_ptr(), rsc.data_ptr<float>(), x.data_ptr(), x.stride(0), M, K, cur_stream());
+}
+
+// prefill GEMM on the tiled GGUF parts (gguf_mfma.hip qpf_kernel) over x16 / rsc from
+// x_f16_pairs: epi 0 store at each part's column, 1 residual add (out += x . W^T, in
+// place), 2 / 3 SiLU / GELU GLU of parts 0 (gate) and 1 (up) into out[M, rows]. Returns
+// false when the kernel does not take it.
+bool gguf_prefill(at::Tensor& out, const at::Tensor& x16, const at::Tensor& rsc, const std::vector<at::Tensor>& qs,
                   const std::vector<int64_t>& qtypes, const std::vector<int64_t>& rows, const std::vector<int64_t>& cols,
                   int64_t K, int64_t epi) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  CHECK_DEV(x16); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   const int np = qs.size();
   TORCH_CHECK(np >= 1 && np <= 4 && (int)qtypes.size() == np && (int)rows.size() == np && (int)cols.size() == np,
               "gguf_prefill: 1-4 parts");
-  TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && x.stride(0) % 8 == 0, "gguf_prefill: K % 256, 16-byte x rows");
-  const int M = x.size(0);
+  TORCH_CHECK(x16.scalar_type() == at::kHalf && x16.is_contiguous() && x16.dim() == 2 && x16.size(1) == K &&
+                  K % 256 == 0, "gguf_prefill: x16 f16 [M, K] contiguous (x_f16_pairs), K % 256");
+  const int M = x16.size(0);
+  TORCH_CHECK(rsc.scalar_type() == at::kFloat && rsc.is_contiguous() && rsc.numel() >= M && rsc.device() == x16.device(),
+              "gguf_prefill: rsc fp32 [M]");
   const bool glu = epi == 2 || epi == 3;
-  TORCH_CHECK(out.size(0) == M && out.stride(0) % 4 == 0 && out.device() == x.device(), "gguf_prefill: out rows");
+  TORCH_CHECK(out.size(0) == M && out.stride(0) % 4 == 0 && out.device() == x16.device(), "gguf_prefill: out rows");
   const int nsb = K / 256;
   hipserve::GgufPart P[4];
   long ncols = 0;
   for (int i = 0; i < np; ++i) {
-    TORCH_CHECK(qs[i].scalar_type() == at::kByte && qs[i].is_contiguous() && qs[i].device() == x.device());
+    TORCH_CHECK(qs[i].scalar_type() == at::kByte && qs[i].is_contiguous() && qs[i].device() == x16.device());
     TORCH_CHECK(rows[i] % 16 == 0 && rows[i] > 0 && cols[i] % 4 == 0, "gguf_prefill: 16-row parts, 4-aligned columns");
     TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 8 &&
                     qs[i].numel() == rows[i] / 16 * nsb * hipserve::gguf_tiled_chunk_bytes(qtypes[i]),
@@ -354,9 +373,9 @@ bool gguf_prefill(at::Tensor& out, const at::Tensor& x, const std::vector<at::Te
   }
   TORCH_CHECK(out.size(1) >= (glu ? rows[0] : ncols), "gguf_prefill: out narrower than the parts");
   if (M == 0) return true;
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  return hipserve::launch_gguf_prefill((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), P, np, M,
-                                       (int)K, cur_stream());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x16.device());
+  return hipserve::launch_gguf_prefill((int)epi, out.data_ptr(), out.stride(0), x16.data_ptr(), rsc.data_ptr<float>(),
+                                       P, np, M, (int)K, cur_stream());
 }
 
 int64_t qmoe_gemm(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const at::Tensor& q, const at::Tensor& rs,
@@ -1221,7 +1240,8 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_dequant(Tensor(a!) out, Tensor q, Tensor d, Tensor m, int qtype, int row_bytes, int N, int K) -> ()");
   // custom all-reduce control ops carry an opaque state handle: catch-all kernels
   m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits, Tensor? x16=None) -> int", &gguf_gemm_parts);
-  m.def("gguf_prefill(Tensor(a!) out, Tensor x, Tensor[] qs, int[] qtypes, int[] rows, int[] cols, int K, int epi) -> bool", &gguf_prefill);
+  m.def("gguf_prefill(Tensor(a!) out, Tensor x16, Tensor rsc, Tensor[] qs, int[] qtypes, int[] rows, int[] cols, int K, int epi) -> bool", &gguf_prefill);
+  m.def("x_f16_pairs(Tensor(a!) x16, Tensor(b!) rsc, Tensor x) -> ()", &x_f16_pairs);
   m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
   m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits) -> int", &qmoe_gemm);
   m.def("car_create(int rank, int world, int max_bytes, int nb_large=512) -> int", &car_create);

@@ -612,6 +612,17 @@ def _qargs(w: QuantWeight):
     return a[0], a[2], a[3], a[4]
 
 
+def x_f16_pairs(x: torch.Tensor, K: int):
+    """(x16, rsc): x[:, :K] as f16 in the GGUF kernels' pair order with each row scaled by
+    1 / rsc[m] (a power of two keeping it inside the f16 range) — the block prefill
+    GEMM's operand, converted once per activation."""
+    M = x.shape[0]
+    x16 = torch.empty(M, K, dtype=torch.float16, device=x.device)
+    rsc = torch.empty(M, dtype=torch.float32, device=x.device)
+    torch.ops.hipserve.x_f16_pairs(x16, rsc, x)
+    return x16, rsc
+
+
 def qprefill(x: torch.Tensor, w: QuantWeight, epi: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
     """x @ w.T from the blocks: epi 0 store (into ``out`` or a new [M, N]), 1 residual add
     (``out`` += ...), 2 / 3 SiLU / GELU GLU of the (gate, up) parts into [M, N/2]."""
@@ -620,7 +631,8 @@ def qprefill(x: torch.Tensor, w: QuantWeight, epi: int = 0, out: torch.Tensor | 
         out = torch.empty(M, w.N // 2 if epi in (2, 3) else w.N, dtype=torch.bfloat16, device=x.device)
     if x.stride(1) != 1 or x.stride(0) % 8:
         x = x.contiguous()
-    if not torch.ops.hipserve.gguf_prefill(out, x, *_qargs(w), w.K, epi):
+    x16, rsc = x_f16_pairs(x, w.K)
+    if not torch.ops.hipserve.gguf_prefill(out, x16, rsc, *_qargs(w), w.K, epi):
         raise RuntimeError(f"gguf_prefill refused parts {[(p.kqt, p.N) for p in w.parts]} K={w.K} epi={epi}")
     return out
 

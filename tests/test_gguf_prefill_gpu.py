@@ -1,12 +1,14 @@
 """GGUF prefill GEMM straight from the tiled blocks (gguf_mfma.hip qpf_kernel) vs a plain
 PyTorch fp32 reference on the numpy block decoder's weights: plain store into part
 columns (mixed formats, as Q4_K_M's q|k|v), residual add, SiLU / GELU GLU of gate / up
-parts, ragged M / N, and the f16-range rescale pass for activations beyond 65504."""
+parts, ragged M / N, and rows beyond the f16 range (x_f16_pairs' power-of-two row
+pre-scale, undone in the epilogue)."""
 import numpy as np
 import pytest
 import torch
 
 from hipserve.ops import load_library
+from hipserve.ops import quant as Q
 from hipserve.ops.quant import QuantWeight
 from hipserve.weights import gguf as G
 
@@ -23,10 +25,21 @@ def _mat(N, K, seed):
     return np.random.default_rng(seed).standard_normal((N, K)).astype(np.float32) * 0.05
 
 
+def _raw(w, qt, seed=0):
+    """ggml blocks of w (Q4_1 has no quantiser here: random valid blocks of its shape)."""
+    if qt == G.Q4_1:
+        return Q.random_blocks(np.random.default_rng(seed), qt, *w.shape)
+    return G.quantize(w, qt)
+
+
 def _ref_w(w, qt):
     """fp32 weights as the numpy block decoder reads the quantised blocks."""
     N, K = w.shape
-    return torch.from_numpy(G.dequantize(G.quantize(w, qt), qt, N * K).reshape(N, K)).cuda()
+    return torch.from_numpy(G.dequantize(_raw(w, qt), qt, N * K).reshape(N, K)).cuda()
+
+
+def _qw(mats, qts):
+    return QuantWeight.from_raw([(qt, m.shape[0], m.shape[1], _raw(m, qt)) for m, qt in zip(mats, qts)], "cuda")
 
 
 def _args(qw):
@@ -43,10 +56,10 @@ def _close(got, want, tol=1e-2):
 @pytest.mark.parametrize("M,N,K", [(130, 272, 512), (1000, 512, 1024), (37, 1024, 256), (300, 4096, 512)])
 def test_store(qt, M, N, K):
     w = _mat(N, K, M + N)
-    qw = QuantWeight.from_float(w, qt, "cuda")
+    qw = _qw([w], [qt])
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 0)
+    assert torch.ops.hipserve.gguf_prefill(out, *Q.x_f16_pairs(x, K), *_args(qw), K, 0)
     _close(out, x.float() @ _ref_w(w, qt).T)
 
 
@@ -60,7 +73,7 @@ def test_mixed_formats_strided():
     xb = torch.randn(M, K + 64, device="cuda", dtype=torch.bfloat16)
     x = xb[:, 16:16 + K]
     out = torch.full((M, 800), float("nan"), device="cuda", dtype=torch.bfloat16)
-    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 0)
+    assert torch.ops.hipserve.gguf_prefill(out, *Q.x_f16_pairs(x, K), *_args(qw), K, 0)
     wd = torch.cat([_ref_w(m, t) for m, t in zip(mats, (G.Q4_K, G.Q4_K, G.Q6_K))])
     _close(out[:, :768], x.float() @ wd.T)
     assert out[:, 768:].isnan().all()  # untouched past the parts
@@ -74,7 +87,7 @@ def test_residual_add(qt):
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     res0 = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
     res = res0.clone()
-    assert torch.ops.hipserve.gguf_prefill(res, x, *_args(qw), K, 1)
+    assert torch.ops.hipserve.gguf_prefill(res, *Q.x_f16_pairs(x, K), *_args(qw), K, 1)
     h = (x.float() @ _ref_w(w, qt).T).to(torch.bfloat16).float()
     _close(res, h + res0.float(), tol=2e-2)
 
@@ -85,10 +98,10 @@ def test_residual_add(qt):
 def test_glu(qt, act, M, I):
     K = 512
     g, u = _mat(I, K, 3), _mat(I, K, 4)
-    qw = QuantWeight.from_float([g, u], qt, "cuda")
+    qw = _qw([g, u], [qt, qt])
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     out = torch.full((M, I), float("nan"), device="cuda", dtype=torch.bfloat16)
-    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 2 if act == "silu" else 3)
+    assert torch.ops.hipserve.gguf_prefill(out, *Q.x_f16_pairs(x, K), *_args(qw), K, 2 if act == "silu" else 3)
     gv = (x.float() @ _ref_w(g, qt).T).to(torch.bfloat16).float()
     uv = (x.float() @ _ref_w(u, qt).T).to(torch.bfloat16).float()
     f = torch.nn.functional.silu if act == "silu" else (lambda t: torch.nn.functional.gelu(t, approximate="tanh"))
@@ -97,8 +110,8 @@ def test_glu(qt, act, M, I):
 
 @pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K])
 def test_f16_range_rescale(qt):
-    """Rows with activations beyond the f16 range take the per-row power-of-two rescale
-    pass and stay exact; the other rows are unaffected."""
+    """Rows with activations beyond the f16 range are pre-scaled by a power of two
+    (x_f16_pairs) and stay exact; the other rows are unaffected."""
     M, N, K = 200, 256, 512
     w = _mat(N, K, 5)
     qw = QuantWeight.from_float(w, qt, "cuda")
@@ -106,7 +119,7 @@ def test_f16_range_rescale(qt):
     x[3, 7] = 3.0e5
     x[150, :] *= 1.0e6
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    assert torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 0)
+    assert torch.ops.hipserve.gguf_prefill(out, *Q.x_f16_pairs(x, K), *_args(qw), K, 0)
     want = x.float() @ _ref_w(w, qt).T
     assert out.isfinite().all()
     for r in (3, 150, 0, 199):
@@ -119,4 +132,18 @@ def test_rejects():
     qw.parts[1] = QuantWeight.from_float(_mat(64, K, 2), G.Q6_K, "cuda").parts[0]
     x = torch.randn(10, K, device="cuda", dtype=torch.bfloat16)
     out = torch.empty(10, 64, device="cuda", dtype=torch.bfloat16)
-    assert not torch.ops.hipserve.gguf_prefill(out, x, *_args(qw), K, 2)  # GLU over two formats
+    assert not torch.ops.hipserve.gguf_prefill(out, *Q.x_f16_pairs(x, K), *_args(qw), K, 2)  # GLU over two formats
+
+
+def test_x_f16_pairs():
+    """The operand conversion: pair order {0, 2, 1, 3, 4, 6, 5, 7} per 8-run, rows past
+    the f16 range scaled by 2^-k with max |x| 2^-k < 2^15, rsc = 2^k."""
+    M, K = 5, 512
+    x = torch.randn(M, K + 8, device="cuda", dtype=torch.bfloat16)[:, :K]
+    x[2] *= 1.0e6
+    x16, rsc = Q.x_f16_pairs(x, K)
+    perm = torch.tensor([0, 2, 1, 3, 4, 6, 5, 7], device="cuda")
+    back = x16.float().view(M, K // 8, 8)[:, :, perm.argsort()].reshape(M, K) * rsc[:, None]
+    assert torch.allclose(back, x.float(), rtol=1e-3, atol=1e-4 * x.float().abs().amax(1, keepdim=True).max().item())
+    assert rsc[0].item() == 1.0 and rsc[2].item() > 1.0 and x16.isfinite().all()
+    assert (x16[2].float().abs().max() < 32768).item()

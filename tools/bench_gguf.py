@@ -104,9 +104,11 @@ def main():
                 cols = np.cumsum([0] + [p.N for p in qw.parts])[:-1].tolist()
                 qargs = ([p.q for p in qw.parts], [p.kqt for p in qw.parts], [p.N for p in qw.parts], cols)
                 act = torch.empty(M, qw.N // 2, device="cuda", dtype=torch.bfloat16)
-                kerns = [("qpf_prefill", lambda: torch.ops.hipserve.gguf_prefill(out, x, *qargs, qw.K, 0))]
+                x16, rsc = Q.x_f16_pairs(x, qw.K)
+                kerns = [("qpf_prefill", lambda: torch.ops.hipserve.gguf_prefill(out, x16, rsc, *qargs, qw.K, 0)),
+                         ("qpf_prefill+x_conv", lambda: Q.qprefill(x, qw, 0, out))]
                 if name == "gate_up":
-                    kerns.append(("qpf_prefill_glu", lambda: torch.ops.hipserve.gguf_prefill(act, x, *qargs, qw.K, 2)))
+                    kerns.append(("qpf_prefill_glu", lambda: torch.ops.hipserve.gguf_prefill(act, x16, rsc, *qargs, qw.K, 2)))
                 if not a.no_mtiled:
                     kerns.append(("m_tiled_mfma", lambda: Q._launch_v2(out, Q._empty(x.device, torch.float32), x, qw, 1)))
                 kerns += [("dequant+hipblaslt", deq_blas),
