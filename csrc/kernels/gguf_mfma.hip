@@ -1085,11 +1085,12 @@ void qpf_launch_rt(int epi, const QfArgs& A, hipStream_t s) {
   }
 }
 
-// HIPSERVE_QPF_RT: row groups per wave (2: 8 waves, 4: 4 waves); default 4
+// HIPSERVE_QPF_RT: row groups per wave (2: 8 waves, default — measured 10-37 % faster than
+// 4: 4 waves at 8,192 tokens on the Llama-3-8B Q4_K_M shapes, profiles/r4_qpf_bench.log)
 int qpf_rt() {
   static const int v = [] {
     const char* e = getenv("HIPSERVE_QPF_RT");
-    return e != nullptr && atoi(e) == 2 ? 2 : 4;
+    return e != nullptr && atoi(e) == 4 ? 4 : 2;
   }();
   return v;
 }

@@ -158,10 +158,19 @@ class ModelRunner:
                 from ..ops import quant as Q
 
                 self.gguf_split_report = Q.tune_splits(qws, self.device, [m for m in Q.M_BUCKETS if m <= 64])
+                # GGUF prefill: the block kernel or dequant + hipBLASLt per shape, timed at the
+                # token budget (the LM head only sees a few rows per prefill: not timed)
+                lm = getattr(self.model, "lm_head", None)
+                self.qprefill_report = Q.tune_qprefill([w for w in qws if w is not lm], self.device,
+                                                       min(ecfg.max_num_batched_tokens, 8192)) \
+                    if Q.QPREFILL_MODE == "auto" else []
                 if ecfg.extra.get("quant_dense_shadow", True):
                     total = torch.cuda.get_device_properties(self.device).total_memory
+                    # GGUF blocks get a resident bf16 shadow only on request (HBM holds the
+                    # quantised blocks only); INT8 weights keep theirs for hipBLASLt prefill
+                    gguf = ecfg.extra.get("gguf_dense_shadow", os.environ.get("HIPSERVE_QUANT_SHADOW", "0") == "1")
                     self.quant_shadow_bytes = getattr(self, "quant_shadow_bytes", 0) + Q.make_dense_shadows(
-                        qws, self.device, (24 << 30) + total // 4)
+                        qws, self.device, (24 << 30) + total // 4, gguf=gguf)
                     # FP8: plain e4m3 copies for the hipBLASLt FP8 prefill GEMMs
                     self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()

@@ -587,23 +587,60 @@ def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = No
 # Prefill (M > MAX_FUSED_M) straight from the tiled GGUF blocks (gguf_mfma.hip qpf_kernel:
 # each weight dequantised once per 64-128-token tile, f16 MFMA, store / residual-add / GLU
 # epilogues): no resident bf16 shadow and no per-call dequantise-into-scratch pass.
-# HIPSERVE_QPREFILL=0 restores the scratch + hipBLASLt path.
-QPREFILL = os.environ.get("HIPSERVE_QPREFILL", "1") != "0"
+# HIPSERVE_QPREFILL: "1" always, "0" never (dequantise into scratch + hipBLASLt), "auto"
+# (default): per weight shape, whichever tune_qprefill timed faster at engine start
+# (untimed shapes take the block kernel).
+QPREFILL_MODE = os.environ.get("HIPSERVE_QPREFILL", "auto")
+QPREFILL = QPREFILL_MODE != "0"
+QPF_CHOICE: dict = {}  # weight signature -> the block kernel was faster at start-up
 GGUF_KQT = (0, 1, 2, 3, 4, 5)  # kernel qtypes Q4_0 .. Q6_K
 
 
-def qprefill_ok(w, M: int, glu: bool = False) -> bool:
+def qprefill_ok(w, M: int, glu: bool = False, timed: bool = True) -> bool:
     """The block prefill GEMM takes ``w`` at ``M`` rows: a prefill-sized batch, a GGUF
     QuantWeight without a bf16 shadow whose parts are all tiled with block scales in the
-    subnormal-dequant range; ``glu``: exactly two parts (gate, up) of one format."""
+    subnormal-dequant range; ``glu``: exactly two parts (gate, up) of one format;
+    ``timed``: and the start-up timing (``auto``) did not prefer dequant + hipBLASLt."""
     if not (QPREFILL and isinstance(w, QuantWeight) and M > MAX_FUSED_M and w.dense is None):
         return False
     if not (w.v2 and all(p.kqt in GGUF_KQT for p in w.parts) and hasattr(torch.ops.hipserve, "gguf_prefill")):
         return False
     if glu:
         ps = w.parts
-        return len(ps) == 2 and ps[0].kqt == ps[1].kqt and ps[0].N == ps[1].N
-    return True
+        if not (len(ps) == 2 and ps[0].kqt == ps[1].kqt and ps[0].N == ps[1].N):
+            return False
+    return not (timed and QPREFILL_MODE == "auto" and not QPF_CHOICE.get(_sig(w), True))
+
+
+def tune_qprefill(weights, device, M: int) -> list:
+    """Start-up timing, per distinct GGUF weight shape, of the block prefill GEMM (x
+    conversion + qpf_kernel, GLU epilogue for (gate, up) pairs) against dequantise into
+    scratch + hipBLASLt (+ silu_and_mul) at M rows; fills QPF_CHOICE for ``auto``."""
+    from . import pgemm
+    seen, rows = {}, []
+    for w in weights:
+        if qprefill_ok(w, M, timed=False):
+            seen.setdefault(_sig(w), w)
+    for sig, w in seen.items():
+        x = torch.randn(M, w.K, device=device, dtype=torch.bfloat16)
+        glu = qprefill_ok(w, M, glu=True, timed=False)
+        act = torch.empty(M, w.N // 2, device=device, dtype=torch.bfloat16)
+
+        def blas():
+            y = quant_linear_dequant(x, w)
+            if glu:
+                torch.ops.hipserve.silu_and_mul(act, y)
+
+        def block():
+            qprefill(x, w, 2 if glu else 0)
+        t_b = pgemm._time(lambda i: blas())
+        t_q = pgemm._time(lambda i: block())
+        QPF_CHOICE[sig] = t_q <= t_b
+        rows.append({"K": w.K, "N": w.N, "M": M, "glu": glu, "block_ms": round(t_q, 4),
+                     "dequant_blas_ms": round(t_b, 4), "block": t_q <= t_b})
+        del x, act
+    torch.cuda.empty_cache()
+    return rows
 
 
 def _qargs(w: QuantWeight):
@@ -681,7 +718,11 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
     if w.v2 and x.is_cuda and M <= QPREFILL_MAX_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
         _launch_v2(out, _empty(x.device, torch.float32), x, w, 1)  # K15: M-tiled dequant-MFMA GEMM
         return out
-    # prefill: every part dequantised into one contiguous [N, K] scratch, one GEMM
+    return quant_linear_dequant(x, w)
+
+
+def quant_linear_dequant(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
+    """Prefill: every part dequantised into one contiguous [N, K] bf16 scratch, one GEMM."""
     buf = _dequant_scratch(x.device, w.N * w.K)[: w.N * w.K].view(w.N, w.K)
     off = 0
     for p in w.parts:
@@ -726,26 +767,25 @@ def make_fp8_plain(weights, device, reserve_bytes: int) -> int:
     return added
 
 
-def make_dense_shadows(weights, device, reserve_bytes: int) -> int:
+def make_dense_shadows(weights, device, reserve_bytes: int, gguf: bool = True) -> int:
     """Keep a dequantised bf16 copy of quantised projections for the prefill GEMMs
     while ``reserve_bytes`` of HBM stay free (288 GB per MI355X: an 8B GGUF model's
     16 GB of bf16 shadows next to its 4.5 GB of blocks). Decode keeps streaming the
     quantised blocks (the v2 dequant-MFMA kernel: 3.6x fewer bytes); prefill skips the
     per-call dequant pass (~18 GB of HBM traffic per 8K-token Llama-3-8B chunk) and
     runs hipBLASLt on the copy. Largest weights first (lm_head, gate|up, ...). GGUF
-    weights the block prefill GEMM takes (``qprefill_ok``) get none: their prefill reads
-    the blocks. Returns the bytes added. HIPSERVE_QUANT_SHADOW=0 disables it."""
-    import os
-
-    if os.environ.get("HIPSERVE_QUANT_SHADOW", "1") == "0" or torch.device(device).type != "cuda":
+    weights only with ``gguf`` (the engine passes HIPSERVE_QUANT_SHADOW=1 /
+    extra gguf_dense_shadow; default off: a GGUF model's footprint is its blocks, prefill
+    reads them through qpf_kernel or a per-call scratch). Returns the bytes added."""
+    if torch.device(device).type != "cuda":
         return 0
     from . import pgemm
     added = 0
     for w in sorted(weights, key=lambda w: -w.N * w.K):
         if w.dense is not None or pgemm.f8_fits(w) or pgemm.f8_fits(w, glu=True):
             continue  # FP8 prefill runs on the e4m3 MFMA from the quantised weights
-        if qprefill_ok(w, MAX_FUSED_M + 1):
-            continue  # GGUF: prefill runs from the blocks (qpf_kernel), HBM holds blocks only
+        if not gguf and all(p.kqt in GGUF_KQT for p in w.parts):
+            continue  # GGUF: prefill from the blocks or a per-call scratch, no resident copy
         need = w.N * w.K * 2
         free, _ = torch.cuda.mem_get_info(device)
         if free - need < reserve_bytes:

@@ -8,7 +8,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 pass() {  # pass <name> <counters...>
   local n=$1; shift
-  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$n -o run -- python3 $HERE/tools/pg_pmc.py \
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$n -o run -- python3 $HERE/${PMC_PY:-tools/pg_pmc.py} \
     ${PG_SHAPE:-8192 28672 4096} > $OUT/$n.log 2>&1 || { tail -5 $OUT/$n.log; return 1; }
   find $OUT/$n -name '*counter_collection.csv' -exec cp {} $OUT/$n.csv \;
   rm -rf $OUT/$n
