@@ -918,8 +918,9 @@ HS_DEVICE void qpf_body(_Float16* xs_, const QfArgs& A, int pi, int tm, int tn) 
     base[r] = q + (long)min(gi[r], ngroups - 1) * nsb * CB;
   }
   constexpr int XP = XR * 32 / NT;  // 16-byte x fragments per thread and super-chunk
-  // thread -> x row 8 i + (tid >> 5) (i < XP), fragment tid & 31: one VGPR offset, the row
-  // step a scalar; rows >= M lie outside the buffer range and read as zero
+  // thread -> x row RS i + (tid >> 5) (i < XP), fragment tid & 31; the row offset rides
+  // in the VGPR offset (the range check covers it, not the scalar one): rows >= M read
+  // as zero
   static_assert(NT % 32 == 0 && XP * NT == XR * 32, "x staging must divide evenly");
   constexpr int RS = NT / 32;  // rows per staging pass
   const int mrow0 = tm * XR;
@@ -932,7 +933,7 @@ HS_DEVICE void qpf_body(_Float16* xs_, const QfArgs& A, int pi, int tm, int tn) 
   u32x4 xv[XP];
   auto load_x = [&](int sb) {
 #pragma unroll
-    for (int i = 0; i < XP; ++i) xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, xo, i * xstep + sb * 512, 0);
+    for (int i = 0; i < XP; ++i) xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, xo + i * xstep, sb * 512, 0);
   };
   auto store_x = [&](int buf) {
 #pragma unroll
@@ -1074,6 +1075,238 @@ void qpf_kernel(QfArgs A) {
   qpf_body<QT, EPI, RT>(xs, A, pi, tm, tn);
 }
 
+// ---- big-tile variant (qpg): 4 waves x 4 row groups = 256 weight rows x 256 tokens
+// (128 for Q5_K / Q6_K), one wave per SIMD, the 256 (128) accumulators in AGPRs. The
+// 8-wave qpf above is bound by its dequant VALU per MFMA (a weight fragment feeds only
+// 8 MFMAs: 2.6 VALU per MFMA, MFMA pipe 45 % busy, profiles/r4_qpf_pmc_v1.log); here a
+// fragment feeds 16, and x never passes through registers:
+//   * x16 is staged by LDS-DMA (buffer_load ... lds, 1 KiB per wave instruction) in
+//     half super-chunks (steps 0-3 / 4-7) into two LDS buffers; wave w loads plane
+//     g = w, lane i of instruction j row 16 j + i / 4 and 16-byte slot i & 3, holding
+//     fragment (i & 3) ^ ((i >> 4) & 3): the XOR swizzle makes every 16-lane group of
+//     a B-fragment ds_read_b128 (rows 16 t .. 16 t + 15) hit 16 distinct bank quads;
+//   * the next super-chunk's weight blocks load into the second register set while
+//     this one is dequantised; each half buffer is refilled right after the barrier
+//     that retires it, so a DMA has half a super-chunk (~4K MFMA cycles) to land;
+//   * at 256 accumulators the MFMAs are inline asm on "+a" registers (no compiler AGPR
+//     shuffles); the first one reading a freshly dequantised A operand carries the 2
+//     wait states a VALU-written operand needs (s_nop 1).
+template <int QT>
+constexpr int qg_mt() { return QT == Q5_K || QT == Q6_K || QT == Q8_0 ? 8 : 16; }
+
+// kAsm (256 accumulators, MT 16): the builtin had hipcc move accumulators between AGPRs
+// and spill (tools/asm_stats.py); kNop: the first use of a freshly dequantised A operand
+// (2 wait states after its VALU write; later uses of it are far from the write)
+template <bool kAsm, bool kNop>
+HS_DEVICE void qg_mfma(f32x4& acc, const f16x8& a, const f16x8& b) {
+  if constexpr (!kAsm)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc, 0, 0, 0);
+  else if constexpr (kNop)
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <int QT, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void qpg_kernel(QfArgs A) {
+  constexpr int RT = 4, NW = 4, MT = qg_mt<QT>(), XR = 16 * MT;
+  constexpr int PLANE = XR * 64;  // bytes of one lane-group plane of a half buffer
+  constexpr int NDMA = XR / 16;   // 1 KiB DMA instructions per wave and half
+  constexpr int CB = chunk_bytes<QT>();
+  constexpr bool kGlu = EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU;
+  __shared__ __attribute__((aligned(1024))) unsigned char xs0[4 * PLANE];
+  __shared__ __attribute__((aligned(1024))) unsigned char xs1[4 * PLANE];
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int grp = L / (GM * A.tiles_n), first = grp * GM;
+  const int gsz = min(GM, A.tiles_m - first);
+  const int rrr = L - first * A.tiles_n;
+  const int tm = first + rrr % gsz, tn = rrr / gsz;
+  int pi = 0;
+  if constexpr (!kGlu) {
+#pragma unroll
+    for (int i = 1; i < kMaxParts; ++i)
+      if (i < A.parts.n && tn >= A.parts.p[i].tile0) pi = i;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int K = A.K, M = A.M, nsb = K >> 8;
+  const Part& P = A.parts.p[pi];
+  const int ngroups = P.rows >> 4;
+  int gi[RT];
+  const unsigned char* base[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    gi[r] = kGlu ? (tn * NW + wave) * (RT / 2) + r % (RT / 2) : (tn - P.tile0) * (QF_ROWS / 16) + wave * RT + r;
+    const unsigned char* q = kGlu && r >= RT / 2 ? A.parts.p[1].q : P.q;
+    base[r] = q + (long)min(gi[r], ngroups - 1) * nsb * CB;
+  }
+  // x16 rows of this tile; rows >= M lie outside the buffer range and read as zero
+  const int mrow0 = tm * XR;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A.x16 + (long)mrow0 * A.ldx), 0, (int)((long)min(XR, M - mrow0) * A.ldx * 2), 0x00020000);
+  const int sl = (lane & 3) ^ ((lane >> 4) & 3);  // fragment held by this lane's slot
+  const int dvo0 = (((lane >> 2) * (int)A.ldx) + kbase<QT>(wave, sl)) * 2;
+  const int dvo1 = (((lane >> 2) * (int)A.ldx) + kbase<QT>(wave, 4 + sl)) * 2;
+  const int dstep = 16 * (int)A.ldx * 2;
+  auto dma = [&](int sb, int h) {  // half h of super-chunk sb -> buffer h
+    unsigned char* dst = (h ? xs1 : xs0) + wave * PLANE;
+    const int vo = h ? dvo1 : dvo0;
+#pragma unroll
+    for (int j = 0; j < NDMA; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                               vo + j * dstep, sb * 512, 0, 0);  // rows in the range-checked offset
+  };
+  // B fragment (step s, token tile t): row 16 t + c, slot (s & 3) ^ ((c >> 2) & 3)
+  const int rb = g * PLANE + c * 64;
+  auto bfrag = [&](int s, int t) -> f16x8 {
+    const unsigned char* src = (s < 4 ? xs0 : xs1) + rb + t * 1024 + (((s & 3) ^ ((c >> 2) & 3)) << 4);
+    return *reinterpret_cast<const f16x8*>(src);
+  };
+
+  f32x4 acc[RT][MT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Raw rawA[RT], rawB[RT];
+  dma(0, 0);
+  dma(0, 1);
+#pragma unroll
+  for (int r = 0; r < RT; ++r) load_raw<QT>(base[r], g, c, lane, rawA[r]);
+  __syncthreads();
+  auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
+    const int sn = min(sb + 1, nsb - 1);  // the last super-chunk re-reads itself: no branch
+#pragma unroll
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
+    Dec<QT> dec[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
+    // the A fragments of step s + 1 are dequantised between step s's MFMA groups (one
+    // fragment per group of 4 x RT MFMAs): the MFMA pipe never waits for a dequant burst
+    f16x8 a[RT], bq[4];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s == 4) {  // buffer 0 retired by every wave: refill it with the next half A
+        __syncthreads();
+        dma(sn, 0);
+      }
+      f16x8 an[RT];
+      constexpr int NQ = MT / 4, PER = (RT + NQ - 1) / NQ;  // next-step fragments per group
+      // x fragments one group ahead (from LDS, inside a half: the other half's buffer is
+      // only complete after the barrier that opens it)
+      if (s == 0 || s == 4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bq[t] = bfrag(s, t);
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        f16x8 b[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[t] = bq[t];
+        const bool more = q + 1 < NQ || (s & 3) != 3;
+        if (more) {
+          const int sq = q + 1 < NQ ? s : s + 1, tq = q + 1 < NQ ? 4 * (q + 1) : 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) bq[t] = bfrag(sq, tq + t);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < RT; ++r) {
+            if (q == 0 && t == 0)
+              qg_mfma<MT == 16, true>(acc[r][4 * q + t], a[r], b[t]);
+            else
+              qg_mfma<MT == 16, false>(acc[r][4 * q + t], a[r], b[t]);
+          }
+        if (s < 7) {
+#pragma unroll
+          for (int r = q * PER; r < min(RT, (q + 1) * PER); ++r) an[r] = dec[r].step(cur[r], g, s + 1);
+        }
+      }
+      if (s < 7) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) a[r] = an[r];
+      }
+    }
+    __syncthreads();  // buffer 1 retired
+    dma(sn, 1);
+  };
+  int sb = 0;
+  for (; sb + 1 < nsb; sb += 2) {
+    iter(sb, rawA, rawB);
+    iter(sb + 1, rawB, rawA);
+  }
+  if (sb < nsb) iter(sb, rawA, rawB);
+  if constexpr (MT == 16)  // asm MFMAs: the hazard recognizer does not see them
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA -> accumulator reads
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {  // undo the row pre-scale (exact: a power of two)
+    const float sc = A.rsc[min(mrow0 + 16 * t + c, M - 1)];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][t] *= sc;
+  }
+  if constexpr (kGlu) {
+#pragma unroll
+    for (int r = 0; r < RT / 2; ++r) {
+      if (gi[r] >= ngroups) continue;
+      const int col = 16 * gi[r] + 4 * g;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = mrow0 + 16 * t + c;
+        if (m >= M) continue;
+        unsigned short o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned short gv = f32_to_bf16(acc[r][t][j]), uv = f32_to_bf16(acc[r + RT / 2][t][j]);
+          o[j] = EPI == PW_EPI_GEGLU ? gelu_mul1(gv, uv) : silu_mul1(gv, uv);
+        }
+        *reinterpret_cast<uint2*>(A.out + (long)m * A.ldo + col) =
+            uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      if (gi[r] >= ngroups) continue;
+      const int col = P.col + 16 * gi[r] + 4 * g;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = mrow0 + 16 * t + c;
+        if (m >= M) continue;
+        uint2* dst = reinterpret_cast<uint2*>(A.out + (long)m * A.ldo + col);
+        float o[4];
+        if constexpr (EPI == PW_EPI_ADD) {
+          const uint2 rv = *dst;
+          const unsigned short rr[4] = {(unsigned short)(rv.x & 0xffff), (unsigned short)(rv.x >> 16),
+                                        (unsigned short)(rv.y & 0xffff), (unsigned short)(rv.y >> 16)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[r][t][j])) + bf16_to_f32(rr[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = acc[r][t][j];
+        }
+        *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+      }
+    }
+  }
+}
+
+template <int QT>
+void qpg_launch(int epi, QfArgs A, hipStream_t s) {
+  A.tiles_m = (A.M + 16 * qg_mt<QT>() - 1) / (16 * qg_mt<QT>());
+  const dim3 grid(A.tiles_n * A.tiles_m), block(256);
+  switch (epi) {
+    case PW_EPI_STORE: qpg_kernel<QT, PW_EPI_STORE><<<grid, block, 0, s>>>(A); break;
+    case PW_EPI_ADD: qpg_kernel<QT, PW_EPI_ADD><<<grid, block, 0, s>>>(A); break;
+    case PW_EPI_GLU: qpg_kernel<QT, PW_EPI_GLU><<<grid, block, 0, s>>>(A); break;
+    case PW_EPI_GEGLU: qpg_kernel<QT, PW_EPI_GEGLU><<<grid, block, 0, s>>>(A); break;
+  }
+}
+
 template <int QT, int RT>
 void qpf_launch_rt(int epi, const QfArgs& A, hipStream_t s) {
   const dim3 grid(A.tiles_n * A.tiles_m), block(64 * qf_waves(RT));
@@ -1085,18 +1318,24 @@ void qpf_launch_rt(int epi, const QfArgs& A, hipStream_t s) {
   }
 }
 
-// HIPSERVE_QPF_RT: row groups per wave (2: 8 waves, default — measured 10-37 % faster than
-// 4: 4 waves at 8,192 tokens on the Llama-3-8B Q4_K_M shapes, profiles/r4_qpf_bench.log)
+// HIPSERVE_QPF_RT: kernel shape — 2: 8 waves x 2 row groups, 4: 4 waves x 4 row groups
+// (measured 10-37 % slower than 2, profiles/r4_qpf_bench_rt4.log), 16 (default): the
+// big-tile qpg_kernel
 int qpf_rt() {
   static const int v = [] {
     const char* e = getenv("HIPSERVE_QPF_RT");
-    return e != nullptr && atoi(e) == 4 ? 4 : 2;
+    const int r = e != nullptr ? atoi(e) : 16;
+    return r == 2 || r == 4 ? r : 16;
   }();
   return v;
 }
 
 template <int QT>
 void qpf_launch(int epi, QfArgs A, hipStream_t s) {
+  if (qpf_rt() == 16) {
+    qpg_launch<QT>(epi, A, s);
+    return;
+  }
   const int rt = QT == Q8_0 ? 2 : qpf_rt();  // Q8_0 spills at RT 4
   const int bm = 16 * (rt == 2 ? qf_mt<QT, 2>() : qf_mt<QT, 4>());
   A.tiles_m = (A.M + bm - 1) / bm;
