@@ -122,6 +122,7 @@ for s in $steps; do
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     prof70) prof_run prof70 --model llama-3-70b ;;
+    prof32k) prof_run prof32k --model llama-3.1-8b --input-len 32768 --output-len 64 --concurrency 4 --max-num-batched-tokens 8192 ;;
     long8k) bench_named long8k X=1 -- --model llama-3.1-8b --input-len 8192 --output-len 256 --concurrency 16 --max-num-batched-tokens 8192 --steps 2 ;;
     long32k) bench_named long32k X=1 -- --model llama-3.1-8b --input-len 32768 --output-len 256 --concurrency 4 --max-num-batched-tokens 8192 --steps 2 ;;
     bench_mixtral_packed) bench_named mixtral_packed HIPSERVE_MOE_PACKED_PREFILL=1 -- --model mixtral-8x7b --concurrency 32 ;;
