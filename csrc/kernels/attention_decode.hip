@@ -393,27 +393,67 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   }
 }
 
-// Merge partitions: one workgroup per (head, sequence), one lane per d.
+// Merge partitions: one workgroup per (head, sequence) of G lane groups (reduce_groups), one
+// lane per d. The partitions are split over the groups (p = grp, grp + G, ...) and each
+// lane keeps 4 independent partial sums, so a long context's 100+ partitions are 4 x G
+// loads in flight per lane instead of one serial L2 round trip per partition (32K-token
+// contexts, 128 partitions: 22 us per layer serially, profiles/r4_prof32k_summary.md).
+// lane groups: G * D <= 512 lanes in whole waves (D = 96: 4 groups, 384 lanes)
 template <int D>
-__global__ __launch_bounds__(D) void paged_decode_reduce_kernel(
+constexpr int reduce_groups() { return D == 96 ? 4 : 512 / D; }
+
+template <int D>
+__global__ __launch_bounds__(512) void paged_decode_reduce_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
     const int* __restrict__ context_lens, int nq, int part_size, int max_parts, int window) {
-  const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  constexpr int G = reduce_groups<D>();
+  static_assert(G * D % 64 == 0, "whole waves");
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int d = tid % D, grp = tid / D;
   const int ctx = context_lens[b];
   const int lo_al = (window > 0 ? max(0, ctx - window) : 0) & ~(kChunk - 1);
   const int np = (ctx - lo_al + part_size - 1) / part_size;
   if (np <= 1) return;
   const long base = ((long)b * nq + h) * max_parts;
+  __shared__ float red[G * D + G + 16];
+  // M = max over the partitions' running maxima (block reduction)
   float M = -1e30f;
-  for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
-  float L = 0.f, acc = 0.f;
-  for (int p = 0; p < np; ++p) {
-    const float w = exp2f(tmp_ml[(base + p) * 2] - M) * tmp_ml[(base + p) * 2 + 1];
-    L += w;
-    acc += w * tmp_out[(base + p) * D + d];
+  for (int p = tid; p < np; p += G * D) M = fmaxf(M, tmp_ml[(base + p) * 2]);
+  for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+  if ((tid & 63) == 0) red[G * D + G + (tid >> 6)] = M;
+  __syncthreads();
+  M = -1e30f;
+#pragma unroll
+  for (int w = 0; w < G * D / 64; ++w) M = fmaxf(M, red[G * D + G + w]);
+  float L[4] = {0.f, 0.f, 0.f, 0.f}, acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int p = grp;
+  for (; p + 3 * G < np; p += 4 * G) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long q = base + p + u * G;
+      const float w = exp2f(tmp_ml[q * 2] - M) * tmp_ml[q * 2 + 1];
+      L[u] += w;
+      acc[u] += w * tmp_out[q * D + d];
+    }
   }
-  out[(long)b * out_stride + (long)h * D + d] = f32_to_bf16(acc / L);
+  for (; p < np; p += G) {
+    const float w = exp2f(tmp_ml[(base + p) * 2] - M) * tmp_ml[(base + p) * 2 + 1];
+    L[0] += w;
+    acc[0] += w * tmp_out[(base + p) * D + d];
+  }
+  red[grp * D + d] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  if (d == 0) red[G * D + grp] = (L[0] + L[1]) + (L[2] + L[3]);
+  __syncthreads();
+  if (grp == 0) {
+    float a = 0.f, l = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a += red[g * D + d];
+      l += red[G * D + g];
+    }
+    out[(long)b * out_stride + (long)h * D + d] = f32_to_bf16(a / l);
+  }
 }
 
 static size_t smem_bytes(int D, int waves) {
@@ -478,7 +518,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
     if (waves == 8) HS_DECODE(DD, 8);                                                                       \
     else HS_DECODE(DD, 4);                                                                                  \
     if (max_parts > 1)                                                                                      \
-      paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,        \
+      paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(reduce_groups<DD>() * DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml, \
                                                                        context_lens, nq, part_size, max_parts, \
                                                                        window);                             \
   } while (0)
@@ -519,7 +559,7 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
     if (waves == 8) HS_DECODE_QKV(DD, 8);                                                                     \
     else HS_DECODE_QKV(DD, 4);                                                                                \
     if (max_parts > 1)                                                                                        \
-      paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,          \
+      paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(reduce_groups<DD>() * DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,   \
                                                                        context_lens, nq, part_size, max_parts,   \
                                                                        window);                               \
   } while (0)

@@ -108,6 +108,7 @@ for s in $steps; do
     pgtest) run_one tests/test_prefill_gemm_gpu.py ;;
     pwtest) run_one tests/test_prefill_gemm_packed_gpu.py ;;
     longtest) run_one tests/test_long_context_gpu.py ;;
+    kerneltest) run_one tests/test_kernels_gpu.py ;;
     qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
     qpfpmc) PMC_PY=tools/qpf_pmc.py PG_SHAPE=8192 bash scripts/pg_pmc.sh > $OUT/qpf_pmc.log 2>&1; rc=$?; tail -n 12 $OUT/qpf_pmc.log; [ $rc -eq 0 ] ;;
     qpfbench) timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 2048 8192 > $OUT/bench_qpf.log 2>&1; rc=$?; tail -n 40 $OUT/bench_qpf.log; [ $rc -eq 0 ] ;;
