@@ -748,7 +748,7 @@ __global__ __launch_bounds__(64 * NWAVES) void qgemm2_kernel(unsigned short* __r
 
 // 33 <= M <= 64 body shape (HIPSERVE_QGEMM_M64, for A/B measurement): 0 = 8 waves x 1
 // row group (default: measured 3-8 % faster at M = 64), 1 = 4 waves x 2 (both 128
-// weight rows per workgroup)
+// weight rows per workgroup), 2 = 8 waves x 2 (256 rows: half the x staging per weight byte)
 int m64_variant() {
   static const int v = [] {
     const char* e = getenv("HIPSERVE_QGEMM_M64");
@@ -756,6 +756,11 @@ int m64_variant() {
   }();
   return v;
 }
+
+// the 256-row body for 33-64 rows: HIPSERVE_QGEMM_M64=2, and by default for LM-head
+// widths (N >= 32K: 152 -> 136 us on the Q6_K 128K-vocab head, profiles/r4_gguf_m64_bodies.log;
+// 8 waves x 1 row group stays faster on the layer projections)
+bool m64_wide(int M, int Ntot) { return M > 32 && M <= 64 && (m64_variant() == 2 || (m64_variant() == 0 && Ntot >= 32768)); }
 
 template <int QA, int QB>
 void launch_t(void* out, long out_stride, float* ws, const void* x, long x_stride, const Parts& P, int tiles,
@@ -772,6 +777,12 @@ void launch_t(void* out, long out_stride, float* ws, const void* x, long x_strid
     qgemm2_kernel<QA, QB, 1, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per, nullptr);
   else if (M <= 32)
     qgemm2_kernel<QA, QB, 2, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per, nullptr);
+  else if (m64_wide(M, Ntot) && xh != nullptr)  // 8 waves x 2 row groups: 256 rows share one x staging
+    qgemm2_kernel<QA, QB, 4, 2, 8, true><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per,
+                                                                    xh);
+  else if (m64_wide(M, Ntot))
+    qgemm2_kernel<QA, QB, 4, 2, 8><<<grid, dim3(512), 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per,
+                                                              nullptr);
   else if (m64_variant() == 1)  // 4 waves x 2 row groups
     qgemm2_kernel<QA, QB, 4, RT, NW><<<grid, block, 0, s>>>(o, out_stride, ws, xi, x_stride, P, M, Ntot, K, per, nullptr);
   else if (xh != nullptr && M <= 64)  // 8 waves x 1 row group, x staged from the producer's f16 copy
@@ -1410,7 +1421,8 @@ int gguf_tiled_chunk_bytes(int qtype) {
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16) {
-  constexpr int ROWS = 16 * 2 * kWaves;
+  // weight rows per workgroup: 128, or 256 for the wide M = 33-64 body (m64_wide)
+  const int ROWS = m64_wide(M, Ntot) ? 256 : 16 * 2 * kWaves;
   int fmts[kMaxParts], nf = 0;
   for (int i = 0; i < nparts; ++i) {
     bool seen = false;
@@ -1484,8 +1496,8 @@ bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x16, const fl
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (M < 1 || K < 256 || K % 256 || nparts < 1 || nparts > kMaxParts || (glu && nparts != 2)) return false;
   if (epi != PW_EPI_STORE && epi != PW_EPI_ADD && !glu) return false;
-  // 32-bit x offsets inside one 128-row tile
-  if ((long)16 * QF_MT * ldx * 2 >= (1L << 31)) return false;
+  // 32-bit buffer offsets inside one x tile
+  if ((long)256 * ldx * 2 >= (1L << 31)) return false;  // the largest tile's x rows (qpg: 256)
   for (int i = 0; i < nparts; ++i)
     if (parts[i].qtype < Q4_0 || parts[i].qtype > Q6_K || parts[i].rows % 16) return false;
   if (glu && (parts[0].qtype != parts[1].qtype || parts[0].rows != parts[1].rows)) return false;

@@ -109,6 +109,8 @@ for s in $steps; do
     pwtest) run_one tests/test_prefill_gemm_packed_gpu.py ;;
     longtest) run_one tests/test_long_context_gpu.py ;;
     kerneltest) run_one tests/test_kernels_gpu.py ;;
+    gguf64) timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64.log; [ $rc -eq 0 ] ;;
+    gguf64v2) HIPSERVE_QGEMM_M64=2 timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64_v2.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64_v2.log; [ $rc -eq 0 ] ;;
     qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
     qpfpmc) PMC_PY=tools/qpf_pmc.py PG_SHAPE=8192 bash scripts/pg_pmc.sh > $OUT/qpf_pmc.log 2>&1; rc=$?; tail -n 12 $OUT/qpf_pmc.log; [ $rc -eq 0 ] ;;
     qpfbench) timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 2048 8192 > $OUT/bench_qpf.log 2>&1; rc=$?; tail -n 40 $OUT/bench_qpf.log; [ $rc -eq 0 ] ;;

@@ -576,3 +576,20 @@ def test_mfma_v2_tiny_scales(qt):
     want = x.float() @ _dense([(qt, N, K, raw)]).T
     y = quant_linear(x, qw).float()
     assert (y - want).abs().max().item() < 1e-2 * want.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("qt", [G.Q6_K, G.Q4_K])
+@pytest.mark.parametrize("M", [33, 64])
+def test_qgemm_m64_wide_body(qt, M):
+    """33-64 rows at an LM-head width (N >= 32K) take the 256-row body (8 waves x 2 row
+    groups, m64_wide), plain and as split-K partials, vs an fp32 matmul of the decoded
+    weights; N not a multiple of 256 (a partial last tile)."""
+    from hipserve.ops.quant import quant_partial
+    N, K = 32768 + 144, 512
+    qw, raws = _rand_qw([(qt, N, K)], seed=M)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    want = x.float() @ _dense(raws).T
+    tol = 1e-2 * want.abs().max().item() + 1e-3
+    assert (quant_linear(x, qw).float() - want).abs().max().item() < tol
+    ws, S = quant_partial(x, qw)
+    assert (ws.view(S, M, N).sum(0) - want).abs().max().item() < tol
