@@ -863,40 +863,22 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
 }
 
 // ---------------------------------------------------------------- prefill GEMM
-// qpf_kernel (GGUF prefill without the resident bf16 shadow):
+// qpg_kernel (GGUF prefill without the resident bf16 shadow):
 // C[M, N] = X[M, K] . W^T straight from the tiled blocks, every weight dequantised ONCE
-// per 64-128-token tile (the M-swept qgemm2 above does it once per 64 tokens and stages
-// x for 128 weight rows; a dequantise-into-scratch + hipBLASLt pass writes and re-reads a
+// per 256-token tile (the M-swept qgemm2 above does it once per 64 tokens and stages x
+// for 128 weight rows; a dequantise-into-scratch + hipBLASLt pass writes and re-reads a
 // bf16 copy of the whole matrix per call).
 //   * X arrives as x16 (x_f16_pairs_kernel below): f16 in the weights' pair order, each
 //     row pre-scaled by a power of two 2^-k that keeps it inside the f16 range, the
-//     2^k in rsc[m] applied in the epilogue. Staging is then a plain 16-byte copy into
-//     LDS: converting bf16 x in every workgroup was 40 % of the kernel's VALU
-//     (tools/asm_stats.py: 380 VALU per super-chunk and wave, 160 of them x conversion);
-//   * workgroup = 8 waves x 2 row groups = 256 weight rows x 128 tokens, two waves per
-//     SIMD (64 accumulators, <= 256 registers each: one wave's dequant VALU runs beside
-//     the other's MFMAs); x staged once per 256-k super-chunk into a double-buffered LDS
-//     image (2 x 72 KiB), ONE barrier per super-chunk; the next super-chunk's x and
-//     weight blocks are in flight while this one is dequantised and multiplied;
-//   * per 32-k step a wave dequantises 2 weight fragments (2 VALU per pair,
-//     Dec::step) and issues 16 f16 MFMAs against 8 x fragments read from LDS;
+//     2^k in rsc[m] applied in the epilogue: converting bf16 x in every workgroup was
+//     40 % of an earlier 8-wave body's VALU (tools/asm_stats.py; that body and a
+//     4-wave / 128-token one: profiles/r4_qpf_bench_rt2.log, r4_qpf_bench_rt4.log);
 //   * weight bytes per MFMA are 3.5x (Q4_K) fewer than a bf16 GEMM's, which is what
 //     bounded the bf16 packed-layout kernel (profiles/r4_pw_diag_and_bench.log);
 //   * epilogues: STORE (part columns), ADD (C is the residual: C = bf16(bf16(acc) + C)),
-//     GLU (parts 0 / 1 = gate / up of the same format: a wave's row group 0 is gate
-//     rows, 1 the matching up rows, act = silu(gate) * up in registers).
-// Two shapes, both 256 weight rows x (64 or 128) tokens per workgroup (QF_ROWS):
-//   (RT 2, 8 waves): two waves per SIMD, <= 256 registers each; every x fragment read
-//     from LDS feeds 2 MFMAs — at 128 B per clock of LDS per CU that caps the MFMA pipe;
-//   (RT 4, 4 waves): one wave per SIMD (512 registers), every x fragment feeds 4 MFMAs:
-//     half the LDS traffic per MFMA, dequant VALU and MFMAs interleaved in one wave.
+//     GLU (parts 0 / 1 = gate / up of the same format: a wave's first row groups are
+//     gate rows, the others the matching up rows, act = silu(gate) * up in registers).
 constexpr int QF_ROWS = 256;  // weight rows per STORE / ADD tile (GLU: 128 act columns)
-constexpr int QF_MT = 8;
-HS_HOST_DEVICE constexpr int qf_waves(int rt) { return QF_ROWS / 16 / rt; }
-// tokens per tile: 128 (MT = 8); at RT 4, Q5_K / Q6_K (larger raw blocks: 16-19
-// registers per row group and buffer) 64, which keeps them within 512 registers
-template <int QT, int RT>
-constexpr int qf_mt() { return RT == 4 && (QT == Q5_K || QT == Q6_K) ? 4 : 8; }
 struct QfArgs {
   Parts parts;
   const unsigned short* x16;  // [M, ldx] f16, pair order, row m scaled by 1 / rsc[m]
@@ -907,190 +889,11 @@ struct QfArgs {
   int M, K, tiles_n, tiles_m;
 };
 
-template <int QT, int EPI, int RT>
-HS_DEVICE void qpf_body(_Float16* xs_, const QfArgs& A, int pi, int tm, int tn) {
-  constexpr int NW = qf_waves(RT), MT = qf_mt<QT, RT>(), NT = 64 * NW, XR = 16 * MT;
-  constexpr int XSZ = 4 * x_plane<MT>();  // one LDS buffer (f16)
-  auto xs = [&](int buf) { return xs_ + buf * XSZ; };
-  constexpr int CB = chunk_bytes<QT>();
-  constexpr bool kGlu = EPI == PW_EPI_GLU || EPI == PW_EPI_GEGLU;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, c = lane & 15;
-  const int K = A.K, M = A.M, nsb = K >> 8;
-  const Part& P = A.parts.p[pi];
-  const int ngroups = P.rows >> 4;
-  int gi[RT];
-  const unsigned char* base[RT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-    // GLU: row groups 0 .. RT/2 - 1 gate, RT/2 .. RT - 1 the matching up rows
-    gi[r] = kGlu ? (tn * NW + wave) * (RT / 2) + r % (RT / 2) : (tn - P.tile0) * (QF_ROWS / 16) + wave * RT + r;
-    const unsigned char* q = kGlu && r >= RT / 2 ? A.parts.p[1].q : P.q;
-    base[r] = q + (long)min(gi[r], ngroups - 1) * nsb * CB;
-  }
-  constexpr int XP = XR * 32 / NT;  // 16-byte x fragments per thread and super-chunk
-  // thread -> x row RS i + (tid >> 5) (i < XP), fragment tid & 31; the row offset rides
-  // in the VGPR offset (the range check covers it, not the scalar one): rows >= M read
-  // as zero
-  static_assert(NT % 32 == 0 && XP * NT == XR * 32, "x staging must divide evenly");
-  constexpr int RS = NT / 32;  // rows per staging pass
-  const int mrow0 = tm * XR;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(A.x16 + (long)mrow0 * A.ldx), 0, (int)((long)min(XR, M - mrow0) * A.ldx * 2), 0x00020000);
-  const int xfr = tid & 31, xrow = tid >> 5;
-  const int xo = (xrow * (int)A.ldx + kbase<QT>(xfr >> 3, xfr & 7)) * 2;
-  const int xd = (xfr >> 3) * x_plane<MT>() + xrow * kXR + (xfr & 7) * 8;
-  const int xstep = RS * (int)A.ldx * 2;
-  u32x4 xv[XP];
-  auto load_x = [&](int sb) {
-#pragma unroll
-    for (int i = 0; i < XP; ++i) xv[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, xo + i * xstep, sb * 512, 0);
-  };
-  auto store_x = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < XP; ++i) *reinterpret_cast<u32x4*>(xs(buf) + xd + i * RS * kXR) = xv[i];
-  };
-
-  f32x4 acc[RT][MT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Raw rawA[RT], rawB[RT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r) load_raw<QT>(base[r], g, c, lane, rawA[r]);
-  load_x(0);
-  store_x(0);
-  __syncthreads();
-  // per super-chunk: the next one's x and weight blocks go out first (x first: the
-  // in-order vmcnt wait before its LDS store leaves the weights in flight) and the x is
-  // written to the other LDS buffer (read last in the previous super-chunk, free since
-  // its barrier) at the end. The last super-chunk re-reads itself (no branch; its store
-  // lands in the unused buffer).
-  auto iter = [&](int sb, Raw (&cur)[RT], Raw (&nxt)[RT]) {
-    const int buf = sb & 1;
-    const int sn = min(sb + 1, nsb - 1);
-    load_x(sn);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
-    __builtin_amdgcn_sched_barrier(0);
-    const _Float16* xb = xs(buf) + g * x_plane<MT>() + c * kXR;
-    Dec<QT> dec[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) dec[r].setup(cur[r], g);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      f16x8 a[RT];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        // half the step's x fragments read from LDS ahead of their MFMAs (left alone the
-        // compiler reuses one register and every MFMA waits out an LDS round trip)
-        f16x8 b[MT / 2];
-#pragma unroll
-        for (int t = 0; t < MT / 2; ++t) b[t] = *reinterpret_cast<const f16x8*>(xb + 16 * (h * MT / 2 + t) * kXR + 8 * s);
-        __builtin_amdgcn_sched_barrier(0);
-        if (h == 0) {
-#pragma unroll
-          for (int r = 0; r < RT; ++r) a[r] = dec[r].step(cur[r], g, s);
-        }
-#pragma unroll
-        for (int t = 0; t < MT / 2; ++t)
-#pragma unroll
-          for (int r = 0; r < RT; ++r)
-            acc[r][h * MT / 2 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[r], b[t], acc[r][h * MT / 2 + t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    store_x(buf ^ 1);
-    __syncthreads();
-  };
-  int sb = 0;
-  for (; sb + 1 < nsb; sb += 2) {
-    iter(sb, rawA, rawB);
-    iter(sb + 1, rawB, rawA);
-  }
-  if (sb < nsb) iter(sb, rawA, rawB);
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {  // undo the row pre-scale (exact: a power of two)
-    const float sc = A.rsc[min(mrow0 + 16 * t + c, M - 1)];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r][t] *= sc;
-  }
-  // lane holds C[m = mrow0 + 16 t + c][rows 16 gi + 4 g + j]
-  if constexpr (kGlu) {
-#pragma unroll
-    for (int r = 0; r < RT / 2; ++r) {
-      if (gi[r] >= ngroups) continue;
-      const int col = 16 * gi[r] + 4 * g;
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const int m = mrow0 + 16 * t + c;
-        if (m >= M) continue;
-        unsigned short o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const unsigned short gv = f32_to_bf16(acc[r][t][j]), uv = f32_to_bf16(acc[r + RT / 2][t][j]);
-          o[j] = EPI == PW_EPI_GEGLU ? gelu_mul1(gv, uv) : silu_mul1(gv, uv);
-        }
-        *reinterpret_cast<uint2*>(A.out + (long)m * A.ldo + col) =
-            uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
-      }
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      if (gi[r] >= ngroups) continue;
-      const int col = P.col + 16 * gi[r] + 4 * g;
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const int m = mrow0 + 16 * t + c;
-        if (m >= M) continue;
-        uint2* dst = reinterpret_cast<uint2*>(A.out + (long)m * A.ldo + col);
-        float o[4];
-        if constexpr (EPI == PW_EPI_ADD) {
-          const uint2 rv = *dst;
-          const unsigned short rr[4] = {(unsigned short)(rv.x & 0xffff), (unsigned short)(rv.x >> 16),
-                                        (unsigned short)(rv.y & 0xffff), (unsigned short)(rv.y >> 16)};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = bf16_to_f32(f32_to_bf16(acc[r][t][j])) + bf16_to_f32(rr[j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = acc[r][t][j];
-        }
-        *dst = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
-      }
-    }
-  }
-}
-
-// tiles: n-major groups of 8 m-tiles (an XCD's concurrent workgroups share x rows and
-// weight blocks in its L2), blockIdx remapped so an XCD holds consecutive tiles
-template <int QT, int EPI, int RT>
-__global__ __launch_bounds__(64 * qf_waves(RT)) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 2 : 1, RT == 2 ? 2 : 1)))
-void qpf_kernel(QfArgs A) {
-  constexpr int XSZ = 4 * x_plane<qf_mt<QT, RT>()>();
-  __shared__ __attribute__((aligned(16))) _Float16 xs[2 * XSZ];
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 8;
-  const int grp = L / (GM * A.tiles_n), first = grp * GM;
-  const int gsz = min(GM, A.tiles_m - first);
-  const int rr = L - first * A.tiles_n;
-  const int tm = first + rr % gsz, tn = rr / gsz;
-  int pi = 0;
-  if constexpr (EPI != PW_EPI_GLU && EPI != PW_EPI_GEGLU) {
-#pragma unroll
-    for (int i = 1; i < kMaxParts; ++i)
-      if (i < A.parts.n && tn >= A.parts.p[i].tile0) pi = i;
-  }
-  qpf_body<QT, EPI, RT>(xs, A, pi, tm, tn);
-}
-
-// ---- big-tile variant (qpg): 4 waves x 4 row groups = 256 weight rows x 256 tokens
-// (128 for Q5_K / Q6_K), one wave per SIMD, the 256 (128) accumulators in AGPRs. The
-// 8-wave qpf above is bound by its dequant VALU per MFMA (a weight fragment feeds only
-// 8 MFMAs: 2.6 VALU per MFMA, MFMA pipe 45 % busy, profiles/r4_qpf_pmc_v1.log); here a
-// fragment feeds 16, and x never passes through registers:
+// Shape: 4 waves x 4 row groups = 256 weight rows x 256 tokens (128 for Q5_K / Q6_K /
+// Q8_0), one wave per SIMD, the 256 (128) accumulators in AGPRs. The earlier 8-wave body
+// was bound by its dequant VALU per MFMA (a weight fragment fed only 8 MFMAs: 2.6 VALU per
+// MFMA, MFMA pipe 45 % busy, profiles/r4_qpf_pmc_v1.log); here a fragment feeds 16, and x
+// never passes through registers:
 //   * x16 is staged by LDS-DMA (buffer_load ... lds, 1 KiB per wave instruction) in
 //     half super-chunks (steps 0-3 / 4-7) into two LDS buffers; wave w loads plane
 //     g = w, lane i of instruction j row 16 j + i / 4 and 16-byte slot i & 3, holding
@@ -1318,48 +1121,6 @@ void qpg_launch(int epi, QfArgs A, hipStream_t s) {
   }
 }
 
-template <int QT, int RT>
-void qpf_launch_rt(int epi, const QfArgs& A, hipStream_t s) {
-  const dim3 grid(A.tiles_n * A.tiles_m), block(64 * qf_waves(RT));
-  switch (epi) {
-    case PW_EPI_STORE: qpf_kernel<QT, PW_EPI_STORE, RT><<<grid, block, 0, s>>>(A); break;
-    case PW_EPI_ADD: qpf_kernel<QT, PW_EPI_ADD, RT><<<grid, block, 0, s>>>(A); break;
-    case PW_EPI_GLU: qpf_kernel<QT, PW_EPI_GLU, RT><<<grid, block, 0, s>>>(A); break;
-    case PW_EPI_GEGLU: qpf_kernel<QT, PW_EPI_GEGLU, RT><<<grid, block, 0, s>>>(A); break;
-  }
-}
-
-// HIPSERVE_QPF_RT: kernel shape — 2: 8 waves x 2 row groups, 4: 4 waves x 4 row groups
-// (measured 10-37 % slower than 2, profiles/r4_qpf_bench_rt4.log), 16 (default): the
-// big-tile qpg_kernel
-int qpf_rt() {
-  static const int v = [] {
-    const char* e = getenv("HIPSERVE_QPF_RT");
-    const int r = e != nullptr ? atoi(e) : 16;
-    return r == 2 || r == 4 ? r : 16;
-  }();
-  return v;
-}
-
-template <int QT>
-void qpf_launch(int epi, QfArgs A, hipStream_t s) {
-  if (qpf_rt() == 16) {
-    qpg_launch<QT>(epi, A, s);
-    return;
-  }
-  const int rt = QT == Q8_0 ? 2 : qpf_rt();  // Q8_0 spills at RT 4
-  const int bm = 16 * (rt == 2 ? qf_mt<QT, 2>() : qf_mt<QT, 4>());
-  A.tiles_m = (A.M + bm - 1) / bm;
-  if constexpr (QT == Q8_0) {
-    qpf_launch_rt<QT, 2>(epi, A, s);
-  } else {
-    if (rt == 2)
-      qpf_launch_rt<QT, 2>(epi, A, s);
-    else
-      qpf_launch_rt<QT, 4>(epi, A, s);
-  }
-}
-
 // x [M, K] bf16 -> x16 [M, K] f16 in the pair order {0, 2, 1, 3, 4, 6, 5, 7} of every
 // aligned 8-run, each row scaled by 2^-k (k >= 0, the smallest keeping max |x| below
 // 2^15), rsc[m] = 2^k: the prefill GEMM's operand, converted once per activation instead
@@ -1479,7 +1240,7 @@ bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long
   return false;
 }
 
-// Prefill GEMM over tiled GGUF parts (qpf_kernel) on x16 / rsc from launch_x_f16_pairs
+// Prefill GEMM over tiled GGUF parts (qpg_kernel) on x16 / rsc from launch_x_f16_pairs
 // (row stride K). STORE: out[:, col .. col + rows) per
 // part; ADD: out is the residual (updated in place); GLU / GEGLU: parts 0 / 1 are gate / up
 // (same format and rows), out[M, rows] = act(gate) * up. Formats: GGUF (Q4_0 .. Q6_K);
@@ -1526,7 +1287,7 @@ bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x16, const fl
     A.tiles_n = glu ? (parts[0].rows + QF_ROWS / 2 - 1) / (QF_ROWS / 2) : tiles;
 #define QF_CASE(QT_)          \
   if (fa == QT_) {              \
-    qpf_launch<QT_>(epi, A, s); \
+    qpg_launch<QT_>(epi, A, s); \
     return;                     \
   }
     QF_CASE(Q4_0) QF_CASE(Q4_1) QF_CASE(Q8_0) QF_CASE(Q4_K) QF_CASE(Q5_K) QF_CASE(Q6_K)

@@ -584,8 +584,8 @@ def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = No
     return ws, S
 
 
-# Prefill (M > MAX_FUSED_M) straight from the tiled GGUF blocks (gguf_mfma.hip qpf_kernel:
-# each weight dequantised once per 64-128-token tile, f16 MFMA, store / residual-add / GLU
+# Prefill (M > MAX_FUSED_M) straight from the tiled GGUF blocks (gguf_mfma.hip qpg_kernel:
+# each weight dequantised once per 128-256-token tile, f16 MFMA, store / residual-add / GLU
 # epilogues): no resident bf16 shadow and no per-call dequantise-into-scratch pass.
 # HIPSERVE_QPREFILL: "1" always, "0" never (dequantise into scratch + hipBLASLt), "auto"
 # (default): per weight shape, whichever tune_qprefill timed faster at engine start
@@ -614,7 +614,7 @@ def qprefill_ok(w, M: int, glu: bool = False, timed: bool = True) -> bool:
 
 def tune_qprefill(weights, device, M: int) -> list:
     """Start-up timing, per distinct GGUF weight shape, of the block prefill GEMM (x
-    conversion + qpf_kernel, GLU epilogue for (gate, up) pairs) against dequantise into
+    conversion + qpg_kernel, GLU epilogue for (gate, up) pairs) against dequantise into
     scratch + hipBLASLt (+ silu_and_mul) at M rows; fills QPF_CHOICE for ``auto``."""
     from . import pgemm
     seen, rows = {}, []
@@ -776,7 +776,7 @@ def make_dense_shadows(weights, device, reserve_bytes: int, gguf: bool = True) -
     runs hipBLASLt on the copy. Largest weights first (lm_head, gate|up, ...). GGUF
     weights only with ``gguf`` (the engine passes HIPSERVE_QUANT_SHADOW=1 /
     extra gguf_dense_shadow; default off: a GGUF model's footprint is its blocks, prefill
-    reads them through qpf_kernel or a per-call scratch). Returns the bytes added."""
+    reads them through qpg_kernel or a per-call scratch). Returns the bytes added."""
     if torch.device(device).type != "cuda":
         return 0
     from . import pgemm

@@ -114,10 +114,6 @@ for s in $steps; do
     qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
     qpfpmc) PMC_PY=tools/qpf_pmc.py PG_SHAPE=8192 bash scripts/pg_pmc.sh > $OUT/qpf_pmc.log 2>&1; rc=$?; tail -n 12 $OUT/qpf_pmc.log; [ $rc -eq 0 ] ;;
     qpfbench) timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 2048 8192 > $OUT/bench_qpf.log 2>&1; rc=$?; tail -n 40 $OUT/bench_qpf.log; [ $rc -eq 0 ] ;;
-    qpfbench4) HIPSERVE_QPF_RT=4 timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 8192 --only qkv gate_up down > $OUT/bench_qpf_rt4.log 2>&1; rc=$?; grep qpf $OUT/bench_qpf_rt4.log; [ $rc -eq 0 ] ;;
-    qpftest4) HIPSERVE_QPF_RT=4 run_one tests/test_gguf_prefill_gpu.py ;;
-    qpftest2) HIPSERVE_QPF_RT=2 run_one tests/test_gguf_prefill_gpu.py ;;
-    qpfbench2) HIPSERVE_QPF_RT=2 timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 8192 --only qkv o gate_up down > $OUT/bench_qpf_rt2.log 2>&1; rc=$?; grep qpf $OUT/bench_qpf_rt2.log; [ $rc -eq 0 ] ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
     tptest) timeout -k 10 1000 python -u -m pytest tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread \
               -p no:cacheprovider > $OUT/test_tp_gpu.log 2>&1; rc=$?; tail -n 20 $OUT/test_tp_gpu.log; [ $rc -eq 0 ] ;;
