@@ -412,7 +412,7 @@ def test_dense_shadow_prefill_matches_dequant_path(monkeypatch):
 
 @pytest.mark.parametrize("M", [65, 130, 256])
 def test_prefill_m_tiled_kernel_vs_fp32(M):
-    """K15: prefill chunks without a bf16 shadow run the block prefill GEMM (qpf_kernel,
+    """K15: prefill chunks without a bf16 shadow run the block prefill GEMM (qpg_kernel,
     one launch per format), vs an fp32 matmul of the decoded weights."""
     from hipserve.ops import quant as Q
     qw, raws = _rand_qw([(G.Q4_K, 512, 2048), (G.Q6_K, 272, 2048)], seed=M)

@@ -1,4 +1,4 @@
-"""GGUF prefill GEMM straight from the tiled blocks (gguf_mfma.hip qpf_kernel) vs a plain
+"""GGUF prefill GEMM straight from the tiled blocks (gguf_mfma.hip qpg_kernel) vs a plain
 PyTorch fp32 reference on the numpy block decoder's weights: plain store into part
 columns (mixed formats, as Q4_K_M's q|k|v), residual add, SiLU / GELU GLU of gate / up
 parts, ragged M / N, and rows beyond the f16 range (x_f16_pairs' power-of-two row
