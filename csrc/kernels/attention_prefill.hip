@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     const unsigned short* __restrict__ k_cache, const unsigned short* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ cu_q,
     const int* __restrict__ ctx_lens, const int* __restrict__ tiles, int nq, int nkv, int block_size,
-    float scale, int window) {
+    float scale, int window, int prio) {
   constexpr int D = 128, KS = 8, NB = 4;
   constexpr int RB = NWV / HG, QR = 32 * RB, SUB = 128 / QR;
   constexpr int NT = 64 * NWV, NP = 1024 / NT;  // threads; K (and V^T) 16-byte pieces per thread
@@ -282,6 +282,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
       for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[h2][r] = 0.f;
+      if (prio) __builtin_amdgcn_s_setprio(1);  // MFMA cluster: the partner wave's softmax VALU waits
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -289,6 +290,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
           const u16x8 a = *reinterpret_cast<const u16x8*>(kb + (32 * h2) * PA2_KLD + 16 * ks);
           st[h2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], st[h2], 0, 0, 0);
         }
+      if (prio) __builtin_amdgcn_s_setprio(0);
       // diagonal tile (causal mask) or a tile crossing some row's window start
       if (kbase + PA2_KT - 1 > wmin_pos || (window > 0 && kbase <= wmax_key - window)) {
 #pragma unroll
@@ -328,6 +330,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
           psum += p;
           pb[r >> 3][r & 7] = static_cast<__bf16>(p);
         }
+        if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const unsigned short* vb = &vl[buf][qi * PA2_VLD + 32 * h2 + 16 * s2 + 8 * half];
@@ -337,6 +340,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
             o[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pb[s2], o[nb], 0, 0, 0);
           }
         }
+        if (prio) __builtin_amdgcn_s_setprio(0);
       }
       l_run += psum;
     }
@@ -389,6 +393,12 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
     const char* ew = getenv("HIPSERVE_PREFILL_ATTN_WAVES");  // 8 (default) or 4 waves per workgroup
     const int nwv = (ew != nullptr && atoi(ew) == 4) ? 4 : 8;
     const int HG = G >= nwv ? nwv : G;
+    // s_setprio 1 around each MFMA cluster (the partner wave's softmax VALU yields to it):
+    // 3 % faster at 1K-32K tokens (profiles/r4_prefill_attn_setprio.log; a static
+    // priority for the younger wave of each SIMD gained 1 %); HIPSERVE_PREFILL_ATTN_PRIO=0
+    // turns it off
+    const char* ep = getenv("HIPSERVE_PREFILL_ATTN_PRIO");
+    const int prio = ep != nullptr && atoi(ep) == 0 ? 0 : 1;
     const int sub = 128 / (32 * (nwv / HG));
     dim3 g2(ntiles * sub, nkv * (G / HG));
     auto* o2 = static_cast<unsigned short*>(out);
@@ -398,7 +408,7 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
 #define PA2_LAUNCH(hg, nw)                                                                                  \
   prefill_attn_v2_kernel<hg, nw><<<g2, 64 * nw, 0, s>>>(o2, out_stride, q2, q_stride, k2, v2, block_tables, \
                                                         bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale, \
-                                                        window)
+                                                        window, prio)
     if (nwv == 8) {
       if (HG == 8) PA2_LAUNCH(8, 8);
       else if (HG == 4) PA2_LAUNCH(4, 8);

@@ -120,7 +120,11 @@ def bench_decode(ops):
 
 def bench_prefill(ops):
     D, bs = 128, 16
-    for S, nseq, nq, nkv in [(1024, 8, 32, 8), (4096, 2, 32, 8), (8192, 1, 32, 8), (1024, 8, 8, 1)]:
+    shapes = [(1024, 8, 32, 8), (4096, 2, 32, 8), (8192, 1, 32, 8), (1024, 8, 8, 1)]
+    if os.environ.get("BENCH_PREFILL_LONG"):
+        shapes = [(1024, 8, 32, 8), (8192, 1, 32, 8), (32768, 1, 32, 8)]
+    vers = os.environ.get("BENCH_PREFILL_VERS", "v2w4,v2w8,v1").split(",")
+    for S, nseq, nq, nkv in shapes:
         mb = S // bs
         kc = torch.randn(nseq * mb, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
         vc = torch.randn(nseq * mb, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
@@ -132,7 +136,7 @@ def bench_prefill(ops):
         q = torch.randn(nseq * S, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
         out = torch.empty(nseq * S, nq * D, device=DEV, dtype=torch.bfloat16)
         flops = 4 * nseq * (S * S / 2) * D * nq
-        for ver in ("v2w4", "v2w8", "v1"):  # v1: per-wave L2 K/V reads (HIPSERVE_PREFILL_ATTN_V1=1)
+        for ver in vers:  # v1: per-wave L2 K/V reads (HIPSERVE_PREFILL_ATTN_V1=1)
             os.environ["HIPSERVE_PREFILL_ATTN_V1"] = "1" if ver == "v1" else "0"
             os.environ["HIPSERVE_PREFILL_ATTN_WAVES"] = "8" if ver == "v2w8" else "4"
             us = timeit(lambda: ops.prefill_attention(out, q, kc, vc, bt, cu, ctx, tiles, nq, nkv,
