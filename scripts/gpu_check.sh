@@ -126,6 +126,8 @@ for s in $steps; do
     prof32k) prof_run prof32k --model llama-3.1-8b --input-len 32768 --output-len 64 --concurrency 4 --max-num-batched-tokens 8192 ;;
     long8k) bench_named long8k X=1 -- --model llama-3.1-8b --input-len 8192 --output-len 256 --concurrency 16 --max-num-batched-tokens 8192 --steps 2 ;;
     long32k) bench_named long32k X=1 -- --model llama-3.1-8b --input-len 32768 --output-len 256 --concurrency 4 --max-num-batched-tokens 8192 --steps 2 ;;
+    long32k_p0) bench_named long32k_p0 HIPSERVE_PREFILL_ATTN_PRIO=0 -- --model llama-3.1-8b --input-len 32768 --output-len 256 --concurrency 4 --max-num-batched-tokens 8192 --steps 2 ;;
+    long32k_p1) bench_named long32k_p1 HIPSERVE_PREFILL_ATTN_PRIO=1 -- --model llama-3.1-8b --input-len 32768 --output-len 256 --concurrency 4 --max-num-batched-tokens 8192 --steps 2 ;;
     bench_mixtral_packed) bench_named mixtral_packed HIPSERVE_MOE_PACKED_PREFILL=1 -- --model mixtral-8x7b --concurrency 32 ;;
     bench_mixtral_old) bench_named mixtral_old HIPSERVE_MOE_PACKED_PREFILL=0 -- --model mixtral-8x7b --concurrency 32 ;;
     prof_qwen3moe) prof_run profqm --model qwen3-30b-a3b ;;
