@@ -603,7 +603,8 @@ def qprefill_ok(w, M: int, glu: bool = False, timed: bool = True) -> bool:
     ``timed``: and the start-up timing (``auto``) did not prefer dequant + hipBLASLt."""
     if not (QPREFILL and isinstance(w, QuantWeight) and M > MAX_FUSED_M and w.dense is None):
         return False
-    if not (w.v2 and all(p.kqt in GGUF_KQT for p in w.parts) and hasattr(torch.ops.hipserve, "gguf_prefill")):
+    if not (w.v2 and w.parts[0].q.is_cuda and all(p.kqt in GGUF_KQT for p in w.parts)
+            and hasattr(torch.ops.hipserve, "gguf_prefill")):
         return False
     if glu:
         ps = w.parts
