@@ -88,11 +88,15 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
   }
 
   const unsigned short* wr[RT];
+  // packed: [128-row tile][kstep][row group][slot s][lane][8]; a 64-row workgroup
+  // (NW = 64) streams half the row groups of one packed tile
+  constexpr int PT = 128 / NW;
+  static_assert(!kGlu || PT == 1, "the GLU epilogue pairs the two halves of a 128-row tile");
   if constexpr (kPacked) {
-    // [tile][kstep][row group = wave*RT + r][slot s][lane][8]
-    const unsigned short* wp = w + ((long)tile * (K >> 8) + (long)split * NSTEPS) * (NW * 256) + lane * 8;
+    const int ptile = tile / PT, prg0 = (tile - ptile * PT) * (NW / 16);
+    const unsigned short* wp = w + ((long)ptile * (K >> 8) + (long)split * NSTEPS) * 32768 + lane * 8;
 #pragma unroll
-    for (int r = 0; r < RT; ++r) wr[r] = wp + (long)(wave * RT + r) * (8 * 512);
+    for (int r = 0; r < RT; ++r) wr[r] = wp + (long)(prg0 + wave * RT + r) * (8 * 512);
   } else {
 #pragma unroll
     for (int r = 0; r < RT; ++r) wr[r] = w + (long)min(nbase + 16 * r + c, N - 1) * K + k0 + 8 * g;
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(64 * NWAVES) void decode_gemm_kernel(
 #pragma unroll
       for (int s = 0; s < 8; ++s)
         ring[slot][r][s] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(
-            kPacked ? wr[r] + (long)step * (NW * 256) + 512 * s : wr[r] + step * 256 + 32 * s));
+            kPacked ? wr[r] + (long)step * 32768 + 512 * s : wr[r] + step * 256 + 32 * s));
   };
   // prologue: x(0) -> LDS[0]; x(1) in registers; W(0), W(1) in flight
   load_x(0);
@@ -307,10 +311,13 @@ void launch_splitk_reduce(void* out, long out_stride, const float* ws, int M, in
   splitk_reduce_kernel<<<(n8 + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out), out_stride, ws, M, N, S);
 }
 
-template <int MT, int RT, int NSTEPS, bool kPacked, bool kGlu>
+// rt 1: 8 waves x 1 row group, 2: 4 waves x 2 (both 128 weight rows per workgroup);
+// 3: 4 waves x 1 (64 rows: twice the workgroups at the same K split, for projections
+// whose 128-row tiles do not fill the chip without more split-K partials)
+template <int MT, int RT, int NSTEPS, bool kPacked, bool kGlu, int NWAVES = RT == 1 ? 8 : 4>
 static void dg_launch(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                       int N, int K, int S, int flags, hipStream_t s) {
-  constexpr int NWAVES = RT == 1 ? 8 : 4, NW = 16 * RT * NWAVES;  // 128 weight rows per workgroup
+  constexpr int NW = 16 * RT * NWAVES;
   const int tiles = (N + NW - 1) / NW;
   decode_gemm_kernel<MT, RT, NWAVES, NSTEPS, kPacked, kGlu><<<tiles * S, 64 * NWAVES, 0, s>>>(
       static_cast<unsigned short*>(out), out_stride, ws, static_cast<const unsigned short*>(x), x_stride,
@@ -328,22 +335,21 @@ static void dg_launch(void* out, long out_stride, float* ws, const void* x, long
   }
 }
 
-template <int MT, int RT, bool kPacked, bool kGlu>
+template <int MT, int RT, bool kPacked, bool kGlu, int NWAVES = RT == 1 ? 8 : 4>
 static bool dg_steps(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M, int N,
                      int K, int S, int flags, hipStream_t s) {
   const int nsteps = K / S / 256;
+#define DG_CASE(NS)                                                                                       \
+  case NS:                                                                                                \
+    dg_launch<MT, RT, NS, kPacked, kGlu, NWAVES>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); \
+    return true;
   switch (nsteps) {
-    case 1: dg_launch<MT, RT, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
-    case 2: dg_launch<MT, RT, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
-    case 4: dg_launch<MT, RT, 4, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
-    case 7: dg_launch<MT, RT, 7, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
-    case 8: dg_launch<MT, RT, 8, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
-    case 16: dg_launch<MT, RT, 16, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    DG_CASE(1) DG_CASE(2) DG_CASE(4) DG_CASE(7) DG_CASE(8) DG_CASE(16)
     // K = 3072 (Phi-3, Llama-3.2-3B) and K = 5376 (Gemma-3-27B) in one K slice
-    case 12: dg_launch<MT, RT, 12, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
-    case 21: dg_launch<MT, RT, 21, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s); return true;
+    DG_CASE(12) DG_CASE(21)
     default: return false;
   }
+#undef DG_CASE
 }
 
 template <bool kPacked, bool kGlu>
@@ -358,6 +364,9 @@ static bool dg_dispatch(void* out, long out_stride, float* ws, const void* x, lo
   } else {
     if (rt == 1) return dg_steps<4, 1, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
     if (rt == 2) return dg_steps<4, 2, kPacked, kGlu>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
+    if constexpr (!kGlu) {  // 64-row workgroups (33-64 rows: the decode batch of the headline load)
+      if (rt == 3) return dg_steps<4, 1, kPacked, kGlu, 4>(out, out_stride, ws, x, x_stride, w, M, N, K, S, flags, s);
+    }
   }
   return false;
 }

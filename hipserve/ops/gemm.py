@@ -22,7 +22,7 @@ log = logging.getLogger("hipserve.gemm")
 SKINNY_CONFIGS = [(1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (2, 1), (2, 2), (2, 4), (2, 8)]
 # split-K MFMA GEMM with an LDS-staged x chunk shared by 64 rows (gguf.hip, qtype 6 = bf16)
 SPLITK_CONFIGS = [1, 2, 4, 8]
-DG_RT = [1, 2]
+DG_RT = [1, 2, 3]  # 3: 64-row workgroups (4 waves x 1 row group), 33-64 rows, no GLU epilogue
 DG_STEPS = [1, 2, 4, 7, 8, 12, 16, 21]  # 256-k steps per workgroup (compile-time in decode_gemm.hip)
 # decode weights pre-shuffled for the packed decode GEMM, keyed by the plain
 # weight's data_ptr (the plain [N, K] copy stays for prefill / hipBLASLt)
@@ -130,7 +130,7 @@ class GemmTuner:
                     (lambda i: F.linear(x, ws_[i % ncopy]))
                 best, best_t = "blas", self._time(blas_fn, n=n)
                 t_blas = best_t
-                for cfg in self.candidates(M, N, K, packed=wp_ is not None):
+                for cfg in self.candidates(M, N, K, packed=wp_ is not None, glu=glu):
                     if unit is not None:
                         if cfg[0] == "sk":
                             continue
@@ -152,10 +152,12 @@ class GemmTuner:
         return self.report
 
     @staticmethod
-    def candidates(M, N, K, packed=False):
+    def candidates(M, N, K, packed=False, glu=False):
         out = []
-        tiles = -(-N // 128)
         for rt in DG_RT:
+            if rt == 3 and (glu or not 32 < M <= 64):
+                continue
+            tiles = -(-N // (64 if rt == 3 else 128))
             for ns in DG_STEPS:
                 if K % (256 * ns):
                     continue

@@ -536,3 +536,29 @@ def test_moe_grouped_prefill_vs_fp32(ops, T, E, k, norm):
     x_big = torch.randn(MOE_KERNEL_MAX_ROWS_PER_EXPERT * E // k + 64, H, device=DEV, dtype=torch.bfloat16)
     m.moe(x_big, lw)
     assert calls, "prefill-sized MoE did not take the grouped path"
+
+
+@pytest.mark.parametrize("M", [33, 50, 64])
+@pytest.mark.parametrize("packed", [True, False])
+@pytest.mark.parametrize("N,K,splits", [(6144, 4096, 4), (4096, 4096, 8), (1000, 512, 1), (4160, 1792, 1),
+                                        (4096, 14336, 8)])
+def test_decode_gemm_64_row_workgroups(ops, M, N, K, splits, packed):
+    """rt = 3: 64-row workgroups (4 waves x 1 row group; a packed 128-row tile split over
+    two workgroups), plain and as split-K partials, vs fp32 torch; N tails inside a
+    packed tile's second half."""
+    from hipserve.ops import gemm
+    torch.manual_seed(M + N + K)
+    xb = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
+    x = xb[:, :K]
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    want = x.float() @ w.float().T
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    if packed:
+        gemm.decode_gemm_packed(out, x, gemm.pack(w), N, 3, splits)
+    else:
+        gemm.decode_gemm(out, x, w, 3, splits)
+    assert not torch.isnan(out).any(), "unwritten outputs"
+    _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
+    ws = torch.full((splits * M * N,), float("nan"), device=DEV, dtype=torch.float32)
+    torch.ops.hipserve.decode_gemm_partial(ws, x, gemm.pack(w) if packed else w, N, 3, splits, packed)
+    _close(ws.view(splits, M, N).sum(0), want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
