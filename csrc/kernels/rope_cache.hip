@@ -123,7 +123,7 @@ template <int kMode>
 __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
     unsigned short* __restrict__ qkv, long qkv_stride, const long* __restrict__ positions,
     const long* __restrict__ slots, const float* __restrict__ cos_sin, unsigned short* __restrict__ k_cache,
-    unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D, int block_size) {
+    unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D, int block_size, int vfast) {
   extern __shared__ __attribute__((aligned(16))) unsigned short vs[];  // [16][nkv * D + 8]
   const int t0 = blockIdx.x * kRopeTile;
   const int nt = min(kRopeTile, T - t0);
@@ -210,14 +210,35 @@ __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
         *reinterpret_cast<const u16x8*>(qkv + (t0 + tt) * qkv_stride + (nq + nkv) * D + c * 8);
   }
   __syncthreads();
-  for (int it = threadIdx.x; it < kRopeTile * VW; it += blockDim.x) {
-    const int tt = it & (kRopeTile - 1), r = it / kRopeTile;
-    if (tt >= nt) continue;
-    const long slot = slots[t0 + tt];
-    if (slot < 0) continue;
+  // The 16 tokens usually fill 16 consecutive slots of one block (prefill of a
+  // block-aligned sequence): each V^T row segment is then 32 contiguous bytes, written
+  // as two 16-byte stores gathered from 8 LDS rows each (8 stores per thread instead
+  // of 64 2-byte stores, each with its own slot load and 64-bit divide).
+  const long s0 = slots[t0];
+  const int off0 = s0 >= 0 ? (int)(s0 % block_size) : 1;
+  bool contig = vfast && nt == kRopeTile && (block_size & 7) == 0 && (off0 & 7) == 0 && off0 + kRopeTile <= block_size;
+  for (int i = 1; contig && i < kRopeTile; ++i) contig = slots[t0 + i] == s0 + i;  // block-uniform
+  if (contig) {
+    const long blk = s0 / block_size;
+    for (int it = threadIdx.x; it < 2 * VW; it += blockDim.x) {
+      const int r = it >> 1, hl = it & 1;
+      const int kh = r / D, d = r % D;
+      u16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = vs[(hl * 8 + j) * VR + r];
+      *reinterpret_cast<u16x8*>(v_cache + (blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off0 +
+                                hl * 8) = v;
+    }
+    return;
+  }
+  // general case: lane -> one token (blockDim.x % 16 == 0), its slot decoded once
+  const int tt = threadIdx.x & (kRopeTile - 1);
+  const long slot = tt < nt ? slots[t0 + tt] : -1;
+  if (slot < 0) return;  // after the only barrier
+  const long blk = slot / block_size;
+  const int off = (int)(slot % block_size);
+  for (int r = threadIdx.x / kRopeTile; r < VW; r += blockDim.x / kRopeTile) {
     const int kh = r / D, d = r % D;
-    const long blk = slot / block_size;
-    const int off = (int)(slot % block_size);
     v_cache[(blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off] = vs[tt * VR + r];
   }
 }
@@ -226,6 +247,14 @@ static bool rope_tile_enabled() {
   static const bool on = [] {
     const char* e = getenv("HIPSERVE_ROPE_TILE");
     return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+static int rope_vfast() {  // HIPSERVE_ROPE_VFAST=0: 2-byte V^T stores for every tile (A/B)
+  static const int on = [] {
+    const char* e = getenv("HIPSERVE_ROPE_VFAST");
+    return !(e && atoi(e) == 0) ? 1 : 0;
   }();
   return on;
 }
@@ -244,10 +273,10 @@ void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
     const size_t smem = (size_t)kRopeTile * (nkv * D + 8) * sizeof(unsigned short);
     if (mode == 0)
       rope_cache_tile_kernel<0><<<tg, block, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq, nkv,
-                                                        D, block_size);
+                                                        D, block_size, rope_vfast());
     else
       rope_cache_tile_kernel<1><<<tg, block, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq, nkv,
-                                                        D, block_size);
+                                                        D, block_size, rope_vfast());
     return;
   }
   if (mode == 0)

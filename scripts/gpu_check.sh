@@ -114,6 +114,9 @@ for s in $steps; do
     gguf64) timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64.log; [ $rc -eq 0 ] ;;
     gguf64v2) HIPSERVE_QGEMM_M64=2 timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64_v2.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64_v2.log; [ $rc -eq 0 ] ;;
     qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
+    rope) timeout -k 10 180 python -u tools/bench_rope.py > $OUT/bench_rope.log 2>&1 && \
+          HIPSERVE_ROPE_VFAST=0 timeout -k 10 180 python -u tools/bench_rope.py > $OUT/bench_rope_v0.log 2>&1; rc=$?
+          cat $OUT/bench_rope.log $OUT/bench_rope_v0.log; [ $rc -eq 0 ] ;;
     qpfpmc) PMC_PY=tools/qpf_pmc.py PG_SHAPE=8192 bash scripts/pg_pmc.sh > $OUT/qpf_pmc.log 2>&1; rc=$?; tail -n 12 $OUT/qpf_pmc.log; [ $rc -eq 0 ] ;;
     qpfbench) timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 2048 8192 > $OUT/bench_qpf.log 2>&1; rc=$?; tail -n 40 $OUT/bench_qpf.log; [ $rc -eq 0 ] ;;
     enginetest) run_one tests/test_engine_gpu.py ;;

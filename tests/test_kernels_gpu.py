@@ -58,11 +58,13 @@ def _caches(nblocks, nkv, bs, D, fill=True):
 
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("bs", [16, 32])
-@pytest.mark.parametrize("T,layout", [(37, "random"), (300, "random"), (300, "contig"), (1000, "contig")])
+@pytest.mark.parametrize("T,layout", [(37, "random"), (300, "random"), (300, "contig"), (1000, "contig"),
+                                      (300, "aligned"), (1000, "aligned")])
 def test_rope_cache(ops, mode, bs, T, layout):
     """Per-token kernel (T < 128) and the 16-token tile kernel of prefill chunks
     (LDS-staged V, token-fastest V^T stores), scattered and contiguous slots
-    (contig: a chunk starting mid-block), vs the fp32 oracle."""
+    (contig: a chunk starting mid-block; aligned: block-aligned, so whole tiles take the
+    16-byte V^T store path), vs the fp32 oracle."""
     torch.manual_seed(1)
     nq, nkv, D = 32, 8, 128
     qkv = torch.randn(T, (nq + 2 * nkv) * D + 64, device=DEV, dtype=torch.bfloat16)[:, : (nq + 2 * nkv) * D]
@@ -70,7 +72,7 @@ def test_rope_cache(ops, mode, bs, T, layout):
     if layout == "random":
         slots = torch.randperm(64 * bs, device=DEV)[:T]
     else:
-        slots = torch.arange(T, device=DEV) + 5
+        slots = torch.arange(T, device=DEV) + (5 if layout == "contig" else bs)
     slots[3] = -1
     cs = ref.rope_cos_sin(D, 4096, 500000.0).to(DEV)
     kc, vc = _caches(64, nkv, bs, D, fill=False)
