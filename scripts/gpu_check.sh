@@ -114,6 +114,9 @@ for s in $steps; do
     gguf64) timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64.log; [ $rc -eq 0 ] ;;
     gguf64v2) HIPSERVE_QGEMM_M64=2 timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64_v2.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64_v2.log; [ $rc -eq 0 ] ;;
     qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
+    attnpmc) for S in 1024 32768; do
+          PMC_PY=tools/attn_pmc.py PG_SHAPE=$S bash scripts/pg_pmc.sh > $OUT/attn_pmc_$S.log 2>&1 || { tail -5 $OUT/attn_pmc_$S.log; exit 1; }
+          tail -n 9 $OUT/attn_pmc_$S.log; done ;;
     rope) timeout -k 10 180 python -u tools/bench_rope.py > $OUT/bench_rope.log 2>&1 && \
           HIPSERVE_ROPE_VFAST=0 timeout -k 10 180 python -u tools/bench_rope.py > $OUT/bench_rope_v0.log 2>&1; rc=$?
           cat $OUT/bench_rope.log $OUT/bench_rope_v0.log; [ $rc -eq 0 ] ;;
