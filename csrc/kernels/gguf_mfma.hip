@@ -1122,8 +1122,7 @@ void qpg_launch(int epi, QfArgs A, hipStream_t s) {
 }
 
 // x [M, K] bf16 -> x16 [M, K] f16 in the pair order {0, 2, 1, 3, 4, 6, 5, 7} of every
-// aligned 8-run, each row scaled by 2^-k (k >= 0, the smallest keeping max |x| below
-// 2^15), rsc[m] = 2^k: the prefill GEMM's operand, converted once per activation instead
+// aligned 8-run, each row scaled by 2^-k (max |x| 2^-k in [2^14, 2^15)), rsc[m] = 2^k: the prefill GEMM's operand, converted once per activation instead
 // of in every workgroup; bf16 -> f32 exact, -> f16 round to nearest (values below the f16
 // normal range lose low bits, as in the decode kernel's staging)
 __global__ __launch_bounds__(256) void x_f16_pairs_kernel(unsigned short* __restrict__ x16, float* __restrict__ rsc,
@@ -1143,9 +1142,12 @@ __global__ __launch_bounds__(256) void x_f16_pairs_kernel(unsigned short* __rest
   if ((tid & 63) == 0) red[tid >> 6] = mx;
   __syncthreads();
   mx = max(max(red[0], red[1]), max(red[2], red[3]));
-  // 2^-k with max |x| 2^-k < 2^15 (inf / NaN rows: k = 126, the result stays non-finite)
+  // 2^-k with max |x| 2^-k in [2^14, 2^15): rows of small activations are scaled UP as
+  // well (their elements would otherwise sit in the f16 subnormal range and lose bits);
+  // k >= -100 keeps both 2^k and 2^-k normal floats (all-zero rows); inf / NaN rows:
+  // k = 126, the result stays non-finite
   const int ex = (int)(mx >> 23) - 127;
-  const int k = min(126, max(0, ex - 14));
+  const int k = min(126, max(-100, ex - 14));
   const float down = __builtin_bit_cast(float, (unsigned)(127 - k) << 23);
   if (tid == 0) rsc[row] = __builtin_bit_cast(float, (unsigned)(127 + k) << 23);
   constexpr int ord[8] = {0, 2, 1, 3, 4, 6, 5, 7};

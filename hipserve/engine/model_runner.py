@@ -285,7 +285,12 @@ class ModelRunner:
         per_layer = sum(w.numel() * w.element_size() for w in ws if gemm.packable(*w.shape))
         need = per_layer * len(m.layers)
         free, total = torch.cuda.mem_get_info(self.device)
-        if free - need < (24 << 30) + total // 4:
+        # TP ranks decide together (min over ranks): ranks with different weight layouts
+        # would run different prefill GEMMs and round differently
+        margin = (free - need - (24 << 30) - total // 4) >> 20  # MiB
+        if self.tp.world_size > 1:
+            margin = self.tp.min_int(int(margin))
+        if margin < 0:
             return "memory"
         units = []
         for kind, w in (("plain", lw.wqkv), ("add", lw.wo), ("glu", lw.wgu), ("add", lw.wd)):

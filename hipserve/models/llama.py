@@ -798,6 +798,10 @@ class LlamaModel:
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                 act16 = self._x16(act, lw.wd)
                 op.splitk_glu(act, pt[0], pt[1], gelu, act16)
+            elif isinstance(lw.wgu, gemm.PackedLinear) and lw.wgu.glu:
+                # single weight layout: a GLU-interleaved gate|up has no plain x W^T (decode
+                # graph buckets above 64 rows, GeGLU at any row count)
+                act = gemm.packed_glu(xn, lw.wgu, gelu)
             else:
                 gu = self.linear(xn, lw.wgu)
                 act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)

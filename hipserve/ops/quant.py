@@ -610,6 +610,8 @@ def qprefill_ok(w, M: int, glu: bool = False, timed: bool = True) -> bool:
         ps = w.parts
         if not (len(ps) == 2 and ps[0].kqt == ps[1].kqt and ps[0].N == ps[1].N):
             return False
+    if timed and QPREFILL_MODE == "auto" and M <= QPREFILL_MAX_M:
+        return False  # small chunks: the M-tiled K15 kernel (a 256-token tile would be mostly padding)
     return not (timed and QPREFILL_MODE == "auto" and not QPF_CHOICE.get(_sig(w), True))
 
 
@@ -778,8 +780,8 @@ def make_dense_shadows(weights, device, reserve_bytes: int, gguf: bool = True) -
     weights only with ``gguf`` (the engine passes HIPSERVE_QUANT_SHADOW=1 /
     extra gguf_dense_shadow; default off: a GGUF model's footprint is its blocks, prefill
     reads them through qpg_kernel or a per-call scratch). Returns the bytes added."""
-    if torch.device(device).type != "cuda":
-        return 0
+    if torch.device(device).type != "cuda" or os.environ.get("HIPSERVE_QUANT_SHADOW") == "0":
+        return 0  # HIPSERVE_QUANT_SHADOW=0: no bf16 shadow for any format
     from . import pgemm
     added = 0
     for w in sorted(weights, key=lambda w: -w.N * w.K):
