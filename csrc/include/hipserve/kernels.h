@@ -191,7 +191,7 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
 // prefill_gemm_lds.hip — the same product with both operands staged by LDS-DMA (256 x 256
 // tiles, 8 waves, 4-slot LDS ring); epilogues and grouped mode (256-row m-tiles) as above.
 bool launch_prefill_gemm_lds(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N, int K,
-                             const void* bias, hipStream_t s, const PwGroup* group = nullptr);
+                             const void* bias, hipStream_t s, const PwGroup* group = nullptr, int variant = -1);
 // FP8 (W8A8) form: A = per-token e4m3 activations [M, K] bytes (row scale xs[M]),
 // B = e4m3 weights in the decode kernel's tiled layout (gguf_mfma.hip: [N/16][K/256]
 // [4096 B]) as up to 4 parts stacked along N (each rows % 256 == 0; GLU: part 0 =

@@ -41,13 +41,14 @@
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
+#include <cstdlib>
+
 namespace hipserve {
 
 namespace {
 
 constexpr int PL_T = 512;
 constexpr int PL_SLOT = 32768;  // bytes of one 32-deep K step: X 256 x 32 + W 256 x 32 bf16
-constexpr int PL_NBUF = 4;
 constexpr int PL_WB = 16384;    // W pieces after the X image in a slot
 constexpr int PL_GM = 8;        // m-tiles per tile group (L2 sharing of an XCD's workgroups)
 
@@ -71,9 +72,12 @@ struct PlArgs {
   int M, N, K, tiles_m, tiles_n;
 };
 
-template <int EPI, bool kGroup>
+// NBUF: LDS ring slots (4: 128 KiB, DMA two K steps ahead; 5: all 160 KiB, three ahead);
+// PRIO: s_setprio 1 around each MFMA cluster (cdna_hip_programming.md §5.5 T5)
+template <int EPI, bool kGroup, int NBUF = 4, bool PRIO = false>
 __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void pgl_kernel(PlArgs A) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[PL_NBUF * PL_SLOT];
+  constexpr int LEAD = NBUF - 1;  // K steps in flight ahead of the one being computed
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[NBUF * PL_SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -106,8 +110,8 @@ __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(Wp + (long)wtile * KS * 32768), 0, KS * 65536, 0x00020000);
   const int wvo0 = (2 * (w & 3)) * 8192 + 16 * lane, wvo1 = wvo0 + 8192;
-  auto dma = [&](int q) {  // K step q (< nq) -> ring slot q & 3
-    unsigned char* s = lds + (q & 3) * PL_SLOT + 2 * w * 1024;
+  auto dma = [&](int q) {  // K step q (< nq) -> ring slot q % NBUF
+    unsigned char* s = lds + (q % NBUF) * PL_SLOT + 2 * w * 1024;
     const int xk = q * 64, wk = (q >> 3) * 65536 + (q & 7) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_p)(s), 16, xvo0, xk, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_p)(s + 1024), 16, xvo1, xk, 0, 0);
@@ -122,10 +126,10 @@ __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   const unsigned char* xrd = lds + (128 * wm + xl) * 64 + 16 * ((lane >> 4) ^ ((4 - ((xl >> 2) & 3)) & 3));
   constexpr int RGO[4] = {0, 1, 4, 5};
   auto wfrag = [&](int q, int r) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(wrd + (q & 3) * PL_SLOT + RGO[r] * 1024);
+    return *reinterpret_cast<const bf16x8*>(wrd + (q % NBUF) * PL_SLOT + RGO[r] * 1024);
   };
   auto xfrag = [&](int q, int i) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(xrd + (q & 3) * PL_SLOT + i * 1024);
+    return *reinterpret_cast<const bf16x8*>(xrd + (q % NBUF) * PL_SLOT + i * 1024);
   };
 
   f32x4 acc[4][8];
@@ -134,11 +138,10 @@ __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[r][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: K steps 0, 1, 2 in flight; wait for 0
-  dma(0);
-  dma(1);
-  dma(2);
-  vm_wait<8>();
+  // prologue: K steps 0 .. LEAD - 1 in flight; wait for 0
+#pragma unroll
+  for (int q = 0; q < LEAD; ++q) dma(q);
+  vm_wait<4 * (LEAD - 1)>();
   __builtin_amdgcn_s_barrier();
   bf16x8 wa[4], wb[4], xa[4], xb[4];
 #pragma unroll
@@ -150,21 +153,28 @@ __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     // phase A
 #pragma unroll
     for (int i = 0; i < 4; ++i) xb[i] = xfrag(q, 4 + i);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[r][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[r], xa[i], acc[r][i], 0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     // phase B
     if (q + 1 < nq) {
-      if (q + 2 < nq)
-        vm_wait<4>();  // own DMA of step q + 1 landed; step q + 2's still in flight
+      // own DMA of step q + 1 landed; the steps after it already issued (up to
+      // q + LEAD - 1) stay in flight
+      const int ahead = min(LEAD - 2, nq - 2 - q);
+      if (ahead >= 2)
+        vm_wait<8>();
+      else if (ahead == 1)
+        vm_wait<4>();
       else
         vm_wait<0>();
       // every LDS read this wave issued has returned before any wave may refill a slot
       // (hipcc may sink MFMAs, and with them their lgkmcnt waits, below the barrier)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (q + 3 < nq) dma(q + 3);
+      if (q + LEAD < nq) dma(q + LEAD);
     }
     // unconditional (after the last step: a stale, unused read): a branch around these
     // reads made hipcc's lgkmcnt waits for the phase-B fragments count only the short path
@@ -172,11 +182,13 @@ __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     for (int r = 0; r < 4; ++r) wnx[r] = wfrag(q + 1, r);
 #pragma unroll
     for (int i = 0; i < 4; ++i) xa[i] = xfrag(q + 1, i);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         acc[r][4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[r], xb[i], acc[r][4 + i], 0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
   for (int q = 0; q < nq; q += 2) {  // nq % 8 == 0
     step(q, wa, wb);
@@ -238,8 +250,19 @@ __global__ __launch_bounds__(PL_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 
 }  // namespace
 
+// variant (A/B measurement; < 0: HIPSERVE_PGL_VAR, default 0): bit 0 = 5-slot ring, bit 1 = setprio
+static int pgl_variant(int v) {
+  if (v >= 0) return v;
+  static const int e = [] {
+    const char* s = getenv("HIPSERVE_PGL_VAR");
+    return s ? atoi(s) : 0;
+  }();
+  return e;
+}
+
 bool launch_prefill_gemm_lds(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N, int K,
-                             const void* bias, hipStream_t s, const PwGroup* group) {
+                             const void* bias, hipStream_t s, const PwGroup* group, int variant) {
+  variant = pgl_variant(variant) & 3;
   const bool grouped = group != nullptr;
   if (M < 1 || N < 1 || K < 256 || K % 256) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
@@ -265,12 +288,21 @@ bool launch_prefill_gemm_lds(int epi, void* C, long ldc, const void* X, long ldx
   a.tiles_m = (M + 255) / 256;
   a.tiles_n = ((N + 127) / 128 + 1) / 2;
   const dim3 grid(a.tiles_m * a.tiles_n), block(PL_T);
-#define PL_LAUNCH(E_)                                                    \
-  do {                                                                   \
-    if (grouped)                                                         \
-      pgl_kernel<E_, true><<<grid, block, 0, s>>>(a);                    \
-    else                                                                 \
-      pgl_kernel<E_, false><<<grid, block, 0, s>>>(a);                   \
+#define PL_LAUNCH2(E_, G_)                                                  \
+  do {                                                                      \
+    switch (variant) {                                                      \
+      case 0: pgl_kernel<E_, G_, 4, false><<<grid, block, 0, s>>>(a); break; \
+      case 1: pgl_kernel<E_, G_, 5, false><<<grid, block, 0, s>>>(a); break; \
+      case 2: pgl_kernel<E_, G_, 4, true><<<grid, block, 0, s>>>(a); break;  \
+      default: pgl_kernel<E_, G_, 5, true><<<grid, block, 0, s>>>(a); break; \
+    }                                                                       \
+  } while (0)
+#define PL_LAUNCH(E_)          \
+  do {                         \
+    if (grouped)               \
+      PL_LAUNCH2(E_, true);    \
+    else                       \
+      PL_LAUNCH2(E_, false);   \
   } while (0)
   switch (epi) {
     case PW_EPI_STORE: PL_LAUNCH(PW_EPI_STORE); return true;
@@ -279,6 +311,7 @@ bool launch_prefill_gemm_lds(int epi, void* C, long ldc, const void* X, long ldx
     case PW_EPI_GEGLU: PL_LAUNCH(PW_EPI_GEGLU); return true;
   }
 #undef PL_LAUNCH
+#undef PL_LAUNCH2
   return false;
 }
 

@@ -796,7 +796,7 @@ void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at:
 // num_tiles are given (x = expert-sorted slots in 256-row tiles, wp = [E, packed]).
 void prefill_gemm_lds(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
                       const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& tile_expert,
-                      const c10::optional<at::Tensor>& num_tiles) {
+                      const c10::optional<at::Tensor>& num_tiles, int64_t variant) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(wp.is_contiguous(), "prefill_gemm_lds: packed weight must be contiguous");
   const int M = x.size(0), K = x.size(1);
@@ -823,7 +823,8 @@ void prefill_gemm_lds(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_prefill_gemm_lds((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
-                                                wp.data_ptr(), M, (int)N, K, bp, cur_stream(), grouped ? &grp : nullptr),
+                                                wp.data_ptr(), M, (int)N, K, bp, cur_stream(), grouped ? &grp : nullptr,
+                                                (int)variant),
               "prefill_gemm_lds: unsupported (glu needs N % 128, bias only with epi 0, 32-bit offsets)");
 }
 
@@ -1298,7 +1299,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
-  m.def("prefill_gemm_lds(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, Tensor? tile_expert=None, Tensor? num_tiles=None) -> ()");
+  m.def("prefill_gemm_lds(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, Tensor? tile_expert=None, Tensor? num_tiles=None, int variant=-1) -> ()");
   m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");

@@ -35,12 +35,13 @@ SHAPES = [(256, 256, 256), (300, 640, 1024), (1000, 200, 512), (77, 1536, 768), 
           (1, 128, 256), (8192, 512, 4096), (513, 4096, 14336)]
 
 
+@pytest.mark.parametrize("var", [0, 1, 2, 3])  # LDS ring 4 / 5 slots, setprio off / on
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_lds_store(M, N, K):
+def test_lds_store(M, N, K, var):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
     out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm_lds(out, x, _pack(w), N, 0)
+    torch.ops.hipserve.prefill_gemm_lds(out, x, _pack(w), N, 0, variant=var)
     want = x.float() @ w.float().t()
     torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 
@@ -94,17 +95,18 @@ def test_lds_glu(M, I, K, act):
     torch.testing.assert_close(out.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
 
 
-def test_lds_repeat_is_deterministic():
+@pytest.mark.parametrize("var", [0, 1, 2, 3])
+def test_lds_repeat_is_deterministic(var):
     """Back-to-back launches give bit-identical outputs (a DMA / read race would show as
-    rare differing tiles)."""
+    rare differing tiles), the same in every ring / priority variant."""
     g = torch.Generator(device=DEV).manual_seed(21)
     M, N, K = 4096, 2048, 2048
     x, wp = _rnd(g, M, K), _pack(_rnd(g, N, K, scale=0.05))
     ref = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm_lds(ref, x, wp, N, 0)
+    torch.ops.hipserve.prefill_gemm_lds(ref, x, wp, N, 0, variant=0)
     out = torch.empty_like(ref)
     for _ in range(20):
-        torch.ops.hipserve.prefill_gemm_lds(out, x, wp, N, 0)
+        torch.ops.hipserve.prefill_gemm_lds(out, x, wp, N, 0, variant=var)
         assert torch.equal(out, ref)
 
 

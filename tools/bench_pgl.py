@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--model", default="8b")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-old", action="store_true")
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
     a = ap.parse_args()
     load_library()
     op = torch.ops.hipserve
@@ -74,10 +75,12 @@ def main():
                     op.prefill_gemm_packed(res if res is not None else out, x, wps[i % ncopy], N, epi, None, 1,
                                            1 << 30, 4)
 
-                def new(i):
-                    op.prefill_gemm_lds(res if res is not None else out, x, wps[i % ncopy], N, epi)
+                def new(i, v=0):
+                    op.prefill_gemm_lds(res if res is not None else out, x, wps[i % ncopy], N, epi, variant=v)
 
-                arms = {"blas": blas, "lds": new}
+                arms = {"blas": blas}
+                for v in a.variants:
+                    arms[f"lds{v}"] = lambda i, v=v: new(i, v)
                 if not a.no_old:
                     arms["packed"] = old
                 for f in arms.values():
