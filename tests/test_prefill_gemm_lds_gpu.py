@@ -35,7 +35,7 @@ SHAPES = [(256, 256, 256), (300, 640, 1024), (1000, 200, 512), (77, 1536, 768), 
           (1, 128, 256), (8192, 512, 4096), (513, 4096, 14336)]
 
 
-@pytest.mark.parametrize("var", [0, 1, 2, 3])  # LDS ring 4 / 5 slots, setprio off / on
+@pytest.mark.parametrize("var", [0, 1, 2, 3, 4])  # 8 waves: ring 4 / 5 slots, setprio off / on; 4: 4 waves
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_lds_store(M, N, K, var):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
@@ -55,6 +55,9 @@ def test_lds_identity_asymmetric():
     out = torch.full((256, N), float("nan"), device=DEV, dtype=torch.bfloat16)
     torch.ops.hipserve.prefill_gemm_lds(out, x, _pack(w), N, 0)
     assert torch.equal(out, w.t()[:256].contiguous())
+    out.fill_(float("nan"))
+    torch.ops.hipserve.prefill_gemm_lds(out, x, _pack(w), N, 0, variant=4)
+    assert torch.equal(out, w.t()[:256].contiguous())
 
 
 def test_lds_store_bias_and_strided_x():
@@ -69,33 +72,35 @@ def test_lds_store_bias_and_strided_x():
     torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 
 
+@pytest.mark.parametrize("var", [0, 4])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 1024), (1000, 384, 512), (2049, 1024, 256), (8192, 4096, 4096)])
-def test_lds_residual_add(M, N, K):
+def test_lds_residual_add(M, N, K, var):
     g = torch.Generator(device=DEV).manual_seed(7 + M)
     x, w = _rnd(g, M, K), _rnd(g, N, K, scale=0.05)
     res0 = _rnd(g, M, N)
     res = res0.clone()
-    torch.ops.hipserve.prefill_gemm_lds(res, x, _pack(w), N, 1)
+    torch.ops.hipserve.prefill_gemm_lds(res, x, _pack(w), N, 1, variant=var)
     h = (x.float() @ w.float().t()).to(torch.bfloat16).float()
     want = (h + res0.float()).to(torch.bfloat16).float()
     torch.testing.assert_close(res.float(), want, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("var", [0, 4])
 @pytest.mark.parametrize("act", ["silu", "gelu"])
 @pytest.mark.parametrize("M,I,K", [(300, 256, 1024), (1000, 192, 512), (2049, 64, 256), (513, 1344, 768),
                                    (4096, 14336, 4096)])
-def test_lds_glu(M, I, K, act):
+def test_lds_glu(M, I, K, act, var):
     g = torch.Generator(device=DEV).manual_seed(11 + M)
     x, w = _rnd(g, M, K), _rnd(g, 2 * I, K, scale=0.05)
     out = torch.full((M, I), float("nan"), device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.prefill_gemm_lds(out, x, _pack(w, glu=True), 2 * I, 2 if act == "silu" else 3)
+    torch.ops.hipserve.prefill_gemm_lds(out, x, _pack(w, glu=True), 2 * I, 2 if act == "silu" else 3, variant=var)
     gu = (x.float() @ w.float().t()).to(torch.bfloat16).float()
     f = torch.nn.functional.silu if act == "silu" else (lambda t: torch.nn.functional.gelu(t, approximate="tanh"))
     want = f(gu[:, :I]) * gu[:, I:]
     torch.testing.assert_close(out.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
 
 
-@pytest.mark.parametrize("var", [0, 1, 2, 3])
+@pytest.mark.parametrize("var", [0, 1, 2, 3, 4])
 def test_lds_repeat_is_deterministic(var):
     """Back-to-back launches give bit-identical outputs (a DMA / read race would show as
     rare differing tiles), the same in every ring / priority variant."""
@@ -110,8 +115,9 @@ def test_lds_repeat_is_deterministic(var):
         assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("var", [0, 4])
 @pytest.mark.parametrize("E,I,K,glu", [(8, 512, 1024, True), (8, 256, 512, False), (16, 128, 256, True)])
-def test_lds_grouped_moe(E, I, K, glu):
+def test_lds_grouped_moe(E, I, K, glu, var):
     """Grouped expert GEMM over moe_align's expert-sorted 256-row tiles with each expert's
     weight in the packed decode layout, the valid tile count read on the device, vs a
     per-expert fp32 reference."""
@@ -134,7 +140,7 @@ def test_lds_grouped_moe(E, I, K, glu):
     xs = torch.empty(cap, K, dtype=torch.bfloat16, device=DEV)
     op.moe_gather(xs, x, slots, k)
     out = torch.full((cap, I), float("nan"), device=DEV, dtype=torch.bfloat16)
-    op.prefill_gemm_lds(out, xs, wp, N, 2 if glu else 0, None, tile_expert, ntiles)
+    op.prefill_gemm_lds(out, xs, wp, N, 2 if glu else 0, None, tile_expert, ntiles, var)
     ps = pair_slot.long()
     for p in range(0, P, 37):  # a spread of pairs
         t, j = p // k, p % k

@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--model", default="8b")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-old", action="store_true")
-    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 4])
     a = ap.parse_args()
     load_library()
     op = torch.ops.hipserve
