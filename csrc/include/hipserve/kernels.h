@@ -100,6 +100,12 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16 = nullptr);
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s);
+// gguf_decode.hip — the v3 decode GEMM (both operands by LDS-DMA) on x16; same outputs as
+// launch_gguf_gemm_parts. false if it does not take the shape (the caller runs v2).
+// HIPSERVE_QGEMM3=0 disables it (qgemm3_enabled).
+bool qgemm3_enabled();
+bool launch_qgemm3(void* out, long out_stride, float* ws, const void* x, const void* x16, long ldx,
+                   const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s);
 // prefill GEMM straight from the tiled GGUF blocks on launch_x_f16_pairs' x16 / rsc (epi:
 // PW_EPI_STORE / ADD / GLU / GEGLU; GLU: parts 0 / 1 = gate / up); false if the formats /
 // shapes are not taken

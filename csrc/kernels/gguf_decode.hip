@@ -128,7 +128,7 @@ struct Q3Args {
 };
 
 template <int QT, int MT>
-__global__ __launch_bounds__(64 * q3_nw<QT, MT>()) void qgemm3_kernel(Q3Args A) {
+__global__ __launch_bounds__((64 * q3_nw<QT, MT>())) void qgemm3_kernel(Q3Args A) {
   constexpr int NW = q3_nw<QT, MT>(), CB = chunk_bytes<QT>(), SLOT = q3_slot<QT, MT>();
   constexpr int XB = MT * 16 * 512;           // x image bytes of a slot
   constexpr int XI = XB / 1024;               // x DMA instructions per slot
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(64 * q3_nw<QT, MT>()) void qgemm3_kernel(Q3Args A) 
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(acc[t][e]);
-  if (__builtin_amdgcn_read_exec() != 0 && __any(bad))  // per wave: only this wave's rows
+  if (__any(bad))  // per wave: this wave's rows
     q3_slow<QT, MT>(acc, A.x, A.ldx, M, P.q + (long)gl * nsb * CB, nsb, sb0, sb1);
 
   if (gi >= ngroups) return;
