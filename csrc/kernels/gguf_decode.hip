@@ -127,14 +127,24 @@ struct Q3Args {
   int M, Ntot, K, per;  // per: super-chunks per K split
 };
 
+// compile-time geometry of one (format, row tile) instantiation. (The DMA lambda computes
+// its per-lane x offsets inline: with them precomputed into local int arrays read inside
+// the lambda, hipcc (ROCm 7.2) silently emitted no host stub for the kernel.)
 template <int QT, int MT>
-__global__ __launch_bounds__((64 * q3_nw<QT, MT>())) void qgemm3_kernel(Q3Args A) {
-  constexpr int NW = q3_nw<QT, MT>(), CB = chunk_bytes<QT>(), SLOT = q3_slot<QT, MT>();
-  constexpr int XB = MT * 16 * 512;           // x image bytes of a slot
-  constexpr int XI = XB / 1024;               // x DMA instructions per slot
-  constexpr int NXW = (XI + NW - 1) / NW;     // ... per wave (the last ones may repeat a piece)
-  constexpr int N4 = CB / 1024, N1 = (CB % 1024) / 256, TAIL = CB % 256;
-  constexpr int NDMA = NXW + N4 + N1 + (TAIL ? 1 : 0);  // DMA instructions per wave and slot
+struct Q3G {
+  static constexpr int NW = q3_nw<QT, MT>(), CB = chunk_bytes<QT>(), SLOT = q3_slot<QT, MT>();
+  static constexpr int XB = MT * 16 * 512;           // x image bytes of a slot
+  static constexpr int XI = XB / 1024;               // x DMA instructions per slot
+  static constexpr int NXW = (XI + NW - 1) / NW;     // ... per wave (the last ones may repeat a piece)
+  static constexpr int N4 = CB / 1024, N1 = (CB % 1024) / 256, TAIL = CB % 256;
+  static constexpr int NDMA = NXW + N4 + N1 + (TAIL ? 1 : 0);  // DMA instructions per wave and slot
+};
+
+template <int QT, int MT, int NT>
+__global__ __launch_bounds__(NT) void qgemm3_kernel(Q3Args A) {
+  using C_ = Q3G<QT, MT>;
+  constexpr int NW = C_::NW, CB = C_::CB, SLOT = C_::SLOT, XB = C_::XB, XI = C_::XI, NXW = C_::NXW;
+  constexpr int NDMA = C_::NDMA;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Q3_NSLOT * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -154,35 +164,33 @@ __global__ __launch_bounds__((64 * q3_nw<QT, MT>())) void qgemm3_kernel(Q3Args A
   // ---- DMA sources
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)A.x16, 0, (int)((long)M * A.ldx * 2), 0x00020000);
-  int xvo[NXW], xdst[NXW];
-#pragma unroll
-  for (int i = 0; i < NXW; ++i) {
-    const int j = min(w + NW * i, XI - 1);  // 1 KiB piece = x rows 2 j, 2 j + 1
-    const int m = 2 * j + (lane >> 5), jl = (lane & 31) ^ q3_swz(m & 15, q3_d<QT>());
-    xvo[i] = m * (int)A.ldx * 2 + jl * 16;
-    xdst[i] = __builtin_amdgcn_readfirstlane(j * 1024);
-  }
+  const int ldx2 = (int)A.ldx * 2;
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc((void*)P.q, 0, ngroups * nsb * CB, 0x00020000);
   const int wbase = gl * nsb * CB;  // byte offset of this wave's row group
   auto dma = [&](int sb, int slot) {
-    unsigned char* s = lds + slot * SLOT;
+    unsigned char* s = lds + slot * C_::SLOT;
 #pragma unroll
-    for (int i = 0; i < NXW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_p)(s + xdst[i]), 16, xvo[i], sb * 512, 0, 0);
-    unsigned char* d = s + XB + w * CB;
-    const int so = wbase + sb * CB;
+    for (int i = 0; i < C_::NXW; ++i) {
+      // 1 KiB piece j = x rows 2 j, 2 j + 1 (the last waves may repeat piece XI - 1);
+      // lane -> row m, LDS chunk lane & 31 holding x chunk (lane & 31) ^ f(m & 15)
+      const int j = min(w + C_::NW * i, C_::XI - 1);
+      const int m = 2 * j + (lane >> 5), jl = (lane & 31) ^ q3_swz(m & 15, q3_d<QT>());
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_p)(s + j * 1024), 16, m * ldx2 + jl * 16, sb * 512, 0, 0);
+    }
+    unsigned char* d = s + C_::XB + w * C_::CB;
+    const int so = wbase + sb * C_::CB;
 #pragma unroll
-    for (int n = 0; n < N4; ++n)
+    for (int n = 0; n < C_::N4; ++n)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * n), 16, lane * 16 + 1024 * n, so, 0, 0);
 #pragma unroll
-    for (int n = 0; n < N1; ++n)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * N4 + 256 * n), 4,
-                                               lane * 4 + 1024 * N4 + 256 * n, so, 0, 0);
-    if constexpr (TAIL > 0) {
-      if (lane < TAIL / 4)  // lanes 0 .. TAIL/4 - 1 are active in every wave: always issued
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * N4 + 256 * N1), 4,
-                                                 lane * 4 + 1024 * N4 + 256 * N1, so, 0, 0);
+    for (int n = 0; n < C_::N1; ++n)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * C_::N4 + 256 * n), 4,
+                                               lane * 4 + 1024 * C_::N4 + 256 * n, so, 0, 0);
+    if constexpr (C_::TAIL > 0) {
+      if (lane < C_::TAIL / 4)  // lanes 0 .. TAIL/4 - 1 are active in every wave: always issued
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * C_::N4 + 256 * C_::N1), 4,
+                                                 lane * 4 + 1024 * C_::N4 + 256 * C_::N1, so, 0, 0);
     }
   };
 
@@ -258,7 +266,8 @@ __global__ __launch_bounds__((64 * q3_nw<QT, MT>())) void qgemm3_kernel(Q3Args A
 
 template <int QT, int MT>
 void q3_launch(const Q3Args& a, int tiles, int S, hipStream_t s) {
-  qgemm3_kernel<QT, MT><<<dim3(tiles, S), 64 * q3_nw<QT, MT>(), 0, s>>>(a);
+  constexpr int NT = 64 * q3_nw<QT, MT>();
+  qgemm3_kernel<QT, MT, NT><<<dim3(tiles, S), NT, 0, s>>>(a);
 }
 
 template <int QT>
