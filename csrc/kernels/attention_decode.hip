@@ -30,6 +30,14 @@ constexpr int kDecWavesMax = 8;
 constexpr int kChunk = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 
+// out16 (optional): an f16 copy of the bf16 output in the quantised decode GEMMs' staging
+// pair order {0, 2, 1, 3, 4, 6, 5, 7} per aligned 8-run — the o-projection's x16 operand
+// (gguf_decode.hip), written here instead of by a conversion kernel
+HS_DEVICE void store_o16(unsigned short* __restrict__ out16, long row_off, int e, unsigned short bf) {
+  const int p = (e & ~7) | (e & 4) | ((e & 1) << 1) | ((e >> 1) & 1);
+  out16[row_off + p] = __builtin_bit_cast(unsigned short, static_cast<_Float16>(bf16_to_f32(bf)));
+}
+
 // Fused decode input (kQKV): the qkv projection's fp32 split-K partials instead of a
 // bf16 q row. The kernel sums them, applies RoPE to q (and to the new token's k),
 // writes the new token's k / v into the paged cache and attends — replacing the
@@ -69,7 +77,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int nq, int nkv, int block_size, int part_size,
-    int max_parts, float scale, int window, QkvIn qi = QkvIn{}) {
+    int max_parts, float scale, int window, QkvIn qi = QkvIn{}, unsigned short* __restrict__ out16 = nullptr) {
   static_assert(D == 128 || D == 96 || D == 64, "head_dim 64, 96 or 128");
   constexpr int KS = D / 32;  // k-steps of the QK MFMA
   constexpr int NB = D / 16;  // 16-column blocks of the PV output
@@ -381,7 +389,9 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     }
     const int hq = kh * G + h;
     if (nparts_seq == 1) {
-      out[(long)b * out_stride + (long)hq * D + d] = f32_to_bf16(acc / L);
+      const unsigned short ob = f32_to_bf16(acc / L);
+      out[(long)b * out_stride + (long)hq * D + d] = ob;
+      if (out16 != nullptr) store_o16(out16, (long)b * out_stride, hq * D + d, ob);
     } else {
       const long base = ((long)b * nq + hq) * max_parts + part;
       tmp_out[base * D + d] = acc / L;
@@ -406,7 +416,8 @@ template <int D>
 __global__ __launch_bounds__(512) void paged_decode_reduce_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
-    const int* __restrict__ context_lens, int nq, int part_size, int max_parts, int window) {
+    const int* __restrict__ context_lens, int nq, int part_size, int max_parts, int window,
+    unsigned short* __restrict__ out16 = nullptr) {
   constexpr int G = reduce_groups<D>();
   static_assert(G * D % 64 == 0, "whole waves");
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -452,7 +463,9 @@ __global__ __launch_bounds__(512) void paged_decode_reduce_kernel(
       a += red[g * D + d];
       l += red[G * D + g];
     }
-    out[(long)b * out_stride + (long)h * D + d] = f32_to_bf16(a / l);
+    const unsigned short ob = f32_to_bf16(a / l);
+    out[(long)b * out_stride + (long)h * D + d] = ob;
+    if (out16 != nullptr) store_o16(out16, (long)b * out_stride, h * D + d, ob);
   }
 }
 
@@ -493,8 +506,9 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
                          const int* context_lens, float* tmp_out, float* tmp_ml,
                          int B, int nq, int nkv, int D, int block_size,
                          int part_size, int max_parts, float scale, int window,
-                         hipStream_t s) {
+                         hipStream_t s, void* out16) {
   if (B <= 0) return;
+  auto* o16 = static_cast<unsigned short*>(out16);
   const int waves = decode_waves();
   dim3 grid(max_parts, nkv, B), block(64 * waves);
   const size_t smem = smem_bytes(D, waves);
@@ -507,11 +521,11 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
     if (decode_nt((long)max_parts * nkv * B))                                                               \
       paged_decode_kernel<DD, WW, false, true><<<grid, block, smem, s>>>(                                   \
           o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq,  \
-          nkv, block_size, part_size, max_parts, scale, window);                                            \
+          nkv, block_size, part_size, max_parts, scale, window, QkvIn{}, o16);                              \
     else                                                                                                    \
       paged_decode_kernel<DD, WW, false, false><<<grid, block, smem, s>>>(                                  \
           o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq,  \
-          nkv, block_size, part_size, max_parts, scale, window);                                            \
+          nkv, block_size, part_size, max_parts, scale, window, QkvIn{}, o16);                              \
   } while (0)
 #define HS_DECODE_D(DD)                                                                                      \
   do {                                                                                                      \
@@ -520,7 +534,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
     if (max_parts > 1)                                                                                      \
       paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(reduce_groups<DD>() * DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml, \
                                                                        context_lens, nq, part_size, max_parts, \
-                                                                       window);                             \
+                                                                       window, o16);                        \
   } while (0)
   if (D == 128) HS_DECODE_D(128);
   else if (D == 96) HS_DECODE_D(96);
@@ -534,8 +548,9 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
                              const long* slots, const float* cos_sin, int mode, void* k_cache, void* v_cache,
                              const int* block_tables, int bt_stride, const int* context_lens, float* tmp_out,
                              float* tmp_ml, int B, int nq, int nkv, int D, int block_size, int part_size,
-                             int max_parts, float scale, int window, hipStream_t s) {
+                             int max_parts, float scale, int window, hipStream_t s, void* out16) {
   if (B <= 0) return;
+  auto* o16 = static_cast<unsigned short*>(out16);
   const int waves = decode_waves();
   dim3 grid(max_parts, nkv, B), block(64 * waves);
   const size_t smem = smem_bytes(D, waves);
@@ -548,11 +563,11 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
     if (decode_nt((long)max_parts * nkv * B))                                                                 \
       paged_decode_kernel<DD, WW, true, true><<<grid, block, smem, s>>>(                                      \
           o, out_stride, nullptr, 0, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, \
-          block_size, part_size, max_parts, scale, window, qi);                                               \
+          block_size, part_size, max_parts, scale, window, qi, o16);                                          \
     else                                                                                                      \
       paged_decode_kernel<DD, WW, true, false><<<grid, block, smem, s>>>(                                     \
           o, out_stride, nullptr, 0, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, nkv, \
-          block_size, part_size, max_parts, scale, window, qi);                                               \
+          block_size, part_size, max_parts, scale, window, qi, o16);                                          \
   } while (0)
 #define HS_DECODE_QKV_D(DD)                                                                                   \
   do {                                                                                                        \
@@ -561,7 +576,7 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
     if (max_parts > 1)                                                                                        \
       paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(reduce_groups<DD>() * DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,   \
                                                                        context_lens, nq, part_size, max_parts,   \
-                                                                       window);                               \
+                                                                       window, o16);                          \
   } while (0)
   if (D == 128) HS_DECODE_QKV_D(128);
   else HS_DECODE_QKV_D(64);

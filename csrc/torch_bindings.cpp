@@ -112,10 +112,20 @@ void rope_cache(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& 
                               head_dim, k_cache.size(2), mode, cur_stream());
 }
 
+// the f16 pair-order copy of a bf16 [B, >= nq D] output (same shape and row stride) or null
+static void* out16_ptr(const c10::optional<at::Tensor>& out16, const at::Tensor& out) {
+  if (!out16.has_value() || !out16->defined()) return nullptr;
+  TORCH_CHECK(out16->scalar_type() == at::kHalf && out16->device() == out.device() && out16->size(0) == out.size(0) &&
+                  out16->size(1) == out.size(1) && out16->stride(0) == out.stride(0) && out16->stride(1) == 1,
+              "out16: f16 with out's shape and row stride");
+  return out16->data_ptr();
+}
+
 void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
                   const at::Tensor& v_cache, const at::Tensor& block_tables,
                   const at::Tensor& context_lens, at::Tensor& tmp_out, at::Tensor& tmp_ml,
-                  int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window) {
+                  int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window,
+                  const c10::optional<at::Tensor>& out16) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_ROWMAJOR(q); CHECK_ROWMAJOR(out);
   const int D = k_cache.size(3), bs = k_cache.size(2);
   TORCH_CHECK(D == 64 || D == 96 || D == 128, "paged_decode: head_dim 64/96/128");
@@ -138,14 +148,14 @@ void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cach
                                 block_tables.data_ptr<int>(), block_tables.stride(0),
                                 context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
                                 tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size,
-                                max_parts, (float)scale, (int)window, cur_stream());
+                                max_parts, (float)scale, (int)window, cur_stream(), out16_ptr(out16, out));
 }
 
 void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
                       const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
                       const at::Tensor& block_tables, const at::Tensor& context_lens, at::Tensor& tmp_out,
                       at::Tensor& tmp_ml, int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window,
-                      int64_t mode) {
+                      int64_t mode, const c10::optional<at::Tensor>& out16) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   const int D = k_cache.size(3), bs = k_cache.size(2);
   TORCH_CHECK(D == 64 || D == 128, "paged_decode_qkv: head_dim 64/128");
@@ -175,7 +185,7 @@ void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, con
                                     mode, k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                     block_tables.stride(0), context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
                                     tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size, max_parts, (float)scale,
-                                    (int)window, cur_stream());
+                                    (int)window, cur_stream(), out16_ptr(out16, out));
 }
 
 void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
@@ -1269,7 +1279,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps, Tensor(c!)? out8=None, Tensor(d!)? xs8=None) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");
-  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale, int window=0) -> ()");
+  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor context_lens, Tensor(b!) tmp_out, Tensor(c!) tmp_ml, int nq, int nkv, int part_size, float scale, int window=0, Tensor(d!)? out16=None) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q, Tensor ctx_lens, Tensor tiles, int nq, int nkv, float scale, int window=0) -> ()");
   m.def("qk_rmsnorm(Tensor(a!) qkv, Tensor q_w, Tensor k_w, int nq, int nkv, int head_dim, float eps) -> ()");
   m.def("gelu_and_mul(Tensor(a!) out, Tensor x) -> ()");
@@ -1310,7 +1320,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
-  m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode) -> ()");
+  m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode, Tensor(f!)? out16=None) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode, Tensor? bias=None, Tensor? q_w=None, Tensor? k_w=None, float eps=1e-6) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");

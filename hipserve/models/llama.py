@@ -749,11 +749,12 @@ class LlamaModel:
             win = cfg.window_of(i)
             cs = self.cos_sin_local if win else self.cos_sin
             pt = self._partial(xn, lw.wqkv, xn16, xn8)
+            attn16 = self._x16(attn, lw.wo)  # the attention's f16 pair-order copy for a quantised o_proj
             if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras and not win:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
                                     meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part, self.scale,
-                                    0, cfg.rope_mode)
+                                    0, cfg.rope_mode, attn16)
             elif pt is not None:  # + q/k/v bias and per-head q/k RMSNorm of the family, if any
                 ws, S = pt
                 qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)
@@ -769,8 +770,8 @@ class LlamaModel:
                                cfg.rope_mode)
             if pt is None or not (self.fused_qkv_attention and D in (64, 128) and not extras and not win):
                 ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
-                                 nq, nkv, part, self.scale, win)
-            pt = self._partial(attn, lw.wo)
+                                 nq, nkv, part, self.scale, win, attn16)
+            pt = self._partial(attn, lw.wo, attn16)
             if lw.post_attn_norm is not None:  # Gemma sandwich norm
                 xn16 = self._x16(xn, lw.wgu) if pt is not None else None
                 xn8 = self._x8(xn, lw.wgu) if pt is not None else None

@@ -88,9 +88,9 @@ class KernelOps:
         self._op.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
 
     def paged_decode(self, out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
-                     nq, nkv, part_size, scale, window=0):
+                     nq, nkv, part_size, scale, window=0, out16=None):
         self._op.paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
-                              nq, nkv, part_size, scale, window)
+                              nq, nkv, part_size, scale, window, out16)
         return out
 
     def prefill_attention(self, out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tiles,
@@ -178,7 +178,7 @@ class ReferenceOps:
         ref.rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode)
 
     def paged_decode(self, out, q, k_cache, v_cache, block_tables, context_lens, tmp_out, tmp_ml,
-                     nq, nkv, part_size, scale, window=0):
+                     nq, nkv, part_size, scale, window=0, out16=None):
         B = context_lens.shape[0]
         D = k_cache.shape[3]
         out[:B, : nq * D].copy_(ref.paged_decode(q, k_cache, v_cache, block_tables, context_lens,

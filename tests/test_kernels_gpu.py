@@ -106,9 +106,14 @@ def test_paged_decode(ops, nq, nkv, D, bs, part, window):
     tmp_ml = torch.empty(B, nq, max_parts, 2, device=DEV, dtype=torch.float32)
     out = torch.zeros(B, nq * D, device=DEV, dtype=torch.bfloat16)
     scale = 1.0 / math.sqrt(D)
-    ops.paged_decode(out, q, kc, vc, bt, cl, tmp_out, tmp_ml, nq, nkv, part, scale, window)
+    out16 = torch.full((B, nq * D), float("nan"), device=DEV, dtype=torch.float16)
+    ops.paged_decode(out, q, kc, vc, bt, cl, tmp_out, tmp_ml, nq, nkv, part, scale, window, out16)
     want = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), nq, nkv, scale, window)
     _close(out.view(B, nq, D), want, atol=2e-2, rtol=2e-2)
+    # out16: the f16 pair-order copy {0, 2, 1, 3, 4, 6, 5, 7} of the bf16 output, exactly
+    # (one- and multi-partition sequences: the attention and the merge kernel write it)
+    h = out.float().to(torch.float16).view(B, -1, 8)[:, :, [0, 2, 1, 3, 4, 6, 5, 7]].reshape(B, -1)
+    assert torch.equal(out16, h)
 
 
 @pytest.mark.parametrize("nq,nkv,D,bs,v1", [(32, 8, 128, 16, False), (32, 8, 128, 16, True), (64, 8, 128, 16, False),
