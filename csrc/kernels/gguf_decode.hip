@@ -1,32 +1,32 @@
 // Quantised decode GEMM v3: y[M, N] = x[M, K] . W^T for M <= 64 with
-// W in the tiled quantised layout (gguf_tiles.h: GGUF Q4_0 .. Q6_K, FP8, INT8), both
-// operands staged by LDS-DMA.
+// W in the tiled quantised layout (gguf_tiles.h: GGUF Q4_0 .. Q6_K, FP8, INT8).
 //
 // Why v2 (gguf_mfma.hip qgemm2_kernel) streamed only 1.1-2.2 TB/s of quantised bytes at
 // M = 64 (profiles/r4_gguf_m64_bodies.log, r2_qgemm_m64_pmc.md: 42 % of wave cycles in
-// s_waitcnt, 11 VALU per MFMA): its weights went global -> VGPR one super-chunk ahead
-// (deeper register rings cost occupancy: r2_qgemm_deep_ring_negative.md) and x was staged
-// through registers. Here:
-//  * a workgroup of NW waves = NW row groups of 16 rows; per 256-deep super-chunk (SC) its
-//    LDS slot holds x (MT * 16 rows x 256 f16, from the producer's f16 pair-order copy
-//    x16) and each wave's raw weight chunk (CB bytes, the tiled chunk exactly as stored);
-//  * a ring of 3 slots: the DMA of SC sb + 2 is issued when SC sb starts, so every
-//    byte has two SCs (~1.3 us) to land without holding a register; in-flight bytes
-//    per CU = two slots (100+ KB);
-//  * a wave reads its chunk with ds_reads at the global layout's offsets (gq::load_raw on
-//    the LDS copy) and dequantises in registers as v2 does (subnormal-integer f16, one
-//    v_pk_fma per pair); x fragments are conflict-free ds_read_b128s: chunk j of row m
-//    sits at chunk j ^ f(m & 15), f(c) = c ^ (((c >> 2) ^ (c >> 3)) & 1) * D with D = the
-//    chunk distance between lane groups 0 and 1 (8; Q6_K: 4), which puts every 16-lane
-//    group of a B-fragment read on 16 distinct 16-byte bank slots;
-//  * one s_barrier per SC (x is shared); the weight half of a slot is private to its wave
-//    (its own vmcnt orders it). Raw s_barrier + counted vmcnt: the DMAs stay in flight.
+// s_waitcnt): every workgroup staged x (64 rows x 256 f16 = 32 KiB per super-chunk, more
+// bytes than its 128 weight rows' blocks) through registers and LDS once per super-chunk,
+// with one super-chunk of weights in flight. A first v3 moved both operands to LDS-DMA
+// rings: the x re-staging then dominated the per-CU DMA path (lm_head 234 vs 138 us).
+// The fix is to stage x ONCE per workgroup:
+//  * split K into S slices of at most XSC super-chunks (x slice <= 128 KiB of LDS); a
+//    persistent grid of one workgroup per CU, S | grid, workgroup b takes slice b % S;
+//  * the workgroup DMAs its x slice (f16, the producer's pair-order copy x16) into LDS
+//    once, one barrier, and from then on its waves never synchronise again: each wave
+//    walks its row groups (16 weight rows, round-robin over the slice's waves) x the
+//    slice's super-chunks as one flat item stream, the raw weight chunk of item i + 3
+//    loading into registers while item i is dequantised (gq::Dec, subnormal-integer
+//    f16) and multiplied (v_mfma_f32_16x16x32_f16) against x fragments read from LDS;
+//  * x fragments are conflict-free ds_read_b128s: 16-byte chunk j of row m sits at
+//    chunk j ^ f(m & 15), f(c) = c ^ (((c >> 2) ^ (c >> 3)) & 1) * D, D = the chunk
+//    distance between lane groups 0 and 1 (8; Q6_K: 4), so every 16-lane group of a
+//    B-fragment read hits 16 distinct 16-byte bank slots.
 // x16 holds f16 copies of bf16 activations; a value beyond the f16 range becomes inf
-// there, so a workgroup whose accumulators come out non-finite (rare: Gemma-family
-// hidden states) recomputes its rows from the bf16 x with power-of-two row pre-scales
-// (q3_slow, plain loads) — the same contract as v2.
+// there, so a wave whose accumulators come out non-finite (rare: Gemma-family hidden
+// states) recomputes that row group from the bf16 x with power-of-two row pre-scales
+// (q3_slow, plain loads) — the same result as v2's rerun, bit for bit.
 // Outputs as v2: fp32 split-K partials ws[S, M, Ntot] for the fused decode epilogues, or
-// bf16 out when S == 1.
+// bf16 out when S == 1; bit-identical to v2 (same dequant, same MFMA order per
+// accumulator: super-chunks in order, steps in order).
 #include "hipserve/common.h"
 #include "hipserve/gguf_tiles.h"
 #include "hipserve/kernels.h"
@@ -40,38 +40,22 @@ using namespace gq;
 
 typedef __attribute__((address_space(3))) void* lds_p;
 
-constexpr int Q3_LDS = 163840;  // the whole CU
-constexpr int Q3_NSLOT = 3;
+constexpr int Q3_XLDS = 131072;  // x slice bytes of LDS
+constexpr int Q3_NW = 8;         // waves per workgroup (2 per SIMD)
 
-template <int QT, int MT>
-constexpr int q3_nw() {  // waves (16-row groups) per workgroup: 3 slots fit the LDS
-  constexpr int xb = MT * 16 * 512, cb = chunk_bytes<QT>();
-  int nw = MT == 4 ? 8 : 16;
-  while (nw > 4 && Q3_NSLOT * (xb + nw * cb) > Q3_LDS) --nw;
-  return nw;
-}
-template <int QT, int MT>
-constexpr int q3_slot() { return MT * 16 * 512 + q3_nw<QT, MT>() * chunk_bytes<QT>(); }
+template <int MT>
+constexpr int q3_xsc() { return Q3_XLDS / (MT * 16 * 512); }  // super-chunks of x per slice
 
 template <int QT>
 constexpr int q3_d() { return QT == Q6_K ? 4 : 8; }  // chunk distance of lane groups 0 / 1
 
-// 16-byte chunk (0..31) of the 256 f16 of an x row that lane group g reads at step s
-template <int QT>
-HS_DEVICE int q3_chunk(int g, int s) { return kbase<QT>(g, s) >> 3; }
-
 HS_DEVICE int q3_swz(int c, int d) { return c ^ ((((c >> 2) ^ (c >> 3)) & 1) * d); }
-
-template <int N>
-HS_DEVICE void q3_vmwait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 // rows of this wave recomputed from bf16 x with per-row power-of-two pre-scales (the
 // accumulators of the fast pass were non-finite: an x value beyond the f16 range)
 template <int QT, int MT>
 HS_DEVICE void q3_slow(f32x4 (&acc)[MT], const unsigned short* __restrict__ x, long ldx, int M,
-                       const unsigned char* __restrict__ wq, int nsb, int sb0, int sb1) {
+                       const unsigned char* __restrict__ wq, int sb0, int sb1) {
   constexpr int CB = chunk_bytes<QT>();
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   // max |x| of row `lane` over [sb0, sb1) -> scale 2^-k with max 2^-k < 2^15
@@ -123,103 +107,65 @@ struct Q3Args {
   const unsigned short* x;    // bf16 [M, >= K] (the slow path)
   const unsigned short* x16;  // f16 pair order, same row stride
   long ldx;
-  Parts parts;
-  int M, Ntot, K, per;  // per: super-chunks per K split
+  Parts parts;          // tile0 = first global row group of the part
+  int ngroups;          // row groups of all parts
+  int M, Ntot, K, per, S;  // per: super-chunks per K slice
 };
 
-// compile-time geometry of one (format, row tile) instantiation. (The DMA lambda computes
-// its per-lane x offsets inline: with them precomputed into local int arrays read inside
-// the lambda, hipcc (ROCm 7.2) silently emitted no host stub for the kernel.)
 template <int QT, int MT>
-struct Q3G {
-  static constexpr int NW = q3_nw<QT, MT>(), CB = chunk_bytes<QT>(), SLOT = q3_slot<QT, MT>();
-  static constexpr int XB = MT * 16 * 512;           // x image bytes of a slot
-  static constexpr int XI = XB / 1024;               // x DMA instructions per slot
-  static constexpr int NXW = (XI + NW - 1) / NW;     // ... per wave (the last ones may repeat a piece)
-  static constexpr int N4 = CB / 1024, N1 = (CB % 1024) / 256, TAIL = CB % 256;
-  static constexpr int NDMA = NXW + N4 + N1 + (TAIL ? 1 : 0);  // DMA instructions per wave and slot
-};
-
-template <int QT, int MT, int NT>
-__global__ __launch_bounds__(NT) void qgemm3_kernel(Q3Args A) {
-  using C_ = Q3G<QT, MT>;
-  constexpr int NW = C_::NW, CB = C_::CB, SLOT = C_::SLOT, XB = C_::XB, XI = C_::XI, NXW = C_::NXW;
-  constexpr int NDMA = C_::NDMA;
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[Q3_NSLOT * SLOT];
+__global__ __launch_bounds__(64 * Q3_NW) void qgemm3_kernel(Q3Args A) {
+  constexpr int CB = chunk_bytes<QT>(), XSC = MT * 16 * 512;  // x bytes per super-chunk
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[q3_xsc<MT>() * XSC];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
-  const int tile = blockIdx.x;
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < kMaxParts; ++i)
-    if (i < A.parts.n && tile >= A.parts.p[i].tile0) pi = i;
-  const Part& P = A.parts.p[pi];
-  const int ngroups = P.rows >> 4, nsb = A.K >> 8, M = A.M;
-  const int gi = (tile - P.tile0) * NW + w;  // this wave's row group (>= ngroups: computes a copy, stores nothing)
-  const int gl = min(gi, ngroups - 1);
-  const int sb0 = blockIdx.y * A.per, sb1 = min(nsb, sb0 + A.per);
+  const int M = A.M, nsb = A.K >> 8;
+  const int split = blockIdx.x % A.S, wg = blockIdx.x / A.S, nwg = gridDim.x / A.S;
+  const int sb0 = split * A.per, sb1 = min(nsb, sb0 + A.per), nsc = sb1 - sb0;
 
-  // ---- DMA sources
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)A.x16, 0, (int)((long)M * A.ldx * 2), 0x00020000);
-  const int ldx2 = (int)A.ldx * 2;
-  const __amdgpu_buffer_rsrc_t wr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)P.q, 0, ngroups * nsb * CB, 0x00020000);
-  const int wbase = gl * nsb * CB;  // byte offset of this wave's row group
-  auto dma = [&](int sb, int slot) {
-    unsigned char* s = lds + slot * C_::SLOT;
-#pragma unroll
-    for (int i = 0; i < C_::NXW; ++i) {
-      // 1 KiB piece j = x rows 2 j, 2 j + 1 (the last waves may repeat piece XI - 1);
-      // lane -> row m, LDS chunk lane & 31 holding x chunk (lane & 31) ^ f(m & 15)
-      const int j = min(w + C_::NW * i, C_::XI - 1);
-      const int m = 2 * j + (lane >> 5), jl = (lane & 31) ^ q3_swz(m & 15, q3_d<QT>());
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_p)(s + j * 1024), 16, m * ldx2 + jl * 16, sb * 512, 0, 0);
+  // ---- x slice -> LDS, once: piece j (1 KiB) = rows 2 jr, 2 jr + 1 of super-chunk j / (8 MT)
+  {
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.x16, 0, (int)((long)M * A.ldx * 2), 0x00020000);
+    const int ldx2 = (int)A.ldx * 2, pieces = nsc * MT * 8;
+    for (int j = w; j < pieces; j += Q3_NW) {
+      const int sc = j / (MT * 8), jr = j - sc * MT * 8;
+      const int m = 2 * jr + (lane >> 5), jl = (lane & 31) ^ q3_swz(m & 15, q3_d<QT>());
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_p)(lds + j * 1024), 16, m * ldx2 + jl * 16,
+                                               (sb0 + sc) * 512, 0, 0);
     }
-    unsigned char* d = s + C_::XB + w * C_::CB;
-    const int so = wbase + sb * C_::CB;
-#pragma unroll
-    for (int n = 0; n < C_::N4; ++n)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * n), 16, lane * 16 + 1024 * n, so, 0, 0);
-#pragma unroll
-    for (int n = 0; n < C_::N1; ++n)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * C_::N4 + 256 * n), 4,
-                                               lane * 4 + 1024 * C_::N4 + 256 * n, so, 0, 0);
-    if constexpr (C_::TAIL > 0) {
-      if (lane < C_::TAIL / 4)  // lanes 0 .. TAIL/4 - 1 are active in every wave: always issued
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_p)(d + 1024 * C_::N4 + 256 * C_::N1), 4,
-                                                 lane * 4 + 1024 * C_::N4 + 256 * C_::N1, so, 0, 0);
-    }
-  };
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
 
-  // x fragment addresses (slot-relative): row 16 t + c, chunk q3_chunk(g, s) ^ f(c)
+  // x fragment addresses: row 16 t + c, chunk (kbase(g, s) / 8) ^ f(c) of the super-chunk
   const int fc = q3_swz(c, q3_d<QT>());
   int xa[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) xa[s] = c * 512 + ((q3_chunk<QT>(g, s) ^ fc) << 4);
+  for (int s = 0; s < 8; ++s) xa[s] = c * 512 + (((kbase<QT>(g, s) >> 3) ^ fc) << 4);
+
+  // ---- this wave's items: row groups r = gw, gw + TW, ... x super-chunks of the slice
+  const int TW = nwg * Q3_NW, gw = wg * Q3_NW + w;
+  const int nrg = gw < A.ngroups ? (A.ngroups - 1 - gw) / TW + 1 : 0;
+  const int nitems = nrg * nsc;
+  auto chunk = [&](int i) -> const unsigned char* {  // raw chunk of item i (clamped: no branch)
+    i = min(i, nitems - 1);
+    const int rr = i / nsc, sc = i - rr * nsc;
+    const int r = gw + rr * TW;
+    int pi = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxParts; ++k)
+      if (k < A.parts.n && r >= A.parts.p[k].tile0) pi = k;
+    const Part& P = A.parts.p[pi];
+    return P.q + ((long)(r - P.tile0) * nsb + sb0 + sc) * CB;
+  };
 
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (sb0 < sb1) {
-    dma(sb0, 0);
-    if (sb0 + 1 < sb1) dma(sb0 + 1, 1);
-  }
-  int slot = 0;
-  for (int sb = sb0; sb < sb1; ++sb) {
-    if (sb + 1 < sb1)
-      q3_vmwait<NDMA>();  // own DMA of sb landed; sb + 1's in flight
-    else
-      q3_vmwait<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot sb - 1 returned
-    __builtin_amdgcn_s_barrier();                        // every wave's x DMA of sb landed
-    if (sb + 2 < sb1) dma(sb + 2, slot == 0 ? 2 : slot - 1);
-    const unsigned char* sp = lds + slot * SLOT;
-    Raw raw;
-    load_raw<QT>(sp + XB + w * CB, g, c, lane, raw);
+  auto compute = [&](const Raw& raw, int sc) {
+    const unsigned char* sp = lds + sc * XSC;
     Dec<QT> dec;
     dec.setup(raw, g);
 #pragma unroll
@@ -231,58 +177,91 @@ __global__ __launch_bounds__(NT) void qgemm3_kernel(Q3Args A) {
 #pragma unroll
       for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[t], acc[t], 0, 0, 0);
     }
-    slot = slot == Q3_NSLOT - 1 ? 0 : slot + 1;
-  }
-
-  bool bad = false;
+  };
+  auto finish = [&](int i) {  // item i ended its row group: epilogue, then zero the accumulators
+    const int r = gw + (i / nsc) * TW;
+    int pi = 0;
 #pragma unroll
-  for (int t = 0; t < MT; ++t)
+    for (int k = 1; k < kMaxParts; ++k)
+      if (k < A.parts.n && r >= A.parts.p[k].tile0) pi = k;
+    const Part& P = A.parts.p[pi];
+    const int gi = r - P.tile0;
+    bool bad = false;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(acc[t][e]);
-  if (__any(bad))  // per wave: this wave's rows
-    q3_slow<QT, MT>(acc, A.x, A.ldx, M, P.q + (long)gl * nsb * CB, nsb, sb0, sb1);
-
-  if (gi >= ngroups) return;
-  const int col = P.col + 16 * gi + 4 * g;
-  if constexpr (QT == FP8 || QT == FP8B) {
-    const f32x4 rs = *reinterpret_cast<const f32x4*>(P.rs + 16 * gi + 4 * g);
+    for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] *= rs;
-  }
+      for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(acc[t][e]);
+    if (__any(bad)) q3_slow<QT, MT>(acc, A.x, A.ldx, M, P.q + (long)gi * nsb * CB, sb0, sb1);
+    const int col = P.col + 16 * gi + 4 * g;
+    if constexpr (QT == FP8 || QT == FP8B) {
+      const f32x4 rs = *reinterpret_cast<const f32x4*>(P.rs + 16 * gi + 4 * g);
 #pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    const int m = 16 * t + c;
-    if (m >= M) continue;
-    if (A.ws != nullptr) {
-      *reinterpret_cast<f32x4*>(A.ws + ((long)blockIdx.y * M + m) * A.Ntot + col) = acc[t];
-    } else {
-      uint2 v;
-      v.x = pack_bf16x2(acc[t][0], acc[t][1]);
-      v.y = pack_bf16x2(acc[t][2], acc[t][3]);
-      *reinterpret_cast<uint2*>(A.out + (long)m * A.out_stride + col) = v;
+      for (int t = 0; t < MT; ++t) acc[t] *= rs;
     }
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = 16 * t + c;
+      if (m < M) {
+        if (A.ws != nullptr) {
+          *reinterpret_cast<f32x4*>(A.ws + ((long)split * M + m) * A.Ntot + col) = acc[t];
+        } else {
+          uint2 v;
+          v.x = pack_bf16x2(acc[t][0], acc[t][1]);
+          v.y = pack_bf16x2(acc[t][2], acc[t][3]);
+          *reinterpret_cast<uint2*>(A.out + (long)m * A.out_stride + col) = v;
+        }
+      }
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  // three raw register sets, used in rotation (loop unrolled by three: static indices),
+  // each refilled with item i + 3 right after item i's dequant has read it
+  Raw r0, r1, r2;
+  if (nitems > 0) {
+    load_raw<QT>(chunk(0), g, c, lane, r0);
+    load_raw<QT>(chunk(1), g, c, lane, r1);
+    load_raw<QT>(chunk(2), g, c, lane, r2);
   }
+  auto item = [&](int i, Raw& cur) {
+    const int sc = i % nsc;
+    compute(cur, sc);
+    load_raw<QT>(chunk(i + 3), g, c, lane, cur);  // the last items re-load the last chunk (unused)
+    if (sc == nsc - 1) finish(i);
+  };
+  int i = 0;
+  for (; i + 2 < nitems; i += 3) {
+    item(i, r0);
+    item(i + 1, r1);
+    item(i + 2, r2);
+  }
+  if (i < nitems) item(i, r0);
+  if (i + 1 < nitems) item(i + 1, r1);
 }
 
 template <int QT, int MT>
-void q3_launch(const Q3Args& a, int tiles, int S, hipStream_t s) {
-  constexpr int NT = 64 * q3_nw<QT, MT>();
-  qgemm3_kernel<QT, MT, NT><<<dim3(tiles, S), NT, 0, s>>>(a);
+void q3_launch(const Q3Args& a, int grid, hipStream_t s) {
+  qgemm3_kernel<QT, MT><<<grid, 64 * Q3_NW, 0, s>>>(a);
 }
 
 template <int QT>
-void q3_launch_m(const Q3Args& a, int tiles, int S, hipStream_t s) {
+void q3_launch_m(const Q3Args& a, int grid, hipStream_t s) {
   if (a.M <= 16)
-    q3_launch<QT, 1>(a, tiles, S, s);
+    q3_launch<QT, 1>(a, grid, s);
   else if (a.M <= 32)
-    q3_launch<QT, 2>(a, tiles, S, s);
+    q3_launch<QT, 2>(a, grid, s);
   else
-    q3_launch<QT, 4>(a, tiles, S, s);
+    q3_launch<QT, 4>(a, grid, s);
 }
 
-template <int QT>
-int q3_rows(int M) {
-  return 16 * (M <= 16 ? q3_nw<QT, 1>() : M <= 32 ? q3_nw<QT, 2>() : q3_nw<QT, 4>());
+int q3_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  }
+  return ncu;
 }
 
 }  // namespace
@@ -295,20 +274,24 @@ bool qgemm3_enabled() {
   return e != 0;
 }
 
-// parts of one launch: every part of format qt (one kernel instantiation per format)
+// every part in one launch (one instantiation per format: formats launch separately)
 bool launch_qgemm3(void* out, long out_stride, float* ws, const void* x, const void* x16, long ldx,
                    const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s) {
   if (M < 1 || M > 64 || x16 == nullptr || K % 256 || ldx % 8) return false;
   if ((long)M * ldx * 2 >= (1L << 31)) return false;
   const int nsb = K / 256, per = (nsb + S - 1) / S, Sx = (nsb + per - 1) / per;
+  const int xsc = M <= 16 ? q3_xsc<1>() : M <= 32 ? q3_xsc<2>() : q3_xsc<4>();
+  if (per > xsc) return false;  // the x slice would not fit the LDS: the caller runs v2
+  if (ws == nullptr && Sx != 1) return false;
   int fmts[kMaxParts], nf = 0;
   for (int i = 0; i < nparts; ++i) {
-    if (parts[i].qtype < Q4_0 || parts[i].qtype > INT8) return false;
-    if ((long)(parts[i].rows / 16) * nsb * gguf_tiled_chunk_bytes(parts[i].qtype) >= (1L << 31)) return false;
+    if (parts[i].qtype < Q4_0 || parts[i].qtype > INT8 || parts[i].rows % 16) return false;
     bool seen = false;
     for (int j = 0; j < nf; ++j) seen |= fmts[j] == parts[i].qtype;
     if (!seen) fmts[nf++] = parts[i].qtype;
   }
+  // persistent grid: one workgroup per CU, a multiple of the slice count
+  const int grid = max(1, q3_cus() / Sx) * Sx;
   for (int f = 0; f < nf; ++f) {
     Q3Args a{};
     a.out = static_cast<unsigned short*>(out);
@@ -321,35 +304,25 @@ bool launch_qgemm3(void* out, long out_stride, float* ws, const void* x, const v
     a.Ntot = Ntot;
     a.K = K;
     a.per = per;
-    int rows = 0;
-    switch (fmts[f]) {
-      case Q4_0: rows = q3_rows<Q4_0>(M); break;
-      case Q4_1: rows = q3_rows<Q4_1>(M); break;
-      case Q8_0: rows = q3_rows<Q8_0>(M); break;
-      case Q4_K: rows = q3_rows<Q4_K>(M); break;
-      case Q5_K: rows = q3_rows<Q5_K>(M); break;
-      case Q6_K: rows = q3_rows<Q6_K>(M); break;
-      case FP8: rows = q3_rows<FP8>(M); break;
-      case FP8B: rows = q3_rows<FP8B>(M); break;
-      case INT8: rows = q3_rows<INT8>(M); break;
-    }
-    int tiles = 0;
+    a.S = Sx;
+    int groups = 0;
     for (int i = 0; i < nparts; ++i) {
       if (parts[i].qtype != fmts[f]) continue;
       a.parts.p[a.parts.n++] = Part{static_cast<const unsigned char*>(parts[i].q), parts[i].rs, parts[i].qtype,
-                                    parts[i].rows, parts[i].col, tiles};
-      tiles += (parts[i].rows + rows - 1) / rows;
+                                    parts[i].rows, parts[i].col, groups};
+      groups += parts[i].rows / 16;
     }
+    a.ngroups = groups;
     switch (fmts[f]) {
-      case Q4_0: q3_launch_m<Q4_0>(a, tiles, Sx, s); break;
-      case Q4_1: q3_launch_m<Q4_1>(a, tiles, Sx, s); break;
-      case Q8_0: q3_launch_m<Q8_0>(a, tiles, Sx, s); break;
-      case Q4_K: q3_launch_m<Q4_K>(a, tiles, Sx, s); break;
-      case Q5_K: q3_launch_m<Q5_K>(a, tiles, Sx, s); break;
-      case Q6_K: q3_launch_m<Q6_K>(a, tiles, Sx, s); break;
-      case FP8: q3_launch_m<FP8>(a, tiles, Sx, s); break;
-      case FP8B: q3_launch_m<FP8B>(a, tiles, Sx, s); break;
-      case INT8: q3_launch_m<INT8>(a, tiles, Sx, s); break;
+      case Q4_0: q3_launch_m<Q4_0>(a, grid, s); break;
+      case Q4_1: q3_launch_m<Q4_1>(a, grid, s); break;
+      case Q8_0: q3_launch_m<Q8_0>(a, grid, s); break;
+      case Q4_K: q3_launch_m<Q4_K>(a, grid, s); break;
+      case Q5_K: q3_launch_m<Q5_K>(a, grid, s); break;
+      case Q6_K: q3_launch_m<Q6_K>(a, grid, s); break;
+      case FP8: q3_launch_m<FP8>(a, grid, s); break;
+      case FP8B: q3_launch_m<FP8B>(a, grid, s); break;
+      case INT8: q3_launch_m<INT8>(a, grid, s); break;
     }
   }
   return true;

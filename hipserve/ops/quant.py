@@ -473,12 +473,15 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
             continue
         for M in ms:
             x = torch.randn(M, w.K, device=device, dtype=torch.bfloat16)
+            # the decode producers hand the GEMM an f16 pair-order copy (out16 / act16): with it
+            # M <= 64 runs the x-resident v3 kernel where the K slice fits its LDS, v2 elsewhere
+            x16 = x.to(torch.float16) if M <= 64 else None
             cands = sorted({_actual_splits(nsb, s) for s in (1, 2, 4, 8, 16, 32, 64) if s <= nsb})
             cost = {}
             for S in cands:
                 if S * M * w.N > ws.numel():
                     continue
-                t = _graph_time_us(lambda S=S: _launch_v2(empty, ws, x, w, S))
+                t = _graph_time_us(lambda S=S: _launch_v2(empty, ws, x, w, S, x16))
                 cost[S] = t + 1e6 * S * M * w.N * 4 / PARTIAL_READ_BPS
             best = min(cost, key=cost.get)
             SPLIT_TABLE[(sig, _bucket(M))] = best

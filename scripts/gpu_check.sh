@@ -111,7 +111,7 @@ for s in $steps; do
     kerneltest) run_one tests/test_kernels_gpu.py ;;
     attnab) HIPSERVE_PREFILL_ATTN_PRIO=0 BENCH_PREFILL_LONG=1 BENCH_PREFILL_VERS=v2w8 timeout -k 10 300 python -u tools/bench_ops.py prefill > $OUT/attn_prio0.log 2>&1 && \
             HIPSERVE_PREFILL_ATTN_PRIO=1 BENCH_PREFILL_LONG=1 BENCH_PREFILL_VERS=v2w8 timeout -k 10 300 python -u tools/bench_ops.py prefill > $OUT/attn_prio1.log 2>&1; rc=$?; cat $OUT/attn_prio0.log $OUT/attn_prio1.log | grep prefill_attention; [ $rc -eq 0 ] ;;
-    gguf64) timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64.log; [ $rc -eq 0 ] ;;
+    gguf64) timeout -k 10 300 python -u tools/bench_gguf.py --m ${GGUF_M:-64} > $OUT/bench_gguf64.log 2>&1; rc=$?; cat $OUT/bench_gguf64.log; [ $rc -eq 0 ] ;;
     gguf64v2) HIPSERVE_QGEMM_M64=2 timeout -k 10 300 python -u tools/bench_gguf.py --m 64 > $OUT/bench_gguf64_v2.log 2>&1; rc=$?; grep v2_partial $OUT/bench_gguf64_v2.log; [ $rc -eq 0 ] ;;
     qpftest) run_one tests/test_gguf_prefill_gpu.py ;;
     attnpmc) for S in 1024 32768; do

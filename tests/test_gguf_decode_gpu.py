@@ -1,8 +1,9 @@
-"""Quantised decode GEMM v3 (csrc/kernels/gguf_decode.hip: x and the tiled weight chunks
-staged by LDS-DMA into a 3-slot ring) vs a plain PyTorch fp32 matmul of the numpy block
-decoder's weights, for every tiled format (GGUF Q4_0 .. Q6_K, FP8 per-channel, INT8), every
-decode row bucket (1, 16, 33, 64 rows: MT = 1 / 2 / 4), split-K slices of every length
-(1 .. 11 super-chunks: the ring's prologue / tail paths), mixed formats in one merged
+"""Quantised decode GEMM v3 (csrc/kernels/gguf_decode.hip: the x slice resident in LDS per
+persistent workgroup, weight chunks streamed into registers three items ahead) vs a plain
+PyTorch fp32 matmul of the numpy block decoder's weights, for every tiled format (GGUF
+Q4_0 .. Q6_K, FP8 per-channel, INT8), every decode row bucket (1, 16, 33, 64 rows: MT =
+1 / 2 / 4), split-K slices of every length (1 .. 11 super-chunks: item streams shorter
+than the three-deep register rotation, slices past the LDS fall back to v2), mixed formats in one merged
 weight (two launches into one output), parts whose rows are not a multiple of the
 workgroup's rows. The v3 kernel is bit-identical to v2 on the same f16 operands (same
 dequant, same MFMA order per accumulator), and rows past the f16 range take the
@@ -70,8 +71,8 @@ def test_v3_formats_vs_fp32_and_v2(qt, M):
 @pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K])
 @pytest.mark.parametrize("S", [1, 2, 3, 5, 7, 11])
 def test_v3_every_slice_length(qt, S):
-    """K slices of 1 .. 11 super-chunks at M = 64 (ring prologue with one / two slots,
-    steady state, tail), a Q4_K + Q6_K merged weight (two launches, one output)."""
+    """K slices of 1 .. 11 super-chunks at M = 64 (up to 4 run v3, longer ones v2), a
+    Q4_K + Q6_K merged weight (two launches, one output)."""
     K, M = 2816, 64
     qw, raws = _rand_qw([(qt, 256, K), (G.Q6_K if qt == G.Q4_K else G.Q4_K, 128, K)], seed=S)
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
