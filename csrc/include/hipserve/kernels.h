@@ -101,12 +101,6 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16 = nullptr);
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s);
-// gguf_decode.hip — the v3 decode GEMM (both operands by LDS-DMA) on x16; same outputs as
-// launch_gguf_gemm_parts. false if it does not take the shape (the caller runs v2).
-// HIPSERVE_QGEMM3=0 disables it (qgemm3_enabled).
-bool qgemm3_enabled();
-bool launch_qgemm3(void* out, long out_stride, float* ws, const void* x, const void* x16, long ldx,
-                   const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s);
 // prefill GEMM straight from the tiled GGUF blocks on launch_x_f16_pairs' x16 / rsc (epi:
 // PW_EPI_STORE / ADD / GLU / GEGLU; GLU: parts 0 / 1 = gate / up); false if the formats /
 // shapes are not taken
@@ -195,10 +189,6 @@ struct PwGroup {
 bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
                                 int K, const void* bias, int wm, int grid_req, hipStream_t s,
                                 const PwGroup* group = nullptr, int rw = 4);
-// prefill_gemm_lds.hip — the same product with both operands staged by LDS-DMA (256 x 256
-// tiles, 8 waves, 4-slot LDS ring); epilogues and grouped mode (256-row m-tiles) as above.
-bool launch_prefill_gemm_lds(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N, int K,
-                             const void* bias, hipStream_t s, const PwGroup* group = nullptr, int variant = -1);
 // FP8 (W8A8) form: A = per-token e4m3 activations [M, K] bytes (row scale xs[M]),
 // B = e4m3 weights in the decode kernel's tiled layout (gguf_mfma.hip: [N/16][K/256]
 // [4096 B]) as up to 4 parts stacked along N (each rows % 256 == 0; GLU: part 0 =

@@ -733,10 +733,6 @@ int gguf_tiled_chunk_bytes(int qtype) {
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16) {
-  // decode batches with the producer's f16 copy of x: the v3 kernel (gguf_decode.hip)
-  if (x16 != nullptr && M <= 64 && qgemm3_enabled() &&
-      launch_qgemm3(out, out_stride, ws, x, x16, x_stride, parts, nparts, M, Ntot, K, S, s))
-    return;
   // weight rows per workgroup: 128, or 256 for the wide M = 33-64 body (m64_wide)
   const int ROWS = m64_wide(M, Ntot) ? 256 : 16 * 2 * kWaves;
   int fmts[kMaxParts], nf = 0;

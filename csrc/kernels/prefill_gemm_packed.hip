@@ -101,7 +101,7 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
 // (moe_align with tile BM, moe_gather); m-tile tm multiplies expert grp.tile_expert[tm]'s
 // packed weight (Wp + e * estride) and only the first *grp.num_tiles m-tiles (the
 // device-side count: no host round trip, graph-capturable) are walked.
-template <int WM, int EPI, bool kGroup, int RW, bool LDLY = false, int DBG = 0>
+template <int WM, int EPI, bool kGroup, int RW, bool LDLY = false>
 __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
     const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
     unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n,
@@ -200,10 +200,7 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
       // slot J's 1 KiB offset rides in a per-slot VGPR offset: 8 scalar adds per body, not 32.
       // LDLY: reload a group's weight register one group later, so the load is not issued
       // right behind the MFMAs still reading that register
-      if constexpr (DBG & 1) {  // diagnostic: no weight loads (registers keep stale data)
-      } else if constexpr (DBG & 4) {  // diagnostic: half the weight loads (even row groups)
-        if ((rg & 1) == 0) w[J][rg] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + rg * 8192, 0);
-      } else if constexpr (LDLY) {
+      if constexpr (LDLY) {
         if (rg > 0) w[J][rg - 1] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + (rg - 1) * 8192, 0);
         if (rg == 7) w[J][7] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoj[J], wk + 7 * 8192, 0);
       } else {
@@ -211,10 +208,8 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
       }
       if constexpr (H == 0) {
         xb[rg] = xfrag(buf, 1, rg);
-        if constexpr ((DBG & 2) == 0) {  // diagnostic 2: no X staging (LDS keeps stale data)
-          if (rg == 2) xstore(buf ^ 1, xst[XI]);     // stage s + 1 (loaded XS stages ago)
-          if (rg == 3) xload(s + 1 + XS, xst[XI]);
-        }
+        if (rg == 2) xstore(buf ^ 1, xst[XI]);     // stage s + 1 (loaded XS stages ago)
+        if (rg == 3) xload(s + 1 + XS, xst[XI]);
       } else {
         xa[rg] = xfrag(buf ^ 1, 0, rg);            // stage s + 1, visible since the barrier
       }
@@ -312,7 +307,7 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   const PwGroup grp = group != nullptr ? *group : PwGroup{nullptr, nullptr, 0};
   const bool grouped = group != nullptr;
   if (grouped && (bias != nullptr || epi == PW_EPI_ADD)) return false;
-  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4 && rw != 5 && (rw < 11 || rw > 15))) return false;
+  if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4 && rw != 5)) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;
   if (epi == PW_EPI_ADD && bias != nullptr) return false;
@@ -346,13 +341,7 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
       PW_LAUNCH1(WM_, E_, 4);                                                                                \
     else if (rw == 2)                                                                                        \
       PW_LAUNCH1(WM_, E_, 2);                                                                                \
-    else if (rw >= 11 && rw <= 15 && !grouped && WM_ == 1 && E_ == 0) {                                        \
-      if (rw == 11) pgw_kernel<1, 0, false, 4, false, 1><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
-      if (rw == 12) pgw_kernel<1, 0, false, 4, false, 2><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
-      if (rw == 13) pgw_kernel<1, 0, false, 4, false, 3><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
-      if (rw == 14) pgw_kernel<1, 0, false, 4, false, 4><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
-      if (rw == 15) pgw_kernel<1, 0, false, 4, false, 6><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
-    } else if (grouped)                                                                                      \
+    else if (grouped)                                                                                        \
       pgw_kernel<WM_, E_, true, 4, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp);  \
     else                                                                                                     \
       pgw_kernel<WM_, E_, false, 4, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \

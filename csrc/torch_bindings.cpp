@@ -801,43 +801,6 @@ void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at:
               "prefill_gemm_packed_grouped: unsupported");
 }
 
-// Prefill GEMM over the packed layout with both operands staged by LDS-DMA
-// (prefill_gemm_lds.hip): arguments as prefill_gemm_packed; grouped when tile_expert /
-// num_tiles are given (x = expert-sorted slots in 256-row tiles, wp = [E, packed]).
-void prefill_gemm_lds(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
-                      const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& tile_expert,
-                      const c10::optional<at::Tensor>& num_tiles, int64_t variant) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
-  TORCH_CHECK(wp.is_contiguous(), "prefill_gemm_lds: packed weight must be contiguous");
-  const int M = x.size(0), K = x.size(1);
-  const bool grouped = tile_expert.has_value();
-  TORCH_CHECK(grouped == num_tiles.has_value(), "prefill_gemm_lds: tile_expert and num_tiles together");
-  const long per = (N + 127) / 128 * 128 * (long)K;
-  TORCH_CHECK(K % 256 == 0 && (grouped ? wp.dim() == 2 && wp.size(1) == per : wp.numel() == per),
-              "prefill_gemm_lds: wp = pack(w[N, K % 256]) ([E, packed] when grouped)");
-  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "prefill_gemm_lds: alignment");
-  const bool glu = epi == 2 || epi == 3;
-  TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? N / 2 : N), "prefill_gemm_lds: out shape");
-  const void* bp = nullptr;
-  if (bias.has_value()) {
-    CHECK_BF16((*bias));
-    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "prefill_gemm_lds: bias [N]");
-    bp = bias->data_ptr();
-  }
-  hipserve::PwGroup grp{nullptr, nullptr, 0};
-  if (grouped) {
-    TORCH_CHECK(tile_expert->scalar_type() == at::kInt && num_tiles->scalar_type() == at::kInt, "int32 tile tables");
-    TORCH_CHECK(M % 256 == 0 && tile_expert->numel() >= M / 256, "prefill_gemm_lds: 256-row expert tiles");
-    TORCH_CHECK(epi == 0 || glu, "prefill_gemm_lds: grouped = store or glu epilogue");
-    grp = hipserve::PwGroup{tile_expert->data_ptr<int>(), num_tiles->data_ptr<int>(), per};
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  TORCH_CHECK(hipserve::launch_prefill_gemm_lds((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
-                                                wp.data_ptr(), M, (int)N, K, bp, cur_stream(), grouped ? &grp : nullptr,
-                                                (int)variant),
-              "prefill_gemm_lds: unsupported (glu needs N % 128, bias only with epi 0, 32-bit offsets)");
-}
-
 // FP8 W8A8 form: xq [M, K] uint8 e4m3 + xs [M] fp32 (act_quant_fp8), the weight as
 // tiled FP8 parts (ops/quant.py QuantPart.from_fp8: q [N/16, K/256, 4096] uint8 and
 // rs [N] fp32) stacked along N. epi 0 / 1 as prefill_gemm; 2 / 3: parts = (gate, up),
@@ -1309,7 +1272,6 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
-  m.def("prefill_gemm_lds(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, Tensor? tile_expert=None, Tensor? num_tiles=None, int variant=-1) -> ()");
   m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");
   m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
@@ -1362,7 +1324,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("prefill_gemm", &prefill_gemm);
   m.impl("prefill_gemm_packed", &prefill_gemm_packed);
   m.impl("prefill_gemm_packed_grouped", &prefill_gemm_packed_grouped);
-  m.impl("prefill_gemm_lds", &prefill_gemm_lds);
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);
   m.impl("splitk_post_add_rmsnorm", &splitk_post_add_rmsnorm);
   m.impl("act_quant_fp8", &act_quant_fp8);

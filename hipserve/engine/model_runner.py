@@ -174,18 +174,10 @@ class ModelRunner:
                     # FP8: plain e4m3 copies for the hipBLASLt FP8 prefill GEMMs
                     self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()
-        # opt-in: TunableOp solution choice for the prefill GEMMs at the full token
-        # budget (measured no faster than the heuristic on sustained prefill chains,
-        # profiles/r1_prefill_gemm_tunableop.md)
         self.init_times["decode_gemm_tune_s"] = round(time.time() - t1, 2)
         t1 = time.time()
-        self.prefill_gemm_report = []
-        if self.device.type == "cuda" and ecfg.extra.get("prefill_gemm_tune", False):
-            from ..ops import prefill_tune
-
-            shapes = [s for s in self.model.gemm_shapes() if s != tuple(getattr(self.model.lm_head, "shape", ()))]
-            self.prefill_gemm_report = prefill_tune.tune(shapes, [ecfg.max_num_batched_tokens], self.device)
-            torch.cuda.empty_cache()
+        # (TunableOp solution choice for the prefill GEMMs was measured no faster than the
+        # heuristic on sustained prefill chains, profiles/r1_prefill_gemm_tunableop.md: removed)
         # prefill GEMMs: the hand-written kernel with fused epilogues where it beats
         # hipBLASLt + the separate elementwise kernel (ops/pgemm.py), timed per shape
         self.pgemm_report = []

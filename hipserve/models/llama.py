@@ -848,11 +848,11 @@ class LlamaModel:
 
     def _x16(self, like: torch.Tensor, consumer):
         """f16 buffer for the pair-order copy of ``like`` that its producer
-        (splitk_add_rmsnorm / splitk_glu) writes when the consumer is a quantised
-        decode GEMM (<= 64 rows): the v3 kernel (gguf_decode.hip) stages it by LDS-DMA;
-        None otherwise."""
+        (splitk_add_rmsnorm / splitk_glu / the decode attention) writes when the consumer is
+        a quantised decode GEMM at 33-64 rows (gguf_mfma.hip stages it as is instead of
+        converting x in every workgroup); None otherwise."""
         from ..ops import quant as Q
-        if (not self.X16 or self.tp.world_size != 1 or not like.is_cuda or like.shape[0] > 64
+        if (not self.X16 or self.tp.world_size != 1 or not like.is_cuda or not 32 < like.shape[0] <= 64
                 or not getattr(consumer, "v2", False) or not hasattr(torch.ops.hipserve, "splitk_glu")
                 or Q.f8_decode_ok(consumer)):  # the W8A8 decode GEMM quantises x itself
             return None

@@ -473,9 +473,9 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
             continue
         for M in ms:
             x = torch.randn(M, w.K, device=device, dtype=torch.bfloat16)
-            # the decode producers hand the GEMM an f16 pair-order copy (out16 / act16): with it
-            # M <= 64 runs the x-resident v3 kernel where the K slice fits its LDS, v2 elsewhere
-            x16 = x.to(torch.float16) if M <= 64 else None
+            # at 33-64 rows the decode producers hand the GEMM an f16 pair-order copy of x
+            # (out16 / act16), staged as is: time that form
+            x16 = x.to(torch.float16) if 32 < M <= 64 else None
             cands = sorted({_actual_splits(nsb, s) for s in (1, 2, 4, 8, 16, 32, 64) if s <= nsb})
             cost = {}
             for S in cands:

@@ -123,9 +123,6 @@ for s in $steps; do
     qpfpmc) PMC_PY=tools/qpf_pmc.py PG_SHAPE=8192 bash scripts/pg_pmc.sh > $OUT/qpf_pmc.log 2>&1; rc=$?; tail -n 12 $OUT/qpf_pmc.log; [ $rc -eq 0 ] ;;
     qpfbench) timeout -k 10 300 python -u tools/bench_gguf.py --prefill --no-mtiled --m 2048 8192 > $OUT/bench_qpf.log 2>&1; rc=$?; tail -n 40 $OUT/bench_qpf.log; [ $rc -eq 0 ] ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
-    pglpmc) PG_VARIANTS="l p1" bash scripts/pg_pmc.sh > $OUT/pgl_pmc.log 2>&1; rc=$?; tail -n 16 $OUT/pgl_pmc.log; [ $rc -eq 0 ] ;;
-    gdtest) run_one tests/test_gguf_decode_gpu.py ;;
-    pgltest) run_one tests/test_prefill_gemm_lds_gpu.py ;;
     pglbench) timeout -k 10 300 python -u tools/bench_pgl.py --model ${PGL_MODEL:-both} > $OUT/bench_pgl.log 2>&1; rc=$?; cat $OUT/bench_pgl.log; [ $rc -eq 0 ] ;;
     tptest) timeout -k 10 1000 python -u -m pytest tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread \
               -p no:cacheprovider > $OUT/test_tp_gpu.log 2>&1; rc=$?; tail -n 20 $OUT/test_tp_gpu.log; [ $rc -eq 0 ] ;;

@@ -7,8 +7,7 @@ on the Llama-3-8B Q4_K_M projection shapes, random valid ggml blocks.
 
 One JSON line per (projection, M, kernel): µs per call and the weight-byte
 bandwidth (TB/s) — decode GEMMs are bound by streaming the quantised weights.
-Each M also sweeps the split-K factor (``--splits``) for v2 (bf16 x) and the x-resident
-v3 (gguf_decode.hip, f16 pair-order x16) where its K slice fits the LDS.
+Each M also sweeps the split-K factor (``--splits``, default 1 .. 32).
 """
 from __future__ import annotations
 
@@ -122,21 +121,16 @@ def main():
                 continue
             rows = []
             rows.append(("v2_partial", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw))))
-            # x staged from a producer's f16 pair-order copy (out16 / act16): the x-resident v3
-            # kernel (gguf_decode.hip) where a K slice fits its LDS (<= 16 / 8 / 4 super-chunks
-            # at M <= 16 / 32 / 64), else v2
-            h = x.float().to(torch.float16).reshape(M, -1, 8)[:, :, [0, 2, 1, 3, 4, 6, 5, 7]].reshape(M, -1)
-            x16 = h.contiguous()
-            rows.append(("partial_x16", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw, x16))))
-            xsc = 16 if M <= 16 else 8 if M <= 32 else 4
+            x16 = None
+            if 32 < M <= 64:  # x staged from a producer's f16 pair-order copy (out16 / act16)
+                h = x.float().to(torch.float16).reshape(M, -1, 8)[:, :, [0, 2, 1, 3, 4, 6, 5, 7]].reshape(M, -1)
+                x16 = h.contiguous()
+                rows.append(("v2_partial_x16", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw, x16))))
             nsb = qw.K // 256
             for Sx in sorted({-(-nsb // -(-nsb // S)) for S in (a.splits or (1, 2, 4, 8, 16, 32)) if S <= nsb}):
-                per = -(-nsb // Sx)
                 ws = torch.empty(Sx * M * qw.N, dtype=torch.float32, device="cuda")
                 e = Q._empty(x.device, torch.bfloat16)
-                rows.append((f"v2_S{Sx}", Sx, _time(lambda: Q._launch_v2(e, ws, x, qw, Sx))))
-                if per <= xsc:
-                    rows.append((f"v3_S{Sx}", Sx, _time(lambda: Q._launch_v2(e, ws, x, qw, Sx, x16))))
+                rows.append((f"v2_S{Sx}", Sx, _time(lambda: Q._launch_v2(e, ws, x, qw, Sx, x16))))
             for kern, S, us in rows:
                 print(json.dumps({"proj": name, "M": M, "kernel": kern, "splits": S, "us": round(us, 2),
                                   "weight_MB": round(qw.nbytes / 1e6, 2),

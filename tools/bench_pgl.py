@@ -1,6 +1,6 @@
 """Prefill GEMM units at prefill row counts: hipBLASLt (+ the separate GLU / residual-add
-kernel) vs the packed-layout kernels (prefill_gemm_packed.hip: weights global -> VGPR;
-prefill_gemm_lds.hip: both operands by LDS-DMA). Llama-3-8B / 70B layer shapes, random
+kernel) vs the packed-layout kernel (prefill_gemm_packed.hip: weights global -> VGPR; an
+LDS-DMA form lost on every shape, profiles/r5_pgl_lds_dma_negative.log). Llama-3-8B / 70B layer shapes, random
 operands, 4 weight copies streamed round-robin like a prefill step, interleaved rounds in
 one process (cdna_hip_programming.md §5.4 rule 24): median and min per unit.
 
@@ -39,8 +39,6 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[8192])
     ap.add_argument("--model", default="8b")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--no-old", action="store_true")
-    ap.add_argument("--variants", type=int, nargs="+", default=[0, 4])
     a = ap.parse_args()
     load_library()
     op = torch.ops.hipserve
@@ -71,18 +69,11 @@ def main():
                     elif res is not None:
                         res.add_(y)
 
-                def old(i):
+                def packed(i):
                     op.prefill_gemm_packed(res if res is not None else out, x, wps[i % ncopy], N, epi, None, 1,
                                            1 << 30, 4)
 
-                def new(i, v=0):
-                    op.prefill_gemm_lds(res if res is not None else out, x, wps[i % ncopy], N, epi, variant=v)
-
-                arms = {"blas": blas}
-                for v in a.variants:
-                    arms[f"lds{v}"] = lambda i, v=v: new(i, v)
-                if not a.no_old:
-                    arms["packed"] = old
+                arms = {"blas": blas, "packed": packed}
                 for f in arms.values():
                     f(0)
                 torch.cuda.synchronize()

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Packed-layout prefill GEMM (prefill_gemm_packed.hip) time vs K at fixed M x N, against
 hipBLASLt: the slope is the main loop's cost per 64-deep K stage, the intercept the
-per-tile prologue + epilogue that a workgroup does not overlap with MFMA work.
+per-tile prologue + epilogue that a workgroup does not overlap with MFMA work. (The
+diagnostic no-weight-load / no-X-staging variants behind profiles/r4_pw_scaling_v3.log
+were removed from the kernel library in round 5.)
 usage: python tools/bench_pw_scaling.py [--m 8192] [--n 28672]"""
 import argparse
 import json
@@ -49,7 +51,7 @@ def main():
             return best
         r = {"M": M, "N": N, "K": K, "epi": a.epi, "blas_ms": round(t(lambda: [F.linear(x, w) for w in ws]), 4)}
         for wm in (1, 2):
-            for rw in ((4, 11, 12, 13, 14, 15) if wm == 1 else (2,)):
+            for rw in ((4,) if wm == 1 else (2,)):
                 r[f"wm{wm}_rw{rw}_ms"] = round(t(lambda: [op.prefill_gemm_packed(out, x, wp, N, a.epi, None, wm, 0, rw)
                                                           for wp in wps]), 4)
         # one tile per workgroup (non-persistent launch)

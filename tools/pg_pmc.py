@@ -23,12 +23,7 @@ torch.cuda.synchronize()
 wp = None
 for v in os.environ.get("PG_VARIANTS", "2").split():
     for _ in range(3):
-        if v == "l":  # LDS-DMA packed-layout kernel (prefill_gemm_lds.hip)
-            if wp is None:
-                wp = torch.empty(-(-N // 128) * 128 * K, device="cuda", dtype=torch.bfloat16)
-                torch.ops.hipserve.pack_decode_weight(wp, w, False)
-            torch.ops.hipserve.prefill_gemm_lds(out, x, wp, N, 0)
-        elif v.startswith("p"):  # packed-layout kernel (prefill_gemm_packed.hip), p1 / p2 = wm
+        if v.startswith("p"):  # packed-layout kernel (prefill_gemm_packed.hip), p1 / p2 = wm
             if wp is None:
                 wp = torch.empty(-(-N // 128) * 128 * K, device="cuda", dtype=torch.bfloat16)
                 torch.ops.hipserve.pack_decode_weight(wp, w, False)
