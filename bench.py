@@ -407,6 +407,7 @@ def run_phase(args):
         },
         "engine_init_s": round(init_s, 1),
         "init_breakdown_s": getattr(engine.runner, "init_times", {}),
+        "init_breakdown_s_per_rank": getattr(engine.runner, "init_times_ranks", None),
         "single_weight_layout": getattr(engine.runner, "single_layout", None),
         "packed_prefill_timing": getattr(engine.runner, "packed_prefill_report", None),
         "kv_blocks": engine.runner.num_blocks,
@@ -430,6 +431,7 @@ def run_phase(args):
                    "warmup": args.warmup, "global_batch": args.concurrency,
                    "input_len": args.input_len, "output_len": args.output_len,
                    "engine_init_s": out["engine_init_s"], "init_breakdown_s": out["init_breakdown_s"],
+                   "init_breakdown_s_per_rank": out["init_breakdown_s_per_rank"],
                    "kv_blocks": out["kv_blocks"], **out["tp_info"]}
     if lg is not None:
         lg.close()

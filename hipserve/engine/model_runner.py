@@ -226,6 +226,8 @@ class ModelRunner:
         if self.use_graphs:
             self._capture_graphs()
         self.init_times["graph_capture_s"] = round(getattr(self, "graph_capture_time", 0.0), 2)
+        # every rank's breakdown on rank 0 (a TP pod's start-up is as slow as its slowest rank)
+        self.init_times_ranks = tp.gather_obj(dict(self.init_times))
 
     # ------------------------------------------------------------ setup
     def _load_weights(self):
@@ -295,8 +297,16 @@ class ModelRunner:
             return None
         key = (tuple(units), M)
         r = _PACKED_TIMING.get(key)
-        if r is None:  # one timing per shape set and process: engines in one process agree
-            r = _PACKED_TIMING[key] = pgemm.tune_packed(units, M, self.device, self.ops)
+        if r is None:  # one timing per shape set and process (engines in one process agree),
+            # and per device / kernel build across starts (ops/tune_cache.py)
+            from ..ops import tune_cache as TC
+
+            r = TC.get(self.device, "packed_prefill", [units, M])
+            if r is None:
+                r = pgemm.tune_packed(units, M, self.device, self.ops)
+                TC.put(self.device, "packed_prefill", [units, M], r)
+                TC.flush()
+            _PACKED_TIMING[key] = r
         self.packed_prefill_report = r
         return "prefill timing" if r["packed_ms"] <= r["blas_ms"] else None
 
@@ -369,6 +379,14 @@ class ModelRunner:
         ms = list(range(1024, budget + 1, 256))
         if len(ms) < 2:
             return None
+        from ..ops import tune_cache as TC
+
+        ck = [[list(w.shape) for w in ws], budget]
+        hit = TC.get(self.device, "prefill_pad", ck)
+        if hit is not None:  # timed by a previous start on this device and kernel build
+            times = {int(m): t for m, t in hit.items()}
+            self.prefill_pad_times = {m: round(t / 2, 3) for m, t in times.items()}
+            return pad_table(times)
         x = torch.randn(budget, max(w.shape[1] for w in ws), device=self.device, dtype=torch.bfloat16)
 
         def chain(m):
@@ -386,6 +404,8 @@ class ModelRunner:
             e1.synchronize()
             times[m] = e0.elapsed_time(e1)
         del x
+        TC.put(self.device, "prefill_pad", ck, times)
+        TC.flush()
         self.prefill_pad_times = {m: round(t / 2, 3) for m, t in times.items()}
         return pad_table(times)
 

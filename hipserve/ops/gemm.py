@@ -113,10 +113,21 @@ class GemmTuner:
         ("glu",); those are timed as GEMM + epilogue units."""
         # inference mode like the engine's graph capture: the generator state tensors a
         # capture registers must not switch between inference and normal tensors
+        from . import tune_cache as TC
+
         fused = fused or {}
         ms = [m for m in (ms or TUNE_MS) if m <= 64]
         for (N, K) in sorted(set(shapes)):
             spec = fused.get((N, K))
+            # a previous start on this device and kernel build timed this shape: reuse it
+            hits = [TC.get(device, "decode_gemm", [M, N, K, spec]) for M in ms]
+            if all(h is not None for h in hits):
+                for M, h in zip(ms, hits):
+                    self.table[(M, N, K)] = TC.tup(h["best"])
+                    if h["bp"] is not None:
+                        self.best_packed[(M, N, K)] = (TC.tup(h["bp"][0]), h["bp"][1])
+                    self.report.append(dict(h["row"], cached=True))
+                continue
             ncopy = max(1, min(16, -(-COLD_BYTES // (N * K * 2))))
             ws_ = [torch.randn(N, K, device=device, dtype=torch.bfloat16) for _ in range(ncopy)]
             glu = spec is not None and spec[0] == "glu"
@@ -145,10 +156,15 @@ class GemmTuner:
                     if t < best_t * 0.97:
                         best, best_t = cfg, t
                 self.table[(M, N, K)] = best
-                self.report.append({"M": M, "N": N, "K": K, "unit": spec[0] if spec else "gemm",
-                                    "blas_us": round(t_blas, 1), "best": str(best), "best_us": round(best_t, 1),
-                                    "best_TBps": round(N * K * 2 / best_t / 1e6, 2)})
+                row = {"M": M, "N": N, "K": K, "unit": spec[0] if spec else "gemm",
+                       "blas_us": round(t_blas, 1), "best": str(best), "best_us": round(best_t, 1),
+                       "best_TBps": round(N * K * 2 / best_t / 1e6, 2)}
+                self.report.append(row)
+                bp = self.best_packed.get((M, N, K))
+                TC.put(device, "decode_gemm", [M, N, K, spec],
+                       {"best": best, "bp": [bp[0], bp[1]] if bp else None, "row": row})
             del ws_, wp_
+        TC.flush()
         return self.report
 
     @staticmethod

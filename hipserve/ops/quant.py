@@ -459,10 +459,20 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
     S in {1, 2, 4, ...} and keep the S minimising kernel time + the epilogue's
     re-read of the partials (S*M*N*4 B at PARTIAL_READ_BPS). Timed inside a
     hipGraph (the decode step's launch mode). Returns report rows."""
+    from . import tune_cache as TC
+
     seen, report = {}, []
     for w in weights:
         if isinstance(w, QuantWeight) and w.v2:
             seen.setdefault(_sig(w), w)
+    for sig in list(seen):  # timed by a previous start on this device and kernel build
+        kind = "f8_splits" if f8_decode_ok(seen[sig]) else "gguf_splits"
+        hits = [TC.get(device, kind, [list(map(list, sig[1])), sig[0], M]) for M in ms]
+        if all(h is not None for h in hits):
+            for M, h in zip(ms, hits):
+                (F8_SPLIT_TABLE if kind == "f8_splits" else SPLIT_TABLE)[(sig, _bucket(M))] = h["S"]
+                report.append(dict(h["row"], cached=True))
+            del seen[sig]
     nbuf = max((4 * w.N * max(ms) * 32 for w in seen.values()), default=0)
     ws = torch.empty(min(nbuf, max_ws_bytes) // 4, dtype=torch.float32, device=device)
     empty = _empty(device, torch.bfloat16)
@@ -485,9 +495,11 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
                 cost[S] = t + 1e6 * S * M * w.N * 4 / PARTIAL_READ_BPS
             best = min(cost, key=cost.get)
             SPLIT_TABLE[(sig, _bucket(M))] = best
-            report.append({"K": w.K, "N": w.N, "M": M, "S": best,
-                           "us": {k: round(v, 2) for k, v in sorted(cost.items())}})
+            row = {"K": w.K, "N": w.N, "M": M, "S": best, "us": {k: round(v, 2) for k, v in sorted(cost.items())}}
+            report.append(row)
+            TC.put(device, "gguf_splits", [list(map(list, sig[1])), sig[0], M], {"S": best, "row": row})
     del ws
+    TC.flush()
     return report
 
 
@@ -568,8 +580,11 @@ def _tune_f8_decode(w, ms, ws) -> list:
         if cost:
             best = min(cost, key=cost.get)
             F8_SPLIT_TABLE[(_sig(w), _bucket(M))] = best
-            rows.append({"K": w.K, "N": w.N, "M": M, "S": best, "kernel": "fp8_w8a8",
-                         "us": {k: round(v, 2) for k, v in sorted(cost.items())}})
+            row = {"K": w.K, "N": w.N, "M": M, "S": best, "kernel": "fp8_w8a8",
+                   "us": {k: round(v, 2) for k, v in sorted(cost.items())}}
+            rows.append(row)
+            from . import tune_cache as TC
+            TC.put(ws.device, "f8_splits", [list(map(list, _sig(w)[1])), w.K, M], {"S": best, "row": row})
     return rows
 
 

@@ -307,6 +307,14 @@ class TPGroup:
         dist.broadcast_object_list(lst, src=0, group=self._cpu_group)
         return lst[0]
 
+    def gather_obj(self, obj):
+        """[obj of rank 0, rank 1, ...] on rank 0 (None on the others); CPU group."""
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size if self.rank == 0 else None
+        dist.gather_object(obj, out, dst=0, group=self._cpu_group)
+        return out
+
     def barrier(self):
         if self.world_size > 1:
             dist.barrier(group=self._cpu_group)

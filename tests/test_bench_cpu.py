@@ -95,6 +95,11 @@ def test_bench_tp_strong_phase(n):
     assert tp["custom_allreduce"] is False  # CPU: no IPC collectives
     assert tp["tok_s"] > 0 and tp["p50_ttft_ms"] > 0 and tp["steps"] >= 1
     assert abs(tp["tok_s"] - tp["steps"] * 2 * 4 / (tp["ms_per_step"] * tp["steps"] / 1000)) / tp["tok_s"] < 0.02
+    # every rank's start-up breakdown: a TP pod starts as slow as its slowest rank
+    per = tp["init_breakdown_s_per_rank"]
+    assert isinstance(per, list) and len(per) == n
+    assert all(set(r) >= {"weights_s", "collectives_s", "decode_gemm_tune_s", "graph_capture_s"} for r in per)
+    assert per[0] == tp["init_breakdown_s"]
 
 
 def test_bench_tp_phase_time_box():
