@@ -411,6 +411,32 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
   }
 }
 
+// ---------------------------------------------------------------- tiled FP8 -> plain e4m3
+// The per-channel FP8 tiled layout (ops/quant.py QuantPart.from_fp8: 16-byte piece (row n,
+// k 16 c) of 128-k tile kt at [(n >> 4) nsb + kt / 2] 4096 + (c & 3) 1024 + (kt & 1) 512 +
+// (c >> 2) 256 + (n & 15) 16) back to row-major [N, K] e4m3 bytes, for hipBLASLt's FP8
+// prefill GEMM on a per-call scratch: the tiled decode copy stays the ONLY resident copy.
+// One thread per 16-byte destination piece (coalesced writes; each wave's gathered reads
+// cover whole 1 KiB source runs of 4 consecutive pieces x 16 rows).
+__global__ __launch_bounds__(256) void fp8_untile_kernel(u32x4* __restrict__ out, const unsigned char* __restrict__ q,
+                                                         int N, int K) {
+  const int kp = K >> 4;  // 16-byte pieces per row
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * kp) return;
+  const int n = (int)(i / kp), k = (int)(i - (long)n * kp) * 16;
+  const int sb = k >> 8, kin = k & 255, c = (kin & 127) >> 4;
+  const long src = ((long)(n >> 4) * (K >> 8) + sb) * 4096 + (c & 3) * 1024 + (kin >> 7) * 512 + (c >> 2) * 256 +
+                   (n & 15) * 16;
+  out[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + src));
+}
+
+void launch_fp8_untile(void* out, const void* q, int N, int K, hipStream_t s) {
+  const long pieces = (long)N * (K / 16);
+  if (pieces <= 0) return;
+  fp8_untile_kernel<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(static_cast<u32x4*>(out),
+                                                                     static_cast<const unsigned char*>(q), N, K);
+}
+
 // ---------------------------------------------------------------- prefill GEMM
 // qpg_kernel (GGUF prefill without the resident bf16 shadow):
 // C[M, N] = X[M, K] . W^T straight from the tiled blocks, every weight dequantised ONCE

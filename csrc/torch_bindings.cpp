@@ -442,6 +442,17 @@ void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& 
                                       qtype, N, K, cur_stream());
 }
 
+// per-channel FP8 tiled part q [N/16, K/256, 4096] -> out: row-major [N, K] e4m3 bytes
+void fp8_untile(at::Tensor& out, const at::Tensor& q, int64_t N, int64_t K) {
+  CHECK_DEV(q); CHECK_DEV(out);
+  TORCH_CHECK(N % 16 == 0 && K % 256 == 0 && q.scalar_type() == at::kByte && q.is_contiguous() &&
+              q.numel() == N * K, "fp8_untile: q must be a tiled FP8 part of N x K");
+  TORCH_CHECK(out.is_contiguous() && out.element_size() == 1 && out.numel() == N * K, "fp8_untile: out [N, K] bytes");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "fp8_untile: 16-byte aligned out");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  hipserve::launch_fp8_untile(out.data_ptr(), q.data_ptr(), (int)N, (int)K, cur_stream());
+}
+
 void gguf_dequant(at::Tensor& out, const at::Tensor& q, const at::Tensor& d, const at::Tensor& mn,
                   int64_t qtype, int64_t row_bytes, int64_t N, int64_t K) {
   CHECK_DEV(q); CHECK_BF16(out); TORCH_CHECK(out.is_contiguous() && out.numel() >= N * K);
@@ -1253,6 +1264,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_prefill(Tensor(a!) out, Tensor x16, Tensor rsc, Tensor[] qs, int[] qtypes, int[] rows, int[] cols, int K, int epi) -> bool", &gguf_prefill);
   m.def("x_f16_pairs(Tensor(a!) x16, Tensor(b!) rsc, Tensor x) -> ()", &x_f16_pairs);
   m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K) -> ()", &gguf_dequant_tiled);
+  m.def("fp8_untile(Tensor(a!) out, Tensor q, int N, int K) -> ()", &fp8_untile);
   m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits) -> int", &qmoe_gemm);
   m.def("car_create(int rank, int world, int max_bytes, int nb_large=512) -> int", &car_create);
   m.def("car_handle(int state) -> Tensor", &car_handle);

@@ -128,8 +128,9 @@ def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x
         n = ps[0].N if epi in (2, 3) else w.N
         out = torch.empty(M, n, dtype=torch.bfloat16, device=dev)
     xq, xs = x8 if x8 is not None else act_quant(x)
-    wp = getattr(w, "f8_plain", None)
-    if wp is not None and M % 16 == 0:  # hipBLASLt FP8, row-wise scales, on the plain e4m3 copy
+    from . import quant as Q
+    wp = Q.f8_lib_weight(w) if M % 16 == 0 else None
+    if wp is not None:  # hipBLASLt FP8, row-wise scales, on the plain e4m3 weight
         y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wp.t(), scale_a=xs.reshape(-1, 1),
                              scale_b=w.f8_scale, out_dtype=torch.bfloat16)
         if epi == 0:
@@ -146,14 +147,15 @@ def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x
 
 
 def f8_glu_q8(x: torch.Tensor, w, gelu: bool, x8=None):
-    """FP8 gate|up on hipBLASLt FP8 (the plain e4m3 copy), then GLU and the per-token e4m3
+    """FP8 gate|up on hipBLASLt FP8 (the plain e4m3 weight), then GLU and the per-token e4m3
     quantisation of act in one kernel (glu_quant): (xq, xs) of act for the FP8 down
     projection — no bf16 act round trip and no separate act_quant. None when the
-    weight has no plain copy (the caller runs f8_gemm's GLU epilogue instead)."""
-    wp = getattr(w, "f8_plain", None)
+    weight runs the hand-written kernel (the caller runs f8_gemm's GLU epilogue instead)."""
+    from . import quant as Q
     M = x.shape[0]
-    if wp is None or M % 16 or not hasattr(torch.ops.hipserve, "glu_quant"):
+    if getattr(w, "f8_scale", None) is None or M % 16 or not hasattr(torch.ops.hipserve, "glu_quant"):
         return None
+    wp = Q.f8_lib_weight(w)
     xq, xs = x8 if x8 is not None else act_quant(x)
     y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wp.t(), scale_a=xs.reshape(-1, 1),
                          scale_b=w.f8_scale, out_dtype=torch.bfloat16)

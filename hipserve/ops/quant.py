@@ -731,7 +731,7 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
         return out
     from . import pgemm
     if pgemm.f8_use(w, M):  # FP8 W8A8: the scaled e4m3 MFMA from the tiled weights, or hipBLASLt FP8
-        return pgemm.f8_gemm(x, w, 0, None if getattr(w, "f8_plain", None) is not None else out)
+        return pgemm.f8_gemm(x, w, 0, None if getattr(w, "f8_scale", None) is not None else out)
     if w.dense is not None:  # prefill on the resident bf16 copy: no per-call dequant pass
         return torch.nn.functional.linear(x, w.dense)
     if x.is_cuda and qprefill_ok(w, M):
@@ -760,32 +760,58 @@ def fp8_plain(p: QuantPart) -> torch.Tensor:
     return p.q.reshape(R, nsb, 4, 4, 16, 16).permute(0, 4, 1, 3, 2, 5).reshape(p.N, p.K)
 
 
-def make_fp8_plain(weights, device, reserve_bytes: int) -> int:
-    """Plain [N, K] e4m3 copies (and [1, N] fp32 scales) of the FP8 projections for the
-    prefill GEMMs on hipBLASLt's FP8 kernels with row-wise scales (torch._scaled_mm:
-    2.0-2.4 PFLOP/s on the Gemma-3-27B shapes vs 1.6-1.9 for the hand-written e4m3
-    kernel, tools/bench_pgemm.py --fp8), while ``reserve_bytes`` of HBM stay free: the
-    same bytes as the tiled decode copy (27 GB for Gemma-3-27B on a 288 GB part). The
-    decode GEMMs keep the tiled copy. HIPSERVE_FP8_PREFILL_LIB=0 disables it."""
-    import os
+# FP8 prefill runs hipBLASLt's FP8 GEMM (torch._scaled_mm, row-wise scales: 2.0-2.4
+# PFLOP/s on the Gemma-3-27B shapes vs 1.6-1.9 for the hand-written e4m3 kernel,
+# tools/bench_pgemm.py --fp8), which needs the weight as plain row-major e4m3.
+# HIPSERVE_FP8_PREFILL_LIB:
+#   scratch (default): re-laid out per call from the tiled decode copy into a per-device
+#       scratch (fp8_untile, one HBM read + write of the weight's bytes): the tiled copy is
+#       the ONLY resident copy (the reference hands 0.90 of HBM to the
+#       engine, /root/reference/vllm-models/helm-chart/templates/model-deployments.yaml:35-36)
+#   resident: a resident plain copy beside the tiled one while HBM allows
+#   0: the hand-written e4m3 kernel on the tiled layout (prefill_gemm_f8)
+FP8_LIB = os.environ.get("HIPSERVE_FP8_PREFILL_LIB", "scratch")
+_F8_SCRATCH: dict = {}
 
-    if os.environ.get("HIPSERVE_FP8_PREFILL_LIB", "1") == "0" or torch.device(device).type != "cuda":
+
+def make_fp8_plain(weights, device, reserve_bytes: int) -> int:
+    """Marks the FP8 projections whose prefill GEMM runs on hipBLASLt (``f8_scale``, the
+    [1, N] fp32 channel scales) and, in ``resident`` mode, keeps plain [N, K] e4m3 copies
+    while ``reserve_bytes`` of HBM stay free. Returns the resident bytes added."""
+    if FP8_LIB not in ("scratch", "resident") or torch.device(device).type != "cuda":
         return 0
     from . import pgemm
     added = 0
     for w in sorted(weights, key=lambda w: -w.N * w.K):
-        if getattr(w, "f8_plain", None) is not None or not (pgemm.f8_fits(w) or pgemm.f8_fits(w, glu=True)):
+        if getattr(w, "f8_scale", None) is not None or not (pgemm.f8_fits(w) or pgemm.f8_fits(w, glu=True)):
             continue
         if not all(p.qtype == FP8 for p in w.parts):
             continue
-        need = w.N * w.K
-        free, _ = torch.cuda.mem_get_info(device)
-        if free - need < reserve_bytes:
-            continue
-        w.f8_plain = torch.cat([fp8_plain(p) for p in w.parts]).view(torch.float8_e4m3fn)
         w.f8_scale = (torch.cat([p.rs for p in w.parts]) / 256.0).reshape(1, -1).contiguous()
-        added += need
+        need = w.N * w.K
+        if FP8_LIB == "resident" and torch.cuda.mem_get_info(device)[0] - need >= reserve_bytes:
+            w.f8_plain = torch.cat([fp8_plain(p) for p in w.parts]).view(torch.float8_e4m3fn)
+            added += need
     return added
+
+
+def f8_lib_weight(w):
+    """The plain [N, K] e4m3 weight for hipBLASLt's FP8 GEMM: the resident copy, or the
+    tiled parts re-laid out now into the device's scratch (valid until the next call on
+    the stream); None when ``w`` runs the hand-written kernel."""
+    wp = getattr(w, "f8_plain", None)
+    if wp is not None or getattr(w, "f8_scale", None) is None:
+        return wp
+    dev = w.parts[0].q.device
+    n = w.N * w.K
+    buf = _F8_SCRATCH.get(dev)
+    if buf is None or buf.numel() < n:
+        buf = _F8_SCRATCH[dev] = torch.empty(n, dtype=torch.uint8, device=dev)
+    off = 0
+    for p in w.parts:
+        torch.ops.hipserve.fp8_untile(buf[off * w.K:(off + p.N) * w.K].view(p.N, p.K), p.q, p.N, p.K)
+        off += p.N
+    return buf[:n].view(w.N, w.K).view(torch.float8_e4m3fn)
 
 
 def make_dense_shadows(weights, device, reserve_bytes: int, gguf: bool = True) -> int:
@@ -842,9 +868,10 @@ class QuantMoE:
     def dequantize(self, out: torch.Tensor | None = None) -> torch.Tensor:
         out = out if out is not None else torch.empty(self.E, self.N, self.K, dtype=torch.bfloat16,
                                                       device=self.q.device)
-        for e in range(self.E):
-            torch.ops.hipserve.gguf_dequant_tiled(out[e], self.q[e], self.rs[e] if self.rs.numel() else self.rs,
-                                                  self.kqt, self.N, self.K)
+        # the stacked experts [E][N/16][K/256][chunk] are one tiled [E N, K] matrix: one launch
+        torch.ops.hipserve.gguf_dequant_tiled(out.view(self.E * self.N, self.K), self.q.view(-1),
+                                              self.rs.view(-1) if self.rs.numel() else self.rs,
+                                              self.kqt, self.E * self.N, self.K)
         return out
 
     @staticmethod

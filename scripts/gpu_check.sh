@@ -92,6 +92,10 @@ for s in $steps; do
     pgemm) run_pgemm 8b ;;
     gguf) timeout -k 10 300 python -u tools/bench_gguf.py --m 1 16 64 > $OUT/bench_gguf.log 2>&1; rc=$?; tail -n 30 $OUT/bench_gguf.log; [ $rc -eq 0 ] ;;
     g27fp8) bench_named g27fp8 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b --quantization fp8 ;;
+    g27fp8_res) bench_named g27fp8_res HIPSERVE_FP8_PREFILL_LIB=resident -- --model gemma-3-27b --quantization fp8 ;;
+    q3int8_noshadow) bench_named q3int8_noshadow HIPSERVE_FUSED_DECODE=1 HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 ;;
+    f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
+    qmoetest) run_one tests/test_quant_moe_gpu.py ;;
     g27fp8_shadow) bench_named g27fp8_shadow HIPSERVE_FP8_PREFILL=0 -- --model gemma-3-27b --quantization fp8 ;;
     g27bf16) bench_named g27bf16 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b ;;
     q3int8) bench_named q3int8 HIPSERVE_FUSED_DECODE=1 -- --model qwen3-30b-a3b --quantization int8 ;;

@@ -135,12 +135,14 @@ def test_quant_linear_prefill_uses_f8():
     assert rel < 5e-2, rel  # e4m3 activations: ~2.6 % RMS relative rounding per element
 
 
+@pytest.mark.parametrize("mode", ["scratch", "resident"])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
-def test_f8_gemm_library_path_matches_kernel(epi):
-    """With the plain e4m3 copy (quant.make_fp8_plain) f8_gemm runs hipBLASLt's FP8 GEMM
-    (row-wise scales) + the elementwise epilogue; it matches the hand-written e4m3 kernel
-    on the same per-token activations (fp32 accumulation of exact e4m3 products, bf16
-    outputs within a rounding step)."""
+def test_f8_gemm_library_path_matches_kernel(epi, mode, monkeypatch):
+    """On hipBLASLt's FP8 GEMM (row-wise scales) f8_gemm reads the plain e4m3 weight —
+    re-laid out per call from the tiled decode copy into a scratch (default: the tiled
+    copy stays the only resident one) or a resident plain copy — + the elementwise
+    epilogue; it matches the hand-written e4m3 kernel on the same per-token activations
+    (fp32 accumulation of exact e4m3 products, bf16 outputs within a rounding step)."""
     from hipserve.ops import pgemm, quant as Q
 
     g = torch.Generator(device=DEV).manual_seed(21 + epi)
@@ -151,12 +153,31 @@ def test_f8_gemm_library_path_matches_kernel(epi):
     res0 = (torch.rand(1024, n, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
     a = res0.clone() if epi == 1 else None
     a = pgemm.f8_gemm(x, w, epi, a)
-    assert Q.make_fp8_plain([w], DEV, 0) > 0 and w.f8_plain is not None
-    assert torch.equal(torch.cat([Q.fp8_plain(p) for p in w.parts]).view(torch.float8_e4m3fn).float() *
-                       w.f8_scale.reshape(-1, 1), wd)
+    monkeypatch.setattr(Q, "FP8_LIB", mode)
+    added = Q.make_fp8_plain([w], DEV, 0)
+    assert w.f8_scale is not None and (added > 0) == (mode == "resident")
+    assert (getattr(w, "f8_plain", None) is not None) == (mode == "resident")
+    plain = Q.f8_lib_weight(w)
+    assert torch.equal(plain.view(torch.uint8), torch.cat([Q.fp8_plain(p) for p in w.parts]))
+    assert torch.equal(plain.float() * w.f8_scale.reshape(-1, 1), wd)
     b = res0.clone() if epi == 1 else None
     b = pgemm.f8_gemm(x, w, epi, b)
     torch.testing.assert_close(b.float(), a.float(), rtol=2e-2, atol=2e-2 * a.float().abs().max().item())
+
+
+@pytest.mark.parametrize("N,K", [(16, 256), (272, 5376), (4096, 1024)])
+def test_fp8_untile_inverts_tiling(N, K):
+    """fp8_untile (tiled FP8 part -> row-major e4m3 bytes) against the torch permutation
+    of quant.fp8_plain, on random bytes (every position distinct enough to catch a
+    misplaced 16-byte piece)."""
+    from hipserve.ops import quant as Q
+
+    g = torch.Generator(device=DEV).manual_seed(N + K)
+    q = torch.randint(0, 256, (N // 16, K // 256, 4096), device=DEV, dtype=torch.uint8, generator=g)
+    p = Q.QuantPart(Q.FP8, N, K, q, None, None, 0, tiled=True)
+    out = torch.full((N, K), 7, device=DEV, dtype=torch.uint8)
+    torch.ops.hipserve.fp8_untile(out, q, N, K)
+    assert torch.equal(out, Q.fp8_plain(p))
 
 
 @pytest.mark.parametrize("M,K", [(7, 5376), (64, 21504), (33, 512), (100, 4096)])
