@@ -430,13 +430,6 @@ __global__ __launch_bounds__(256) void fp8_untile_kernel(u32x4* __restrict__ out
   out[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + src));
 }
 
-void launch_fp8_untile(void* out, const void* q, int N, int K, hipStream_t s) {
-  const long pieces = (long)N * (K / 16);
-  if (pieces <= 0) return;
-  fp8_untile_kernel<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(static_cast<u32x4*>(out),
-                                                                     static_cast<const unsigned char*>(q), N, K);
-}
-
 // ---------------------------------------------------------------- prefill GEMM
 // qpg_kernel (GGUF prefill without the resident bf16 shadow):
 // C[M, N] = X[M, K] . W^T straight from the tiled blocks, every weight dequantised ONCE
@@ -873,6 +866,13 @@ bool launch_gguf_prefill(int epi, void* out, long ldo, const void* x16, const fl
   if (glu && nf != 1) return false;
   for (int f = 0; f < nf; ++f) run(fmts[f]);
   return true;
+}
+
+void launch_fp8_untile(void* out, const void* q, int N, int K, hipStream_t s) {
+  const long pieces = (long)N * (K / 16);
+  if (pieces <= 0) return;
+  fp8_untile_kernel<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(static_cast<u32x4*>(out),
+                                                                     static_cast<const unsigned char*>(q), N, K);
 }
 
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s) {

@@ -128,6 +128,14 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
                 "-L", libdir, "-Wl,-rpath," + libdir,
                 "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip"]
         _run(link)
+        # a launcher declared in kernels.h but defined inside an anonymous namespace (or
+        # not at all) links fine into a shared object and only fails at dlopen on the GPU
+        # box: refuse the build here instead
+        und = subprocess.run(["nm", "-D", "--undefined-only", "-C", so + ".tmp"], capture_output=True, text=True)
+        missing = [ln.split(None, 1)[-1] for ln in und.stdout.splitlines() if "hipserve::" in ln]
+        if missing:
+            os.remove(so + ".tmp")
+            raise RuntimeError("hipserve/_C.so has undefined hipserve symbols: " + "; ".join(missing))
         os.replace(so + ".tmp", so)
     return so
 
