@@ -92,6 +92,21 @@ for s in $steps; do
     pgemm) run_pgemm 8b ;;
     gguf) timeout -k 10 300 python -u tools/bench_gguf.py --m 1 16 64 > $OUT/bench_gguf.log 2>&1; rc=$?; tail -n 30 $OUT/bench_gguf.log; [ $rc -eq 0 ] ;;
     g27fp8) bench_named g27fp8 HIPSERVE_FP8_PREFILL=1 -- --model gemma-3-27b --quantization fp8 ;;
+    b8a) bench_named b8a -- ;;
+    b8b) bench_named b8b -- ;;
+    untile) timeout -k 10 120 python -u -c "
+import torch, time
+from hipserve.ops import load_library
+load_library()
+for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
+    q = torch.randint(0, 256, (N // 16, K // 256, 4096), dtype=torch.uint8, device='cuda')
+    out = torch.empty(N, K, dtype=torch.uint8, device='cuda')
+    for _ in range(3): torch.ops.hipserve.fp8_untile(out, q, N, K)
+    torch.cuda.synchronize(); t = time.perf_counter()
+    for _ in range(20): torch.ops.hipserve.fp8_untile(out, q, N, K)
+    torch.cuda.synchronize(); dt = (time.perf_counter() - t) / 20
+    print(N, K, round(dt * 1e6, 1), 'us', round(2 * N * K / dt / 1e12, 2), 'TB/s (read + write)')
+" ;;
     g27fp8_res) bench_named g27fp8_res HIPSERVE_FP8_PREFILL_LIB=resident -- --model gemma-3-27b --quantization fp8 ;;
     q3int8_noshadow) bench_named q3int8_noshadow HIPSERVE_FUSED_DECODE=1 HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 ;;
     f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
