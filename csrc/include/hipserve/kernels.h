@@ -158,20 +158,12 @@ constexpr int DG_GLU = 1, DG_PARTIAL = 2;
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, bool packed, int flags, hipStream_t s);
 
-// prefill_gemm.hip — C[M, N] = A[M, K] . B[N, K]^T (bf16, 256x256x64 MFMA tiles, LDS-DMA
-// staging), N % 256 == 0, K % 64 == 0, any M. Epilogues:
+// prefill epilogues (prefill_gemm.hip FP8 kernel, prefill_gemm_packed.hip):
 //   PG_EPI_STORE  C = bf16(acc)
 //   PG_EPI_ADD    C (the residual, in place) = bf16(bf16(acc) + C)
-//   PG_EPI_GLU    B = the merged [gate; up] weight (N = 2I, I % 128 == 0); C = act [M, I] = silu(gate) * up
+//   PG_EPI_GLU    C = act [M, I] = silu(gate) * up of a merged [gate; up] weight
 //   PG_EPI_GEGLU  as GLU with tanh-GELU(gate) * up (Gemma)
 constexpr int PG_EPI_STORE = 0, PG_EPI_ADD = 1, PG_EPI_GLU = 2, PG_EPI_GEGLU = 3;
-struct PgEpi {
-  int variant;               // kept for the API: 2 = the half-tile pipeline (the only one left)
-  const int* tile_expert;    // grouped (MoE): expert of each 256-row tile of A, -1 = unused
-  long b_estride;            // grouped: elements between consecutive experts' weights
-};
-bool launch_prefill_gemm(int epi, void* C, long ldc, const void* A, long lda, const void* B, long ldb, int M, int N,
-                         int K, const PgEpi& E, hipStream_t s);
 // prefill_gemm_packed.hip — C[M, N] = X[M, K] . W[N, K]^T with W in pack_decode_weight's
 // layout (the decode GEMMs' copy; no second copy of the weight), K % 256 == 0, any M, N.
 // wm = 1: 128 x 512 workgroup tiles, wm = 2: 256 x 256. bias (bf16 [N], STORE only) may be null.
@@ -220,7 +212,6 @@ bool launch_glu_quant(bool gelu, void* out, void* q8, float* xs, const void* in,
                       long in_stride, hipStream_t s);
 // per-token dynamic e4m3 quantisation: xs[m] = max|x[m, :]| / 448, q = sat(x / xs)
 void launch_act_quant_fp8(void* q, float* xs, const void* x, long x_stride, int M, int K, hipStream_t s);
-void launch_pack_glu_rows(void* out, const void* w, int I, int K, hipStream_t s);
 
 // decode_fused.hip — split-K partial reductions fused with the next op of the layer
 // ws: [S, M, N] fp32 partials. h = bf16(sum_s ws); residual = bf16(h + residual);

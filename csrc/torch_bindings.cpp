@@ -745,28 +745,9 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
               "decode_gemm_glu: unsupported (rt, K/splits)");
 }
 
-// Prefill GEMM (prefill_gemm.hip): out = x @ w^T with a fused epilogue.
-// epi 0: out [M, N] bf16; 1: out is the residual [M, N], out = bf16(bf16(x w^T) + out);
-// 2 / 3: w = merged [gate; up] (N = 2I, I % 128 == 0), out = act [M, I] = silu / gelu_tanh(gate) * up.
-void prefill_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int64_t epi, int64_t variant) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w);
-  CHECK_ROWMAJOR(out);
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && N % 256 == 0 && K % 64 == 0, "prefill_gemm: w [N % 256, K % 64]");
-  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "prefill_gemm: alignment");
-  const bool glu = epi == 2 || epi == 3;
-  TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? N / 2 : N), "prefill_gemm: out shape");
-  TORCH_CHECK(!glu || (N / 2) % 128 == 0, "prefill_gemm: GLU needs I % 128 == 0");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  hipserve::PgEpi E{};
-  E.variant = (int)variant;
-  TORCH_CHECK(hipserve::launch_prefill_gemm((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
-                                            w.data_ptr(), w.stride(0), M, N, K, E, cur_stream()),
-              "prefill_gemm: unsupported");
-}
 
 // Prefill GEMM over the packed decode layout (prefill_gemm_packed.hip): wp =
-// pack_decode_weight(w[N, K], glu) (flat, ceil(N/128)*128*K bf16). epi as prefill_gemm
+// pack_decode_weight(w[N, K], glu) (flat, ceil(N/128)*128*K bf16). epi as the FP8 prefill GEMM (PG_EPI_*)
 // (2 / 3 need the glu packing); bias (epi 0 only) bf16 [N] or None; wm 1 or 2.
 void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
                          const c10::optional<at::Tensor>& bias, int64_t wm, int64_t grid, int64_t rw) {
@@ -814,7 +795,7 @@ void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at:
 
 // FP8 W8A8 form: xq [M, K] uint8 e4m3 + xs [M] fp32 (act_quant_fp8), the weight as
 // tiled FP8 parts (ops/quant.py QuantPart.from_fp8: q [N/16, K/256, 4096] uint8 and
-// rs [N] fp32) stacked along N. epi 0 / 1 as prefill_gemm; 2 / 3: parts = (gate, up),
+// rs [N] fp32) stacked along N. epi 0 / 1 = store / residual add; 2 / 3: parts = (gate, up),
 // out = act [M, I] = silu / gelu_tanh(gate) * up.
 void prefill_gemm_f8(at::Tensor& out, const at::Tensor& xq, const at::Tensor& xs, const std::vector<at::Tensor>& q,
                      const std::vector<at::Tensor>& rs, int64_t epi) {
@@ -904,39 +885,6 @@ void act_quant_fp8(at::Tensor& xq, at::Tensor& xs, const at::Tensor& x) {
   hipserve::launch_act_quant_fp8(xq.data_ptr(), xs.data_ptr<float>(), x.data_ptr(), x.stride(0), M, K, cur_stream());
 }
 
-// Grouped (MoE prefill) form: x [tiles * 256, K] expert-sorted rows (moe_align with
-// tile 256, moe_gather), w [E, N, K] (GLU: each expert's merged [gate; up] weight),
-// tile_expert [tiles] int32 from moe_align. No host synchronisation.
-void prefill_gemm_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& tile_expert,
-                          int64_t epi, int64_t variant) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_CONTIG(w);
-  CHECK_ROWMAJOR(out); CHECK_CONTIG(tile_expert);
-  TORCH_CHECK(w.dim() == 3 && tile_expert.scalar_type() == at::kInt, "prefill_gemm_grouped: w [E, N, K], int32 tiles");
-  const int M = x.size(0), K = x.size(1), N = w.size(1);
-  TORCH_CHECK(w.size(2) == K && N % 256 == 0 && K % 64 == 0 && M == tile_expert.numel() * 256,
-              "prefill_gemm_grouped: x rows = 256 * tiles, w [E, N % 256, K % 64]");
-  TORCH_CHECK(epi == 0 || epi == 2, "prefill_gemm_grouped: store or glu epilogue");
-  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 2 ? N / 2 : N), "prefill_gemm_grouped: out shape");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  hipserve::PgEpi E{};
-  E.variant = (int)variant;
-  E.tile_expert = tile_expert.data_ptr<int>();
-  E.b_estride = (long)N * K;
-  TORCH_CHECK(hipserve::launch_prefill_gemm((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
-                                            w.data_ptr(), K, M, N, K, E, cur_stream()),
-              "prefill_gemm_grouped: unsupported");
-}
-
-void pack_glu_rows(at::Tensor& out, const at::Tensor& w) {
-  CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(out);
-  const int N = w.size(-2), K = w.size(-1);
-  const long E = w.dim() == 3 ? w.size(0) : 1;  // [E, 2I, K]: every expert's matrix
-  TORCH_CHECK(N % 256 == 0 && K % 8 == 0 && out.numel() == w.numel(), "pack_glu_rows: [(E,) 2I % 256, K]");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
-  for (long e = 0; e < E; ++e)
-    hipserve::launch_pack_glu_rows(static_cast<unsigned short*>(out.data_ptr()) + e * N * K,
-                                   static_cast<const unsigned short*>(w.data_ptr()) + e * N * K, N / 2, K, cur_stream());
-}
 
 static const void* opt_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
@@ -1282,15 +1230,12 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
-  m.def("prefill_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi, int variant=2) -> ()");
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
   m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");
-  m.def("pack_glu_rows(Tensor(a!) out, Tensor w) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
   m.def("glu_quant(Tensor(a!)? out, Tensor(b!) q8, Tensor(c!) xs, Tensor x, bool gelu) -> ()");
   m.def("act_quant_fp8(Tensor(a!) xq, Tensor(b!) xs, Tensor x) -> ()");
-  m.def("prefill_gemm_grouped(Tensor(a!) out, Tensor x, Tensor w, Tensor tile_expert, int epi, int variant=2) -> ()");
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
@@ -1333,7 +1278,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("pack_decode_weight", &pack_decode_weight);
   m.impl("decode_gemm_partial", &decode_gemm_partial);
   m.impl("decode_gemm_glu", &decode_gemm_glu);
-  m.impl("prefill_gemm", &prefill_gemm);
   m.impl("prefill_gemm_packed", &prefill_gemm_packed);
   m.impl("prefill_gemm_packed_grouped", &prefill_gemm_packed_grouped);
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);
@@ -1341,8 +1285,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("act_quant_fp8", &act_quant_fp8);
   m.impl("fp8_decode_gemm", &fp8_decode_gemm);
   m.impl("glu_quant", &glu_quant);
-  m.impl("pack_glu_rows", &pack_glu_rows);
-  m.impl("prefill_gemm_grouped", &prefill_gemm_grouped);
   m.impl("splitk_add_rmsnorm", &splitk_add_rmsnorm);
   m.impl("splitk_rope_cache", &splitk_rope_cache);
   m.impl("splitk_glu", &splitk_glu);

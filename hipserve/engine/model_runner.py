@@ -171,29 +171,22 @@ class ModelRunner:
                     gguf = ecfg.extra.get("gguf_dense_shadow", os.environ.get("HIPSERVE_QUANT_SHADOW", "0") == "1")
                     self.quant_shadow_bytes = getattr(self, "quant_shadow_bytes", 0) + Q.make_dense_shadows(
                         qws, self.device, (24 << 30) + total // 4, gguf=gguf)
-                    # FP8: plain e4m3 copies for the hipBLASLt FP8 prefill GEMMs
+                    # FP8: which projections prefill on hipBLASLt's FP8 GEMM (a per-call
+                    # re-layout of the tiled copy by default, ops/quant.py FP8_LIB)
                     self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()
         self.init_times["decode_gemm_tune_s"] = round(time.time() - t1, 2)
         t1 = time.time()
         # (TunableOp solution choice for the prefill GEMMs was measured no faster than the
-        # heuristic on sustained prefill chains, profiles/r1_prefill_gemm_tunableop.md: removed)
-        # prefill GEMMs: the hand-written kernel with fused epilogues where it beats
-        # hipBLASLt + the separate elementwise kernel (ops/pgemm.py), timed per shape
-        self.pgemm_report = []
-        if self.device.type == "cuda" and ecfg.extra.get("prefill_gemm", True):
-            self.pgemm_report = self._tune_prefill_gemm()
+        # heuristic on sustained prefill chains, profiles/r1_prefill_gemm_tunableop.md, and
+        # the bf16 prefill_gemm.hip kernels lost to hipBLASLt everywhere: both removed)
         # ragged prefill chunks: hipBLASLt's heuristic picks slower kernels for some
         # token counts (Llama-3-8B: the 4-projection chain takes 21.7 ms at 7,393 rows
         # vs 18.8 ms at 8,192, tools/bench_prefill_m.py); rank 0 times the model's
         # prefill GEMMs per 256-row count once and pads a chunk to the fastest count at
         # or above it (padding rows: token 0, no KV write, outputs unused)
-        self.init_times["prefill_gemm_tune_s"] = round(time.time() - t1, 2)
-        t1 = time.time()
         self.prefill_pad = None
-        pg_all = bool(self.pgemm_report) and all(r["pgemm"] for r in self.pgemm_report)
-        if (self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0
-                and not pg_all):  # the hand-written GEMM has no row-count cliffs
+        if self.device.type == "cuda" and ecfg.extra.get("prefill_pad", True) and tp.rank == 0:
             self.prefill_pad = self._probe_prefill_pad()
         # device penalty state: one slot per concurrently running sequence (a slot is
         # held from the first sample to finish / abort / preemption), so a slot is
@@ -334,33 +327,6 @@ class ModelRunner:
             raise RuntimeError(f"not enough GPU memory for the KV cache (budget {budget / 2**30:.1f} GiB)")
         # all TP ranks must agree on the pool size
         return self.tp.min_int(n)
-
-    @torch.inference_mode()
-    def _tune_prefill_gemm(self) -> list[dict]:
-        from ..ops import pgemm
-
-        layers = getattr(self.model, "layers", None)
-        if pgemm.MODE == "0" or not layers:
-            return []
-        lw = layers[0]
-        units = set()
-        for kind, w in (("plain", lw.wqkv), ("add", lw.wo), ("glu", lw.wgu), ("add", lw.wd)):
-            if not pgemm.fits(w):
-                continue
-            if kind == "add" and (self.tp.world_size > 1 or getattr(lw, "post_attn_norm", None) is not None):
-                continue
-            if kind == "glu" and (self.mcfg.hidden_act not in ("silu", "gelu_tanh") or (w.shape[0] // 2) % 128):
-                continue
-            units.add((kind, w.shape[0], w.shape[1]))
-        if lw.w13 is not None and pgemm.moe_ok(lw.w13, lw.w2) and self.mcfg.hidden_act == "silu":
-            E, N13, H = lw.w13.shape
-            units.add(("moe", E, N13 // 2, H, self.mcfg.num_experts_per_tok))
-        if not units:
-            return []
-        M = min(self.ecfg.max_num_batched_tokens, 8192)
-        if M < pgemm.MIN_ROWS:
-            return []
-        return pgemm.tune(units, M, self.device, self.ops)
 
     def _probe_prefill_pad(self) -> dict | None:
         """{rows rounded up to 256: the row count (>= it, <= the token budget) whose

@@ -616,12 +616,12 @@ class LlamaModel:
         L = len(self.layers)
         tp1 = self.tp.world_size == 1
         for i, lw in enumerate(self.layers):
-            # prefill-sized batches: the hand-written GEMM where start-up timing chose it
-            # (ops/pgemm.py), with the residual add / SiLU-GLU in its epilogue
+            # prefill-sized batches: FP8 W8A8 (ops/pgemm.py), the packed-layout GEMM of a
+            # single-layout model (gemm.linear dispatches PackedLinear), else hipBLASLt
             if x8 is not None:
                 qkv = pgemm.f8_gemm(xn, lw.wqkv, 0, x8=x8)
             else:
-                qkv = pgemm.gemm(xn, lw.wqkv) if pgemm.use("plain", lw.wqkv, T) else self.linear(xn, lw.wqkv)
+                qkv = self.linear(xn, lw.wqkv)
             if lw.bqkv is not None:
                 qkv += lw.bqkv
             if lw.q_norm is not None:  # per-head RMSNorm of q and k, before RoPE
@@ -639,9 +639,6 @@ class LlamaModel:
             x8 = self._x8p(xn, lw.wgu, glu=True)
             if tp1 and lw.post_attn_norm is None and isinstance(lw.wo, gemm.PackedLinear) and T > 64:
                 gemm.packed_prefill(attn, lw.wo, 1, out=residual)  # residual += o_proj(attn), packed layout
-                ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
-            elif tp1 and lw.post_attn_norm is None and pgemm.use("add", lw.wo, T):
-                pgemm.gemm_add_(residual, attn, lw.wo)  # residual += o_proj(attn), in the GEMM epilogue
                 ops.rmsnorm(xn, residual, lw.ln2, eps, out8=x8)
             elif tp1 and lw.post_attn_norm is None and Q.qprefill_ok(lw.wo, T):
                 Q.qprefill(attn, lw.wo, 1, out=residual)  # GGUF blocks, residual add in the epilogue
@@ -668,8 +665,6 @@ class LlamaModel:
                         act = pgemm.f8_gemm(xn, lw.wgu, 3 if gelu else 2, x8=x8)
                 elif isinstance(lw.wgu, gemm.PackedLinear) and lw.wgu.glu:  # GLU in the packed GEMM's epilogue
                     act = gemm.packed_glu(xn, lw.wgu, gelu)
-                elif cfg.hidden_act in ("silu", "gelu_tanh") and pgemm.use("glu", lw.wgu, T):
-                    act = pgemm.gemm_glu(xn, lw.wgu, gelu)
                 elif cfg.hidden_act in ("silu", "gelu_tanh") and Q.qprefill_ok(lw.wgu, T, glu=True):
                     act = Q.qprefill(xn, lw.wgu, 3 if gelu else 2)  # GGUF blocks, GLU in the epilogue
                 if act8 is not None:
@@ -679,14 +674,12 @@ class LlamaModel:
                     act = torch.empty(T, self.inter, device=xn.device, dtype=xn.dtype)
                     self.act_and_mul(act, gu)
                 if act8 is None and (tp1 and lw.post_ff_norm is None and not (ds is not None and i < len(ds))
-                                     and (pgemm.use("add", lw.wd, T) or Q.qprefill_ok(lw.wd, T)
+                                     and (Q.qprefill_ok(lw.wd, T)
                                           or (isinstance(lw.wd, gemm.PackedLinear) and T > 64))):
                     if isinstance(lw.wd, gemm.PackedLinear):
                         gemm.packed_prefill(act, lw.wd, 1, out=residual)
-                    elif isinstance(lw.wd, Q.QuantWeight):
-                        Q.qprefill(act, lw.wd, 1, out=residual)
                     else:
-                        pgemm.gemm_add_(residual, act, lw.wd)
+                        Q.qprefill(act, lw.wd, 1, out=residual)
                     ops.rmsnorm(xn, residual, nxt, eps, out8=x8n)
                     x8 = x8n
                     continue
@@ -970,25 +963,24 @@ class LlamaModel:
         return opts[-1]
 
     def moe_grouped(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
-        """Prefill-sized MoE without a host synchronisation: routing (top-k kernel),
-        expert-sorted 16-row-padded slots with per-expert end offsets (moe_align),
-        the token rows gathered into that order (moe_gather), the two expert GEMMs
-        as ONE grouped launch each on the hand-written prefill GEMM
-        (csrc/kernels/prefill_gemm.hip, 256-row expert tiles, expert ids read on the
-        device: no host round trip, graph-capturable) with the SiLU-GLU in the
-        gate|up epilogue, then the weighted combine (moe_combine). Shapes it does not
-        cover fall back to hipBLASLt grouped GEMMs (``torch._grouped_mm``, which reads
-        the group offsets on the host on this ROCm build) + silu_and_mul."""
+        """Prefill-sized MoE: routing (top-k kernel), expert-sorted padded slots with
+        per-expert end offsets (moe_align), the token rows gathered into that order
+        (moe_gather), the two expert GEMMs as ONE grouped launch each, then the weighted
+        combine (moe_combine). The grouped GEMMs: the packed-layout kernel
+        (prefill_gemm_packed.hip kGroup, expert ids read on the device: no host round
+        trip, graph-capturable, SiLU-GLU in the gate|up epilogue) when the experts are
+        kept only in the packed layout or HIPSERVE_MOE_PACKED_PREFILL=1, else hipBLASLt's
+        grouped GEMM (``torch._grouped_mm``, which reads the group offsets on the host on
+        this ROCm build) + silu_and_mul."""
         op = torch.ops.hipserve
         cfg = self.cfg
         E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
         T, dev = x.shape[0], x.device
         # packed experts (the decode copy, moe_packed): the packed-layout grouped GEMM
-        # (prefill_gemm_packed.hip kGroup) over (128 * wm)-row tiles; else 256-row tiles
-        # for the hand-written grouped GEMM (ops/pgemm.py), 16-row ones for hipBLASLt's
+        # (prefill_gemm_packed.hip kGroup) over (128 * wm)-row tiles; 16-row ones for hipBLASLt's
         packed = self.moe_packed_prefill(lw)
         P = T * k
-        tile = 128 * gemm.PW_WM if packed else (256 if pgemm.moe_ok(lw.w13, lw.w2) else 16)
+        tile = 128 * gemm.PW_WM if packed else 16
         cap = -(-(P + E * (tile - 1)) // tile) * tile
         logits = gemm.linear(x, lw.router)
         w = torch.empty(T, k, dtype=torch.float32, device=dev)
@@ -1008,11 +1000,6 @@ class LlamaModel:
             op.prefill_gemm_packed_grouped(act, xs, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
             op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
-        elif tile == 256:  # hand-written grouped expert GEMMs, SiLU-GLU in the first's epilogue
-            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-            op.prefill_gemm_grouped(act, xs, lw.w13, tile_expert, 2, pgemm.VARIANT)
-            y = torch.empty(cap, H, dtype=x.dtype, device=dev)
-            op.prefill_gemm_grouped(y, act, lw.w2, tile_expert, 0, pgemm.VARIANT)
         else:
             gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)

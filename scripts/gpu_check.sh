@@ -124,7 +124,6 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
     f16test) run_one tests/test_gguf_gpu.py ;;
     fusedtest) run_one tests/test_fused_decode_gpu.py ;;
-    pgtest) run_one tests/test_prefill_gemm_gpu.py ;;
     pwtest) run_one tests/test_prefill_gemm_packed_gpu.py ;;
     longtest) run_one tests/test_long_context_gpu.py ;;
     kerneltest) run_one tests/test_kernels_gpu.py ;;

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""The hand-written prefill GEMM (csrc/kernels/prefill_gemm.hip) vs hipBLASLt
+"""The hand-written prefill GEMMs (packed bf16: prefill_gemm_packed.hip; FP8 W8A8:
+prefill_gemm.hip) vs hipBLASLt
 (``F.linear``) on the Llama-3-8B / 70B-TP8 prefill shapes at M = 8192 rows, random
 [-1, 1) operands (cdna_hip_programming.md rule 25), one weight per layer so the 32
 calls stream 32 different weights. Also the fused units: GLU (gate|up GEMM + SiLU·mul)
@@ -61,7 +62,6 @@ def main():
         ws = [rnd(N, K) * 0.05 for _ in range(L)]
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         t_blas = time_fn(lambda: [F.linear(x, w) for w in ws])
-        t_pg = time_fn(lambda: [op.prefill_gemm(out, x, w, 0, 2) for w in ws])
         # the packed-layout kernel (prefill_gemm_packed.hip) on the decode copy of each weight
         glu_pack = name == "gu"
         wps = []
@@ -70,9 +70,9 @@ def main():
             op.pack_decode_weight(wp, w, False)
             wps.append(wp)
         t_pw = {wm: time_fn(lambda: [op.prefill_gemm_packed(out, x, wp, N, 0, None, wm) for wp in wps]) for wm in (1, 2)}
-        r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4), "pgemm_ms": round(t_pg, 4),
+        r = {"shape": name, "M": M, "N": N, "K": K, "blas_ms": round(t_blas, 4),
              "packed_wm1_ms": round(t_pw[1], 4), "packed_wm2_ms": round(t_pw[2], 4),
-             "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1), "pgemm_TFs": round(2 * M * N * K / t_pg / 1e9, 1),
+             "blas_TFs": round(2 * M * N * K / t_blas / 1e9, 1),
              "packed_TFs": round(2 * M * N * K / min(t_pw.values()) / 1e9, 1)}
         if a.fp8:
             from hipserve.ops import pgemm, quant as Q
@@ -103,13 +103,11 @@ def main():
                 r["blas_fp8_rowwise"] = f"unsupported: {type(e).__name__}: {str(e)[:120]}"
         if name == "gu":  # GEMM + SiLU-GLU unit
             act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
-            wg = ws  # the GLU epilogue reads the merged [gate; up] weight as stored
 
             def blas_glu():
                 for w in ws:
                     ops.silu_and_mul(act, F.linear(x, w))
             r["blas_unit_ms"] = round(time_fn(blas_glu), 4)
-            r["pgemm_unit_ms"] = round(time_fn(lambda: [op.prefill_gemm(act, x, p, 2) for p in wg]), 4)
             for w, wp in zip(ws, wps):
                 op.pack_decode_weight(wp, w, True)
             r["packed_unit_ms"] = {wm: round(time_fn(lambda: [op.prefill_gemm_packed(act, x, wp, N, 2, None, wm)
@@ -121,21 +119,20 @@ def main():
                 for w in ws:
                     res.add_(F.linear(x, w))
             r["blas_unit_ms"] = round(time_fn(blas_add), 4)
-            r["pgemm_unit_ms"] = round(time_fn(lambda: [op.prefill_gemm(res, x, w, 1) for w in ws]), 4)
             r["packed_unit_ms"] = {wm: round(time_fn(lambda: [op.prefill_gemm_packed(res, x, wp, N, 1, None, wm)
                                                               for wp in wps]), 4) for wm in (1, 2)}
         rows.append(r)
         print(json.dumps(r), flush=True)
         del ws, wps, x, out
         torch.cuda.empty_cache()
-    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | prefill_gemm ms (TF/s) | packed wm1 / wm2 ms (TF/s) "
-          f"| unit: hipBLASLt + ew | unit: fused | unit: packed | FP8 quant + GEMM ms (TF/s) |")
-    print("|---|---|---:|---:|---:|---:|---:|---:|---:|")
+    print(f"\n| shape | M x N x K | hipBLASLt ms (TF/s) | packed wm1 / wm2 ms (TF/s) "
+          f"| unit: hipBLASLt + ew | unit: packed | FP8 quant + GEMM ms (TF/s) |")
+    print("|---|---|---:|---:|---:|---:|---:|")
     for r in rows:
         f8 = f"{r['fp8_ms']} ({r['fp8_TFs']})" if "fp8_ms" in r else "—"
         print(f"| {r['shape']} | {r['M']}x{r['N']}x{r['K']} | {r['blas_ms']} ({r['blas_TFs']}) | "
-              f"{r['pgemm_ms']} ({r['pgemm_TFs']}) | {r['packed_wm1_ms']} / {r['packed_wm2_ms']} ({r['packed_TFs']}) | "
-              f"{r.get('blas_unit_ms', '—')} | {r.get('pgemm_unit_ms', '—')} | {r.get('packed_unit_ms', '—')} | {f8} |")
+              f"{r['packed_wm1_ms']} / {r['packed_wm2_ms']} ({r['packed_TFs']}) | "
+              f"{r.get('blas_unit_ms', '—')} | {r.get('packed_unit_ms', '—')} | {f8} |")
 
 
 if __name__ == "__main__":

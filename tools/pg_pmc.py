@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Minimal driver for PMC passes on one prefill-GEMM shape: 3 hipBLASLt calls then 3
-hand-written prefill_gemm calls per variant in $PG_VARIANTS (default 2) on the same operands, so one rocprofv3
+hand-written packed prefill GEMM calls per variant in $PG_VARIANTS (p1 / p2 = wm; default p1) on the same operands, so one rocprofv3
 --pmc pass gives per-dispatch counters of both kernels side by side.
 usage: python tools/pg_pmc.py [M N K]"""
 import os
@@ -21,14 +21,12 @@ for _ in range(3):
     F.linear(x, w)
 torch.cuda.synchronize()
 wp = None
-for v in os.environ.get("PG_VARIANTS", "2").split():
+for v in os.environ.get("PG_VARIANTS", "p1").split():
     for _ in range(3):
         if v.startswith("p"):  # packed-layout kernel (prefill_gemm_packed.hip), p1 / p2 = wm
             if wp is None:
                 wp = torch.empty(-(-N // 128) * 128 * K, device="cuda", dtype=torch.bfloat16)
                 torch.ops.hipserve.pack_decode_weight(wp, w, False)
             torch.ops.hipserve.prefill_gemm_packed(out, x, wp, N, 0, None, int(v[1]), 0, int(os.environ.get("PW_RW", "4")))
-        else:
-            torch.ops.hipserve.prefill_gemm(out, x, w, 0, int(v))
     torch.cuda.synchronize()
 print("ok", M, N, K)
