@@ -223,26 +223,33 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
   const int kt0 = window > 0 ? max(0, ctx - qlen + r0 - window + 1) / PA2_KT : 0;
   const int* btab = block_tables + (long)seq * bt_stride;
   const long hstride = (long)block_size * D;
+  // block sizes are powers of two (launcher check): shifts, not integer divisions,
+  // in the per-tile paging math (the divisions were ~1/3 of the tile's VALU)
+  const int bsh = __builtin_ctz(block_size), bmask = block_size - 1;
+  // the block ids of this workgroup's key range, staged in LDS once: a per-piece global
+  // load of the id right before each K / V load made hipcc wait vmcnt(0) four times per
+  // tile, draining the two tiles of K / V loads kept in flight ahead of the MFMAs
+  extern __shared__ int bts[];
+  const int blk_lo = (kt0 * PA2_KT) >> bsh, blk_hi = (min(nkt * PA2_KT, ctx) - 1) >> bsh;
+  for (int i = threadIdx.x; i <= blk_hi - blk_lo; i += 64 * NWV) bts[i] = btab[blk_lo + i];
+  __syncthreads();
 
   // staging: NP K pieces + NP V^T pieces of 16 B per thread per tile
   // two register sets: tile kt+2 loads while tile kt+1's registers wait for their LDS write
   u16x8 ska[NP], sva[NP], skb[NP], svb[NP];
-  // block sizes are powers of two (launcher check): shifts, not integer divisions,
-  // in the per-tile paging math (the divisions were ~1/3 of the tile's VALU)
-  const int bsh = __builtin_ctz(block_size), bmask = block_size - 1;
   auto stage_load = [&](u16x8(&sk)[NP], u16x8(&sv)[NP], int kt) {
     const int kbase = kt * PA2_KT;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int p = tid + NT * i;
       const int key = min(kbase + (p >> 4), ctx - 1);
-      sk[i] = *reinterpret_cast<const u16x8*>(k_cache + ((long)btab[key >> bsh] * nkv + kh) * hstride +
+      sk[i] = *reinterpret_cast<const u16x8*>(k_cache + ((long)bts[(key >> bsh) - blk_lo] * nkv + kh) * hstride +
                                               (long)(key & bmask) * D + (p & 15) * 8);
       // V^T: 16-key group sc, row d, 8-key half: one block's [D][16] chunk per 256 threads
       const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
       int vkey = kbase + 16 * sc + 8 * k8;
       if (vkey > ctx - 1) vkey = (ctx - 1) & ~7;
-      sv[i] = *reinterpret_cast<const u16x8*>(v_cache + ((long)btab[vkey >> bsh] * nkv + kh) * hstride +
+      sv[i] = *reinterpret_cast<const u16x8*>(v_cache + ((long)bts[(vkey >> bsh) - blk_lo] * nkv + kh) * hstride +
                                               (long)d * block_size + (vkey & bmask));
     }
   };
@@ -283,13 +290,25 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[h2][r] = 0.f;
       if (prio) __builtin_amdgcn_s_setprio(1);  // MFMA cluster: the partner wave's softmax VALU waits
+      // K fragments read one k-step ahead of their MFMAs (two register sets): hipcc left to
+      // itself waited out each fragment's LDS latency right before its MFMA
+      u16x8 kf[2][2];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+      for (int h2 = 0; h2 < 2; ++h2) kf[0][h2] = *reinterpret_cast<const u16x8*>(kb + (32 * h2) * PA2_KLD);
 #pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {  // two independent accumulation chains interleaved
-          const u16x8 a = *reinterpret_cast<const u16x8*>(kb + (32 * h2) * PA2_KLD + 16 * ks);
-          st[h2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), qf[ks], st[h2], 0, 0, 0);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) {
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+            kf[(ks + 1) & 1][h2] = *reinterpret_cast<const u16x8*>(kb + (32 * h2) * PA2_KLD + 16 * (ks + 1));
         }
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads of k-step ks + 1 ahead of k-step ks's MFMAs
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)  // two independent accumulation chains interleaved
+          st[h2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[ks & 1][h2]), qf[ks], st[h2],
+                                                           0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (prio) __builtin_amdgcn_s_setprio(0);
       // diagonal tile (causal mask) or a tile crossing some row's window start
       if (kbase + PA2_KT - 1 > wmin_pos || (window > 0 && kbase <= wmax_key - window)) {
@@ -388,7 +407,9 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               int block_size, float scale, int window, hipStream_t s) {
   if (ntiles <= 0) return;
   const int G = nq / nkv;
+  // v2 keeps the sequence's block ids in LDS next to its 70 KiB K / V ring (160 KiB per CU)
   if (D == 128 && block_size % 16 == 0 && (block_size & (block_size - 1)) == 0 && G >= 2 && (G & (G - 1)) == 0 &&
+      (size_t)bt_stride * sizeof(int) <= 64 * 1024 &&
       !getenv_flag("HIPSERVE_PREFILL_ATTN_V1")) {
     const char* ew = getenv("HIPSERVE_PREFILL_ATTN_WAVES");  // 8 (default) or 4 waves per workgroup
     const int nwv = (ew != nullptr && atoi(ew) == 4) ? 4 : 8;
@@ -405,10 +426,19 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
     auto* q2 = static_cast<const unsigned short*>(q);
     auto* k2 = static_cast<const unsigned short*>(k_cache);
     auto* v2 = static_cast<const unsigned short*>(v_cache);
+    // block ids of one sequence (the per-workgroup key range is at most this) in dynamic LDS
+    const size_t bt_lds = (size_t)bt_stride * sizeof(int);
 #define PA2_LAUNCH(hg, nw)                                                                                  \
-  prefill_attn_v2_kernel<hg, nw><<<g2, 64 * nw, 0, s>>>(o2, out_stride, q2, q_stride, k2, v2, block_tables, \
-                                                        bt_stride, cu_q, ctx_lens, tiles, nq, nkv, block_size, scale, \
-                                                        window, prio)
+  do {                                                                                                      \
+    static bool attr = [] { /* static 70 KiB + the block ids: above the 64 KiB default (160 KiB per CU) */ \
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&prefill_attn_v2_kernel<hg, nw>),            \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;      \
+    }();                                                                                                    \
+    (void)attr;                                                                                             \
+    prefill_attn_v2_kernel<hg, nw><<<g2, 64 * nw, bt_lds, s>>>(o2, out_stride, q2, q_stride, k2, v2,         \
+                                                               block_tables, bt_stride, cu_q, ctx_lens, tiles,  \
+                                                               nq, nkv, block_size, scale, window, prio);     \
+  } while (0)
     if (nwv == 8) {
       if (HG == 8) PA2_LAUNCH(8, 8);
       else if (HG == 4) PA2_LAUNCH(4, 8);
