@@ -22,6 +22,20 @@
 
 namespace hipserve {
 
+// max / sum of v over lanes l and l ^ 32 with one v_permlane32_swap (gfx950: the two
+// results hold, per lane, v of lane l and of lane l ^ 32 in some order) instead of an
+// LDS round trip (ds_bpermute) that the next instruction waits on
+HS_DEVICE float xor32_max(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+HS_DEVICE float xor32_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
 typedef unsigned short u16x4v __attribute__((ext_vector_type(4)));
 
 template <int D>
@@ -139,7 +153,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
         o[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pb[s], o[nb], 0, 0, 0);
       }
   }
-  l_run += __shfl_xor(l_run, 32, 64);
+  l_run = xor32_sum(l_run);
   const float inv = 1.f / l_run;
   if (wrow0 + qi < qlen) {
     unsigned short* op = out + (long)(q0 + wrow0 + qi) * out_stride + (long)h * D;
@@ -237,20 +251,28 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
   // staging: NP K pieces + NP V^T pieces of 16 B per thread per tile
   // two register sets: tile kt+2 loads while tile kt+1's registers wait for their LDS write
   u16x8 ska[NP], sva[NP], skb[NP], svb[NP];
+  // staging addresses: block id x the elements of one block of all kv heads (< 2^32: one
+  // 32 x 32 -> 64-bit multiply-add per piece) + a 32-bit in-block offset; the kv head's
+  // base is folded into the workgroup's K / V pointers
+  const unsigned blk_elems = (unsigned)(nkv * hstride);
+  const unsigned short* kc_h = k_cache + (long)kh * hstride;
+  const unsigned short* vc_h = v_cache + (long)kh * hstride;
   auto stage_load = [&](u16x8(&sk)[NP], u16x8(&sv)[NP], int kt) {
     const int kbase = kt * PA2_KT;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int p = tid + NT * i;
       const int key = min(kbase + (p >> 4), ctx - 1);
-      sk[i] = *reinterpret_cast<const u16x8*>(k_cache + ((long)bts[(key >> bsh) - blk_lo] * nkv + kh) * hstride +
-                                              (long)(key & bmask) * D + (p & 15) * 8);
+      const unsigned kid = (unsigned)bts[(key >> bsh) - blk_lo];
+      sk[i] = *reinterpret_cast<const u16x8*>(kc_h + ((unsigned long)kid * blk_elems +
+                                                      (unsigned)((key & bmask) * D + (p & 15) * 8)));
       // V^T: 16-key group sc, row d, 8-key half: one block's [D][16] chunk per 256 threads
       const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
       int vkey = kbase + 16 * sc + 8 * k8;
       if (vkey > ctx - 1) vkey = (ctx - 1) & ~7;
-      sv[i] = *reinterpret_cast<const u16x8*>(v_cache + ((long)bts[(vkey >> bsh) - blk_lo] * nkv + kh) * hstride +
-                                              (long)d * block_size + (vkey & bmask));
+      const unsigned vid = (unsigned)bts[(vkey >> bsh) - blk_lo];
+      sv[i] = *reinterpret_cast<const u16x8*>(vc_h + ((unsigned long)vid * blk_elems +
+                                                      (unsigned)(d * block_size + (vkey & bmask))));
     }
   };
   auto stage_store = [&](const u16x8(&sk)[NP], const u16x8(&sv)[NP], int buf) {
@@ -311,21 +333,33 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
       }
       if (prio) __builtin_amdgcn_s_setprio(0);
       // diagonal tile (causal mask) or a tile crossing some row's window start
+      // (key offsets inside the tile are compile-time per accumulator slot: one compare +
+      // select per score against the lane's limit, the window test only when one is set)
       if (kbase + PA2_KT - 1 > wmin_pos || (window > 0 && kbase <= wmax_key - window)) {
+        const int lim = pos - kbase - 8 * half;  // slot offset > lim: a future key
+        if (window <= 0) {
 #pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
+          for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kbase + 32 * h2 + 16 * (r >> 3) + 8 * half + 4 * ((r >> 2) & 1) + (r & 3);
-            if (key > pos || (window > 0 && key <= pos - window)) st[h2][r] = -INFINITY;
-          }
+            for (int r = 0; r < 16; ++r)
+              if (32 * h2 + 16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3) > lim) st[h2][r] = -INFINITY;
+        } else {
+          const int wlo = lim - window;  // slot offset <= wlo: before the window
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int off = 32 * h2 + 16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3);
+              if (off > lim || off <= wlo) st[h2][r] = -INFINITY;
+            }
+        }
       }
       float mx = -1e30f;
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[h2][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor32_max(mx);
       const float m_new = fmaxf(m_run, mx * sl2);
       // deferred rescale: the running max is kept while no row's max grew by more than
       // 8 (log2 units), so P = exp2(s - m_run) stays <= 256 (exact enough in bf16 / fp32;
@@ -339,14 +373,14 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
           for (int r = 0; r < 16; ++r) o[nb][r] *= alpha;
         m_run = m_new;
       }
-      float psum = 0.f;
+      float ps[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains, not one 32-add dependency chain
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         bf16x8 pb[2];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = __builtin_amdgcn_exp2f(fmaf(st[h2][r], sl2, -m_run));
-          psum += p;
+          ps[r & 3] += p;
           pb[r >> 3][r & 7] = static_cast<__bf16>(p);
         }
         if (prio) __builtin_amdgcn_s_setprio(1);
@@ -361,7 +395,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
         }
         if (prio) __builtin_amdgcn_s_setprio(0);
       }
-      l_run += psum;
+      l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
     }
   };
 
@@ -383,7 +417,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     __syncthreads();
   }
   if (!wactive) return;
-  l_run += __shfl_xor(l_run, 32, 64);
+  l_run = xor32_sum(l_run);
   const float inv = 1.f / l_run;
   if (wrow0 + qi < qlen) {
     unsigned short* op = out + (long)(q0 + wrow0 + qi) * out_stride + (long)h * D;
