@@ -196,6 +196,9 @@ static bool getenv_flag(const char* name) {
 
 constexpr int PA2_KT = 64, PA2_KLD = 128 + 8, PA2_VLD = 64 + 8;
 
+// (A stagger — waves 4-7 issuing each tile's P.V one tile late, a third LDS buffer holding
+// its V^T, MI355X_MICROARCH.md "Two waves per SIMD" item 9 — needed 16 more VGPRs than the
+// 256 of two waves per SIMD and spilled: 1.4-1.5x slower, profiles/r5_prefill_attn_bench.log.)
 template <int HG, int NWV>
 __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     unsigned short* __restrict__ out, long out_stride, const unsigned short* __restrict__ q, long q_stride,
@@ -206,8 +209,9 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
   constexpr int D = 128, KS = 8, NB = 4;
   constexpr int RB = NWV / HG, QR = 32 * RB, SUB = 128 / QR;
   constexpr int NT = 64 * NWV, NP = 1024 / NT;  // threads; K (and V^T) 16-byte pieces per thread
-  __shared__ __attribute__((aligned(16))) unsigned short kl[2][PA2_KT * PA2_KLD];
-  __shared__ __attribute__((aligned(16))) unsigned short vl[2][D * PA2_VLD];
+  constexpr int NBUF = 2;
+  __shared__ __attribute__((aligned(16))) unsigned short kl[NBUF][PA2_KT * PA2_KLD];
+  __shared__ __attribute__((aligned(16))) unsigned short vl[NBUF][D * PA2_VLD];
 
   // dispatch order (x fastest) -> (kv-head group fastest, host tile, heavier sub-tile first):
   // with the host tiles sorted by descending causal work (model_runner) the largest
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     for (int r = 0; r < 16; ++r) o[nb][r] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
 
-  auto compute = [&](int kt, int buf) {
+  auto compute = [&](int kt, int buf) __attribute__((always_inline)) {
     const int kbase = kt * PA2_KT;
     if (wactive && kbase <= wmax_key && (window <= 0 || kbase + PA2_KT - 1 > wmin_pos - window)) {
       const unsigned short* kb = &kl[buf][qi * PA2_KLD + 8 * half];
@@ -399,22 +403,28 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     }
   };
 
+  auto run = [&](int kt, int buf) __attribute__((always_inline)) { compute(kt, buf); };
+  auto nxt = [](int b) __attribute__((always_inline)) { return b + 1 == NBUF ? 0 : b + 1; };
+
   stage_load(ska, sva, kt0);
   if (kt0 + 1 < nkt) stage_load(skb, svb, kt0 + 1);
   stage_store(ska, sva, 0);
   __syncthreads();
+  int bc = 0;  // LDS buffer of tile kt
   for (int kt = kt0; kt < nkt; kt += 2) {
-    // tile kt in LDS buffer 0; set b holds tile kt+1
+    const int b1 = nxt(bc), b2 = nxt(b1);
+    // tile kt in buffer bc; set b holds tile kt+1
     if (kt + 2 < nkt) stage_load(ska, sva, kt + 2);
-    compute(kt, 0);
-    if (kt + 1 < nkt) stage_store(skb, svb, 1);
+    run(kt, bc);
+    if (kt + 1 < nkt) stage_store(skb, svb, b1);
     __syncthreads();
     if (kt + 1 >= nkt) break;
-    // tile kt+1 in buffer 1; set a holds tile kt+2
+    // tile kt+1 in buffer b1; set a holds tile kt+2
     if (kt + 3 < nkt) stage_load(skb, svb, kt + 3);
-    compute(kt + 1, 1);
-    if (kt + 2 < nkt) stage_store(ska, sva, 0);
+    run(kt + 1, b1);
+    if (kt + 2 < nkt) stage_store(ska, sva, b2);
     __syncthreads();
+    bc = b2;
   }
   if (!wactive) return;
   l_run = xor32_sum(l_run);
