@@ -112,6 +112,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     attnbench) BENCH_PREFILL_LONG=1 BENCH_PREFILL_VERS=v2w8 timeout -k 10 300 python -u tools/bench_ops.py prefill > $OUT/attn_bench.log 2>&1; rc=$?; cat $OUT/attn_bench.log; [ $rc -eq 0 ] ;;
     b8_chunk16k) bench_named b8_chunk16k -- --max-num-batched-tokens 16384 ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
+    enginetest) run_one tests/test_engine_gpu.py ;;
     g27fp8_res) bench_named g27fp8_res HIPSERVE_FP8_PREFILL_LIB=resident -- --model gemma-3-27b --quantization fp8 ;;
     q3int8_noshadow) bench_named q3int8_noshadow HIPSERVE_FUSED_DECODE=1 HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 ;;
     f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
