@@ -49,7 +49,7 @@ def test_single_layout_decode_above_64_rows():
     sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
     prompts = [[1] + [(7 * i + j) % 500 + 3 for j in range(5 + i % 13)] for i in range(80)]
     g = _engine(False, single="1", max_num_seqs=96)
-    assert g.runner.single_layout and max(g.runner.graphs) > 64
+    assert g.runner.single_layout and max(k[0] for k in g.runner.graphs) > 64
     e = _engine(True, single="1", max_num_seqs=96)
     two = _engine(True, single="0", max_num_seqs=96)
     rg, re_, rt = g.generate(prompts, sp), e.generate(prompts, sp), two.generate(prompts, sp)
