@@ -151,6 +151,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     tptest) timeout -k 10 1000 python -u -m pytest tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread \
               -p no:cacheprovider > $OUT/test_tp_gpu.log 2>&1; rc=$?; tail -n 20 $OUT/test_tp_gpu.log; [ $rc -eq 0 ] ;;
     prof_q4) prof_run profq --quantization q4_k_m ;;
+    prof_g27) prof_run profg27 --model gemma-3-27b ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     prof70) prof_run prof70 --model llama-3-70b ;;
