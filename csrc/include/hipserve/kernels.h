@@ -166,7 +166,8 @@ int decode_chain_sync_words(int tilesA);
 bool decode_chain_supported(int M, int NA, int KA, int SA, int NB, int SB, bool glu);
 bool launch_decode_chain(const void* xa, long xa_stride, const void* wa, float* wsa, void* residual, float* sq,
                          int NA, int KA, int SA, const void* wb, const void* gamma, float eps, void* act,
-                         long act_stride, float* wsb, int NB, int SB, bool glu, int* sync, int M, hipStream_t s);
+                         long act_stride, float* wsb, int NB, int SB, bool glu, int* sync, int M, hipStream_t s,
+                         unsigned long long* dbg = nullptr);
 
 // prefill epilogues (prefill_gemm.hip FP8 kernel, prefill_gemm_packed.hip):
 //   PG_EPI_STORE  C = bf16(acc)

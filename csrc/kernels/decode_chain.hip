@@ -16,10 +16,12 @@
 //    1 / rms from the tile sums (fixed order) and stage x = bf16(h * rs * w) into LDS
 //    instead of reading a materialised normalised copy. The result equals the unfused
 //    chain except where the reassociated sum of squares moves 1 / rms by an ulp.
-//  * Hand-offs use the agent-scope recipe (cdna_hip_programming.md §6 Guideline 16):
-//    plain stores -> every wave s_waitcnt vmcnt(0) -> barrier -> one lane release fence
-//    -> vmcnt(0) -> relaxed agent atomic; the receiving lane acquires (buffer_inv sc1) and
-//    waits before the barrier that precedes every load of the handed-off bytes.
+//  * Hand-offs are write-through (cdna_hip_programming.md §6 Guideline 16 R1, the sc1
+//    rows of the hand-off table): every handed-off byte (partial slabs, the new residual,
+//    the tile sums) is stored sc1, every storing wave drains (s_waitcnt vmcnt(0)) before
+//    the barrier behind which one lane adds to the counter, and EVERY load of those bytes
+//    is an sc1 load — so no release fence (buffer_wbl2: ~10 us here with the slabs dirty
+//    in L2) and no acquire fence is needed.
 //  * No deadlock: producers never wait, and blocks are dispatched in index order, so
 //    every producer is resident or finished before a consumer takes a slot. (At 64 rows
 //    the norm staging needs ~146 VGPRs, so one block per CU: consumers start on the CUs
@@ -49,6 +51,39 @@ HS_DEVICE void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 typedef __attribute__((address_space(1))) int gint;
 HS_DEVICE gint* gw(int* p) { return (gint*)p; }
 
+// write-through hand-off stores / loads (sc1): buffer ops over a raw resource
+constexpr int kSc1 = 16;  // buffer aux bit of sc1 on gfx950
+HS_DEVICE __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// sum over S slabs (byte stride `slab`) of 8 consecutive fp32 at byte offset `off`, slab
+// order 0, 1, ... (splitk_add_rmsnorm's order), every load sc1; batches of 8 in flight
+HS_DEVICE void sum_slabs_sc1(f32x4& lo, f32x4& hi, __amdgpu_buffer_rsrc_t r, int off, int slab, int S) {
+  for (int s0 = 0; s0 < S; s0 += 8) {
+    u32x4 a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = off + min(s0 + j, S - 1) * slab;
+      a[j] = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, kSc1);
+      b[j] = __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, kSc1);
+    }
+    if (s0 == 0) {
+      lo = __builtin_bit_cast(f32x4, a[0]);
+      hi = __builtin_bit_cast(f32x4, b[0]);
+    } else {
+      lo += __builtin_bit_cast(f32x4, a[0]);
+      hi += __builtin_bit_cast(f32x4, b[0]);
+    }
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+      if (s0 + j < S) {
+        lo += __builtin_bit_cast(f32x4, a[j]);
+        hi += __builtin_bit_cast(f32x4, b[j]);
+      }
+  }
+}
+
 template <int MT>
 struct ChainLds {
   static constexpr int XR = 16 * MT;
@@ -66,7 +101,7 @@ struct ChainLds {
 template <int MT, int NS, bool kNorm, bool kEarlyW, typename PreX>
 HS_DEVICE void chain_gemm(f32x4 (&acc)[MT], unsigned short* xs, const unsigned short* wp,
                           const unsigned short* x, long x_stride, int M, int k0, const float* rsv,
-                          const unsigned short* gl, PreX&& pre_x) {
+                          const unsigned short* gl, PreX&& pre_x, __amdgpu_buffer_rsrc_t xr) {
   constexpr int XR = 16 * MT, NT = 512;
   constexpr int XPASS = XR * 32 / NT > 0 ? XR * 32 / NT : 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -83,8 +118,12 @@ HS_DEVICE void chain_gemm(f32x4 (&acc)[MT], unsigned short* xs, const unsigned s
 #pragma unroll
     for (int p = 0; p < XPASS; ++p) {
       const int idx = p * NT + tid, row = idx >> 5, col = (idx & 31) * 8;
-      if (XR * 32 >= NT || idx < XR * 32)
-        xv[p] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + k0 + step * 256 + col);
+      if (XR * 32 < NT && idx >= XR * 32) continue;
+      const long e = (long)min(row, M - 1) * x_stride + k0 + step * 256 + col;
+      if constexpr (kNorm)  // x = the residual another block just stored sc1: sc1 loads
+        xv[p] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(e * 2), 0, kSc1));
+      else
+        xv[p] = *reinterpret_cast<const u16x8*>(x + e);
     }
   };
   auto store_x = [&](int buf, int step) __attribute__((always_inline)) {
@@ -160,6 +199,7 @@ struct ChainArgs {
   int NB, SB, tilesB;
   int* sync;
   int M;
+  unsigned long long* dbg;    // optional: per block {start, gemm done / wait done, end, role} (100 MHz)
 };
 
 template <int MT, int NSA, int NSB, bool kGlu>
@@ -176,6 +216,8 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
   const int M = a.M;
   const int nA = a.tilesA * a.SA;
   f32x4 acc[MT];
+  unsigned long long* dbg = a.dbg != nullptr && tid == 0 ? a.dbg + 4 * blockIdx.x : nullptr;
+  if (dbg) dbg[0] = __builtin_amdgcn_s_memrealtime();
 
   if ((int)blockIdx.x < nA) {
     // ---------------- producer ----------------
@@ -183,41 +225,49 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
     const int N = a.NA, K = a.KA, S = a.SA;
     const unsigned short* wp = a.wa + ((long)tile * (K >> 8) + (long)split * NSA) * 32768;
     chain_gemm<MT, NSA, false, false>(acc, xs, wp, a.xa, a.xa_stride, M, split * 256 * NSA, nullptr, nullptr,
-                                      [] {});
+                                      [] {}, buf_rsrc(nullptr, 0));
+    // partials stored write-through (sc1): no release fence, the ticket add follows the
+    // drain of every storing wave (Guideline 16 R1)
+    const auto rws = buf_rsrc(a.wsa, (unsigned)((long)S * M * N * 4));
     const int n = tile * 128 + wave * 16 + 4 * g;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int m = 16 * t + c;
-      if (m < M) *reinterpret_cast<f32x4*>(a.wsa + ((long)split * M + m) * N + n) = acc[t];
+      if (m < M)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t]), rws,
+                                               (int)((((long)split * M + m) * N + n) * 4), 0, kSc1);
     }
+    if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
     vm_drain();
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      vm_drain();
       gint* tk = gw(a.sync + CH_TICK + tile);
       const int last = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-      if (last) {
-        __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        vm_drain();
-      }
+      if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last;
     }
     __syncthreads();
-    if (*flag == 0) return;
-    // the tile's reduction: 16 threads per row (8 columns each), 32 rows per pass
-    const long slice = (long)M * N;
+    if (*flag == 0) {
+      if (dbg) {
+        dbg[2] = __builtin_amdgcn_s_memrealtime();
+        dbg[3] = 0;
+      }
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
+    // the tile's reduction: 16 threads per row (8 columns each), 32 rows per pass; every
+    // slab load is sc1 (the bytes were stored sc1 by other blocks: no acquire needed)
+    const auto rres = buf_rsrc(a.residual, (unsigned)((long)M * N * 2));
 #pragma unroll
     for (int pass = 0; pass < (XR + 31) / 32; ++pass) {
       const int row = pass * 32 + (tid >> 4), ch = tid & 15;
       const int col = tile * 128 + ch * 8;
       float ss = 0.f;
       if (row < M) {
-        unsigned short* rp = a.residual + (long)row * N + col;
-        const u16x8 res = *reinterpret_cast<const u16x8*>(rp);
+        const int roff = (int)(((long)row * N + col) * 2);
+        const u16x8 res = *reinterpret_cast<const u16x8*>(a.residual + (long)row * N + col);
         f32x4 lo, hi;
-        sum_slices8(lo, hi, a.wsa + (long)row * N + col, slice, S);
+        sum_slabs_sc1(lo, hi, rws, (int)(((long)row * N + col) * 4), (int)((long)M * N * 4), S);
         u16x8 r;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -226,20 +276,24 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
           const float v = bf16_to_f32(r[j]);
           ss += v * v;
         }
-        *reinterpret_cast<u16x8*>(rp) = r;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), rres, roff, 0, kSc1);
       }
       ss += __shfl_xor(ss, 1, 64);
       ss += __shfl_xor(ss, 2, 64);
       ss += __shfl_xor(ss, 4, 64);
       ss += __shfl_xor(ss, 8, 64);
-      if (ch == 0 && row < XR) a.sq[tile * 64 + row] = ss;
+      if (ch == 0 && row < XR)
+        __hip_atomic_store(gw(reinterpret_cast<int*>(a.sq) + tile * 64 + row), __float_as_int(ss), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     vm_drain();
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      vm_drain();
       __hip_atomic_fetch_add(gw(a.sync + CH_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (dbg) {
+        dbg[2] = __builtin_amdgcn_s_memrealtime();
+        dbg[3] = 1;
+      }
     }
     return;
   }
@@ -263,28 +317,34 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
           break;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      vm_drain();
       if (__hip_atomic_fetch_add(gw(a.sync + CH_PASSED), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nB - 1) {
         __hip_atomic_store(gw(a.sync + CH_DONE), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(gw(a.sync + CH_PASSED), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    // every load of the handed-off bytes below (tile sums, residual rows) is sc1: no
+    // acquire fence (Guideline 16, the sc1 row of the hand-off table); this fence emits
+    // nothing and only keeps the compiler from hoisting them above the wait
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (tid < kvec) *reinterpret_cast<u16x8*>(gl + tid * 8) = gv;
     __syncthreads();
     // 1 / rms per row: 8 threads per row sum the tile sums (fixed order)
     if (tid < XR * 8) {
       const int row = tid >> 3, j = tid & 7;
       float ss = 0.f;
-      for (int t = j; t < a.tilesA; t += 8) ss += a.sq[t * 64 + row];
+      for (int t = j; t < a.tilesA; t += 8)
+        ss += __int_as_float(__hip_atomic_load(gw(reinterpret_cast<int*>(a.sq) + t * 64 + row), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT));
       ss += __shfl_xor(ss, 1, 64);
       ss += __shfl_xor(ss, 2, 64);
       ss += __shfl_xor(ss, 4, 64);
       if (j == 0) rsv[row] = rsqrtf(ss / K + a.eps);
     }
     __syncthreads();
+    if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
   };
-  chain_gemm<MT, NSB, true, true>(acc, xs, wp, a.residual, a.NA, M, split * 256 * NSB, rsv, gl, wait_rows);
+  chain_gemm<MT, NSB, true, true>(acc, xs, wp, a.residual, a.NA, M, split * 256 * NSB, rsv, gl, wait_rows,
+                                  buf_rsrc(a.residual, (unsigned)((long)M * a.NA * 2)));
 
   if constexpr (kGlu) {
     // rows of wave w: 0-3 gate row groups, 4-7 the matching up rows (decode_gemm.hip kGlu)
@@ -325,6 +385,10 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
         if (m < M) *reinterpret_cast<f32x4*>(a.wsb + ((long)split * M + m) * N + n) = acc[t];
       }
     }
+  }
+  if (dbg) {
+    dbg[2] = __builtin_amdgcn_s_memrealtime();
+    dbg[3] = 2;
   }
 }
 
@@ -369,7 +433,8 @@ bool decode_chain_supported(int M, int NA, int KA, int SA, int NB, int SB, bool 
 
 bool launch_decode_chain(const void* xa, long xa_stride, const void* wa, float* wsa, void* residual, float* sq,
                          int NA, int KA, int SA, const void* wb, const void* gamma, float eps, void* act,
-                         long act_stride, float* wsb, int NB, int SB, bool glu, int* sync, int M, hipStream_t s) {
+                         long act_stride, float* wsb, int NB, int SB, bool glu, int* sync, int M, hipStream_t s,
+                         unsigned long long* dbg) {
   if (!decode_chain_supported(M, NA, KA, SA, NB, SB, glu)) return false;
   ChainArgs a;
   a.xa = static_cast<const unsigned short*>(xa);
@@ -393,6 +458,7 @@ bool launch_decode_chain(const void* xa, long xa_stride, const void* wa, float* 
   a.tilesB = NB / 128;
   a.sync = sync;
   a.M = M;
+  a.dbg = dbg;
   const int nsa = KA / (256 * SA), nsb = NA / (256 * SB);
   if (M > 32) return glu ? chain_a<4, true>(a, nsa, nsb, s) : chain_a<4, false>(a, nsa, nsb, s);
   return glu ? chain_a<2, true>(a, nsa, nsb, s) : chain_a<2, false>(a, nsa, nsb, s);

@@ -752,7 +752,8 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
 // kept across calls; sq: fp32 scratch of NA / 128 * 64.
 void decode_chain(at::Tensor& act, at::Tensor& wsb, at::Tensor& residual, at::Tensor& wsa, at::Tensor& sq,
                   at::Tensor& sync, const at::Tensor& xa, const at::Tensor& wa, const at::Tensor& wb,
-                  const at::Tensor& gamma, int64_t SA, int64_t NB, int64_t SB, bool glu, double eps) {
+                  const at::Tensor& gamma, int64_t SA, int64_t NB, int64_t SB, bool glu, double eps,
+                  const c10::optional<at::Tensor>& dbg) {
   CHECK_DEV(xa); CHECK_BF16(xa); CHECK_BF16(wa); CHECK_BF16(wb); CHECK_BF16(residual); CHECK_BF16(gamma);
   CHECK_ROWMAJOR(xa); CHECK_CONTIG(wa); CHECK_CONTIG(wb); CHECK_CONTIG(residual); CHECK_CONTIG(gamma);
   const int M = xa.size(0), KA = xa.size(1);
@@ -767,6 +768,11 @@ void decode_chain(at::Tensor& act, at::Tensor& wsb, at::Tensor& residual, at::Te
   TORCH_CHECK(sync.scalar_type() == at::kInt && sync.is_contiguous() &&
                   sync.numel() >= hipserve::decode_chain_sync_words(NA / 128),
               "decode_chain: sync words");
+  if (dbg.has_value()) {
+    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->is_contiguous() &&
+                    dbg->numel() >= 4 * (NA / 128 * SA + NB / 128 * SB) && dbg->device() == xa.device(),
+                "decode_chain: dbg int64 [4 * blocks]");
+  }
   if (glu) {
     CHECK_BF16(act); CHECK_ROWMAJOR(act);
     TORCH_CHECK(act.size(0) == M && act.size(1) == NB / 2 && act.stride(0) % 4 == 0, "decode_chain: act [M, NB/2]");
@@ -781,7 +787,9 @@ void decode_chain(at::Tensor& act, at::Tensor& wsb, at::Tensor& residual, at::Te
                                             residual.data_ptr(), sq.data_ptr<float>(), NA, KA, SA, wb.data_ptr(),
                                             gamma.data_ptr(), (float)eps, glu ? act.data_ptr() : nullptr,
                                             glu ? act.stride(0) : 0, glu ? nullptr : wsb.data_ptr<float>(), NB, SB,
-                                            glu, sync.data_ptr<int>(), M, cur_stream()),
+                                            glu, sync.data_ptr<int>(), M, cur_stream(),
+                                            dbg.has_value() ? reinterpret_cast<unsigned long long*>(dbg->data_ptr<int64_t>())
+                                                            : nullptr),
               "decode_chain: launch failed");
 }
 
@@ -1276,7 +1284,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("decode_chain(Tensor(a!) act, Tensor(b!) wsb, Tensor(c!) residual, Tensor(d!) wsa, Tensor(e!) sq, "
         "Tensor(f!) sync, Tensor xa, Tensor wa, Tensor wb, Tensor gamma, int SA, int NB, int SB, bool glu, "
-        "float eps) -> ()");
+        "float eps, Tensor(g!)? dbg=None) -> ()");
   m.def("decode_chain_ok(int M, int NA, int KA, int SA, int NB, int SB, bool glu) -> bool", &decode_chain_ok);
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
   m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");

@@ -8,11 +8,16 @@ zero with no consumer having given up waiting."""
 import pytest
 import torch
 
-from hipserve.ops import gemm
+from hipserve.ops import gemm, load_library
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 EPS = 1e-5
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    load_library()
 
 
 def _w(N, K, g, scale=0.02):

@@ -47,6 +47,32 @@ def graph_us(fn, iters=8, reps=20):
     return best
 
 
+def timeline(name, run, blocks):
+    """One launch with per-block timestamps (s_memrealtime, 100 MHz): when the producers'
+    GEMMs end, when the reducers finish, when consumers start / pass the wait / end."""
+    flush = torch.empty(1 << 28, device=DEV, dtype=torch.int32)
+    dbg = torch.zeros(4 * blocks, device=DEV, dtype=torch.int64)
+    for _ in range(3):
+        flush.add_(1)
+        run(dbg)
+    torch.cuda.synchronize()
+    d = dbg.view(-1, 4).cpu()
+    t0 = d[:, 0].min().item()
+    us = lambda v: round((v - t0) / 100.0, 2)  # noqa: E731
+    prod, red, cons = d[d[:, 3] == 0], d[d[:, 3] == 1], d[d[:, 3] == 2]
+    allp = d[d[:, 3] <= 1]
+    out = {"timeline": name, "producers": len(allp), "reducers": len(red), "consumers": len(cons),
+           "prod_start_max": us(allp[:, 0].max().item()), "prod_gemm_end_med": us(allp[:, 1].median().item()),
+           "prod_gemm_end_max": us(allp[:, 1].max().item()), "nonreducer_exit_max": us(prod[:, 2].max().item()),
+           "reducer_end_min": us(red[:, 2].min().item()), "reducer_end_max": us(red[:, 2].max().item()),
+           "cons_start_min": us(cons[:, 0].min().item()), "cons_start_med": us(cons[:, 0].median().item()),
+           "cons_start_max": us(cons[:, 0].max().item()), "cons_wait_end_min": us(cons[:, 1].min().item()),
+           "cons_wait_end_max": us(cons[:, 1].max().item()), "cons_end_med": us(cons[:, 2].median().item()),
+           "cons_end_max": us(cons[:, 2].max().item())}
+    print(json.dumps(out), flush=True)
+    del flush
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=64)
@@ -90,6 +116,8 @@ def main():
     for SA in (8, 4):
         rows.append({"chain": "o->ln2->gate|up", "path": f"decode_chain SA{SA}", "us": graph_us(lambda i: o_chain(i, SA))})
     # the parts alone
+    timeline("o->ln2->gate|up", lambda dbg: op.decode_chain(act, e, res, ws8, sq, sync, attn, wo[1], wgu[1], gamma, 8,
+                                                               2 * I, 1, True, 1e-5, dbg), H // 128 * 8 + 2 * I // 128)
     rows.append({"chain": "o->ln2->gate|up", "path": "gate|up glu alone",
                  "us": graph_us(lambda i: op.decode_gemm_glu(act, xn, wgu[i % nc], e, 2 * I, 1, 1))})
     del wo, wgu
@@ -107,6 +135,8 @@ def main():
     def d_chain(i):
         op.decode_chain(e16, ws_q, res, ws8, sq, sync, a_in, wd[i % nc], wqkv[i % nc], gamma, 8, Q, 4, False, 1e-5)
 
+    timeline("down->ln1->qkv", lambda dbg: op.decode_chain(e16, ws_q, res, ws8, sq, sync, a_in, wd[1], wqkv[1], gamma,
+                                                              8, Q, 4, False, 1e-5, dbg), H // 128 * 8 + Q // 128 * 4)
     rows.append({"chain": "down->ln1->qkv", "path": "unfused", "us": graph_us(d_unfused)})
     rows.append({"chain": "down->ln1->qkv", "path": "decode_chain SA8 SB4", "us": graph_us(d_chain)})
     torch.cuda.synchronize()
