@@ -6,16 +6,19 @@
 // and two kernel boundaries, during which the chip streams no weights.
 //
 //  * Blocks [0, nA) run the producer GEMM (decode_gemm.hip's packed body: 8 waves x 128
-//    weight rows, K slice 256 * NSA) and store fp32 partials. Each draws a ticket for its
-//    128-column tile; the block that draws S - 1 sums the tile's S slabs in slice order,
-//    adds the residual and writes it back in bf16 (exactly splitk_add_rmsnorm's
-//    rounding), stores the tile's per-row sum of squares, then adds 1 to `done`.
+//    weight rows, K slice 256 * NSA), store their fp32 partial slabs and count into `done`.
 //  * Blocks [nA, nA + nB) run the consumer GEMM. They issue their first two weight steps
-//    and the RMSNorm weight BEFORE waiting (the weight stream starts while the producer
-//    finishes), poll `done` (one lane, relaxed, with s_sleep), then form each row's
-//    1 / rms from the tile sums (fixed order) and stage x = bf16(h * rs * w) into LDS
-//    instead of reading a materialised normalised copy. The result equals the unfused
-//    chain except where the reassociated sum of squares moves 1 / rms by an ulp.
+//    and load the RMSNorm weight BEFORE waiting, so the weight stream starts while the
+//    producers finish. The first tilesA * MT consumers then each reduce one unit (one
+//    128-column tile x 16 rows: the S slabs summed in slice order + the residual, written
+//    back in bf16 exactly as splitk_add_rmsnorm rounds, and the unit's per-row sums of
+//    squares) once `done` == nA, and count into `rdone`. Every consumer waits for
+//    `rdone`, forms each row's 1 / rms from the unit sums (fixed order) and stages
+//    x = bf16(h * rs * w) into LDS instead of reading a materialised normalised copy.
+//    The result equals the three-launch chain except where the reassociated sum of
+//    squares moves 1 / rms by an ulp. (A per-tile last-arriver reducer — one block reading
+//    all S slabs of its tile, 256 KB — took 9-12 us: too few blocks for the reduction;
+//    the units spread it over 128 blocks of 64 KB each.)
 //  * Hand-offs are write-through (cdna_hip_programming.md §6 Guideline 16 R1, the sc1
 //    rows of the hand-off table): every handed-off byte (partial slabs, the new residual,
 //    the tile sums) is stored sc1, every storing wave drains (s_waitcnt vmcnt(0)) before
@@ -24,13 +27,12 @@
 //    in L2) and no acquire fence is needed.
 //  * No deadlock: producers never wait, and blocks are dispatched in index order, so
 //    every producer is resident or finished before a consumer takes a slot. (At 64 rows
-//    the norm staging needs ~146 VGPRs, so one block per CU: consumers start on the CUs
-//    whose producers have retired and stream their first weights while the reducers
-//    finish; capping at 128 VGPRs for two blocks per CU spills.) A consumer that polls
-//    2^22 times anyway counts into `err` and proceeds (wrong output, never a hang); the
-//    host checks `err` (tests, engine warm-up).
-//  * The counters clean up after themselves: the reducer zeroes its ticket and the last
-//    consumer to pass (a second counter) zeroes `done`; the buffer starts zeroed.
+//    the norm staging needs ~142 VGPRs, so one block per CU: consumers start on the CUs
+//    whose producers have retired; capping at 128 VGPRs for two blocks per CU spills.)
+//    A consumer that polls 2^22 times anyway counts into `err` and proceeds (wrong
+//    output, never a hang); the host checks `err` (tests, engine warm-up).
+//  * The counters clean up after themselves: the last consumer past both waits (a third
+//    counter) zeroes them; the buffer starts zeroed.
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -42,8 +44,9 @@ constexpr int CH_ROW = 264;        // x ring row stride (bf16), as decode_gemm.h
 constexpr int CH_KMAX = 4096;      // consumer K (= producer N) held in LDS for the norm weight
 constexpr int CH_SPIN_MAX = 1 << 22;
 
-// sync words, each on its own 128-byte line; tickets from CH_TICK on
-constexpr int CH_DONE = 0, CH_PASSED = 32, CH_ERR = 64, CH_TICK = 96;
+// sync words, each on its own 128-byte line: producers done, consumers past the wait,
+// give-ups, reduction units done
+constexpr int CH_DONE = 0, CH_PASSED = 32, CH_ERR = 64, CH_RDONE = 96, CH_WORDS = 128;
 
 HS_DEVICE void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -90,8 +93,7 @@ struct ChainLds {
   static constexpr int X = 2 * XR * CH_ROW;          // x ring (bf16)
   static constexpr int G = CH_KMAX;                  // norm weight (bf16)
   static constexpr int RS = 2 * 64;                  // 64 fp32 row scales
-  static constexpr int FLAG = 8;                     // reducer flag (one int, 16-byte slot)
-  static constexpr int TOTAL = X + G + RS + FLAG;
+  static constexpr int TOTAL = X + G + RS;
 };
 
 // The packed decode GEMM main loop (decode_gemm_kernel<MT, 1, 8, NS, true, ...>): the
@@ -199,7 +201,8 @@ struct ChainArgs {
   int NB, SB, tilesB;
   int* sync;
   int M;
-  unsigned long long* dbg;    // optional: per block {start, gemm done / wait done, end, role} (100 MHz)
+  unsigned long long* dbg;    // optional, 8 per block: start, gemm done | wait done, end, role, reduce
+                              // wait done, reduce done, rdone seen (s_memrealtime, 100 MHz)
 };
 
 template <int MT, int NSA, int NSB, bool kGlu>
@@ -210,13 +213,12 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
   unsigned short* xs = lds;
   unsigned short* gl = lds + L::X;
   float* rsv = reinterpret_cast<float*>(lds + L::X + L::G);
-  int* flag = reinterpret_cast<int*>(lds + L::X + L::G + L::RS);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int M = a.M;
   const int nA = a.tilesA * a.SA;
   f32x4 acc[MT];
-  unsigned long long* dbg = a.dbg != nullptr && tid == 0 ? a.dbg + 4 * blockIdx.x : nullptr;
+  unsigned long long* dbg = a.dbg != nullptr && tid == 0 ? a.dbg + 8 * blockIdx.x : nullptr;
   if (dbg) dbg[0] = __builtin_amdgcn_s_memrealtime();
 
   if ((int)blockIdx.x < nA) {
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
     const unsigned short* wp = a.wa + ((long)tile * (K >> 8) + (long)split * NSA) * 32768;
     chain_gemm<MT, NSA, false, false>(acc, xs, wp, a.xa, a.xa_stride, M, split * 256 * NSA, nullptr, nullptr,
                                       [] {}, buf_rsrc(nullptr, 0));
-    // partials stored write-through (sc1): no release fence, the ticket add follows the
+    // partials stored write-through (sc1): no release fence, the counter add follows the
     // drain of every storing wave (Guideline 16 R1)
     const auto rws = buf_rsrc(a.wsa, (unsigned)((long)S * M * N * 4));
     const int n = tile * 128 + wave * 16 + 4 * g;
@@ -241,58 +243,10 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
     vm_drain();
     __syncthreads();
     if (tid == 0) {
-      gint* tk = gw(a.sync + CH_TICK + tile);
-      const int last = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-      if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    __syncthreads();
-    if (*flag == 0) {
-      if (dbg) {
-        dbg[2] = __builtin_amdgcn_s_memrealtime();
-        dbg[3] = 0;
-      }
-      return;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
-    // the tile's reduction: 16 threads per row (8 columns each), 32 rows per pass; every
-    // slab load is sc1 (the bytes were stored sc1 by other blocks: no acquire needed)
-    const auto rres = buf_rsrc(a.residual, (unsigned)((long)M * N * 2));
-#pragma unroll
-    for (int pass = 0; pass < (XR + 31) / 32; ++pass) {
-      const int row = pass * 32 + (tid >> 4), ch = tid & 15;
-      const int col = tile * 128 + ch * 8;
-      float ss = 0.f;
-      if (row < M) {
-        const int roff = (int)(((long)row * N + col) * 2);
-        const u16x8 res = *reinterpret_cast<const u16x8*>(a.residual + (long)row * N + col);
-        f32x4 lo, hi;
-        sum_slabs_sc1(lo, hi, rws, (int)(((long)row * N + col) * 4), (int)((long)M * N * 4), S);
-        u16x8 r;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float h = bf16_to_f32(f32_to_bf16(j < 4 ? lo[j] : hi[j - 4]));
-          r[j] = f32_to_bf16(h + bf16_to_f32(res[j]));
-          const float v = bf16_to_f32(r[j]);
-          ss += v * v;
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), rres, roff, 0, kSc1);
-      }
-      ss += __shfl_xor(ss, 1, 64);
-      ss += __shfl_xor(ss, 2, 64);
-      ss += __shfl_xor(ss, 4, 64);
-      ss += __shfl_xor(ss, 8, 64);
-      if (ch == 0 && row < XR)
-        __hip_atomic_store(gw(reinterpret_cast<int*>(a.sq) + tile * 64 + row), __float_as_int(ss), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    vm_drain();
-    __syncthreads();
-    if (tid == 0) {
       __hip_atomic_fetch_add(gw(a.sync + CH_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (dbg) {
         dbg[2] = __builtin_amdgcn_s_memrealtime();
-        dbg[3] = 1;
+        dbg[3] = 0;
       }
     }
     return;
@@ -307,20 +261,72 @@ __global__ __launch_bounds__(512) void decode_chain_kernel(ChainArgs a) {
   // the norm weight does not depend on the producer: load it now, store it after the wait
   const u16x8 gv = *reinterpret_cast<const u16x8*>(a.gamma + (long)min(tid, kvec - 1) * 8);
   const unsigned short* wp = a.wb + ((long)tile * (K >> 8) + (long)split * NSB) * 32768;
-  auto wait_rows = [&]() __attribute__((always_inline)) {
+  // bounded relaxed poll of one counter by one lane (sc1 loads), then the block barrier
+  auto wait_count = [&](int word, int target) __attribute__((always_inline)) {
     if (tid == 0) {
       int spins = 0;
-      while (__hip_atomic_load(gw(a.sync + CH_DONE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.tilesA) {
+      while (__hip_atomic_load(gw(a.sync + word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > CH_SPIN_MAX) {
           __hip_atomic_fetch_add(gw(a.sync + CH_ERR), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
-      if (__hip_atomic_fetch_add(gw(a.sync + CH_PASSED), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nB - 1) {
-        __hip_atomic_store(gw(a.sync + CH_DONE), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gw(a.sync + CH_PASSED), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  const int units = a.tilesA * MT;  // (128-column tile, 16-row group) reduction units
+  auto wait_rows = [&]() __attribute__((always_inline)) {
+    if (bid < units) {
+      // this consumer also reduces one unit: sum the S slabs in slice order, add the
+      // residual, store it back (bf16, sc1) and the unit's per-row sums of squares
+      wait_count(CH_DONE, nA);
+      if (dbg) dbg[4] = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
+      __syncthreads();
+      const int ut = bid % a.tilesA, rg = bid / a.tilesA;
+      const int NAc = a.NA;
+      if (tid < 256) {
+        const int row = rg * 16 + (tid >> 4), ch = tid & 15;
+        const int col = ut * 128 + ch * 8;
+        float ss = 0.f;
+        if (row < M) {
+          const auto rws = buf_rsrc(a.wsa, (unsigned)((long)a.SA * M * NAc * 4));
+          const u16x8 res = *reinterpret_cast<const u16x8*>(a.residual + (long)row * NAc + col);
+          f32x4 lo, hi;
+          sum_slabs_sc1(lo, hi, rws, (int)(((long)row * NAc + col) * 4), (int)((long)M * NAc * 4), a.SA);
+          u16x8 r;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float h = bf16_to_f32(f32_to_bf16(j < 4 ? lo[j] : hi[j - 4]));
+            r[j] = f32_to_bf16(h + bf16_to_f32(res[j]));
+            const float v = bf16_to_f32(r[j]);
+            ss += v * v;
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r),
+                                                 buf_rsrc(a.residual, (unsigned)((long)M * NAc * 2)),
+                                                 (int)(((long)row * NAc + col) * 2), 0, kSc1);
+        }
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        ss += __shfl_xor(ss, 4, 64);
+        ss += __shfl_xor(ss, 8, 64);
+        if (ch == 0)
+          __hip_atomic_store(gw(reinterpret_cast<int*>(a.sq) + ut * 64 + row), __float_as_int(ss), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
+      vm_drain();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(gw(a.sync + CH_RDONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (dbg) dbg[5] = __builtin_amdgcn_s_memrealtime();
+    }
+    wait_count(CH_RDONE, units);
+    if (dbg) dbg[6] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(gw(a.sync + CH_PASSED), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nB - 1) {
+      // every consumer is past both waits and every producer has counted: reset for the next call
+      __hip_atomic_store(gw(a.sync + CH_DONE), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gw(a.sync + CH_RDONE), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gw(a.sync + CH_PASSED), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // every load of the handed-off bytes below (tile sums, residual rows) is sc1: no
     // acquire fence (Guideline 16, the sc1 row of the hand-off table); this fence emits
@@ -421,12 +427,14 @@ bool chain_a(const ChainArgs& a, int nsa, int nsb, hipStream_t s) {
 
 }  // namespace
 
-int decode_chain_sync_words(int tilesA) { return CH_TICK + tilesA; }
+int decode_chain_sync_words(int) { return CH_WORDS; }
 
 bool decode_chain_supported(int M, int NA, int KA, int SA, int NB, int SB, bool glu) {
   if (M < 17 || M > 64 || NA % 128 || NB % 128 || NA > CH_KMAX || NA % 256 || KA % (256 * SA) || NA % (256 * SB))
     return false;
   if (glu && SB != 1) return false;
+  // every (tile, 16-row group) reduction unit needs a consumer block to run it
+  if (NB / 128 * SB < NA / 128 * (M > 32 ? 4 : 2)) return false;
   const int nsa = KA / (256 * SA), nsb = NA / (256 * SB);
   return (nsa == 2 || nsa == 4 || nsa == 7) && (nsb == 2 || nsb == 4 || nsb == 8 || nsb == 16);
 }

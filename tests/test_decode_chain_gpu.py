@@ -77,11 +77,11 @@ def _fp32(xa, wa, wb, gamma, res0, glu):
 
 SHAPES = [
     # M, NA, KA, SA, NB, SB, glu
-    (64, 4096, 4096, 8, 4096, 1, True),      # o_proj -> ln2 -> gate|up (Llama-3-8B widths, short I)
+    (64, 4096, 4096, 8, 16384, 1, True),     # o_proj -> ln2 -> gate|up (Llama-3-8B widths, I = 8192)
     (64, 4096, 14336, 8, 6144, 4, False),    # down -> next ln1 -> qkv partials (Llama-3-8B)
-    (48, 2048, 4096, 4, 2048, 2, False),
-    (20, 4096, 4096, 8, 2048, 1, True),      # 17-32 rows: the 32-row body
-    (33, 1024, 1792, 1, 2048, 1, True),      # K slice 7 steps, one slice: the ticket is trivially last
+    (48, 2048, 4096, 4, 8192, 2, False),
+    (20, 4096, 4096, 8, 8192, 1, True),      # 17-32 rows: the 32-row body
+    (33, 1024, 1792, 1, 4096, 1, True),      # K slice 7 steps, one slice
 ]
 
 

@@ -51,24 +51,27 @@ def timeline(name, run, blocks):
     """One launch with per-block timestamps (s_memrealtime, 100 MHz): when the producers'
     GEMMs end, when the reducers finish, when consumers start / pass the wait / end."""
     flush = torch.empty(1 << 28, device=DEV, dtype=torch.int32)
-    dbg = torch.zeros(4 * blocks, device=DEV, dtype=torch.int64)
+    dbg = torch.zeros(8 * blocks, device=DEV, dtype=torch.int64)
     for _ in range(3):
         flush.add_(1)
         run(dbg)
     torch.cuda.synchronize()
-    d = dbg.view(-1, 4).cpu()
+    d = dbg.view(-1, 8).cpu()
     t0 = d[:, 0].min().item()
     us = lambda v: round((v - t0) / 100.0, 2)  # noqa: E731
-    prod, red, cons = d[d[:, 3] == 0], d[d[:, 3] == 1], d[d[:, 3] == 2]
-    allp = d[d[:, 3] <= 1]
-    out = {"timeline": name, "producers": len(allp), "reducers": len(red), "consumers": len(cons),
-           "prod_start_max": us(allp[:, 0].max().item()), "prod_gemm_end_med": us(allp[:, 1].median().item()),
-           "prod_gemm_end_max": us(allp[:, 1].max().item()), "nonreducer_exit_max": us(prod[:, 2].max().item()),
-           "reducer_end_min": us(red[:, 2].min().item()), "reducer_end_max": us(red[:, 2].max().item()),
+    prod, cons = d[d[:, 3] == 0], d[d[:, 3] == 2]
+    out = {"timeline": name, "producers": len(prod), "consumers": len(cons),
+           "prod_start_max": us(prod[:, 0].max().item()), "prod_gemm_end_med": us(prod[:, 1].median().item()),
+           "prod_gemm_end_max": us(prod[:, 1].max().item()), "prod_exit_max": us(prod[:, 2].max().item()),
            "cons_start_min": us(cons[:, 0].min().item()), "cons_start_med": us(cons[:, 0].median().item()),
            "cons_start_max": us(cons[:, 0].max().item()), "cons_wait_end_min": us(cons[:, 1].min().item()),
            "cons_wait_end_max": us(cons[:, 1].max().item()), "cons_end_med": us(cons[:, 2].median().item()),
            "cons_end_max": us(cons[:, 2].max().item())}
+    red = cons[cons[:, 4] > 0]
+    out.update({"reducers": len(red), "red_wait_end_min": us(red[:, 4].min().item()),
+                "red_wait_end_max": us(red[:, 4].max().item()), "red_end_min": us(red[:, 5].min().item()),
+                "red_end_max": us(red[:, 5].max().item()), "rdone_seen_min": us(cons[:, 6].min().item()),
+                "rdone_seen_max": us(cons[:, 6].max().item())})
     print(json.dumps(out), flush=True)
     del flush
 
