@@ -158,16 +158,6 @@ constexpr int DG_GLU = 1, DG_PARTIAL = 2;
 bool launch_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w, int M,
                         int N, int K, int rt, int S, bool packed, int flags, hipStream_t s);
 
-// decode_chain.hip — producer GEMM (packed Wa, split-K SA) -> residual += sum -> RMSNorm(gamma)
-// -> consumer GEMM (packed Wb: glu -> act [M, NB/2] with SB == 1, else partials wsb
-// [SB, M, NB]) in one launch. sync: decode_chain_sync_words(NA / 128) zeroed ints, kept
-// across calls (the kernel resets them); sync[64] counts consumers that gave up waiting.
-int decode_chain_sync_words(int tilesA);
-bool decode_chain_supported(int M, int NA, int KA, int SA, int NB, int SB, bool glu);
-bool launch_decode_chain(const void* xa, long xa_stride, const void* wa, float* wsa, void* residual, float* sq,
-                         int NA, int KA, int SA, const void* wb, const void* gamma, float eps, void* act,
-                         long act_stride, float* wsb, int NB, int SB, bool glu, int* sync, int M, hipStream_t s,
-                         unsigned long long* dbg = nullptr);
 
 // prefill epilogues (prefill_gemm.hip FP8 kernel, prefill_gemm_packed.hip):
 //   PG_EPI_STORE  C = bf16(acc)

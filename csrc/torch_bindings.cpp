@@ -745,57 +745,6 @@ void decode_gemm_glu(at::Tensor& act, const at::Tensor& x, const at::Tensor& wp,
               "decode_gemm_glu: unsupported (rt, K/splits)");
 }
 
-// Decode GEMM chain in one launch (decode_chain.hip): residual += xa . Wa^T (split-K SA,
-// partials in wsa); x = RMSNorm(residual) * gamma; glu: act = silu(x Wg^T) * (x Wu^T)
-// (SB == 1), else wsb = split-K partials of x . Wb^T for a fused epilogue. wa / wb in the
-// pack_decode_weight layout (wb with glu interleaving when glu). sync: int32, zeroed once,
-// kept across calls; sq: fp32 scratch of NA / 128 * 64.
-void decode_chain(at::Tensor& act, at::Tensor& wsb, at::Tensor& residual, at::Tensor& wsa, at::Tensor& sq,
-                  at::Tensor& sync, const at::Tensor& xa, const at::Tensor& wa, const at::Tensor& wb,
-                  const at::Tensor& gamma, int64_t SA, int64_t NB, int64_t SB, bool glu, double eps,
-                  const c10::optional<at::Tensor>& dbg) {
-  CHECK_DEV(xa); CHECK_BF16(xa); CHECK_BF16(wa); CHECK_BF16(wb); CHECK_BF16(residual); CHECK_BF16(gamma);
-  CHECK_ROWMAJOR(xa); CHECK_CONTIG(wa); CHECK_CONTIG(wb); CHECK_CONTIG(residual); CHECK_CONTIG(gamma);
-  const int M = xa.size(0), KA = xa.size(1);
-  TORCH_CHECK(residual.dim() == 2 && residual.size(0) == M, "decode_chain: residual [M, NA]");
-  const int NA = residual.size(1);
-  TORCH_CHECK(xa.stride(0) % 8 == 0 && gamma.numel() == NA, "decode_chain: alignment / gamma [NA]");
-  TORCH_CHECK(wa.numel() == (long)NA * KA && wb.numel() == (long)NB * NA, "decode_chain: packed weight sizes");
-  TORCH_CHECK(hipserve::decode_chain_supported(M, NA, KA, SA, NB, SB, glu), "decode_chain: unsupported shape");
-  TORCH_CHECK(wsa.scalar_type() == at::kFloat && wsa.is_contiguous() && wsa.numel() >= SA * M * NA,
-              "decode_chain: wsa must hold SA*M*NA fp32");
-  TORCH_CHECK(sq.scalar_type() == at::kFloat && sq.numel() >= NA / 128 * 64, "decode_chain: sq");
-  TORCH_CHECK(sync.scalar_type() == at::kInt && sync.is_contiguous() &&
-                  sync.numel() >= hipserve::decode_chain_sync_words(NA / 128),
-              "decode_chain: sync words");
-  if (dbg.has_value()) {
-    TORCH_CHECK(dbg->scalar_type() == at::kLong && dbg->is_contiguous() &&
-                    dbg->numel() >= 4 * (NA / 128 * SA + NB / 128 * SB) && dbg->device() == xa.device(),
-                "decode_chain: dbg int64 [4 * blocks]");
-  }
-  if (glu) {
-    CHECK_BF16(act); CHECK_ROWMAJOR(act);
-    TORCH_CHECK(act.size(0) == M && act.size(1) == NB / 2 && act.stride(0) % 4 == 0, "decode_chain: act [M, NB/2]");
-  } else {
-    TORCH_CHECK(wsb.scalar_type() == at::kFloat && wsb.is_contiguous() && wsb.numel() >= SB * M * NB,
-                "decode_chain: wsb must hold SB*M*NB fp32");
-  }
-  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&residual, &wsa, &sq, &sync, &wa, &wb, &gamma})
-    TORCH_CHECK(t->device() == xa.device(), "decode_chain: tensors on one device");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(xa.device());
-  TORCH_CHECK(hipserve::launch_decode_chain(xa.data_ptr(), xa.stride(0), wa.data_ptr(), wsa.data_ptr<float>(),
-                                            residual.data_ptr(), sq.data_ptr<float>(), NA, KA, SA, wb.data_ptr(),
-                                            gamma.data_ptr(), (float)eps, glu ? act.data_ptr() : nullptr,
-                                            glu ? act.stride(0) : 0, glu ? nullptr : wsb.data_ptr<float>(), NB, SB,
-                                            glu, sync.data_ptr<int>(), M, cur_stream(),
-                                            dbg.has_value() ? reinterpret_cast<unsigned long long*>(dbg->data_ptr<int64_t>())
-                                                            : nullptr),
-              "decode_chain: launch failed");
-}
-
-bool decode_chain_ok(int64_t M, int64_t NA, int64_t KA, int64_t SA, int64_t NB, int64_t SB, bool glu) {
-  return hipserve::decode_chain_supported(M, NA, KA, SA, NB, SB, glu);
-}
 
 
 // Prefill GEMM over the packed decode layout (prefill_gemm_packed.hip): wp =
@@ -1282,10 +1231,6 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
-  m.def("decode_chain(Tensor(a!) act, Tensor(b!) wsb, Tensor(c!) residual, Tensor(d!) wsa, Tensor(e!) sq, "
-        "Tensor(f!) sync, Tensor xa, Tensor wa, Tensor wb, Tensor gamma, int SA, int NB, int SB, bool glu, "
-        "float eps, Tensor(g!)? dbg=None) -> ()");
-  m.def("decode_chain_ok(int M, int NA, int KA, int SA, int NB, int SB, bool glu) -> bool", &decode_chain_ok);
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
   m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
@@ -1334,7 +1279,6 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("pack_decode_weight", &pack_decode_weight);
   m.impl("decode_gemm_partial", &decode_gemm_partial);
   m.impl("decode_gemm_glu", &decode_gemm_glu);
-  m.impl("decode_chain", &decode_chain);
   m.impl("prefill_gemm_packed", &prefill_gemm_packed);
   m.impl("prefill_gemm_packed_grouped", &prefill_gemm_packed_grouped);
   m.impl("prefill_gemm_f8", &prefill_gemm_f8);

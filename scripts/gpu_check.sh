@@ -113,8 +113,6 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     b8_chunk16k) bench_named b8_chunk16k -- --max-num-batched-tokens 16384 ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
-    chaintest) run_one tests/test_decode_chain_gpu.py ;;
-    chainbench) timeout -k 10 300 python -u tools/bench_chain.py > $OUT/bench_chain.log 2>&1; rc=$?; cat $OUT/bench_chain.log; [ $rc -eq 0 ] ;;
     g27fp8_res) bench_named g27fp8_res HIPSERVE_FP8_PREFILL_LIB=resident -- --model gemma-3-27b --quantization fp8 ;;
     q3int8_noshadow) bench_named q3int8_noshadow HIPSERVE_FUSED_DECODE=1 HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 ;;
     f8test) run_one tests/test_prefill_gemm_f8_gpu.py ;;
