@@ -146,6 +146,29 @@ def bench_prefill(ops):
         os.environ.pop("HIPSERVE_PREFILL_ATTN_V1", None)
 
 
+def bench_prefill_chunked(ops):
+    """Chunked prefill attention: ``chunk`` new query rows at the end of a ``ctx``-token
+    context per sequence (the shape of every step of a long prompt under an 8K token
+    budget), TFLOP/s over the causal work of the chunk."""
+    D, bs, nq, nkv = 128, 16, 32, 8
+    for ctx_len, chunk, nseq in [(32768, 2048, 4), (32768, 8192, 1), (16384, 2048, 4), (8192, 2048, 4)]:
+        mb = ctx_len // bs
+        kc = torch.randn(nseq * mb, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
+        vc = torch.randn(nseq * mb, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+        bt = torch.arange(nseq * mb, device=DEV).int().view(nseq, mb)
+        cu = torch.arange(0, (nseq + 1) * chunk, chunk, device=DEV, dtype=torch.int32)
+        ctx = torch.full((nseq,), ctx_len, device=DEV, dtype=torch.int32)
+        tiles = torch.tensor(sorted(((s, r) for s in range(nseq) for r in range(0, chunk, 128)), key=lambda t: -t[1]),
+                             device=DEV, dtype=torch.int32)
+        q = torch.randn(nseq * chunk, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+        out = torch.empty(nseq * chunk, nq * D, device=DEV, dtype=torch.bfloat16)
+        flops = 4 * nseq * chunk * (ctx_len - chunk / 2) * D * nq
+        us = timeit(lambda: ops.prefill_attention(out, q, kc, vc, bt, cu, ctx, tiles, nq, nkv, 1 / math.sqrt(D)), n=10)
+        emit(op="prefill_attention_chunked", ctx=ctx_len, chunk=chunk, nseq=nseq, us=round(us, 1),
+             TFLOPs=round(flops / us / 1e6, 1))
+        del kc, vc, q, out
+
+
 def bench_gemm(ops):
     for M in (1, 16, 64, 128, 256):
         for N, K, name in [(6144, 4096, "qkv"), (4096, 4096, "o"), (28672, 4096, "gate_up"),
@@ -171,6 +194,7 @@ def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     ops = KernelOps()
     for name, fn in [("sample", bench_sample), ("decode", bench_decode), ("prefill", bench_prefill),
+                     ("prefill_chunked", bench_prefill_chunked),
                      ("gemm", bench_gemm), ("norm", bench_norm)]:
         if which in ("all", name):
             fn(ops)
