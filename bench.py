@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=64)
     ap.add_argument("--input-len", type=int, default=1024)
     ap.add_argument("--output-len", type=int, default=256)
-    ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=None)
     ap.add_argument("--path", choices=["engine", "gateway"], default="gateway")
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
@@ -252,7 +252,7 @@ def run_phase(args):
         stack = GatewayStack({args.model: [eport]}).start()
         lg = LoadgenProc()
 
-    from hipserve.config import EngineConfig
+    from hipserve.config import EngineConfig, default_batched_tokens
     from hipserve.engine.llm_engine import LLMEngine
     from hipserve.engine.request import SamplingParams
     from hipserve.parallel.comm import TPGroup, init_tp
@@ -270,7 +270,8 @@ def run_phase(args):
     cfg = EngineConfig(model=args.model, device=args.device, max_num_seqs=max(args.concurrency, 1),
                        dtype="bfloat16" if cuda else "float32", num_kv_blocks=args.num_kv_blocks,
                        tensor_parallel_size=args.tp,
-                       max_num_batched_tokens=args.max_num_batched_tokens,
+                       max_num_batched_tokens=args.max_num_batched_tokens or default_batched_tokens(
+                           args.model, quantization=args.quantization),
                        max_model_len=args.input_len + args.output_len + 64,
                        enforce_eager=args.enforce_eager, seed=0 if tp_mode else rank,
                        load_format="dummy" if args.quantization else "auto",
@@ -404,6 +405,7 @@ def run_phase(args):
             "concurrency_per_gpu": args.concurrency,
             "parallelism": f"tp{args.tp}" if tp_mode else (f"dp{world}" if world > 1 else "tp1"),
             "sampling": {"temperature": args.temperature, "top_p": args.top_p},
+            "prefill_tokens_per_step": cfg.max_num_batched_tokens,
         },
         "engine_init_s": round(init_s, 1),
         "init_breakdown_s": getattr(engine.runner, "init_times", {}),

@@ -22,7 +22,7 @@ import os
 import socket
 import sys
 
-from ..config import EngineConfig
+from ..config import EngineConfig, default_batched_tokens
 
 
 def build_parser(prog="hipserve") -> argparse.ArgumentParser:
@@ -43,7 +43,8 @@ def build_parser(prog="hipserve") -> argparse.ArgumentParser:
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
     ap.add_argument("--block-size", type=int, default=16)
     ap.add_argument("--max-num-seqs", type=int, default=256)
-    ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=None,
+                    help="prefill token budget per step (default 8192; 16384 for GGUF weights)")
     ap.add_argument("--num-kv-blocks", type=int, default=None)
     ap.add_argument("--enable-prefix-caching", action=argparse.BooleanOptionalAction, default=True)
     ap.add_argument("--enforce-eager", action="store_true")
@@ -68,7 +69,9 @@ def config_from_args(a) -> EngineConfig:
         load_format=a.load_format, dtype=dtype, device=device,
         tensor_parallel_size=a.tensor_parallel_size, gpu_memory_utilization=a.gpu_memory_utilization,
         max_model_len=a.max_model_len, block_size=a.block_size, max_num_seqs=a.max_num_seqs,
-        max_num_batched_tokens=a.max_num_batched_tokens, num_kv_blocks=a.num_kv_blocks,
+        max_num_batched_tokens=a.max_num_batched_tokens or default_batched_tokens(a.model, a.load_format,
+                                                                                   a.quantization),
+        num_kv_blocks=a.num_kv_blocks,
         enable_prefix_caching=a.enable_prefix_caching, enforce_eager=a.enforce_eager, seed=a.seed,
         trust_remote_code=a.trust_remote_code, host=a.host, port=a.port,
         extra={"quantization": a.quantization} if a.quantization else {})

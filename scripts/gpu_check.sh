@@ -111,7 +111,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
                 --timeout-method thread -p no:cacheprovider -k "prefill_attention or 32k" > $OUT/attn_test.log 2>&1; rc=$?; tail -n 3 $OUT/attn_test.log; [ $rc -eq 0 ] ;;
     attnbench) BENCH_PREFILL_LONG=1 BENCH_PREFILL_VERS=v2w8 timeout -k 10 300 python -u tools/bench_ops.py prefill > $OUT/attn_bench.log 2>&1; rc=$?; cat $OUT/attn_bench.log; [ $rc -eq 0 ] ;;
     b8_chunk16k) bench_named b8_chunk16k -- --max-num-batched-tokens 16384 ;;
-    q4km_chunk16k) bench_named q4km_chunk16k -- --quantization q4_k_m --max-num-batched-tokens 16384 ;;
+    q4km_chunk8k) bench_named q4km_chunk8k -- --quantization q4_k_m --max-num-batched-tokens 8192 ;;
     q4km_default) bench_named q4km_default -- --quantization q4_k_m ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
     enginetest) run_one tests/test_engine_gpu.py ;;

@@ -208,3 +208,21 @@ def test_prefill_pad_table():
     assert pad_table(t) == {6912: 7168, 7424: 7936, 7680: 7936}
     assert pad_table({1024: 1.0, 1280: 1.0, 1536: 0.99}) == {}  # within 3 %: keep the smaller count
     assert pad_table({}) == {}
+
+
+def test_default_prefill_budget_per_weight_format():
+    """8192 prefill tokens per step by default, 16384 for GGUF weights (their per-step
+    dequantise pass is amortised over twice the tokens); an explicit flag wins."""
+    from hipserve.config import default_batched_tokens
+    from hipserve.server.cli import build_parser, config_from_args
+
+    assert default_batched_tokens("llama-3-8b") == 8192
+    assert default_batched_tokens("llama-3-8b", quantization="fp8") == 8192
+    assert default_batched_tokens("llama-3-8b", quantization="q4_k_m") == 16384
+    assert default_batched_tokens("/models/Meta-Llama-3-8B.Q8_0.gguf") == 16384
+    p = build_parser()
+    assert config_from_args(p.parse_args(["--model", "llama-3-8b", "--device", "cpu"])).max_num_batched_tokens == 8192
+    assert config_from_args(p.parse_args(["--model", "llama-3-8b", "--device", "cpu", "--quantization", "q8_0"])
+                            ).max_num_batched_tokens == 16384
+    assert config_from_args(p.parse_args(["--model", "llama-3-8b", "--device", "cpu", "--quantization", "q8_0",
+                                          "--max-num-batched-tokens", "4096"])).max_num_batched_tokens == 4096
