@@ -453,7 +453,8 @@ def default_batched_tokens(model: str, load_format: str = "auto", quantization: 
     Their prefill dequantises each projection into a bf16 scratch once per step (~6 ms a
     step for Llama-3-8B Q4_K_M), and twice the tokens per step halve that cost per token:
     7,726 -> 8,044 tok/s, p50 TTFT 482 -> 530 ms (profiles/r5_bench_q4km_chunk16k.json).
-    bf16 models keep 8192 (16384 measured no faster there)."""
+    bf16 models keep 8192: 16384 gave the same 7,730 tok/s at 480 vs 434 ms TTFT and 4096
+    7,607 / 432 ms (profiles/r5_bench_8b_chunk16k.json, r5_bench_8b_chunk4k.json)."""
     gguf = quantization in GGUF_QUANTS or load_format == "gguf" or str(model).lower().endswith(".gguf")
     return 16384 if gguf else 8192
 
