@@ -449,14 +449,48 @@ GGUF_QUANTS = ("q4_k_m", "q8_0", "q4_0")
 
 
 def default_batched_tokens(model: str, load_format: str = "auto", quantization: str | None = None) -> int:
-    """Prefill token budget per step when none is given: 8192, or 16384 for GGUF weights.
-    Their prefill dequantises each projection into a bf16 scratch once per step (~6 ms a
-    step for Llama-3-8B Q4_K_M), and twice the tokens per step halve that cost per token:
-    7,726 -> 8,044 tok/s, p50 TTFT 482 -> 530 ms (profiles/r5_bench_q4km_chunk16k.json).
+    """Prefill token budget per step when none is given: 8192; 16384 for GGUF weights and
+    32768 for INT8 weight-only ones. Both keep only their quantised weights and dequantise
+    each projection (every expert, for MoE) into a bf16 scratch once per prefill step, a
+    cost that more tokens per step spread thinner:
+      * Llama-3-8B Q4_K_M: 7,726 -> 8,044 tok/s, p50 TTFT 482 -> 530 ms
+        (profiles/r5_bench_q4km_chunk8k.json, r5_bench_q4km_chunk16k.json);
+      * Qwen3-30B-A3B INT8: 3,912 / 774 ms (8K) -> 4,079 / 755 (16K) -> 4,327 / 691 (32K),
+        above the 4,155 / 623 ms of bf16 prefill shadows at 8K with 34 % more KV blocks
+        (profiles/r5_bench_q3int8_*.json).
+    FP8 keeps 8192 (Gemma-3-27B: 2,839 vs 2,854 tok/s at 16K, TTFT 1,110 vs 1,186 ms).
     bf16 models keep 8192: 16384 gave the same 7,730 tok/s at 480 vs 434 ms TTFT and 4096
     7,607 / 432 ms (profiles/r5_bench_8b_chunk16k.json, r5_bench_8b_chunk4k.json)."""
+    if quantization is None:
+        quantization = checkpoint_quantization(model)
+    if quantization == "int8":
+        return 32768
     gguf = quantization in GGUF_QUANTS or load_format == "gguf" or str(model).lower().endswith(".gguf")
     return 16384 if gguf else 8192
+
+
+def checkpoint_quantization(model: str) -> str | None:
+    """"int8" / "fp8" from a local HF checkpoint's ``quantization_config`` (compressed-
+    tensors weight groups, AWQ / GPTQ bits), else None (presets, Hub ids not yet
+    downloaded: the caller's default applies)."""
+    path = os.path.join(str(model), "config.json")
+    if not os.path.isfile(path):
+        return None
+    try:
+        with open(path) as f:
+            q = json.load(f).get("quantization_config") or {}
+    except (OSError, ValueError):
+        return None
+    method = str(q.get("quant_method", "")).lower()
+    if method == "fp8":
+        return "fp8"
+    if method in ("awq", "gptq"):
+        return "int8" if int(q.get("bits", 0)) == 8 else None
+    for grp in (q.get("config_groups") or {}).values():
+        w = (grp or {}).get("weights") or {}
+        if int(w.get("num_bits", 0)) == 8:
+            return "fp8" if str(w.get("type", "")).lower() == "float" else "int8"
+    return None
 
 
 @dataclass(frozen=True)

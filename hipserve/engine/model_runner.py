@@ -147,8 +147,13 @@ class ModelRunner:
                     self.single_layout = {"reason": why, "weights": n, "row_major_gb_freed": round(freed / 2**30, 2)}
                 else:
                     self.model.pack_decode_weights(gemm.TUNER.packed_shapes())
+            # bf16 shadows of quantised weights for hipBLASLt prefill: opt-in (HIPSERVE_QUANT_SHADOW=1
+            # or extra quant_dense_shadow). By default a quantised model keeps only its quantised
+            # weights (more KV blocks); its prefill dequantises per step into a scratch, which a
+            # larger token budget amortises (config.default_batched_tokens)
+            shadow = ecfg.extra.get("quant_dense_shadow", os.environ.get("HIPSERVE_QUANT_SHADOW", "0") == "1")
             moes = self.model.quant_moes() if hasattr(self.model, "quant_moes") else []
-            if moes and ecfg.extra.get("quant_dense_shadow", True):  # bf16 experts for prefill
+            if moes and shadow:  # bf16 experts for prefill
                 from ..ops import quant as Q
 
                 total = torch.cuda.get_device_properties(self.device).total_memory
@@ -164,16 +169,15 @@ class ModelRunner:
                 self.qprefill_report = Q.tune_qprefill([w for w in qws if w is not lm], self.device,
                                                        min(ecfg.max_num_batched_tokens, 8192)) \
                     if Q.QPREFILL_MODE == "auto" else []
-                if ecfg.extra.get("quant_dense_shadow", True):
-                    total = torch.cuda.get_device_properties(self.device).total_memory
-                    # GGUF blocks get a resident bf16 shadow only on request (HBM holds the
-                    # quantised blocks only); INT8 weights keep theirs for hipBLASLt prefill
-                    gguf = ecfg.extra.get("gguf_dense_shadow", os.environ.get("HIPSERVE_QUANT_SHADOW", "0") == "1")
-                    self.quant_shadow_bytes = getattr(self, "quant_shadow_bytes", 0) + Q.make_dense_shadows(
-                        qws, self.device, (24 << 30) + total // 4, gguf=gguf)
-                    # FP8: which projections prefill on hipBLASLt's FP8 GEMM (a per-call
-                    # re-layout of the tiled copy by default, ops/quant.py FP8_LIB)
-                    self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
+                total = torch.cuda.get_device_properties(self.device).total_memory
+                self.quant_shadow_bytes = getattr(self, "quant_shadow_bytes", 0)
+                if shadow:
+                    gguf = ecfg.extra.get("gguf_dense_shadow", shadow)
+                    self.quant_shadow_bytes += Q.make_dense_shadows(qws, self.device, (24 << 30) + total // 4,
+                                                                    gguf=gguf)
+                # FP8: which projections prefill on hipBLASLt's FP8 GEMM (a per-call
+                # re-layout of the tiled copy by default, ops/quant.py FP8_LIB)
+                self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
             torch.cuda.empty_cache()
         self.init_times["decode_gemm_tune_s"] = round(time.time() - t1, 2)
         t1 = time.time()

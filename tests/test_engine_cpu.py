@@ -220,9 +220,37 @@ def test_default_prefill_budget_per_weight_format():
     assert default_batched_tokens("llama-3-8b", quantization="fp8") == 8192
     assert default_batched_tokens("llama-3-8b", quantization="q4_k_m") == 16384
     assert default_batched_tokens("/models/Meta-Llama-3-8B.Q8_0.gguf") == 16384
+    assert default_batched_tokens("qwen3-30b-a3b", quantization="int8") == 32768
     p = build_parser()
     assert config_from_args(p.parse_args(["--model", "llama-3-8b", "--device", "cpu"])).max_num_batched_tokens == 8192
     assert config_from_args(p.parse_args(["--model", "llama-3-8b", "--device", "cpu", "--quantization", "q8_0"])
                             ).max_num_batched_tokens == 16384
     assert config_from_args(p.parse_args(["--model", "llama-3-8b", "--device", "cpu", "--quantization", "q8_0",
                                           "--max-num-batched-tokens", "4096"])).max_num_batched_tokens == 4096
+
+
+def test_checkpoint_quantization_detection(tmp_path):
+    """INT8 / FP8 read from a local checkpoint's quantization_config (compressed-tensors
+    groups, AWQ bits) pick the budget without a --quantization flag."""
+    import json
+
+    from hipserve.config import checkpoint_quantization, default_batched_tokens
+
+    def ckpt(name, q):
+        d = tmp_path / name
+        d.mkdir()
+        (d / "config.json").write_text(json.dumps({"model_type": "qwen3_moe", "quantization_config": q}))
+        return str(d)
+
+    ct8 = ckpt("ct8", {"quant_method": "compressed-tensors",
+                       "config_groups": {"group_0": {"weights": {"num_bits": 8, "type": "int"}}}})
+    fp8 = ckpt("fp8", {"quant_method": "compressed-tensors",
+                       "config_groups": {"group_0": {"weights": {"num_bits": 8, "type": "float"}}}})
+    awq = ckpt("awq", {"quant_method": "awq", "bits": 8})
+    awq4 = ckpt("awq4", {"quant_method": "awq", "bits": 4})
+    assert checkpoint_quantization(ct8) == "int8" and default_batched_tokens(ct8) == 32768
+    assert checkpoint_quantization(fp8) == "fp8" and default_batched_tokens(fp8) == 8192
+    assert checkpoint_quantization(awq) == "int8"
+    assert checkpoint_quantization(awq4) is None
+    assert checkpoint_quantization(str(tmp_path / "missing")) is None
+    assert checkpoint_quantization("llama-3-8b") is None
