@@ -458,7 +458,11 @@ def default_batched_tokens(model: str, load_format: str = "auto", quantization: 
       * Qwen3-30B-A3B INT8: 3,912 / 774 ms (8K) -> 4,079 / 755 (16K) -> 4,327 / 691 (32K),
         above the 4,155 / 623 ms of bf16 prefill shadows at 8K with 34 % more KV blocks
         (profiles/r5_bench_q3int8_*.json).
-    FP8 keeps 8192 (Gemma-3-27B: 2,839 vs 2,854 tok/s at 16K, TTFT 1,110 vs 1,186 ms).
+    FP8 keeps 8192 (Gemma-3-27B: 2,839 vs 2,854 tok/s at 16K, TTFT 1,110 vs 1,186 ms), and
+    so do bf16 MoE models (Mixtral-8x7B: 1,648 / 1,655 / 1,675 tok/s at 8K / 16K / 32K for
+    TTFT 558 / 616 / 753 ms, profiles/r5_bench_mixtral*.json). A larger budget also
+    lengthens the decode stall of running requests during a prefill step: latency-bound
+    deployments pass a smaller --max-num-batched-tokens.
     bf16 models keep 8192: 16384 gave the same 7,730 tok/s at 480 vs 434 ms TTFT and 4096
     7,607 / 432 ms (profiles/r5_bench_8b_chunk16k.json, r5_bench_8b_chunk4k.json)."""
     if quantization is None:

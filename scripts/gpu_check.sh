@@ -113,6 +113,8 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     b8_chunk16k) bench_named b8_chunk16k -- --max-num-batched-tokens 16384 ;;
     q4km_chunk8k) bench_named q4km_chunk8k -- --quantization q4_k_m --max-num-batched-tokens 8192 ;;
     q4km_default) bench_named q4km_default -- --quantization q4_k_m ;;
+    mixtral16k) bench_named mixtral16k X=1 -- --model mixtral-8x7b --concurrency 32 --max-num-batched-tokens 16384 ;;
+    mixtral32k) bench_named mixtral32k X=1 -- --model mixtral-8x7b --concurrency 32 --max-num-batched-tokens 32768 ;;
     q3int8_noshadow16k) bench_named q3int8_noshadow16k HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 --max-num-batched-tokens 16384 ;;
     q3int8_noshadow32k) bench_named q3int8_noshadow32k HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 --max-num-batched-tokens 32768 ;;
     g27fp8_16k) bench_named g27fp8_16k X=1 -- --model gemma-3-27b --quantization fp8 --max-num-batched-tokens 16384 ;;
