@@ -50,8 +50,11 @@ def main(argv=None):
     i.add_argument("--service", action="append", help="HOST[:PORT]=URL (k8s Service -> local address)")
     i.add_argument("--workers", type=int, default=1)
     ap.add_argument("--log-level", default="INFO")
+    ap.add_argument("--log-format", default=None, choices=["text", "json"],
+                    help="text (default) or one JSON object per line (HIPSERVE_LOG_FORMAT)")
     a = ap.parse_args(argv)
-    logging.basicConfig(level=a.log_level.upper())
+    from ..utils.logs import setup_logging
+    setup_logging(a.log_level, a.log_format)
     if a.workers > 1:  # SO_REUSEPORT worker processes, like nginx workers
         procs = [mp.get_context("fork").Process(target=_run, args=(a,)) for _ in range(a.workers)]
         for p in procs:

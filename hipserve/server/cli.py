@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import argparse
 import asyncio
-import logging
 import multiprocessing as mp
 import os
 import socket
@@ -52,6 +51,8 @@ def build_parser(prog="hipserve") -> argparse.ArgumentParser:
     ap.add_argument("--n-gpu-layers", "-ngl", dest="ngl", type=int, default=None,
                     help="accepted for llama-server compatibility (all layers always run on the GPU)")
     ap.add_argument("--log-level", default=os.environ.get("HIPSERVE_LOG_LEVEL", "INFO"))
+    ap.add_argument("--log-format", default=None, choices=["text", "json"],
+                    help="text (default) or one JSON object per line (HIPSERVE_LOG_FORMAT)")
     return ap
 
 
@@ -102,8 +103,8 @@ def _worker(cfg: EngineConfig, rank: int, world: int, port: int):
 
 def main(argv=None, prog="hipserve"):
     a = build_parser(prog).parse_args(argv)
-    logging.basicConfig(level=a.log_level.upper(),
-                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    from ..utils.logs import setup_logging
+    setup_logging(a.log_level, a.log_format)
     cfg = config_from_args(a)
     world = cfg.tensor_parallel_size
     procs = []

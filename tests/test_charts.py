@@ -203,3 +203,14 @@ def test_argocd_applications_render(app):
     assert any(d["kind"] == "Deployment" for d in docs)
     sp = a["spec"]["syncPolicy"]["automated"]
     assert sp["prune"] and sp["selfHeal"]
+
+
+def test_hf_engine_log_format_env():
+    """engine.logFormat reaches the pod as HIPSERVE_LOG_FORMAT (text by default)."""
+    def env_of(values):
+        d = by_kind(render(HF, values), "Deployment")["hipserve-llama-3-8b"]
+        env = d["spec"]["template"]["spec"]["containers"][0]["env"]
+        return {e["name"]: e.get("value") for e in env}
+
+    assert env_of({})["HIPSERVE_LOG_FORMAT"] == "text"
+    assert env_of({"engine": {"logFormat": "json"}})["HIPSERVE_LOG_FORMAT"] == "json"
