@@ -201,3 +201,56 @@ def test_client_disconnect_aborts_generation():
         await r1.cleanup()
 
     asyncio.run(main())
+
+
+def test_asyncio_debug_mode_clean(caplog):
+    """The request path under asyncio debug mode (SURVEY §5 race detection: "CPU-side
+    asyncio debug mode"): concurrent streaming and non-streaming requests plus a client
+    that disconnects mid-stream leave no never-retrieved task exception, no coroutine
+    that was never awaited and no non-threadsafe loop call from the engine thread."""
+    import gc
+    import logging
+    import warnings
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        loop.slow_callback_duration = 10.0  # CPU model steps are slow; only correctness is checked
+        ae, runner, port = await start_engine_server()
+        base = f"http://127.0.0.1:{port}"
+        async with aiohttp.ClientSession() as s:
+            async def stream(i):
+                r = await s.post(base + "/v1/chat/completions", json={
+                    "model": "tiny", "messages": [{"role": "user", "content": f"hi {i}"}], "max_tokens": 5,
+                    "stream": True, "ignore_eos": True})
+                return await sse_events(r)
+
+            async def plain(i):
+                r = await s.post(base + "/v1/completions", json={"model": "tiny", "prompt": [1, 2, i + 3],
+                                                                 "max_tokens": 4, "ignore_eos": True})
+                return await r.json()
+
+            res = await asyncio.gather(*[stream(i) for i in range(4)], *[plain(i) for i in range(4)])
+            assert all(r[-1] == "[DONE]" for r in res[:4])
+            assert all(r["usage"]["completion_tokens"] == 4 for r in res[4:])
+            # a client that goes away mid-stream
+            reader, writer = await asyncio.open_connection("127.0.0.1", port)
+            body = json.dumps({"model": "tiny", "prompt": [5, 6], "max_tokens": 200, "stream": True,
+                               "ignore_eos": True}).encode()
+            writer.write(b"POST /v1/completions HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                         b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+            await writer.drain()
+            await reader.readline()
+            writer.close()
+            await asyncio.sleep(0.3)
+            assert (await s.get(base + "/health")).status == 200
+        ae.stop()
+        await runner.cleanup()
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)  # "coroutine ... was never awaited"
+        with caplog.at_level(logging.WARNING, logger="asyncio"):
+            asyncio.run(main(), debug=True)
+            gc.collect()
+    bad = [r for r in caplog.records if r.name == "asyncio" and r.levelno >= logging.WARNING
+           and "took" not in r.getMessage()]
+    assert not bad, [r.getMessage() for r in bad]
