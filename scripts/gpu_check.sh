@@ -120,6 +120,9 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     g27fp8_16k) bench_named g27fp8_16k X=1 -- --model gemma-3-27b --quantization fp8 --max-num-batched-tokens 16384 ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
+    blocking) HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py \
+      tests/test_fused_decode_gpu.py tests/test_engine_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+      > $OUT/pytest_blocking.log 2>&1; rc=$?; tail -n 5 $OUT/pytest_blocking.log; [ $rc -eq 0 ] ;;
     attnchunk) timeout -k 10 300 python -u tools/bench_ops.py prefill_chunked > $OUT/attn_chunked.log 2>&1; rc=$?; cat $OUT/attn_chunked.log; [ $rc -eq 0 ] ;;
     g27fp8_res) bench_named g27fp8_res HIPSERVE_FP8_PREFILL_LIB=resident -- --model gemma-3-27b --quantization fp8 ;;
     q3int8_noshadow) bench_named q3int8_noshadow HIPSERVE_FUSED_DECODE=1 HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 ;;
