@@ -141,20 +141,39 @@ class GemmTuner:
                     (lambda i: F.linear(x, ws_[i % ncopy]))
                 best, best_t = "blas", self._time(blas_fn, n=n)
                 t_blas = best_t
+                timed = []
                 for cfg in self.candidates(M, N, K, packed=wp_ is not None, glu=glu):
                     if unit is not None:
                         if cfg[0] == "sk":
                             continue
-                        fn = (lambda i: unit.fused(cfg, x, ws_[i % ncopy], wp_[i % ncopy] if wp_ else None))
+                        fn = (lambda i, cfg=cfg: unit.fused(cfg, x, ws_[i % ncopy], wp_[i % ncopy] if wp_ else None))
                     else:
-                        fn = (lambda i: run_choice(cfg, out, x, ws_[i % ncopy], wp_[i % ncopy] if wp_ else None))
-                    t = self._time(fn, n=n)
+                        fn = (lambda i, cfg=cfg: run_choice(cfg, out, x, ws_[i % ncopy],
+                                                            wp_[i % ncopy] if wp_ else None))
+                    timed.append((self._time(fn, n=n), cfg, fn))
+                # confirmation round: the three fastest re-timed in interleaved rounds (median),
+                # so one noisy first-round sample cannot pick a config that runs ~20 % slower in
+                # the engine (a box once kept the 128-row o_proj body at 12 us over the 64-row
+                # one at 9.7 us on a 2 % first-round difference)
+                finalists = sorted(timed, key=lambda e: e[0])[:3]
+                rounds = {id(e): [e[0]] for e in finalists}
+                for _ in range(2):
+                    for e in finalists:
+                        rounds[id(e)].append(self._time(e[2], n=n))
+                for e in finalists:
+                    v = sorted(rounds[id(e)])
+                    t, cfg = v[len(v) // 2], e[1]
                     if cfg[0] == "dgp":
                         bp = self.best_packed.get((M, N, K))
                         if bp is None or t < bp[1]:
                             self.best_packed[(M, N, K)] = (cfg, t)
-                    if t < best_t * 0.97:
+                    if t < best_t * (0.97 if best == "blas" else 1.0):
                         best, best_t = cfg, t
+                if (M, N, K) not in self.best_packed:  # no packed finalist: the fastest packed config
+                    dg = [(t, cfg) for t, cfg, _ in timed if cfg[0] == "dgp"]
+                    if dg:
+                        t, cfg = min(dg)
+                        self.best_packed[(M, N, K)] = (cfg, t)
                 self.table[(M, N, K)] = best
                 row = {"M": M, "N": N, "K": K, "unit": spec[0] if spec else "gemm",
                        "blas_us": round(t_blas, 1), "best": str(best), "best_us": round(best_t, 1),
