@@ -48,6 +48,10 @@ run_bench_q4() {
 # summarised by tools/prof_db.py into $OUT/<name>_summary.md.
 prof_run() {
   local here=$PWD name=$1; shift
+  # an unprofiled start first fills the tuning cache, so the profiled run replays the
+  # decode GEMM choices of an unprofiled engine (kernel tracing skews start-up timings)
+  timeout -k 10 480 python -u bench.py --path engine --steps 1 --warmup 0 --tp-phase off "$@" \
+    > $OUT/${name}_tune.log 2>&1 || return $?
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 480 rocprofv3 --kernel-trace --stats -d $here/$OUT/$name \
      -o run -- python3 $here/bench.py --path engine --steps 1 --warmup 1 --tp-phase off "$@" > $here/$OUT/$name.log 2>&1)
   local rc=$?; tail -n 3 $OUT/$name.log
@@ -120,6 +124,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     g27fp8_16k) bench_named g27fp8_16k X=1 -- --model gemma-3-27b --quantization fp8 --max-num-batched-tokens 16384 ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
+    tuneprobe) timeout -k 10 300 python -u tools/tune_probe.py > $OUT/tune_probe.log 2>&1; rc=$?; cat $OUT/tune_probe.log; [ $rc -eq 0 ] ;;
     blocking) HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py \
       tests/test_fused_decode_gpu.py tests/test_engine_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
       > $OUT/pytest_blocking.log 2>&1; rc=$?; tail -n 5 $OUT/pytest_blocking.log; [ $rc -eq 0 ] ;;
