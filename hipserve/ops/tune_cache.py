@@ -11,7 +11,7 @@ kernels, so they are stored in one JSON file per fingerprint:
 
     $HIPSERVE_TUNE_CACHE/<fingerprint>.json     (default ~/.cache/hipserve/tune)
 
-fingerprint = sha1(device name, gfx arch, CU count, torch version, hipserve/_C.so bytes):
+fingerprint = sha1(device capability, CU count, HBM GiB, torch version, hipserve/_C.so bytes):
 a new GPU model, a driver-visible CU count change or a rebuilt kernel library re-tunes.
 ``HIPSERVE_TUNE_CACHE=0`` disables the cache (every start times everything). Writers
 merge with the file on disk and replace it atomically, so TP ranks sharing a volume
@@ -55,8 +55,11 @@ def fingerprint(device) -> str:
     idx = torch.device(device).index or 0
     fp = _FP.get(idx)
     if fp is None:
+        # not the marketing name: it reads "" under rocprofv3, which would make profiled
+        # runs miss the tables of unprofiled ones (and re-tune with tracing overhead)
         pr = torch.cuda.get_device_properties(idx)
-        ident = [pr.name, getattr(pr, "gcnArchName", ""), pr.multi_processor_count, torch.__version__, _lib_digest()]
+        ident = [list(torch.cuda.get_device_capability(idx)), pr.multi_processor_count,
+                 round(pr.total_memory / 2**30), torch.__version__, _lib_digest()]
         fp = _FP[idx] = hashlib.sha1(json.dumps(ident).encode()).hexdigest()[:16]
     return fp
 
