@@ -417,6 +417,8 @@ def run_phase(args):
     if args.quantization:  # resident bytes beyond the quantised weights, GGUF prefill path per shape
         out["quant_shadow_gb"] = round(getattr(engine.runner, "quant_shadow_bytes", 0) / 2**30, 2)
         out["gguf_prefill_timing"] = getattr(engine.runner, "qprefill_report", None)
+    if getattr(engine.runner, "moe_prefill_report", None) is not None:
+        out["moe_prefill_timing"] = engine.runner.moe_prefill_report
     if ol_summary:  # open loop: TTFT tail and inter-token latency of every request
         out["open_loop"] = {"rate_req_s": args.request_rate, "requests": ol_summary["requests"],
                             **{k: round(ol_summary[k], 2) for k in ("p50_ttft_ms", "p90_ttft_ms", "p50_itl_ms",

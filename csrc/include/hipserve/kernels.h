@@ -240,7 +240,7 @@ void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S
                               const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
                               int nkv, int D, int block_size, int mode, hipStream_t s, const void* bias = nullptr,
                               const float* qw = nullptr, const float* kw = nullptr, float eps = 1e-6f);
-void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s);
+void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s, int batch = 1);
 }  // namespace hipserve
 
 namespace hipserve {

@@ -615,6 +615,9 @@ __global__ __launch_bounds__(256) void pack_decode_weight_kernel(unsigned short*
                                                                  long pieces, int glu) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= pieces) return;
+  // blockIdx.y: one matrix of a stacked batch (MoE experts), packed back to back
+  out += (long)blockIdx.y * pieces * 8;
+  w += (long)blockIdx.y * N * K;
   // piece index = ((((tile * KS + kstep) * 8 + rg) * 8 + s) * 64 + lane)
   const int lane = i & 63, sl = (i >> 6) & 7, rg = (i >> 9) & 7;
   const long ts = i >> 12;
@@ -633,12 +636,12 @@ __global__ __launch_bounds__(256) void pack_decode_weight_kernel(unsigned short*
   *reinterpret_cast<u16x8*>(out + i * 8) = v;
 }
 
-void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s) {
+void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s, int batch) {
   const long tiles = (N + 127) / 128;
   const long pieces = tiles * (K / 256) * 8 * 8 * 64;
-  pack_decode_weight_kernel<<<(pieces + 255) / 256, 256, 0, s>>>(static_cast<unsigned short*>(out),
-                                                                 static_cast<const unsigned short*>(w), N, K, pieces,
-                                                                 glu ? 1 : 0);
+  if (batch <= 0) return;
+  pack_decode_weight_kernel<<<dim3((pieces + 255) / 256, batch), 256, 0, s>>>(
+      static_cast<unsigned short*>(out), static_cast<const unsigned short*>(w), N, K, pieces, glu ? 1 : 0);
 }
 
 }  // namespace hipserve

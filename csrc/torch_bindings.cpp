@@ -1022,14 +1022,17 @@ void splitk_glu(at::Tensor& act, const at::Tensor& ws, int64_t splits, bool gelu
                               cur_stream(), a16);
 }
 
+// w [N, K], or a stack [E, N, K] (MoE experts: one launch, out = E packed copies back to back)
 void pack_decode_weight(at::Tensor& out, const at::Tensor& w, bool glu) {
   CHECK_DEV(w); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_BF16(out); CHECK_CONTIG(out);
-  TORCH_CHECK(w.dim() == 2 && w.size(1) % 256 == 0, "pack_decode_weight: w [N, K], K % 256 == 0");
-  const long N = w.size(0), K = w.size(1);
-  TORCH_CHECK(out.numel() == (N + 127) / 128 * 128 * K, "pack_decode_weight: out must hold ceil(N/128)*128*K");
+  TORCH_CHECK((w.dim() == 2 || w.dim() == 3) && w.size(-1) % 256 == 0,
+              "pack_decode_weight: w [N, K] or [E, N, K], K % 256 == 0");
+  const long E = w.dim() == 3 ? w.size(0) : 1, N = w.size(-2), K = w.size(-1);
+  TORCH_CHECK(out.numel() == E * ((N + 127) / 128 * 128 * K), "pack_decode_weight: out must hold E*ceil(N/128)*128*K");
   TORCH_CHECK(!glu || N % 128 == 0, "pack_decode_weight: glu packing needs N % 128 == 0");
+  TORCH_CHECK(E <= 65535, "pack_decode_weight: at most 65535 stacked matrices");
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
-  hipserve::launch_pack_decode_weight(out.data_ptr(), w.data_ptr(), N, K, glu, cur_stream());
+  hipserve::launch_pack_decode_weight(out.data_ptr(), w.data_ptr(), N, K, glu, cur_stream(), (int)E);
 }
 
 void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots, at::Tensor& tile_expert,

@@ -178,6 +178,9 @@ class ModelRunner:
                 # FP8: which projections prefill on hipBLASLt's FP8 GEMM (a per-call
                 # re-layout of the tiled copy by default, ops/quant.py FP8_LIB)
                 self.quant_shadow_bytes += Q.make_fp8_plain(qws, self.device, (24 << 30) + total // 4)
+            if getattr(self.mcfg, "num_experts", 0) and hasattr(self.model, "tune_moe_prefill"):
+                # MoE prefill expert GEMMs: hipBLASLt grouped vs the packed one-launch kernel
+                self.moe_prefill_report = self.model.tune_moe_prefill(min(ecfg.max_num_batched_tokens, 16384))
             torch.cuda.empty_cache()
         self.init_times["decode_gemm_tune_s"] = round(time.time() - t1, 2)
         t1 = time.time()

@@ -474,9 +474,8 @@ class LlamaModel:
                 _, N2, K2 = lw.w2.shape
                 p13 = torch.empty(E, N13 * K13, dtype=lw.w13.dtype, device=lw.w13.device)
                 p2 = torch.empty(E, -(-N2 // 128) * 128 * K2, dtype=lw.w2.dtype, device=lw.w2.device)
-                for e in range(E):
-                    op.pack_decode_weight(p13[e], lw.w13[e], True)
-                    op.pack_decode_weight(p2[e], lw.w2[e], False)
+                op.pack_decode_weight(p13, lw.w13.contiguous(), True)  # all experts in one launch
+                op.pack_decode_weight(p2, lw.w2.contiguous(), False)
                 lw.moe_packed = (p13, p2)
             if drop_plain and self.moe_packed_prefill(lw, for_drop=True):
                 freed += 2 * (lw.w13.numel() + lw.w2.numel())
@@ -906,12 +905,19 @@ class LlamaModel:
                 return self.moe_quant(x, lw)
             from ..ops import quant as Q
 
+            if self.moe_prefill_packed and self._moe_packed_shape_ok() and lw.w13.dense is None:
+                # experts dequantised + packed per step, then the one-launch grouped GEMMs
+                lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router,
+                                  moe_packed=(Q.moe_packed_scratch(lw.w13, 0, True),
+                                              Q.moe_packed_scratch(lw.w2, 1, False)))
+                return self.moe_grouped(x, lw)
             lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router,
                               w13=Q.moe_dense(lw.w13, 0), w2=Q.moe_dense(lw.w2, 1))
         if (self.ops.name == "hip" and cfg.num_experts <= 128 and cfg.hidden_size % 256 == 0
                 and self.inter % 256 == 0
                 and (P <= MOE_KERNEL_MAX_PAIRS
-                     or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts and self._moe_decode_ok(lw)))):
+                     or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts and self._moe_decode_ok(lw)
+                         and self.moe_prefill_path in (None, "hip")))):
             return self.moe_hip(x, lw)
         if self.ops.name == "hip" and cfg.num_experts <= 128 and self.moe_packed_prefill(lw):
             return self.moe_grouped(x, lw)
@@ -1010,20 +1016,98 @@ class LlamaModel:
         return out
 
     # packed-layout grouped expert GEMMs for prefill: always when the row-major experts were
-    # dropped (single weight layout), else opt-in — with both copies resident, hipBLASLt's
-    # grouped GEMM measured faster on Mixtral-8x7B (1,632 vs 1,602 tok/s, TTFT 561 vs 641 ms,
-    # profiles/r4_bench_mixtral_*.json) despite its host round trip
+    # dropped (single weight layout); otherwise ``auto`` follows the start-up timing of the
+    # layer's expert shape (``tune_moe_prefill``): hipBLASLt's grouped GEMM (per-expert
+    # launches after a host read of the offsets) wins with few large experts (Mixtral-8x7B:
+    # 5.4 vs 6.4 ms per layer at 8K tokens), the one-launch packed kernel with many small
+    # ones (Qwen3-30B-A3B, 128 experts: 1.0 vs 4.8 ms at 8K, 3.6 vs 6.3 at 32K;
+    # profiles/r5_bench_moe_prefill.log)
     MOE_PACKED_PREFILL = os.environ.get("HIPSERVE_MOE_PACKED_PREFILL", "auto")
+    moe_prefill_path: str | None = None  # "hip" | "blas" | "packed", set by tune_moe_prefill
+
+    @property
+    def moe_prefill_packed(self) -> bool:
+        return self.moe_prefill_path == "packed"
+
+    def _moe_packed_shape_ok(self) -> bool:
+        return (self.cfg.hidden_act == "silu" and self.cfg.hidden_size % 256 == 0 and self.inter % 256 == 0
+                and (2 * self.inter) % 128 == 0 and hasattr(torch.ops.hipserve, "prefill_gemm_packed_grouped"))
 
     def moe_packed_prefill(self, lw: LayerWeights, for_drop: bool = False) -> bool:
         """Prefill experts on the packed-layout grouped GEMM (the decode kernels' copy of
         the experts, ``pack_moe_weights``): SiLU-GLU experts, K of both GEMMs % 256."""
         mode = self.MOE_PACKED_PREFILL
-        if mode == "0" or (mode == "auto" and not for_drop and lw.w13 is not None):
+        if mode == "0" or lw.moe_packed is None or not self._moe_packed_shape_ok():
             return False
-        return (lw.moe_packed is not None and self.cfg.hidden_act == "silu"
-                and self.cfg.hidden_size % 256 == 0 and self.inter % 256 == 0 and (2 * self.inter) % 128 == 0
-                and hasattr(torch.ops.hipserve, "prefill_gemm_packed_grouped"))
+        if mode == "1" or for_drop or lw.w13 is None:
+            return True
+        return self.moe_prefill_path == "packed"
+
+    @torch.inference_mode()
+    def tune_moe_prefill(self, T: int) -> dict | None:
+        """Start-up timing of one MoE layer's prefill at ``T`` tokens on random bf16 experts
+        of the layer's shape, through the model's own paths: the weight-streaming expert
+        kernel (``moe_hip``, where its row limit allows), hipBLASLt's grouped GEMM and the
+        packed one-launch grouped kernel (``moe_grouped``; for quantised experts with the
+        per-step pack of the dequantised experts added). Sets ``moe_prefill_path``;
+        cached per device and kernel build."""
+        from ..ops import tune_cache as TC
+
+        cfg = self.cfg
+        lw = next((lw for lw in self.layers if lw.router is not None), None)
+        if (lw is None or not self._moe_packed_shape_ok() or not hasattr(torch, "_grouped_mm")
+                or self.MOE_PACKED_PREFILL != "auto" or getattr(self.ops, "name", "") != "hip"
+                or self.device.type != "cuda" or cfg.num_experts > 128):
+            return None
+        E, k, H, I = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size, self.inter
+        quant = lw.w13 is not None and not isinstance(lw.w13, torch.Tensor)
+        if not quant and (lw.moe_packed is None or lw.w13 is None):
+            return None
+        key = [E, k, H, I, T, quant]
+        hit = TC.get(self.device, "moe_prefill", key)
+        if hit is not None:
+            self.moe_prefill_path = hit["path"]
+            return dict(hit, cached=True)
+        op, dev = torch.ops.hipserve, self.device
+        g = torch.Generator(device=dev).manual_seed(E * H + I)
+        w13 = (torch.randn(E, 2 * I, H, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        w2 = (torch.randn(E, H, I, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        p13 = torch.empty(E, 2 * I * H, dtype=torch.bfloat16, device=dev)
+        p2 = torch.empty(E, -(-H // 128) * 128 * I, dtype=torch.bfloat16, device=dev)
+        op.pack_decode_weight(p13, w13, True)
+        op.pack_decode_weight(p2, w2, False)
+        router = (torch.randn(E, H, device=dev, generator=g) * 0.3).to(torch.bfloat16)
+        x = torch.randn(T, H, device=dev, generator=g).to(torch.bfloat16)
+        syn = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=router, w13=w13, w2=w2,
+                           moe_packed=(p13, p2))
+        saved = self.moe_prefill_path
+
+        def via(path):
+            def fn(i):
+                self.moe_prefill_path = path
+                if path == "hip":
+                    return self.moe_hip(x, syn)
+                if path == "packed" and quant:  # the per-step pack of the dequantised experts
+                    op.pack_decode_weight(p13, w13, True)
+                    op.pack_decode_weight(p2, w2, False)
+                return self.moe_grouped(x, syn)
+            return fn
+
+        paths = ["blas", "packed"]
+        if not quant and T * k <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * E and self._moe_decode_ok(syn):
+            paths.insert(0, "hip")
+        times = {p_: pgemm._time(via(p_), reps=2) for p_ in paths}
+        self.moe_prefill_path = saved
+        del w13, w2, p13, p2, x, syn
+        torch.cuda.empty_cache()
+        best = min(times, key=times.get)
+        self.moe_prefill_path = best
+        r = {"E": E, "H": H, "I": I, "tokens": T, "quant": quant, "path": best,
+             **{f"{p_}_ms": round(t, 3) for p_, t in times.items()}}
+        TC.put(self.device, "moe_prefill", key, r)
+        TC.flush()
+        log.info("MoE prefill expert GEMMs: %s", r)
+        return r
 
     def moe_hip(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Graph-capturable MoE on the gfx950 kernels (decode-sized batches): top-k

@@ -895,6 +895,25 @@ def moe_dense(w: QuantMoE, slot: int) -> torch.Tensor:
     return w.dequantize(buf[:n].view(w.E, w.N, w.K))
 
 
+_MOE_PACKED_SCRATCH: dict = {}
+
+
+def moe_packed_scratch(w: QuantMoE, slot: int, glu: bool) -> torch.Tensor:
+    """[E, packed] bf16 experts in the packed prefill GEMM's layout (``pack_decode_weight``,
+    gate/up-interleaved for w13): dequantised into the row-major scratch of ``moe_dense``,
+    then packed in one launch into a second per-device scratch — the operand of the
+    one-launch grouped expert GEMM (prefill_gemm_packed.hip kGroup)."""
+    dense = moe_dense(w, slot)
+    key = (w.q.device, slot)
+    n = w.E * (-(-w.N // 128) * 128) * w.K
+    buf = _MOE_PACKED_SCRATCH.get(key)
+    if buf is None or buf.numel() < n:
+        buf = _MOE_PACKED_SCRATCH[key] = torch.empty(n, dtype=torch.bfloat16, device=w.q.device)
+    out = buf[:n].view(w.E, n // w.E)
+    torch.ops.hipserve.pack_decode_weight(out, dense.contiguous(), glu)
+    return out
+
+
 def make_moe_shadows(moes, device, reserve_bytes: int) -> int:
     """bf16 shadows of quantised experts for prefill while ``reserve_bytes`` stay free."""
     import os

@@ -117,6 +117,9 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     b8_chunk16k) bench_named b8_chunk16k -- --max-num-batched-tokens 16384 ;;
     q4km_chunk8k) bench_named q4km_chunk8k -- --quantization q4_k_m --max-num-batched-tokens 8192 ;;
     q4km_default) bench_named q4km_default -- --quantization q4_k_m ;;
+    q3bf16) bench_named q3bf16 X=1 -- --model qwen3-30b-a3b ;;
+    q3int8_8k) bench_named q3int8_8k X=1 -- --model qwen3-30b-a3b --quantization int8 --max-num-batched-tokens 8192 ;;
+    q3int8_16k) bench_named q3int8_16k X=1 -- --model qwen3-30b-a3b --quantization int8 --max-num-batched-tokens 16384 ;;
     mixtral16k) bench_named mixtral16k X=1 -- --model mixtral-8x7b --concurrency 32 --max-num-batched-tokens 16384 ;;
     mixtral32k) bench_named mixtral32k X=1 -- --model mixtral-8x7b --concurrency 32 --max-num-batched-tokens 32768 ;;
     q3int8_noshadow16k) bench_named q3int8_noshadow16k HIPSERVE_QUANT_SHADOW=0 -- --model qwen3-30b-a3b --quantization int8 --max-num-batched-tokens 16384 ;;
@@ -124,6 +127,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     g27fp8_16k) bench_named g27fp8_16k X=1 -- --model gemma-3-27b --quantization fp8 --max-num-batched-tokens 16384 ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
+    moeprefill) timeout -k 10 300 python -u tools/bench_moe_prefill.py > $OUT/bench_moe_prefill.log 2>&1; rc=$?; cat $OUT/bench_moe_prefill.log; [ $rc -eq 0 ] ;;
     tuneprobe) timeout -k 10 300 python -u tools/tune_probe.py > $OUT/tune_probe.log 2>&1; rc=$?; cat $OUT/tune_probe.log; [ $rc -eq 0 ] ;;
     blocking) HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py \
       tests/test_fused_decode_gpu.py tests/test_engine_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
@@ -168,6 +172,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
               -p no:cacheprovider > $OUT/test_tp_gpu.log 2>&1; rc=$?; tail -n 20 $OUT/test_tp_gpu.log; [ $rc -eq 0 ] ;;
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof_g27) prof_run profg27 --model gemma-3-27b ;;
+    prof_q3int8) prof_run profq3 --model qwen3-30b-a3b --quantization int8 ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     prof70) prof_run prof70 --model llama-3-70b ;;

@@ -178,3 +178,50 @@ def test_int8_expert_checkpoint_native(tmp_path):
     assert a.shape == b.shape
     assert (a - b).abs().max().item() < 5e-2 * b.abs().max().item() + 1e-3
     assert (a.argmax(-1) == b.argmax(-1)).float().mean().item() >= 0.85
+
+
+@pytest.mark.parametrize("kind", ["int8", "fp8"])
+@pytest.mark.parametrize("packed", [False, True])
+def test_quant_moe_prefill_paths_vs_fp32(kind, packed):
+    """Prefill-sized routing of quantised experts: the row-major dequantised scratch with
+    hipBLASLt's grouped GEMM, and the dequantised + packed scratch with the one-launch
+    packed grouped GEMM (``moe_prefill_path = "packed"``), both against the fp32 reference."""
+    from hipserve.config import PRESETS
+    from hipserve.models import llama as L
+    from hipserve.models.llama import LayerWeights, LlamaModel
+    from hipserve.ops import KernelOps
+    from hipserve.ops import quant as Q
+    from hipserve.parallel.comm import TPGroup
+
+    H, I, E, k = 512, 512, 16, 4
+    T = L.MOE_KERNEL_MAX_PAIRS // k + 300
+    cfg = PRESETS["tiny-mixtral"].replace(hidden_size=H, intermediate_size=I, num_experts=E, num_experts_per_tok=k)
+    m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, KernelOps())
+    m.moe_prefill_path = "packed" if packed else "blas"
+    torch.manual_seed(7)
+    router = torch.randn(E, H, device=DEV, dtype=torch.bfloat16) * 0.3
+    w13, d13 = _qmoe(torch.randn(E, 2 * I, H, device=DEV) * 0.05, kind)
+    w2, d2 = _qmoe(torch.randn(E, H, I, device=DEV) * 0.05, kind)
+    lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=router, w13=w13, w2=w2)
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    got = m.moe(x, lw).float()
+    logits = torch.nn.functional.linear(x, router).float()
+    wts, idx = torch.topk(torch.softmax(logits, -1), k, -1)
+    wts = wts / wts.sum(-1, keepdim=True)
+    want = torch.zeros(T, H, device=DEV)
+    xf = x.float()
+    for e in range(E):
+        rows, slot = (idx == e).nonzero(as_tuple=True)
+        if rows.numel() == 0:
+            continue
+        gu = xf[rows] @ d13[e].T
+        act = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+        want.index_add_(0, rows, (act @ d2[e].T) * wts[rows, slot].unsqueeze(-1))
+    err = (got - want).abs().max().item()
+    assert err <= 3e-2 * want.abs().max().item() + 1e-3, err
+    if packed:  # the packed scratch is the batched pack of the dequantised experts
+        from hipserve.ops import gemm
+
+        ps = Q.moe_packed_scratch(w13, 0, True)
+        for e in (0, E - 1):
+            assert torch.equal(ps[e], gemm.pack(Q.moe_dense(w13, 0)[e].contiguous(), glu=True))
