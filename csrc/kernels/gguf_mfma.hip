@@ -383,9 +383,14 @@ void moe_launch_t(void* out, long out_stride, float* ws, const void* x, long x_s
 // ---------------------------------------------------------------- tiled -> bf16
 // Prefill: one wave per (row group, super-chunk) chunk, out[N, K] row-major bf16.
 template <int QT>
+// pack: 0 = row-major [N, K]; 1 / 2 = the packed prefill / decode GEMM layout of
+// pack_decode_weight (2: gate/up-interleaved) for each stacked matrix of `nrows` rows
+// (MoE experts: the row groups of expert e are [e nrows / 16, (e + 1) nrows / 16)) —
+// every 8-value store of a lane is exactly one packed 16-byte piece.
 __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __restrict__ out,
                                                             const unsigned char* __restrict__ q,
-                                                            const float* __restrict__ rs, int ngroups, int K) {
+                                                            const float* __restrict__ rs, int ngroups, int K,
+                                                            int pack, int nrows) {
   constexpr int CB = chunk_bytes<QT>();
   const int nsb = K >> 8;
   const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -397,6 +402,21 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
   Dec<QT> dec;
   dec.setup(r, g);
   unsigned short* row = out + (long)(16 * gi + c) * K + sb * 256;
+  if (pack) {  // base of this lane's pieces in the packed copy of its matrix
+    const int e = (16 * gi) / nrows, n = 16 * gi + c - e * nrows;
+    int t, rgi;
+    if (pack == 2) {  // tile t: gate rows [64 t, 64 t + 64), then the matching up rows
+      const int half = nrows >> 1, up = n >= half, nn = up ? n - half : n;
+      t = nn >> 6;
+      rgi = (up ? 64 : 0) + (nn & 63);
+    } else {
+      t = n >> 7;
+      rgi = n & 127;
+    }
+    // piece ((((t KS + sb) 8 + rg) 8 + s) 64 + lane), rg = rgi / 16, lane = g' 16 + (rgi % 16)
+    row = out + (long)e * ((nrows + 127) / 128 * 128) * K +
+          ((((long)t * (K >> 8) + sb) * 8 + (rgi >> 4)) * 8 * 64 + (rgi & 15)) * 8;
+  }
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const f16x8 q = dec.ints(r, g, s);  // exact integers, pair order {0, 2, 1, 3, 4, 6, 5, 7}
@@ -407,7 +427,11 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16((float)q[src[j]] * d + m);
-    *reinterpret_cast<u16x8*>(row + kbase<QT>(g, s)) = o;
+    const int kb = kbase<QT>(g, s);
+    if (pack)  // k = 32 s' + 8 g' within the superblock -> slot s', lane g' 16 + row
+      *reinterpret_cast<u16x8*>(row + ((kb >> 5) * 64 + ((kb >> 3) & 3) * 16) * 8) = o;
+    else
+      *reinterpret_cast<u16x8*>(row + kb) = o;
   }
 }
 
@@ -881,21 +905,23 @@ void launch_fp8_untile(void* out, const void* q, int N, int K, hipStream_t s) {
                                                      static_cast<const unsigned char*>(q), K);
 }
 
-void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s) {
+void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s,
+                               int pack, int nrows) {
+  if (nrows <= 0) nrows = N;
   const long items = (long)(N / 16) * (K / 256);
   const dim3 grid((unsigned)((items + 3) / 4)), block(256);
   auto* o = static_cast<unsigned short*>(out);
   auto* qq = static_cast<const unsigned char*>(q);
   switch (qtype) {
-    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
-    case INT8: dequant_tiled_kernel<INT8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K); break;
+    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case INT8: dequant_tiled_kernel<INT8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
   }
 }
 

@@ -455,8 +455,9 @@ def default_batched_tokens(model: str, load_format: str = "auto", quantization: 
     cost that more tokens per step spread thinner:
       * Llama-3-8B Q4_K_M: 7,726 -> 8,044 tok/s, p50 TTFT 482 -> 530 ms
         (profiles/r5_bench_q4km_chunk8k.json, r5_bench_q4km_chunk16k.json);
-      * Qwen3-30B-A3B INT8 (experts dequantised + packed per step for the one-launch grouped
-        GEMM): 4,134 / 646 ms (8K) -> 4,380 / 570 (16K) -> 4,531 / 570 (32K), above the
+      * Qwen3-30B-A3B INT8 (experts dequantised into the one-launch grouped GEMM's packed
+        layout): 4,134 / 646 ms (8K) -> 4,380 / 570 (16K) -> 4,531 / 570 (32K) with a separate
+        pack pass, 4,666 / 490 (32K) dequantising straight into the layout; above the
         4,155 / 623 ms of bf16 prefill shadows at 8K with 34 % more KV blocks
         (profiles/r5_bench_q3int8_packed_moe_*.json, r5_bench_q3int8_shadows.json).
     FP8 keeps 8192 (Gemma-3-27B: 2,839 vs 2,854 tok/s at 16K, TTFT 1,110 vs 1,186 ms), and

@@ -906,7 +906,7 @@ class LlamaModel:
             from ..ops import quant as Q
 
             if self.moe_prefill_packed and self._moe_packed_shape_ok() and lw.w13.dense is None:
-                # experts dequantised + packed per step, then the one-launch grouped GEMMs
+                # experts dequantised straight into the packed layout, then the one-launch grouped GEMMs
                 lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router,
                                   moe_packed=(Q.moe_packed_scratch(lw.w13, 0, True),
                                               Q.moe_packed_scratch(lw.w2, 1, False)))
@@ -1048,8 +1048,7 @@ class LlamaModel:
         """Start-up timing of one MoE layer's prefill at ``T`` tokens on random bf16 experts
         of the layer's shape, through the model's own paths: the weight-streaming expert
         kernel (``moe_hip``, where its row limit allows), hipBLASLt's grouped GEMM and the
-        packed one-launch grouped kernel (``moe_grouped``; for quantised experts with the
-        per-step pack of the dequantised experts added). Sets ``moe_prefill_path``;
+        packed one-launch grouped kernel (``moe_grouped``). Sets ``moe_prefill_path``;
         cached per device and kernel build."""
         from ..ops import tune_cache as TC
 
@@ -1087,9 +1086,8 @@ class LlamaModel:
                 self.moe_prefill_path = path
                 if path == "hip":
                     return self.moe_hip(x, syn)
-                if path == "packed" and quant:  # the per-step pack of the dequantised experts
-                    op.pack_decode_weight(p13, w13, True)
-                    op.pack_decode_weight(p2, w2, False)
+                # (quantised experts: both grouped paths dequantise once per step, into the
+                # row-major or straight into the packed scratch, at the same cost: not timed)
                 return self.moe_grouped(x, syn)
             return fn
 

@@ -900,17 +900,19 @@ _MOE_PACKED_SCRATCH: dict = {}
 
 def moe_packed_scratch(w: QuantMoE, slot: int, glu: bool) -> torch.Tensor:
     """[E, packed] bf16 experts in the packed prefill GEMM's layout (``pack_decode_weight``,
-    gate/up-interleaved for w13): dequantised into the row-major scratch of ``moe_dense``,
-    then packed in one launch into a second per-device scratch — the operand of the
-    one-launch grouped expert GEMM (prefill_gemm_packed.hip kGroup)."""
-    dense = moe_dense(w, slot)
+    gate/up-interleaved for w13), dequantised straight into it (one launch over all
+    experts, gguf_mfma.hip dequant_tiled_kernel pack mode): the operand of the one-launch
+    grouped expert GEMM (prefill_gemm_packed.hip kGroup), in a per-device scratch."""
+    if w.dense is not None:
+        raise ValueError("moe_packed_scratch: experts with a bf16 shadow take the shadow path")
     key = (w.q.device, slot)
     n = w.E * (-(-w.N // 128) * 128) * w.K
     buf = _MOE_PACKED_SCRATCH.get(key)
     if buf is None or buf.numel() < n:
         buf = _MOE_PACKED_SCRATCH[key] = torch.empty(n, dtype=torch.bfloat16, device=w.q.device)
     out = buf[:n].view(w.E, n // w.E)
-    torch.ops.hipserve.pack_decode_weight(out, dense.contiguous(), glu)
+    torch.ops.hipserve.gguf_dequant_tiled(out.view(-1), w.q.view(-1), w.rs.view(-1) if w.rs.numel() else w.rs,
+                                          w.kqt, w.E * w.N, w.K, 2 if glu else 1, w.N)
     return out
 
 

@@ -219,9 +219,12 @@ def test_quant_moe_prefill_paths_vs_fp32(kind, packed):
         want.index_add_(0, rows, (act @ d2[e].T) * wts[rows, slot].unsqueeze(-1))
     err = (got - want).abs().max().item()
     assert err <= 3e-2 * want.abs().max().item() + 1e-3, err
-    if packed:  # the packed scratch is the batched pack of the dequantised experts
+    if packed:  # the packed dequant equals packing the row-major dequant, bit for bit
         from hipserve.ops import gemm
 
-        ps = Q.moe_packed_scratch(w13, 0, True)
-        for e in (0, E - 1):
-            assert torch.equal(ps[e], gemm.pack(Q.moe_dense(w13, 0)[e].contiguous(), glu=True))
+        p13 = Q.moe_packed_scratch(w13, 0, True).clone()
+        p2 = Q.moe_packed_scratch(w2, 1, False).clone()
+        d13r, d2r = Q.moe_dense(w13, 0), Q.moe_dense(w2, 1)
+        for e in range(E):
+            assert torch.equal(p13[e], gemm.pack(d13r[e].contiguous(), glu=True))
+            assert torch.equal(p2[e], gemm.pack(d2r[e].contiguous()))
