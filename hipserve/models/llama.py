@@ -384,7 +384,7 @@ class LlamaModel:
             return free - w.numel() * w.element_size() >= reserve
 
         for lw in self.layers:
-            for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd):
+            for w in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.router):
                 if (isinstance(w, torch.Tensor) and w.dim() == 2 and tuple(w.shape) in shapes
                         and fits(w)):
                     gemm.register_packed(w, glu=glu and w is lw.wgu and w.shape[0] % 128 == 0)

@@ -197,7 +197,9 @@ class GemmTuner:
                 if K % (256 * ns):
                     continue
                 sp = K // (256 * ns)
-                if (sp > 1 and N % 8) or tiles * sp > 4096 or tiles * sp < 64:
+                # under 64 workgroups only for small weights (an MoE router [E, H]: 0.5 MB,
+                # where hipBLASLt took 11 us at 64 rows); larger ones must fill the chip
+                if (sp > 1 and N % 8) or tiles * sp > 4096 or (tiles * sp < 64 and N * K > (1 << 21)):
                     continue
                 out.append(("dg", rt, sp))
                 if packed:
