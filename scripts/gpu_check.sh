@@ -173,6 +173,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     prof_q4) prof_run profq --quantization q4_k_m ;;
     prof_g27) prof_run profg27 --model gemma-3-27b ;;
     prof_q3int8) prof_run profq3 --model qwen3-30b-a3b --quantization int8 ;;
+    prof_g27fp8) prof_run profg27f8 --model gemma-3-27b --quantization fp8 ;;
     prof) prof_run prof ;;
     prof_mixtral) prof_run profmx --model mixtral-8x7b --concurrency 32 ;;
     prof70) prof_run prof70 --model llama-3-70b ;;
