@@ -881,9 +881,14 @@ class LlamaModel:
         context (512) to occupy the CUs. Workspace views are sized to the chosen
         partition count so the grid carries no dead partitions."""
         part = self.decode_partition
-        if Td * self.nkv >= 512:
-            part = max(part, 2048)
         width = meta.bt_decode.shape[1] * self.block_size_hint
+        # one partition per (sequence, kv head) when the grid is already wide: from 512
+        # workgroups at any width, from 128 when every context fits one 2048-token
+        # partition (GQA 8:1 shapes such as Qwen3-30B-A3B: B = 64 x 4 kv heads, ctx 1152,
+        # 29.0 vs 46.9 us; B = 32: 21.3 vs 29.4; at 64 workgroups splitting still wins,
+        # 17.4 vs 19.1 — profiles/r5_decode_partition_sweep.log)
+        if Td * self.nkv >= 512 or (Td * self.nkv >= 128 and width <= 2048):
+            part = max(part, 2048)
         mp = max(1, -(-width // part))
         to, tm = meta.tmp_out, meta.tmp_ml
         if to is None or mp > to.shape[2]:

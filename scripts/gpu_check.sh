@@ -127,6 +127,10 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     g27fp8_16k) bench_named g27fp8_16k X=1 -- --model gemma-3-27b --quantization fp8 --max-num-batched-tokens 16384 ;;
     b8_chunk4k) bench_named b8_chunk4k -- --max-num-batched-tokens 4096 ;;
     enginetest) run_one tests/test_engine_gpu.py ;;
+    decsweep) DECODE_COLD=1 DECODE_SHAPES=8x1152x32x4,16x1152x32x4,32x1152x32x4,64x1152x32x4,16x4096x32x4,32x4096x32x4,64x4096x32x4,8x1152x32x8,16x1152x32x8,32x1152x32x8,32x4096x32x8 DECODE_PARTS=512,1024,2048 \
+      timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/decsweep.log 2>&1; rc=$?; cat $OUT/decsweep.log; [ $rc -eq 0 ] ;;
+    decq3) for w in 4 8; do HIPSERVE_DECODE_WAVES=$w DECODE_COLD=1 DECODE_SHAPES=64x1152x32x4,64x1152x32x8 DECODE_PARTS=256,512,1024,2048 \
+      timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/decq3_w$w.log 2>&1 || exit 1; echo waves $w; cat $OUT/decq3_w$w.log; done ;;
     moeprefill) timeout -k 10 300 python -u tools/bench_moe_prefill.py > $OUT/bench_moe_prefill.log 2>&1; rc=$?; cat $OUT/bench_moe_prefill.log; [ $rc -eq 0 ] ;;
     tuneprobe) timeout -k 10 300 python -u tools/tune_probe.py > $OUT/tune_probe.log 2>&1; rc=$?; cat $OUT/tune_probe.log; [ $rc -eq 0 ] ;;
     blocking) HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py \

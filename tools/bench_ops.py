@@ -88,8 +88,10 @@ def bench_decode(ops):
     import os
     D, bs = 128, 16
     parts = [int(x) for x in os.environ.get("DECODE_PARTS", "512").split(",")]
-    for (B, ctx, nq, nkv), part in [(c, p) for c in [(64, 1152, 32, 8), (64, 1280, 32, 8), (256, 1152, 32, 8),
-                                                     (1, 4096, 32, 8), (64, 4096, 64, 8)] for p in parts]:
+    shapes = [(64, 1152, 32, 8), (64, 1280, 32, 8), (256, 1152, 32, 8), (1, 4096, 32, 8), (64, 4096, 64, 8)]
+    if os.environ.get("DECODE_SHAPES"):  # "BxCTXxNQxNKV,..." e.g. 64x1152x32x4 (Qwen3-30B-A3B)
+        shapes = [tuple(int(v) for v in sh.split("x")) for sh in os.environ["DECODE_SHAPES"].split(",")]
+    for (B, ctx, nq, nkv), part in [(c, p) for c in shapes for p in parts]:
         mb = math.ceil(ctx / bs) + 1
         nblocks = B * mb
         # DECODE_COLD=1: rotate over enough KV copies (> 2x the 256 MB MALL) that every
