@@ -132,6 +132,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
       timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/decsweep.log 2>&1; rc=$?; cat $OUT/decsweep.log; [ $rc -eq 0 ] ;;
     decq3) for w in 4 8; do HIPSERVE_DECODE_WAVES=$w DECODE_COLD=1 DECODE_SHAPES=64x1152x32x4,64x1152x32x8 DECODE_PARTS=256,512,1024,2048 \
       timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/decq3_w$w.log 2>&1 || exit 1; echo waves $w; cat $OUT/decq3_w$w.log; done ;;
+    prof_moeprefill) cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_moeprefill -o run -- python3 -u tools/bench_moe_prefill.py > $OUT/prof_moeprefill.log 2>&1; rc=$?; cat $OUT/prof_moeprefill.log; [ $rc -eq 0 ] ;;
     moeprefill) timeout -k 10 300 python -u tools/bench_moe_prefill.py > $OUT/bench_moe_prefill.log 2>&1; rc=$?; cat $OUT/bench_moe_prefill.log; [ $rc -eq 0 ] ;;
     tuneprobe) timeout -k 10 300 python -u tools/tune_probe.py > $OUT/tune_probe.log 2>&1; rc=$?; cat $OUT/tune_probe.log; [ $rc -eq 0 ] ;;
     blocking) HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py \
