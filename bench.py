@@ -417,6 +417,9 @@ def run_phase(args):
     if args.quantization:  # resident bytes beyond the quantised weights, GGUF prefill path per shape
         out["quant_shadow_gb"] = round(getattr(engine.runner, "quant_shadow_bytes", 0) / 2**30, 2)
         out["gguf_prefill_timing"] = getattr(engine.runner, "qprefill_report", None)
+    if engine.tracer.times:  # HIPSERVE_PROFILE=timing: host time per engine-step phase
+        out["host_phase_ms"] = {k: {"calls": n, "avg": round(1000 * t / max(n, 1), 4)}
+                                for k, (n, t) in engine.tracer.times.items()}
     if getattr(engine.runner, "moe_prefill_report", None) is not None:
         out["moe_prefill_timing"] = engine.runner.moe_prefill_report
     if ol_summary:  # open loop: TTFT tail and inter-token latency of every request

@@ -117,6 +117,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     b8_chunk16k) bench_named b8_chunk16k -- --max-num-batched-tokens 16384 ;;
     q4km_chunk8k) bench_named q4km_chunk8k -- --quantization q4_k_m --max-num-batched-tokens 8192 ;;
     q4km_default) bench_named q4km_default -- --quantization q4_k_m ;;
+    hosttime) bench_named hosttime_engine HIPSERVE_PROFILE=timing -- --path engine && bench_named hosttime_gw HIPSERVE_PROFILE=timing -- ;;
     q80) bench_named q80 X=1 -- --quantization q8_0 ;;
     q3bf16) bench_named q3bf16 X=1 -- --model qwen3-30b-a3b ;;
     q3int8_8k) bench_named q3int8_8k X=1 -- --model qwen3-30b-a3b --quantization int8 --max-num-batched-tokens 8192 ;;
