@@ -52,7 +52,7 @@ def main():
         P = T * k
         flops = 2 * P * (2 * I * H + H * I)
 
-        def route(tile):
+        def route(tile, ids=ids):
             cap = -(-(P + E * (tile - 1)) // tile) * tile
             slots = torch.empty(cap, dtype=torch.int32, device=DEV)
             te = torch.empty(cap // tile, dtype=torch.int32, device=DEV)
@@ -71,18 +71,31 @@ def main():
             op.silu_and_mul(act, gu)
             return torch._grouped_mm(act, w2.transpose(1, 2), offs=ends)
 
-        def packed():
+        ids0 = torch.zeros_like(ids)  # every pair on expert 0: the grouped kernel's own overhead
+
+        def packed(ids=ids):
             tile = 128 * gemm.PW_WM
-            cap, xs, te, nt, ends = route(tile)
+            cap, xs, te, nt, ends = route(tile, ids)
             act = torch.empty(cap, I, dtype=x.dtype, device=DEV)
             op.prefill_gemm_packed_grouped(act, xs, p13, 2 * I, 2, te, nt, gemm.PW_WM, gemm.PW_RW)
             y = torch.empty(cap, H, dtype=x.dtype, device=DEV)
             op.prefill_gemm_packed_grouped(y, act, p2, H, 0, te, nt, gemm.PW_WM, gemm.PW_RW)
             return y
 
-        tb, tp = timed(blas), timed(packed)
+        def dense():  # the same FLOPs as one dense packed GEMM pair on expert 0's weights
+            tile = 128 * gemm.PW_WM
+            cap, xs, te, nt, ends = route(tile)
+            Pp = P // tile * tile
+            act = torch.empty(Pp, I, dtype=x.dtype, device=DEV)
+            op.prefill_gemm_packed(act, xs[:Pp], p13[0], 2 * I, 2, None, gemm.PW_WM, gemm.PW_GRID, gemm.PW_RW)
+            y = torch.empty(Pp, H, dtype=x.dtype, device=DEV)
+            op.prefill_gemm_packed(y, act, p2[0], H, 0, None, gemm.PW_WM, gemm.PW_GRID, gemm.PW_RW)
+            return y
+
+        tb, tp, td, t0 = timed(blas), timed(packed), timed(dense), timed(lambda: packed(ids0))
         print(json.dumps({"model": name, "tokens": T, "pairs": P, "grouped_mm_ms": round(tb, 3),
-                          "packed_grouped_ms": round(tp, 3), "grouped_mm_TFLOPs": round(flops / tb / 1e9, 1),
+                          "packed_grouped_ms": round(tp, 3), "dense_packed_same_flops_ms": round(td, 3),
+                          "packed_grouped_one_expert_ms": round(t0, 3), "grouped_mm_TFLOPs": round(flops / tb / 1e9, 1),
                           "packed_TFLOPs": round(flops / tp / 1e9, 1)}), flush=True)
         del w13, w2, p13, p2, x
         torch.cuda.empty_cache()
