@@ -89,7 +89,10 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
   T.m0 = tm * BM;
   T.t = tn * WN + wn;
   const int tl = min(T.t, ntiles - 1);  // waves past the last weight tile compute a copy, store nothing
-  if constexpr (kGroup) Wp += (long)grp.tile_expert[tm] * grp.estride;  // this m-tile's expert
+  // this m-tile's expert. readfirstlane: a load through a generic pointer counts as
+  // divergent, which put the weight descriptor in VGPRs and wrapped every weight load of
+  // the main loop in a waterfall loop (tools/asm_stats.py: 197 VALU per loop body vs 0)
+  if constexpr (kGroup) Wp += (long)__builtin_amdgcn_readfirstlane(grp.tile_expert[tm]) * grp.estride;
   T.w = __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + (long)tl * KS * 32768), 0, KS * 65536, 0x00020000);
   // rows >= M fall outside the buffer range and read as zero
   T.x = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long)T.m0 * ldx), 0,
