@@ -181,6 +181,11 @@ struct PwGroup {
   const int* tile_expert;
   const int* num_tiles;
   long estride;  // elements between consecutive experts' packed weights
+  // optional fused moe_gather: X is the token rows [x_rows, K] and slot row s of the
+  // expert-sorted tiles reads token gather_slots[s] / gather_k (zeros for padding, -1)
+  const int* gather_slots = nullptr;
+  int gather_k = 1;
+  int x_rows = 0;
 };
 bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long ldx, const void* Wp, int M, int N,
                                 int K, const void* bias, int wm, int grid_req, hipStream_t s,

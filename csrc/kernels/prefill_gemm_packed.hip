@@ -77,9 +77,10 @@ HS_DEVICE void pw_mfma(f32x4& acc, const u32x4& w, const u32x4& x) {
 struct PwTile {
   __amdgpu_buffer_rsrc_t w, x;
   int m0, t;
+  int xo[8];  // kGather: this thread's byte offsets of its X rows (row p * 32 + (tid >> 3))
 };
 
-template <int WM, bool kGroup>
+template <int WM, bool kGroup, bool kGather = false>
 HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned short* X, long ldx,
                          const unsigned short* Wp, int M, int ntiles, int KS, const PwGroup& grp) {
   constexpr int WN = 4 / WM, BM = 128 * WM;
@@ -94,9 +95,21 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
   // the main loop in a waterfall loop (tools/asm_stats.py: 197 VALU per loop body vs 0)
   if constexpr (kGroup) Wp += (long)__builtin_amdgcn_readfirstlane(grp.tile_expert[tm]) * grp.estride;
   T.w = __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + (long)tl * KS * 32768), 0, KS * 65536, 0x00020000);
-  // rows >= M fall outside the buffer range and read as zero
-  T.x = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long)T.m0 * ldx), 0,
-                                          (int)((long)min(BM, M - T.m0) * ldx * 2), 0x00020000);
+  if constexpr (kGather) {  // token rows through the slot table; padding slots read past the end = zero
+    const int bytes = (int)((long)grp.x_rows * ldx * 2);
+    T.x = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, bytes, 0x00020000);
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < BM / 32; ++p) {
+      const int row = T.m0 + p * 32 + (tid >> 3);
+      const int s = row < M ? grp.gather_slots[row] : -1;
+      T.xo[p] = (s >= 0 ? (s / grp.gather_k) * (int)ldx * 2 : bytes) + (tid & 7) * 16;
+    }
+  } else {
+    // rows >= M fall outside the buffer range and read as zero
+    T.x = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long)T.m0 * ldx), 0,
+                                            (int)((long)min(BM, M - T.m0) * ldx * 2), 0x00020000);
+  }
   return T;
 }
 
@@ -104,7 +117,7 @@ HS_DEVICE PwTile pw_make(int L, int tiles_m, int tiles_n, int wn, const unsigned
 // (moe_align with tile BM, moe_gather); m-tile tm multiplies expert grp.tile_expert[tm]'s
 // packed weight (Wp + e * estride) and only the first *grp.num_tiles m-tiles (the
 // device-side count: no host round trip, graph-capturable) are walked.
-template <int WM, int EPI, bool kGroup, int RW, bool LDLY = false>
+template <int WM, int EPI, bool kGroup, int RW, bool LDLY = false, bool kGather = false>
 __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) void pgw_kernel(
     const unsigned short* __restrict__ X, long ldx, const unsigned short* __restrict__ Wp,
     unsigned short* __restrict__ C, long ldc, int M, int N, int K, int tiles_m, int tiles_n,
@@ -123,8 +136,8 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 
   // cur: the tile whose MFMAs run; nxt: the one the loads past cur's end stream in, so
   // the pipeline runs on across the tile boundary (only the epilogue sits between)
-  PwTile cur = pw_make<WM, kGroup>(r, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp);
-  PwTile nxt = r + G < total ? pw_make<WM, kGroup>(r + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp) : cur;
+  PwTile cur = pw_make<WM, kGroup, kGather>(r, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp);
+  PwTile nxt = r + G < total ? pw_make<WM, kGroup, kGather>(r + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp) : cur;
 
   const int wvo = lane * 16;
   auto wload = [&](int q, int rg) -> u32x4 {  // 32-deep slot q of cur (q >= nq: of nxt), row group rg
@@ -153,7 +166,8 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     st = n ? st - nst : st;
 #pragma unroll
     for (int p = 0; p < XP; ++p)
-      xs[p] = __builtin_amdgcn_raw_buffer_load_b128(n ? nxt.x : cur.x, xvo[p], st * 128, 0);
+      xs[p] = __builtin_amdgcn_raw_buffer_load_b128(n ? nxt.x : cur.x, kGather ? (n ? nxt.xo[p] : cur.xo[p]) : xvo[p],
+                                                    st * 128, 0);
   };
   auto xstore = [&](int buf, const u32x4 (&xs)[XP]) {
 #pragma unroll
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(PW_T) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     L += G;
     if (L >= total) break;
     cur = nxt;
-    if (L + G < total) nxt = pw_make<WM, kGroup>(L + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp);
+    if (L + G < total) nxt = pw_make<WM, kGroup, kGather>(L + G, tiles_m, tiles_n, wn, X, ldx, Wp, M, ntiles, KS, grp);
   }
 }
 
@@ -309,7 +323,9 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
                                 int rw) {
   const PwGroup grp = group != nullptr ? *group : PwGroup{nullptr, nullptr, 0};
   const bool grouped = group != nullptr;
+  const bool gather = grouped && grp.gather_slots != nullptr;
   if (grouped && (bias != nullptr || epi == PW_EPI_ADD)) return false;
+  if (gather && (rw != 4 || grp.gather_k < 1 || (long)grp.x_rows * ldx * 2 >= (1L << 31) - 4096)) return false;
   if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4 && rw != 5)) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;
@@ -333,7 +349,9 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   auto* b = static_cast<const unsigned short*>(bias);
 #define PW_LAUNCH1(WM_, E_, RW_)                                                                               \
   do {                                                                                                         \
-    if (grouped)                                                                                               \
+    if (gather)                                                                                                \
+      pgw_kernel<WM_, E_, true, 4, false, true><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \
+    else if (grouped)                                                                                          \
       pgw_kernel<WM_, E_, true, RW_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp);  \
     else                                                                                                       \
       pgw_kernel<WM_, E_, false, RW_><<<grid, PW_T, 0, s>>>(x, ldx, w, c, ldc, M, N, K, tiles_m, tiles_n, b, grp); \

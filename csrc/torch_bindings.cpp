@@ -786,10 +786,17 @@ void prefill_gemm_packed(at::Tensor& out, const at::Tensor& x, const at::Tensor&
 // with tile 128 * wm + moe_gather), wp = [E, packed expert] (pack_decode_weight per
 // expert, glu for w13), tile_expert / num_tiles from moe_align. epi 0 or 2 / 3.
 void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at::Tensor& wp, int64_t N, int64_t epi,
-                                 const at::Tensor& tile_expert, const at::Tensor& num_tiles, int64_t wm, int64_t rw) {
+                                 const at::Tensor& tile_expert, const at::Tensor& num_tiles, int64_t wm, int64_t rw,
+                                 const c10::optional<at::Tensor>& gather_slots, int64_t gather_k) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(wp.dim() == 2 && wp.is_contiguous(), "prefill_gemm_packed_grouped: wp [E, packed]");
-  const int M = x.size(0), K = x.size(1);
+  // gather: x holds the token rows and slot row s reads x[gather_slots[s] / gather_k] (moe_align's slots)
+  const bool gather = gather_slots.has_value() && gather_slots->numel() > 0;
+  if (gather)
+    TORCH_CHECK(gather_slots->scalar_type() == at::kInt && gather_slots->is_contiguous() &&
+                    gather_slots->numel() == out.size(0) && gather_k >= 1 && x.stride(0) % 8 == 0,
+                "prefill_gemm_packed_grouped: gather_slots [slot rows] int32, gather_k >= 1");
+  const int M = gather ? out.size(0) : x.size(0), K = x.size(1);
   TORCH_CHECK(K % 256 == 0 && wp.size(1) == (N + 127) / 128 * 128 * K, "prefill_gemm_packed_grouped: wp per expert");
   TORCH_CHECK(M % (128 * wm) == 0 && tile_expert.numel() >= M / (128 * wm), "prefill_gemm_packed_grouped: tiles");
   TORCH_CHECK(tile_expert.scalar_type() == at::kInt && num_tiles.scalar_type() == at::kInt, "int32 tile tables");
@@ -798,6 +805,11 @@ void prefill_gemm_packed_grouped(at::Tensor& out, const at::Tensor& x, const at:
   TORCH_CHECK(out.size(0) == M && out.size(1) == (glu ? N / 2 : N), "prefill_gemm_packed_grouped: out shape");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::PwGroup grp{tile_expert.data_ptr<int>(), num_tiles.data_ptr<int>(), (long)wp.size(1)};
+  if (gather) {
+    grp.gather_slots = gather_slots->data_ptr<int>();
+    grp.gather_k = (int)gather_k;
+    grp.x_rows = (int)x.size(0);
+  }
   TORCH_CHECK(hipserve::launch_prefill_gemm_packed((int)epi, out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0),
                                                    wp.data_ptr(), M, (int)N, K, nullptr, (int)wm, 0, cur_stream(),
                                                    &grp, (int)rw),
@@ -1246,7 +1258,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("decode_gemm_partial(Tensor(a!) ws, Tensor x, Tensor w, int N, int rt, int splits, bool packed) -> ()");
   m.def("decode_gemm_glu(Tensor(a!) act, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("prefill_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor? bias=None, int wm=1, int grid=0, int rw=4) -> ()");
-  m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4) -> ()");
+  m.def("prefill_gemm_packed_grouped(Tensor(a!) out, Tensor x, Tensor wp, int N, int epi, Tensor tile_expert, Tensor num_tiles, int wm=1, int rw=4, Tensor? gather_slots=None, int gather_k=1) -> ()");
   m.def("prefill_gemm_f8(Tensor(a!) out, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int epi) -> ()");
   m.def("fp8_decode_gemm(Tensor(a!) ws, Tensor xq, Tensor xs, Tensor[] q, Tensor[] rs, int splits) -> ()");
   m.def("glu_quant(Tensor(a!)? out, Tensor(b!) q8, Tensor(c!) xs, Tensor x, bool gelu) -> ()");

@@ -1003,15 +1003,17 @@ class LlamaModel:
         pair_slot = torch.empty(P, dtype=torch.int32, device=dev)
         ends = torch.empty(E, dtype=torch.int32, device=dev)
         op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
-        xs = torch.empty(cap, H, dtype=x.dtype, device=dev)
-        op.moe_gather(xs, x, slots, k)
         if packed:  # packed-layout grouped expert GEMMs, SiLU-GLU in the first's epilogue
             p13, p2 = lw.moe_packed
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-            op.prefill_gemm_packed_grouped(act, xs, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
+            # the first GEMM reads its token rows through the slot table (moe_gather fused)
+            op.prefill_gemm_packed_grouped(act, x, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW,
+                                           slots, k)
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
             op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
         else:
+            xs = torch.empty(cap, H, dtype=x.dtype, device=dev)
+            op.moe_gather(xs, x, slots, k)
             gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
             act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
             self.ops.silu_and_mul(act, gu)

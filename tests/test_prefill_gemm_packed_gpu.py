@@ -100,9 +100,10 @@ def test_packed_rejects_bad_shapes():
                                                128, 0, None, 1)
 
 
+@pytest.mark.parametrize("gather", [False, True])
 @pytest.mark.parametrize("wm", [1, 2])
 @pytest.mark.parametrize("E,I,K,glu", [(8, 512, 1024, True), (8, 256, 512, False), (16, 128, 256, True)])
-def test_packed_grouped_moe(E, I, K, glu, wm):
+def test_packed_grouped_moe(E, I, K, glu, wm, gather):
     """Grouped expert GEMM over moe_align's expert-sorted (128 * wm)-row tiles with each
     expert's weight in the packed decode layout (moe_packed: w13 GLU-interleaved), the
     valid tile count read on the device, vs a per-expert fp32 reference."""
@@ -126,6 +127,12 @@ def test_packed_grouped_moe(E, I, K, glu, wm):
     op.moe_gather(xs, x, slots, k)
     out = torch.full((cap, I), float("nan"), device=DEV, dtype=torch.bfloat16)
     op.prefill_gemm_packed_grouped(out, xs, wp, N, 2 if glu else 0, tile_expert, ntiles, wm)
+    if gather:  # token rows read through the slot table inside the GEMM (moe_gather fused): bit-identical
+        used = torch.arange(cap, device=DEV) < int(ntiles.item()) * tile
+        fused = torch.full_like(out, float("nan"))
+        op.prefill_gemm_packed_grouped(fused, x, wp, N, 2 if glu else 0, tile_expert, ntiles, wm, 4, slots, k)
+        assert torch.equal(fused[used], out[used])
+        assert bool((fused[used & (slots < 0)] == 0).all())  # padding slots multiply zero rows
     ps = pair_slot.long()
     for p in range(0, P, 37):  # a spread of pairs
         t, j = p // k, p % k

@@ -92,10 +92,26 @@ def main():
             op.prefill_gemm_packed(y, act, p2[0], H, 0, None, gemm.PW_WM, gemm.PW_GRID, gemm.PW_RW)
             return y
 
+        def packed_gather():  # moe_gather fused into the first GEMM's X loads
+            tile = 128 * gemm.PW_WM
+            cap = -(-(P + E * (tile - 1)) // tile) * tile
+            slots = torch.empty(cap, dtype=torch.int32, device=DEV)
+            te = torch.empty(cap // tile, dtype=torch.int32, device=DEV)
+            nt = torch.empty(1, dtype=torch.int32, device=DEV)
+            ps = torch.empty(P, dtype=torch.int32, device=DEV)
+            op.moe_align(ids, E, tile, slots, te, nt, ps)
+            act = torch.empty(cap, I, dtype=x.dtype, device=DEV)
+            op.prefill_gemm_packed_grouped(act, x, p13, 2 * I, 2, te, nt, gemm.PW_WM, gemm.PW_RW, slots, k)
+            y = torch.empty(cap, H, dtype=x.dtype, device=DEV)
+            op.prefill_gemm_packed_grouped(y, act, p2, H, 0, te, nt, gemm.PW_WM, gemm.PW_RW)
+            return y
+
         tb, tp, td, t0 = timed(blas), timed(packed), timed(dense), timed(lambda: packed(ids0))
+        tg = timed(packed_gather)
         print(json.dumps({"model": name, "tokens": T, "pairs": P, "grouped_mm_ms": round(tb, 3),
                           "packed_grouped_ms": round(tp, 3), "dense_packed_same_flops_ms": round(td, 3),
-                          "packed_grouped_one_expert_ms": round(t0, 3), "grouped_mm_TFLOPs": round(flops / tb / 1e9, 1),
+                          "packed_grouped_one_expert_ms": round(t0, 3),
+                          "packed_gather_fused_ms": round(tg, 3), "grouped_mm_TFLOPs": round(flops / tb / 1e9, 1),
                           "packed_TFLOPs": round(flops / tp / 1e9, 1)}), flush=True)
         del w13, w2, p13, p2, x
         torch.cuda.empty_cache()
