@@ -254,7 +254,11 @@ namespace hipserve {
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
                              bool renorm, hipStream_t s);
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
-                      int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s);
+                      int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s,
+                      int* hist = nullptr);
+// blocks of the multi-workgroup moe_align for npairs (1: the single-workgroup kernel);
+// it needs hist = int32 [blocks * 128] scratch
+int moe_align_blocks(int npairs);
 // xs[slot, H] = x[slots[slot] / k] (zeros for padding slots): grouped-GEMM input rows
 void launch_moe_gather(void* out, const void* x, long x_stride, const int* slots, int nslots, int k, int H,
                        hipStream_t s);

@@ -125,6 +125,89 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
   }
 }
 
+// Multi-workgroup moe_align for prefill-sized pair counts (one workgroup scatters ~0.6 ns
+// per pair: 157 us per layer at 262K pairs). Pass 1: per-block expert histograms
+// hist[b][E]. Pass 2: every block sums the table (nb x E ints) into the padded expert
+// offsets and its own prefix, then scatters its chunk; block 0 also writes the tile table,
+// the tile count and the padding slots (disjoint from every real slot, so no ordering
+// between blocks is needed).
+constexpr int kAlignChunk = 4096;
+__global__ __launch_bounds__(1024) void moe_count_kernel(const int* __restrict__ ids, int npairs,
+                                                         int* __restrict__ hist) {
+  __shared__ int cnt[128];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  if (tid < 128) cnt[tid] = 0;
+  __syncthreads();
+  const int end = min(npairs, (b + 1) * kAlignChunk);
+  for (int p = b * kAlignChunk + tid; p < end; p += 1024) atomicAdd(&cnt[ids[p]], 1);
+  __syncthreads();
+  if (tid < 128) hist[b * 128 + tid] = cnt[tid];
+}
+
+__global__ __launch_bounds__(1024) void moe_place_kernel(const int* __restrict__ ids, int npairs, int E, int tile,
+                                                         const int* __restrict__ hist, int nb,
+                                                         int* __restrict__ slots, int slots_cap,
+                                                         int* __restrict__ tile_expert, int tiles_cap,
+                                                         int* __restrict__ num_tiles, int* __restrict__ pair_slot,
+                                                         int* __restrict__ group_end) {
+  __shared__ int cnt[128], pre[128], off[129], cur[128];
+  const int tid = threadIdx.x, lane = tid & 63, b = blockIdx.x;
+  if (tid < 128) {  // expert totals and this block's prefix over the blocks before it
+    int c = 0, q = 0;
+    for (int j = 0; j < nb; ++j) {
+      const int h = hist[j * 128 + tid];
+      c += h;
+      q += j < b ? h : 0;
+    }
+    cnt[tid] = c;
+    pre[tid] = q;
+    cur[tid] = 0;
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the tile-padded counts, 2 experts per lane (E <= 128)
+    const int e0 = 2 * lane, e1 = 2 * lane + 1;
+    const int a = e0 < E ? (cnt[e0] + tile - 1) / tile * tile : 0;
+    const int c = e1 < E ? (cnt[e1] + tile - 1) / tile * tile : 0;
+    int incl = a + c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - a - c;
+    off[e0] = excl;
+    off[e1] = excl + a;
+    if (b == 0 && group_end != nullptr) {
+      if (e0 < E) group_end[e0] = excl + a;
+      if (e1 < E) group_end[e1] = incl;
+    }
+    if (lane == 63) {
+      off[128] = incl;
+      if (b == 0) *num_tiles = incl / tile;
+    }
+  }
+  __syncthreads();
+  if (b == 0) {
+    const int total = off[128];
+    for (int e = 0; e < E; ++e) {  // padding slots of each expert, then the unused tail
+      const int lo = off[e] + cnt[e], hi = off[e] + (cnt[e] + tile - 1) / tile * tile;
+      for (int s = lo + tid; s < hi; s += 1024) slots[s] = -1;
+      for (int t = off[e] / tile + tid; t < hi / tile; t += 1024) tile_expert[t] = e;
+    }
+    for (int s = total + tid; s < slots_cap; s += 1024) slots[s] = -1;
+    for (int t = total / tile + tid; t < tiles_cap; t += 1024) tile_expert[t] = -1;
+  }
+  const int end = min(npairs, (b + 1) * kAlignChunk);
+  for (int p = b * kAlignChunk + tid; p < end; p += 1024) {
+    const int e = ids[p];
+    const int pos = off[e] + pre[e] + atomicAdd(&cur[e], 1);
+    slots[pos] = p;
+    pair_slot[p] = pos;
+  }
+}
+
+int moe_align_blocks(int npairs) { return npairs > 4 * kAlignChunk ? (npairs + kAlignChunk - 1) / kAlignChunk : 1; }
+
 // out[slot, N] = x[row(slot), K] . W[e, N, K]^T; row(slot) = pair / k (gather) or slot.
 // A tile = 16*MT consecutive slots of one expert; each W fragment feeds MT MFMAs.
 template <int MT, int KW>
@@ -247,7 +330,14 @@ void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int*
 }
 
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
-                      int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s) {
+                      int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s, int* hist) {
+  const int nb = moe_align_blocks(npairs);
+  if (nb > 1 && hist != nullptr) {
+    moe_count_kernel<<<nb, 1024, 0, s>>>(ids, npairs, hist);
+    moe_place_kernel<<<nb, 1024, 0, s>>>(ids, npairs, E, tile, hist, nb, slots, slots_cap, tile_expert, tiles_cap,
+                                         num_tiles, pair_slot, group_end);
+    return;
+  }
   moe_align_kernel<<<1, 1024, 0, s>>>(ids, npairs, E, tile, slots, slots_cap, tile_expert, tiles_cap, num_tiles,
                                       pair_slot, group_end);
 }

@@ -1073,9 +1073,12 @@ void moe_align(const at::Tensor& ids, int64_t E, int64_t tile, at::Tensor& slots
     ge = group_end->data_ptr<int>();
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(ids.device());
+  const int nb = hipserve::moe_align_blocks(npairs);
+  at::Tensor hist;  // multi-workgroup form (prefill): per-block expert histograms
+  if (nb > 1) hist = at::empty({(long)nb * 128}, ids.options().dtype(at::kInt));
   hipserve::launch_moe_align(ids.data_ptr<int>(), npairs, E, tile, slots.data_ptr<int>(), slots.numel(),
                              tile_expert.data_ptr<int>(), tile_expert.numel(), num_tiles.data_ptr<int>(),
-                             pair_slot.data_ptr<int>(), ge, cur_stream());
+                             pair_slot.data_ptr<int>(), ge, cur_stream(), nb > 1 ? hist.data_ptr<int>() : nullptr);
 }
 
 void moe_gather(at::Tensor& out, const at::Tensor& x, const at::Tensor& slots, int64_t k) {

@@ -144,3 +144,40 @@ def test_packed_grouped_moe(E, I, K, glu, wm, gather):
         else:
             want = h
         torch.testing.assert_close(out[ps[p]].float(), want, rtol=2e-2, atol=2e-2 * max(1.0, want.abs().max().item()))
+
+
+@pytest.mark.parametrize("T,k,E,tile", [(700, 2, 8, 128), (8192, 8, 128, 128), (20000, 2, 8, 128), (9000, 8, 60, 16)])
+def test_moe_align_layout(T, k, E, tile):
+    """moe_align (single workgroup below 16K pairs, per-block histograms + scatter above):
+    every pair has exactly one slot inside its expert's tile-padded segment, segments are in
+    expert order, padding slots are -1, and the tile table / tile count / group ends match
+    a host recount."""
+    g = torch.Generator(device=DEV).manual_seed(T + E)
+    logits = torch.randn(T, E, device=DEV, generator=g)
+    ids = logits.topk(k, dim=-1).indices.int().contiguous()
+    P = T * k
+    cap = -(-(P + E * (tile - 1)) // tile) * tile
+    op = torch.ops.hipserve
+    slots = torch.empty(cap, dtype=torch.int32, device=DEV)
+    tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=DEV)
+    ntiles = torch.empty(1, dtype=torch.int32, device=DEV)
+    pair_slot = torch.empty(P, dtype=torch.int32, device=DEV)
+    ends = torch.empty(E, dtype=torch.int32, device=DEV)
+    op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
+    flat = ids.view(-1).long().cpu()
+    cnt = torch.bincount(flat, minlength=E)
+    padded = (cnt + tile - 1) // tile * tile
+    off = torch.cumsum(padded, 0) - padded
+    assert int(ntiles.item()) == int(padded.sum()) // tile
+    assert torch.equal(ends.cpu().long(), off + padded)
+    s, ps, te = slots.cpu().long(), pair_slot.cpu().long(), tile_expert.cpu().long()
+    assert torch.equal(s[ps], torch.arange(P))  # slots[pair_slot[p]] == p: a bijection on the real slots
+    e_of = flat
+    assert bool(((ps >= off[e_of]) & (ps < off[e_of] + cnt[e_of])).all())  # inside its expert's segment
+    real = torch.zeros(cap, dtype=torch.bool)
+    real[ps] = True
+    assert bool((s[~real] == -1).all())
+    want_te = torch.full((cap // tile,), -1, dtype=torch.long)
+    for e in range(E):
+        want_te[int(off[e]) // tile:int(off[e] + padded[e]) // tile] = e
+    assert torch.equal(te, want_te)
