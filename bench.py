@@ -109,10 +109,31 @@ def _free_port() -> int:
     return port
 
 
-def _run_child(argv, world, rank, local, port, result_file, timeout=None):
+PEER_FAILED = 125  # exit code recorded for a phase child killed because a peer rank's child failed
+
+
+def _peer_failures(fail_dir, rank) -> dict:
+    """{rank: exit code} of the OTHER ranks whose child of this phase failed."""
+    out = {}
+    if fail_dir and os.path.isdir(fail_dir):
+        for f in os.listdir(fail_dir):
+            if f.startswith("rank") and f[4:].isdigit() and int(f[4:]) != rank:
+                try:
+                    with open(os.path.join(fail_dir, f)) as fh:
+                        out[int(f[4:])] = int(fh.read().strip() or 1)
+                except (OSError, ValueError):
+                    out[int(f[4:])] = 1
+    return out
+
+
+def _run_child(argv, world, rank, local, port, result_file, timeout=None, fail_dir=None):
     """One phase as a child process of this rank (own process group on ``port``);
     returns (exit code, result dict or None). ``timeout``: kill the child's
-    whole process group at that many seconds (exit code 124)."""
+    whole process group at that many seconds (exit code 124). ``fail_dir`` (one
+    directory per phase shared by the node's ranks): a child that fails records its
+    exit code there, and every rank kills its own child as soon as a peer's failure
+    appears (exit code ``PEER_FAILED``) — the surviving ranks would otherwise sit in a
+    collective with the dead one until the phase budget runs out."""
     import signal
     import subprocess
 
@@ -123,15 +144,32 @@ def _run_child(argv, world, rank, local, port, result_file, timeout=None):
     cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--result-file", result_file]
     # the child's stdout goes to our stderr: the ONE JSON line on stdout is ours
     p = subprocess.Popen(cmd, env=env, stdout=sys.stderr, start_new_session=True)
-    try:
-        rc = p.wait(timeout=timeout)
-    except subprocess.TimeoutExpired:
+    t_end = time.time() + timeout if timeout else None
+
+    def kill():
         try:
             os.killpg(p.pid, signal.SIGKILL)
         except ProcessLookupError:
             pass
         p.wait()
-        rc = 124
+
+    while True:
+        try:
+            rc = p.wait(timeout=0.5)
+            break
+        except subprocess.TimeoutExpired:
+            pass
+        if _peer_failures(fail_dir, rank):
+            kill()
+            rc = PEER_FAILED
+            break
+        if t_end is not None and time.time() > t_end:
+            kill()
+            rc = 124
+            break
+    if rc not in (0, 124, PEER_FAILED) and fail_dir:
+        with open(os.path.join(fail_dir, f"rank{rank}"), "w") as f:
+            f.write(str(rc))
     res = None
     if rank == 0 and os.path.exists(result_file):
         with open(result_file) as f:
@@ -169,6 +207,9 @@ def orchestrate(args) -> int:
         and not args.quantization and not args.request_rate)
     dist = None
     ports = [_free_port(), _free_port()]
+    # one directory shared by the node's ranks (single node: one rendezvous host), where
+    # a rank whose phase child fails leaves its exit code for the others (_run_child)
+    shared = tempfile.mkdtemp(prefix="hipserve_bench_fail_") if rank == 0 else None
     if world > 1:
         import datetime
 
@@ -176,12 +217,18 @@ def orchestrate(args) -> int:
 
         dist.init_process_group("gloo", rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=3600))
-        lst = [ports]
+        lst = [(ports, shared)]
         dist.broadcast_object_list(lst, src=0)
-        ports = lst[0]
+        ports, shared = lst[0]
+    fail1, fail2 = os.path.join(shared, "phase1"), os.path.join(shared, "phase2")
+    if rank == 0:
+        os.makedirs(fail1)
+        os.makedirs(fail2)
+    if dist is not None:
+        dist.barrier()
     tmp = tempfile.mkdtemp(prefix="hipserve_bench_")
     argv = sys.argv[1:]
-    rc1, res = _run_child(argv, world, rank, local, ports[0], os.path.join(tmp, "phase1.json"))
+    rc1, res = _run_child(argv, world, rank, local, ports[0], os.path.join(tmp, "phase1.json"), fail_dir=fail1)
     if dist is not None:
         ok = [rc1 == 0] * world
         dist.all_gather_object(ok, rc1 == 0)
@@ -196,13 +243,19 @@ def orchestrate(args) -> int:
         if args.num_kv_blocks and args.device == "cpu":
             argv2 += ["--num-kv-blocks", str(args.num_kv_blocks)]
         rc2, tp = _run_child(argv2, world, rank, local, ports[1], os.path.join(tmp, "phase2.json"),
-                             timeout=args.tp_budget_s)
+                             timeout=args.tp_budget_s, fail_dir=fail2)
         if dist is not None:
             dist.barrier()
         if rank == 0:
+            failed = _peer_failures(fail2, -1)  # every rank whose child failed (rank 0's included)
             if rc2 != 0 or tp is None:
-                tp = {"model": args.tp_model, "tp": world,
-                      "status": "timeout" if rc2 == 124 else f"failed (exit {rc2})"}
+                if failed:
+                    code = failed[min(failed)]
+                    tp = {"model": args.tp_model, "tp": world, "status": f"failed (exit {code})",
+                          "failed_ranks": {str(r): c for r, c in sorted(failed.items())}}
+                else:
+                    tp = {"model": args.tp_model, "tp": world,
+                          "status": "timeout" if rc2 == 124 else f"failed (exit {rc2})"}
             tp["phase_wall_s"] = round(time.time() - t0, 1)
             res = dict(res or {}, tp_strong=tp)
     if rank == 0 and res is not None:
@@ -213,6 +266,11 @@ def orchestrate(args) -> int:
                 f.write(line + "\n")
     if dist is not None:
         dist.destroy_process_group()
+    import shutil
+
+    shutil.rmtree(tmp, ignore_errors=True)
+    if rank == 0:
+        shutil.rmtree(shared, ignore_errors=True)
     return rc1
 
 

@@ -1,5 +1,5 @@
 // Shared device helpers of the tiled quantised-weight kernels (gguf_mfma.hip: the v2
-// decode GEMM, K15 / qpg prefill, dequant; gguf_decode.hip: the LDS-DMA decode GEMM):
+// decode GEMM, K15 / qpg prefill, dequant; fp8_decode.hip):
 // the per-format tiled chunk layouts, raw loads, and the subnormal-integer dequant.
 #pragma once
 

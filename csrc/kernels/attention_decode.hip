@@ -32,7 +32,7 @@ constexpr float kLog2e = 1.4426950408889634f;
 
 // out16 (optional): an f16 copy of the bf16 output in the quantised decode GEMMs' staging
 // pair order {0, 2, 1, 3, 4, 6, 5, 7} per aligned 8-run — the o-projection's x16 operand
-// (gguf_decode.hip), written here instead of by a conversion kernel
+// (gguf_mfma.hip), written here instead of by a conversion kernel
 HS_DEVICE void store_o16(unsigned short* __restrict__ out16, long row_off, int e, unsigned short bf) {
   const int p = (e & ~7) | (e & 4) | ((e & 1) << 1) | ((e >> 1) & 1);
   out16[row_off + p] = __builtin_bit_cast(unsigned short, static_cast<_Float16>(bf16_to_f32(bf)));

@@ -104,6 +104,9 @@ class ModelRunner:
         t0 = time.time()
         self._load_weights()
         self.load_time = time.time() - t0
+        from ..utils.faults import FaultInjector
+
+        FaultInjector.from_env().on_init(tp.rank, tp.world_size)  # HIPSERVE_FAULT=rankK:init@0 (tests)
         # start-up breakdown (bench.py reports it: the 70B TP=8 phase must visibly fit its box)
         self.init_times = {"weights_s": round(self.load_time, 2)}
         t1 = time.time()
@@ -742,13 +745,23 @@ class ModelRunner:
         # weight packing take different times per rank; a custom-collective
         # barrier must not spin through a peer's whole setup)
         self.tp.barrier()
+        # every bucket and variant runs eagerly once, on the stream the graphs are then
+        # captured on, before any capture starts: a library's first-use work for a shape
+        # (hipBLASLt's workspace / code-object load, a lazily built table) must never
+        # happen under capture. Which shapes reach hipBLASLt at decode depends on the
+        # tuner's per-box timing or on a tuning-cache hit (round 5's TP=2 capture abort:
+        # 'operation not permitted when stream is capturing' from hipBLASLt), so warming
+        # only the largest bucket was not enough
         stream = torch.cuda.Stream(device=dev)
         stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(stream):
-            for _ in range(2):
-                self._graph_forward(self.buckets[-1])
-        torch.cuda.current_stream(dev).wait_stream(stream)
+            self._graph_forward(self.buckets[-1])
+            for b in reversed(self.buckets):
+                for full in (True, False):
+                    self._graph_forward(b, full)
+        stream.synchronize()
         torch.cuda.synchronize(dev)
+        self.tp.barrier()
         self.graph_pool = torch.cuda.graph_pool_handle()
         for b in reversed(self.buckets):
             # staging kernel: one graph per staging-set parity with the H2D and D2H
@@ -757,7 +770,7 @@ class ModelRunner:
             for par in ((0, 1) if self._stage_kernel else (None,)):
                 for full in (True, False):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self.graph_pool):
+                    with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                         if par is not None:
                             self._stage_in(b, self._stage[par])
                         self._graph_forward(b, full)

@@ -900,17 +900,25 @@ class LlamaModel:
 
     def moe(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Sparse MoE: softmax over the E router logits, top-k experts, weights
-        renormalised over the k (Mixtral; Qwen3-MoE when ``norm_topk_prob``)."""
+        renormalised over the k (Mixtral; Qwen3-MoE when ``norm_topk_prob``).
+
+        On the GPU every batch runs one of the two graph-capturable kernel paths:
+        ``moe_hip`` (the weight-streaming expert decode GEMM; decode batches, and
+        prefill batches below the start-up-timed crossover ``moe_packed_from_tokens``)
+        or ``moe_grouped`` (the packed-layout one-launch grouped GEMM). The per-expert
+        loop at the end is the CPU reference path only."""
         cfg = self.cfg
         k = cfg.num_experts_per_tok
         T = x.shape[0]
         P = T * k
+        hip = self.ops.name == "hip"
         if lw.w13 is not None and not isinstance(lw.w13, torch.Tensor):  # quantised experts (ops/quant.py QuantMoE)
             if P <= MOE_KERNEL_MAX_PAIRS:
                 return self.moe_quant(x, lw)
             from ..ops import quant as Q
 
-            if self.moe_prefill_packed and self._moe_packed_shape_ok() and lw.w13.dense is None:
+            if (hip and self._moe_packed_shape_ok() and lw.w13.dense is None
+                    and self.moe_prefill_choice(T) == "packed"):
                 # experts dequantised straight into the packed layout, then the one-launch grouped GEMMs
                 lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router,
                                   moe_packed=(Q.moe_packed_scratch(lw.w13, 0, True),
@@ -918,17 +926,18 @@ class LlamaModel:
                 return self.moe_grouped(x, lw)
             lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router,
                               w13=Q.moe_dense(lw.w13, 0), w2=Q.moe_dense(lw.w2, 1))
-        if (self.ops.name == "hip" and cfg.num_experts <= 128 and cfg.hidden_size % 256 == 0
-                and self.inter % 256 == 0
-                and (P <= MOE_KERNEL_MAX_PAIRS
-                     or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts and self._moe_decode_ok(lw)
-                         and self.moe_prefill_path in (None, "hip")))):
-            return self.moe_hip(x, lw)
-        if self.ops.name == "hip" and cfg.num_experts <= 128 and self.moe_packed_prefill(lw):
-            return self.moe_grouped(x, lw)
-        if self.ops.name == "hip" and hasattr(torch, "_grouped_mm") and cfg.num_experts <= 128 \
-                and cfg.hidden_size % 8 == 0 and self.inter % 8 == 0 and isinstance(lw.w13, torch.Tensor):
-            return self.moe_grouped(x, lw)
+        if hip:
+            kernel_ok = (cfg.num_experts <= 128 and cfg.hidden_size % 256 == 0 and self.inter % 256 == 0
+                         and (lw.w13 is not None or lw.moe_packed is not None))
+            grouped_ok = self.moe_packed_prefill(lw)
+            if kernel_ok and (P <= MOE_KERNEL_MAX_PAIRS or not grouped_ok
+                              or (P <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * cfg.num_experts
+                                  and self.moe_prefill_choice(T) == "hip")):
+                return self.moe_hip(x, lw)
+            if grouped_ok:
+                return self.moe_grouped(x, lw)
+            raise NotImplementedError(f"MoE shape (E={cfg.num_experts}, H={cfg.hidden_size}, I={self.inter}) "
+                                      "has no gfx950 expert kernel")
         logits = F.linear(x, lw.router).float()
         w, idx = torch.topk(torch.softmax(logits, dim=-1), k, dim=-1)
         if cfg.norm_topk_prob:
@@ -974,24 +983,25 @@ class LlamaModel:
         return opts[-1]
 
     def moe_grouped(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
-        """Prefill-sized MoE: routing (top-k kernel), expert-sorted padded slots with
-        per-expert end offsets (moe_align), the token rows gathered into that order
-        (moe_gather), the two expert GEMMs as ONE grouped launch each, then the weighted
-        combine (moe_combine). The grouped GEMMs: the packed-layout kernel
-        (prefill_gemm_packed.hip kGroup, expert ids read on the device: no host round
-        trip, graph-capturable, SiLU-GLU in the gate|up epilogue) when the experts are
-        kept only in the packed layout or HIPSERVE_MOE_PACKED_PREFILL=1, else hipBLASLt's
-        grouped GEMM (``torch._grouped_mm``, which reads the group offsets on the host on
-        this ROCm build) + silu_and_mul."""
+        """Prefill-sized MoE: routing (top-k kernel), expert-sorted slots padded to the
+        GEMM's row tile (moe_align), then the two expert GEMMs as ONE launch each on the
+        packed expert layout (prefill_gemm_packed.hip kGroup: expert ids read on the
+        device, no host round trip, graph-capturable; the token rows gathered through the
+        slot table inside the first GEMM's X loads, SiLU-GLU in its epilogue), and the
+        weighted combine (moe_combine). Row-major experts without a packed copy (tests)
+        are packed into a scratch first."""
         op = torch.ops.hipserve
         cfg = self.cfg
         E, k, H = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size
         T, dev = x.shape[0], x.device
-        # packed experts (the decode copy, moe_packed): the packed-layout grouped GEMM
-        # (prefill_gemm_packed.hip kGroup) over (128 * wm)-row tiles; 16-row ones for hipBLASLt's
-        packed = self.moe_packed_prefill(lw)
+        if lw.moe_packed is None:
+            p13 = torch.empty(E, 2 * self.inter * H, dtype=lw.w13.dtype, device=dev)
+            p2 = torch.empty(E, -(-H // 128) * 128 * self.inter, dtype=lw.w2.dtype, device=dev)
+            op.pack_decode_weight(p13, lw.w13.contiguous(), True)
+            op.pack_decode_weight(p2, lw.w2.contiguous(), False)
+            lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=lw.router, moe_packed=(p13, p2))
         P = T * k
-        tile = 128 * gemm.PW_WM if packed else 16
+        tile = 128 * gemm.PW_WM
         cap = -(-(P + E * (tile - 1)) // tile) * tile
         logits = gemm.linear(x, lw.router)
         w = torch.empty(T, k, dtype=torch.float32, device=dev)
@@ -1003,76 +1013,84 @@ class LlamaModel:
         pair_slot = torch.empty(P, dtype=torch.int32, device=dev)
         ends = torch.empty(E, dtype=torch.int32, device=dev)
         op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot, ends)
-        if packed:  # packed-layout grouped expert GEMMs, SiLU-GLU in the first's epilogue
-            p13, p2 = lw.moe_packed
-            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-            # the first GEMM reads its token rows through the slot table (moe_gather fused)
-            op.prefill_gemm_packed_grouped(act, x, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW,
-                                           slots, k)
-            y = torch.empty(cap, H, dtype=x.dtype, device=dev)
-            op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
-        else:
-            xs = torch.empty(cap, H, dtype=x.dtype, device=dev)
-            op.moe_gather(xs, x, slots, k)
-            gu = torch._grouped_mm(xs, lw.w13.transpose(1, 2), offs=ends)
-            act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
-            self.ops.silu_and_mul(act, gu)
-            y = torch._grouped_mm(act, lw.w2.transpose(1, 2), offs=ends)
+        p13, p2 = lw.moe_packed
+        act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
+        # the first GEMM reads its token rows through the slot table (moe_gather fused)
+        op.prefill_gemm_packed_grouped(act, x, p13, 2 * self.inter, 2, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW,
+                                       slots, k)
+        y = torch.empty(cap, H, dtype=x.dtype, device=dev)
+        op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         op.moe_combine(out, y, w, pair_slot, k)
         return out
 
-    # packed-layout grouped expert GEMMs for prefill: always when the row-major experts were
-    # dropped (single weight layout); otherwise ``auto`` follows the start-up timing of the
-    # layer's expert shape (``tune_moe_prefill``): hipBLASLt's grouped GEMM (per-expert
-    # launches after a host read of the offsets) wins with few large experts (Mixtral-8x7B:
-    # 5.4 vs 6.4 ms per layer at 8K tokens), the one-launch packed kernel with many small
-    # ones (Qwen3-30B-A3B, 128 experts: 1.0 vs 4.8 ms at 8K, 3.6 vs 6.3 at 32K;
-    # profiles/r5_bench_moe_prefill.log)
+    # prefill-sized MoE batches: the packed one-launch grouped GEMM (``moe_grouped``) or the
+    # weight-streaming expert kernel (``moe_hip``). ``auto``: by the start-up timing of the
+    # layer's expert shape at several token counts (``tune_moe_prefill``): the grouped GEMM
+    # from ``moe_packed_from_tokens`` tokens up, the streaming kernel below (its 128-row
+    # tiles are mostly padding when 128 experts share a few hundred tokens). ``1`` / ``0``
+    # force the grouped GEMM / the streaming kernel. hipBLASLt's grouped GEMM
+    # (torch._grouped_mm) lost to the packed kernel on every shipped MoE config (Mixtral
+    # 4.82 vs 5.10 ms, Qwen3-30B-A3B 1.52 vs 5.17 ms per layer at 16K tokens,
+    # profiles/r5_bench_mixtral_gather_fused.json, r5_bench_q3int8_align_multiblock.json)
+    # and read its group offsets on the host: removed
     MOE_PACKED_PREFILL = os.environ.get("HIPSERVE_MOE_PACKED_PREFILL", "auto")
-    moe_prefill_path: str | None = None  # "hip" | "blas" | "packed", set by tune_moe_prefill
+    moe_prefill_path: str | None = None  # "hip" | "packed" at the timed budget, set by tune_moe_prefill
+    moe_packed_from_tokens: int = 0     # "packed": the grouped GEMM from this many tokens up
 
     @property
     def moe_prefill_packed(self) -> bool:
         return self.moe_prefill_path == "packed"
+
+    def moe_prefill_choice(self, T: int) -> str:
+        """'packed' (grouped GEMM) or 'hip' (streaming expert kernel) for a T-token batch."""
+        mode = self.MOE_PACKED_PREFILL
+        if mode in ("0", "1"):
+            return "packed" if mode == "1" else "hip"
+        if self.moe_prefill_path == "packed" and T >= self.moe_packed_from_tokens:
+            return "packed"
+        if self.moe_prefill_path is None:  # untimed (tests, CPU): the grouped GEMM above the kernel row limit
+            E, k = self.cfg.num_experts, self.cfg.num_experts_per_tok
+            return "packed" if T * k > MOE_KERNEL_MAX_ROWS_PER_EXPERT * E else "hip"
+        return "hip"
 
     def _moe_packed_shape_ok(self) -> bool:
         return (self.cfg.hidden_act == "silu" and self.cfg.hidden_size % 256 == 0 and self.inter % 256 == 0
                 and (2 * self.inter) % 128 == 0 and hasattr(torch.ops.hipserve, "prefill_gemm_packed_grouped"))
 
     def moe_packed_prefill(self, lw: LayerWeights, for_drop: bool = False) -> bool:
-        """Prefill experts on the packed-layout grouped GEMM (the decode kernels' copy of
-        the experts, ``pack_moe_weights``): SiLU-GLU experts, K of both GEMMs % 256."""
-        mode = self.MOE_PACKED_PREFILL
-        if mode == "0" or lw.moe_packed is None or not self._moe_packed_shape_ok():
+        """The packed-layout grouped GEMM can run this layer's prefill: SiLU-GLU experts,
+        K of both GEMMs % 256, a packed copy (or row-major experts to pack from)."""
+        if not self._moe_packed_shape_ok() or (lw.moe_packed is None and lw.w13 is None):
             return False
-        if mode == "1" or for_drop or lw.w13 is None:
-            return True
-        return self.moe_prefill_path == "packed"
+        if for_drop:
+            return self.MOE_PACKED_PREFILL != "0" and lw.moe_packed is not None
+        return True
 
     @torch.inference_mode()
     def tune_moe_prefill(self, T: int) -> dict | None:
-        """Start-up timing of one MoE layer's prefill at ``T`` tokens on random bf16 experts
-        of the layer's shape, through the model's own paths: the weight-streaming expert
-        kernel (``moe_hip``, where its row limit allows), hipBLASLt's grouped GEMM and the
-        packed one-launch grouped kernel (``moe_grouped``). Sets ``moe_prefill_path``;
-        cached per device and kernel build."""
+        """Start-up timing of one MoE layer's prefill on random bf16 experts of the layer's
+        shape through the model's own paths, the weight-streaming expert kernel
+        (``moe_hip``, where its row limit allows) vs the packed one-launch grouped GEMM
+        (``moe_grouped``), at ``T`` tokens and at halvings of it down to the decode
+        kernels' pair limit. Sets ``moe_prefill_path`` (the winner at T) and
+        ``moe_packed_from_tokens`` (the smallest timed count from which the grouped GEMM
+        wins at every larger count). Cached per device and kernel build."""
         from ..ops import tune_cache as TC
 
         cfg = self.cfg
         lw = next((lw for lw in self.layers if lw.router is not None), None)
-        if (lw is None or not self._moe_packed_shape_ok() or not hasattr(torch, "_grouped_mm")
-                or self.MOE_PACKED_PREFILL != "auto" or getattr(self.ops, "name", "") != "hip"
-                or self.device.type != "cuda" or cfg.num_experts > 128):
+        if (lw is None or not self._moe_packed_shape_ok() or self.MOE_PACKED_PREFILL != "auto"
+                or getattr(self.ops, "name", "") != "hip" or self.device.type != "cuda" or cfg.num_experts > 128):
             return None
         E, k, H, I = cfg.num_experts, cfg.num_experts_per_tok, cfg.hidden_size, self.inter
         quant = lw.w13 is not None and not isinstance(lw.w13, torch.Tensor)
-        if not quant and (lw.moe_packed is None or lw.w13 is None):
+        if not quant and lw.moe_packed is None and lw.w13 is None:
             return None
-        key = [E, k, H, I, T, quant]
+        key = [E, k, H, I, T, quant, "v2"]
         hit = TC.get(self.device, "moe_prefill", key)
         if hit is not None:
-            self.moe_prefill_path = hit["path"]
+            self.moe_prefill_path, self.moe_packed_from_tokens = hit["path"], hit["packed_from_tokens"]
             return dict(hit, cached=True)
         op, dev = torch.ops.hipserve, self.device
         g = torch.Generator(device=dev).manual_seed(E * H + I)
@@ -1083,32 +1101,35 @@ class LlamaModel:
         op.pack_decode_weight(p13, w13, True)
         op.pack_decode_weight(p2, w2, False)
         router = (torch.randn(E, H, device=dev, generator=g) * 0.3).to(torch.bfloat16)
-        x = torch.randn(T, H, device=dev, generator=g).to(torch.bfloat16)
         syn = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=router, w13=w13, w2=w2,
                            moe_packed=(p13, p2))
-        saved = self.moe_prefill_path
-
-        def via(path):
-            def fn(i):
-                self.moe_prefill_path = path
-                if path == "hip":
-                    return self.moe_hip(x, syn)
-                # (quantised experts: both grouped paths dequantise once per step, into the
-                # row-major or straight into the packed scratch, at the same cost: not timed)
-                return self.moe_grouped(x, syn)
-            return fn
-
-        paths = ["blas", "packed"]
-        if not quant and T * k <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * E and self._moe_decode_ok(syn):
-            paths.insert(0, "hip")
-        times = {p_: pgemm._time(via(p_), reps=2) for p_ in paths}
-        self.moe_prefill_path = saved
-        del w13, w2, p13, p2, x, syn
+        counts = []
+        t = T
+        while t * k > MOE_KERNEL_MAX_PAIRS and len(counts) < 5:
+            counts.append(t)
+            t //= 2
+        rows = []
+        for t in counts:
+            x = torch.randn(t, H, device=dev, generator=g).to(torch.bfloat16)
+            # quantised experts dequantise once per step on either path: only the GEMMs are timed
+            row = {"tokens": t, "packed_ms": round(pgemm._time(lambda i: self.moe_grouped(x, syn), reps=2), 3)}
+            if not quant and t * k <= MOE_KERNEL_MAX_ROWS_PER_EXPERT * E and self._moe_decode_ok(syn):
+                row["hip_ms"] = round(pgemm._time(lambda i: self.moe_hip(x, syn), reps=2), 3)
+            rows.append(row)
+        del w13, w2, p13, p2, syn
         torch.cuda.empty_cache()
-        best = min(times, key=times.get)
-        self.moe_prefill_path = best
-        r = {"E": E, "H": H, "I": I, "tokens": T, "quant": quant, "path": best,
-             **{f"{p_}_ms": round(t, 3) for p_, t in times.items()}}
+        wins = [r.get("hip_ms") is None or r["packed_ms"] < r["hip_ms"] for r in rows]
+        best = "packed" if not rows or wins[0] else "hip"
+        frm = T
+        for r, w_ in zip(rows, wins):  # counts descend: the grouped GEMM's run of wins from the top
+            if not w_:
+                break
+            frm = r["tokens"]
+        if best == "packed" and len(rows) and all(wins):
+            frm = 0  # wins down to the pair limit: every prefill-sized batch
+        self.moe_prefill_path, self.moe_packed_from_tokens = best, frm
+        r = {"E": E, "H": H, "I": I, "tokens": T, "quant": quant, "path": best, "packed_from_tokens": frm,
+             "timing": rows}
         TC.put(self.device, "moe_prefill", key, r)
         TC.flush()
         log.info("MoE prefill expert GEMMs: %s", r)

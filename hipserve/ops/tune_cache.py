@@ -11,9 +11,12 @@ kernels, so they are stored in one JSON file per fingerprint:
 
     $HIPSERVE_TUNE_CACHE/<fingerprint>.json     (default ~/.cache/hipserve/tune)
 
-fingerprint = sha1(device capability, CU count, HBM GiB, torch version, hipserve/_C.so bytes):
-a new GPU model, a driver-visible CU count change or a rebuilt kernel library re-tunes.
-``HIPSERVE_TUNE_CACHE=0`` disables the cache (every start times everything). Writers
+fingerprint = sha1(device capability, CU count, HBM GiB, torch version, hipserve/_C.so bytes,
+the kernel-choice knobs of ``TUNING_KNOBS`` that are set): a new GPU model, a driver-visible
+CU count change, a rebuilt kernel library or a start with other knob values re-tunes.
+``HIPSERVE_TUNE_CACHE=0`` disables the cache (every start times everything); deleting the
+directory (or one ``<fingerprint>.json``) invalidates it. The charts put it on the model
+volume so a restarted pod skips the timing (deploy/charts/*/templates/model-deployments.yaml). Writers
 merge with the file on disk and replace it atomically, so TP ranks sharing a volume
 never leave a torn table behind.
 """
@@ -50,17 +53,33 @@ def _lib_digest() -> str:
 
 _FP: dict = {}
 
+# knobs that change a tuner's candidate set or the kernels a timed unit runs: a start
+# with other values must not reuse tables timed under these (docs/ENV.md)
+TUNING_KNOBS = ("HIPSERVE_FP8_DECODE", "HIPSERVE_FP8_PREFILL", "HIPSERVE_FP8_PREFILL_LIB",
+                "HIPSERVE_FUSED_DECODE", "HIPSERVE_FUSED_QKV_ATTN", "HIPSERVE_MOE_PACK",
+                "HIPSERVE_MOE_PACKED_PREFILL", "HIPSERVE_PW_GRID", "HIPSERVE_PW_RW", "HIPSERVE_PW_WM",
+                "HIPSERVE_QGEMM_X16", "HIPSERVE_QPREFILL", "HIPSERVE_QPREFILL_MAX_M",
+                "HIPSERVE_QUANT_SHADOW", "HIPSERVE_SINGLE_LAYOUT")
+
+
+def knob_values() -> dict:
+    return {k: os.environ[k] for k in TUNING_KNOBS if k in os.environ}
+
 
 def fingerprint(device) -> str:
     idx = torch.device(device).index or 0
-    fp = _FP.get(idx)
+    knobs = knob_values()
+    key = (idx, json.dumps(knobs, sort_keys=True))
+    fp = _FP.get(key)
     if fp is None:
         # not the marketing name: it reads "" under rocprofv3, which would make profiled
         # runs miss the tables of unprofiled ones (and re-tune with tracing overhead)
         pr = torch.cuda.get_device_properties(idx)
         ident = [list(torch.cuda.get_device_capability(idx)), pr.multi_processor_count,
                  round(pr.total_memory / 2**30), torch.__version__, _lib_digest()]
-        fp = _FP[idx] = hashlib.sha1(json.dumps(ident).encode()).hexdigest()[:16]
+        if knobs:  # default settings keep the knob-free fingerprint of earlier tables
+            ident.append(sorted(knobs.items()))
+        fp = _FP[key] = hashlib.sha1(json.dumps(ident).encode()).hexdigest()[:16]
     return fp
 
 

@@ -23,6 +23,12 @@ Injection (tests and chaos drills only), ``HIPSERVE_FAULT`` = comma-separated
   ``raise@N``        the engine step N raises ``InjectedFault``
   ``stall@N:SECS``   step N sleeps SECS seconds (heartbeat stalls)
   ``exit@N[:CODE]``  the process exits with CODE (default 13) at step N
+  ``init@0[:CODE]``  model-runner construction raises ``InjectedFault`` (or exits with
+                     CODE): a rank that dies while its peers build their engines
+
+Role ``rankK`` matches TP rank K of a sharded (TP > 1) engine only, e.g.
+``rank3:init@0`` fails rank 3 of the 70B TP=8 phase of bench.py but none of the
+unsharded DP replicas before it.
 """
 from __future__ import annotations
 
@@ -63,9 +69,9 @@ def parse_faults(spec: str) -> list[FaultSpec]:
         if ":" in rest:
             rest, a = rest.split(":", 1)
             arg = float(a)
-        if kind not in ("raise", "stall", "exit"):
+        if kind not in ("raise", "stall", "exit", "init"):
             raise ValueError(f"unknown fault kind {kind!r}")
-        if role not in ("any", "rank0", "worker"):
+        if role not in ("any", "rank0", "worker") and not (role.startswith("rank") and role[4:].isdigit()):
             raise ValueError(f"unknown fault role {role!r}")
         out.append(FaultSpec(role, kind, int(rest), arg))
     return out
@@ -86,11 +92,26 @@ class FaultInjector:
     def active(self) -> bool:
         return bool(self.specs)
 
+    def on_init(self, tp_rank: int, tp_world: int):
+        """Model-runner construction on TP rank ``tp_rank`` of ``tp_world``."""
+        for f in self.specs:
+            if f.kind != "init" or f in self.fired:
+                continue
+            role = f"rank{tp_rank}" if tp_world > 1 else None
+            if f.role not in ("any", role, "rank0" if tp_rank == 0 else "worker"):
+                continue
+            self.fired.append(f)
+            log.warning("fault injection: init on TP rank %d of %d", tp_rank, tp_world)
+            if f.arg is not None:
+                os._exit(int(f.arg))
+            raise InjectedFault(f"injected fault in engine construction (TP rank {tp_rank} of {tp_world})")
+
     def on_step(self, role: str, step: int):
         if not self.specs:
             return
         for f in self.specs:
-            if f.step != step or (f.role != "any" and f.role != role) or f in self.fired:
+            if (f.kind == "init" or f.step != step or (f.role != "any" and f.role != role)
+                    or f in self.fired):
                 continue
             self.fired.append(f)
             log.warning("fault injection: %s@%d on %s", f.kind, f.step, role)

@@ -125,3 +125,27 @@ def test_bench_open_loop_request_rate():
     assert ol["rate_req_s"] == 20 and ol["p90_ttft_ms"] >= ol["p50_ttft_ms"] > 0
     # the tiny CPU model can emit a request's tokens back to back (median gap rounds to 0.00 ms)
     assert ol["p90_itl_ms"] >= ol["p50_itl_ms"] >= 0
+
+
+def test_bench_tp_strong_rank_failure_fails_fast():
+    """VERDICT r5 item 9 (multi-GPU first-run safety): one rank of the world-8 TP phase
+    dies while the engines are being built (fault injection: TP rank 3 raises in
+    model-runner construction). Every rank must be out within 30 s of the failure
+    instead of waiting in a collective for the phase budget, and rank 0 still prints
+    the headline line with ``tp_strong.status`` 'failed (exit N)' — not 'timeout'."""
+    import time
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", HIPSERVE_FAULT="rank3:init@0")
+    cmd = _torchrun(8, 29690, ARGS + ["--tp-phase", "on", "--tp-model", "tiny-llama-tp8",
+                                      "--tp-budget-s", "600"])
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    tp = lines[0]["tp_strong"]
+    assert tp["status"] == "failed (exit 1)", tp
+    assert tp["failed_ranks"] == {"3": 1}, tp
+    assert lines[0]["value"] > 0  # the headline phase (no TP ranks) was unaffected
+    assert tp["phase_wall_s"] < 30, tp  # every rank out within 30 s (3.5 s measured here)
+    assert time.time() - t0 < 300

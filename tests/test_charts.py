@@ -214,3 +214,32 @@ def test_hf_engine_log_format_env():
 
     assert env_of({})["HIPSERVE_LOG_FORMAT"] == "text"
     assert env_of({"engine": {"logFormat": "json"}})["HIPSERVE_LOG_FORMAT"] == "json"
+
+
+def _env(dep):
+    return {e["name"]: e.get("value") for e in dep["spec"]["template"]["spec"]["containers"][0]["env"]}
+
+
+def test_tune_cache_persisted_on_model_volume():
+    """the start-up tuning tables live on storage that outlives the
+    pod (the reference keeps its engine cache on the model PVC,
+    vllm-models/helm-chart/templates/model-deployments.yaml:45-47,71-74)."""
+    d = by_kind(render(HF), "Deployment")["hipserve-llama-3-8b"]
+    path = _env(d)["HIPSERVE_TUNE_CACHE"]
+    c = d["spec"]["template"]["spec"]["containers"][0]
+    mounts = {m["name"]: m["mountPath"] for m in c["volumeMounts"]}
+    assert path.startswith(mounts["model-cache"] + "/")  # on the per-model PVC
+    vols = {v["name"]: v for v in d["spec"]["template"]["spec"]["volumes"]}
+    assert "persistentVolumeClaim" in vols["model-cache"]
+    d = by_kind(render(HF, {"engine": {"tuneCacheDir": "0"}}), "Deployment")["hipserve-llama-3-8b"]
+    assert _env(d)["HIPSERVE_TUNE_CACHE"] == "0"
+
+    g = by_kind(render(GG), "Deployment")["gguf-models-tinyllama"]
+    spec = g["spec"]["template"]["spec"]
+    mounts = {m["name"]: m for m in spec["containers"][0]["volumeMounts"]}
+    vols = {v["name"]: v for v in spec["volumes"]}
+    assert _env(g)["HIPSERVE_TUNE_CACHE"] == mounts["tune-cache"]["mountPath"]
+    assert not mounts["tune-cache"].get("readOnly")
+    assert vols["tune-cache"]["hostPath"]["type"] == "DirectoryOrCreate"
+    g = by_kind(render(GG, {"tuneCache": {"hostPath": ""}}), "Deployment")["gguf-models-tinyllama"]
+    assert "emptyDir" in {v["name"]: v for v in g["spec"]["template"]["spec"]["volumes"]}["tune-cache"]

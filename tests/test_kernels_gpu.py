@@ -501,10 +501,9 @@ def test_penalty_and_top_logprobs_kernels(V, dt):
 
 @pytest.mark.parametrize("T,E,k,norm", [(700, 8, 2, True), (3000, 8, 2, True), (400, 128, 8, True), (300, 64, 4, False)])
 def test_moe_grouped_prefill_vs_fp32(ops, T, E, k, norm):
-    """Prefill MoE (routing kernel, moe_align with group offsets, moe_gather, two
-    grouped expert GEMMs over device offsets, SiLU-GLU, combine) vs an fp32 reference
-    of the same routed computation. (torch._grouped_mm on ROCm reads the offsets on
-    the host internally, so this path is not graph-capturable; prefill runs eager.)"""
+    """Prefill MoE (routing kernel, moe_align, the two packed-layout grouped expert
+    GEMMs with the token gather fused into the first and SiLU-GLU in its epilogue,
+    combine) vs an fp32 reference of the same routed computation."""
     from hipserve.config import PRESETS
     from hipserve.models.llama import LayerWeights, LlamaModel
     from hipserve.parallel.comm import TPGroup

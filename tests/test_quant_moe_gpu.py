@@ -184,8 +184,9 @@ def test_int8_expert_checkpoint_native(tmp_path):
 @pytest.mark.parametrize("packed", [False, True])
 def test_quant_moe_prefill_paths_vs_fp32(kind, packed):
     """Prefill-sized routing of quantised experts: the row-major dequantised scratch with
-    hipBLASLt's grouped GEMM, and the dequantised + packed scratch with the one-launch
-    packed grouped GEMM (``moe_prefill_path = "packed"``), both against the fp32 reference."""
+    the weight-streaming expert kernel (``MOE_PACKED_PREFILL = "0"``), and the dequantised
+    + packed scratch with the one-launch packed grouped GEMM (``"1"``), both against the
+    fp32 reference."""
     from hipserve.config import PRESETS
     from hipserve.models import llama as L
     from hipserve.models.llama import LayerWeights, LlamaModel
@@ -197,7 +198,7 @@ def test_quant_moe_prefill_paths_vs_fp32(kind, packed):
     T = L.MOE_KERNEL_MAX_PAIRS // k + 300
     cfg = PRESETS["tiny-mixtral"].replace(hidden_size=H, intermediate_size=I, num_experts=E, num_experts_per_tok=k)
     m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, KernelOps())
-    m.moe_prefill_path = "packed" if packed else "blas"
+    m.MOE_PACKED_PREFILL = "1" if packed else "0"
     torch.manual_seed(7)
     router = torch.randn(E, H, device=DEV, dtype=torch.bfloat16) * 0.3
     w13, d13 = _qmoe(torch.randn(E, 2 * I, H, device=DEV) * 0.05, kind)

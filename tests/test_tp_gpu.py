@@ -206,11 +206,48 @@ def _logit_bound(eng, ref_model, prompts, want, wtop, n):
     return {"tp1_vs_fp32": err1, "tpn_vs_tp1": dmax, "bound": 2 * err1, "where": where}
 
 
-def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK):
+def force_blas_tuning_cache(cache_dir):
+    """Pre-populate the start-up tuning cache (ops/tune_cache.py) in ``cache_dir`` with
+    hipBLASLt as the decode choice for EVERY shape and row bucket the tuner is asked
+    about, before it looks: the tuner then takes its cache-hit path for all of them and
+    never runs hipBLASLt itself, so every decode-time hipBLASLt call of every graph
+    bucket is that shape's first. Round 5's driver run aborted exactly there
+    ('operation not permitted when stream is capturing' from hipBLASLt under the TP=2
+    graph capture after a cache hit): the engine must warm every bucket before capture."""
+    os.environ["HIPSERVE_TUNE_CACHE"] = cache_dir
+    from hipserve.ops import gemm
+    from hipserve.ops import tune_cache as TC
+
+    orig = gemm.GemmTuner.tune
+
+    def tune(self, shapes, device, ms=None, fused=None):
+        fused = fused or {}
+        for (N, K) in set(shapes):
+            for M in [m for m in (ms or gemm.TUNE_MS) if m <= 64]:
+                row = {"M": M, "N": N, "K": K, "unit": "forced", "best": "blas"}
+                TC.put(device, "decode_gemm", [M, N, K, fused.get((N, K))], {"best": "blas", "bp": None, "row": row})
+        TC.flush()
+        rep = orig(self, shapes, device, ms, fused)
+        assert rep and all(r.get("cached") for r in rep), "tuner re-timed a pre-populated shape"
+        assert all(self.table[k] == "blas" for k in self.table), self.table
+        return rep
+
+    gemm.GemmTuner.tune = tune
+
+
+def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK, force_blas=None, timeout=140):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK="0",
                       WORLD_SIZE=str(world), HIPSERVE_CAR_TIMEOUT_S="60")
+    import faulthandler
+
+    # a rank stuck in a collective, the shm ring or a capture prints its stack to stderr
+    # (shown with the failure) before the harness gives up on it
+    faulthandler.dump_traceback_later(max(timeout - 15, 30), exit=False)
     import torch
     import torch.distributed as dist
+
+    if force_blas:
+        force_blas_tuning_cache(force_blas)
 
     from hipserve.engine.llm_engine import LLMEngine, worker_loop
     from hipserve.engine.model_runner import ModelRunner
@@ -255,38 +292,68 @@ def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK):
             if _split(shape)[0] != "gemma":  # the fp32 oracle covers Llama / MoE / Qwen3 / 8-bit weights
                 info["logit"] = _logit_bound(eng, ref.runner.model, prompts, want, top2, N_BOUND)
             info["car_failed"] = tp.custom_ar.failed() if tp.custom_ar else None
+            info["graph_steps"] = (eng.runner.stats["graph_steps"], ref.runner.stats["graph_steps"])
             eng.shutdown()
             out = ("ok", None, info)
         else:
             worker_loop(ModelRunner(cfg, _model_cfg(shape), tp), tp)
-    except Exception:
+    except BaseException:
         import traceback
-        out = ("error", traceback.format_exc(), None)
-        if rank != 0:
-            q.put(out)
+        out = ("error", f"rank {rank}:\n" + traceback.format_exc(), None)
+        # report BEFORE touching the device again: after a failed capture a device sync can
+        # abort the process, and a report still in the queue's feeder thread is then lost
+        q.put(out)
+        q.close()
+        q.join_thread()
+        os._exit(1)
     if rank == 0:
         q.put(out)
-    torch.cuda.synchronize()
-    dist.destroy_process_group()
     q.close()
     q.join_thread()
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
     os._exit(0)
 
 
-def _run_tp(world, exact, shape="small", n_tok=N_TOK, timeout=140):
+def _run_tp(world, exact, shape="small", n_tok=N_TOK, timeout=140, force_blas=None):
+    """Runs the ranks and returns rank 0's report. Fails fast: a rank that reports an
+    exception, or dies (non-zero exit: abort, segfault) without reporting, fails the
+    test within ~2 s with its traceback / exit code instead of leaving the parent
+    waiting for the full timeout."""
+    import queue
+    import time
+
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, exact, q, shape, n_tok)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, exact, q, shape, n_tok, force_blas, timeout))
+          for r in range(world)]
     for p in ps:
         p.start()
+    t_end = time.time() + timeout
+    res = None
     try:
-        status, err, info = q.get(timeout=timeout)
+        while res is None:
+            try:
+                res = q.get(timeout=1.0)
+                break
+            except queue.Empty:
+                pass
+            dead = [(r, p.exitcode) for r, p in enumerate(ps) if p.exitcode not in (None, 0)]
+            if dead:
+                try:  # a report may still be in flight from the dying rank
+                    res = q.get(timeout=2.0)
+                except queue.Empty:
+                    res = ("error", f"rank(s) died without a report (rank, exit code): {dead}", None)
+            elif time.time() > t_end:
+                alive = [r for r, p in enumerate(ps) if p.is_alive()]
+                res = ("error", f"timeout after {timeout} s; ranks still running: {alive}", None)
     finally:
         for p in ps:
-            p.join(20)
+            p.join(20 if res and res[0] == "ok" else 2)
             if p.is_alive():
                 p.kill()
+    status, err, info = res
     assert status == "ok", err
     return None, info
 
@@ -309,6 +376,21 @@ def test_tp2_shared_gpu_matches_tp1(exact):
     assert info["car_failed"] is False
     _check_ties(info)
     _check_bound(info["logit"], exact)
+
+
+def test_tp2_capture_with_all_blas_tuning_cache(tmp_path):
+    """a pre-populated tuning cache that maps every decode shape to
+    hipBLASLt (so the tuner times nothing and no decode hipBLASLt shape has run before
+    the graphs are captured). The TP=2 and the TP=1 engines both capture every bucket
+    and replay them, and TP=2 still reproduces TP=1 up to near-ties."""
+    _, info = _run_tp(2, False, force_blas=str(tmp_path / "tune"))
+    # 4 buckets (max_num_seqs 8) x 2 staging parities x full / lean
+    assert info["graphs"] == 16, info
+    assert min(info["graph_steps"]) > 0, info  # both engines replayed their graphs
+    assert info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
+    assert info["car_failed"] is False
+    _check_ties(info)
+    _check_bound(info["logit"], False)
 
 
 # The logit bound (VERDICT r2 / r3): max |log-softmax(TP=N) - log-softmax(TP=1)| over the
