@@ -325,7 +325,8 @@ bool launch_prefill_gemm_packed(int epi, void* C, long ldc, const void* X, long 
   const bool grouped = group != nullptr;
   const bool gather = grouped && grp.gather_slots != nullptr;
   if (grouped && (bias != nullptr || epi == PW_EPI_ADD)) return false;
-  if (gather && (rw != 4 || grp.gather_k < 1 || (long)grp.x_rows * ldx * 2 >= (1L << 31) - 4096)) return false;
+  // (the gather form always runs rw = 4, PW_LAUNCH1: any rw knob value is accepted)
+  if (gather && (grp.gather_k < 1 || (long)grp.x_rows * ldx * 2 >= (1L << 31) - 4096)) return false;
   if (M < 1 || N < 1 || K < 256 || K % 256 || (wm != 1 && wm != 2) || (rw != 2 && rw != 4 && rw != 5)) return false;
   const bool glu = epi == PW_EPI_GLU || epi == PW_EPI_GEGLU;
   if (glu && (N % 128 || bias != nullptr)) return false;

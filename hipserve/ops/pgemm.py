@@ -27,6 +27,19 @@ OFFSET_LIMIT = 1 << 31
 # (prefill_gemm.hip pgemm_f8_kernel). No bf16 shadow of the weights is needed.
 FP8_MODE = os.environ.get("HIPSERVE_FP8_PREFILL", "1")
 F8_MIN_ROWS = 128
+# hipBLASLt's FP8 GEMM on a per-call re-laid-out copy (quant.f8_lib_weight, FP8_LIB
+# "scratch") only above this many rows: the re-layout reads and writes the whole weight
+# (~54 GB per Gemma-3-27B step), which a decode-only batch (graph buckets up to 512
+# rows) cannot amortise — those run the hand-written kernel on the tiled copy
+F8_SCRATCH_MIN_ROWS = 512
+
+
+def f8_lib_ok(w, M: int) -> bool:
+    """Route an M-row FP8 GEMM to hipBLASLt: a resident plain copy at any M % 16 == 0,
+    the per-call scratch re-layout only for prefill-sized batches."""
+    if M % 16:
+        return False
+    return getattr(w, "f8_plain", None) is not None or M > F8_SCRATCH_MIN_ROWS
 
 
 def _f8_parts(w):
@@ -73,7 +86,7 @@ def f8_gemm(x: torch.Tensor, w, epi: int = 0, out: torch.Tensor | None = None, x
         out = torch.empty(M, n, dtype=torch.bfloat16, device=dev)
     xq, xs = x8 if x8 is not None else act_quant(x)
     from . import quant as Q
-    wp = Q.f8_lib_weight(w) if M % 16 == 0 else None
+    wp = Q.f8_lib_weight(w) if f8_lib_ok(w, M) else None
     if wp is not None:  # hipBLASLt FP8, row-wise scales, on the plain e4m3 weight
         y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wp.t(), scale_a=xs.reshape(-1, 1),
                              scale_b=w.f8_scale, out_dtype=torch.bfloat16)
@@ -97,7 +110,7 @@ def f8_glu_q8(x: torch.Tensor, w, gelu: bool, x8=None):
     weight runs the hand-written kernel (the caller runs f8_gemm's GLU epilogue instead)."""
     from . import quant as Q
     M = x.shape[0]
-    if getattr(w, "f8_scale", None) is None or M % 16 or not hasattr(torch.ops.hipserve, "glu_quant"):
+    if getattr(w, "f8_scale", None) is None or not f8_lib_ok(w, M) or not hasattr(torch.ops.hipserve, "glu_quant"):
         return None
     wp = Q.f8_lib_weight(w)
     xq, xs = x8 if x8 is not None else act_quant(x)

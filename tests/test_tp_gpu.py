@@ -206,14 +206,20 @@ def _logit_bound(eng, ref_model, prompts, want, wtop, n):
     return {"tp1_vs_fp32": err1, "tpn_vs_tp1": dmax, "bound": 2 * err1, "where": where}
 
 
-def force_blas_tuning_cache(cache_dir):
-    """Pre-populate the start-up tuning cache (ops/tune_cache.py) in ``cache_dir`` with
-    hipBLASLt as the decode choice for EVERY shape and row bucket the tuner is asked
-    about, before it looks: the tuner then takes its cache-hit path for all of them and
-    never runs hipBLASLt itself, so every decode-time hipBLASLt call of every graph
-    bucket is that shape's first. Round 5's driver run aborted exactly there
-    ('operation not permitted when stream is capturing' from hipBLASLt under the TP=2
-    graph capture after a cache hit): the engine must warm every bucket before capture."""
+def force_blas_tuning_cache(cache_dir, mode="all"):
+    """Pre-populate the start-up tuning cache (ops/tune_cache.py) in ``cache_dir`` before
+    the tuner looks, so it takes its cache-hit path for every shape and never runs
+    hipBLASLt itself:
+      ``all``    hipBLASLt is the decode choice for every shape and row bucket;
+      ``below``  hipBLASLt below the largest decode bucket, the hand-written decode GEMM
+                 at it — the round-5 engine warmed ONLY the largest bucket before
+                 capture, so there a shape's first hipBLASLt call ever is made under
+                 graph capture;
+      ``pinned`` the first hand-written decode GEMM config at every bucket: a fixed,
+                 box-independent table (deterministic reduction orders).
+    Round 5's driver run aborted in the TP=2 capture after a cache hit ('operation not
+    permitted when stream is capturing' from hipBLASLt): the engine must run every
+    bucket eagerly before it captures."""
     os.environ["HIPSERVE_TUNE_CACHE"] = cache_dir
     from hipserve.ops import gemm
     from hipserve.ops import tune_cache as TC
@@ -222,20 +228,29 @@ def force_blas_tuning_cache(cache_dir):
 
     def tune(self, shapes, device, ms=None, fused=None):
         fused = fused or {}
+        ms_ = [m for m in (ms or gemm.TUNE_MS) if m <= 64]
         for (N, K) in set(shapes):
-            for M in [m for m in (ms or gemm.TUNE_MS) if m <= 64]:
-                row = {"M": M, "N": N, "K": K, "unit": "forced", "best": "blas"}
-                TC.put(device, "decode_gemm", [M, N, K, fused.get((N, K))], {"best": "blas", "bp": None, "row": row})
+            spec = fused.get((N, K))
+            glu = spec is not None and spec[0] == "glu"
+            for M in ms_:
+                best = "blas"
+                if mode == "pinned" or (mode == "below" and M == max(ms_)):
+                    dg = [c for c in self.candidates(M, N, K, glu=glu) if c[0] == "dg" and c[1] != 3]
+                    best = dg[0] if dg else "blas"
+                row = {"M": M, "N": N, "K": K, "unit": "forced", "best": str(best)}
+                TC.put(device, "decode_gemm", [M, N, K, spec], {"best": best, "bp": None, "row": row})
         TC.flush()
         rep = orig(self, shapes, device, ms, fused)
         assert rep and all(r.get("cached") for r in rep), "tuner re-timed a pre-populated shape"
-        assert all(self.table[k] == "blas" for k in self.table), self.table
+        if mode != "pinned":
+            assert all(c == "blas" for (M, _, _), c in self.table.items() if M < max(ms_)), self.table
         return rep
 
     gemm.GemmTuner.tune = tune
 
 
 def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK, force_blas=None, timeout=140):
+    """force_blas: None or (cache dir, mode) for force_blas_tuning_cache."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK="0",
                       WORLD_SIZE=str(world), HIPSERVE_CAR_TIMEOUT_S="60")
     import faulthandler
@@ -247,7 +262,7 @@ def _worker(rank, world, port, exact, q, shape="small", n_tok=N_TOK, force_blas=
     import torch.distributed as dist
 
     if force_blas:
-        force_blas_tuning_cache(force_blas)
+        force_blas_tuning_cache(*force_blas)
 
     from hipserve.engine.llm_engine import LLMEngine, worker_loop
     from hipserve.engine.model_runner import ModelRunner
@@ -378,12 +393,13 @@ def test_tp2_shared_gpu_matches_tp1(exact):
     _check_bound(info["logit"], exact)
 
 
-def test_tp2_capture_with_all_blas_tuning_cache(tmp_path):
-    """a pre-populated tuning cache that maps every decode shape to
-    hipBLASLt (so the tuner times nothing and no decode hipBLASLt shape has run before
-    the graphs are captured). The TP=2 and the TP=1 engines both capture every bucket
-    and replay them, and TP=2 still reproduces TP=1 up to near-ties."""
-    _, info = _run_tp(2, False, force_blas=str(tmp_path / "tune"))
+@pytest.mark.parametrize("mode", ["all", "below"])
+def test_tp2_capture_with_blas_tuning_cache(tmp_path, mode):
+    """a pre-populated tuning cache that maps the decode shapes to
+    hipBLASLt (so the tuner times nothing; ``below``: only under the largest bucket, so
+    no warm-up of that bucket runs them). The TP=2 and the TP=1 engines both capture
+    every bucket and replay them, and TP=2 still reproduces TP=1 up to near-ties."""
+    _, info = _run_tp(2, False, force_blas=(str(tmp_path / "tune"), mode))
     # 4 buckets (max_num_seqs 8) x 2 staging parities x full / lean
     assert info["graphs"] == 16, info
     assert min(info["graph_steps"]) > 0, info  # both engines replayed their graphs
@@ -455,19 +471,24 @@ def test_tp8_70b_shapes_shared_gpu_matches_tp1():
     decode with lookahead, in-house IPC all-reduce / fused add+RMSNorm / logits
     all-gather across 8 ranks) reproduces TP=1 token for token up to near-ties, as the
     TP=2 test. Reference: BASELINE.json config "Llama-3 70B TP=8 over xGMI"."""
-    _, info = _run_tp(8, True, shape="70b", n_tok=N_TOK_70B, timeout=400)
+    # the decode GEMM table is pinned (not timed on this box): the split-K reduction
+    # orders, and so TP=8's divergences from TP=1, are the same on every box (ADVICE r5)
+    import tempfile
+    _, info = _run_tp(8, True, shape="70b", n_tok=N_TOK_70B, timeout=400,
+                      force_blas=(tempfile.mkdtemp(prefix="hipserve_tune_"), "pinned"))
     _check_bound(info["logit"])
     assert info["graphs"] and info["lookahead"] and info["custom_ar"] and info["shm_ring"], info
     assert info["car_failed"] is False
     print("exact prefix per prompt:", info["exact_prefix"], "divergences:", len(info["ties"]))
     # exact (fp32) exchange: a divergence is only allowed where TP=1's margin is within
-    # the measured logit bound (asserted per divergence below), and at most 6 of the 128
+    # the measured logit bound (asserted per divergence below), and at most 2 of the 128
     # positions besides exact ties (TP=1's two candidates with the same log-prob: either
-    # is the greedy choice). The count varies from box to box: the decode GEMMs' split-K
-    # factors are timed at start-up, which reorders fp32 sums, and this random-init model
-    # has many top-2 margins of one bf16 logit step (1/32 nat): round 5 saw 0 and 4
+    # is the greedy choice). This random-init model has many top-2 margins of one bf16
+    # logit step (1/32 nat); with the pinned decode GEMM table the count no longer moves
+    # with per-box start-up timing
     strict = [t for t in info["ties"] if t[4] is None or t[5] is None or t[4] - t[5] > 1e-6]
-    assert len(strict) <= 6, info["ties"]
+    print("strict divergences:", len(strict))
+    assert len(strict) <= 2, info["ties"]
     for i, j, t1, t2, lp1, lp2 in info["ties"]:
         assert lp1 is not None and lp2 is not None, f"prompt {i} pos {j}: TP=8 token {t2} not in TP=1's top-5"
         assert lp1 - lp2 <= min(TIE_70B, info["logit"]["bound"]), \

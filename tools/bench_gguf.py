@@ -69,6 +69,10 @@ def main():
                     help="M > 64: the prefill GEMM from the blocks (qpf) and the M-tiled dequant-MFMA kernel vs "
                          "dequant-to-scratch + hipBLASLt vs a bf16 shadow")
     ap.add_argument("--no-mtiled", action="store_true", help="--prefill: skip the (slow at large M) M-tiled kernel")
+    ap.add_argument("--v3", action="store_true", help="also the v3 decode GEMM (qgemm3_kernel) at NS = 1, 2, 4")
+    ap.add_argument("--cold", action="store_true",
+                    help="rotate every timed call over copies of the blocks (>= 768 MiB): HBM-cold weights, "
+                         "as in a decode step, instead of MALL-resident ones")
     a = ap.parse_args()
     load_library()
     rng = np.random.default_rng(0)
@@ -120,6 +124,13 @@ def main():
                 del dense, buf
                 continue
             rows = []
+            qw.groups
+            ncopy = max(1, min(64, -(-(768 << 20) // qw.nbytes))) if a.cold else 1
+            copies = [qw.v2_args[0]] + [[q.clone() for q in qw.v2_args[0]] for _ in range(ncopy - 1)]
+
+            def timed(launch):  # µs per call, over the block copies
+                return _time(lambda: [launch(qs) for qs in copies], reps=max(1, 20 // ncopy)) / ncopy
+
             rows.append(("v2_partial", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw))))
             x16 = None
             if 32 < M <= 64:  # x staged from a producer's f16 pair-order copy (out16 / act16)
@@ -127,14 +138,23 @@ def main():
                 x16 = h.contiguous()
                 rows.append(("v2_partial_x16", Q.v2_splits(qw, M), _time(lambda: Q.quant_partial(x, qw, x16))))
             nsb = qw.K // 256
+            e = Q._empty(x.device, torch.bfloat16)
             for Sx in sorted({-(-nsb // -(-nsb // S)) for S in (a.splits or (1, 2, 4, 8, 16, 32)) if S <= nsb}):
                 ws = torch.empty(Sx * M * qw.N, dtype=torch.float32, device="cuda")
-                e = Q._empty(x.device, torch.bfloat16)
-                rows.append((f"v2_S{Sx}", Sx, _time(lambda: Q._launch_v2(e, ws, x, qw, Sx, x16))))
+                rows.append((f"v2_S{Sx}", Sx, timed(lambda qs: Q._launch_v2(e, ws, x, qw, Sx, x16, qs))))
+            if a.v3 and M <= 64:
+                for ns in (1, 2, 4):
+                    if nsb % ns:
+                        continue
+                    Sx = nsb // ns
+                    ws = torch.empty(Sx * M * qw.N, dtype=torch.float32, device="cuda")
+                    rows.append((f"v3_NS{ns}", Sx, timed(lambda qs: Q._launch_v2(e, ws, x, qw, -ns, None, qs))))
+            del copies
             for kern, S, us in rows:
                 print(json.dumps({"proj": name, "M": M, "kernel": kern, "splits": S, "us": round(us, 2),
-                                  "weight_MB": round(qw.nbytes / 1e6, 2),
-                                  "TBps": round(qw.nbytes / us / 1e6, 3)}), flush=True)
+                                  "weight_MB": round(qw.nbytes / 1e6, 2), "cold": a.cold,
+                                  "TBps": round(qw.nbytes / us / 1e6, 3),
+                                  "partial_MB": round(S * M * qw.N * 4 / 1e6, 2)}), flush=True)
         del qw
         torch.cuda.empty_cache()
 
