@@ -759,221 +759,6 @@ __global__ __launch_bounds__(256) void x_f16_pairs_kernel(unsigned short* __rest
   }
 }
 
-// ---------------------------------------------------------------- decode GEMM v3
-// at M = 64 the v2 body above spends 42 % of its wave cycles in
-// s_waitcnt (profiles/r2_qgemm_m64_pmc.md): one super-chunk of weights in flight per
-// wave, and a workgroup barrier per super-chunk (x restaging) that makes every wave
-// wait for the slowest load of its workgroup at every step. v3 changes the SCHEDULE,
-// not the math — the same tiled chunks, subnormal-integer dequant (Dec::step), f16
-// MFMA and k order, so results differ from v2 only by the K-slice split:
-//  * a workgroup stages the x of ONE K slice (NS super-chunks) into LDS once, then its
-//    8 waves stream row groups of that slice with no barrier at all: each wave walks its
-//    own row groups (wave index + k * waves of the slice, over the launch's parts);
-//  * every wave keeps 4 super-chunks of raw blocks in flight in a register ring: the
-//    slot a chunk was just decoded from is reloaded with the chunk 4 ahead, across
-//    row-group boundaries (~9 KB per wave, ~74 KB per CU in flight for Q4_K);
-//  * one launch per format (the staged x image is in the format's k order), grid = K
-//    slices x workgroups per slice, about one 8-wave workgroup per CU;
-//  * f16 range: a staged value beyond +-65504 sets a flag; the workgroup then restages
-//    its slice with a power-of-two pre-scale per row and undoes it at the store (exact).
-// Output: fp32 partials ws[S, M, Ntot] (S = K / (256 NS)) for the decode layer's fused
-// epilogues, or bf16 out when S == 1 and ws == nullptr.
-template <int QT, int MT, int NS>
-__global__ __launch_bounds__(512) void qgemm3_kernel(unsigned short* __restrict__ out, long out_stride,
-                                                     float* __restrict__ ws, const unsigned short* __restrict__ x,
-                                                     long x_stride, Parts parts, int ntot_rg, int M, int Ntot, int K,
-                                                     int S) {
-  constexpr int XPL = x_plane<MT>();  // f16 of one lane-group plane of one super-chunk
-  constexpr int XSB = 4 * XPL;        // f16 of one super-chunk's x image
-  constexpr int XR = 16 * MT;         // staged x rows
-  constexpr int CB = chunk_bytes<QT>();
-  constexpr int R = 4 / NS;           // row groups per 4-chunk loop body
-  constexpr int IT = NS * MT;         // 16-byte x staging items per thread (NS * XR * 32 / 512)
-  static_assert(NS == 1 || NS == 2 || NS == 4, "NS divides the 4-deep ring");
-  __shared__ __attribute__((aligned(16))) _Float16 xs[NS * XSB];
-  __shared__ float xrow[XR];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c = lane & 15;
-  const int slice = blockIdx.x % S, wgi = blockIdx.x / S, W = gridDim.x / S;
-  const int nsb = K >> 8, sb0 = slice * NS;
-  const int wid = wgi * 8 + wave, nwaves = W * 8;
-  const int nk = wid < ntot_rg ? (ntot_rg - wid + nwaves - 1) / nwaves : 0;  // this wave's row groups
-
-  // row group k of this wave -> (part, row group in the part); parts.p[i].tile0 holds the
-  // part's first row group in the launch. Selected by unrolled compares: every value is
-  // wave-uniform (scalar registers), no runtime-indexed argument array
-  auto locate = [&](int k, const unsigned char*& q, int& gi, int& col) {
-    const int G = min(wid + k * nwaves, ntot_rg - 1);
-    q = parts.p[0].q;
-    int t0 = 0;
-    col = parts.p[0].col;
-#pragma unroll
-    for (int i = 1; i < kMaxParts; ++i)
-      if (i < parts.n && G >= parts.p[i].tile0) {
-        q = parts.p[i].q;
-        t0 = parts.p[i].tile0;
-        col = parts.p[i].col;
-      }
-    gi = G - t0;
-  };
-  auto load_chunk = [&](int k, int j, Raw& r) {  // past the wave's last row group: re-read it (never used)
-    const unsigned char* q;
-    int gi, col;
-    locate(min(k, max(nk - 1, 0)), q, gi, col);
-    load_raw<QT>(q + ((long)gi * nsb + sb0 + j) * CB, g, c, lane, r);
-  };
-
-  // x first, then the weight ring: vmcnt retires loads in issue order, so the x
-  // conversion's wait leaves the (younger) weight loads in flight across the staging
-  u16x8 xv[IT];
-  auto load_x = [&]() {
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int idx = i * 512 + tid, j = idx / (XR * 32), rem = idx - j * (XR * 32), row = rem >> 5, fr = rem & 31;
-      // rows >= M are clamped: they feed output rows that are never stored
-      xv[i] = *reinterpret_cast<const u16x8*>(x + (long)min(row, M - 1) * x_stride + (sb0 + j) * 256 +
-                                              kbase<QT>(fr >> 3, fr & 7));
-    }
-  };
-  load_x();
-  Raw ring[4];
-  if (nk > 0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) load_chunk(q / NS, q % NS, ring[q]);
-  }
-  auto stage = [&](bool scaled) {
-    bool big = false;
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int idx = i * 512 + tid, j = idx / (XR * 32), rem = idx - j * (XR * 32), row = rem >> 5, fr = rem & 31;
-      const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);  // bf16 pairs (0,1) (2,3) (4,5) (6,7)
-      float f[8] = {bf_lo(w[0]), bf_lo(w[1]), bf_hi(w[0]), bf_hi(w[1]),
-                    bf_lo(w[2]), bf_lo(w[3]), bf_hi(w[2]), bf_hi(w[3])};  // pair order {0,2,1,3,4,6,5,7}
-      const float sc = scaled ? xrow[row] : 1.f;
-      f16x8 h;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = f[e] * sc;
-        big |= __builtin_fabsf(v) > 65504.f;
-        h[e] = static_cast<_Float16>(v);
-      }
-      *reinterpret_cast<f16x8*>(&xs[j * XSB + (fr >> 3) * XPL + row * kXR + (fr & 7) * 8]) = h;
-    }
-    return big;
-  };
-  const bool scaled = __syncthreads_or(stage(false));
-  if (scaled) {  // rare: some |x| beyond the f16 range -> per-row 2^-k pre-scale of this slice
-    unsigned* xb = reinterpret_cast<unsigned*>(xrow);
-    if (tid < XR) xb[tid] = 0u;
-    __syncthreads();
-    load_x();  // again (not kept live across the common path: it would hold IT x 4 VGPRs)
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int idx = i * 512 + tid, j = idx / (XR * 32), row = (idx - j * (XR * 32)) >> 5;
-      const u32x4 w = __builtin_bit_cast(u32x4, xv[i]);
-      unsigned mx = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mx = max(mx, max((w[e] << 16) & 0x7FFF0000u, w[e] & 0x7FFF0000u));
-      atomicMax(&xb[row], mx);
-    }
-    __syncthreads();
-    if (tid < XR) {  // 2^-k with max |x| 2^-k < 2^15 (inf / NaN rows: k = 126, the result stays non-finite)
-      const int ex = (int)(xb[tid] >> 23) - 127;
-      xrow[tid] = __builtin_bit_cast(float, (unsigned)(127 - min(126, max(0, ex - 14))) << 23);
-    }
-    __syncthreads();
-    stage(true);
-    __syncthreads();
-  }
-  if (nk == 0) return;  // no barrier follows
-
-  const _Float16* xw = xs + g * XPL + c * kXR;  // fragment (g, s) of row 16 t + c at + 16 t kXR + 8 s
-  float un[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) un[t] = scaled ? 1.f / xrow[16 * t + c] : 1.f;  // exact: powers of two
-  f32x4 acc[MT];
-  const int nbody = (nk + R - 1) / R;
-  for (int b = 0; b < nbody; ++b) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = q % NS, kq = q / NS;
-      if (j == 0) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      Dec<QT> dec;
-      dec.setup(ring[q], g);
-      const _Float16* xj = xw + j * XSB;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        f16x8 bx[MT];  // read before the dequant VALU: the MFMAs do not wait out an LDS round trip
-#pragma unroll
-        for (int t = 0; t < MT; ++t) bx[t] = *reinterpret_cast<const f16x8*>(xj + 16 * t * kXR + 8 * s);
-        __builtin_amdgcn_sched_barrier(0);
-        const f16x8 a = dec.step(ring[q], g, s);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bx[t], acc[t], 0, 0, 0);
-      }
-      // slot q is free: the chunk 4 ahead (the next body's q)
-      load_chunk((b + 1) * R + kq, j, ring[q]);
-      if (j == NS - 1) {
-        const int k = b * R + kq;
-        if (k < nk) {
-          const unsigned char* qp;
-          int gi, col;
-          locate(k, qp, gi, col);
-          const int n0 = col + 16 * gi + 4 * g;  // rows n0 .. n0 + 3 of the output, token 16 t + c
-#pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            const int m = 16 * t + c;
-            if (m >= M) continue;
-            const f32x4 v = acc[t] * un[t];
-            if (ws != nullptr) {
-              *reinterpret_cast<f32x4*>(ws + ((long)slice * M + m) * Ntot + n0) = v;
-            } else {
-              *reinterpret_cast<uint2*>(out + (long)m * out_stride + n0) =
-                  uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-            }
-          }
-        }
-      }
-    }
-  }
-}
-
-template <int QT, int MT>
-void v3_launch_ns(int NS, void* out, long out_stride, float* ws, const void* x, long x_stride, const Parts& P,
-                  int ntot_rg, int M, int Ntot, int K, hipStream_t s) {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-  }
-  const int S = (K / 256) / NS;
-  // one 8-wave workgroup per CU in total (the x slice fills most of the LDS at MT = 4),
-  // and no more waves per slice than the row groups need
-  const int W = max(1, min(ncu / S, (ntot_rg + 7) / 8));
-  const dim3 grid(S * W);
-  auto* o = static_cast<unsigned short*>(out);
-  auto* xi = static_cast<const unsigned short*>(x);
-  if (NS == 4)
-    qgemm3_kernel<QT, MT, 4><<<grid, 512, 0, s>>>(o, out_stride, ws, xi, x_stride, P, ntot_rg, M, Ntot, K, S);
-  else if (NS == 2)
-    qgemm3_kernel<QT, MT, 2><<<grid, 512, 0, s>>>(o, out_stride, ws, xi, x_stride, P, ntot_rg, M, Ntot, K, S);
-  else
-    qgemm3_kernel<QT, MT, 1><<<grid, 512, 0, s>>>(o, out_stride, ws, xi, x_stride, P, ntot_rg, M, Ntot, K, S);
-}
-
-template <int QT>
-void v3_launch(int NS, void* out, long out_stride, float* ws, const void* x, long x_stride, const Parts& P,
-               int ntot_rg, int M, int Ntot, int K, hipStream_t s) {
-  if (M <= 16) v3_launch_ns<QT, 1>(NS, out, out_stride, ws, x, x_stride, P, ntot_rg, M, Ntot, K, s);
-  else if (M <= 32) v3_launch_ns<QT, 2>(NS, out, out_stride, ws, x, x_stride, P, ntot_rg, M, Ntot, K, s);
-  else v3_launch_ns<QT, 4>(NS, out, out_stride, ws, x, x_stride, P, ntot_rg, M, Ntot, K, s);
-}
-
 }  // namespace
 
 int gguf_tiled_chunk_bytes(int qtype) {
@@ -997,34 +782,6 @@ int gguf_tiled_chunk_bytes(int qtype) {
 void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x, long x_stride,
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16) {
-  if (S < 0) {  // decode GEMM v3 with NS = -S super-chunks per K slice (gguf_v3_ok checked by the caller)
-    const int NS = -S;
-    int fmts[kMaxParts], nf = 0;
-    for (int i = 0; i < nparts; ++i) {
-      bool seen = false;
-      for (int j = 0; j < nf; ++j) seen |= fmts[j] == parts[i].qtype;
-      if (!seen) fmts[nf++] = parts[i].qtype;
-    }
-    for (int f = 0; f < nf; ++f) {  // one launch per format (x is staged in the format's k order)
-      Parts P{};
-      int rg = 0;
-      for (int i = 0; i < nparts; ++i) {
-        if (parts[i].qtype != fmts[f]) continue;
-        P.p[P.n++] = Part{static_cast<const unsigned char*>(parts[i].q), parts[i].rs, parts[i].qtype, parts[i].rows,
-                          parts[i].col, rg};
-        rg += parts[i].rows / 16;
-      }
-      switch (fmts[f]) {
-        case Q4_0: v3_launch<Q4_0>(NS, out, out_stride, ws, x, x_stride, P, rg, M, Ntot, K, s); break;
-        case Q4_1: v3_launch<Q4_1>(NS, out, out_stride, ws, x, x_stride, P, rg, M, Ntot, K, s); break;
-        case Q8_0: v3_launch<Q8_0>(NS, out, out_stride, ws, x, x_stride, P, rg, M, Ntot, K, s); break;
-        case Q4_K: v3_launch<Q4_K>(NS, out, out_stride, ws, x, x_stride, P, rg, M, Ntot, K, s); break;
-        case Q5_K: v3_launch<Q5_K>(NS, out, out_stride, ws, x, x_stride, P, rg, M, Ntot, K, s); break;
-        case Q6_K: v3_launch<Q6_K>(NS, out, out_stride, ws, x, x_stride, P, rg, M, Ntot, K, s); break;
-      }
-    }
-    return;
-  }
   // weight rows per workgroup: 128, or 256 for the wide M = 33-64 body (m64_wide)
   const int ROWS = m64_wide(M, Ntot) ? 256 : 16 * 2 * kWaves;
   int fmts[kMaxParts], nf = 0;

@@ -291,23 +291,13 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   const int np = qs.size();
   TORCH_CHECK(np >= 1 && np <= 4 && (int)qtypes.size() == np && (int)rss.size() == np && (int)rows.size() == np && (int)cols.size() == np,
               "gguf_gemm_parts: 1-4 parts");
-  TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && splits != 0);
+  TORCH_CHECK(K % 256 == 0 && x.size(1) >= K && splits >= 1);
   const int M = x.size(0);
   TORCH_CHECK(M >= 1, "gguf_gemm_parts: M >= 1 (M > 64 sweeps 64-row tiles)");
   TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
   const int nsb = K / 256;
-  int S;
-  if (splits < 0) {  // decode GEMM v3 (gguf_mfma.hip qgemm3_kernel): NS = -splits super-chunks per K slice
-    const int NS = -splits;
-    TORCH_CHECK((NS == 1 || NS == 2 || NS == 4) && nsb % NS == 0 && M <= 64,
-                "gguf_gemm_parts v3: NS in {1, 2, 4} dividing K / 256, M <= 64");
-    for (size_t i = 0; i < qtypes.size(); ++i)
-      TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 5, "gguf_gemm_parts v3: GGUF block formats only");
-    S = nsb / NS;
-  } else {
-    const int per = (nsb + splits - 1) / splits;
-    S = (nsb + per - 1) / per;
-  }
+  const int per = (nsb + splits - 1) / splits;
+  const int S = (nsb + per - 1) / per;
   hipserve::GgufPart P[4];
   for (int i = 0; i < np; ++i) {
     TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 8, "gguf_gemm_parts: kernel qtype 0-8");

@@ -393,29 +393,10 @@ def _bucket(M: int) -> int:
     return M_BUCKETS[-1]
 
 
-# decode GEMM v3 (gguf_mfma.hip qgemm3_kernel): a K slice of NS super-chunks staged once
-# per workgroup, no barrier in the weight stream, 4 chunks in flight per wave. A split
-# choice S < 0 in SPLIT_TABLE means v3 with NS = -S (K / (256 NS) slices).
-V3 = os.environ.get("HIPSERVE_QGEMM_V3", "1") != "0"
-V3_NS = (1, 2, 4)
-
-
-def v3_ok(w) -> bool:
-    """v3 takes ``w``: tiled GGUF block formats only (no FP8 / INT8 parts)."""
-    return (V3 and isinstance(w, QuantWeight) and w.v2 and all(p.kqt in (0, 1, 2, 3, 4, 5) for p in w.parts)
-            and hasattr(torch.ops.hipserve, "gguf_gemm_parts"))
-
-
-def split_count(w: QuantWeight, S: int) -> int:
-    """Partial slabs a split choice writes: S for v2, K / (256 NS) for v3 (S = -NS)."""
-    return (w.K // 256) // -S if S < 0 else S
-
-
 def v2_splits(w: QuantWeight, M: int) -> int:
     """K slices for the v2 kernel: the tuned choice for (weight shape, M bucket) if
     any, else enough (row tile, K slice) workgroups to fill the chip, capped so the
-    fp32 partials (S*M*N*4 B) stay below the weight bytes. A negative value selects
-    the v3 kernel (``split_count`` gives its slab count)."""
+    fp32 partials (S*M*N*4 B) stay below the weight bytes."""
     S = SPLIT_TABLE.get((_sig(w), _bucket(M)))
     if S is not None:
         return S
@@ -444,13 +425,12 @@ def _empty(device, dtype):
 
 
 def _launch_v2(out, ws, x, w: QuantWeight, S: int, x16=None, qs=None):
-    """S > 0: the v2 kernel with S K slices; S < 0: v3 with NS = -S (x16 unused: v3
-    stages each K slice once per workgroup). ``qs``: other copies of the parts' blocks
+    """The v2 kernel with S K slices; ``qs``: other copies of the parts' blocks
     (cold-cache timing)."""
     w.groups  # (re)builds v2_args
     a = w.v2_args
     return torch.ops.hipserve.gguf_gemm_parts(out, ws, x, qs if qs is not None else a[0], a[1], a[2], a[3], a[4],
-                                              w.N, w.K, S, x16 if S > 0 else None)
+                                              w.N, w.K, S, x16)
 
 
 def _graph_time_us(fn, reps: int = 10, rounds: int = 3) -> float:
@@ -497,7 +477,7 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
                 (F8_SPLIT_TABLE if kind == "f8_splits" else SPLIT_TABLE)[(sig, _bucket(M))] = h["S"]
                 report.append(dict(h["row"], cached=True))
             del seen[sig]
-    nbuf = max((4 * w.N * max(ms) * max(32, w.K // 256) for w in seen.values()), default=0)
+    nbuf = max((4 * w.N * max(ms) * 32 for w in seen.values()), default=0)
     ws = torch.empty(min(nbuf, max_ws_bytes) // 4, dtype=torch.float32, device=device)
     empty = _empty(device, torch.bfloat16)
     for sig, w in seen.items():
@@ -517,16 +497,13 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
             # (out16 / act16), staged as is: time that form
             x16 = x.to(torch.float16) if 32 < M <= 64 else None
             cands = sorted({_actual_splits(nsb, s) for s in (1, 2, 4, 8, 16, 32, 64) if s <= nsb})
-            if v3_ok(w) and M <= 64:
-                cands += [-ns for ns in V3_NS if nsb % ns == 0]
             cost = {}
             for S in cands:
-                nS = split_count(w, S)
-                if nS * M * w.N > ws.numel():
+                if S * M * w.N > ws.numel():
                     continue
                 t = _graph_time_us(lambda S=S: [_launch_v2(empty, ws, x, w, S, x16, qs) for qs in copies],
                                    reps=max(1, 10 // ncopy)) / ncopy
-                cost[S] = t + 1e6 * nS * M * w.N * 4 / PARTIAL_READ_BPS
+                cost[S] = t + 1e6 * S * M * w.N * 4 / PARTIAL_READ_BPS
             best = min(cost, key=cost.get)
             SPLIT_TABLE[(sig, _bucket(M))] = best
             row = {"K": w.K, "N": w.N, "M": M, "S": best, "us": {k: round(v, 2) for k, v in sorted(cost.items())}}
@@ -632,10 +609,9 @@ def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = No
     if M <= MAX_FUSED_M and f8_decode_ok(w):
         return f8_decode_partial(x, w, x8)
     S = v2_splits(w, M)
-    nS = split_count(w, S)
-    ws = torch.empty(nS * M * w.N, dtype=torch.float32, device=x.device)
+    ws = torch.empty(S * M * w.N, dtype=torch.float32, device=x.device)
     _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S, x16)
-    return ws, nS
+    return ws, S
 
 
 # Prefill (M > MAX_FUSED_M) straight from the tiled GGUF blocks (gguf_mfma.hip qpg_kernel:
@@ -743,13 +719,12 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
             return out
         if w.v2 and x.is_cuda:
             S = v2_splits(w, M)
-            nS = split_count(w, S)
-            if nS == 1:
-                _launch_v2(out, _empty(x.device, torch.float32), x, w, S)
+            if S == 1:
+                _launch_v2(out, _empty(x.device, torch.float32), x, w, 1)
                 return out
-            ws = torch.empty(nS, M, w.N, dtype=torch.float32, device=x.device)
+            ws = torch.empty(S, M, w.N, dtype=torch.float32, device=x.device)
             _launch_v2(_empty(x.device, torch.bfloat16), ws, x, w, S)
-            torch.ops.hipserve.splitk_reduce(out, ws, nS)
+            torch.ops.hipserve.splitk_reduce(out, ws, S)
             return out
         off = 0
         for p in w.parts:  # v1: row-layout parts only

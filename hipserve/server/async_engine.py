@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import queue
 import threading
 import time
@@ -16,6 +17,16 @@ from ..engine.llm_engine import LLMEngine
 from ..engine.request import RequestOutput, SamplingParams
 
 log = logging.getLogger("hipserve.engine")
+
+# Idle-arrival coalescing: when requests arrive at an idle engine (nothing running or in
+# flight), the engine keeps admitting arrivals before its first step until they pause for
+# COALESCE_GAP, the waiting prompts fill one prefill step, or COALESCE_MAX has passed. A
+# burst of requests (OpenWebUI fan-out, the bench's closed-loop waves through three HTTP
+# hops: 64 arrivals over ~20 ms) otherwise starts with a one-request prefill step and
+# needs one prefill step more than its tokens fill (profiles/r6_burst_coalescing.md).
+# A lone request waits at most COALESCE_GAP. 0 disables.
+COALESCE_GAP = float(os.environ.get("HIPSERVE_COALESCE_GAP_MS", "2")) / 1000.0
+COALESCE_MAX = float(os.environ.get("HIPSERVE_COALESCE_MAX_MS", "10")) / 1000.0
 
 
 class EngineDeadError(RuntimeError):
@@ -66,7 +77,9 @@ class AsyncEngine:
         try:
             while not self._stop:
                 self.heartbeat = time.monotonic()
-                self._drain()
+                idle = not eng.has_unfinished()
+                if self._drain() and idle:
+                    self._coalesce()
                 if not eng.has_unfinished():
                     self._wake.wait(timeout=0.5)
                     self._wake.clear()
@@ -80,13 +93,36 @@ class AsyncEngine:
             log.error("engine loop died: %s", traceback.format_exc())
             self.loop.call_soon_threadsafe(self._fail_all, e)
 
-    def _drain(self):
+    def _coalesce(self):
+        """The engine was idle and requests arrived: admit further arrivals until they
+        pause for COALESCE_GAP, the waiting prompt tokens fill one prefill step, or
+        COALESCE_MAX has passed since the first."""
+        sch = self.engine.scheduler
+        if COALESCE_MAX <= 0 or COALESCE_GAP <= 0:
+            return
+        t0 = last = time.monotonic()
+        while not self._stop:
+            if sum(s.num_uncomputed for s in sch.waiting) >= sch.max_tokens:
+                return
+            now = time.monotonic()
+            left = min(COALESCE_GAP - (now - last), COALESCE_MAX - (now - t0))
+            if left <= 0:
+                return
+            self._wake.wait(timeout=left)
+            self._wake.clear()
+            if self._drain():
+                last = time.monotonic()
+
+    def _drain(self) -> int:
+        """Moves submitted requests / aborts into the engine; returns the requests added."""
+        added = 0
         while True:
             try:
                 kind, args = self._submit.get_nowait()
             except queue.Empty:
-                return
+                return added
             if kind == "add":
+                added += 1
                 rid, prompt, params, arrival = args
                 try:
                     self.engine.add_request(rid, prompt, params, arrival_time=arrival)

@@ -1,4 +1,4 @@
-# PMC passes: v2 (qgemm2) vs v3 (qgemm3) quantised decode GEMM, M=64 Q4_K gate|up, cold blocks
+# PMC passes: v2 (qgemm2) quantised decode GEMM, M=64 Q4_K gate|up, cold blocks
 set -o pipefail
 cd $GRAFT_REPO_ROOT; here=$PWD; OUT=$here/gpurun_out/pmcq3; mkdir -p $OUT
 i=0
@@ -6,7 +6,7 @@ for counters in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_A
                 "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
   i=$((i + 1))
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $counters --output-format csv -d $OUT/p$i -o run -- \
-     python3 $here/tools/bench_gguf.py --m 64 --only gate_up --v3 --cold --splits 1 > $OUT/p$i.log 2>&1) || { tail -5 $OUT/p$i.log; exit 1; }
+     python3 $here/tools/bench_gguf.py --m 64 --only gate_up --cold --splits 1 2 4 > $OUT/p$i.log 2>&1) || { tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 - <<'PY'
 import csv, glob, collections, os

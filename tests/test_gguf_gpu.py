@@ -594,79 +594,3 @@ def test_qgemm_m64_wide_body(qt, M):
     ws, S = quant_partial(x, qw)
     assert (ws.view(S, M, N).sum(0) - want).abs().max().item() < tol
 
-
-@pytest.mark.parametrize("qt", QTYPES + [G.Q4_1])
-@pytest.mark.parametrize("M", [1, 9, 16, 24, 33, 64])
-@pytest.mark.parametrize("NS", [1, 2, 4])
-def test_mfma_v3_formats(qt, M, NS):
-    """Decode GEMM v3 (qgemm3_kernel: a K slice of NS super-chunks staged once per
-    workgroup, per-wave 4-deep weight ring, no barrier in the stream) vs an fp32 matmul of
-    the numpy-decoded weights: every format, three parts of one weight (row groups walked
-    across part boundaries), the sum of every slice's fp32 partials."""
-    from hipserve.ops.quant import _launch_v2
-    K = 2048
-    qw, raws = _rand_qw([(qt, 512, K), (qt, 80, K), (qt, 272, K)], seed=M + 10 * NS)
-    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-    want = x.float() @ _dense(raws).T
-    tol = 1e-2 * want.abs().max().item() + 1e-3
-    nS = (K // 256) // NS
-    ws = torch.full((nS * M * qw.N,), float("nan"), dtype=torch.float32, device="cuda")
-    assert _launch_v2(torch.empty(0, dtype=torch.bfloat16, device="cuda"), ws, x, qw, -NS) == nS
-    got = ws.view(nS, M, qw.N).sum(0)
-    assert torch.isfinite(got).all()
-    assert (got - want).abs().max().item() < tol
-
-
-@pytest.mark.parametrize("M", [1, 16, 64])
-def test_mfma_v3_direct_bf16_and_mixed_formats(M):
-    """v3 on a Q4_K_M-style q|k|v (Q4_K parts + a Q6_K part: one launch per format into
-    one output), K = 1024 with NS = 4 (one slice: the kernel writes bf16 itself), and
-    through quant_linear / quant_partial when the split table picks v3."""
-    from hipserve.ops import quant as Q
-    K = 1024
-    qw, raws = _rand_qw([(G.Q4_K, 1024, K), (G.Q4_K, 256, K), (G.Q6_K, 256, K)], seed=M)
-    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-    want = x.float() @ _dense(raws).T
-    tol = 1e-2 * want.abs().max().item() + 1e-3
-    out = torch.full((M, qw.N), float("nan"), dtype=torch.bfloat16, device="cuda")
-    assert Q._launch_v2(out, torch.empty(0, dtype=torch.float32, device="cuda"), x, qw, -4) == 1
-    assert (out.float() - want).abs().max().item() < tol
-    key = (Q._sig(qw), Q._bucket(M))
-    old = Q.SPLIT_TABLE.get(key)
-    try:
-        Q.SPLIT_TABLE[key] = -2
-        y = quant_linear(x, qw).float()
-        ws, S = Q.quant_partial(x, qw)
-        assert S == 2 and ws.numel() == 2 * M * qw.N
-        assert (y - want).abs().max().item() < tol
-        assert (ws.view(S, M, qw.N).sum(0) - want).abs().max().item() < tol
-    finally:
-        if old is None:
-            Q.SPLIT_TABLE.pop(key, None)
-        else:
-            Q.SPLIT_TABLE[key] = old
-
-
-@pytest.mark.parametrize("qt", [G.Q4_K, G.Q6_K, G.Q8_0])
-@pytest.mark.parametrize("M", [1, 16, 64])
-def test_mfma_v3_beyond_f16_range(qt, M):
-    """v3 staging: rows past the f16 range are caught per workgroup (each K slice) and
-    restaged with power-of-two row pre-scales, undone exactly at the store."""
-    from hipserve.ops.quant import _launch_v2
-    K = 2048
-    qw, raws = _rand_qw([(qt, 512, K), (qt, 256, K)], seed=3 + M)
-    g = torch.Generator(device="cuda").manual_seed(M)
-    x = torch.randn(M, K, device="cuda", generator=g)
-    big = list(range(0, M, 3))
-    x[big] *= torch.logspace(5, 6.5, len(big), device="cuda").unsqueeze(1)
-    x[M // 2, 5] = 2.0e5
-    x = x.to(torch.bfloat16)
-    want = x.float() @ _dense(raws).T
-    rowmax = want.abs().amax(1, keepdim=True)
-    for NS in (2, 4):
-        nS = (K // 256) // NS
-        ws = torch.empty(nS * M * qw.N, dtype=torch.float32, device="cuda")
-        _launch_v2(torch.empty(0, dtype=torch.bfloat16, device="cuda"), ws, x, qw, -NS)
-        got = ws.view(nS, M, qw.N).sum(0)
-        assert torch.isfinite(got).all()
-        assert ((got - want).abs() / rowmax).max().item() < 1e-2

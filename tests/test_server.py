@@ -254,3 +254,61 @@ def test_asyncio_debug_mode_clean(caplog):
     bad = [r for r in caplog.records if r.name == "asyncio" and r.levelno >= logging.WARNING
            and "took" not in r.getMessage()]
     assert not bad, [r.getMessage() for r in bad]
+
+
+def test_idle_arrival_coalescing(monkeypatch):
+    """Requests that reach an idle engine a few ms apart start together: the loop keeps
+    admitting arrivals until they pause (COALESCE_GAP) or fill a prefill step, so the
+    first step is not a lone one-request prefill (profiles/r6_burst_coalescing.md)."""
+    import threading
+    import time
+
+    from hipserve.server import async_engine as AE
+
+    class Seq:
+        num_uncomputed = 100
+
+    class Sched:
+        def __init__(self):
+            self.waiting = []
+            self.max_tokens = 1000
+
+    class Eng:
+        def __init__(self):
+            self.scheduler = Sched()
+            self.steps = []
+
+        def has_unfinished(self):
+            return bool(self.scheduler.waiting)
+
+        def add_request(self, rid, prompt, params, arrival_time=None):
+            self.scheduler.waiting.append(Seq())
+
+        def step(self):
+            self.steps.append(len(self.scheduler.waiting))
+            self.scheduler.waiting.clear()
+            return []
+
+    monkeypatch.setattr(AE, "COALESCE_GAP", 0.05)
+    monkeypatch.setattr(AE, "COALESCE_MAX", 1.0)
+    eng = Eng()
+    ae = AE.AsyncEngine(eng)
+    ae.loop = None
+
+    def feed(n, gap):
+        for i in range(n):
+            ae._submit.put(("add", (str(i), [1], None, time.monotonic())))
+            ae._wake.set()
+            time.sleep(gap)
+
+    t = threading.Thread(target=ae._run, daemon=True)
+    t.start()
+    feed(5, 0.01)  # 5 arrivals 10 ms apart: one step of 5
+    time.sleep(0.3)
+    assert eng.steps == [5], eng.steps
+    feed(12, 0.005)  # 12 x 100 prompt tokens > the 1000-token budget: the step starts at 10
+    time.sleep(0.3)
+    assert eng.steps[1] == 10 and sum(eng.steps) == 17, eng.steps
+    ae._stop = True
+    ae._wake.set()
+    t.join(2)

@@ -69,7 +69,6 @@ def main():
                     help="M > 64: the prefill GEMM from the blocks (qpf) and the M-tiled dequant-MFMA kernel vs "
                          "dequant-to-scratch + hipBLASLt vs a bf16 shadow")
     ap.add_argument("--no-mtiled", action="store_true", help="--prefill: skip the (slow at large M) M-tiled kernel")
-    ap.add_argument("--v3", action="store_true", help="also the v3 decode GEMM (qgemm3_kernel) at NS = 1, 2, 4")
     ap.add_argument("--cold", action="store_true",
                     help="rotate every timed call over copies of the blocks (>= 768 MiB): HBM-cold weights, "
                          "as in a decode step, instead of MALL-resident ones")
@@ -142,13 +141,6 @@ def main():
             for Sx in sorted({-(-nsb // -(-nsb // S)) for S in (a.splits or (1, 2, 4, 8, 16, 32)) if S <= nsb}):
                 ws = torch.empty(Sx * M * qw.N, dtype=torch.float32, device="cuda")
                 rows.append((f"v2_S{Sx}", Sx, timed(lambda qs: Q._launch_v2(e, ws, x, qw, Sx, x16, qs))))
-            if a.v3 and M <= 64:
-                for ns in (1, 2, 4):
-                    if nsb % ns:
-                        continue
-                    Sx = nsb // ns
-                    ws = torch.empty(Sx * M * qw.N, dtype=torch.float32, device="cuda")
-                    rows.append((f"v3_NS{ns}", Sx, timed(lambda qs: Q._launch_v2(e, ws, x, qw, -ns, None, qs))))
             del copies
             for kern, S, us in rows:
                 print(json.dumps({"proj": name, "M": M, "kernel": kern, "splits": S, "us": round(us, 2),
