@@ -24,9 +24,10 @@ log = logging.getLogger("hipserve.engine")
 # burst of requests (OpenWebUI fan-out, the bench's closed-loop waves through three HTTP
 # hops: 64 arrivals over ~20 ms) otherwise starts with a one-request prefill step and
 # needs one prefill step more than its tokens fill (profiles/r6_burst_coalescing.md).
-# A lone request waits at most COALESCE_GAP. 0 disables.
-COALESCE_GAP = float(os.environ.get("HIPSERVE_COALESCE_GAP_MS", "2")) / 1000.0
-COALESCE_MAX = float(os.environ.get("HIPSERVE_COALESCE_MAX_MS", "10")) / 1000.0
+# A lone request waits at most COALESCE_GAP. 0 disables. (2 ms measured too short: a
+# burst's first request, on a kept-alive connection, leads the rest by several ms)
+COALESCE_GAP = float(os.environ.get("HIPSERVE_COALESCE_GAP_MS", "5")) / 1000.0
+COALESCE_MAX = float(os.environ.get("HIPSERVE_COALESCE_MAX_MS", "20")) / 1000.0
 
 
 class EngineDeadError(RuntimeError):
