@@ -287,8 +287,6 @@ struct StageCopyArgs {
   int n;
   unsigned int host_mask;
 };
-// read `bytes` at `p` once (16-byte loads, `blocks` workgroups) so the MALL holds them
-void launch_mall_prefetch(const void* p, long bytes, int blocks, hipStream_t s);
 void launch_stage_copy(const StageCopyArgs& a, hipStream_t s);
 
 }  // namespace hipserve

@@ -41,24 +41,5 @@ void launch_stage_copy(const StageCopyArgs& a, hipStream_t s) {
   stage_copy_kernel<<<dim3(bx, a.n), 256, 0, s>>>(a);
 }
 
-// MALL prefetch (Infinity Cache, 256 MiB memory-side cache): read `bytes` at `p` once so
-// the next kernel that streams them finds them in the MALL instead of HBM. Plain
-// 16-byte loads (cached), folded into one register that an empty asm statement keeps
-// live (so the loads are not dead code); nothing is written.
-__global__ __launch_bounds__(256) void mall_prefetch_kernel(const u32x4* __restrict__ p, long n16) {
-  unsigned acc = 0;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) {
-    const u32x4 v = p[i];
-    acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
-  }
-  asm volatile("" ::"v"(acc));
-}
-
-void launch_mall_prefetch(const void* p, long bytes, int blocks, hipStream_t s) {
-  const long n16 = bytes / 16;
-  if (n16 <= 0) return;
-  mall_prefetch_kernel<<<blocks, 256, 0, s>>>(static_cast<const u32x4*>(p), n16);
-}
-
 }  // namespace hipserve
 

@@ -642,15 +642,6 @@ void fill_uniform(at::Tensor& out, int64_t row0, int64_t col0, int64_t gcols, in
 // Pinned host tensors are addressed through their device mapping; every pair must
 // match in byte size (a multiple of 4) and be contiguous. Runs on `device`'s
 // current stream.
-// Read the first `nbytes` of t once (MALL prefetch for the kernel that streams t next).
-void mall_prefetch(const at::Tensor& t, int64_t nbytes, int64_t blocks) {
-  CHECK_DEV(t);
-  TORCH_CHECK(t.is_contiguous() && nbytes >= 0 && blocks >= 1, "mall_prefetch: contiguous tensor");
-  const long n = std::min<long>(nbytes, (long)t.nbytes()) & ~15L;
-  c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
-  hipserve::launch_mall_prefetch(t.data_ptr(), n, (int)blocks, cur_stream());
-}
-
 void stage_copy(const std::vector<at::Tensor>& dst, const std::vector<at::Tensor>& src, int64_t device) {
   TORCH_CHECK(dst.size() == src.size() && dst.size() <= (size_t)hipserve::kMaxStageCopies,
               "stage_copy: matching lists of at most 8 tensors");
@@ -1264,7 +1255,6 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("car_destroy(int state) -> ()", &car_destroy);
   m.def("fill_uniform(Tensor(a!) out, int row0, int col0, int gcols, int key, float scale) -> ()");
   m.def("stage_copy(Tensor(a!)[] dst, Tensor[] src, int device) -> ()", &stage_copy);
-  m.def("mall_prefetch(Tensor t, int nbytes, int blocks) -> ()", &mall_prefetch);
   m.def("decode_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor(b!) ws, int rt, int splits) -> ()");
   m.def("decode_gemm_packed(Tensor(a!) out, Tensor x, Tensor wp, Tensor(b!) ws, int N, int rt, int splits) -> ()");
   m.def("pack_decode_weight(Tensor(a!) out, Tensor w, bool glu=False) -> ()");
