@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--quantization", default=None, choices=["q4_k_m", "q8_0", "q4_0", "fp8", "int8"],
                     help="GGUF tier: random-init GGUF-quantised weights (BASELINE config: Llama-3-8B Q4_K_M)")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
+                    help="paged KV cache element (fp8: e4m3, per-tensor scale 1; not the BASELINE config)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: fp32 on the host with gloo collectives (tests of the DP / TP paths)")
@@ -327,6 +329,7 @@ def run_phase(args):
     dev = torch.device("cuda", local) if cuda else torch.device("cpu")
     cfg = EngineConfig(model=args.model, device=args.device, max_num_seqs=max(args.concurrency, 1),
                        dtype="bfloat16" if cuda else "float32", num_kv_blocks=args.num_kv_blocks,
+                       kv_cache_dtype=args.kv_cache_dtype,
                        tensor_parallel_size=args.tp,
                        max_num_batched_tokens=args.max_num_batched_tokens or default_batched_tokens(
                            args.model, quantization=args.quantization),
@@ -446,7 +449,8 @@ def run_phase(args):
         "dtype": ("bf16" if cuda else "fp32") if not args.quantization else (
             "bf16 activations, FP8 e4m3 weights (per-channel scales)" if args.quantization == "fp8"
             else "bf16 activations, INT8 weight-only (per-channel scales)" if args.quantization == "int8"
-            else f"bf16 activations, GGUF {args.quantization.upper()} weights"),
+            else f"bf16 activations, GGUF {args.quantization.upper()} weights")
+        + ("; fp8 e4m3 KV cache" if args.kv_cache_dtype == "fp8" else ""),
         "data": "synthetic prompts (random token ids), random-init weights",
         "p50_ttft_ms": round(1000 * float(p50), 2),
         "load": f"open-loop Poisson {args.request_rate} req/s" if args.request_rate else "closed-loop waves",
@@ -464,6 +468,7 @@ def run_phase(args):
             "parallelism": f"tp{args.tp}" if tp_mode else (f"dp{world}" if world > 1 else "tp1"),
             "sampling": {"temperature": args.temperature, "top_p": args.top_p},
             "prefill_tokens_per_step": cfg.max_num_batched_tokens,
+            **({"kv_cache_dtype": "fp8_e4m3"} if args.kv_cache_dtype == "fp8" else {}),
         },
         "engine_init_s": round(init_s, 1),
         "init_breakdown_s": getattr(engine.runner, "init_times", {}),

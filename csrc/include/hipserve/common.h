@@ -92,6 +92,55 @@ HS_DEVICE uint2 e4m3_8(const u16x8 o, float inv) {
   return r;
 }
 
+// ---- paged KV cache elements: bf16 (unsigned short) or OCP e4m3 (unsigned char) ----
+// The e4m3 cache (--kv-cache-dtype fp8) holds K / V with a per-tensor scale of 1 (vLLM's
+// fp8 KV cache without calibrated scales): writers round the bf16 value to e4m3 (RNE,
+// saturated to +-448), readers widen e4m3 -> bf16 exactly (v_cvt_scalef32_pk_bf16_fp8),
+// so attention math is unchanged and only the stored K / V lose precision.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+template <typename KV> struct KvVec;  // 8 cache elements in registers
+template <> struct KvVec<unsigned short> { using T = u16x8; };
+template <> struct KvVec<unsigned char> { using T = u32x2; };
+
+HS_DEVICE u16x8 kv_widen8(const u16x8 v) { return v; }
+// two e4m3 in the low 16 bits of w -> two bf16 (exact). The high pair goes through a shift
+// rather than the instruction's word select: with op_sel the paged decode kernel read wrong
+// keys on the GPU although a standalone probe of the same builtin matched (round 6)
+HS_DEVICE unsigned kv_widen2(unsigned w) {
+  return __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.f, false));
+}
+HS_DEVICE u16x8 kv_widen8(const u32x2 v) {
+  const u32x4 r{kv_widen2(v[0]), kv_widen2(v[0] >> 16), kv_widen2(v[1]), kv_widen2(v[1] >> 16)};
+  return __builtin_bit_cast(u16x8, r);
+}
+// 4 elements (the v1 prefill attention's V^T runs)
+HS_DEVICE u16x4 kv_widen4(const u16x4 v) { return v; }
+HS_DEVICE u16x4 kv_widen4(const unsigned v) {
+  const u32x2 r{kv_widen2(v), kv_widen2(v >> 16)};
+  return __builtin_bit_cast(u16x4, r);
+}
+HS_DEVICE unsigned char e4m3_1(unsigned short bf) {
+  const float f = __builtin_amdgcn_fmed3f(bf16_to_f32(bf), -448.f, 448.f);
+  return (unsigned char)((unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(f, 0.f, 0, false) & 0xff);
+}
+// 8 consecutive elements (16-byte bf16 / 8-byte e4m3 store)
+HS_DEVICE void kv_store8(unsigned short* p, const u16x8 v) { *reinterpret_cast<u16x8*>(p) = v; }
+HS_DEVICE void kv_store8(unsigned char* p, const u16x8 v) {
+  const uint2 r = e4m3_8(v, 1.f);
+  *reinterpret_cast<u32x2*>(p) = u32x2{r.x, r.y};
+}
+HS_DEVICE void kv_store1(unsigned short* p, unsigned short bf) { *p = bf; }
+HS_DEVICE void kv_store1(unsigned char* p, unsigned short bf) { *p = e4m3_1(bf); }
+template <typename KV>
+HS_DEVICE typename KvVec<KV>::T kv_load8(const KV* p) {
+  return *reinterpret_cast<const typename KvVec<KV>::T*>(p);
+}
+template <typename KV>
+HS_DEVICE typename KvVec<KV>::T kv_load8_nt(const KV* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const typename KvVec<KV>::T*>(p));
+}
+
 template <int VPT, int NT>
 HS_DEVICE void row_e4m3(const u16x8 (&ov)[VPT], int nvec, int row, int N, unsigned char* __restrict__ out8,
                         float* __restrict__ xs8, float* scratch) {

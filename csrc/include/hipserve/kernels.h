@@ -10,7 +10,7 @@ namespace hipserve {
 // norm.hip — residual != nullptr selects the fused add (residual updated in place)
 void launch_embed_rmsnorm(void* out, void* residual, const void* table, const long* ids, const long* src,
                           const long* tok, const void* w, bool weight_f32, int rows, int hidden, float eps,
-                          hipStream_t s);
+                          hipStream_t s, float scale = 1.f, void* out8 = nullptr, float* xs8 = nullptr);
 // out8 / xs8 (optional): out also as per-token e4m3 + row scale (= act_quant_fp8 of out)
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                     bool weight_f32, int rows, int hidden, long x_stride,
@@ -29,7 +29,7 @@ void launch_gelu_and_mul(void* out, const void* in, long rows, int inter,
 void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
                        const long* slots, const float* cos_sin, void* k_cache,
                        void* v_cache, int T, int nq, int nkv, int D,
-                       int block_size, int mode, hipStream_t s);
+                       int block_size, int mode, hipStream_t s, bool kv_f8 = false);
 
 // attention_decode.hip
 size_t paged_decode_smem_bytes(int D);
@@ -46,7 +46,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
                          const int* context_lens, float* tmp_out, float* tmp_ml,
                          int B, int nq, int nkv, int D, int block_size,
                          int part_size, int max_parts, float scale, int window,
-                         hipStream_t s, void* out16 = nullptr);
+                         hipStream_t s, void* out16 = nullptr, bool kv_f8 = false);
 
 // attention_prefill.hip — window > 0: sliding-window attention (keys within
 // window - 1 positions before the query), 0 = full causal
@@ -55,7 +55,7 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               const void* v_cache, const int* block_tables,
                               int bt_stride, const int* cu_q, const int* ctx_lens,
                               const int* tiles, int ntiles, int nq, int nkv, int D,
-                              int block_size, float scale, int window, hipStream_t s);
+                              int block_size, float scale, int window, hipStream_t s, bool kv_f8 = false);
 
 // sampling.hip
 // ws: fp32 workspace of sample_workspace_floats(rows, V) for the multi-CU path
@@ -245,7 +245,8 @@ void launch_splitk_glu(void* act, long act_stride, const float* ws, int S, int M
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
                               const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
                               int nkv, int D, int block_size, int mode, hipStream_t s, const void* bias = nullptr,
-                              const float* qw = nullptr, const float* kw = nullptr, float eps = 1e-6f);
+                              const float* qw = nullptr, const float* kw = nullptr, float eps = 1e-6f,
+                              bool kv_f8 = false);
 void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu, hipStream_t s, int batch = 1);
 }  // namespace hipserve
 

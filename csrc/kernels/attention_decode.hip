@@ -68,17 +68,20 @@ HS_DEVICE void qkv_sum8(float (&o)[8], const float* p, long slice, int S) {
 
 // two register sets for the chunk pipeline: keep VGPR + AGPR <= 256 so two waves fit
 // per SIMD (two 4-wave workgroups per CU — B = 64 x 8 kv heads is 2 per CU)
-template <int D, int kDecWaves, bool kQKV = false, bool kNT = true>
+// KV: the cache element, bf16 (unsigned short) or e4m3 (unsigned char, widened to bf16
+// in registers right before its MFMA: half the HBM bytes of the memory-bound stream)
+template <int D, int kDecWaves, bool kQKV = false, bool kNT = true, typename KV = unsigned short>
 __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(2, 8))) void paged_decode_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const unsigned short* __restrict__ q, long q_stride,
-    const unsigned short* __restrict__ k_cache,
-    const unsigned short* __restrict__ v_cache,
+    const KV* __restrict__ k_cache,
+    const KV* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, int nq, int nkv, int block_size, int part_size,
     int max_parts, float scale, int window, QkvIn qi = QkvIn{}, unsigned short* __restrict__ out16 = nullptr) {
   static_assert(D == 128 || D == 96 || D == 64, "head_dim 64, 96 or 128");
+  static_assert(!kQKV || sizeof(KV) == 2, "the fused qkv decode writes a bf16 cache");
   constexpr int KS = D / 32;  // k-steps of the QK MFMA
   constexpr int NB = D / 16;  // 16-column blocks of the PV output
   const int part = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
@@ -117,14 +120,15 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   // register sets used alternately (loop unrolled by 2, no exit inside a pair, loads
   // unconditional with the chunk index clamped), so each chunk's HBM latency hides
   // behind the previous chunk's math instead of being exposed once per chunk.
+  using KV8 = typename KvVec<KV>::T;
   struct Chunk {
-    u16x8 ka[KS], kb[KS], vv[NB];
+    KV8 ka[KS], kb[KS], vv[NB];
   };
   // K / V are read exactly once per step by one wave: non-temporal loads (aux nt) keep
   // them from evicting the weights' and partials' lines and shorten issue -> landed
-  auto ld = [](const unsigned short* p) -> u16x8 {
-    if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
-    else return *reinterpret_cast<const u16x8*>(p);
+  auto ld = [](const KV* p) -> KV8 {
+    if constexpr (kNT) return kv_load8_nt(p);
+    else return kv_load8(p);
   };
   auto load_chunk = [&](int c, Chunk& ch) {
     const int cs = start + min(c, nchunks - 1) * kChunk;
@@ -134,10 +138,10 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     int tb = ta + 4;
     ta = min(ta, last_tok);
     tb = min(tb, last_tok);
-    const unsigned short* ka = k_cache +
+    const KV* ka = k_cache +
         ((long)bt[(ta - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
         (long)(ta & bmask) * D + 8 * grp;
-    const unsigned short* kb = k_cache +
+    const KV* kb = k_cache +
         ((long)bt[(tb - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
         (long)(tb & bmask) * D + 8 * grp;
 #pragma unroll
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     // V: lane holds V^T[d = 16n + col][tokens 8*grp .. +7]
     int tv = cs + 8 * grp;
     if (tv > last_tok) tv = last_tok & ~7;
-    const unsigned short* vb = v_cache +
+    const KV* vb = v_cache +
         ((long)bt[(tv - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
         (tv & bmask) + (long)col * block_size;
 #pragma unroll
@@ -303,8 +307,8 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ch.ka[ks]), qf[ks], sa, 0, 0, 0);
-      sb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ch.kb[ks]), qf[ks], sb, 0, 0, 0);
+      sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv_widen8(ch.ka[ks])), qf[ks], sa, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv_widen8(ch.kb[ks])), qf[ks], sb, 0, 0, 0);
     }
     // lane holds scores of tokens cs + 8*grp + r (sa) and + 4 + r (sb) for head col
     float sc[8];
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     // ---- O += P . V
 #pragma unroll
     for (int n = 0; n < NB; ++n)
-      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, ch.vv[n]), o[n], 0, 0, 0);
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, kv_widen8(ch.vv[n])), o[n], 0, 0, 0);
   };
   constexpr int W = kDecWaves;
   int c = wave;
@@ -506,7 +510,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
                          const int* context_lens, float* tmp_out, float* tmp_ml,
                          int B, int nq, int nkv, int D, int block_size,
                          int part_size, int max_parts, float scale, int window,
-                         hipStream_t s, void* out16) {
+                         hipStream_t s, void* out16, bool kv_f8) {
   if (B <= 0) return;
   auto* o16 = static_cast<unsigned short*>(out16);
   const int waves = decode_waves();
@@ -516,16 +520,23 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
   auto* qq = static_cast<const unsigned short*>(q);
   auto* kc = static_cast<const unsigned short*>(k_cache);
   auto* vc = static_cast<const unsigned short*>(v_cache);
-#define HS_DECODE(DD, WW)                                                                                   \
+  auto* kc8 = static_cast<const unsigned char*>(k_cache);
+  auto* vc8 = static_cast<const unsigned char*>(v_cache);
+#define HS_DECODE_KV(DD, WW, NT)                                                                              \
   do {                                                                                                      \
-    if (decode_nt((long)max_parts * nkv * B))                                                               \
-      paged_decode_kernel<DD, WW, false, true><<<grid, block, smem, s>>>(                                   \
-          o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq,  \
+    if (kv_f8)                                                                                              \
+      paged_decode_kernel<DD, WW, false, NT, unsigned char><<<grid, block, smem, s>>>(                      \
+          o, out_stride, qq, q_stride, kc8, vc8, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq, \
           nkv, block_size, part_size, max_parts, scale, window, QkvIn{}, o16);                              \
     else                                                                                                    \
-      paged_decode_kernel<DD, WW, false, false><<<grid, block, smem, s>>>(                                  \
+      paged_decode_kernel<DD, WW, false, NT><<<grid, block, smem, s>>>(                                     \
           o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, context_lens, tmp_out, tmp_ml, nq,  \
           nkv, block_size, part_size, max_parts, scale, window, QkvIn{}, o16);                              \
+  } while (0)
+#define HS_DECODE(DD, WW)                                                                                   \
+  do {                                                                                                      \
+    if (decode_nt((long)max_parts * nkv * B)) HS_DECODE_KV(DD, WW, true);                                   \
+    else HS_DECODE_KV(DD, WW, false);                                                                       \
   } while (0)
 #define HS_DECODE_D(DD)                                                                                      \
   do {                                                                                                      \
@@ -541,6 +552,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
   else HS_DECODE_D(64);
 #undef HS_DECODE_D
 #undef HS_DECODE
+#undef HS_DECODE_KV
 }
 
 // Fused decode: qkv partials -> RoPE + KV write + attention (see QkvIn). D in {64, 128}.

@@ -17,6 +17,8 @@
 //  * online softmax in the log2 domain.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "hipserve/common.h"
 #include "hipserve/kernels.h"
 
@@ -38,12 +40,12 @@ HS_DEVICE float xor32_sum(float v) {
 
 typedef unsigned short u16x4v __attribute__((ext_vector_type(4)));
 
-template <int D>
+template <int D, typename KV>
 __global__ __launch_bounds__(256) void prefill_attn_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const unsigned short* __restrict__ q, long q_stride,
-    const unsigned short* __restrict__ k_cache,
-    const unsigned short* __restrict__ v_cache,
+    const KV* __restrict__ k_cache,
+    const KV* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ tiles, int nq, int nkv, int block_size,
@@ -88,12 +90,12 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     const int kbase = kt * 32;
     // K fragment rows: key kbase + qi (clamped into the valid context)
     const int key = min(kbase + qi, ctx - 1);
-    const unsigned short* kp = k_cache +
+    const KV* kp = k_cache +
         ((long)btab[key / block_size] * nkv + kh) * head_stride +
         (long)(key % block_size) * D + 8 * half;
     u16x8 kf[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const u16x8*>(kp + 16 * ks);
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = kv_widen8(kv_load8(kp + 16 * ks));
     // V^T fragments: row d = 32*nb + qi; k-slot j of half h, step s ->
     // key kbase + 16s + 8(j>>2) + 4h + (j&3): two runs of 4 contiguous tokens.
     u16x4v vf[NB][2][2];
@@ -103,12 +105,13 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
       for (int run = 0; run < 2; ++run) {
         int k4 = kbase + 16 * s + 8 * run + 4 * half;
         if (k4 > ctx - 1) k4 = (ctx - 1) & ~3;
-        const unsigned short* vp = v_cache +
+        const KV* vp = v_cache +
             ((long)btab[k4 / block_size] * nkv + kh) * head_stride + (k4 % block_size) +
             (long)qi * block_size;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
-          vf[nb][s][run] = *reinterpret_cast<const u16x4v*>(vp + (long)32 * nb * block_size);
+          vf[nb][s][run] = kv_widen4(*reinterpret_cast<const std::conditional_t<sizeof(KV) == 2, u16x4v, unsigned>*>(
+              vp + (long)32 * nb * block_size));
       }
 
     f32x16 st;
@@ -199,10 +202,12 @@ constexpr int PA2_KT = 64, PA2_KLD = 128 + 8, PA2_VLD = 64 + 8;
 // (A stagger — waves 4-7 issuing each tile's P.V one tile late, a third LDS buffer holding
 // its V^T, MI355X_MICROARCH.md "Two waves per SIMD" item 9 — needed 16 more VGPRs than the
 // 256 of two waves per SIMD and spilled: 1.4-1.5x slower, profiles/r5_prefill_attn_bench.log.)
-template <int HG, int NWV>
+// KV: cache element, bf16 or e4m3; e4m3 pieces (8 bytes) are widened to bf16 on their way
+// into the LDS ring, so the MFMA / softmax body is the same for both
+template <int HG, int NWV, typename KV>
 __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
     unsigned short* __restrict__ out, long out_stride, const unsigned short* __restrict__ q, long q_stride,
-    const unsigned short* __restrict__ k_cache, const unsigned short* __restrict__ v_cache,
+    const KV* __restrict__ k_cache, const KV* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ cu_q,
     const int* __restrict__ ctx_lens, const int* __restrict__ tiles, int nq, int nkv, int block_size,
     float scale, int window, int prio) {
@@ -254,40 +259,39 @@ __global__ __launch_bounds__(64 * NWV) void prefill_attn_v2_kernel(
 
   // staging: NP K pieces + NP V^T pieces of 16 B per thread per tile
   // two register sets: tile kt+2 loads while tile kt+1's registers wait for their LDS write
-  u16x8 ska[NP], sva[NP], skb[NP], svb[NP];
+  using KV8 = typename KvVec<KV>::T;
+  KV8 ska[NP], sva[NP], skb[NP], svb[NP];
   // staging addresses: block id x the elements of one block of all kv heads (< 2^32: one
   // 32 x 32 -> 64-bit multiply-add per piece) + a 32-bit in-block offset; the kv head's
   // base is folded into the workgroup's K / V pointers
   const unsigned blk_elems = (unsigned)(nkv * hstride);
-  const unsigned short* kc_h = k_cache + (long)kh * hstride;
-  const unsigned short* vc_h = v_cache + (long)kh * hstride;
-  auto stage_load = [&](u16x8(&sk)[NP], u16x8(&sv)[NP], int kt) {
+  const KV* kc_h = k_cache + (long)kh * hstride;
+  const KV* vc_h = v_cache + (long)kh * hstride;
+  auto stage_load = [&](KV8(&sk)[NP], KV8(&sv)[NP], int kt) {
     const int kbase = kt * PA2_KT;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int p = tid + NT * i;
       const int key = min(kbase + (p >> 4), ctx - 1);
       const unsigned kid = (unsigned)bts[(key >> bsh) - blk_lo];
-      sk[i] = *reinterpret_cast<const u16x8*>(kc_h + ((unsigned long)kid * blk_elems +
-                                                      (unsigned)((key & bmask) * D + (p & 15) * 8)));
+      sk[i] = kv_load8(kc_h + ((unsigned long)kid * blk_elems + (unsigned)((key & bmask) * D + (p & 15) * 8)));
       // V^T: 16-key group sc, row d, 8-key half: one block's [D][16] chunk per 256 threads
       const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
       int vkey = kbase + 16 * sc + 8 * k8;
       if (vkey > ctx - 1) vkey = (ctx - 1) & ~7;
       const unsigned vid = (unsigned)bts[(vkey >> bsh) - blk_lo];
-      sv[i] = *reinterpret_cast<const u16x8*>(vc_h + ((unsigned long)vid * blk_elems +
-                                                      (unsigned)(d * block_size + (vkey & bmask))));
+      sv[i] = kv_load8(vc_h + ((unsigned long)vid * blk_elems + (unsigned)(d * block_size + (vkey & bmask))));
     }
   };
-  auto stage_store = [&](const u16x8(&sk)[NP], const u16x8(&sv)[NP], int buf) {
+  auto stage_store = [&](const KV8(&sk)[NP], const KV8(&sv)[NP], int buf) {
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int p = tid + NT * i;
       const int kk = p >> 4;
       const int krow = (kk & ~12) | ((kk & 4) << 1) | ((kk & 8) >> 1);  // swap key bits 2 and 3
-      *reinterpret_cast<u16x8*>(&kl[buf][krow * PA2_KLD + (p & 15) * 8]) = sk[i];
+      *reinterpret_cast<u16x8*>(&kl[buf][krow * PA2_KLD + (p & 15) * 8]) = kv_widen8(sk[i]);
       const int sc = p >> 8, d = (p >> 1) & 127, k8 = p & 1;
-      *reinterpret_cast<u16x8*>(&vl[buf][d * PA2_VLD + 16 * sc + 8 * k8]) = sv[i];
+      *reinterpret_cast<u16x8*>(&vl[buf][d * PA2_VLD + 16 * sc + 8 * k8]) = kv_widen8(sv[i]);
     }
   };
 
@@ -448,7 +452,7 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
                               const void* v_cache, const int* block_tables,
                               int bt_stride, const int* cu_q, const int* ctx_lens,
                               const int* tiles, int ntiles, int nq, int nkv, int D,
-                              int block_size, float scale, int window, hipStream_t s) {
+                              int block_size, float scale, int window, hipStream_t s, bool kv_f8) {
   if (ntiles <= 0) return;
   const int G = nq / nkv;
   // v2 keeps the sequence's block ids in LDS next to its 70 KiB K / V ring (160 KiB per CU)
@@ -470,18 +474,26 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
     auto* q2 = static_cast<const unsigned short*>(q);
     auto* k2 = static_cast<const unsigned short*>(k_cache);
     auto* v2 = static_cast<const unsigned short*>(v_cache);
+    auto* k28 = static_cast<const unsigned char*>(k_cache);
+    auto* v28 = static_cast<const unsigned char*>(v_cache);
     // block ids of one sequence (the per-workgroup key range is at most this) in dynamic LDS
     const size_t bt_lds = (size_t)bt_stride * sizeof(int);
-#define PA2_LAUNCH(hg, nw)                                                                                  \
+#define PA2_LAUNCH_KV(hg, nw, KVT, KP, VP)                                                                   \
   do {                                                                                                      \
     static bool attr = [] { /* static 70 KiB + the block ids: above the 64 KiB default (160 KiB per CU) */ \
-      return hipFuncSetAttribute(reinterpret_cast<const void*>(&prefill_attn_v2_kernel<hg, nw>),            \
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&prefill_attn_v2_kernel<hg, nw, KVT>),       \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;      \
     }();                                                                                                    \
     (void)attr;                                                                                             \
-    prefill_attn_v2_kernel<hg, nw><<<g2, 64 * nw, bt_lds, s>>>(o2, out_stride, q2, q_stride, k2, v2,         \
-                                                               block_tables, bt_stride, cu_q, ctx_lens, tiles,  \
-                                                               nq, nkv, block_size, scale, window, prio);     \
+    prefill_attn_v2_kernel<hg, nw, KVT><<<g2, 64 * nw, bt_lds, s>>>(o2, out_stride, q2, q_stride, KP, VP,    \
+                                                                    block_tables, bt_stride, cu_q, ctx_lens, \
+                                                                    tiles, nq, nkv, block_size, scale, window, \
+                                                                    prio);                                  \
+  } while (0)
+#define PA2_LAUNCH(hg, nw)                                                                                  \
+  do {                                                                                                      \
+    if (kv_f8) PA2_LAUNCH_KV(hg, nw, unsigned char, k28, v28);                                             \
+    else PA2_LAUNCH_KV(hg, nw, unsigned short, k2, v2);                                                     \
   } while (0)
     if (nwv == 8) {
       if (HG == 8) PA2_LAUNCH(8, 8);
@@ -492,6 +504,7 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
       else PA2_LAUNCH(2, 4);
     }
 #undef PA2_LAUNCH
+#undef PA2_LAUNCH_KV
     return;
   }
   dim3 grid(ntiles, nq), block(256);
@@ -500,8 +513,17 @@ void launch_prefill_attention(void* out, long out_stride, const void* q,
   auto* kc = static_cast<const unsigned short*>(k_cache);
   auto* vc = static_cast<const unsigned short*>(v_cache);
 #define PA1_LAUNCH(dd)                                                                                          \
-  prefill_attn_kernel<dd><<<grid, block, 0, s>>>(o, out_stride, qq, q_stride, kc, vc, block_tables, bt_stride, cu_q, \
-                                                 ctx_lens, tiles, nq, nkv, block_size, scale, window)
+  do {                                                                                                          \
+    if (kv_f8)                                                                                                  \
+      prefill_attn_kernel<dd, unsigned char><<<grid, block, 0, s>>>(                                            \
+          o, out_stride, qq, q_stride, static_cast<const unsigned char*>(k_cache),                              \
+          static_cast<const unsigned char*>(v_cache), block_tables, bt_stride, cu_q, ctx_lens, tiles, nq, nkv,  \
+          block_size, scale, window);                                                                           \
+    else                                                                                                        \
+      prefill_attn_kernel<dd, unsigned short><<<grid, block, 0, s>>>(o, out_stride, qq, q_stride, kc, vc,        \
+                                                                     block_tables, bt_stride, cu_q, ctx_lens,   \
+                                                                     tiles, nq, nkv, block_size, scale, window); \
+  } while (0)
   if (D == 128) PA1_LAUNCH(128);
   else if (D == 96) PA1_LAUNCH(96);
   else PA1_LAUNCH(64);

@@ -278,11 +278,11 @@ void launch_splitk_post_add_rmsnorm(void* out, void* residual, const float* ws, 
 // again) and per-head q/k RMSNorm (Qwen3: fp32 weights [D]; a head's lanes are
 // consecutive, its sum of squares is reduced in qk_rmsnorm_vec_kernel's order: each
 // lane's two chunks (d and d + D/2) are the kernel's first xor pair, then xor 4, 2, 1).
-template <int kMode, bool kNorm>
+template <int kMode, bool kNorm, typename KV>
 __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
     unsigned short* __restrict__ qkv, long qkv_stride, const float* __restrict__ ws, int S,
     const long* __restrict__ positions, const long* __restrict__ slots, const float* __restrict__ cos_sin,
-    unsigned short* __restrict__ k_cache, unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D,
+    KV* __restrict__ k_cache, KV* __restrict__ v_cache, int T, int nq, int nkv, int D,
     int block_size, const unsigned short* __restrict__ bias, const float* __restrict__ qw,
     const float* __restrict__ kw, float eps) {
   const int t = blockIdx.x;
@@ -308,9 +308,9 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
     float x[8];
     sum8_bf16(x, wrow + (nq + nkv) * D + kh * D + c * 8, slice, S);
     if (bias != nullptr) add_bias8(x, bias + (nq + nkv) * D + kh * D + c * 8);
-    unsigned short* vc = v_cache + (blk * nkv + kh) * (long)D * block_size + off;
+    KV* vc = v_cache + (blk * nkv + kh) * (long)D * block_size + off;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vc[(c * 8 + j) * block_size] = f32_to_bf16(x[j]);
+    for (int j = 0; j < 8; ++j) kv_store1(vc + (c * 8 + j) * block_size, f32_to_bf16(x[j]));
     return;
   }
   const int h = it / qk_chunks, c = it % qk_chunks;
@@ -348,10 +348,14 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
       va[j] = f32_to_bf16(ra);
       vb[j] = f32_to_bf16(rb);
     }
-    unsigned short* dst = h < nq ? row + h * D
-                                 : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
-    *reinterpret_cast<u16x8*>(dst + c * 8) = va;
-    *reinterpret_cast<u16x8*>(dst + half + c * 8) = vb;
+    if (h < nq) {
+      *reinterpret_cast<u16x8*>(row + h * D + c * 8) = va;
+      *reinterpret_cast<u16x8*>(row + h * D + half + c * 8) = vb;
+    } else {
+      KV* dst = k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
+      kv_store8(dst + c * 8, va);
+      kv_store8(dst + half + c * 8, vb);
+    }
   } else {
     float x[8];
     sum8_bf16(x, wrow + h * D + c * 8, slice, S);
@@ -366,33 +370,45 @@ __global__ __launch_bounds__(64) void splitk_rope_cache_kernel(
       v[2 * p] = f32_to_bf16(ra);
       v[2 * p + 1] = f32_to_bf16(rb);
     }
-    unsigned short* dst = h < nq ? row + h * D
-                                 : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
-    *reinterpret_cast<u16x8*>(dst + c * 8) = v;
+    if (h < nq) *reinterpret_cast<u16x8*>(row + h * D + c * 8) = v;
+    else kv_store8(k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D + c * 8, v);
   }
+}
+
+template <typename KV>
+static void splitk_rope_cache_t(unsigned short* q, long qkv_stride, const float* ws, int S, const long* positions,
+                                const long* slots, const float* cos_sin, KV* kc, KV* vc, int T, int nq, int nkv,
+                                int D, int block_size, int mode, hipStream_t s, const unsigned short* b,
+                                const float* qw, const float* kw, float eps) {
+  const int qk_chunks = mode == 0 ? D / 16 : D / 8;
+  const int items = (nq + nkv) * qk_chunks + nkv * (D / 8);
+  const dim3 grid(T, (items + 63) / 64);
+  if (mode == 0 && qw != nullptr)
+    splitk_rope_cache_kernel<0, true, KV><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc,
+                                                               vc, T, nq, nkv, D, block_size, b, qw, kw, eps);
+  else if (mode == 0)
+    splitk_rope_cache_kernel<0, false, KV><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc,
+                                                                vc, T, nq, nkv, D, block_size, b, nullptr, nullptr,
+                                                                eps);
+  else
+    splitk_rope_cache_kernel<1, false, KV><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc,
+                                                                vc, T, nq, nkv, D, block_size, b, nullptr, nullptr,
+                                                                eps);
 }
 
 void launch_splitk_rope_cache(void* qkv, long qkv_stride, const float* ws, int S, const long* positions,
                               const long* slots, const float* cos_sin, void* k_cache, void* v_cache, int T, int nq,
                               int nkv, int D, int block_size, int mode, hipStream_t s, const void* bias,
-                              const float* qw, const float* kw, float eps) {
+                              const float* qw, const float* kw, float eps, bool kv_f8) {
   if (T <= 0) return;
   auto* q = static_cast<unsigned short*>(qkv);
-  auto* kc = static_cast<unsigned short*>(k_cache);
-  auto* vc = static_cast<unsigned short*>(v_cache);
   auto* b = static_cast<const unsigned short*>(bias);
-  const int qk_chunks = mode == 0 ? D / 16 : D / 8;
-  const int items = (nq + nkv) * qk_chunks + nkv * (D / 8);
-  const dim3 grid(T, (items + 63) / 64);
-  if (mode == 0 && qw != nullptr)
-    splitk_rope_cache_kernel<0, true><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc, T,
-                                                           nq, nkv, D, block_size, b, qw, kw, eps);
-  else if (mode == 0)
-    splitk_rope_cache_kernel<0, false><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc,
-                                                            T, nq, nkv, D, block_size, b, nullptr, nullptr, eps);
+  if (kv_f8)
+    splitk_rope_cache_t(q, qkv_stride, ws, S, positions, slots, cos_sin, static_cast<unsigned char*>(k_cache),
+                        static_cast<unsigned char*>(v_cache), T, nq, nkv, D, block_size, mode, s, b, qw, kw, eps);
   else
-    splitk_rope_cache_kernel<1, false><<<grid, 64, 0, s>>>(q, qkv_stride, ws, S, positions, slots, cos_sin, kc, vc,
-                                                            T, nq, nkv, D, block_size, b, nullptr, nullptr, eps);
+    splitk_rope_cache_t(q, qkv_stride, ws, S, positions, slots, cos_sin, static_cast<unsigned short*>(k_cache),
+                        static_cast<unsigned short*>(v_cache), T, nq, nkv, D, block_size, mode, s, b, qw, kw, eps);
 }
 
 // GLU over the split-K partials of a merged [gate | up] projection in the plain

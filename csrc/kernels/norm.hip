@@ -18,12 +18,14 @@ struct GatherIds {
   const long* ids;
   const long* src;
   const long* tok;
+  float scale;  // embedding multiplier (Gemma: sqrt(hidden) rounded to bf16), 1 = none
 };
 
-// kGather: x is the embedding table, row r reads table row id(r) (GatherIds) and
-// also writes that raw row to `residual` (the layer-0 residual stream): one kernel
-// instead of the id select + embedding gather + residual copy + RMSNorm chain, with
-// the same per-row arithmetic as the plain RMSNorm (bit-identical output).
+// kGather: x is the embedding table, row r reads table row id(r) (GatherIds), scales
+// it by gi.scale (bf16(row * scale), as a bf16 tensor times a float scalar rounds) and
+// also writes that row to `residual` (the layer-0 residual stream): one kernel
+// instead of the id select + embedding gather + scale + residual copy + RMSNorm chain,
+// with the same per-row arithmetic as the plain RMSNorm (bit-identical output).
 template <int NT, int VPT, bool kAdd, bool kWF32, bool kGather = false>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     unsigned short* __restrict__ out, unsigned short* __restrict__ residual,
@@ -59,9 +61,15 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
         }
         rr[idx] = s;
       } else {
+        if constexpr (kGather) {
+          if (gi.scale != 1.f) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = f32_to_bf16(bf16_to_f32(a[j]) * gi.scale);
+          }
+          rr[idx] = a;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] = bf16_to_f32(a[j]);
-        if constexpr (kGather) rr[idx] = a;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
@@ -209,35 +217,37 @@ void launch_qk_rmsnorm(void* qkv, long stride, const float* qw, const float* kw,
 
 template <bool kWF32>
 static void launch_embed_rmsnorm_t(unsigned short* out, unsigned short* residual, const unsigned short* table,
-                                   const void* w, int rows, int hidden, float eps, GatherIds gi, hipStream_t s) {
+                                   const void* w, int rows, int hidden, float eps, GatherIds gi, hipStream_t s,
+                                   unsigned char* o8, float* x8) {
   const int nvec = hidden / 8;
   dim3 grid(rows);
   const long xs = hidden;
   if (norm_threads(hidden) == 256) {
     if (nvec <= 256)
-      rmsnorm_kernel<256, 1, false, kWF32, true><<<grid, 256, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+      rmsnorm_kernel<256, 1, false, kWF32, true><<<grid, 256, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi, o8, x8);
     else
-      rmsnorm_kernel<256, 2, false, kWF32, true><<<grid, 256, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+      rmsnorm_kernel<256, 2, false, kWF32, true><<<grid, 256, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi, o8, x8);
   } else {
     if (nvec <= 512)
-      rmsnorm_kernel<512, 1, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+      rmsnorm_kernel<512, 1, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi, o8, x8);
     else if (nvec <= 1024)
-      rmsnorm_kernel<512, 2, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+      rmsnorm_kernel<512, 2, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi, o8, x8);
     else
-      rmsnorm_kernel<512, 4, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi);
+      rmsnorm_kernel<512, 4, false, kWF32, true><<<grid, 512, 0, s>>>(out, residual, table, w, hidden, xs, hidden, eps, gi, o8, x8);
   }
 }
 
 void launch_embed_rmsnorm(void* out, void* residual, const void* table, const long* ids, const long* src,
                           const long* tok, const void* w, bool weight_f32, int rows, int hidden, float eps,
-                          hipStream_t s) {
+                          hipStream_t s, float scale, void* out8, float* xs8) {
   if (rows <= 0) return;
   auto* o = static_cast<unsigned short*>(out);
   auto* r = static_cast<unsigned short*>(residual);
   auto* t = static_cast<const unsigned short*>(table);
-  const GatherIds gi{ids, src, tok};
-  if (weight_f32) launch_embed_rmsnorm_t<true>(o, r, t, w, rows, hidden, eps, gi, s);
-  else launch_embed_rmsnorm_t<false>(o, r, t, w, rows, hidden, eps, gi, s);
+  auto* o8 = static_cast<unsigned char*>(out8);
+  const GatherIds gi{ids, src, tok, scale};
+  if (weight_f32) launch_embed_rmsnorm_t<true>(o, r, t, w, rows, hidden, eps, gi, s, o8, xs8);
+  else launch_embed_rmsnorm_t<false>(o, r, t, w, rows, hidden, eps, gi, s, o8, xs8);
 }
 
 void launch_rmsnorm(void* out, void* residual, const void* x, const void* w,

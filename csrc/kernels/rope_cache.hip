@@ -10,6 +10,7 @@
 //                                              16-byte loads straight to VGPRs)
 // cos_sin: [max_pos, D] fp32 = [cos(D/2) | sin(D/2)].
 // mode: 0 = NeoX rotate-half (HF Llama), 1 = interleaved pairs (GGUF llama).
+// KV: cache element, bf16 (unsigned short) or e4m3 (unsigned char, common.h kv_store*).
 #include <cstdlib>
 
 #include "hipserve/common.h"
@@ -30,12 +31,12 @@ HS_DEVICE void rotate8(float (&x)[8], float (&y)[8], const float* cs, int i0,
 }
 
 // One workgroup per token; threads stride over (head, 8-wide chunk) work items.
-template <int kMode>
+template <int kMode, typename KV>
 __global__ __launch_bounds__(256) void rope_cache_kernel(
     unsigned short* __restrict__ qkv, long qkv_stride,
     const long* __restrict__ positions, const long* __restrict__ slots,
-    const float* __restrict__ cos_sin, unsigned short* __restrict__ k_cache,
-    unsigned short* __restrict__ v_cache, int nq, int nkv, int D,
+    const float* __restrict__ cos_sin, KV* __restrict__ k_cache,
+    KV* __restrict__ v_cache, int nq, int nkv, int D,
     int block_size) {
   const int t = blockIdx.x;
   const long pos = positions[t];
@@ -66,9 +67,9 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
         *reinterpret_cast<u16x8*>(base + half + c * 8) = vb;
       } else if (slot >= 0) {
         const int kh = h - nq;
-        unsigned short* kc = k_cache + ((blk * nkv + kh) * block_size + off) * (long)D;
-        *reinterpret_cast<u16x8*>(kc + c * 8) = va;
-        *reinterpret_cast<u16x8*>(kc + half + c * 8) = vb;
+        KV* kc = k_cache + ((blk * nkv + kh) * block_size + off) * (long)D;
+        kv_store8(kc + c * 8, va);
+        kv_store8(kc + half + c * 8, vb);
       }
     }
   } else {
@@ -93,8 +94,8 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
         *reinterpret_cast<u16x8*>(base + c * 8) = v;
       } else if (slot >= 0) {
         const int kh = h - nq;
-        unsigned short* kc = k_cache + ((blk * nkv + kh) * block_size + off) * (long)D;
-        *reinterpret_cast<u16x8*>(kc + c * 8) = v;
+        KV* kc = k_cache + ((blk * nkv + kh) * block_size + off) * (long)D;
+        kv_store8(kc + c * 8, v);
       }
     }
   }
@@ -105,9 +106,9 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
     for (int it = threadIdx.x; it < nkv * chunks; it += blockDim.x) {
       const int kh = it / chunks, c = it % chunks;
       const u16x8 v = *reinterpret_cast<const u16x8*>(vrow + kh * D + c * 8);
-      unsigned short* vc = v_cache + (blk * nkv + kh) * (long)D * block_size + off;
+      KV* vc = v_cache + (blk * nkv + kh) * (long)D * block_size + off;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vc[(c * 8 + j) * block_size] = v[j];
+      for (int j = 0; j < 8; ++j) kv_store1(vc + (c * 8 + j) * block_size, v[j]);
     }
   }
 }
@@ -119,11 +120,11 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
 // per-token kernel's scattered V stores cost about half of its time at 8K-token chunks.
 constexpr int kRopeTile = 16;
 
-template <int kMode>
+template <int kMode, typename KV>
 __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
     unsigned short* __restrict__ qkv, long qkv_stride, const long* __restrict__ positions,
-    const long* __restrict__ slots, const float* __restrict__ cos_sin, unsigned short* __restrict__ k_cache,
-    unsigned short* __restrict__ v_cache, int T, int nq, int nkv, int D, int block_size, int vfast) {
+    const long* __restrict__ slots, const float* __restrict__ cos_sin, KV* __restrict__ k_cache,
+    KV* __restrict__ v_cache, int T, int nq, int nkv, int D, int block_size, int vfast) {
   extern __shared__ __attribute__((aligned(16))) unsigned short vs[];  // [16][nkv * D + 8]
   const int t0 = blockIdx.x * kRopeTile;
   const int nt = min(kRopeTile, T - t0);
@@ -168,10 +169,14 @@ __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
             va[q][j] = f32_to_bf16(ra);
             vb[q][j] = f32_to_bf16(rb);
           }
-          unsigned short* dst = h < nq ? row + h * D
-                                       : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
-          *reinterpret_cast<u16x8*>(dst + c * 8) = va[q];
-          *reinterpret_cast<u16x8*>(dst + half + c * 8) = vb[q];
+          if (h < nq) {
+            *reinterpret_cast<u16x8*>(row + h * D + c * 8) = va[q];
+            *reinterpret_cast<u16x8*>(row + h * D + half + c * 8) = vb[q];
+          } else {
+            KV* dst = k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
+            kv_store8(dst + c * 8, va[q]);
+            kv_store8(dst + half + c * 8, vb[q]);
+          }
         }
       }
     } else {
@@ -194,9 +199,8 @@ __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
             v[q][2 * p] = f32_to_bf16(ra);
             v[q][2 * p + 1] = f32_to_bf16(rb);
           }
-          unsigned short* dst = h < nq ? row + h * D
-                                       : k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D;
-          *reinterpret_cast<u16x8*>(dst + c * 8) = v[q];
+          if (h < nq) *reinterpret_cast<u16x8*>(row + h * D + c * 8) = v[q];
+          else kv_store8(k_cache + ((blk * nkv + (h - nq)) * block_size + off) * (long)D + c * 8, v[q]);
         }
       }
     }
@@ -226,8 +230,7 @@ __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
       u16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = vs[(hl * 8 + j) * VR + r];
-      *reinterpret_cast<u16x8*>(v_cache + (blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off0 +
-                                hl * 8) = v;
+      kv_store8(v_cache + (blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off0 + hl * 8, v);
     }
     return;
   }
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(256) void rope_cache_tile_kernel(
   const int off = (int)(slot % block_size);
   for (int r = threadIdx.x / kRopeTile; r < VW; r += blockDim.x / kRopeTile) {
     const int kh = r / D, d = r % D;
-    v_cache[(blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off] = vs[tt * VR + r];
+    kv_store1(v_cache + (blk * nkv + kh) * (long)D * block_size + (long)d * block_size + off, vs[tt * VR + r]);
   }
 }
 
@@ -259,30 +262,41 @@ static int rope_vfast() {  // HIPSERVE_ROPE_VFAST=0: 2-byte V^T stores for every
   return on;
 }
 
-void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
-                       const long* slots, const float* cos_sin, void* k_cache,
-                       void* v_cache, int T, int nq, int nkv, int D,
-                       int block_size, int mode, hipStream_t s) {
-  if (T <= 0) return;
-  dim3 grid(T), block(256);
-  auto* q = static_cast<unsigned short*>(qkv);
-  auto* kc = static_cast<unsigned short*>(k_cache);
-  auto* vc = static_cast<unsigned short*>(v_cache);
+template <typename KV>
+static void rope_cache_t(unsigned short* q, long qkv_stride, const long* positions, const long* slots,
+                         const float* cos_sin, KV* kc, KV* vc, int T, int nq, int nkv, int D, int block_size,
+                         int mode, hipStream_t s) {
   if (T >= 128 && nkv * D <= 2048 && rope_tile_enabled()) {  // prefill chunks
     const dim3 tg((T + kRopeTile - 1) / kRopeTile);
     const size_t smem = (size_t)kRopeTile * (nkv * D + 8) * sizeof(unsigned short);
     if (mode == 0)
-      rope_cache_tile_kernel<0><<<tg, block, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq, nkv,
-                                                        D, block_size, rope_vfast());
+      rope_cache_tile_kernel<0, KV><<<tg, 256, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq,
+                                                          nkv, D, block_size, rope_vfast());
     else
-      rope_cache_tile_kernel<1><<<tg, block, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq, nkv,
-                                                        D, block_size, rope_vfast());
+      rope_cache_tile_kernel<1, KV><<<tg, 256, smem, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, T, nq,
+                                                          nkv, D, block_size, rope_vfast());
     return;
   }
   if (mode == 0)
-    rope_cache_kernel<0><<<grid, block, 0, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, nq, nkv, D, block_size);
+    rope_cache_kernel<0, KV><<<T, 256, 0, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, nq, nkv, D,
+                                               block_size);
   else
-    rope_cache_kernel<1><<<grid, block, 0, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, nq, nkv, D, block_size);
+    rope_cache_kernel<1, KV><<<T, 256, 0, s>>>(q, qkv_stride, positions, slots, cos_sin, kc, vc, nq, nkv, D,
+                                               block_size);
+}
+
+void launch_rope_cache(void* qkv, long qkv_stride, const long* positions,
+                       const long* slots, const float* cos_sin, void* k_cache,
+                       void* v_cache, int T, int nq, int nkv, int D,
+                       int block_size, int mode, hipStream_t s, bool kv_f8) {
+  if (T <= 0) return;
+  auto* q = static_cast<unsigned short*>(qkv);
+  if (kv_f8)
+    rope_cache_t(q, qkv_stride, positions, slots, cos_sin, static_cast<unsigned char*>(k_cache),
+                 static_cast<unsigned char*>(v_cache), T, nq, nkv, D, block_size, mode, s);
+  else
+    rope_cache_t(q, qkv_stride, positions, slots, cos_sin, static_cast<unsigned short*>(k_cache),
+                 static_cast<unsigned short*>(v_cache), T, nq, nkv, D, block_size, mode, s);
 }
 
 }  // namespace hipserve

@@ -58,11 +58,13 @@ void fused_add_rmsnorm(at::Tensor& out, const at::Tensor& x, at::Tensor& residua
                            x.stride(0), out.stride(0), (float)eps, cur_stream(), o8, x8);
 }
 
-// out = RMSNorm(table[id]) * weight, residual = table[id] per row; id = ids[row], or
-// tok[src[row]] where src[row] >= 0 (device-side decode lookahead ids)
+// residual = bf16(table[id] * scale), out = RMSNorm(residual) * weight per row; id =
+// ids[row], or tok[src[row]] where src[row] >= 0 (device-side decode lookahead ids);
+// out8 / xs8 (optional): out also as per-token e4m3 + row scale (= act_quant_fp8 of out)
 void embed_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& table, const at::Tensor& ids,
                    const c10::optional<at::Tensor>& src, const c10::optional<at::Tensor>& tok,
-                   const at::Tensor& weight, double eps) {
+                   const at::Tensor& weight, double eps, double scale, const c10::optional<at::Tensor>& out8,
+                   const c10::optional<at::Tensor>& xs8) {
   CHECK_DEV(table); CHECK_BF16(table); CHECK_BF16(out); CHECK_BF16(residual);
   CHECK_CONTIG(table); CHECK_CONTIG(out); CHECK_CONTIG(residual); CHECK_CONTIG(ids);
   TORCH_CHECK(table.dim() == 2 && out.dim() == 2 && residual.sizes() == out.sizes());
@@ -77,11 +79,15 @@ void embed_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& tabl
   }
   TORCH_CHECK(weight.numel() == hidden && weight.is_contiguous());
   TORCH_CHECK(weight.scalar_type() == at::kBFloat16 || weight.scalar_type() == at::kFloat);
+  void* o8;
+  float* x8;
+  e4m3_out_args(out8, xs8, out, &o8, &x8, "embed_rmsnorm");
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   hipserve::launch_embed_rmsnorm(out.data_ptr(), residual.data_ptr(), table.data_ptr(), ids.data_ptr<long>(),
                                  src.has_value() ? src->data_ptr<long>() : nullptr,
                                  tok.has_value() ? tok->data_ptr<long>() : nullptr, weight.data_ptr(),
-                                 weight.scalar_type() == at::kFloat, rows, hidden, (float)eps, cur_stream());
+                                 weight.scalar_type() == at::kFloat, rows, hidden, (float)eps, cur_stream(),
+                                 (float)scale, o8, x8);
 }
 
 void silu_and_mul(at::Tensor& out, const at::Tensor& x) {
@@ -91,6 +97,15 @@ void silu_and_mul(at::Tensor& out, const at::Tensor& x) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   hipserve::launch_silu_and_mul(out.data_ptr(), x.data_ptr(), x.size(0), out.size(1),
                                 x.stride(0), out.stride(0), cur_stream());
+}
+
+// paged KV cache element type: bf16, or float8_e4m3fn (--kv-cache-dtype fp8: e4m3 with a
+// per-tensor scale of 1, written rounded / read widened by the kernels); K and V alike
+static bool kv_is_f8(const at::Tensor& k, const at::Tensor& v) {
+  const auto t = k.scalar_type();
+  TORCH_CHECK((t == at::kBFloat16 || t == at::kFloat8_e4m3fn) && v.scalar_type() == t,
+              "KV cache: bf16 or float8_e4m3fn, K and V alike");
+  return t == at::kFloat8_e4m3fn;
 }
 
 void rope_cache(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& slots,
@@ -109,7 +124,7 @@ void rope_cache(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& 
   hipserve::launch_rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int64_t>(),
                               slots.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                               k_cache.data_ptr(), v_cache.data_ptr(), qkv.size(0), nq, nkv,
-                              head_dim, k_cache.size(2), mode, cur_stream());
+                              head_dim, k_cache.size(2), mode, cur_stream(), kv_is_f8(k_cache, v_cache));
 }
 
 // the f16 pair-order copy of a bf16 [B, >= nq D] output (same shape and row stride) or null
@@ -148,7 +163,8 @@ void paged_decode(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cach
                                 block_tables.data_ptr<int>(), block_tables.stride(0),
                                 context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
                                 tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size,
-                                max_parts, (float)scale, (int)window, cur_stream(), out16_ptr(out16, out));
+                                max_parts, (float)scale, (int)window, cur_stream(), out16_ptr(out16, out),
+                                kv_is_f8(k_cache, v_cache));
 }
 
 void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, const at::Tensor& positions,
@@ -157,6 +173,7 @@ void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, con
                       at::Tensor& tmp_ml, int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window,
                       int64_t mode, const c10::optional<at::Tensor>& out16) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(!kv_is_f8(k_cache, v_cache), "paged_decode_qkv: bf16 KV cache only");
   const int D = k_cache.size(3), bs = k_cache.size(2);
   TORCH_CHECK(D == 64 || D == 128, "paged_decode_qkv: head_dim 64/128");
   TORCH_CHECK(window >= 0 && (mode == 0 || mode == 1));
@@ -206,7 +223,7 @@ void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k
                                      block_tables.data_ptr<int>(), block_tables.stride(0),
                                      cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(),
                                      tiles.data_ptr<int>(), tiles.size(0), nq, nkv, D, bs,
-                                     (float)scale, (int)window, cur_stream());
+                                     (float)scale, (int)window, cur_stream(), kv_is_f8(k_cache, v_cache));
 }
 
 // Per-head RMSNorm of q and k inside the merged qkv rows, in place (Qwen3 / Gemma-3).
@@ -1014,7 +1031,8 @@ void splitk_rope_cache(at::Tensor& qkv, const at::Tensor& ws, int64_t splits, co
   hipserve::launch_splitk_rope_cache(qkv.data_ptr(), qkv.stride(0), ws.data_ptr<float>(), splits,
                                      positions.data_ptr<int64_t>(), slots.data_ptr<int64_t>(),
                                      cos_sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), T, nq, nkv,
-                                     head_dim, k_cache.size(2), mode, cur_stream(), bp, qwp, kwp, (float)eps);
+                                     head_dim, k_cache.size(2), mode, cur_stream(), bp, qwp, kwp, (float)eps,
+                                     kv_is_f8(k_cache, v_cache));
 }
 
 void splitk_reduce(at::Tensor& out, const at::Tensor& ws, int64_t splits) {
@@ -1226,7 +1244,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("moe_combine_partial(Tensor(a!) out, Tensor ws, Tensor w, Tensor pair_slot, int k) -> ()");
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor weight, float eps, Tensor(b!)? out8=None, Tensor(c!)? xs8=None) -> ()");
   m.def("embed_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor table, Tensor ids, Tensor? src, Tensor? tok, "
-        "Tensor weight, float eps) -> ()");
+        "Tensor weight, float eps, float scale=1.0, Tensor(c!)? out8=None, Tensor(d!)? xs8=None) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) out, Tensor x, Tensor(b!) residual, Tensor weight, float eps, Tensor(c!)? out8=None, Tensor(d!)? xs8=None) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode) -> ()");

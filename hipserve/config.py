@@ -499,6 +499,10 @@ def checkpoint_quantization(model: str) -> str | None:
     return None
 
 
+# --kv-cache-dtype values (vLLM's spellings) -> element kind
+KV_CACHE_DTYPES = {"auto": "auto", "bf16": "auto", "bfloat16": "auto", "fp8": "fp8", "fp8_e4m3": "fp8"}
+
+
 @dataclass(frozen=True)
 class EngineConfig:
     model: str = "llama-3-8b"
@@ -520,6 +524,11 @@ class EngineConfig:
     seed: int = 0
     trust_remote_code: bool = False
     decode_partition: int = 512
+    # paged KV cache element: "auto" (= the activation dtype, bf16) or "fp8" / "fp8_e4m3"
+    # (OCP e4m3, per-tensor scale 1 as vLLM's --kv-cache-dtype fp8 without calibrated
+    # scales: half the KV bytes per token, so 2x the KV blocks and half the decode
+    # attention's HBM stream; K / V are rounded to e4m3 when written)
+    kv_cache_dtype: str = "auto"
     host: str = "0.0.0.0"
     port: int = 8080
     extra: dict = field(default_factory=dict)
@@ -529,6 +538,12 @@ class EngineConfig:
         b = self.block_size
         if b < 16 or b > 256 or b & (b - 1):
             raise ValueError(f"block_size must be a power of two in [16, 256], got {b}")
+        if self.kv_cache_dtype not in KV_CACHE_DTYPES:
+            raise ValueError(f"kv_cache_dtype must be one of {sorted(KV_CACHE_DTYPES)}, got {self.kv_cache_dtype!r}")
+
+    @property
+    def kv_fp8(self) -> bool:
+        return KV_CACHE_DTYPES[self.kv_cache_dtype] == "fp8"
 
     def replace(self, **kw) -> "EngineConfig":
         return dataclasses.replace(self, **kw)

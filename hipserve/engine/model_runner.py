@@ -101,6 +101,9 @@ class ModelRunner:
         self.model = LlamaModel(mcfg, tp, self.device, self.dtype, self.ops, max_pos=self.max_model_len)
         self.model.decode_partition = ecfg.decode_partition
         self.model.block_size_hint = ecfg.block_size
+        if ecfg.kv_fp8:  # e4m3 paged KV cache (the fused qkv -> attention kernel writes bf16 only)
+            self.model.kv_dtype = torch.float8_e4m3fn
+            self.model.fused_qkv_attention = False
         t0 = time.time()
         self._load_weights()
         self.load_time = time.time() - t0

@@ -129,6 +129,7 @@ class LlamaModel:
         self.tp = tp
         self.device = torch.device(device)
         self.dtype = dtype
+        self.kv_dtype = dtype  # paged KV cache element (ModelRunner: float8_e4m3fn for --kv-cache-dtype fp8)
         self.ops = ops
         self.nq, self.nkv, self.inter, self.vpad = shard_sizes(cfg, tp.world_size)
         self.D = cfg.head_dim
@@ -507,10 +508,10 @@ class LlamaModel:
     def fused_embed_ok(self, meta: AttnMeta) -> bool:
         """The fused decode forward can take the lookahead ids unresolved (``meta.id_src``):
         id select + embedding gather + residual copy + first RMSNorm in one kernel
-        (``embed_rmsnorm``, norm.hip). TP=1 only (the vocab-parallel embedding needs a
-        cross-rank sum before the norm)."""
+        (``embed_rmsnorm``, norm.hip), Gemma's embedding scale included. TP=1 only (the
+        vocab-parallel embedding needs a cross-rank sum before the norm)."""
         return (self._fused_ok(meta) and self.tp.world_size == 1 and self.embed.dtype == torch.bfloat16
-                and self.cfg.embed_scale == 1.0 and hasattr(torch.ops.hipserve, "embed_rmsnorm"))
+                and hasattr(torch.ops.hipserve, "embed_rmsnorm"))
 
     @staticmethod
     def resolve_ids(ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
@@ -717,10 +718,17 @@ class LlamaModel:
         T = ids.shape[0]
         D, nq, nkv = self.D, self.nq, self.nkv
         eps = cfg.rms_norm_eps
-        if meta.id_src is not None and self.fused_embed_ok(meta):
+        xn16 = None  # f16 pair-order copy of xn from its producer (quantised GEMM input)
+        xn8 = None   # (e4m3 xn, row scales) from its producer (W8A8 FP8 decode GEMM input)
+        if ids.dtype == torch.long and self.fused_embed_ok(meta):
             residual = torch.empty(T, cfg.hidden_size, device=ids.device, dtype=self.embed.dtype)
             xn = torch.empty_like(residual)
-            op.embed_rmsnorm(xn, residual, self.embed, ids, meta.id_src[0], meta.id_src[1], self.layers[0].ln1, eps)
+            xn8 = self._x8(xn, self.layers[0].wqkv)
+            src, tok = meta.id_src if meta.id_src is not None else (None, None)
+            # Gemma: embeddings * sqrt(hidden), the scale rounded to the dtype (as forward())
+            scale = float(torch.tensor(cfg.embed_scale, dtype=self.embed.dtype))
+            op.embed_rmsnorm(xn, residual, self.embed, ids, src, tok, self.layers[0].ln1, eps, scale,
+                             *(xn8 if xn8 is not None else (None, None)))
             h = residual
         else:
             h = self.embed_tokens(self.resolve_ids(ids, meta))
@@ -734,8 +742,6 @@ class LlamaModel:
         L = len(self.layers)
         lw0 = self.layers[0]
         extras = lw0.bqkv is not None or lw0.q_norm is not None
-        xn16 = None  # f16 pair-order copy of xn from its producer (quantised GEMM input)
-        xn8 = None   # (e4m3 xn, row scales) from its producer (W8A8 FP8 decode GEMM input)
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
             win = cfg.window_of(i)
@@ -1240,10 +1246,10 @@ class LlamaModel:
 
     # ---------------------------------------------------------------- kv cache
     def kv_bytes_per_block(self, block_size: int) -> int:
-        return 2 * self.cfg.num_layers * self.nkv * block_size * self.D * torch.finfo(self.dtype).bits // 8
+        return 2 * self.cfg.num_layers * self.nkv * block_size * self.D * torch.finfo(self.kv_dtype).bits // 8
 
     def allocate_kv_cache(self, num_blocks: int, block_size: int):
         L = self.cfg.num_layers
-        k = torch.zeros(L, num_blocks, self.nkv, block_size, self.D, device=self.device, dtype=self.dtype)
-        v = torch.zeros(L, num_blocks, self.nkv, self.D, block_size, device=self.device, dtype=self.dtype)
+        k = torch.zeros(L, num_blocks, self.nkv, block_size, self.D, device=self.device, dtype=self.kv_dtype)
+        v = torch.zeros(L, num_blocks, self.nkv, self.D, block_size, device=self.device, dtype=self.kv_dtype)
         return [(k[i], v[i]) for i in range(L)]

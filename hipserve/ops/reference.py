@@ -133,6 +133,14 @@ def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, mode: 
     return out.to(x.dtype)
 
 
+def to_cache(x: torch.Tensor, dtype) -> torch.Tensor:
+    """K / V rows in the cache's element type: e4m3 caches saturate to +-448 first (the
+    kernels' rounding, common.h kv_store*); torch's own cast turns overflow into NaN."""
+    if dtype == torch.float8_e4m3fn:
+        return x.float().clamp(-448.0, 448.0).to(dtype)
+    return x.to(dtype)
+
+
 def rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mode):
     """In-place: rotates q inside qkv, writes rotated k and raw v into the caches."""
     T = qkv.shape[0]
@@ -149,8 +157,8 @@ def rope_cache(qkv, positions, slots, cos_sin, k_cache, v_cache, nq, nkv, D, mod
     if valid.any():
         sv = sl[valid]
         blk, off = sv // bs, sv % bs
-        k_cache[blk, :, off, :] = kr[valid].to(k_cache.dtype)
-        v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
+        k_cache[blk, :, off, :] = to_cache(kr[valid], k_cache.dtype)
+        v_cache[blk, :, :, off] = to_cache(v[valid], v_cache.dtype)
 
 
 def _gather_kv(k_cache, v_cache, block_table, n):

@@ -41,6 +41,8 @@ def build_parser(prog="hipserve") -> argparse.ArgumentParser:
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
     ap.add_argument("--block-size", type=int, default=16)
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "bf16", "bfloat16", "fp8", "fp8_e4m3"],
+                    help="paged KV cache element: auto (bf16) or fp8 (e4m3, per-tensor scale 1: 2x the KV blocks)")
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-num-batched-tokens", type=int, default=None,
                     help="prefill token budget per step (default 8192; 16384 for GGUF weights)")
@@ -72,7 +74,7 @@ def config_from_args(a) -> EngineConfig:
         max_model_len=a.max_model_len, block_size=a.block_size, max_num_seqs=a.max_num_seqs,
         max_num_batched_tokens=a.max_num_batched_tokens or default_batched_tokens(a.model, a.load_format,
                                                                                    a.quantization),
-        num_kv_blocks=a.num_kv_blocks,
+        num_kv_blocks=a.num_kv_blocks, kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"),
         enable_prefix_caching=a.enable_prefix_caching, enforce_eager=a.enforce_eager, seed=a.seed,
         trust_remote_code=a.trust_remote_code, host=a.host, port=a.port,
         extra={"quantization": a.quantization} if a.quantization else {})

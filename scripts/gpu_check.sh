@@ -194,6 +194,13 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     prof_qwen3moe) prof_run profqm --model qwen3-30b-a3b ;;
     prof_gemma3) prof_run profg3 --model gemma-3-27b ;;
     prof_g27fp8) prof_run profg3f8 --model gemma-3-27b --quantization fp8 ;;
+    g27fp8d) bench_named g27fp8d X=1 -- --model gemma-3-27b --quantization fp8 ;;
+    fp8dtest) run_one tests/test_fp8_decode_gpu.py ;;
+    famtest) run_one tests/test_families_gpu.py ;;
+    kvf8test) run_one tests/test_kv_fp8_gpu.py ;;
+    b8kvf8) bench_named b8kvf8 X=1 -- --kv-cache-dtype fp8 ;;
+    g27fp8kvf8) bench_named g27fp8kvf8 X=1 -- --model gemma-3-27b --quantization fp8 --kv-cache-dtype fp8 ;;
+    prof_kvf8) prof_run profkvf8 --kv-cache-dtype fp8 ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done

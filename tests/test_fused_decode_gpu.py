@@ -23,12 +23,16 @@ def _partials(S, M, N, seed):
     return torch.randn(S, M, N, device=DEV, generator=g) * 0.5
 
 
-@pytest.mark.parametrize("M,H", [(1, 4096), (64, 4096), (37, 2048), (8, 8192), (3, 1024)])
+@pytest.mark.parametrize("M,H", [(1, 4096), (64, 4096), (37, 2048), (8, 8192), (3, 1024), (64, 5376)])
 @pytest.mark.parametrize("wf32", [False, True])
 @pytest.mark.parametrize("lookahead", [False, True])
-def test_embed_rmsnorm_bit_exact(ops, M, H, wf32, lookahead):
-    """embed_rmsnorm (norm.hip gather mode) == id select + F.embedding + clone +
-    rmsnorm, bit for bit; with lookahead, rows with src >= 0 take tok[src]."""
+@pytest.mark.parametrize("scale", [1.0, 5376 ** 0.5])
+def test_embed_rmsnorm_bit_exact(ops, M, H, wf32, lookahead, scale):
+    """embed_rmsnorm (norm.hip gather mode) == id select + F.embedding (* the Gemma
+    embedding scale, rounded to bf16) + clone + rmsnorm, bit for bit; with lookahead,
+    rows with src >= 0 take tok[src]. Its e4m3 copy == act_quant_fp8 of the output."""
+    from hipserve.ops import pgemm
+
     g = torch.Generator(device=DEV).manual_seed(M * 7 + H)
     V = 5000
     table = torch.randn(V, H, device=DEV, dtype=torch.bfloat16, generator=g)
@@ -41,14 +45,21 @@ def test_embed_rmsnorm_bit_exact(ops, M, H, wf32, lookahead):
         tok = torch.randint(0, V, (80,), device=DEV, generator=g)
         src = torch.randint(-1, 80, (M,), device=DEV, generator=g)
         want_ids = torch.where(src >= 0, tok.index_select(0, src.clamp(min=0)), ids)
+    sc = float(torch.tensor(scale, dtype=torch.bfloat16))
     h = torch.nn.functional.embedding(want_ids, table)
+    if scale != 1.0:
+        h = h * sc
     want = torch.empty_like(h)
     ops.rmsnorm(want, h, w, 1e-5)
     out = torch.full_like(h, float("nan"))
     res = torch.full_like(h, float("nan"))
-    torch.ops.hipserve.embed_rmsnorm(out, res, table, ids, src, tok, w, 1e-5)
+    q8 = torch.empty(M, H, device=DEV, dtype=torch.uint8)
+    s8 = torch.empty(M, device=DEV, dtype=torch.float32)
+    torch.ops.hipserve.embed_rmsnorm(out, res, table, ids, src, tok, w, 1e-5, sc, q8, s8)
     assert torch.equal(res, h)
     assert torch.equal(out, want)
+    xq, xs = pgemm.act_quant(out)
+    assert torch.equal(q8, xq) and torch.equal(s8, xs)
 
 
 @pytest.mark.parametrize("S,M,N", [(1, 5, 4096), (4, 64, 4096), (8, 17, 2048), (3, 1, 8192)])
