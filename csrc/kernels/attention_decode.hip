@@ -84,12 +84,21 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   static_assert(!kQKV || sizeof(KV) == 2, "the fused qkv decode writes a bf16 cache");
   constexpr int KS = D / 32;  // k-steps of the QK MFMA
   constexpr int NB = D / 16;  // 16-column blocks of the PV output
+  // e4m3 cache (head_dim 64 / 128): 64-token chunks so every K / V load is 16 bytes (16 d
+  // of one key, 16 keys of one V^T row) — with 32-token chunks the e4m3 stream ran as
+  // 8-byte loads at ~3.7 TB/s, issue- rather than HBM-bound. The QK MFMA's k index is
+  // permuted to match: k-step ks, lane group g, slot j <-> d = 16 g + 64 (ks >> 1) + 8 (ks & 1) + j
+  // (Q is loaded in the same order); S tile t, row m <-> key 16 (m >> 2) + 4 t + (m & 3), so
+  // lane group g holds keys 16 g .. 16 g + 15 of the chunk: keys 16 g + j feed the first
+  // P.V MFMA's k-slots 8 g + j and keys 16 g + 8 + j the second, as the V^T load splits
+  constexpr bool kWide = sizeof(KV) == 1 && KS % 2 == 0;
+  constexpr int CH = kWide ? 2 * kChunk : kChunk;
   const int part = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
   const int ctx = context_lens[b];
   // sliding window: keys [lo, ctx); partitions start at lo rounded down to a
   // 32-token chunk (aligned V loads), the keys below lo are masked
   const int lo = window > 0 ? max(0, ctx - window) : 0;
-  const int lo_al = lo & ~(kChunk - 1);
+  const int lo_al = lo & ~(CH - 1);
   const int start = lo_al + part * part_size;
   if (start >= ctx) return;
   const int end = min(start + part_size, ctx);
@@ -111,7 +120,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   __syncthreads();
 
   const long kv_head_stride = (long)block_size * D;  // elements per (block, head)
-  const int nchunks = (end - start + kChunk - 1) / kChunk;
+  const int nchunks = (end - start + CH - 1) / CH;
   const int last_tok = ctx - 1;
   const int bt_base_tok = first_blk * block_size;
 
@@ -124,11 +133,35 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
   struct Chunk {
     KV8 ka[KS], kb[KS], vv[NB];
   };
+  struct ChunkW {  // kWide: 16 e4m3 per register quad
+    u32x4 k[4][KS / 2 > 0 ? KS / 2 : 1], v[NB];
+  };
   // K / V are read exactly once per step by one wave: non-temporal loads (aux nt) keep
   // them from evicting the weights' and partials' lines and shorten issue -> landed
   auto ld = [](const KV* p) -> KV8 {
     if constexpr (kNT) return kv_load8_nt(p);
     else return kv_load8(p);
+  };
+  auto ld16 = [](const KV* p) -> u32x4 {
+    if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+  };
+  [[maybe_unused]] auto load_chunk_w = [&](int c, ChunkW& ch) {
+    const int cs = start + min(c, nchunks - 1) * CH;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int tk = min(cs + 16 * (col >> 2) + 4 * t + (col & 3), last_tok);
+      const KV* kp = k_cache + ((long)bt[(tk - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride +
+                     (long)(tk & bmask) * D + 16 * grp;
+#pragma unroll
+      for (int hh = 0; hh < KS / 2; ++hh) ch.k[t][hh] = ld16(kp + 64 * hh);
+    }
+    int tv = cs + 16 * grp;
+    if (tv > last_tok) tv = last_tok & ~15;
+    const KV* vb = v_cache + ((long)bt[(tv - bt_base_tok) >> bsh] * nkv + kh) * kv_head_stride + (tv & bmask) +
+                   (long)col * block_size;
+#pragma unroll
+    for (int n = 0; n < NB; ++n) ch.v[n] = ld16(vb + (long)16 * n * block_size);
   };
   auto load_chunk = [&](int c, Chunk& ch) {
     const int cs = start + min(c, nchunks - 1) * kChunk;
@@ -168,8 +201,8 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     const unsigned short* qrow = q + (long)b * q_stride + (long)h * D;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      u16x8 v = (col < G) ? *reinterpret_cast<const u16x8*>(qrow + 8 * grp + 32 * ks)
-                          : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      const int d0 = kWide ? 16 * grp + 64 * (ks >> 1) + 8 * (ks & 1) : 8 * grp + 32 * ks;
+      u16x8 v = (col < G) ? *reinterpret_cast<const u16x8*>(qrow + d0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       qf[ks] = __builtin_bit_cast(bf16x8, v);
     }
   } else {
@@ -190,7 +223,7 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     //     chunk (chunk c belongs to wave c % W): no workgroup barrier, the other waves
     //     start streaming at once and never read the new token
     const long slot = qi.slots[b];
-    const int nch = (end - start + kChunk - 1) / kChunk;
+    const int nch = (end - start + CH - 1) / CH;
     if (end == ctx && slot >= 0 && wave == (nch - 1) % kDecWaves) {
       const long blk = slot / block_size;
       const int off = (int)(slot % block_size);
@@ -347,9 +380,79 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
     for (int n = 0; n < NB; ++n)
       o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, kv_widen8(ch.vv[n])), o[n], 0, 0, 0);
   };
+  [[maybe_unused]] auto compute_chunk_w = [&](int c, const ChunkW& ch) {
+    const int cs = start + c * CH;
+    f32x4 st[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int hh = 0; hh < KS / 2; ++hh) {
+        const u32x4 w = ch.k[t][hh];
+        st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv_widen8(u32x2{w[0], w[1]})),
+                                                        qf[2 * hh], st[t], 0, 0, 0);
+        st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv_widen8(u32x2{w[2], w[3]})),
+                                                        qf[2 * hh + 1], st[t], 0, 0, 0);
+      }
+    }
+    // lane holds the scores of keys cs + 16 grp + 4 t + r for head col
+    float sc[16];
+    float mx = -1e30f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tk = cs + 16 * grp + 4 * t + r;
+        sc[4 * t + r] = (tk >= lo && tk <= last_tok) ? st[t][r] * sl2 : -1e30f;
+        mx = fmaxf(mx, sc[4 * t + r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float psum = 0.f;
+    bf16x8 p0, p1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a0 = exp2f(sc[j] - m_new), a1 = exp2f(sc[8 + j] - m_new);
+      psum += a0 + a1;
+      p0[j] = static_cast<__bf16>(a0);
+      p1[j] = static_cast<__bf16>(a1);
+    }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a_r = __shfl(alpha, 4 * grp + r, 64);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) o[n][r] *= a_r;
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const u32x4 w = ch.v[n];
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(p0, __builtin_bit_cast(bf16x8, kv_widen8(u32x2{w[0], w[1]})),
+                                                     o[n], 0, 0, 0);
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(p1, __builtin_bit_cast(bf16x8, kv_widen8(u32x2{w[2], w[3]})),
+                                                     o[n], 0, 0, 0);
+    }
+  };
   constexpr int W = kDecWaves;
   int c = wave;
-  if (c < nchunks) {
+  if constexpr (kWide) {
+    ChunkW AW, BW;
+    if (c < nchunks) {
+      load_chunk_w(c, AW);
+      for (; c + W < nchunks; c += 2 * W) {
+        load_chunk_w(c + W, BW);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_chunk_w(c, AW);
+        load_chunk_w(c + 2 * W, AW);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_chunk_w(c + W, BW);
+      }
+      if (c < nchunks) compute_chunk_w(c, AW);
+    }
+  } else if (c < nchunks) {
     if (!pre) load_chunk(c, A);
     for (; c + W < nchunks; c += 2 * W) {
       load_chunk(c + W, B);
@@ -420,14 +523,15 @@ template <int D>
 __global__ __launch_bounds__(512) void paged_decode_reduce_kernel(
     unsigned short* __restrict__ out, long out_stride,
     const float* __restrict__ tmp_out, const float* __restrict__ tmp_ml,
-    const int* __restrict__ context_lens, int nq, int part_size, int max_parts, int window,
+    const int* __restrict__ context_lens, int nq, int part_size, int max_parts, int window, int align,
     unsigned short* __restrict__ out16 = nullptr) {
   constexpr int G = reduce_groups<D>();
   static_assert(G * D % 64 == 0, "whole waves");
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int d = tid % D, grp = tid / D;
   const int ctx = context_lens[b];
-  const int lo_al = (window > 0 ? max(0, ctx - window) : 0) & ~(kChunk - 1);
+  // the attention kernel's partition origin: the window start rounded down to its chunk
+  const int lo_al = (window > 0 ? max(0, ctx - window) : 0) & ~(align - 1);
   const int np = (ctx - lo_al + part_size - 1) / part_size;
   if (np <= 1) return;
   const long base = ((long)b * nq + h) * max_parts;
@@ -504,6 +608,10 @@ static bool decode_nt(long workgroups) {
   return env && workgroups >= 256;
 }
 
+// the decode kernel's chunk (= window-origin alignment): 64 keys for an e4m3 cache at head_dim
+// 64 / 128 (paged_decode_kernel kWide), else 32
+static int dec_align(int D, bool kv_f8) { return kv_f8 && D != 96 ? 2 * kChunk : kChunk; }
+
 void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
                          const void* k_cache, const void* v_cache,
                          const int* block_tables, int bt_stride,
@@ -545,7 +653,7 @@ void launch_paged_decode(void* out, long out_stride, const void* q, long q_strid
     if (max_parts > 1)                                                                                      \
       paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(reduce_groups<DD>() * DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml, \
                                                                        context_lens, nq, part_size, max_parts, \
-                                                                       window, o16);                        \
+                                                                       window, dec_align(DD, kv_f8), o16);  \
   } while (0)
   if (D == 128) HS_DECODE_D(128);
   else if (D == 96) HS_DECODE_D(96);
@@ -588,7 +696,7 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
     if (max_parts > 1)                                                                                        \
       paged_decode_reduce_kernel<DD><<<dim3(nq, B), dim3(reduce_groups<DD>() * DD), 0, s>>>(o, out_stride, tmp_out, tmp_ml,   \
                                                                        context_lens, nq, part_size, max_parts,   \
-                                                                       window, o16);                          \
+                                                                       window, kChunk, o16);                  \
   } while (0)
   if (D == 128) HS_DECODE_QKV_D(128);
   else HS_DECODE_QKV_D(64);

@@ -201,6 +201,11 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     b8kvf8) bench_named b8kvf8 X=1 -- --kv-cache-dtype fp8 ;;
     g27fp8kvf8) bench_named g27fp8kvf8 X=1 -- --model gemma-3-27b --quantization fp8 --kv-cache-dtype fp8 ;;
     prof_kvf8) prof_run profkvf8 --kv-cache-dtype fp8 ;;
+    deckv) for kv in bf16 fp8; do for w in 4 8; do DECODE_KV=$kv HIPSERVE_DECODE_WAVES=$w DECODE_COLD=1 DECODE_SHAPES=64x1152x32x8,64x1152x32x16 DECODE_PARTS=512,2048 \
+      timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/deckv_${kv}_w$w.log 2>&1 || exit 1; echo "kv $kv waves $w"; grep paged_decode $OUT/deckv_${kv}_w$w.log; done; done ;;
+    prefkv) for kv in bf16 fp8; do DECODE_KV=$kv BENCH_PREFILL_VERS=v2w8 timeout -k 10 300 python -u tools/bench_ops.py prefill > $OUT/prefkv_$kv.log 2>&1 || exit 1; echo "kv $kv"; grep prefill_attention $OUT/prefkv_$kv.log; done ;;
+    deckvnt) for nt in 1 0; do DECODE_KV=fp8 HIPSERVE_DECODE_NT=$nt DECODE_COLD=1 DECODE_SHAPES=64x1152x32x8,64x1152x32x16,64x4096x32x8 DECODE_PARTS=2048 \
+      timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/deckv_nt$nt.log 2>&1 || exit 1; echo "fp8 nt $nt"; grep paged_decode $OUT/deckv_nt$nt.log; done ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done

@@ -106,11 +106,16 @@ def test_paged_decode_fp8_cache(ops, nq, nkv, D, part, window):
     ops.paged_decode(out, q, kc, vc, bt, cl, tmp_out, tmp_ml, nq, nkv, part, scale, window)
     want = ref.paged_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), nq, nkv, scale, window)
     _close(out.view(B, nq, D), want, atol=2e-2, rtol=2e-2)
-    # the same cache widened to bf16 through the bf16 kernel: identical math after the load
+    # the same cache widened to bf16 through the bf16 kernel: the same values; at head_dim 96
+    # the e4m3 kernel also keeps the bf16 kernel's chunking, so the sums match bit for bit
+    # (64 / 128 stream 64-key chunks: another fp32 summation order)
     out_b = torch.zeros_like(out)
     ops.paged_decode(out_b, q, kc.to(torch.bfloat16), vc.to(torch.bfloat16), bt, cl, tmp_out, tmp_ml, nq, nkv,
                      part, scale, window)
-    assert torch.equal(out, out_b)
+    if D == 96:
+        assert torch.equal(out, out_b)
+    else:
+        _close(out, out_b, atol=1e-2, rtol=1e-2)
 
 
 @pytest.mark.parametrize("nq,nkv,D,v1", [(32, 8, 128, False), (32, 8, 128, True), (8, 1, 128, False),

@@ -96,10 +96,13 @@ def bench_decode(ops):
         nblocks = B * mb
         # DECODE_COLD=1: rotate over enough KV copies (> 2x the 256 MB MALL) that every
         # call streams cold K / V, as in the engine (one step touches every layer's KV)
-        byts = 2 * B * ctx * nkv * D * 2
+        # DECODE_KV=fp8: e4m3 cache (--kv-cache-dtype fp8), half the bytes
+        f8 = os.environ.get("DECODE_KV") == "fp8"
+        kvt = torch.float8_e4m3fn if f8 else torch.bfloat16
+        byts = 2 * B * ctx * nkv * D * (1 if f8 else 2)
         ncopy = max(1, min(8, -(-(768 << 20) // byts))) if os.environ.get("DECODE_COLD") == "1" else 1
-        kcs = [torch.randn(nblocks, nkv, bs, D, device=DEV, dtype=torch.bfloat16) for _ in range(ncopy)]
-        vcs = [torch.randn(nblocks, nkv, D, bs, device=DEV, dtype=torch.bfloat16) for _ in range(ncopy)]
+        kcs = [torch.randn(nblocks, nkv, bs, D, device=DEV).to(kvt) for _ in range(ncopy)]
+        vcs = [torch.randn(nblocks, nkv, D, bs, device=DEV).to(kvt) for _ in range(ncopy)]
         bt = torch.randperm(nblocks, device=DEV).int().view(B, mb)
         cl = torch.full((B,), ctx, device=DEV, dtype=torch.int32)
         q = torch.randn(B, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
@@ -115,7 +118,7 @@ def bench_decode(ops):
             ops.paged_decode(out, q, kcs[i], vcs[i], bt, cl, to, tm, nq, nkv, part, 1 / math.sqrt(D))
 
         us = timeit(call)
-        emit(op="paged_decode", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, cold=ncopy > 1,
+        emit(op="paged_decode", kv="fp8" if f8 else "bf16", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, cold=ncopy > 1,
              nt=os.environ.get("HIPSERVE_DECODE_NT", "1"), us=round(us, 1), TBps=round(byts / us / 1e6, 2))
         del kcs, vcs
 
@@ -128,8 +131,9 @@ def bench_prefill(ops):
     vers = os.environ.get("BENCH_PREFILL_VERS", "v2w4,v2w8,v1").split(",")
     for S, nseq, nq, nkv in shapes:
         mb = S // bs
-        kc = torch.randn(nseq * mb, nkv, bs, D, device=DEV, dtype=torch.bfloat16)
-        vc = torch.randn(nseq * mb, nkv, D, bs, device=DEV, dtype=torch.bfloat16)
+        kvt = torch.float8_e4m3fn if os.environ.get("DECODE_KV") == "fp8" else torch.bfloat16
+        kc = torch.randn(nseq * mb, nkv, bs, D, device=DEV).to(kvt)
+        vc = torch.randn(nseq * mb, nkv, D, bs, device=DEV).to(kvt)
         bt = torch.arange(nseq * mb, device=DEV).int().view(nseq, mb)
         cu = torch.arange(0, (nseq + 1) * S, S, device=DEV, dtype=torch.int32)
         ctx = torch.full((nseq,), S, device=DEV, dtype=torch.int32)
