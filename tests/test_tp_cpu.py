@@ -24,16 +24,16 @@ def _port():
     return p
 
 
-def _cfg(ckpt, tp):
+def _cfg(ckpt, tp, kv="auto"):
     ckpt, _, quant = ckpt.partition(":")  # "tiny-llama:fp8": random-init 8-bit weights
     fmt = "safetensors" if os.path.isdir(ckpt) else "dummy"
     return EngineConfig(model=ckpt, load_format=fmt, device="cpu", dtype="float32",
                         tensor_parallel_size=tp, num_kv_blocks=128, max_model_len=256,
-                        max_num_batched_tokens=32, max_num_seqs=4,
+                        max_num_batched_tokens=32, max_num_seqs=4, kv_cache_dtype=kv,
                         extra={"quantization": quant} if quant else {})
 
 
-def _worker(rank, world, port, ckpt, q):
+def _worker(rank, world, port, ckpt, q, kv="auto"):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -43,7 +43,7 @@ def _worker(rank, world, port, ckpt, q):
     from hipserve.parallel.comm import init_tp
 
     tp = init_tp(world, backend="gloo", device_type="cpu")
-    cfg = _cfg(ckpt, world)
+    cfg = _cfg(ckpt, world, kv)
     try:
         if rank == 0:
             eng = LLMEngine(cfg, tp=tp)
@@ -62,11 +62,11 @@ def _worker(rank, world, port, ckpt, q):
     os._exit(0)
 
 
-def _run_tp(ckpt, world):
+def _run_tp(ckpt, world, kv="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, q, kv)) for r in range(world)]
     for p in procs:
         p.start()
     out = q.get(timeout=300)
@@ -76,18 +76,21 @@ def _run_tp(ckpt, world):
     return out
 
 
-@pytest.mark.parametrize("preset,world", [("tiny-llama", 2), ("tiny-llama", 4), ("tiny-mixtral", 2)])
-def test_tp_matches_tp1(tmp_path, preset, world):
+@pytest.mark.parametrize("preset,world,kv", [("tiny-llama", 2, "auto"), ("tiny-llama", 4, "auto"),
+                                           ("tiny-mixtral", 2, "auto"), ("tiny-llama", 2, "fp8")])
+def test_tp_matches_tp1(tmp_path, preset, world, kv):
+    """kv fp8: each rank keeps its kv heads' e4m3 blocks (--kv-cache-dtype fp8); the
+    rounding is per element, so TP = N still equals TP = 1 with the same cache type."""
     cfg = PRESETS[preset]
     ckpt = str(tmp_path / preset)
     save_hf_checkpoint(ckpt, cfg, random_hf_tensors(cfg, seed=7))
     from hipserve.engine.llm_engine import LLMEngine
     from hipserve.parallel.comm import TPGroup
 
-    ref = LLMEngine(_cfg(ckpt, 1), tp=TPGroup())
+    ref = LLMEngine(_cfg(ckpt, 1, kv), tp=TPGroup())
     want = [r[0] for r in ref.generate(PROMPTS, SamplingParams(temperature=0.0, max_tokens=8,
                                                                 ignore_eos=True))]
-    got = _run_tp(ckpt, world)
+    got = _run_tp(ckpt, world, kv)
     assert got == want
 
 
