@@ -1,4 +1,4 @@
-// FP8 W8A8 decode GEMM (SURVEY K6/K7 for the FP8-Dynamic checkpoints at M <= 64):
+// FP8 W8A8 decode GEMM (SURVEY K6/K7 for the FP8-Dynamic checkpoints at M <= 256):
 //   ws[s, m, n] = (sum over K slice s of xq[m, k] . wq[n, k]) * xs[m] * rs[n] / 256
 // xq / xs: per-token dynamic e4m3 activations (act_quant_fp8, prefill_gemm.hip), wq / rs:
 // the per-channel e4m3 weight in the decode tiled layout (ops/quant.py
@@ -181,14 +181,20 @@ bool fp8_decode_steps_ok(int steps) {
   }
 }
 
+// M <= 256: the decode graph buckets above 64 rows (max_num_seqs 256, the chart default)
+// stream the weight once too — 8 / 16 x-tiles per wave (acc 32 / 64 VGPRs; the x slice
+// ring is 70 / 139 KiB of LDS, so 2 / 1 workgroups per CU) instead of the prefill GEMM,
+// whose few 256-row tiles left most of the chip idle at these row counts
 bool launch_fp8_decode_gemm(float* ws, const void* xq, const PgF8& W, int M, int N, int K, int S, hipStream_t s) {
-  if (M < 1 || M > 64 || K % 256 || S < 1 || (K >> 8) % S || N % 16) return false;
+  if (M < 1 || M > 256 || K % 256 || S < 1 || (K >> 8) % S || N % 16) return false;
   for (int i = 0; i < W.n; ++i)
     if (W.p[i].rows % 16) return false;
   auto* x = static_cast<const unsigned char*>(xq);
   if (M <= 16) return fd_launch<1>(ws, x, W, M, N, K, S, s);
   if (M <= 32) return fd_launch<2>(ws, x, W, M, N, K, S, s);
-  return fd_launch<4>(ws, x, W, M, N, K, S, s);
+  if (M <= 64) return fd_launch<4>(ws, x, W, M, N, K, S, s);
+  if (M <= 128) return fd_launch<8>(ws, x, W, M, N, K, S, s);
+  return fd_launch<16>(ws, x, W, M, N, K, S, s);
 }
 
 }  // namespace hipserve

@@ -266,7 +266,10 @@ template <typename KV>
 static void rope_cache_t(unsigned short* q, long qkv_stride, const long* positions, const long* slots,
                          const float* cos_sin, KV* kc, KV* vc, int T, int nq, int nkv, int D, int block_size,
                          int mode, hipStream_t s) {
-  if (T >= 128 && nkv * D <= 2048 && rope_tile_enabled()) {  // prefill chunks
+  // prefill chunks: the tile kernel (one workgroup per 16 tokens) only once there are
+  // >= 128 of them; below that the per-token kernel's wider grid wins (tools/bench_rope.py:
+  // 256 tokens 6-7 vs 13-17 us, 1,024 tokens within +-2 us, 4,096 tokens 23-33 vs 32-51 us)
+  if (T >= 2048 && nkv * D <= 2048 && rope_tile_enabled()) {
     const dim3 tg((T + kRopeTile - 1) / kRopeTile);
     const size_t smem = (size_t)kRopeTile * (nkv * D + 8) * sizeof(unsigned short);
     if (mode == 0)

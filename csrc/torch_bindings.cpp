@@ -891,7 +891,7 @@ void fp8_decode_gemm(at::Tensor& ws, const at::Tensor& xq, const at::Tensor& xs,
   c10::hip::HIPGuardMasqueradingAsCUDA g(xq.device());
   TORCH_CHECK(hipserve::launch_fp8_decode_gemm(ws.data_ptr<float>(), xq.data_ptr(), W, M, rows, K, (int)splits,
                                                cur_stream()),
-              "fp8_decode_gemm: unsupported (M <= 64, part rows % 16, (K / 256) / splits in the kernel's step set)");
+              "fp8_decode_gemm: unsupported (M <= 256, part rows % 16, (K / 256) / splits in the kernel's step set)");
 }
 
 // [gate | up] rows -> per-token e4m3 act (q8 [rows, I] uint8, xs [rows] fp32), optionally

@@ -168,7 +168,9 @@ class ModelRunner:
             if qws:  # GGUF: split-K of the dequant-MFMA decode GEMM per shape and batch
                 from ..ops import quant as Q
 
-                self.gguf_split_report = Q.tune_splits(qws, self.device, [m for m in Q.M_BUCKETS if m <= 64])
+                self.gguf_split_report = Q.tune_splits(
+                    qws, self.device, [m for m in Q.M_BUCKETS if m <= 64],
+                    f8_ms=[m for m in Q.F8_M_BUCKETS if m <= max(64, max(self.buckets, default=1))])
                 # GGUF prefill: the block kernel or dequant + hipBLASLt per shape, timed at the
                 # token budget (the LM head only sees a few rows per prefill: not timed)
                 lm = getattr(self.model, "lm_head", None)

@@ -835,7 +835,10 @@ class LlamaModel:
             fc = gemm.fused_choice(x.shape[0], w)
             return gemm.gemm_partial(x, w, fc) if fc is not None else None
         from ..ops import quant as Q
-        if getattr(w, "v2", False) and x.shape[0] <= Q.MAX_FUSED_M and x.is_cuda:
+        M = x.shape[0]
+        # FP8 W8A8 above 64 rows: TP = 1 (the cross-rank epilogues are sized for <= 64 rows)
+        if getattr(w, "v2", False) and x.is_cuda and (M <= Q.MAX_FUSED_M or (
+                M <= Q.F8_DECODE_MAX_M and self.tp.world_size == 1 and Q.f8_decode_ok(w))):
             return Q.quant_partial(x, w, x16, x8)
         return None
 
@@ -873,7 +876,7 @@ class LlamaModel:
         when the consumer runs the W8A8 FP8 decode GEMM (bit-identical to quantising
         ``like`` afterwards; one act_quant_fp8 launch fewer); None otherwise."""
         from ..ops import quant as Q
-        if (self.tp.world_size != 1 or not like.is_cuda or like.shape[0] > Q.MAX_FUSED_M
+        if (self.tp.world_size != 1 or not like.is_cuda or like.shape[0] > Q.F8_DECODE_MAX_M
                 or not Q.f8_decode_ok(consumer)):
             return None
         return (torch.empty(like.shape, dtype=torch.uint8, device=like.device),

@@ -31,6 +31,11 @@ FP8, FP8B = 1000, 1001
 INT8 = 1002
 KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7, INT8: 8}
 MAX_FUSED_M = 64
+# the W8A8 FP8 decode GEMM (fp8_decode.hip) also takes the decode graph buckets above 64
+# rows (up to 256, max_num_seqs' default): one weight stream per step instead of the
+# prefill GEMM, which left most of the chip idle at these row counts — Gemma-3-27B FP8 at
+# 256 sequences: 35.2 ms of FP8 GEMMs per decode step (0.8 TB/s)
+F8_DECODE_MAX_M = 256
 # prefill chunks up to this many tokens without a bf16 shadow run the dequant-MFMA
 # kernel swept over 64-row M tiles (K15: no [N, K] bf16 dequant pass, which costs more
 # than the GEMM itself at small M); larger chunks dequantise into scratch + hipBLASLt.
@@ -378,6 +383,7 @@ def _actual_splits(nsb: int, S: int) -> int:
 # (weight signature, M bucket) -> S, measured by tune_splits at engine start
 SPLIT_TABLE: dict = {}
 M_BUCKETS = (1, 8, 16, 32, 48, 64)
+F8_M_BUCKETS = M_BUCKETS + (128, 256)  # split tables of the FP8 decode GEMM
 PARTIAL_READ_BPS = 5e12   # the fused epilogue re-reads the fp32 partials at ~HBM rate
 COLD_BYTES = 768 << 20    # split timing rotates over block copies of at least this many bytes
 
@@ -387,10 +393,10 @@ def _sig(w: QuantWeight):
 
 
 def _bucket(M: int) -> int:
-    for b in M_BUCKETS:
+    for b in F8_M_BUCKETS:
         if M <= b:
             return b
-    return M_BUCKETS[-1]
+    return F8_M_BUCKETS[-1]
 
 
 def v2_splits(w: QuantWeight, M: int) -> int:
@@ -458,11 +464,14 @@ def _graph_time_us(fn, reps: int = 10, rounds: int = 3) -> float:
 
 @torch.inference_mode()  # like the engine's graph capture: a process may hold several engines, and the
 # generator state tensors a capture registers must not switch between inference and normal tensors
-def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) -> list:
+def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20, f8_ms=None) -> list:
     """Measure the v2 decode GEMM per distinct QuantWeight shape and M bucket for
     S in {1, 2, 4, ...} and keep the S minimising kernel time + the epilogue's
     re-read of the partials (S*M*N*4 B at PARTIAL_READ_BPS). Timed inside a
-    hipGraph (the decode step's launch mode). Returns report rows."""
+    hipGraph (the decode step's launch mode). ``f8_ms``: the M buckets of the FP8 W8A8
+    decode GEMM's weights (default ``ms``; it also serves buckets above 64 rows).
+    Returns report rows."""
+    f8_ms = list(ms) if f8_ms is None else list(f8_ms)
     from . import tune_cache as TC
 
     seen, report = {}, []
@@ -471,19 +480,20 @@ def tune_splits(weights, device, ms=M_BUCKETS, max_ws_bytes: int = 256 << 20) ->
             seen.setdefault(_sig(w), w)
     for sig in list(seen):  # timed by a previous start on this device and kernel build
         kind = "f8_splits" if f8_decode_ok(seen[sig]) else "gguf_splits"
-        hits = [TC.get(device, kind, [list(map(list, sig[1])), sig[0], M]) for M in ms]
+        mlist = f8_ms if kind == "f8_splits" else ms
+        hits = [TC.get(device, kind, [list(map(list, sig[1])), sig[0], M]) for M in mlist]
         if all(h is not None for h in hits):
-            for M, h in zip(ms, hits):
+            for M, h in zip(mlist, hits):
                 (F8_SPLIT_TABLE if kind == "f8_splits" else SPLIT_TABLE)[(sig, _bucket(M))] = h["S"]
                 report.append(dict(h["row"], cached=True))
             del seen[sig]
-    nbuf = max((4 * w.N * max(ms) * 32 for w in seen.values()), default=0)
+    nbuf = max((4 * w.N * max(f8_ms if f8_decode_ok(w) else ms) * 32 for w in seen.values()), default=0)
     ws = torch.empty(min(nbuf, max_ws_bytes) // 4, dtype=torch.float32, device=device)
     empty = _empty(device, torch.bfloat16)
     for sig, w in seen.items():
         nsb = w.K // 256
-        if f8_decode_ok(w):  # these run the W8A8 FP8 decode GEMM at M <= 64
-            report += _tune_f8_decode(w, ms, ws)
+        if f8_decode_ok(w):  # these run the W8A8 FP8 decode GEMM (M <= F8_DECODE_MAX_M)
+            report += _tune_f8_decode(w, f8_ms, ws)
             continue
         # cold weights, as in a decode step (every layer's blocks read once from HBM): the
         # timed calls rotate over copies of the blocks totalling >= COLD_BYTES, so the
@@ -606,7 +616,7 @@ def quant_partial(x: torch.Tensor, w: QuantWeight, x16: torch.Tensor | None = No
     the producer's f16 pair-order copy of x (splitk_add_rmsnorm / splitk_glu
     ``out16``), staged as is instead of converting x in every workgroup."""
     M = x.shape[0]
-    if M <= MAX_FUSED_M and f8_decode_ok(w):
+    if M <= F8_DECODE_MAX_M and f8_decode_ok(w):
         return f8_decode_partial(x, w, x8)
     S = v2_splits(w, M)
     ws = torch.empty(S * M * w.N, dtype=torch.float32, device=x.device)
@@ -712,7 +722,8 @@ def quant_linear(x: torch.Tensor, w: QuantWeight) -> torch.Tensor:
     out = torch.empty(M, w.N, dtype=torch.bfloat16, device=x.device)
     if M == 0:
         return out
-    if M <= MAX_FUSED_M and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+    if (M <= MAX_FUSED_M or (M <= F8_DECODE_MAX_M and x.is_cuda and f8_decode_ok(w))) and x.stride(1) == 1 \
+            and x.stride(0) % 8 == 0:
         if x.is_cuda and f8_decode_ok(w):  # the fused path's partials, reduced: bit-identical to it
             ws, S = f8_decode_partial(x, w)
             torch.ops.hipserve.splitk_reduce(out, ws, S)

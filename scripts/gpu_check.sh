@@ -206,6 +206,10 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     prefkv) for kv in bf16 fp8; do DECODE_KV=$kv BENCH_PREFILL_VERS=v2w8 timeout -k 10 300 python -u tools/bench_ops.py prefill > $OUT/prefkv_$kv.log 2>&1 || exit 1; echo "kv $kv"; grep prefill_attention $OUT/prefkv_$kv.log; done ;;
     deckvnt) for nt in 1 0; do DECODE_KV=fp8 HIPSERVE_DECODE_NT=$nt DECODE_COLD=1 DECODE_SHAPES=64x1152x32x8,64x1152x32x16,64x4096x32x8 DECODE_PARTS=2048 \
       timeout -k 10 300 python -u tools/bench_ops.py decode > $OUT/deckv_nt$nt.log 2>&1 || exit 1; echo "fp8 nt $nt"; grep paged_decode $OUT/deckv_nt$nt.log; done ;;
+    prof_q80) prof_run profq80 --quantization q8_0 ;;
+    g27fp8c256) bench_named g27fp8c256 X=1 -- --model gemma-3-27b --quantization fp8 --concurrency 256 --steps 1 ;;
+    prof_g27c256) prof_run profg27c256 --model gemma-3-27b --quantization fp8 --concurrency 256 ;;
+    ropet) for t in 1 0; do HIPSERVE_ROPE_TILE=$t timeout -k 10 180 python -u tools/bench_rope.py --T 128 256 512 1024 2048 4096 > $OUT/ropet$t.log 2>&1 || exit 1; grep '"aligned"' $OUT/ropet$t.log; done ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done

@@ -38,9 +38,10 @@ def _x(g, M, K):
     return x.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 65, 128, 200, 256])
 @pytest.mark.parametrize("rows,K", [([512, 256, 256], 4096), ([768], 5376), ([256], 21504), ([1024, 1024], 1792)])
 def test_fp8_decode_gemm_vs_fp32(M, rows, K):
+    """M 65..256: the 8 / 16 x-tile bodies of the decode graph buckets above 64 rows."""
     from hipserve.ops import pgemm, quant as Q
 
     g = torch.Generator(device=DEV).manual_seed(M * 7 + K)
@@ -57,14 +58,15 @@ def test_fp8_decode_gemm_vs_fp32(M, rows, K):
         torch.testing.assert_close(got / scale, want / scale, rtol=0, atol=1e-4)
 
 
-def test_quant_linear_and_partial_use_fp8_decode():
-    """At decode sizes quant_linear = the fused path's partials reduced by
-    splitk_reduce (bit-identical), and both are W8A8."""
+@pytest.mark.parametrize("M", [48, 256])
+def test_quant_linear_and_partial_use_fp8_decode(M):
+    """At decode sizes (up to 256 rows) quant_linear = the fused path's partials reduced
+    by splitk_reduce (bit-identical), and both are W8A8."""
     from hipserve.ops import pgemm, quant as Q
 
     g = torch.Generator(device=DEV).manual_seed(9)
     w, wd = _weight(g, [512, 256, 256], 2048)
-    x = _x(g, 48, 2048)
+    x = _x(g, M, 2048)
     y = Q.quant_linear(x, w)
     ws, S = Q.quant_partial(x, w)
     r = torch.empty_like(y)

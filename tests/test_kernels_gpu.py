@@ -59,9 +59,9 @@ def _caches(nblocks, nkv, bs, D, fill=True):
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("bs", [16, 32])
 @pytest.mark.parametrize("T,layout", [(37, "random"), (300, "random"), (300, "contig"), (1000, "contig"),
-                                      (300, "aligned"), (1000, "aligned")])
+                                      (300, "aligned"), (2500, "random"), (2500, "contig"), (2100, "aligned")])
 def test_rope_cache(ops, mode, bs, T, layout):
-    """Per-token kernel (T < 128) and the 16-token tile kernel of prefill chunks
+    """Per-token kernel (T < 2048) and the 16-token tile kernel of prefill chunks
     (LDS-staged V, token-fastest V^T stores), scattered and contiguous slots
     (contig: a chunk starting mid-block; aligned: block-aligned, so whole tiles take the
     16-byte V^T store path), vs the fp32 oracle."""
@@ -69,13 +69,14 @@ def test_rope_cache(ops, mode, bs, T, layout):
     nq, nkv, D = 32, 8, 128
     qkv = torch.randn(T, (nq + 2 * nkv) * D + 64, device=DEV, dtype=torch.bfloat16)[:, : (nq + 2 * nkv) * D]
     pos = torch.randint(0, 4000, (T,), device=DEV)
+    nblk = max(64, (T + 2 * bs) // bs + 1)
     if layout == "random":
-        slots = torch.randperm(64 * bs, device=DEV)[:T]
+        slots = torch.randperm(nblk * bs, device=DEV)[:T]
     else:
         slots = torch.arange(T, device=DEV) + (5 if layout == "contig" else bs)
     slots[3] = -1
     cs = ref.rope_cos_sin(D, 4096, 500000.0).to(DEV)
-    kc, vc = _caches(64, nkv, bs, D, fill=False)
+    kc, vc = _caches(nblk, nkv, bs, D, fill=False)
     kc_r, vc_r, qkv_r = kc.cpu().clone(), vc.cpu().clone(), qkv.cpu().clone()
     ops.rope_cache(qkv, pos, slots, cs, kc, vc, nq, nkv, D, mode)
     ref.rope_cache(qkv_r, pos.cpu(), slots.cpu(), cs.cpu(), kc_r, vc_r, nq, nkv, D, mode)

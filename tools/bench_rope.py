@@ -17,12 +17,13 @@ from hipserve.ops import reference as ref
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--T", type=int, default=8192)
+    ap.add_argument("--T", type=int, nargs="+", default=[8192])
     a = ap.parse_args()
     ops = get_ops("cuda")
     dev = "cuda"
-    T, D, bs = a.T, 128, 16
-    for name, nq, nkv in (("llama-3-8b", 32, 8), ("llama-3-70b", 64, 8)):
+    D, bs = 128, 16
+    for T, (name, nq, nkv) in [(T, m) for T in a.T for m in (("llama-3-8b", 32, 8), ("llama-3-70b", 64, 8),
+                                                               ("gemma-3-27b", 32, 16))]:
         qkv = torch.randn(T, (nq + 2 * nkv) * D, device=dev, dtype=torch.bfloat16)
         pos = torch.arange(T, device=dev)
         cs = ref.rope_cos_sin(D, T + 64, 500000.0).to(dev)
@@ -43,7 +44,8 @@ def main():
             e1.record()
             e1.synchronize()
             us = e0.elapsed_time(e1) * 1000 / n
-            print(json.dumps({"model": name, "T": T, "slots": layout, "us": round(us, 1),
+            print(json.dumps({"model": name, "T": T, "slots": layout, "tile": os.environ.get("HIPSERVE_ROPE_TILE", "1"),
+                              "us": round(us, 1),
                               "TB_s": round(moved / us / 1e6, 2)}), flush=True)
 
 
