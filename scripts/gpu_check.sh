@@ -210,6 +210,12 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     g27fp8c256) bench_named g27fp8c256 X=1 -- --model gemma-3-27b --quantization fp8 --concurrency 256 --steps 1 ;;
     prof_g27c256) prof_run profg27c256 --model gemma-3-27b --quantization fp8 --concurrency 256 ;;
     ropet) for t in 1 0; do HIPSERVE_ROPE_TILE=$t timeout -k 10 180 python -u tools/bench_rope.py --T 128 256 512 1024 2048 4096 > $OUT/ropet$t.log 2>&1 || exit 1; grep '"aligned"' $OUT/ropet$t.log; done ;;
+    b8c256) bench_named b8c256 X=1 -- --concurrency 256 --steps 2 ;;
+    q4c256) bench_named q4c256 X=1 -- --quantization q4_k_m --concurrency 256 --steps 2 ;;
+    q3int8c256) bench_named q3int8c256 X=1 -- --model qwen3-30b-a3b --quantization int8 --concurrency 256 --steps 2 ;;
+    prof_b8c256) prof_run profb8c256 --concurrency 256 ;;
+    hosttime256) bench_named hosttime256 HIPSERVE_PROFILE=timing -- --path engine --concurrency 256 --steps 1 ;;
+    decblas) timeout -k 10 600 python -u tools/bench_decode_blas.py > $OUT/decblas.log 2>&1; rc=$?; cat $OUT/decblas.log; [ $rc -eq 0 ] ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done
