@@ -216,6 +216,9 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     prof_b8c256) prof_run profb8c256 --concurrency 256 ;;
     hosttime256) bench_named hosttime256 HIPSERVE_PROFILE=timing -- --path engine --concurrency 256 --steps 1 ;;
     decblas) timeout -k 10 600 python -u tools/bench_decode_blas.py > $OUT/decblas.log 2>&1; rc=$?; cat $OUT/decblas.log; [ $rc -eq 0 ] ;;
+    coalab) for r in 1 2; do bench_named coal_off_$r HIPSERVE_COALESCE_MAX_MS=0 -- --steps 5 --tp-phase off && \
+              bench_named coal_def_$r X=1 -- --steps 5 --tp-phase off || exit 1; done
+            for f in coal_off_1 coal_def_1 coal_off_2 coal_def_2; do grep -o '"value": [0-9.]*\|"p50_ttft_ms": [0-9.]*' $OUT/bench_$f.json | tr '\n' ' '; echo $f; done ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done
