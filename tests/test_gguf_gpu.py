@@ -241,8 +241,15 @@ def test_fp8_linear_matches_fp32(mode, M):
     assert (ws.view(S, M, qw.N).sum(0) - want).abs().max().item() < tol
     deq = Q.dequantize(qw).float()
     assert torch.allclose(deq, wref.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-6)
-    xp = torch.randn(100, K, device="cuda", dtype=torch.bfloat16)  # prefill path
+    # 100 rows: per-tensor / per-channel weights take the W8A8 decode GEMM up to 256 rows
+    # (decode graph buckets of max_num_seqs 256; x quantised per token, as FP8-Dynamic
+    # checkpoints specify), 128-block weights the dequantising prefill path
+    xp = torch.randn(100, K, device="cuda", dtype=torch.bfloat16)
     wantp = xp.float() @ wref.T
+    if Q.f8_decode_ok(qw):
+        from hipserve.ops import pgemm
+        xq, xs = pgemm.act_quant(xp)
+        wantp = (xq.view(torch.float8_e4m3fn).float() * xs.unsqueeze(1)) @ wref.T
     assert (Q.quant_linear(xp, qw).float() - wantp).abs().max().item() < 1e-2 * wantp.abs().max().item() + 1e-4
 
 
