@@ -253,7 +253,7 @@ void launch_pack_decode_weight(void* out, const void* w, int N, int K, bool glu,
 namespace hipserve {
 // moe.hip — tile in {16, 32, 64}
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
-                             bool renorm, hipStream_t s);
+                             bool renorm, hipStream_t s, int splits = 0);
 void launch_moe_align(const int* ids, int npairs, int E, int tile, int* slots, int slots_cap, int* tile_expert,
                       int tiles_cap, int* num_tiles, int* pair_slot, int* group_end, hipStream_t s,
                       int* hist = nullptr);

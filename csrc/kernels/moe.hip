@@ -25,10 +25,13 @@ HS_DEVICE float ld_f<float>(const float* p, long i) { return p[i]; }
 // One wave per token, expert e on lane e % 64, slot e / 64 (E <= 128). renorm:
 // weights / sum over the selected k (Mixtral, Qwen3-MoE norm_topk_prob); else the
 // plain softmax probabilities of the selected experts.
+// S > 0: ``logits`` are the router decode GEMM's fp32 split-K partials [S, T, E]; each
+// logit is their in-order sum rounded to bf16, as splitk_reduce would have written it
+// (bit-identical to reduce + this kernel, one launch fewer per MoE layer).
 template <typename T>
 __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restrict__ logits, float* __restrict__ w,
                                                                int* __restrict__ ids, int Tn, int E, int k,
-                                                               int renorm) {
+                                                               int renorm, int S = 0) {
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= Tn) return;
@@ -37,6 +40,22 @@ __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restri
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int e = lane + 64 * s;
+    if constexpr (sizeof(T) == 4) {
+      if (S > 0) {  // 8 slices' loads in flight at a time, summed in slice order
+        float acc = 0.f;
+        const int ec = e < E ? e : 0;
+        for (int j0 = 0; j0 < S; j0 += 8) {
+          float pv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) pv[i] = j0 + i < S ? ld_f<T>(logits, ((long)(j0 + i) * Tn + t) * E + ec) : 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (j0 + i < S) acc += pv[i];
+        }
+        v[s] = e < E ? bf16_to_f32(f32_to_bf16(acc)) : -INFINITY;
+        continue;
+      }
+    }
     v[s] = e < E ? ld_f<T>(logits, (long)t * E + e) : -INFINITY;
   }
   const float mx = wave_max(fmaxf(v[0], v[1]));
@@ -318,12 +337,12 @@ __global__ __launch_bounds__(256) void moe_combine_partial_kernel(unsigned short
 }
 
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
-                             bool renorm, hipStream_t s) {
+                             bool renorm, hipStream_t s, int splits) {
   if (T <= 0) return;
   dim3 grid((T + 3) / 4), block(256);
   if (logits_f32)
     moe_topk_softmax_kernel<float><<<grid, block, 0, s>>>(static_cast<const float*>(logits), w, ids, T, E, k,
-                                                          renorm ? 1 : 0);
+                                                          renorm ? 1 : 0, splits);
   else
     moe_topk_softmax_kernel<unsigned short><<<grid, block, 0, s>>>(static_cast<const unsigned short*>(logits), w, ids,
                                                                    T, E, k, renorm ? 1 : 0);

@@ -505,16 +505,29 @@ void skinny_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, int6
               "skinny_gemm: unsupported (rt, kw)");
 }
 
-void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, int64_t k, bool renorm) {
+// splits > 0: logits = the router decode GEMM's fp32 split-K partials, flat [splits, T, E]
+// with T = w.size(0) (summed in order and rounded to bf16 in the kernel: no reduce launch)
+void moe_topk_softmax(at::Tensor& w, at::Tensor& ids, const at::Tensor& logits, int64_t k, bool renorm,
+                      int64_t splits) {
   CHECK_DEV(logits); CHECK_CONTIG(logits); CHECK_CONTIG(w); CHECK_CONTIG(ids);
-  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 128, "moe: <= 128 experts");
   TORCH_CHECK(w.scalar_type() == at::kFloat && ids.scalar_type() == at::kInt);
   TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16);
-  const int T = logits.size(0);
-  TORCH_CHECK(w.numel() >= T * k && ids.numel() >= T * k && k >= 1 && k <= logits.size(1));
+  int T, E;
+  if (splits > 0) {
+    TORCH_CHECK(logits.scalar_type() == at::kFloat && w.dim() == 2, "moe_topk_softmax: fp32 partials, w [T, k]");
+    T = w.size(0);
+    TORCH_CHECK(T > 0 && logits.numel() % (splits * T) == 0, "moe_topk_softmax: partials [splits, T, E]");
+    E = logits.numel() / (splits * T);
+  } else {
+    TORCH_CHECK(logits.dim() == 2, "moe_topk_softmax: logits [T, E]");
+    T = logits.size(0);
+    E = logits.size(1);
+  }
+  TORCH_CHECK(E <= 128, "moe: <= 128 experts");
+  TORCH_CHECK(w.numel() >= T * k && ids.numel() >= T * k && k >= 1 && k <= E);
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   hipserve::launch_moe_topk_softmax(logits.data_ptr(), logits.scalar_type() == at::kFloat, w.data_ptr<float>(),
-                                    ids.data_ptr<int>(), T, logits.size(1), k, renorm, cur_stream());
+                                    ids.data_ptr<int>(), T, E, k, renorm, cur_stream(), (int)splits);
 }
 
 int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes, int64_t nb_large) {
@@ -1235,7 +1248,7 @@ void vision_attention(at::Tensor& out, at::Tensor& qkv, const at::Tensor& cos_si
 }  // namespace
 
 TORCH_LIBRARY(hipserve, m) {
-  m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k, bool renorm=True) -> ()");
+  m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k, bool renorm=True, int splits=0) -> ()");
   m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot, Tensor(e!)? group_end=None) -> ()");
   m.def("moe_gather(Tensor(a!) out, Tensor x, Tensor slots, int k) -> ()");
   m.def("moe_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k) -> ()");

@@ -826,6 +826,25 @@ class LlamaModel:
         ws = [self.lm_head] + [getattr(lw, n) for lw in self.layers for n in ("wqkv", "wo", "wgu", "wd")]
         return [w for w in ws if isinstance(w, Q.QuantWeight)]
 
+    def _route(self, x: torch.Tensor, lw, k: int):
+        """(weights [T, k] fp32, expert ids [T, k] int32) of the top-k softmax over the
+        router logits x @ router^T. When the start-up timing picked the decode GEMM for the
+        router at this row count, its fp32 split-K partials go straight into the top-k
+        kernel, which sums and rounds them as splitk_reduce would (bit-identical, one
+        launch fewer per MoE layer)."""
+        op = torch.ops.hipserve
+        T, dev = x.shape[0], x.device
+        w = torch.empty(T, k, dtype=torch.float32, device=dev)
+        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
+        fc = (gemm.fused_choice(T, lw.router)
+              if x.is_cuda and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None)
+        if fc is not None:
+            ws, S = gemm.gemm_partial(x, lw.router, fc)
+            op.moe_topk_softmax(w, ids, ws, k, self.cfg.norm_topk_prob, S)
+        else:
+            op.moe_topk_softmax(w, ids, gemm.linear(x, lw.router), k, self.cfg.norm_topk_prob)
+        return w, ids
+
     def _partial(self, x: torch.Tensor, w, x16: torch.Tensor | None = None, x8=None):
         """(fp32 split-K partials [S, M, N], S) of ``x @ w.T`` for a fused decode
         epilogue: the tuned bf16 decode GEMM, or the GGUF MFMA GEMM for a
@@ -1012,10 +1031,7 @@ class LlamaModel:
         P = T * k
         tile = 128 * gemm.PW_WM
         cap = -(-(P + E * (tile - 1)) // tile) * tile
-        logits = gemm.linear(x, lw.router)
-        w = torch.empty(T, k, dtype=torch.float32, device=dev)
-        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
-        op.moe_topk_softmax(w, ids, logits, k, cfg.norm_topk_prob)
+        w, ids = self._route(x, lw, k)
         slots = torch.empty(cap, dtype=torch.int32, device=dev)
         tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
         ntiles = torch.empty(1, dtype=torch.int32, device=dev)
@@ -1160,10 +1176,7 @@ class LlamaModel:
         P = T * k
         tile = 16 if P <= 8 * E else (32 if P <= 32 * E else 64)
         cap = -(-(P + E * (tile - 1)) // tile) * tile
-        logits = gemm.linear(x, lw.router)
-        w = torch.empty(T, k, dtype=torch.float32, device=dev)
-        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
-        op.moe_topk_softmax(w, ids, logits, k, cfg.norm_topk_prob)
+        w, ids = self._route(x, lw, k)
         slots = torch.empty(cap, dtype=torch.int32, device=dev)
         tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
         ntiles = torch.empty(1, dtype=torch.int32, device=dev)
@@ -1214,10 +1227,7 @@ class LlamaModel:
         P = T * k
         tile = 16 if P <= 8 * E else (32 if P <= 32 * E else 64)
         cap = -(-(P + E * (tile - 1)) // tile) * tile
-        logits = gemm.linear(x, lw.router)
-        w = torch.empty(T, k, dtype=torch.float32, device=dev)
-        ids = torch.empty(T, k, dtype=torch.int32, device=dev)
-        op.moe_topk_softmax(w, ids, logits, k, cfg.norm_topk_prob)
+        w, ids = self._route(x, lw, k)
         slots = torch.empty(cap, dtype=torch.int32, device=dev)
         tile_expert = torch.empty(cap // tile, dtype=torch.int32, device=dev)
         ntiles = torch.empty(1, dtype=torch.int32, device=dev)

@@ -219,6 +219,7 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
     coalab) for r in 1 2; do bench_named coal_off_$r HIPSERVE_COALESCE_MAX_MS=0 -- --steps 5 --tp-phase off && \
               bench_named coal_def_$r X=1 -- --steps 5 --tp-phase off || exit 1; done
             for f in coal_off_1 coal_def_1 coal_off_2 coal_def_2; do grep -o '"value": [0-9.]*\|"p50_ttft_ms": [0-9.]*' $OUT/bench_$f.json | tr '\n' ' '; echo $f; done ;;
+    topktest) timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_quant_moe_gpu.py tests/test_families_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "topk or moe or family" > $OUT/topktest.log 2>&1; rc=$?; tail -n 5 $OUT/topktest.log; [ $rc -eq 0 ] ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done

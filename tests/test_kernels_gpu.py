@@ -358,6 +358,23 @@ def test_decode_gemm_packed(ops, M, N, K, rt, splits):
     _close(out, want, atol=2e-2 * want.abs().max().item(), rtol=1e-2)
 
 
+@pytest.mark.parametrize("T,E,k,S", [(1, 8, 2, 1), (64, 128, 8, 4), (37, 64, 4, 8), (64, 16, 4, 2)])
+def test_moe_topk_softmax_from_partials(ops, T, E, k, S):
+    """The router's fp32 split-K partials summed inside the top-k kernel == splitk_reduce
+    to bf16 + the top-k kernel over those logits, bit for bit (ids and weights)."""
+    torch.manual_seed(T * 31 + E + S)
+    ws = torch.randn(S, T, E, device=DEV) * 2
+    logits = torch.empty(T, E, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.splitk_reduce(logits, ws.reshape(-1), S)
+    w0 = torch.empty(T, k, device=DEV)
+    i0 = torch.empty(T, k, device=DEV, dtype=torch.int32)
+    torch.ops.hipserve.moe_topk_softmax(w0, i0, logits, k, True)
+    w1 = torch.full((T, k), float("nan"), device=DEV)
+    i1 = torch.full((T, k), -1, device=DEV, dtype=torch.int32)
+    torch.ops.hipserve.moe_topk_softmax(w1, i1, ws.reshape(-1), k, True, S)
+    assert torch.equal(i0, i1) and torch.equal(w0, w1)
+
+
 @pytest.mark.parametrize("mode", ["packed", "rowmajor", "legacy"])
 @pytest.mark.parametrize("T,E,k,norm", [(1, 8, 2, True), (13, 8, 2, True), (64, 8, 2, True), (200, 8, 2, True),
                                         (5, 4, 1, True), (3, 128, 8, True), (40, 128, 8, False), (9, 64, 4, False)])

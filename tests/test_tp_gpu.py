@@ -241,7 +241,7 @@ def force_blas_tuning_cache(cache_dir, mode="all"):
                     dg = [c for c in self.candidates(M, N, K, glu=glu) if c[0] == "dg" and c[1] != 3]
                     best = dg[0] if dg else "blas"
                 row = {"M": M, "N": N, "K": K, "unit": "forced", "best": str(best)}
-                TC.put(device, "decode_gemm", [M, N, K, spec], {"best": best, "bp": None, "row": row})
+                TC.put(device, gemm.TC_KIND, [M, N, K, spec], {"best": best, "bp": None, "row": row})
         TC.flush()
         rep = orig(self, shapes, device, ms, fused)
         assert rep and all(r.get("cached") for r in rep), "tuner re-timed a pre-populated shape"

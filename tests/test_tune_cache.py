@@ -56,7 +56,7 @@ def test_gemm_tuner_reuses_cached_shapes(cache, monkeypatch):
     fallback choice and the report come from the cache."""
     dev = torch.device("cuda", 0)
     for M in (1, 64):
-        TC.put(dev, "decode_gemm", [M, 256, 512, None],
+        TC.put(dev, gemm.TC_KIND, [M, 256, 512, None],
                {"best": ["dgp", 3, 2], "bp": [["dgp", 3, 2], 4.5], "row": {"M": M, "N": 256, "K": 512}})
     t = gemm.GemmTuner()
 
