@@ -270,6 +270,11 @@ void launch_moe_combine(void* out, const void* y, const float* w, const int* pai
 // out[t] = sum_j w[t, j] * bf16(sum_s ws[s, pair_slot[t*k + j], :]) — split-K partials of the w2 GEMM
 void launch_moe_combine_partial(void* out, const float* ws, long slab, int S, const float* w, const int* pair_slot,
                                 int T, int k, int H, hipStream_t s);
+// combine (bf16 y [slots, H] when S == 0, fp32 partials [S, slots, H] else) + residual add +
+// RMSNorm (norm_w bf16 or fp32 [H]) -> out [T, H], residual [T, H] in place
+void launch_moe_combine_add_rmsnorm(void* out, void* residual, const void* y, long slab, int S, const float* w,
+                                    const int* pair_slot, int T, int k, int H, const void* norm_w, bool norm_f32,
+                                    float eps, hipStream_t s);
 // decode_gemm.hip: expert GEMM on moe_align tiles (see there)
 bool launch_moe_decode_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* w,
                             long w_estride, const int* slots, const int* tile_expert, int tiles_cap, int tile,

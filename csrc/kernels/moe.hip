@@ -336,6 +336,112 @@ __global__ __launch_bounds__(256) void moe_combine_partial_kernel(unsigned short
   }
 }
 
+// Decode MoE tail in one kernel: the weighted combine of a token's k expert rows (bf16
+// y [slots, H], or fp32 w2 partials [S, slots, H] summed per pair in slice order) rounded
+// to bf16 as moe_combine(_partial) writes it, then the residual add and the NEXT layer's
+// RMSNorm exactly as fused_add_rmsnorm (norm.hip: same thread -> element map, same block
+// reduction): bit-identical to the two-kernel chain, one launch fewer per MoE layer.
+template <int NT, int VPT, bool kWF32, bool kPartial>
+__global__ __launch_bounds__(NT) void moe_combine_add_rmsnorm_kernel(
+    unsigned short* __restrict__ out, unsigned short* __restrict__ residual, const void* __restrict__ y, long slab,
+    int S, const float* __restrict__ w, const int* __restrict__ pair_slot, int k, int H,
+    const void* __restrict__ weight, float eps) {
+  __shared__ float scratch[16];
+  const int t = blockIdx.x;
+  const int nvec = H >> 3;
+  u16x8* rr = reinterpret_cast<u16x8*>(residual + (long)t * H);
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < k; ++j) {
+        const float wt = w[(long)t * k + j];
+        const long row = (long)pair_slot[t * k + j] * H + 8 * idx;
+        if constexpr (kPartial) {
+          f32x4 lo, hi;
+          sum_slices8(lo, hi, static_cast<const float*>(y) + row, slab, S);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[e] += wt * bf16_to_f32(f32_to_bf16(lo[e]));
+            acc[e + 4] += wt * bf16_to_f32(f32_to_bf16(hi[e]));
+          }
+        } else {
+          const u16x8 yv = *reinterpret_cast<const u16x8*>(static_cast<const unsigned short*>(y) + row);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += wt * bf16_to_f32(yv[e]);
+        }
+      }
+      const u16x8 b = rr[idx];
+      u16x8 sres;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = bf16_to_f32(f32_to_bf16(acc[e])) + bf16_to_f32(b[e]);
+        sres[e] = f32_to_bf16(f);
+        v[i][e] = bf16_to_f32(sres[e]);
+      }
+      rr[idx] = sres;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / H + eps);
+  u16x8* orow = reinterpret_cast<u16x8*>(out + (long)t * H);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (idx < nvec) {
+      float wv[8];
+      if constexpr (kWF32) {
+        const f32x4* wp = reinterpret_cast<const f32x4*>(weight) + idx * 2;
+        const f32x4 w0 = wp[0], w1 = wp[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { wv[e] = w0[e]; wv[e + 4] = w1[e]; }
+      } else {
+        const u16x8 wb = reinterpret_cast<const u16x8*>(weight)[idx];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wv[e] = bf16_to_f32(wb[e]);
+      }
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f32_to_bf16(v[i][e] * inv * wv[e]);
+      orow[idx] = o;
+    }
+  }
+}
+
+template <bool kWF32, bool kPartial>
+static void mcn_launch(void* out, void* residual, const void* y, long slab, int S, const float* w, const int* ps,
+                       int T, int k, int H, const void* nw, float eps, hipStream_t s) {
+  auto* o = static_cast<unsigned short*>(out);
+  auto* r = static_cast<unsigned short*>(residual);
+  const int nvec = H / 8;
+  if (norm_threads(H) == 256) {
+    if (nvec <= 256) moe_combine_add_rmsnorm_kernel<256, 1, kWF32, kPartial><<<T, 256, 0, s>>>(o, r, y, slab, S, w, ps, k, H, nw, eps);
+    else moe_combine_add_rmsnorm_kernel<256, 2, kWF32, kPartial><<<T, 256, 0, s>>>(o, r, y, slab, S, w, ps, k, H, nw, eps);
+  } else {
+    if (nvec <= 512) moe_combine_add_rmsnorm_kernel<512, 1, kWF32, kPartial><<<T, 512, 0, s>>>(o, r, y, slab, S, w, ps, k, H, nw, eps);
+    else if (nvec <= 1024) moe_combine_add_rmsnorm_kernel<512, 2, kWF32, kPartial><<<T, 512, 0, s>>>(o, r, y, slab, S, w, ps, k, H, nw, eps);
+    else moe_combine_add_rmsnorm_kernel<512, 4, kWF32, kPartial><<<T, 512, 0, s>>>(o, r, y, slab, S, w, ps, k, H, nw, eps);
+  }
+}
+
+void launch_moe_combine_add_rmsnorm(void* out, void* residual, const void* y, long slab, int S, const float* w,
+                                    const int* pair_slot, int T, int k, int H, const void* norm_w, bool norm_f32,
+                                    float eps, hipStream_t s) {
+  if (T <= 0) return;
+  if (S > 0) {
+    if (norm_f32) mcn_launch<true, true>(out, residual, y, slab, S, w, pair_slot, T, k, H, norm_w, eps, s);
+    else mcn_launch<false, true>(out, residual, y, slab, S, w, pair_slot, T, k, H, norm_w, eps, s);
+  } else {
+    if (norm_f32) mcn_launch<true, false>(out, residual, y, slab, 0, w, pair_slot, T, k, H, norm_w, eps, s);
+    else mcn_launch<false, false>(out, residual, y, slab, 0, w, pair_slot, T, k, H, norm_w, eps, s);
+  }
+}
+
 void launch_moe_topk_softmax(const void* logits, bool logits_f32, float* w, int* ids, int T, int E, int k,
                              bool renorm, hipStream_t s, int splits) {
   if (T <= 0) return;

@@ -1199,6 +1199,33 @@ void moe_combine_partial(at::Tensor& out, const at::Tensor& ws, const at::Tensor
                                        w.data_ptr<float>(), pair_slot.data_ptr<int>(), T, k, H, cur_stream());
 }
 
+// moe_combine(_partial) + fused_add_rmsnorm in one launch (decode MoE tail, TP = 1):
+// y bf16 [slots, H] (splits 0) or fp32 partials [splits, slots, H]; out = RMSNorm(residual
+// += combine) * norm_w
+void moe_combine_add_rmsnorm(at::Tensor& out, at::Tensor& residual, const at::Tensor& y, int64_t splits,
+                             const at::Tensor& w, const at::Tensor& pair_slot, int64_t k, const at::Tensor& norm_w,
+                             double eps) {
+  CHECK_DEV(y); CHECK_BF16(out); CHECK_BF16(residual); CHECK_CONTIG(out); CHECK_CONTIG(residual); CHECK_CONTIG(y);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && pair_slot.scalar_type() == at::kInt);
+  const int T = out.size(0), H = out.size(1);
+  TORCH_CHECK(residual.sizes() == out.sizes() && H % 8 == 0 && H <= 16384 && w.numel() >= T * k &&
+              pair_slot.numel() >= T * k, "moe_combine_add_rmsnorm: shapes");
+  TORCH_CHECK(norm_w.numel() == H && norm_w.is_contiguous() &&
+              (norm_w.scalar_type() == at::kBFloat16 || norm_w.scalar_type() == at::kFloat));
+  long slab = 0;
+  if (splits > 0) {
+    TORCH_CHECK(y.scalar_type() == at::kFloat && y.dim() == 3 && y.size(0) >= splits && y.size(2) == H,
+                "moe_combine_add_rmsnorm: partials [S, slots, H] fp32");
+    slab = y.stride(0);
+  } else {
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(1) == H, "moe_combine_add_rmsnorm: y [slots, H]");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
+  hipserve::launch_moe_combine_add_rmsnorm(out.data_ptr(), residual.data_ptr(), y.data_ptr(), slab, (int)splits,
+                                           w.data_ptr<float>(), pair_slot.data_ptr<int>(), T, k, H, norm_w.data_ptr(),
+                                           norm_w.scalar_type() == at::kFloat, (float)eps, cur_stream());
+}
+
 // ---- vision tower (vision.hip)
 void layernorm(at::Tensor& out, const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                const c10::optional<at::Tensor>& residual, double eps) {
@@ -1249,6 +1276,7 @@ void vision_attention(at::Tensor& out, at::Tensor& qkv, const at::Tensor& cos_si
 
 TORCH_LIBRARY(hipserve, m) {
   m.def("moe_topk_softmax(Tensor(a!) w, Tensor(b!) ids, Tensor logits, int k, bool renorm=True, int splits=0) -> ()");
+  m.def("moe_combine_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor y, int splits, Tensor w, Tensor pair_slot, int k, Tensor norm_w, float eps) -> ()");
   m.def("moe_align(Tensor ids, int E, int tile, Tensor(a!) slots, Tensor(b!) tile_expert, Tensor(c!) num_tiles, Tensor(d!) pair_slot, Tensor(e!)? group_end=None) -> ()");
   m.def("moe_gather(Tensor(a!) out, Tensor x, Tensor slots, int k) -> ()");
   m.def("moe_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor slots, Tensor tile_expert, int tile, int gather_k) -> ()");
@@ -1353,6 +1381,7 @@ TORCH_LIBRARY_IMPL(hipserve, CUDA, m) {
   m.impl("splitk_reduce", &splitk_reduce);
   m.impl("fill_uniform", &fill_uniform);
   m.impl("moe_topk_softmax", &moe_topk_softmax);
+  m.impl("moe_combine_add_rmsnorm", &moe_combine_add_rmsnorm);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gather", &moe_gather);
   m.impl("moe_gemm", &moe_gemm);

@@ -784,7 +784,14 @@ class LlamaModel:
                 self.add_rmsnorm(xn, residual, self.linear_rowpar(attn, lw.wo), 1, lw.ln2)
             nxt = self.layers[i + 1].ln1 if i + 1 < L else self.norm
             if lw.router is not None:  # MoE MLP: routed expert GEMMs, then residual + next norm
-                self.add_rmsnorm(xn, residual, self.moe(xn, lw), 1, nxt)
+                # TP = 1: the expert combine adds the residual and runs the next norm itself
+                # (moe_combine_add_rmsnorm, via _combine) and returns None
+                self._moe_norm = ((xn, residual, nxt) if self.tp.world_size == 1 and self.ops.name == "hip"
+                                  and residual.dtype == torch.bfloat16 else None)
+                y = self.moe(xn, lw)
+                self._moe_norm = None
+                if y is not None:
+                    self.add_rmsnorm(xn, residual, y, 1, nxt)
                 continue
             gelu = cfg.hidden_act == "gelu_tanh"
             gc = None if gelu else gemm.glu_choice(T, lw.wgu)
@@ -926,7 +933,29 @@ class LlamaModel:
         tm = tm.view(-1)[: Td * nq * mp * 2].view(Td, nq, mp, 2)
         return part, to, tm
 
-    def moe(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
+    # (out, residual, norm weight) of the decode layer's MoE tail: set around ``moe`` by
+    # forward_decode_fused at TP = 1 so the combine also does residual add + next RMSNorm
+    _moe_norm: tuple | None = None
+
+    def _combine(self, out: torch.Tensor, y: torch.Tensor, S: int, w, pair_slot, k: int):
+        """Weighted combine of a token's k expert rows (bf16 ``y`` [slots, H] when S == 0,
+        fp32 split-K partials [S, slots, H] else) into ``out``. Under ``_moe_norm`` the
+        one-kernel combine + residual add + next-layer RMSNorm instead (bit-identical to
+        combine then fused_add_rmsnorm): writes the norm output and the residual in place,
+        returns None."""
+        op = torch.ops.hipserve
+        if self._moe_norm is not None:
+            xn, residual, nw = self._moe_norm
+            self._moe_norm = None
+            op.moe_combine_add_rmsnorm(xn, residual, y, S, w, pair_slot, k, nw, self.cfg.rms_norm_eps)
+            return None
+        if S > 0:
+            op.moe_combine_partial(out, y, w, pair_slot, k)
+        else:
+            op.moe_combine(out, y, w, pair_slot, k)
+        return out
+
+    def moe(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor | None:
         """Sparse MoE: softmax over the E router logits, top-k experts, weights
         renormalised over the k (Mixtral; Qwen3-MoE when ``norm_topk_prob``).
 
@@ -1045,9 +1074,7 @@ class LlamaModel:
                                        slots, k)
         y = torch.empty(cap, H, dtype=x.dtype, device=dev)
         op.prefill_gemm_packed_grouped(y, act, p2, H, 0, tile_expert, ntiles, gemm.PW_WM, gemm.PW_RW)
-        out = torch.empty(T, H, dtype=x.dtype, device=dev)
-        op.moe_combine(out, y, w, pair_slot, k)
-        return out
+        return self._combine(torch.empty(T, H, dtype=x.dtype, device=dev), y, 0, w, pair_slot, k)
 
     # prefill-sized MoE batches: the packed one-launch grouped GEMM (``moe_grouped``) or the
     # weight-streaming expert kernel (``moe_hip``). ``auto``: by the start-up timing of the
@@ -1199,20 +1226,17 @@ class LlamaModel:
             if S == 1:  # one K slice: bf16 expert outputs, no fp32 partial slab
                 y = torch.empty(cap, H, dtype=x.dtype, device=dev)
                 op.moe_decode_gemm(y, act, w2, slots, tile_expert, tile, 0, H, 1, packed, False)
-                op.moe_combine(out, y, w, pair_slot, k)
-                return out
+                return self._combine(out, y, 0, w, pair_slot, k)
             ws = torch.empty(S, cap, H, dtype=torch.float32, device=dev)
             op.moe_decode_gemm(ws, act, w2, slots, tile_expert, tile, 0, H, S, packed, False)
-            op.moe_combine_partial(out, ws, w, pair_slot, k)
-            return out
+            return self._combine(out, ws, S, w, pair_slot, k)
         gu = torch.empty(cap, 2 * self.inter, dtype=x.dtype, device=dev)
         op.moe_gemm(gu, x, lw.w13, slots, tile_expert, tile, k)
         act = torch.empty(cap, self.inter, dtype=x.dtype, device=dev)
         self.ops.silu_and_mul(act, gu)
         y = torch.empty(cap, H, dtype=x.dtype, device=dev)
         op.moe_gemm(y, act, lw.w2, slots, tile_expert, tile, 0)
-        op.moe_combine(out, y, w, pair_slot, k)
-        return out
+        return self._combine(out, y, 0, w, pair_slot, k)
 
     def moe_quant(self, x: torch.Tensor, lw: LayerWeights) -> torch.Tensor:
         """Decode-sized MoE on quantised experts (INT8 / FP8, ``QuantMoE``): routing and
@@ -1245,12 +1269,10 @@ class LlamaModel:
         if S <= 1:
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
             op.qmoe_gemm(y, f32, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, 1)
-            op.moe_combine(out, y, w, pair_slot, k)
-            return out
+            return self._combine(out, y, 0, w, pair_slot, k)
         ws = torch.empty(S, cap, H, dtype=torch.float32, device=dev)
         S = op.qmoe_gemm(out, ws, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, S)
-        op.moe_combine_partial(out, ws[:S], w, pair_slot, k)
-        return out
+        return self._combine(out, ws[:S], S, w, pair_slot, k)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = self.linear(hidden, self.lm_head)

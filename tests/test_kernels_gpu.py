@@ -375,6 +375,31 @@ def test_moe_topk_softmax_from_partials(ops, T, E, k, S):
     assert torch.equal(i0, i1) and torch.equal(w0, w1)
 
 
+@pytest.mark.parametrize("T,k,H", [(1, 8, 2048), (37, 8, 2048), (256, 2, 4096), (5, 4, 7168), (9, 2, 1024)])
+@pytest.mark.parametrize("S", [0, 1, 3])
+@pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
+def test_moe_combine_add_rmsnorm_bit_exact(ops, T, k, H, S, wdt):
+    """The one-kernel decode MoE tail == moe_combine(_partial) + fused_add_rmsnorm, bit for
+    bit (norm output and the updated residual), for bf16 expert rows and fp32 partials."""
+    torch.manual_seed(T + k + H + S)
+    cap = T * k + 64
+    pair_slot = torch.randperm(cap, device=DEV)[: T * k].int()
+    w = torch.rand(T, k, device=DEV)
+    y = (torch.randn(S, cap, H, device=DEV) if S else torch.randn(cap, H, device=DEV).to(torch.bfloat16))
+    res = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    nw = (torch.rand(H, device=DEV) + 0.5).to(wdt)
+    comb = torch.empty(T, H, device=DEV, dtype=torch.bfloat16)
+    if S:
+        torch.ops.hipserve.moe_combine_partial(comb, y, w, pair_slot, k)
+    else:
+        torch.ops.hipserve.moe_combine(comb, y, w, pair_slot, k)
+    r0, o0 = res.clone(), torch.empty_like(res)
+    ops.fused_add_rmsnorm(o0, comb, r0, nw, 1e-6)
+    r1, o1 = res.clone(), torch.full_like(res, float("nan"))
+    torch.ops.hipserve.moe_combine_add_rmsnorm(o1, r1, y, S, w, pair_slot, k, nw, 1e-6)
+    assert torch.equal(r0, r1) and torch.equal(o0, o1)
+
+
 @pytest.mark.parametrize("mode", ["packed", "rowmajor", "legacy"])
 @pytest.mark.parametrize("T,E,k,norm", [(1, 8, 2, True), (13, 8, 2, True), (64, 8, 2, True), (200, 8, 2, True),
                                         (5, 4, 1, True), (3, 128, 8, True), (40, 128, 8, False), (9, 64, 4, False)])
