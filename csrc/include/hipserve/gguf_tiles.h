@@ -12,8 +12,12 @@ namespace gq {
 // GGUF block formats + FP8 e4m3 weights (per-row scale; FP8B adds 128 x 128 block
 // scales, the block-FP8 checkpoints)
 // INT8: unsigned 8-bit weights (compressed-tensors pack-quantized / AWQ 8-bit) with
-// a group scale and zero point per half lane-quarter (32 k): w = (u - 128 - zp) * s
-enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5, FP8 = 6, FP8B = 7, INT8 = 8 };
+// a group scale and zero point per half lane-quarter (32 k): w = (u - 128 - zp) * s.
+// INT8C: the per-channel symmetric case (one scale per row, no zero point — the
+// reference's AWQ-8bit / W8A16 exports): the bytes alone, the row scale applied to the
+// fp32 accumulators in the epilogue as for FP8 (11 % fewer bytes than INT8's per-32-k
+// scale / offset table, and the integers enter the MFMA exactly)
+enum { Q4_0 = 0, Q4_1 = 1, Q8_0 = 2, Q4_K = 3, Q5_K = 4, Q6_K = 5, FP8 = 6, FP8B = 7, INT8 = 8, INT8C = 9 };
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -66,15 +70,19 @@ struct Raw {
 //   FP8   [4 x 64 lanes x 16 q]                                     4096 B
 //   FP8B  FP8 + [16 rows x 2 f32 block scales]                      4224 B
 //   INT8  [4 x 64 lanes x 16 u8][16 rows x 4 g x 2 halves x (f16 scale, f16 offset)]  4608 B
+//   INT8C [4 x 64 lanes x 16 u8]                                    4096 B
 template <int QT>
 constexpr int chunk_bytes() {
   return QT == Q4_K ? 2304 : QT == Q5_K ? 2816 : QT == Q6_K ? 3360 : QT == Q8_0 ? 4352 : QT == Q4_0 ? 2304
-       : QT == Q4_1 ? 2560 : QT == FP8 ? 4096 : QT == FP8B ? 4224 : 4608;
+       : QT == Q4_1 ? 2560 : QT == FP8 || QT == INT8C ? 4096 : QT == FP8B ? 4224 : 4608;
 }
+// formats whose per-row scale (Part::rs) multiplies the accumulators in the epilogue
+template <int QT>
+constexpr bool row_scaled() { return QT == FP8 || QT == FP8B || QT == INT8C; }
 
 struct Part {
   const unsigned char* q;
-  const float* rs;  // per-row output scale (FP8), nullptr for GGUF formats
+  const float* rs;  // per-row output scale (FP8, INT8C), nullptr for GGUF formats
   int qt;       // format of the part
   int rows;     // N of the part (multiple of 16)
   int col;      // first output column
@@ -95,9 +103,11 @@ struct MoeQ {
   const int* slots;        // [nslots] pair index (token * k + j) or -1 (padding)
   const int* tile_expert;  // [tiles_cap] expert of each tile, -1 past the last tile
   long w_estride;          // bytes of one expert's tiled weight
-  long rs_estride;         // floats of one expert's row scales (FP8), 0 otherwise
+  long rs_estride;         // floats of one expert's row scales (FP8, INT8C), 0 otherwise
   int gather_k;            // > 0: x row = pair / gather_k; 0: x row = slot
   int nslots;              // slot rows of out / of each ws split
+  int kmajor = 0;          // expert weights [K/256][N/16][chunk] (super-chunk major), else [N/16][K/256][chunk]
+  int glu = 0;             // 1 / 2: SiLU / GELU-tanh GLU epilogue (w13 rows = gate | up; out [slots, N / 2])
 };
 
 template <int QT>
@@ -125,7 +135,7 @@ HS_DEVICE void load_raw(const unsigned char* ch, int g, int c, int lane, Raw& r)
     const uint2 so = *reinterpret_cast<const uint2*>(ch + 4096 + 32 * c + 8 * g);  // (sA, oA), (sB, oB)
     r.s2[0] = so.x;
     r.s2[1] = so.y;
-  } else if constexpr (QT == FP8 || QT == FP8B) {
+  } else if constexpr (QT == FP8 || QT == FP8B || QT == INT8C) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.v[i] = ld16(ch + 1024 * i + 16 * lane);
     if constexpr (QT == FP8B)  // the lane's 64 k sit in 128-block (g >> 1) of this super-chunk
@@ -224,7 +234,7 @@ struct Dec {
       fcB = -dmin * m2;
     } else if constexpr (QT == Q6_K) {
       d6 = h2f(r.h[0]);
-    } else if constexpr (QT == FP8 || QT == FP8B) {
+    } else if constexpr (QT == FP8 || QT == FP8B || QT == INT8C) {
       fdA = fdB = QT == FP8B ? __builtin_bit_cast(float, r.s2[0]) : 1.f;
     } else if constexpr (QT == INT8) {  // c = offset (-1024 - 128 - zp), applied before the scale
       fdA = h2f(r.s2[0] & 0xFFFF);
@@ -273,6 +283,14 @@ struct Dec {
   }
 
   HS_DEVICE f16x8 ints(const Raw& r, int g, int s) const {
+    if constexpr (QT == INT8C) {  // u - 128 exact: (1024 + u) - 1152
+      const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+      const unsigned wa = qv[s >> 1][2 * (s & 1)], wb = qv[s >> 1][2 * (s & 1) + 1];
+      const h2 cc = splat(-1152.f);
+      const unsigned p0 = (wa & 0x00FF00FFu) | kMagic, p1 = ((wa >> 8) & 0x00FF00FFu) | kMagic;
+      const unsigned p2 = (wb & 0x00FF00FFu) | kMagic, p3 = ((wb >> 8) & 0x00FF00FFu) | kMagic;
+      return frag(as_h2(p0) + cc, as_h2(p1) + cc, as_h2(p2) + cc, as_h2(p3) + cc);
+    }
     if constexpr (QT == INT8) {  // u - 128 - zp, exact
       const u32x4 qv[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
       const unsigned wa = qv[s >> 1][2 * (s & 1)], wb = qv[s >> 1][2 * (s & 1) + 1];
@@ -433,7 +451,7 @@ struct Dec {
       return frag((as_h2(p0) + cc) * dd, (as_h2(p1) + cc) * dd, (as_h2(p2) + cc) * dd, (as_h2(p3) + cc) * dd);
     }
     const f16x8 q = ints(r, g, s);
-    if constexpr (QT == FP8) return q;  // row scale in the epilogue
+    if constexpr (QT == FP8 || QT == INT8C) return q;  // row scale in the epilogue
     if constexpr (QT == FP8B) {
       const u32x4 qu = __builtin_bit_cast(u32x4, q);
       return frag(as_h2(qu[0]) * dA, as_h2(qu[1]) * dA, as_h2(qu[2]) * dA, as_h2(qu[3]) * dA);

@@ -118,7 +118,7 @@ void launch_x_f16_pairs(void* x16, float* rsc, const void* x, long ldx, int M, i
 bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* q,
                       const float* rs, int qtype, long w_estride, long rs_estride, const int* slots,
                       const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, int S,
-                      hipStream_t s);
+                      hipStream_t s, bool kmajor = false, int glu = 0);
 
 }  // namespace hipserve
 

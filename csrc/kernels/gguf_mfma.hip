@@ -64,11 +64,24 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
   const int g = lane >> 4, c = lane & 15;
   const int gi0 = (blockIdx.x - P.tile0) * (NWAVES * RT) + wave * RT;  // first row group of this wave
   const int ngroups = P.rows >> 4;
+  // kMoe GLU (w13, RT 2): the wave's row group 0 is gate group gg, row group 1 the
+  // matching up group gg + ngroups / 2 — equal MFMA layouts, so silu(gate) * up is
+  // elementwise in registers and the bf16 gate|up never goes to HBM
+  [[maybe_unused]] const bool glu = kMoe && RT == 2 && moe.glu != 0;
+  [[maybe_unused]] const int gg = (int)blockIdx.x * NWAVES + wave;
+  int gidx[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    gidx[r] = glu ? min(gg, (ngroups >> 1) - 1) + r * (ngroups >> 1) : gi0 + r;
   const int nsb = K >> 8;
   const int sb0 = blockIdx.y * sb_per_split, sb1 = min(nsb, sb0 + sb_per_split);
   const unsigned char* base[RT];
+  // bytes between consecutive super-chunks of a row group (k-major MoE experts: a whole
+  // super-chunk column of the expert)
+  const long sbs = kMoe && moe.kmajor ? (long)ngroups * CB : (long)CB;
+  const long gstride = kMoe && moe.kmajor ? (long)CB : (long)nsb * CB;
 #pragma unroll
-  for (int r = 0; r < RT; ++r) base[r] = P.q + (long)min(gi0 + r, ngroups - 1) * nsb * CB;
+  for (int r = 0; r < RT; ++r) base[r] = P.q + (long)min(gidx[r], ngroups - 1) * gstride;
 
   // x staging: 32 fragments (g, s) of 8 per row and super-chunk; thread -> (row, fragment)
   constexpr int XP = XR * 32 / NT;
@@ -156,7 +169,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
   if (sb0 < sb1) {
     load_x(sb0, scaled);
 #pragma unroll
-    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sb0 * CB, g, c, lane, rawA[r]);
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + sb0 * sbs, g, c, lane, rawA[r]);
     store_x(0, scaled);
   }
   __syncthreads();
@@ -169,7 +182,7 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
     load_x(sn, scaled);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + (long)sn * CB, g, c, lane, nxt[r]);
+    for (int r = 0; r < RT; ++r) load_raw<QT>(base[r] + sn * sbs, g, c, lane, nxt[r]);
     __builtin_amdgcn_sched_barrier(0);  // the scheduler would sink them below the MFMAs
     const _Float16* xb = &xs[buf][g * x_plane<MT>() + c * kXR];  // fragment (g, s) of row 16t + c at + 8s
     Dec<QT> dec[RT];
@@ -242,12 +255,40 @@ HS_DEVICE void qgemm2_body(_Float16 (&xs)[2][4 * x_plane<MT>()], float* xrow, un
       for (int r = 0; r < RT; ++r) acc[r][t] *= un;
     }
   }
+  if constexpr (kMoe && RT == 2) {
+    if (glu) {
+      if (gg >= (ngroups >> 1)) return;
+      if constexpr (row_scaled<QT>()) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(P.rs + 16 * gidx[r] + 4 * g);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[r][t] *= rs;
+        }
+      }
+      const int col = 16 * gg + 4 * g;  // act column
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = mrow0 + 16 * t + c;
+        if (moe.slots[m] < 0) continue;
+        unsigned short o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned short gv = f32_to_bf16(acc[0][t][j]), uv = f32_to_bf16(acc[1][t][j]);
+          o[j] = moe.glu == 2 ? gelu_mul1(gv, uv) : silu_mul1(gv, uv);
+        }
+        *reinterpret_cast<uint2*>(out + (long)m * out_stride + col) =
+            uint2{(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
+      }
+      return;
+    }
+  }
   // C: col m = 16t + c, rows n = 16 gi + 4g + j
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
     if (gi0 + r >= ngroups) continue;
     const int col = P.col + 16 * (gi0 + r) + 4 * g;
-    if constexpr (QT == FP8 || QT == FP8B) {
+    if constexpr (row_scaled<QT>()) {
       const f32x4 rs = *reinterpret_cast<const f32x4*>(P.rs + 16 * (gi0 + r) + 4 * g);
 #pragma unroll
       for (int t = 0; t < MT; ++t) acc[r][t] *= rs;
@@ -343,9 +384,13 @@ void launch_t(void* out, long out_stride, float* ws, const void* x, long x_strid
 }
 
 // MoE experts: grid (row tiles of N, K splits, expert tiles); workgroups of tiles past
-// the last one (tile_expert -1) exit before any barrier
+// the last one (tile_expert -1) exit before any barrier. The 16-slot body of the formats
+// without a scale table (FP8, INT8C) fits 128 VGPRs without spills: 4 waves per SIMD
+// instead of 3, a third more weight bytes in flight (the expert stream is bound by the
+// loads in flight, not by its bytes: INT8's 12 % larger chunks ran as fast)
 template <int QT, int MT, int RT, int NWAVES>
-__global__ __launch_bounds__(64 * NWAVES) void qmoe_kernel(unsigned short* __restrict__ out, long out_stride,
+__global__ __launch_bounds__(64 * NWAVES) __attribute__((amdgpu_waves_per_eu(MT == 1 && QT != INT8 ? 4 : 1)))
+void qmoe_kernel(unsigned short* __restrict__ out, long out_stride,
                                                           float* __restrict__ ws, const unsigned short* __restrict__ x,
                                                           long x_stride, const unsigned char* __restrict__ q,
                                                           const float* __restrict__ rs, MoeQ moe, int N, int K,
@@ -368,11 +413,13 @@ void moe_launch_t(void* out, long out_stride, float* ws, const void* x, long x_s
   auto* xi = static_cast<const unsigned short*>(x);
   auto* qq = static_cast<const unsigned char*>(q);
   const int ysplit = (nsb + per - 1) / per;
+  // GLU: 4 waves x one gate group (+ its up group) = 64 act columns per workgroup
+  const int xt = moe.glu ? (N / 2 + 63) / 64 : (N + 127) / 128;
   if (tile == 16) {
-    const dim3 grid((N + 127) / 128, ysplit, tiles_cap);
+    const dim3 grid(xt, ysplit, tiles_cap);
     qmoe_kernel<QT, 1, 2, kWaves><<<grid, 64 * kWaves, 0, s>>>(o, out_stride, ws, xi, x_stride, qq, rs, moe, N, K, per);
   } else if (tile == 32) {
-    const dim3 grid((N + 127) / 128, ysplit, tiles_cap);
+    const dim3 grid(xt, ysplit, tiles_cap);
     qmoe_kernel<QT, 2, 2, kWaves><<<grid, 64 * kWaves, 0, s>>>(o, out_stride, ws, xi, x_stride, qq, rs, moe, N, K, per);
   } else {
     const dim3 grid((N + 127) / 128, ysplit, tiles_cap);
@@ -422,7 +469,7 @@ __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __re
     const f16x8 q = dec.ints(r, g, s);  // exact integers, pair order {0, 2, 1, 3, 4, 6, 5, 7}
     float d, m;
     dec.scale(r, g, s, d, m);           // fp32 scale: one rounding, to bf16, like the v1 dequant
-    if constexpr (QT == FP8 || QT == FP8B) d *= rs[16 * gi + c];
+    if constexpr (row_scaled<QT>()) d *= rs[16 * gi + c];
     constexpr int src[8] = {0, 2, 1, 3, 4, 6, 5, 7};
     u16x8 o;
 #pragma unroll
@@ -772,6 +819,7 @@ int gguf_tiled_chunk_bytes(int qtype) {
     case FP8: return chunk_bytes<FP8>();
     case FP8B: return chunk_bytes<FP8B>();
     case INT8: return chunk_bytes<INT8>();
+    case INT8C: return chunk_bytes<INT8C>();
   }
   return 0;
 }
@@ -823,6 +871,7 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
       case FP8: launch_t<FP8, FP8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
       case FP8B: launch_t<FP8B, FP8B>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
       case INT8: launch_t<INT8, INT8>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
+      case INT8C: launch_t<INT8C, INT8C>(out, out_stride, ws, x, x_stride, P, tiles, M, Ntot, K, S, s, x16); break;
     }
   }
 }
@@ -830,12 +879,15 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
 bool launch_qmoe_gemm(void* out, long out_stride, float* ws, const void* x, long x_stride, const void* q,
                       const float* rs, int qtype, long w_estride, long rs_estride, const int* slots,
                       const int* tile_expert, int tiles_cap, int tile, int gather_k, int N, int K, int S,
-                      hipStream_t s) {
+                      hipStream_t s, bool kmajor, int glu) {
   if (tile != 16 && tile != 32 && tile != 64) return false;
-  const MoeQ moe{slots, tile_expert, w_estride, rs_estride, gather_k, tiles_cap * tile};
+  // GLU epilogue: the 16 / 32-slot bodies (two row groups per wave), whole K, N / 2 % 16
+  if (glu && (tile == 64 || S != 1 || ws != nullptr || (N / 2) % 16)) return false;
+  const MoeQ moe{slots, tile_expert, w_estride, rs_estride, gather_k, tiles_cap * tile, kmajor ? 1 : 0, glu};
   switch (qtype) {
     case FP8: moe_launch_t<FP8>(out, out_stride, ws, x, x_stride, q, rs, moe, tiles_cap, tile, N, K, S, s); return true;
     case INT8: moe_launch_t<INT8>(out, out_stride, ws, x, x_stride, q, rs, moe, tiles_cap, tile, N, K, S, s); return true;
+    case INT8C: moe_launch_t<INT8C>(out, out_stride, ws, x, x_stride, q, rs, moe, tiles_cap, tile, N, K, S, s); return true;
   }
   return false;
 }
@@ -922,6 +974,7 @@ void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qt
     case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
     case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
     case INT8: dequant_tiled_kernel<INT8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case INT8C: dequant_tiled_kernel<INT8C><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
   }
 }
 

@@ -300,6 +300,9 @@ void gguf_gemm(at::Tensor& out, const at::Tensor& x, const at::Tensor& q, const 
 // parts in the tiled layout (one uint8 tensor [N/16, K/256, chunk] each), their
 // formats / rows / output columns. ws.numel() > 0: fp32 partials [S_actual, M, Ntot]
 // (returned S_actual = ceil(nsb / ceil(nsb / S))); else bf16 out [M, >= Ntot], S == 1.
+// kernel formats with a per-row fp32 output scale: FP8, FP8B, INT8C (gguf_tiles.h row_scaled)
+static bool row_scaled_qt(int64_t qt) { return qt == 6 || qt == 7 || qt == 9; }
+
 int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const std::vector<at::Tensor>& qs,
                         const std::vector<at::Tensor>& rss, const std::vector<int64_t>& qtypes, const std::vector<int64_t>& rows,
                         const std::vector<int64_t>& cols, int64_t Ntot, int64_t K, int64_t splits,
@@ -317,10 +320,10 @@ int64_t gguf_gemm_parts(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, co
   const int S = (nsb + per - 1) / per;
   hipserve::GgufPart P[4];
   for (int i = 0; i < np; ++i) {
-    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 8, "gguf_gemm_parts: kernel qtype 0-8");
-    const bool fp8 = qtypes[i] == 6 || qtypes[i] == 7;
+    TORCH_CHECK(qtypes[i] >= 0 && qtypes[i] <= 9, "gguf_gemm_parts: kernel qtype 0-9");
+    const bool fp8 = row_scaled_qt(qtypes[i]);
     TORCH_CHECK(!fp8 || (rss[i].scalar_type() == at::kFloat && rss[i].is_contiguous() && rss[i].numel() == rows[i] &&
-                         rss[i].device() == x.device()), "FP8 parts need an fp32 row scale per row");
+                         rss[i].device() == x.device()), "FP8 / INT8C parts need an fp32 row scale per row");
     TORCH_CHECK(qs[i].scalar_type() == at::kByte && qs[i].is_contiguous() && qs[i].device() == x.device());
     TORCH_CHECK(cols[i] % 4 == 0 && rows[i] % 16 == 0 && rows[i] > 0 && cols[i] + rows[i] <= Ntot,
                 "parts: 16-row multiples at 4-aligned columns inside Ntot");
@@ -407,9 +410,9 @@ bool gguf_prefill(at::Tensor& out, const at::Tensor& x16, const at::Tensor& rsc,
 
 int64_t qmoe_gemm(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const at::Tensor& q, const at::Tensor& rs,
                   int64_t qtype, int64_t N, int64_t K, const at::Tensor& slots, const at::Tensor& tile_expert,
-                  int64_t tile, int64_t gather_k, int64_t splits) {
+                  int64_t tile, int64_t gather_k, int64_t splits, bool kmajor, int64_t glu) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x);
-  TORCH_CHECK(qtype == 6 || qtype == 8, "qmoe_gemm: expert formats FP8 (per-row scale) and INT8");
+  TORCH_CHECK(qtype == 6 || qtype == 8 || qtype == 9, "qmoe_gemm: expert formats FP8 (per-row scale), INT8, INT8C");
   TORCH_CHECK(tile == 16 || tile == 32 || tile == 64, "qmoe_gemm: tile 16/32/64");
   TORCH_CHECK(N % 16 == 0 && K % 256 == 0 && x.size(1) >= K && x.stride(0) % 8 == 0, "qmoe_gemm: shapes");
   TORCH_CHECK(slots.scalar_type() == at::kInt && tile_expert.scalar_type() == at::kInt && slots.is_contiguous() &&
@@ -419,9 +422,9 @@ int64_t qmoe_gemm(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const at
               "qmoe_gemm: q uint8 [E, expert bytes]");
   const long per_e = N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype);
   TORCH_CHECK(q.size(1) == per_e, "qmoe_gemm: q rows are not tiled [N/16, K/256, chunk] experts");
-  const bool fp8 = qtype == 6;
+  const bool fp8 = qtype == 6 || qtype == 9;
   TORCH_CHECK(!fp8 || (rs.scalar_type() == at::kFloat && rs.is_contiguous() && rs.dim() == 2 &&
-                       rs.size(0) == q.size(0) && rs.size(1) == N), "qmoe_gemm: FP8 experts need rs [E, N] fp32");
+                       rs.size(0) == q.size(0) && rs.size(1) == N), "qmoe_gemm: FP8 / INT8C experts need rs [E, N] fp32");
   TORCH_CHECK(gather_k > 0 || x.size(0) >= slots.numel(), "qmoe_gemm: slot-indexed x needs a row per slot");
   const int nsb = K / 256;
   const int per = (nsb + splits - 1) / splits;
@@ -435,13 +438,15 @@ int64_t qmoe_gemm(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const at
   } else {
     TORCH_CHECK(S == 1, "qmoe_gemm: split-K needs a partial workspace");
     CHECK_BF16(out); CHECK_ROWMAJOR(out);
-    TORCH_CHECK(out.size(0) == nslots && out.size(1) >= N && out.stride(0) % 4 == 0 && out.device() == x.device());
+    TORCH_CHECK(out.size(0) == nslots && out.size(1) >= (glu ? N / 2 : N) && out.stride(0) % 4 == 0 &&
+                out.device() == x.device());
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   TORCH_CHECK(hipserve::launch_qmoe_gemm(wp ? nullptr : out.data_ptr(), wp ? 0 : out.stride(0), wp, x.data_ptr(),
                                          x.stride(0), q.data_ptr(), fp8 ? rs.data_ptr<float>() : nullptr, qtype,
                                          per_e, fp8 ? N : 0, slots.data_ptr<int>(), tile_expert.data_ptr<int>(),
-                                         tile_expert.numel(), tile, gather_k, N, K, splits, cur_stream()),
+                                         tile_expert.numel(), tile, gather_k, N, K, splits, cur_stream(), kmajor,
+                                         (int)glu),
               "qmoe_gemm: unsupported configuration");
   return S;
 }
@@ -460,10 +465,10 @@ void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& 
                 "gguf_dequant_tiled: packed matrices of nrows rows (glu: nrows % 128 == 0)");
     TORCH_CHECK(out.numel() >= N / nrows * ((nrows + 127) / 128 * 128) * K, "gguf_dequant_tiled: packed out size");
   }
-  TORCH_CHECK(qtype >= 0 && qtype <= 8 && q.scalar_type() == at::kByte && q.is_contiguous());
+  TORCH_CHECK(qtype >= 0 && qtype <= 9 && q.scalar_type() == at::kByte && q.is_contiguous());
   TORCH_CHECK(q.numel() == N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype), "not a tiled tensor");
-  const bool fp8 = qtype == 6 || qtype == 7;
-  TORCH_CHECK(!fp8 || (rs.scalar_type() == at::kFloat && rs.numel() == N), "FP8 needs an fp32 row scale");
+  const bool fp8 = row_scaled_qt(qtype);
+  TORCH_CHECK(!fp8 || (rs.scalar_type() == at::kFloat && rs.numel() == N), "FP8 / INT8C need an fp32 row scale");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), fp8 ? rs.data_ptr<float>() : nullptr,
                                       qtype, N, K, cur_stream(), (int)pack, (int)nrows);
@@ -1302,7 +1307,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K, int pack=0, int nrows=0) -> ()",
         &gguf_dequant_tiled);
   m.def("fp8_untile(Tensor(a!) out, Tensor q, int N, int K) -> ()", &fp8_untile);
-  m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits) -> int", &qmoe_gemm);
+  m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits, bool kmajor=False, int glu=0) -> int", &qmoe_gemm);
   m.def("car_create(int rank, int world, int max_bytes, int nb_large=512) -> int", &car_create);
   m.def("car_handle(int state) -> Tensor", &car_handle);
   m.def("car_open(int state, int peer, Tensor handle) -> ()", &car_open);

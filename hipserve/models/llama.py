@@ -1259,10 +1259,15 @@ class LlamaModel:
         op.moe_align(ids, E, tile, slots, tile_expert, ntiles, pair_slot)
         w13, w2 = lw.w13, lw.w2
         f32 = torch.empty(0, dtype=torch.float32, device=dev)
-        gu = torch.empty(cap, w13.N, dtype=x.dtype, device=dev)
-        op.qmoe_gemm(gu, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1)
         act = torch.empty(cap, w13.N // 2, dtype=x.dtype, device=dev)
-        self.act_and_mul(act, gu)
+        if tile <= 32 and (w13.N // 2) % 16 == 0:  # GLU in the w13 epilogue (bit-identical)
+            glu = 2 if cfg.hidden_act == "gelu_tanh" else 1
+            op.qmoe_gemm(act, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1, False,
+                         glu)
+        else:
+            gu = torch.empty(cap, w13.N, dtype=x.dtype, device=dev)
+            op.qmoe_gemm(gu, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1)
+            self.act_and_mul(act, gu)
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         active = min(E, cap // tile, P)
         S = self._moe_w2_splits(w2.K, -(-H // 128), active)

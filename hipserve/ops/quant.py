@@ -29,7 +29,11 @@ FP8, FP8B = 1000, 1001
 # 8-bit integer weight-only (compressed-tensors pack-quantized 8-bit / AWQ 8-bit):
 # unsigned bytes u = q + 128, per-group scale and zero point
 INT8 = 1002
-KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7, INT8: 8}
+# per-channel symmetric 8-bit (one scale per row, no zero point): the bytes alone in the
+# tiled layout, the scale as the fp32 row scale ``rs`` (gguf_tiles.h INT8C)
+INT8C = 1003
+KERNEL_QT = {G.Q4_0: 0, G.Q4_1: 1, G.Q8_0: 2, G.Q4_K: 3, G.Q5_K: 4, G.Q6_K: 5, FP8: 6, FP8B: 7, INT8: 8,
+             INT8C: 9}
 MAX_FUSED_M = 64
 # the W8A8 FP8 decode GEMM (fp8_decode.hip) also takes the decode graph buckets above 64
 # rows (up to 256, max_num_seqs' default): one weight stream per step instead of the
@@ -74,7 +78,7 @@ def repack(raw: np.ndarray, qtype: int, N: int, K: int):
 
 
 CHUNK_BYTES = {G.Q4_K: 2304, G.Q5_K: 2816, G.Q6_K: 3360, G.Q8_0: 4352, G.Q4_0: 2304, G.Q4_1: 2560,
-               FP8: 4096, FP8B: 4224, INT8: 4608}
+               FP8: 4096, FP8B: 4224, INT8: 4608, INT8C: 4096}
 
 
 def _lanes(a: np.ndarray, n_ld: int) -> np.ndarray:
@@ -165,11 +169,14 @@ class QuantPart:
         self.rs = rs if rs is not None else torch.empty(0, dtype=torch.float32, device=q.device)
 
     @classmethod
-    def from_int8(cls, u: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor | None, device):
+    def from_int8(cls, u: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor | None, device,
+                  channel: bool = True):
         """8-bit weight-only matrix: ``u`` [N, K] unsigned bytes holding q + 128 (the
         compressed-tensors pack-quantized convention), ``scale`` [N, K / group] or
         [N, 1] (per channel), optional signed ``zero_point`` of the same shape:
-        w = (u - 128 - zp) * scale. Groups of >= 32 k; N % 16 == 0, K % 256 == 0."""
+        w = (u - 128 - zp) * scale. Groups of >= 32 k; N % 16 == 0, K % 256 == 0.
+        Per-channel scales without a zero point become INT8C unless ``channel`` is False
+        (a stack of experts that must share one format)."""
         N, K = u.shape
         u = u.to(device=device, dtype=torch.uint8)
         sc = scale.to(device=device, dtype=torch.float32).reshape(N, -1)
@@ -181,6 +188,11 @@ class QuantPart:
               else torch.zeros_like(sc))
         R, nsb = N // 16, K // 256
         lanes = u.reshape(R, 16, nsb, 4, 4, 16).permute(0, 2, 4, 3, 1, 5).reshape(R, nsb, 4096)
+        if channel and ng == 1 and (zero_point is None or not bool(zp.any())):
+            # per channel, symmetric: INT8C (the bytes alone, the scale applied to the
+            # accumulators: 4096 instead of 4608 bytes per 16 x 256 chunk)
+            return cls(INT8C, N, K, lanes.contiguous(), _E16(device), _E16(device), 0, tiled=True,
+                       rs=sc.reshape(N).contiguous())
         # (scale, offset = -(1024 + 128 + zp)) per (row, super-chunk, lane quarter g, half h): k0 = 256 sb + 64 g + 32 h
         k0 = torch.arange(nsb * 8, device=device) * 32                 # [nsb * 4 * 2] in (sb, g, h) order
         gi = k0 // G
@@ -873,14 +885,14 @@ class QuantMoE:
     experts; prefill runs bf16 expert GEMMs on ``dense`` (a resident shadow when HBM
     allows, else a per-call dequantised scratch)."""
 
-    KERNEL_QTS = (6, 8)  # FP8 (per-row scale), INT8
+    KERNEL_QTS = (6, 8, 9)  # FP8 (per-row scale), INT8, INT8C (per-row scale)
 
     def __init__(self, parts: list):
         p0 = parts[0]
         assert all(p.kqt == p0.kqt and p.N == p0.N and p.K == p0.K and p.tiled for p in parts)
         self.E, self.N, self.K, self.kqt = len(parts), p0.N, p0.K, p0.kqt
         self.q = torch.stack([p.q.reshape(-1) for p in parts]).contiguous()
-        self.rs = (torch.stack([p.rs for p in parts]).contiguous() if p0.kqt == 6
+        self.rs = (torch.stack([p.rs for p in parts]).contiguous() if p0.kqt in (6, 9)
                    else torch.empty(0, 0, dtype=torch.float32, device=p0.q.device))
         self.dense = None
 

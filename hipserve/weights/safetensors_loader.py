@@ -386,13 +386,13 @@ def _native_experts(ck, m, names, E, sl, dev):
             raise ValueError("unsupported expert slice")  # a split group / 128-block scales
         return pp
 
-    def build(pps):  # row-stacked pieces of one expert -> QuantPart
+    def build(pps, channel=True):  # row-stacked pieces of one expert -> QuantPart
         if int8:
             zps = [z for _, _, z in pps]
             zp = None if all(z is None for z in zps) else torch.cat(
                 [z if z is not None else torch.zeros_like(sc) for (_, sc, _), z in zip(pps, zps)])
             return Q.QuantPart.from_int8(torch.cat([u for u, _, _ in pps]), torch.cat([sc for _, sc, _ in pps]),
-                                         zp, dev)
+                                         zp, dev, channel)
         qs = torch.cat([q for q, _ in pps])
         sc = torch.cat([s.reshape(-1).expand(q.shape[0]) if s.numel() == 1 else s.reshape(-1) for q, s in pps])
         return Q.QuantPart.from_fp8(qs, sc, dev)
@@ -403,6 +403,10 @@ def _native_experts(ck, m, names, E, sl, dev):
             ep = f"{m}experts.{e}."
             p13.append(build([part(ep + names[0] + ".weight", 0), part(ep + names[1] + ".weight", 0)]))
             p2.append(build([part(ep + names[2] + ".weight", 1)]))
+        if int8 and len({p.kqt for p in p13 + p2}) > 1:  # zero points on some experts only: one format
+            p13 = [build([part(f"{m}experts.{e}." + names[0] + ".weight", 0),
+                          part(f"{m}experts.{e}." + names[1] + ".weight", 0)], False) for e in range(E)]
+            p2 = [build([part(f"{m}experts.{e}." + names[2] + ".weight", 1)], False) for e in range(E)]
     except ValueError:
         return None
     if not (Q.QuantMoE.supported(p13[0].kqt, p13[0].N, p13[0].K) and Q.QuantMoE.supported(p2[0].kqt, p2[0].N, p2[0].K)):

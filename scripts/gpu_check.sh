@@ -220,6 +220,8 @@ for N, K in ((43008, 5376), (5376, 21504), (8192, 5376)):
               bench_named coal_def_$r X=1 -- --steps 5 --tp-phase off || exit 1; done
             for f in coal_off_1 coal_def_1 coal_off_2 coal_def_2; do grep -o '"value": [0-9.]*\|"p50_ttft_ms": [0-9.]*' $OUT/bench_$f.json | tr '\n' ' '; echo $f; done ;;
     topktest) timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_quant_moe_gpu.py tests/test_families_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "topk or moe or family" > $OUT/topktest.log 2>&1; rc=$?; tail -n 5 $OUT/topktest.log; [ $rc -eq 0 ] ;;
+    int8ctest) timeout -k 10 400 python -u -m pytest tests/test_gguf_gpu.py tests/test_quant_moe_gpu.py tests/test_families_gpu.py tests/test_int_quant.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "int8 or moe or quant or family" > $OUT/int8ctest.log 2>&1; rc=$?; tail -n 5 $OUT/int8ctest.log; [ $rc -eq 0 ] ;;
+    qmoebench) timeout -k 10 400 python -u tools/bench_qmoe.py ${QMOE_ARGS:-} > $OUT/qmoebench.log 2>&1; rc=$?; cat $OUT/qmoebench.log | grep -v amdgpu.ids; [ $rc -eq 0 ] ;;
     *) echo "unknown step $s"; false ;;
   esac || { echo "step $s failed (rc=$?)"; exit 1; }
 done

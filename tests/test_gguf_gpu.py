@@ -336,7 +336,7 @@ def test_int8_linear_matches_fp32(group, asym, M):
     scale = torch.rand(N, K // G) * 2e-3 + 1e-4
     zp = torch.randint(-8, 8, (N, K // G)) if asym else None
     qw = Q.QuantWeight([Q.QuantPart.from_int8((q + 128).to(torch.uint8), scale, zp, "cuda")])
-    assert qw.v2 and qw.parts[0].kqt == 8
+    assert qw.v2 and qw.parts[0].kqt == (9 if group == 0 and not asym else 8)  # per channel: INT8C
     wref = ((q - (zp.repeat_interleave(G, 1) if asym else 0)).float() * scale.repeat_interleave(G, 1)).cuda()
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     want = x.float() @ wref.T

@@ -229,3 +229,54 @@ def test_quant_moe_prefill_paths_vs_fp32(kind, packed):
         for e in range(E):
             assert torch.equal(p13[e], gemm.pack(d13r[e].contiguous(), glu=True))
             assert torch.equal(p2[e], gemm.pack(d2r[e].contiguous()))
+
+
+@pytest.mark.parametrize("kind", ["int8", "int8g", "fp8"])
+@pytest.mark.parametrize("T,E,k", [(5, 16, 4), (48, 16, 4), (64, 128, 8)])
+def test_qmoe_glu_epilogue_and_kmajor_bit_exact(kind, T, E, k):
+    """The w13 expert GEMM with the SiLU-GLU in its epilogue == the bf16 gate|up output
+    then silu_and_mul, bit for bit; and super-chunk-major (k-major) expert weights give
+    the same bits as the row-group-major layout (the same sums in the same order)."""
+    from hipserve.ops import quant as Q
+
+    op = torch.ops.hipserve
+    H, I = 512, 768
+    torch.manual_seed(T + E)
+    parts = []
+    for _ in range(E):
+        wf = torch.randn(2 * I, H, device=DEV) * 0.05
+        if kind == "fp8":
+            s = wf.abs().amax(1, keepdim=True) / 448.0
+            parts.append(Q.QuantPart.from_fp8((wf / s).to(torch.float8_e4m3fn), s, DEV))
+        else:
+            G = 32 if kind == "int8g" else H
+            s = wf.view(2 * I, H // G, G).abs().amax(-1) / 127.0
+            q = torch.round(wf / s.repeat_interleave(G, 1)).clamp(-127, 127)
+            parts.append(Q.QuantPart.from_int8((q + 128).to(torch.uint8), s, None, DEV))
+    w = Q.QuantMoE(parts)
+    assert w.kqt == {"fp8": 6, "int8": 9, "int8g": 8}[kind]
+    P = T * k
+    tile = 16 if P <= 8 * E else 32
+    cap = -(-(P + E * (tile - 1)) // tile) * tile
+    ids = torch.topk(torch.rand(T, E, device=DEV), k, dim=-1).indices.int()
+    slots = torch.empty(cap, dtype=torch.int32, device=DEV)
+    te = torch.empty(cap // tile, dtype=torch.int32, device=DEV)
+    nt = torch.empty(1, dtype=torch.int32, device=DEV)
+    ps = torch.empty(P, dtype=torch.int32, device=DEV)
+    op.moe_align(ids, E, tile, slots, te, nt, ps)
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    f32 = torch.empty(0, dtype=torch.float32, device=DEV)
+    gu = torch.zeros(cap, 2 * I, device=DEV, dtype=torch.bfloat16)
+    op.qmoe_gemm(gu, f32, x, w.q, w.rs, w.kqt, w.N, w.K, slots, te, tile, k, 1)
+    want = torch.zeros(cap, I, device=DEV, dtype=torch.bfloat16)
+    torch.ops.hipserve.silu_and_mul(want, gu)
+    real = slots >= 0
+    G, nsb = w.N // 16, w.K // 256
+    qk = w.q.view(w.E, G, nsb, -1).transpose(1, 2).contiguous().view(w.E, -1)
+    for q, km in ((w.q, False), (qk, True)):
+        act = torch.zeros(cap, I, device=DEV, dtype=torch.bfloat16)
+        op.qmoe_gemm(act, f32, x, q, w.rs, w.kqt, w.N, w.K, slots, te, tile, k, 1, km, 1)
+        assert torch.equal(act[real], want[real]), km
+        gk = torch.zeros_like(gu)
+        op.qmoe_gemm(gk, f32, x, q, w.rs, w.kqt, w.N, w.K, slots, te, tile, k, 1, km)
+        assert torch.equal(gk[real], gu[real]), km
