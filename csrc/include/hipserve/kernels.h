@@ -101,7 +101,7 @@ void launch_gguf_gemm_parts(void* out, long out_stride, float* ws, const void* x
                             const GgufPart* parts, int nparts, int M, int Ntot, int K, int S, hipStream_t s,
                             const void* x16 = nullptr);
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s,
-                               int pack = 0, int nrows = 0);
+                               int pack = 0, int nrows = 0, bool kmajor = false);
 // per-channel FP8 tiled part -> row-major [N, K] e4m3 bytes (N % 16 == 0, K % 256 == 0)
 void launch_fp8_untile(void* out, const void* q, int N, int K, hipStream_t s);
 // prefill GEMM straight from the tiled GGUF blocks on launch_x_f16_pairs' x16 / rsc (epi:

@@ -437,15 +437,21 @@ template <int QT>
 __global__ __launch_bounds__(256) void dequant_tiled_kernel(unsigned short* __restrict__ out,
                                                             const unsigned char* __restrict__ q,
                                                             const float* __restrict__ rs, int ngroups, int K,
-                                                            int pack, int nrows) {
+                                                            int pack, int nrows, int kmajor) {
   constexpr int CB = chunk_bytes<QT>();
   const int nsb = K >> 8;
   const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= (long)ngroups * nsb) return;
   const int gi = (int)(item / nsb), sb = (int)(item % nsb);
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  // kmajor: every stacked matrix of nrows rows is [K/256][nrows/16][chunk] (MoE w13)
+  long src = item;
+  if (kmajor) {
+    const int kg = nrows >> 4, e = gi / kg;
+    src = ((long)e * nsb + sb) * kg + (gi - e * kg);
+  }
   Raw r;
-  load_raw<QT>(q + item * CB, g, c, lane, r);
+  load_raw<QT>(q + src * CB, g, c, lane, r);
   Dec<QT> dec;
   dec.setup(r, g);
   unsigned short* row = out + (long)(16 * gi + c) * K + sb * 256;
@@ -958,23 +964,23 @@ void launch_fp8_untile(void* out, const void* q, int N, int K, hipStream_t s) {
 }
 
 void launch_gguf_dequant_tiled(void* out, const void* q, const float* rs, int qtype, int N, int K, hipStream_t s,
-                               int pack, int nrows) {
+                               int pack, int nrows, bool kmajor) {
   if (nrows <= 0) nrows = N;
   const long items = (long)(N / 16) * (K / 256);
   const dim3 grid((unsigned)((items + 3) / 4)), block(256);
   auto* o = static_cast<unsigned short*>(out);
   auto* qq = static_cast<const unsigned char*>(q);
   switch (qtype) {
-    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case INT8: dequant_tiled_kernel<INT8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
-    case INT8C: dequant_tiled_kernel<INT8C><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows); break;
+    case Q4_0: dequant_tiled_kernel<Q4_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case Q4_1: dequant_tiled_kernel<Q4_1><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case Q8_0: dequant_tiled_kernel<Q8_0><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case Q4_K: dequant_tiled_kernel<Q4_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case Q5_K: dequant_tiled_kernel<Q5_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case Q6_K: dequant_tiled_kernel<Q6_K><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case FP8: dequant_tiled_kernel<FP8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case FP8B: dequant_tiled_kernel<FP8B><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case INT8: dequant_tiled_kernel<INT8><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
+    case INT8C: dequant_tiled_kernel<INT8C><<<grid, block, 0, s>>>(o, qq, rs, N / 16, K, pack, nrows, kmajor ? 1 : 0); break;
   }
 }
 

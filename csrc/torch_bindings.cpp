@@ -454,7 +454,7 @@ int64_t qmoe_gemm(at::Tensor& out, at::Tensor& ws, const at::Tensor& x, const at
 // pack 0: out row-major [N, K]; 1 / 2: the stacked matrices of `nrows` rows each (N = E nrows)
 // in the pack_decode_weight layout (2: gate/up-interleaved), E copies back to back
 void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& rs, int64_t qtype, int64_t N,
-                        int64_t K, int64_t pack, int64_t nrows) {
+                        int64_t K, int64_t pack, int64_t nrows, bool kmajor) {
   CHECK_DEV(q); CHECK_BF16(out);
   TORCH_CHECK(out.is_contiguous() && N % 16 == 0 && K % 256 == 0);
   TORCH_CHECK(pack >= 0 && pack <= 2, "gguf_dequant_tiled: pack 0, 1 or 2");
@@ -467,11 +467,12 @@ void gguf_dequant_tiled(at::Tensor& out, const at::Tensor& q, const at::Tensor& 
   }
   TORCH_CHECK(qtype >= 0 && qtype <= 9 && q.scalar_type() == at::kByte && q.is_contiguous());
   TORCH_CHECK(q.numel() == N / 16 * (K / 256) * hipserve::gguf_tiled_chunk_bytes(qtype), "not a tiled tensor");
+  TORCH_CHECK(!kmajor || nrows <= 0 || (nrows % 16 == 0 && N % nrows == 0), "gguf_dequant_tiled: k-major matrices of nrows rows");
   const bool fp8 = row_scaled_qt(qtype);
   TORCH_CHECK(!fp8 || (rs.scalar_type() == at::kFloat && rs.numel() == N), "FP8 / INT8C need an fp32 row scale");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   hipserve::launch_gguf_dequant_tiled(out.data_ptr(), q.data_ptr(), fp8 ? rs.data_ptr<float>() : nullptr,
-                                      qtype, N, K, cur_stream(), (int)pack, (int)nrows);
+                                      qtype, N, K, cur_stream(), (int)pack, (int)nrows, kmajor);
 }
 
 // per-channel FP8 tiled part q [N/16, K/256, 4096] -> out: row-major [N, K] e4m3 bytes
@@ -1304,7 +1305,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("gguf_gemm_parts(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor[] qs, Tensor[] rss, int[] qtypes, int[] rows, int[] cols, int Ntot, int K, int splits, Tensor? x16=None) -> int", &gguf_gemm_parts);
   m.def("gguf_prefill(Tensor(a!) out, Tensor x16, Tensor rsc, Tensor[] qs, int[] qtypes, int[] rows, int[] cols, int K, int epi) -> bool", &gguf_prefill);
   m.def("x_f16_pairs(Tensor(a!) x16, Tensor(b!) rsc, Tensor x) -> ()", &x_f16_pairs);
-  m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K, int pack=0, int nrows=0) -> ()",
+  m.def("gguf_dequant_tiled(Tensor(a!) out, Tensor q, Tensor rs, int qtype, int N, int K, int pack=0, int nrows=0, bool kmajor=False) -> ()",
         &gguf_dequant_tiled);
   m.def("fp8_untile(Tensor(a!) out, Tensor q, int N, int K) -> ()", &fp8_untile);
   m.def("qmoe_gemm(Tensor(a!) out, Tensor(b!) ws, Tensor x, Tensor q, Tensor rs, int qtype, int N, int K, Tensor slots, Tensor tile_expert, int tile, int gather_k, int splits, bool kmajor=False, int glu=0) -> int", &qmoe_gemm);

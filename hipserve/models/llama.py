@@ -324,7 +324,7 @@ class LlamaModel:
         def experts(w, rowpar=False):
             parts = [q8(w[e], rowpar) for e in range(w.shape[0])]
             if all(p is not None for p, _ in parts) and Q.QuantMoE.supported(parts[0][0].kqt, *w.shape[1:]):
-                return Q.QuantMoE([p for p, _ in parts])
+                return Q.QuantMoE([p for p, _ in parts], kmajor=not rowpar)  # w13: super-chunk major
             return torch.stack([d for _, d in parts])
 
         D = self.D
@@ -1262,21 +1262,22 @@ class LlamaModel:
         act = torch.empty(cap, w13.N // 2, dtype=x.dtype, device=dev)
         if tile <= 32 and (w13.N // 2) % 16 == 0:  # GLU in the w13 epilogue (bit-identical)
             glu = 2 if cfg.hidden_act == "gelu_tanh" else 1
-            op.qmoe_gemm(act, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1, False,
-                         glu)
+            op.qmoe_gemm(act, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1,
+                         w13.kmajor, glu)
         else:
             gu = torch.empty(cap, w13.N, dtype=x.dtype, device=dev)
-            op.qmoe_gemm(gu, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1)
+            op.qmoe_gemm(gu, f32, x, w13.q, w13.rs, w13.kqt, w13.N, w13.K, slots, tile_expert, tile, k, 1,
+                         w13.kmajor)
             self.act_and_mul(act, gu)
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         active = min(E, cap // tile, P)
         S = self._moe_w2_splits(w2.K, -(-H // 128), active)
         if S <= 1:
             y = torch.empty(cap, H, dtype=x.dtype, device=dev)
-            op.qmoe_gemm(y, f32, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, 1)
+            op.qmoe_gemm(y, f32, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, 1, w2.kmajor)
             return self._combine(out, y, 0, w, pair_slot, k)
         ws = torch.empty(S, cap, H, dtype=torch.float32, device=dev)
-        S = op.qmoe_gemm(out, ws, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, S)
+        S = op.qmoe_gemm(out, ws, act, w2.q, w2.rs, w2.kqt, w2.N, w2.K, slots, tile_expert, tile, 0, S, w2.kmajor)
         return self._combine(out, ws[:S], S, w, pair_slot, k)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

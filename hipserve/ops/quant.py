@@ -887,11 +887,18 @@ class QuantMoE:
 
     KERNEL_QTS = (6, 8, 9)  # FP8 (per-row scale), INT8, INT8C (per-row scale)
 
-    def __init__(self, parts: list):
+    def __init__(self, parts: list, kmajor: bool = False):
         p0 = parts[0]
         assert all(p.kqt == p0.kqt and p.N == p0.N and p.K == p0.K and p.tiled for p in parts)
         self.E, self.N, self.K, self.kqt = len(parts), p0.N, p0.K, p0.kqt
         self.q = torch.stack([p.q.reshape(-1) for p in parts]).contiguous()
+        # kmajor: each expert [K/256][N/16][chunk] instead of [N/16][K/256][chunk] — at a
+        # given super-chunk the workgroups of an expert stream one contiguous column of it
+        # (w13 at 64 tokens: 84 -> 72 us, profiles/r6_qmoe_int8c_kmajor_bench.log)
+        self.kmajor = bool(kmajor)
+        if self.kmajor:
+            G, nsb = self.N // 16, self.K // 256
+            self.q = self.q.view(self.E, G, nsb, -1).transpose(1, 2).contiguous().view(self.E, -1)
         self.rs = (torch.stack([p.rs for p in parts]).contiguous() if p0.kqt in (6, 9)
                    else torch.empty(0, 0, dtype=torch.float32, device=p0.q.device))
         self.dense = None
@@ -906,7 +913,7 @@ class QuantMoE:
         # the stacked experts [E][N/16][K/256][chunk] are one tiled [E N, K] matrix: one launch
         torch.ops.hipserve.gguf_dequant_tiled(out.view(self.E * self.N, self.K), self.q.view(-1),
                                               self.rs.view(-1) if self.rs.numel() else self.rs,
-                                              self.kqt, self.E * self.N, self.K)
+                                              self.kqt, self.E * self.N, self.K, 0, self.N, self.kmajor)
         return out
 
     @staticmethod
@@ -947,7 +954,7 @@ def moe_packed_scratch(w: QuantMoE, slot: int, glu: bool) -> torch.Tensor:
         buf = _MOE_PACKED_SCRATCH[key] = torch.empty(n, dtype=torch.bfloat16, device=w.q.device)
     out = buf[:n].view(w.E, n // w.E)
     torch.ops.hipserve.gguf_dequant_tiled(out.view(-1), w.q.view(-1), w.rs.view(-1) if w.rs.numel() else w.rs,
-                                          w.kqt, w.E * w.N, w.K, 2 if glu else 1, w.N)
+                                          w.kqt, w.E * w.N, w.K, 2 if glu else 1, w.N, w.kmajor)
     return out
 
 

@@ -411,7 +411,7 @@ def _native_experts(ck, m, names, E, sl, dev):
         return None
     if not (Q.QuantMoE.supported(p13[0].kqt, p13[0].N, p13[0].K) and Q.QuantMoE.supported(p2[0].kqt, p2[0].N, p2[0].K)):
         return None
-    return Q.QuantMoE(p13), Q.QuantMoE(p2)
+    return Q.QuantMoE(p13, kmajor=True), Q.QuantMoE(p2)
 
 
 def save_hf_checkpoint(path: str, cfg, tensors: dict[str, torch.Tensor]):

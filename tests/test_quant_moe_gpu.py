@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _qmoe(w, kind):
+def _qmoe(w, kind, kmajor=False):
     from hipserve.ops import quant as Q
 
     parts, deq = [], []
@@ -27,7 +27,7 @@ def _qmoe(w, kind):
             q = (wf / s).to(torch.float8_e4m3fn)
             parts.append(Q.QuantPart.from_fp8(q, s, DEV))
             deq.append(q.float() * s)
-    return Q.QuantMoE(parts), torch.stack(deq)
+    return Q.QuantMoE(parts, kmajor=kmajor), torch.stack(deq)
 
 
 @pytest.mark.parametrize("kind", ["int8", "fp8"])
@@ -43,7 +43,7 @@ def test_quant_moe_vs_fp32(kind, T, E, k, I):
     m = LlamaModel(cfg, TPGroup(0, 1, None, torch.device(DEV)), DEV, torch.bfloat16, KernelOps())
     torch.manual_seed(T + E + I)
     router = torch.randn(E, H, device=DEV, dtype=torch.bfloat16) * 0.3
-    w13, d13 = _qmoe(torch.randn(E, 2 * I, H, device=DEV) * 0.05, kind)
+    w13, d13 = _qmoe(torch.randn(E, 2 * I, H, device=DEV) * 0.05, kind, kmajor=True)
     w2, d2 = _qmoe(torch.randn(E, H, I, device=DEV) * 0.05, kind)
     lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=router, w13=w13, w2=w2)
     x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
@@ -201,7 +201,7 @@ def test_quant_moe_prefill_paths_vs_fp32(kind, packed):
     m.MOE_PACKED_PREFILL = "1" if packed else "0"
     torch.manual_seed(7)
     router = torch.randn(E, H, device=DEV, dtype=torch.bfloat16) * 0.3
-    w13, d13 = _qmoe(torch.randn(E, 2 * I, H, device=DEV) * 0.05, kind)
+    w13, d13 = _qmoe(torch.randn(E, 2 * I, H, device=DEV) * 0.05, kind, kmajor=True)
     w2, d2 = _qmoe(torch.randn(E, H, I, device=DEV) * 0.05, kind)
     lw = LayerWeights(ln1=None, wqkv=None, wo=None, ln2=None, router=router, w13=w13, w2=w2)
     x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
