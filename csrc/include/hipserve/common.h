@@ -39,16 +39,40 @@ HS_DEVICE unsigned int pack_bf16x2(float lo, float hi) {
 }
 
 // ---- wave64 reductions (xor butterflies over all 64 lanes) ----
-HS_DEVICE float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Wave reductions on the DPP crossbar: quad swaps, half-row and row mirrors (every lane
+// then holds its 16-lane row's result), the row broadcasts 15 / 31 (lane 63 holds the
+// wave's), and a readlane to broadcast it — six VALU steps instead of six dependent
+// ds_bpermute round trips through the LDS crossbar. The result is wave-uniform.
+template <int kCtrl, int kRowMask, bool kMax>
+HS_DEVICE float dpp_step(float x) {
+  const float y = __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), kCtrl, kRowMask, 0xf,
+                                         false));
+  return kMax ? fmaxf(x, y) : x + y;
 }
-HS_DEVICE float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+template <bool kMax>
+HS_DEVICE float wave_reduce(float v) {
+  // masked-off rows keep `old` = x: for the sum those rows must add 0, so the broadcast
+  // steps use the explicit select below instead of dpp_step
+  v = dpp_step<0xB1, 0xf, kMax>(v);   // quad_perm [1, 0, 3, 2]
+  v = dpp_step<0x4E, 0xf, kMax>(v);   // quad_perm [2, 3, 0, 1]
+  v = dpp_step<0x141, 0xf, kMax>(v);  // row_half_mirror
+  v = dpp_step<0x140, 0xf, kMax>(v);  // row_mirror
+  if constexpr (kMax) {
+    v = dpp_step<0x142, 0xa, true>(v);  // row_bcast:15 -> rows 1, 3
+    v = dpp_step<0x143, 0xc, true>(v);  // row_bcast:31 -> rows 2, 3
+  } else {
+    const float b15 = __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xa, 0xf, false));
+    v += b15;  // rows 1, 3 (+0 elsewhere)
+    const float b31 = __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xc, 0xf, false));
+    v += b31;  // rows 2, 3
+  }
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
+HS_DEVICE float wave_sum(float v) { return wave_reduce<false>(v); }
+HS_DEVICE float wave_max(float v) { return wave_reduce<true>(v); }
 
 // Block-wide sum for blockDim.x <= 1024 (16 waves). `scratch` needs >= 16 floats.
 HS_DEVICE float block_sum(float v, float* scratch) {

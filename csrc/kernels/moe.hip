@@ -67,20 +67,13 @@ __global__ __launch_bounds__(256) void moe_topk_softmax_kernel(const T* __restri
   for (int s = 0; s < 2; ++s) p[s] = ex[s] / sum;
   float sel_sum = 0.f;
   for (int j = 0; j < k; ++j) {
-    // argmax over (lane, slot) (ties -> lower expert id)
-    float bv = -1.f;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int e = lane + 64 * s;
-      if (rank[s] < 0 && e < E && (p[s] > bv || (p[s] == bv && e < bi))) { bv = p[s]; bi = e; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(bv, o, 64);
-      const int i2 = __shfl_xor(bi, o, 64);
-      if (v2 > bv || (v2 == bv && i2 < bi)) { bv = v2; bi = i2; }
-    }
+    // argmax over (lane, slot), ties -> lower expert id: the wave max of the unselected
+    // probabilities, then the lowest lane holding it (slot 0 = experts 0-63 first)
+    const float c0 = rank[0] < 0 && lane < E ? p[0] : -1.f;
+    const float c1 = rank[1] < 0 && lane + 64 < E ? p[1] : -1.f;
+    const float bv = wave_max(fmaxf(c0, c1));  // DPP reduction (common.h), wave-uniform
+    const unsigned long long b0 = __ballot(c0 == bv), b1 = __ballot(c1 == bv);
+    const int bi = b0 ? __builtin_ctzll(b0) : 64 + __builtin_ctzll(b1);
     if (bi == lane) rank[0] = j;
     if (bi == lane + 64) rank[1] = j;
     sel_sum += bv;
