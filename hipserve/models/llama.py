@@ -116,9 +116,12 @@ class LlamaModel:
     # First version: 5.57 vs 5.49 ms per Llama-3-8B B=64 decode step (every wave re-read
     # the fp32 partials for q before streaming K/V). Now each wave's first K/V chunk is
     # issued before the partial sums and q is computed once per workgroup (shared via
-    # LDS): 5.322 / 5.332 vs 5.332 / 5.327 ms (tools/decode_gap.py, alternating runs) —
-    # parity, so the separate splitk_rope_cache launch stays the default
-    fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "0") == "1"
+    # LDS): 5.322 / 5.332 vs 5.332 / 5.327 ms in round 2 (parity). Re-measured in round 6
+    # after the non-temporal K/V stream and DPP reductions: 5.257 / 5.247 vs 5.306 / 5.297 ms
+    # (tools/decode_gap.py, alternating runs, profiles/r6_fused_qkv_attn_ab.log) — now the
+    # default for bf16 caches without q/k norm, qkv bias or sliding window; =0 restores the
+    # separate splitk_rope_cache launch
+    fused_qkv_attention = os.environ.get("HIPSERVE_FUSED_QKV_ATTN", "1") == "1"
     # (round 3 tried a "v2" decode layer with the split-K fix-up and the epilogue inside each
     # decode GEMM launch: slower, 6,398 vs 7,650 tok/s, profiles/r3_bench_v2_first.json —
     # an in-launch split-K seam costs more than the kernel boundary it replaces; removed)
@@ -745,10 +748,14 @@ class LlamaModel:
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
             win = cfg.window_of(i)
+            # the fused kernel writes the new token's K / V as bf16 (an e4m3 cache takes
+            # the separate splitk_rope_cache writer)
+            fuse_qa = (self.fused_qkv_attention and D in (64, 128) and not extras and not win
+                       and kc.element_size() == 2)
             cs = self.cos_sin_local if win else self.cos_sin
             pt = self._partial(xn, lw.wqkv, xn16, xn8)
             attn16 = self._x16(attn, lw.wo)  # the attention's f16 pair-order copy for a quantised o_proj
-            if pt is not None and self.fused_qkv_attention and D in (64, 128) and not extras and not win:
+            if pt is not None and fuse_qa:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
                                     meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part, self.scale,
@@ -766,7 +773,7 @@ class LlamaModel:
                     ops.qk_rmsnorm(qkv, lw.q_norm, lw.k_norm, nq, nkv, D, eps)
                 ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cs, kc, vc, nq, nkv, D,
                                cfg.rope_mode)
-            if pt is None or not (self.fused_qkv_attention and D in (64, 128) and not extras and not win):
+            if pt is None or not fuse_qa:
                 ops.paged_decode(attn, qkv, kc, vc, meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml,
                                  nq, nkv, part, self.scale, win, attn16)
             pt = self._partial(attn, lw.wo, attn16)

@@ -86,12 +86,13 @@ def bench_sample(ops):
 
 def bench_decode(ops):
     import os
-    D, bs = 128, 16
+    D = 128
     parts = [int(x) for x in os.environ.get("DECODE_PARTS", "512").split(",")]
+    bss = [int(x) for x in os.environ.get("DECODE_BS", "16").split(",")]  # KV block sizes
     shapes = [(64, 1152, 32, 8), (64, 1280, 32, 8), (256, 1152, 32, 8), (1, 4096, 32, 8), (64, 4096, 64, 8)]
     if os.environ.get("DECODE_SHAPES"):  # "BxCTXxNQxNKV,..." e.g. 64x1152x32x4 (Qwen3-30B-A3B)
         shapes = [tuple(int(v) for v in sh.split("x")) for sh in os.environ["DECODE_SHAPES"].split(",")]
-    for (B, ctx, nq, nkv), part in [(c, p) for c in shapes for p in parts]:
+    for (B, ctx, nq, nkv), part, bs in [(c, p, b) for c in shapes for p in parts for b in bss]:
         mb = math.ceil(ctx / bs) + 1
         nblocks = B * mb
         # DECODE_COLD=1: rotate over enough KV copies (> 2x the 256 MB MALL) that every
@@ -118,7 +119,7 @@ def bench_decode(ops):
             ops.paged_decode(out, q, kcs[i], vcs[i], bt, cl, to, tm, nq, nkv, part, 1 / math.sqrt(D))
 
         us = timeit(call)
-        emit(op="paged_decode", kv="fp8" if f8 else "bf16", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, cold=ncopy > 1,
+        emit(op="paged_decode", kv="fp8" if f8 else "bf16", B=B, ctx=ctx, nq=nq, nkv=nkv, part=part, bs=bs, cold=ncopy > 1,
              nt=os.environ.get("HIPSERVE_DECODE_NT", "1"), us=round(us, 1), TBps=round(byts / us / 1e6, 2))
         del kcs, vcs
 
