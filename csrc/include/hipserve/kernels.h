@@ -38,7 +38,8 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
                              const long* slots, const float* cos_sin, int mode, void* k_cache, void* v_cache,
                              const int* block_tables, int bt_stride, const int* context_lens, float* tmp_out,
                              float* tmp_ml, int B, int nq, int nkv, int D, int block_size, int part_size,
-                             int max_parts, float scale, int window, hipStream_t s, void* out16 = nullptr);
+                             int max_parts, float scale, int window, hipStream_t s, void* out16 = nullptr,
+                             const float* qw = nullptr, const float* kw = nullptr, float eps = 1e-6f);
 // out16 (optional): f16 pair-order copy of out for a quantised o-projection (out's row stride)
 void launch_paged_decode(void* out, long out_stride, const void* q, long q_stride,
                          const void* k_cache, const void* v_cache,

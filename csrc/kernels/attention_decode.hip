@@ -53,7 +53,31 @@ struct QkvIn {
   unsigned short* k_cache;
   unsigned short* v_cache;
   int mode;               // 0 = rotate-half (HF), 1 = interleaved pairs (GGUF llama)
+  const float* qw;        // per-head q / k RMSNorm weights [D] before RoPE (Qwen3), or null;
+  const float* kw;        // rotate-half only; rounding as splitk_rope_cache (bf16 after the norm)
+  float eps;
 };
+
+// per-head RMSNorm of 8 + 8 values (d and d + D/2 of one rotate-half chunk) whose
+// head spans lanes: the same sum order as splitk_rope_cache's kNorm branch (own x
+// terms, own y terms, then the chunk-xor partners), applied and rounded to bf16
+template <int D>
+HS_DEVICE void qk_norm_apply(float (&x)[8], float (&y)[8], float ss, const float* nw, int d0, float eps) {
+  const float inv = rsqrtf(ss / D + eps);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    x[j] = bf16_to_f32(f32_to_bf16(x[j] * inv * nw[d0 + j]));
+    y[j] = bf16_to_f32(f32_to_bf16(y[j] * inv * nw[D / 2 + d0 + j]));
+  }
+}
+HS_DEVICE float sumsq16(const float (&x)[8], const float (&y)[8]) {
+  float ss = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s2 += y[j] * y[j];
+  return ss + s2;
+}
 
 // 8 consecutive partial sums over the S slices, rounded to bf16 (as splitk_rope_cache)
 HS_DEVICE void qkv_sum8(float (&o)[8], const float* p, long slice, int S) {
@@ -244,6 +268,11 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
             float x[8], y[8];
             qkv_sum8(x, kr + it * 8, qi.slice, qi.S);
             qkv_sum8(y, kr + half + it * 8, qi.slice, qi.S);
+            if (qi.kw != nullptr) {  // lanes 0 .. D/16-1 hold the head's chunks: xor within them
+              float ss = sumsq16(x, y);
+              for (int o = nk_items / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+              qk_norm_apply<D>(x, y, ss, qi.kw, it * 8, qi.eps);
+            }
             u16x8 va, vb;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -295,7 +324,39 @@ __global__ __launch_bounds__(64 * kDecWaves) __attribute__((amdgpu_waves_per_eu(
       for (int j = 0; j < 8; ++j) u[j] = col < G ? f32_to_bf16(v[j]) : 0;
       qsh[ks * 64 + lane] = u;
     };
-    if (qi.mode == 0) {
+    if (qi.mode == 0 && qi.qw != nullptr) {
+      // per-head q norm: the head's rotate-half chunk c = 4 ks + grp (D = 128) sits in
+      // fragments ks < KS/2 of lane group grp, so wave 0 computes every fragment: the
+      // chunk-xor tree of splitk_rope_cache is in-lane (xor 4 at D = 128) then lane xor
+      // 32 (chunk xor 2) and 16 (chunk xor 1); bit-identical sums
+      if (wave == 0) {
+        float x[KS / 2][8], y[KS / 2][8];
+        float ssk[KS / 2];
+#pragma unroll
+        for (int ks = 0; ks < KS / 2; ++ks) {
+          q_frag(ks, x[ks]);
+          q_frag(ks + KS / 2, y[ks]);
+          ssk[ks] = sumsq16(x[ks], y[ks]);
+        }
+        float ss = ssk[0];
+        if constexpr (KS / 2 == 2) ss += ssk[1];
+        ss += __shfl_xor(ss, 32, 64);
+        ss += __shfl_xor(ss, 16, 64);
+#pragma unroll
+        for (int ks = 0; ks < KS / 2; ++ks) {
+          qk_norm_apply<D>(x[ks], y[ks], ss, qi.qw, 8 * grp + 32 * ks, qi.eps);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i = 8 * grp + 32 * ks + j;
+            const float co = cs[i], si = cs[half + i];
+            const float a = x[ks][j], bb = y[ks][j];
+            rope_rot(a, bb, co, si, x[ks][j], y[ks][j]);
+          }
+          q_store(ks, x[ks]);
+          q_store(ks + KS / 2, y[ks]);
+        }
+      }
+    } else if (qi.mode == 0) {
       for (int ks = wave; ks < KS / 2; ks += kDecWaves) {
         float x[8], y[8];
         q_frag(ks, x);
@@ -668,7 +729,8 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
                              const long* slots, const float* cos_sin, int mode, void* k_cache, void* v_cache,
                              const int* block_tables, int bt_stride, const int* context_lens, float* tmp_out,
                              float* tmp_ml, int B, int nq, int nkv, int D, int block_size, int part_size,
-                             int max_parts, float scale, int window, hipStream_t s, void* out16) {
+                             int max_parts, float scale, int window, hipStream_t s, void* out16,
+                             const float* qw, const float* kw, float eps) {
   if (B <= 0) return;
   auto* o16 = static_cast<unsigned short*>(out16);
   const int waves = decode_waves();
@@ -677,7 +739,7 @@ void launch_paged_decode_qkv(void* out, long out_stride, const float* ws, int S,
   auto* o = static_cast<unsigned short*>(out);
   auto* kc = static_cast<unsigned short*>(k_cache);
   auto* vc = static_cast<unsigned short*>(v_cache);
-  const QkvIn qi{ws, (long)B * N, S, N, positions, slots, cos_sin, kc, vc, mode};
+  const QkvIn qi{ws, (long)B * N, S, N, positions, slots, cos_sin, kc, vc, mode, qw, kw, eps};
 #define HS_DECODE_QKV(DD, WW)                                                                                  \
   do {                                                                                                        \
     if (decode_nt((long)max_parts * nkv * B))                                                                 \

@@ -171,11 +171,22 @@ void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, con
                       const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& k_cache, at::Tensor& v_cache,
                       const at::Tensor& block_tables, const at::Tensor& context_lens, at::Tensor& tmp_out,
                       at::Tensor& tmp_ml, int64_t nq, int64_t nkv, int64_t part_size, double scale, int64_t window,
-                      int64_t mode, const c10::optional<at::Tensor>& out16) {
+                      int64_t mode, const c10::optional<at::Tensor>& out16, const c10::optional<at::Tensor>& q_w,
+                      const c10::optional<at::Tensor>& k_w, double eps) {
   CHECK_DEV(ws); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   TORCH_CHECK(!kv_is_f8(k_cache, v_cache), "paged_decode_qkv: bf16 KV cache only");
   const int D = k_cache.size(3), bs = k_cache.size(2);
   TORCH_CHECK(D == 64 || D == 128, "paged_decode_qkv: head_dim 64/128");
+  const float *qwp = nullptr, *kwp = nullptr;
+  if (q_w.has_value()) {  // per-head q / k RMSNorm before RoPE (Qwen3)
+    TORCH_CHECK(k_w.has_value() && q_w->scalar_type() == at::kFloat && k_w->scalar_type() == at::kFloat &&
+                q_w->numel() == D && k_w->numel() == D && q_w->is_contiguous() && k_w->is_contiguous(),
+                "paged_decode_qkv: fp32 q/k norm weights [head_dim]");
+    TORCH_CHECK(mode == 0, "paged_decode_qkv: q/k norm needs rotate-half RoPE (mode 0)");
+    CHECK_DEV(*q_w); CHECK_DEV(*k_w);
+    qwp = q_w->data_ptr<float>();
+    kwp = k_w->data_ptr<float>();
+  }
   TORCH_CHECK(window >= 0 && (mode == 0 || mode == 1));
   TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "paged_decode_qkv: GQA group <= 16");
   TORCH_CHECK(bs % 16 == 0 && (bs & (bs - 1)) == 0 && part_size % 128 == 0 && part_size / bs < 255);
@@ -202,7 +213,7 @@ void paged_decode_qkv(at::Tensor& out, const at::Tensor& ws, int64_t splits, con
                                     mode, k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                     block_tables.stride(0), context_lens.data_ptr<int>(), tmp_out.data_ptr<float>(),
                                     tmp_ml.data_ptr<float>(), B, nq, nkv, D, bs, part_size, max_parts, (float)scale,
-                                    (int)window, cur_stream(), out16_ptr(out16, out));
+                                    (int)window, cur_stream(), out16_ptr(out16, out), qwp, kwp, (float)eps);
 }
 
 void prefill_attention(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
@@ -1334,7 +1345,7 @@ TORCH_LIBRARY(hipserve, m) {
   m.def("splitk_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor weight, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_post_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor ws, int splits, Tensor w_post, Tensor w_next, float eps, Tensor(c!)? out16=None, Tensor(d!)? out8=None, Tensor(e!)? xs8=None) -> ()");
   m.def("splitk_glu(Tensor(a!) act, Tensor ws, int splits, bool gelu, Tensor(b!)? act16=None) -> ()");
-  m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode, Tensor(f!)? out16=None) -> ()");
+  m.def("paged_decode_qkv(Tensor(a!) out, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor context_lens, Tensor(d!) tmp_out, Tensor(e!) tmp_ml, int nq, int nkv, int part_size, float scale, int window, int mode, Tensor(f!)? out16=None, Tensor? q_norm=None, Tensor? k_norm=None, float eps=1e-6) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor ws, int splits) -> ()");
   m.def("splitk_rope_cache(Tensor(a!) qkv, Tensor ws, int splits, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(b!) k_cache, Tensor(c!) v_cache, int nq, int nkv, int head_dim, int mode, Tensor? bias=None, Tensor? q_w=None, Tensor? k_w=None, float eps=1e-6) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, int rt, int kw) -> ()");

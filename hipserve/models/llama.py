@@ -499,10 +499,26 @@ class LlamaModel:
         if isinstance(lw.wd, dense):
             out[tuple(lw.wd.shape)] = ("norm",)
         if isinstance(lw.wqkv, dense):
-            out[tuple(lw.wqkv.shape)] = ("rope", self.nq, self.nkv, self.D, self.cfg.rope_mode)
+            # the fused decode attention consumes the partials itself (no epilogue launch):
+            # timed as the partial GEMM alone; else GEMM + splitk_rope_cache
+            kind = "attn" if self.fused_qkv_attn_ok() else "rope"
+            out[tuple(lw.wqkv.shape)] = (kind, self.nq, self.nkv, self.D, self.cfg.rope_mode)
         if isinstance(lw.wgu, dense) and lw.wgu.shape[0] % 128 == 0 and self.cfg.hidden_act == "silu":
             out[tuple(lw.wgu.shape)] = ("glu",)  # GeGLU: plain partials + splitk_glu (tuned as a plain GEMM)
         return out
+
+    def fused_qkv_attn_ok(self, layer: int | None = None) -> bool:
+        """Decode attention straight from the qkv split-K partials (RoPE + KV write inside,
+        attention_decode.hip QkvIn): bf16 cache, head_dim 64 / 128, no qkv bias, per-head q/k
+        RMSNorm (Qwen3) only with rotate-half RoPE, no sliding window (``layer`` None: on
+        every layer)."""
+        lw0 = self.layers[0] if self.layers else None
+        if (not self.fused_qkv_attention or self.D not in (64, 128) or lw0 is None or lw0.bqkv is not None
+                or (lw0.q_norm is not None and self.cfg.rope_mode != 0)
+                or torch.finfo(self.kv_dtype).bits != 16):
+            return False
+        layers = range(len(self.layers)) if layer is None else (layer,)
+        return not any(self.cfg.window_of(i) for i in layers)
 
     def _fused_ok(self, meta: AttnMeta) -> bool:
         return (self.fused_decode and meta.num_prefill_tokens == 0
@@ -744,14 +760,12 @@ class LlamaModel:
         part, tmp_out, tmp_ml = self._decode_split(T, meta)
         L = len(self.layers)
         lw0 = self.layers[0]
-        extras = lw0.bqkv is not None or lw0.q_norm is not None
         for i, lw in enumerate(self.layers):
             kc, vc = kv_caches[i]
             win = cfg.window_of(i)
             # the fused kernel writes the new token's K / V as bf16 (an e4m3 cache takes
             # the separate splitk_rope_cache writer)
-            fuse_qa = (self.fused_qkv_attention and D in (64, 128) and not extras and not win
-                       and kc.element_size() == 2)
+            fuse_qa = self.fused_qkv_attn_ok(i) and kc.element_size() == 2
             cs = self.cos_sin_local if win else self.cos_sin
             pt = self._partial(xn, lw.wqkv, xn16, xn8)
             attn16 = self._x16(attn, lw.wo)  # the attention's f16 pair-order copy for a quantised o_proj
@@ -759,7 +773,7 @@ class LlamaModel:
                 # RoPE + KV write + attention in one kernel, straight from the partials
                 op.paged_decode_qkv(attn, pt[0], pt[1], meta.positions, meta.slot_mapping, self.cos_sin, kc, vc,
                                     meta.bt_decode, meta.ctx_decode, tmp_out, tmp_ml, nq, nkv, part, self.scale,
-                                    0, cfg.rope_mode, attn16)
+                                    0, cfg.rope_mode, attn16, lw.q_norm, lw.k_norm, eps)
             elif pt is not None:  # + q/k/v bias and per-head q/k RMSNorm of the family, if any
                 ws, S = pt
                 qkv = torch.empty(T, lw.wqkv.shape[0], device=h.device, dtype=h.dtype)

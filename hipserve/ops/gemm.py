@@ -111,7 +111,8 @@ class GemmTuner:
     @torch.inference_mode()
     def tune(self, shapes, device, ms=None, fused=None):
         """fused: {(N, K): spec} for projections whose output feeds a fused
-        epilogue in the decode layer — ("norm",), ("rope", nq, nkv, D, mode) or
+        epilogue in the decode layer — ("norm",), ("rope", nq, nkv, D, mode), ("attn", nq,
+        nkv, D, mode) (the fused decode attention reads the partials: GEMM alone) or
         ("glu",); those are timed as GEMM + epilogue units."""
         # inference mode like the engine's graph capture: the generator state tensors a
         # capture registers must not switch between inference and normal tensors
@@ -230,7 +231,7 @@ class _Unit:
             self.res = torch.randn(M, N, **bf)
             self.w = torch.ones(N, **bf)
             self.y = torch.empty(M, N, **bf)
-        elif self.kind == "rope":
+        elif self.kind in ("rope", "attn"):
             _, self.nq, self.nkv, self.D, self.mode = spec
             nb = -(-M // 16) + 1
             self.kc = torch.zeros(nb, self.nkv, 16, self.D, **bf)
@@ -246,7 +247,7 @@ class _Unit:
         op = self.op
         if self.kind == "norm":
             op.fused_add_rmsnorm(self.y, y, self.res, self.w, 1e-5)
-        elif self.kind == "rope":
+        elif self.kind in ("rope", "attn"):  # hipBLASLt: qkv rows, then the RoPE + KV write kernel
             op.rope_cache(y, self.pos, self.slots, self.cs, self.kc, self.vc, self.nq, self.nkv, self.D, self.mode)
         else:
             op.silu_and_mul(self.act, y)
@@ -269,6 +270,8 @@ class _Unit:
         op.decode_gemm_partial(ws, x, wp if packed else w, N, rt, S, packed)
         if self.kind == "norm":
             op.splitk_add_rmsnorm(self.y, self.res, ws, S, self.w, 1e-5)
+        elif self.kind == "attn":
+            pass  # the fused decode attention sums the partials (RoPE + KV write inside)
         else:
             op.splitk_rope_cache(self.qkv, ws, S, self.pos, self.slots, self.cs, self.kc, self.vc,
                                  self.nq, self.nkv, self.D, self.mode)

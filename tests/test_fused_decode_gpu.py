@@ -203,6 +203,13 @@ def test_fused_qkv_attention_forward_bit_exact(ops, choices):
     test_fused_decode_forward_bit_exact(ops, choices, qkv_attn=True)
 
 
+@pytest.mark.parametrize("family", ["qwen3", "qwen3_moe"])
+def test_fused_qkv_attention_qk_norm_forward_bit_exact(ops, family):
+    """Qwen3 decode layer with the per-head q / k norm inside the fused attention vs the
+    unfused path (and the model really takes the fused kernel)."""
+    test_fused_decode_forward_bit_exact(ops, "dgp", family, qkv_attn=True)
+
+
 @pytest.mark.parametrize("choices", ["dgp", "dg", "mixed"])
 def test_fused_decode_forward_bit_exact(ops, choices, family="llama", qkv_attn=False):
     """Model forward on a decode batch: fused epilogues vs the unfused path."""
@@ -211,6 +218,8 @@ def test_fused_decode_forward_bit_exact(ops, choices, family="llama", qkv_attn=F
     m, cfg = _small_model(ops, family=family)
     assert m.fused_family
     m.fused_qkv_attention = qkv_attn
+    if qkv_attn and family in ("llama", "qwen3", "qwen3_moe"):
+        assert m.fused_qkv_attn_ok()
     old = dict(gemm.TUNER.table)
     try:
         gemm.TUNER.table.clear()
@@ -253,14 +262,25 @@ def test_fused_decode_forward_bit_exact(ops, choices, family="llama", qkv_attn=F
         gemm.TUNER.table.update(old)
 
 
+@pytest.mark.parametrize("S,part", [(1, 512), (4, 128), (2, 2048)])
+@pytest.mark.parametrize("D", [128, 64])
+def test_paged_decode_qkv_qk_norm_bit_exact(ops, S, part, D):
+    """Qwen3's per-head q / k RMSNorm inside the fused decode attention == splitk_rope_cache
+    (norm branch) followed by paged_decode, bit for bit."""
+    test_paged_decode_qkv_bit_exact(ops, 0, S, part, D, qk_norm=True)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("S,part", [(1, 512), (4, 128), (3, 256)])
 @pytest.mark.parametrize("D", [128, 64])
-def test_paged_decode_qkv_bit_exact(ops, mode, S, part, D):
+def test_paged_decode_qkv_bit_exact(ops, mode, S, part, D, qk_norm=False):
     """Fused qkv partials -> RoPE + KV write + attention == splitk_rope_cache followed
     by paged_decode, bit for bit (output and both caches), with split contexts
     (several partitions + reduce) and a padding row (slot -1)."""
     B, nq, nkv, bs = 9, 16, 4, 16
+    nw = ((torch.rand(D, device=DEV, generator=torch.Generator(device=DEV).manual_seed(D)) + 0.5),
+          (torch.rand(D, device=DEV, generator=torch.Generator(device=DEV).manual_seed(D + 1)) + 0.5)) \
+        if qk_norm else (None, None)
     N = (nq + 2 * nkv) * D
     ws = _partials(S, B, N, 31 + S + D)
     nblk = 40
@@ -279,14 +299,15 @@ def test_paged_decode_qkv_bit_exact(ops, mode, S, part, D):
     mk = lambda: (torch.empty(B, nq, parts, D, device=DEV), torch.empty(B, nq, parts, 2, device=DEV))
     scale = D ** -0.5
     qkv = torch.zeros(B, N, device=DEV, dtype=torch.bfloat16)
-    torch.ops.hipserve.splitk_rope_cache(qkv, ws.contiguous(), S, pos, slots, cs, kc1, vc1, nq, nkv, D, mode)
+    torch.ops.hipserve.splitk_rope_cache(qkv, ws.contiguous(), S, pos, slots, cs, kc1, vc1, nq, nkv, D, mode,
+                                         None, nw[0], nw[1], 1e-6)
     out1 = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
     t1, m1 = mk()
     ops.paged_decode(out1, qkv, kc1, vc1, bt, ctx, t1, m1, nq, nkv, part, scale)
     out2 = torch.empty(B, nq * D, device=DEV, dtype=torch.bfloat16)
     t2, m2 = mk()
     torch.ops.hipserve.paged_decode_qkv(out2, ws.contiguous(), S, pos, slots, cs, kc2, vc2, bt, ctx, t2, m2,
-                                        nq, nkv, part, scale, 0, mode)
+                                        nq, nkv, part, scale, 0, mode, None, nw[0], nw[1], 1e-6)
     assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
     assert torch.equal(out1, out2)
 
