@@ -758,6 +758,11 @@ class LlamaModel:
             ops.rmsnorm(xn, h, self.layers[0].ln1, eps)
         attn = torch.empty(T, nq * D, device=h.device, dtype=h.dtype)
         part, tmp_out, tmp_ml = self._decode_split(T, meta)
+        # the fused qkv attention only with ONE context partition per (sequence, kv head):
+        # with a split context every partition's workgroup re-sums the qkv partials, and
+        # long contexts ran slower fused (Llama-3.1-8B 8K x 16: 1,189 vs 1,210 tok/s,
+        # 32K x 4: 232 vs 239; profiles/r6_qkv_attn_long_ab.log)
+        one_part = -(-meta.bt_decode.shape[1] * self.block_size_hint // part) == 1
         L = len(self.layers)
         lw0 = self.layers[0]
         for i, lw in enumerate(self.layers):
@@ -765,7 +770,7 @@ class LlamaModel:
             win = cfg.window_of(i)
             # the fused kernel writes the new token's K / V as bf16 (an e4m3 cache takes
             # the separate splitk_rope_cache writer)
-            fuse_qa = self.fused_qkv_attn_ok(i) and kc.element_size() == 2
+            fuse_qa = one_part and self.fused_qkv_attn_ok(i) and kc.element_size() == 2
             cs = self.cos_sin_local if win else self.cos_sin
             pt = self._partial(xn, lw.wqkv, xn16, xn8)
             attn16 = self._x16(attn, lw.wo)  # the attention's f16 pair-order copy for a quantised o_proj

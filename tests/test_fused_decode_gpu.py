@@ -220,6 +220,7 @@ def test_fused_decode_forward_bit_exact(ops, choices, family="llama", qkv_attn=F
     m.fused_qkv_attention = qkv_attn
     if qkv_attn and family in ("llama", "qwen3", "qwen3_moe"):
         assert m.fused_qkv_attn_ok()
+        m.decode_partition = 2048  # one context partition: the fused kernel's regime
     old = dict(gemm.TUNER.table)
     try:
         gemm.TUNER.table.clear()
